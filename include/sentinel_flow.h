@@ -1,0 +1,337 @@
+/*
+ * sentinel_flow.h — C-ABI of the MI355X batch flow-check engine.
+ *
+ * This is the drop-in boundary for Sentinel's statistics-and-check hot path
+ * (SURVEY.md §8b).  A Java shim binds these symbols through JNI / Panama FFM
+ *  from behind two existing SPIs:
+ *
+ *   - SlotChainBuilder / ProcessorSlot   (in-process SphU.entry path)
+ *       replaces  StatisticSlot.entry/exit + SystemSlot + ParamFlowSlot +
+ *       FlowSlot of the default chain:
+ *         sentinel-core/.../slotchain/SlotChainBuilder.java:25-33
+ *         sentinel-core/.../slotchain/ProcessorSlot.java:28-77
+ *         sentinel-core/.../slots/statistic/StatisticSlot.java:55-178
+ *         sentinel-core/.../slots/block/flow/FlowSlot.java:162-174
+ *         sentinel-parameter-flow-control/.../param/ParamFlowSlot.java:38-104
+ *         sentinel-core/.../slots/system/SystemSlot.java:37-42
+ *   - TokenService                        (cluster token server)
+ *       replaces  DefaultTokenService.requestToken/requestParamToken:
+ *         sentinel-core/.../cluster/TokenService.java:26-63
+ *         sentinel-cluster-server-default/.../flow/DefaultTokenService.java:39-64
+ *
+ * Plain C: no exceptions cross the ABI, no torch / HIP types in signatures.
+ * Every function returning int returns SF_OK (0) or a negative SF_ERR_* code;
+ * sf_last_error() gives a human-readable message for the calling thread.
+ *
+ * Threading: one engine instance serialises sf_submit / sf_request_tokens
+ * internally (a submit lock).  The Java shim batches from many application
+ * threads into one flusher thread (SURVEY.md §8b "Threading").
+ *
+ * Ownership: the caller owns all input/output arrays; the engine owns every
+ * byte of device state.  Rules are copied at load.
+ */
+#ifndef SENTINEL_FLOW_H
+#define SENTINEL_FLOW_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SF_ABI_VERSION 1
+
+/* ---- return codes ------------------------------------------------------ */
+#define SF_OK               0
+#define SF_ERR_INVALID     -1   /* bad argument / inconsistent batch        */
+#define SF_ERR_NOMEM       -2   /* host or device allocation failed         */
+#define SF_ERR_DEVICE      -3   /* HIP runtime error / no usable GPU        */
+#define SF_ERR_UNSUPPORTED -4   /* rule or event feature outside the engine */
+#define SF_ERR_CAPACITY    -5   /* batch / table larger than configured     */
+
+/* ---- Sentinel constants (RuleConstant.java:26-66) ------------------------ */
+#define SF_GRADE_THREAD 0
+#define SF_GRADE_QPS    1
+#define SF_STRATEGY_DIRECT 0
+#define SF_STRATEGY_RELATE 1
+#define SF_STRATEGY_CHAIN  2
+#define SF_BEHAVIOR_DEFAULT              0
+#define SF_BEHAVIOR_WARM_UP              1
+#define SF_BEHAVIOR_RATE_LIMITER         2
+#define SF_BEHAVIOR_WARM_UP_RATE_LIMITER 3
+/* ClusterRuleConstant.FLOW_THRESHOLD_AVG_LOCAL = 0, FLOW_THRESHOLD_GLOBAL = 1 */
+#define SF_THRESHOLD_AVG_LOCAL 0
+#define SF_THRESHOLD_GLOBAL    1
+
+#define SF_MAX_SAMPLE_COUNT 16   /* second-window buckets supported          */
+#define SF_MINUTE_BUCKETS   60   /* StatisticNode.java:105 ArrayMetric(60,60000) */
+#define SF_MAX_RULES_PER_RESOURCE 8
+#define SF_MAX_ARGS 4
+
+/* ---- engine configuration (SentinelConfig / *Property defaults) -------- */
+typedef struct sf_config {
+    int32_t  sample_count;        /* SampleCountProperty.SAMPLE_COUNT = 2      */
+    int32_t  interval_ms;         /* IntervalProperty.INTERVAL = 1000          */
+    int32_t  occupy_timeout_ms;   /* OccupyTimeoutProperty = 500               */
+    int32_t  cold_factor;         /* ColdFactorProperty.coldFactor = 3         */
+    int64_t  statistic_max_rt;    /* SentinelConfig.statisticMaxRt = 5000      */
+    uint32_t max_resources;       /* resource ids of this shard: [0, max)      */
+    uint32_t max_batch;           /* largest sf_submit / sf_request_tokens n   */
+    uint32_t param_capacity;      /* exact hot-param table entries             */
+    uint32_t shard_count;         /* resource sharding: res % shard_count ==   */
+    uint32_t shard_index;         /*   shard_index; local id = res/shard_count */
+    int32_t  device;              /* HIP device ordinal                        */
+    /* cluster token server (ServerFlowConfig.java:26-31) */
+    int32_t  cluster_sample_count;/* 10 */
+    int32_t  cluster_interval_ms; /* 1000 */
+    double   exceed_count;        /* 1.0 */
+    double   max_occupy_ratio;    /* 1.0 */
+    uint32_t max_flow_ids;        /* capacity of the flowId table              */
+    uint32_t reserved;
+} sf_config;
+
+/* Fill *cfg with the reference defaults listed above. */
+void sf_config_default(sf_config* cfg);
+
+/* ---- rules ------------------------------------------------------------- */
+/* One FlowRule (FlowRule.java:36-241).  limitApp is "default", no origin;
+ * the caller passes rules already in the order Java iterates them
+ * (FlowRuleUtil.buildFlowRuleMap: HashSet order + stable FlowRuleComparator
+ * sort, FlowRuleUtil.java:83-130).  Rules of one resource keep array order. */
+typedef struct sf_flow_rule {
+    uint32_t resource;            /* resource id (interned name)               */
+    int32_t  grade;               /* SF_GRADE_*                                */
+    double   count;
+    int32_t  strategy;            /* SF_STRATEGY_DIRECT (RELATE/CHAIN: UNSUPPORTED) */
+    int32_t  control_behavior;    /* SF_BEHAVIOR_*                             */
+    int32_t  warm_up_period_sec;  /* default 10                                */
+    int32_t  max_queueing_time_ms;/* default 500                               */
+    int32_t  cluster_mode;        /* 0 only (cluster: see sf_cluster_flow_rule) */
+    uint32_t ref_resource;
+} sf_flow_rule;
+
+/* Param value identity = Java equals(): (type tag, 64-bit payload); strings
+ * are interned by the caller (ParamFlowChecker.java:126-155).            */
+#define SF_TAG_NULL   0
+#define SF_TAG_INT    1
+#define SF_TAG_LONG   2
+#define SF_TAG_STRING 3
+#define SF_TAG_DOUBLE 4
+#define SF_TAG_BOOL   5
+#define SF_TAG_OTHER  6
+
+typedef struct sf_hot_item {      /* ParamFlowItem parsed (ParamFlowRuleUtil.java:188-240) */
+    uint8_t  tag;
+    uint8_t  pad[3];
+    int32_t  count;
+    uint64_t bits;
+} sf_hot_item;
+
+/* One ParamFlowRule (ParamFlowRule.java:45-83). */
+typedef struct sf_param_rule {
+    uint32_t resource;
+    int32_t  grade;               /* SF_GRADE_QPS (default) / SF_GRADE_THREAD  */
+    int32_t  param_idx;           /* may be negative: ParamFlowSlot.applyRealParamIdx */
+    int32_t  control_behavior;    /* SF_BEHAVIOR_DEFAULT / SF_BEHAVIOR_RATE_LIMITER */
+    double   count;
+    int32_t  max_queueing_time_ms;/* default 0 */
+    int32_t  burst_count;         /* default 0 */
+    int64_t  duration_in_sec;     /* default 1 */
+    uint32_t item_offset;         /* hot items: items[item_offset .. +item_count) */
+    uint32_t item_count;
+} sf_param_rule;
+
+/* SystemRule thresholds (SystemRuleManager.java:291-348); negative = unset. */
+typedef struct sf_system_rule {
+    double  highest_system_load;
+    double  highest_cpu_usage;
+    double  qps;
+    int64_t avg_rt;
+    int64_t max_thread;
+} sf_system_rule;
+
+/* ---- events (time-ordered, SoA) ----------------------------------------- */
+#define SF_EV_EXIT   0x01u   /* EXIT event (Entry.exit), else ENTRY            */
+#define SF_EV_IN     0x02u   /* EntryType.IN (feeds ENTRY_NODE / SystemRule)   */
+#define SF_EV_PRIO   0x04u   /* prioritized entry                              */
+#define SF_EV_ERROR  0x08u   /* EXIT: business exception recorded (Tracer)     */
+
+#define SF_MEM_HOST   0
+#define SF_MEM_DEVICE 1
+
+typedef struct sf_event_batch {
+    uint32_t        n;
+    int32_t         mem;          /* SF_MEM_HOST or SF_MEM_DEVICE (all arrays) */
+    const uint32_t* res_id;       /* [n] resource id                          */
+    const int64_t*  ts_ms;        /* [n] mocked TimeUtil clock, non-decreasing */
+    const int32_t*  count;        /* [n] acquireCount (EXIT: the entry's count) */
+    const uint8_t*  flags;        /* [n] SF_EV_*                               */
+    /* EXIT only: index (in this batch) of the ENTRY being exited, or -1 when
+     * that entry passed in an earlier batch (then create_ts supplies rt).   */
+    const int64_t*  entry_ref;    /* [n] or NULL when the batch has no EXIT   */
+    const int64_t*  create_ts;    /* [n] or NULL; read only where entry_ref<0 */
+    /* args: n_args[i] values for event i, stored [slot][n] (slot-major).   */
+    uint32_t        arg_slots;    /* 0..SF_MAX_ARGS                            */
+    const uint8_t*  n_args;       /* [n] or NULL (= arg_slots for every event) */
+    const uint8_t*  arg_tag;      /* [arg_slots*n]                             */
+    const uint64_t* arg_bits;     /* [arg_slots*n]                             */
+} sf_event_batch;
+
+/* ---- verdicts ---------------------------------------------------------- */
+#define SF_V_PASS          0   /* entry passed                                   */
+#define SF_V_PASS_WAIT     1   /* passed after Thread.sleep(wait_ms) (rate limiter) */
+#define SF_V_PRIORITY_WAIT 2   /* PriorityWaitException(wait_ms): passed, borrowed */
+#define SF_V_BLOCK_FLOW    3   /* FlowException (rule_idx = index in resource list) */
+#define SF_V_BLOCK_PARAM   4   /* ParamFlowException                             */
+#define SF_V_BLOCK_SYSTEM  5   /* SystemBlockException (rule_idx: 0 qps 1 thread 2 rt 3 load 4 cpu) */
+#define SF_V_EXIT          6   /* exit of a passed entry: recorded               */
+#define SF_V_EXIT_IGNORED  7   /* exit of a blocked entry: nothing recorded      */
+
+typedef struct sf_verdicts {
+    int32_t  mem;                 /* SF_MEM_HOST or SF_MEM_DEVICE             */
+    uint8_t* status;              /* [n] SF_V_*  (required)                    */
+    int32_t* wait_ms;             /* [n] or NULL                               */
+    uint16_t* rule_idx;           /* [n] or NULL                               */
+} sf_verdicts;
+
+/* ---- cluster token service (TokenService.java:26-63) -------------------- */
+/* TokenResultStatus.java:27-69 */
+#define SF_TOKEN_OK                0
+#define SF_TOKEN_BLOCKED           1
+#define SF_TOKEN_SHOULD_WAIT       2
+#define SF_TOKEN_NO_RULE_EXISTS    3
+#define SF_TOKEN_BAD_REQUEST      -4
+#define SF_TOKEN_TOO_MANY_REQUEST -2
+#define SF_TOKEN_FAIL             -1
+
+typedef struct sf_cluster_flow_rule {   /* cluster-mode FlowRule + ClusterFlowConfig */
+    int64_t  flow_id;
+    double   count;
+    int32_t  threshold_type;      /* SF_THRESHOLD_*                            */
+    uint32_t namespace_id;
+    int32_t  sample_count;        /* ClusterFlowConfig default 10              */
+    int32_t  window_interval_ms;  /* default 1000                              */
+} sf_cluster_flow_rule;
+
+typedef struct sf_cluster_param_rule {  /* cluster-mode ParamFlowRule */
+    int64_t  flow_id;
+    double   count;
+    int32_t  threshold_type;
+    uint32_t namespace_id;
+    int32_t  sample_count;
+    int32_t  window_interval_ms;
+    uint32_t item_offset;         /* hot items (exclusive thresholds) */
+    uint32_t item_count;
+} sf_cluster_param_rule;
+
+typedef struct sf_namespace {
+    uint32_t namespace_id;
+    int32_t  connected_count;     /* ConnectionManager.getConnectedCount       */
+    double   max_allowed_qps;     /* GlobalRequestLimiter; < 0: no limiter     */
+} sf_namespace;
+
+#define SF_TOK_PRIORITIZED 0x01u
+#define SF_TOK_PARAM       0x02u  /* requestParamToken (one param value)       */
+
+typedef struct sf_token_batch {
+    uint32_t        n;
+    int32_t         mem;
+    const int64_t*  flow_id;      /* [n] rule id (Long ruleId)                 */
+    const int32_t*  count;        /* [n] acquireCount                          */
+    const uint8_t*  flags;        /* [n] SF_TOK_*                              */
+    const int64_t*  ts_ms;        /* [n] server clock at request, non-decreasing */
+    const uint8_t*  param_tag;    /* [n] or NULL                               */
+    const uint64_t* param_bits;   /* [n] or NULL                               */
+} sf_token_batch;
+
+typedef struct sf_token_results {
+    int32_t  mem;
+    int8_t*  status;              /* [n] SF_TOKEN_*                            */
+    int32_t* remaining;           /* [n] or NULL                               */
+    int32_t* wait_ms;             /* [n] or NULL                               */
+} sf_token_results;
+
+/* ---- state read-back (parity tests, metric snapshot) -------------------- */
+#define SF_WS_ABSENT INT64_MIN    /* bucket slot never created (Java null)     */
+
+typedef struct sf_bucket {       /* WindowWrap<MetricBucket> (MetricBucket.java:28-142) */
+    int64_t window_start;
+    int64_t pass, block, exception, success, rt, occupied_pass;
+    int64_t min_rt;
+} sf_bucket;
+
+typedef struct sf_node_state {    /* ClusterNode of one resource (StatisticNode.java:97-105) */
+    sf_bucket second[SF_MAX_SAMPLE_COUNT];
+    int64_t   borrow_ws[SF_MAX_SAMPLE_COUNT];    /* FutureBucketLeapArray */
+    int64_t   borrow_pass[SF_MAX_SAMPLE_COUNT];
+    sf_bucket minute[SF_MINUTE_BUCKETS];
+    int64_t   cur_thread_num;
+} sf_node_state;
+
+typedef struct sf_rule_state {    /* controller state (WarmUp / RateLimiter) */
+    int64_t stored_tokens;
+    int64_t last_filled_time;
+    int64_t latest_passed_time;
+} sf_rule_state;
+
+typedef struct sf_metric_row {    /* MetricNode (MetricNode.java:160-229) */
+    uint32_t resource;
+    uint32_t pad;
+    int64_t  timestamp;
+    int64_t  pass_qps, block_qps, success_qps, exception_qps, rt, occupied_pass_qps;
+} sf_metric_row;
+
+typedef struct sf_stats {         /* timings of the last sf_submit (device clock) */
+    double   total_ms;
+    double   sort_ms;
+    double   decide_ms;           /* the dominant per-resource decision kernel */
+    double   scatter_ms;
+    uint64_t n_events;
+    uint64_t n_segments;          /* resources touched                         */
+    uint64_t n_launches;
+} sf_stats;
+
+/* ---- API ------------------------------------------------------------- */
+typedef struct sf_engine sf_engine;
+
+int  sf_abi_version(void);
+int  sf_create(const sf_config* cfg, sf_engine** out);
+void sf_destroy(sf_engine* e);
+const char* sf_last_error(void);
+
+int  sf_load_flow_rules (sf_engine* e, const sf_flow_rule* rules, uint32_t n);
+int  sf_load_param_rules(sf_engine* e, const sf_param_rule* rules, uint32_t n,
+                         const sf_hot_item* items, uint32_t n_items);
+int  sf_load_system_rules(sf_engine* e, const sf_system_rule* rules, uint32_t n);
+/* JMX load / cpu inputs of SystemRule (fixed inputs in a replay). */
+int  sf_set_system_status(sf_engine* e, double avg_load, double cpu_usage);
+
+/* Decide a time-ordered batch: per-event verdicts, state updated in place. */
+int  sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
+
+/* Cluster token server (DefaultTokenService). */
+int  sf_load_namespaces(sf_engine* e, const sf_namespace* ns, uint32_t n);
+int  sf_load_cluster_rules(sf_engine* e, const sf_cluster_flow_rule* flow, uint32_t n_flow,
+                           const sf_cluster_param_rule* param, uint32_t n_param,
+                           const sf_hot_item* items, uint32_t n_items);
+int  sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* out);
+
+/* State read-back and the per-second metric snapshot (StatisticNode.metrics). */
+int  sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out);
+int  sf_read_entry_node(sf_engine* e, sf_node_state* out);
+int  sf_read_rule_state(sf_engine* e, uint32_t rule_index, sf_rule_state* out);
+int  sf_snapshot(sf_engine* e, int64_t now_ms, sf_metric_row* out, uint32_t cap, uint32_t* n_out);
+
+/* Device helpers so hosts without a GPU framework can stage HBM inputs. */
+int  sf_device_alloc(sf_engine* e, size_t bytes, void** ptr);
+int  sf_device_free(sf_engine* e, void* ptr);
+int  sf_memcpy(sf_engine* e, void* dst, const void* src, size_t bytes, int kind /*0 H2D 1 D2H 2 D2D*/);
+int  sf_sync(sf_engine* e);
+int  sf_get_stats(sf_engine* e, sf_stats* out);
+int  sf_set_timing(sf_engine* e, int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SENTINEL_FLOW_H */

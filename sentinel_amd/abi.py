@@ -1,0 +1,315 @@
+"""ctypes mirror of ``include/sentinel_flow.h`` (the C-ABI drop-in boundary).
+
+Every structure here matches the header field for field; ``tests/test_abi.py``
+checks the sizes against the compiled library.  Nothing in this module touches
+a GPU: it only describes memory layouts and wraps numpy arrays.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+SF_ABI_VERSION = 1
+
+SF_OK = 0
+SF_ERR_INVALID = -1
+SF_ERR_NOMEM = -2
+SF_ERR_DEVICE = -3
+SF_ERR_UNSUPPORTED = -4
+SF_ERR_CAPACITY = -5
+
+# RuleConstant.java:26-66
+GRADE_THREAD, GRADE_QPS = 0, 1
+STRATEGY_DIRECT, STRATEGY_RELATE, STRATEGY_CHAIN = 0, 1, 2
+BEHAVIOR_DEFAULT, BEHAVIOR_WARM_UP, BEHAVIOR_RATE_LIMITER, BEHAVIOR_WARM_UP_RATE_LIMITER = 0, 1, 2, 3
+THRESHOLD_AVG_LOCAL, THRESHOLD_GLOBAL = 0, 1
+
+SF_MAX_SAMPLE_COUNT = 16
+SF_MINUTE_BUCKETS = 60
+SF_MAX_RULES_PER_RESOURCE = 8
+SF_MAX_ARGS = 4
+
+TAG_NULL, TAG_INT, TAG_LONG, TAG_STRING, TAG_DOUBLE, TAG_BOOL, TAG_OTHER = range(7)
+
+EV_EXIT, EV_IN, EV_PRIO, EV_ERROR = 0x01, 0x02, 0x04, 0x08
+MEM_HOST, MEM_DEVICE = 0, 1
+
+V_PASS, V_PASS_WAIT, V_PRIORITY_WAIT, V_BLOCK_FLOW, V_BLOCK_PARAM, V_BLOCK_SYSTEM, V_EXIT, V_EXIT_IGNORED = range(8)
+PASSED = (V_PASS, V_PASS_WAIT, V_PRIORITY_WAIT)
+
+TOKEN_OK, TOKEN_BLOCKED, TOKEN_SHOULD_WAIT, TOKEN_NO_RULE_EXISTS = 0, 1, 2, 3
+TOKEN_BAD_REQUEST, TOKEN_TOO_MANY_REQUEST, TOKEN_FAIL = -4, -2, -1
+TOK_PRIORITIZED, TOK_PARAM = 0x01, 0x02
+
+WS_ABSENT = -(2 ** 63)
+
+
+class sf_config(C.Structure):
+    _fields_ = [
+        ("sample_count", C.c_int32), ("interval_ms", C.c_int32),
+        ("occupy_timeout_ms", C.c_int32), ("cold_factor", C.c_int32),
+        ("statistic_max_rt", C.c_int64),
+        ("max_resources", C.c_uint32), ("max_batch", C.c_uint32),
+        ("param_capacity", C.c_uint32), ("shard_count", C.c_uint32),
+        ("shard_index", C.c_uint32), ("device", C.c_int32),
+        ("cluster_sample_count", C.c_int32), ("cluster_interval_ms", C.c_int32),
+        ("exceed_count", C.c_double), ("max_occupy_ratio", C.c_double),
+        ("max_flow_ids", C.c_uint32), ("reserved", C.c_uint32),
+    ]
+
+
+def default_config(**kw) -> sf_config:
+    """``sf_config_default`` restated in Python (reference defaults)."""
+    cfg = sf_config(sample_count=2, interval_ms=1000, occupy_timeout_ms=500, cold_factor=3,
+                    statistic_max_rt=5000, max_resources=1024, max_batch=1 << 20,
+                    param_capacity=1 << 16, shard_count=1, shard_index=0, device=0,
+                    cluster_sample_count=10, cluster_interval_ms=1000, exceed_count=1.0,
+                    max_occupy_ratio=1.0, max_flow_ids=1024, reserved=0)
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+class sf_flow_rule(C.Structure):
+    _fields_ = [
+        ("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double),
+        ("strategy", C.c_int32), ("control_behavior", C.c_int32),
+        ("warm_up_period_sec", C.c_int32), ("max_queueing_time_ms", C.c_int32),
+        ("cluster_mode", C.c_int32), ("ref_resource", C.c_uint32),
+    ]
+
+
+class sf_hot_item(C.Structure):
+    _fields_ = [("tag", C.c_uint8), ("pad", C.c_uint8 * 3), ("count", C.c_int32), ("bits", C.c_uint64)]
+
+
+class sf_param_rule(C.Structure):
+    _fields_ = [
+        ("resource", C.c_uint32), ("grade", C.c_int32), ("param_idx", C.c_int32),
+        ("control_behavior", C.c_int32), ("count", C.c_double),
+        ("max_queueing_time_ms", C.c_int32), ("burst_count", C.c_int32),
+        ("duration_in_sec", C.c_int64), ("item_offset", C.c_uint32), ("item_count", C.c_uint32),
+    ]
+
+
+class sf_system_rule(C.Structure):
+    _fields_ = [
+        ("highest_system_load", C.c_double), ("highest_cpu_usage", C.c_double),
+        ("qps", C.c_double), ("avg_rt", C.c_int64), ("max_thread", C.c_int64),
+    ]
+
+
+class sf_event_batch(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32), ("mem", C.c_int32),
+        ("res_id", C.c_void_p), ("ts_ms", C.c_void_p), ("count", C.c_void_p),
+        ("flags", C.c_void_p), ("entry_ref", C.c_void_p), ("create_ts", C.c_void_p),
+        ("arg_slots", C.c_uint32), ("n_args", C.c_void_p),
+        ("arg_tag", C.c_void_p), ("arg_bits", C.c_void_p),
+    ]
+
+
+class sf_verdicts(C.Structure):
+    _fields_ = [("mem", C.c_int32), ("status", C.c_void_p), ("wait_ms", C.c_void_p), ("rule_idx", C.c_void_p)]
+
+
+class sf_cluster_flow_rule(C.Structure):
+    _fields_ = [
+        ("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
+        ("namespace_id", C.c_uint32), ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32),
+    ]
+
+
+class sf_cluster_param_rule(C.Structure):
+    _fields_ = [
+        ("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
+        ("namespace_id", C.c_uint32), ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32),
+        ("item_offset", C.c_uint32), ("item_count", C.c_uint32),
+    ]
+
+
+class sf_namespace(C.Structure):
+    _fields_ = [("namespace_id", C.c_uint32), ("connected_count", C.c_int32), ("max_allowed_qps", C.c_double)]
+
+
+class sf_token_batch(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32), ("mem", C.c_int32), ("flow_id", C.c_void_p), ("count", C.c_void_p),
+        ("flags", C.c_void_p), ("ts_ms", C.c_void_p), ("param_tag", C.c_void_p), ("param_bits", C.c_void_p),
+    ]
+
+
+class sf_token_results(C.Structure):
+    _fields_ = [("mem", C.c_int32), ("status", C.c_void_p), ("remaining", C.c_void_p), ("wait_ms", C.c_void_p)]
+
+
+class sf_bucket(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in
+                ("window_start", "pass_", "block", "exception", "success", "rt", "occupied_pass", "min_rt")]
+
+
+class sf_node_state(C.Structure):
+    _fields_ = [
+        ("second", sf_bucket * SF_MAX_SAMPLE_COUNT),
+        ("borrow_ws", C.c_int64 * SF_MAX_SAMPLE_COUNT),
+        ("borrow_pass", C.c_int64 * SF_MAX_SAMPLE_COUNT),
+        ("minute", sf_bucket * SF_MINUTE_BUCKETS),
+        ("cur_thread_num", C.c_int64),
+    ]
+
+
+class sf_rule_state(C.Structure):
+    _fields_ = [("stored_tokens", C.c_int64), ("last_filled_time", C.c_int64), ("latest_passed_time", C.c_int64)]
+
+
+class sf_metric_row(C.Structure):
+    _fields_ = [("resource", C.c_uint32), ("pad", C.c_uint32), ("timestamp", C.c_int64),
+                ("pass_qps", C.c_int64), ("block_qps", C.c_int64), ("success_qps", C.c_int64),
+                ("exception_qps", C.c_int64), ("rt", C.c_int64), ("occupied_pass_qps", C.c_int64)]
+
+
+class sf_stats(C.Structure):
+    _fields_ = [("total_ms", C.c_double), ("sort_ms", C.c_double), ("decide_ms", C.c_double),
+                ("scatter_ms", C.c_double), ("n_events", C.c_uint64), ("n_segments", C.c_uint64),
+                ("n_launches", C.c_uint64)]
+
+
+STRUCT_SIZES = {name: C.sizeof(cls) for name, cls in [
+    ("sf_config", sf_config), ("sf_flow_rule", sf_flow_rule), ("sf_hot_item", sf_hot_item),
+    ("sf_param_rule", sf_param_rule), ("sf_system_rule", sf_system_rule),
+    ("sf_event_batch", sf_event_batch), ("sf_verdicts", sf_verdicts),
+    ("sf_cluster_flow_rule", sf_cluster_flow_rule), ("sf_cluster_param_rule", sf_cluster_param_rule),
+    ("sf_namespace", sf_namespace), ("sf_token_batch", sf_token_batch),
+    ("sf_token_results", sf_token_results), ("sf_bucket", sf_bucket), ("sf_node_state", sf_node_state),
+    ("sf_rule_state", sf_rule_state), ("sf_metric_row", sf_metric_row), ("sf_stats", sf_stats)]}
+
+
+def node_state_to_dict(st: sf_node_state, sample_count: int = 2) -> dict:
+    """Plain-python view of a node state, for equality checks in tests."""
+    def b(x):
+        return (x.window_start, x.pass_, x.block, x.exception, x.success, x.rt, x.occupied_pass, x.min_rt)
+    return {
+        "second": [b(st.second[i]) for i in range(sample_count)],
+        "borrow": [(st.borrow_ws[i], st.borrow_pass[i]) for i in range(sample_count)],
+        "minute": [b(st.minute[i]) for i in range(SF_MINUTE_BUCKETS)],
+        "threads": st.cur_thread_num,
+    }
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+class HostBatch:
+    """A time-ordered event batch held in host numpy arrays (SoA).
+
+    Keeps the arrays alive while the ``sf_event_batch`` that points at them is
+    in use.
+    """
+
+    def __init__(self, res_id, ts_ms, count, flags, entry_ref=None, create_ts=None,
+                 arg_tag=None, arg_bits=None, n_args=None):
+        self.res_id = np.ascontiguousarray(res_id, dtype=np.uint32)
+        self.ts_ms = np.ascontiguousarray(ts_ms, dtype=np.int64)
+        self.count = np.ascontiguousarray(count, dtype=np.int32)
+        self.flags = np.ascontiguousarray(flags, dtype=np.uint8)
+        n = self.res_id.shape[0]
+        assert self.ts_ms.shape == (n,) and self.count.shape == (n,) and self.flags.shape == (n,)
+        self.entry_ref = None if entry_ref is None else np.ascontiguousarray(entry_ref, dtype=np.int64)
+        self.create_ts = None if create_ts is None else np.ascontiguousarray(create_ts, dtype=np.int64)
+        if arg_tag is not None:
+            arg_tag = np.ascontiguousarray(arg_tag, dtype=np.uint8)
+            arg_bits = np.ascontiguousarray(arg_bits, dtype=np.uint64)
+            if arg_tag.ndim == 1:
+                arg_tag = arg_tag.reshape(1, n)
+                arg_bits = arg_bits.reshape(1, n)
+            assert arg_tag.shape[1] == n and arg_bits.shape == arg_tag.shape
+        self.arg_tag = arg_tag
+        self.arg_bits = arg_bits
+        self.n_args = None if n_args is None else np.ascontiguousarray(n_args, dtype=np.uint8)
+        self.n = n
+
+    def subset(self, lo: int, hi: int) -> "HostBatch":
+        """Contiguous slice [lo, hi); entry_ref indices are rebased (refs before lo become -1)."""
+        er = None
+        ct = None
+        if self.entry_ref is not None:
+            er = self.entry_ref[lo:hi].copy()
+            ct = np.zeros(hi - lo, np.int64) if self.create_ts is None else self.create_ts[lo:hi].copy()
+            prior = (er >= 0) & (er < lo)
+            ct[prior] = self.ts_ms[er[prior]]
+            er[prior] = -1
+            er[er >= lo] -= lo
+        at = None if self.arg_tag is None else self.arg_tag[:, lo:hi].copy()
+        ab = None if self.arg_bits is None else self.arg_bits[:, lo:hi].copy()
+        na = None if self.n_args is None else self.n_args[lo:hi]
+        return HostBatch(self.res_id[lo:hi], self.ts_ms[lo:hi], self.count[lo:hi], self.flags[lo:hi],
+                         er, ct, at, ab, na)
+
+    def c_struct(self) -> sf_event_batch:
+        b = sf_event_batch()
+        b.n = self.n
+        b.mem = MEM_HOST
+        b.res_id, b.ts_ms, b.count, b.flags = (_ptr(self.res_id), _ptr(self.ts_ms), _ptr(self.count), _ptr(self.flags))
+        b.entry_ref = _ptr(self.entry_ref)
+        b.create_ts = _ptr(self.create_ts)
+        if self.arg_tag is not None:
+            b.arg_slots = self.arg_tag.shape[0]
+            b.arg_tag = _ptr(self.arg_tag)
+            b.arg_bits = _ptr(self.arg_bits)
+        else:
+            b.arg_slots = 0
+        b.n_args = _ptr(self.n_args)
+        return b
+
+
+class HostVerdicts:
+    def __init__(self, n: int):
+        self.status = np.full(n, 255, np.uint8)
+        self.wait_ms = np.zeros(n, np.int32)
+        self.rule_idx = np.zeros(n, np.uint16)
+
+    def c_struct(self) -> sf_verdicts:
+        v = sf_verdicts()
+        v.mem = MEM_HOST
+        v.status, v.wait_ms, v.rule_idx = _ptr(self.status), _ptr(self.wait_ms), _ptr(self.rule_idx)
+        return v
+
+
+class HostTokenBatch:
+    def __init__(self, flow_id, count, flags, ts_ms, param_tag=None, param_bits=None):
+        self.flow_id = np.ascontiguousarray(flow_id, np.int64)
+        self.count = np.ascontiguousarray(count, np.int32)
+        self.flags = np.ascontiguousarray(flags, np.uint8)
+        self.ts_ms = np.ascontiguousarray(ts_ms, np.int64)
+        self.param_tag = None if param_tag is None else np.ascontiguousarray(param_tag, np.uint8)
+        self.param_bits = None if param_bits is None else np.ascontiguousarray(param_bits, np.uint64)
+        self.n = self.flow_id.shape[0]
+
+    def c_struct(self) -> sf_token_batch:
+        t = sf_token_batch()
+        t.n, t.mem = self.n, MEM_HOST
+        t.flow_id, t.count, t.flags, t.ts_ms = (_ptr(self.flow_id), _ptr(self.count), _ptr(self.flags), _ptr(self.ts_ms))
+        t.param_tag, t.param_bits = _ptr(self.param_tag), _ptr(self.param_bits)
+        return t
+
+
+class HostTokenResults:
+    def __init__(self, n: int):
+        self.status = np.full(n, 99, np.int8)
+        self.remaining = np.zeros(n, np.int32)
+        self.wait_ms = np.zeros(n, np.int32)
+
+    def c_struct(self) -> sf_token_results:
+        r = sf_token_results()
+        r.mem = MEM_HOST
+        r.status, r.remaining, r.wait_ms = _ptr(self.status), _ptr(self.remaining), _ptr(self.wait_ms)
+        return r
+
+
+def rules_array(cls, rules):
+    arr = (cls * max(1, len(rules)))()
+    for i, r in enumerate(rules):
+        arr[i] = r
+    return arr
