@@ -1,0 +1,173 @@
+"""Benchmark: flow-check decisions/s on BASELINE.json's headline workload.
+
+Workload (N=1): config 3 — 10M resources, Zipf(1.1) traffic, mixed QPS /
+THREAD / WarmUp / RateLimiter rules, 2^27 events per batch (entries + exits),
+consecutive batches 4 s of trace time apart.  A step = one sf_submit of one
+batch whose inputs are already resident in HBM.  For N>1 each rank owns the
+resources ``res % N == rank`` (hash sharding, no data-path collective) and
+decides its own 2^27-event batch: weak scaling.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for the byte
+model behind ``roofline`` and for the cpu_baseline sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from sentinel_amd import abi, engine, trace  # noqa: E402
+
+engine.lib()   # the HIP runtime of /opt/rocm is loaded before anything else
+
+METRIC = "flow-check decisions/sec (node) + % HBM roofline, 10M resources, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+DURATION_MS = 4000             # trace time per batch
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--resources", type=int, default=10_000_000)
+    ap.add_argument("--events", type=int, default=1 << 27)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 24, help="events replayed by the CPU oracle")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    assert world == args.gpus or world == 1, "launch N>1 with torch.distributed.run"
+
+    R_total = args.resources
+    R_local = (R_total - rank + world - 1) // world
+    t0 = time.time()
+    grade, beh, count = trace.mixed_rule_table(R_local, seed=3 + rank)
+    rules = abi.flow_rules_np(np.arange(R_local, dtype=np.uint32) * world + rank, grade, count, beh)
+    hb = trace.mixed_zipf(R_local, args.events, duration_ms=DURATION_MS, seed=3 + rank)
+    hb.res_id = (hb.res_id.astype(np.uint64) * world + rank).astype(np.uint32)
+    n_entry = int(((hb.flags & abi.EV_EXIT) == 0).sum())
+    n_exit = hb.n - n_entry
+    log(f"[rank {rank}] trace {hb.n} events ({n_entry} entries) over {R_local} resources in {time.time()-t0:.1f}s")
+
+    cfg = abi.default_config(max_resources=R_local, max_batch=hb.n, shard_count=world, shard_index=rank,
+                             device=local)
+    eng = engine.FlowEngine(cfg)
+    eng.load_flow_rules(rules)
+    steps = args.warmup + args.steps
+    # one device-resident copy of the batch per step, timestamps shifted so
+    # consecutive batches continue the same trace
+    batches = []
+    for k in range(steps):
+        shifted = abi.HostBatch(hb.res_id, hb.ts_ms + k * DURATION_MS, hb.count, hb.flags, entry_ref=hb.entry_ref)
+        batches.append(engine.DeviceBatch(eng, shifted))
+    out = engine.DeviceVerdicts(eng, hb.n, with_wait=True, with_rule=False)
+    log(f"[rank {rank}] staged {steps} batches in HBM, t={time.time()-t0:.1f}s")
+
+    for k in range(args.warmup):
+        eng.submit_device(batches[k], out)
+    eng.sync()
+    eng.set_timing(True)
+    if dist:
+        dist.barrier()
+    eng.sync()
+    start = time.perf_counter()
+    for k in range(args.warmup, steps):
+        eng.submit_device(batches[k], out)
+    eng.sync()
+    elapsed = time.perf_counter() - start
+    if dist:
+        dist.barrier()
+    st = eng.stats()
+    status = out.status.numpy()
+    n_pass = int(np.isin(status, abi.PASSED).sum())
+    wait = out.wait_ms.numpy()
+    e_wait = int((wait > 0).sum())
+    n_seg = int(st.n_segments)
+
+    times = np.array([elapsed], np.float64)
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        times[0] = t.item()
+        tot = torch.tensor([n_entry * args.steps], dtype=torch.float64)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        total_decisions = tot.item()
+    else:
+        total_decisions = n_entry * args.steps
+    wall = times[0]
+    value = total_decisions / wall
+
+    # roofline of the dominant kernel (k_decide): SURVEY.md §8(d) byte model
+    decide_ms = st.decide_ms / args.steps
+    b_alg = 25 * hb.n + 4 * e_wait + 12 * n_exit + 528 * n_seg
+    achieved = b_alg / (decide_ms / 1e3) / 1e9
+    roofline = {"bound": "hbm", "kernel": "k_decide", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "alg_bytes_per_launch": b_alg, "avg_launch_ms": round(decide_ms, 4),
+                "pipeline_ms": {"sort+segments": round(st.sort_ms / args.steps, 3),
+                                "decide": round(decide_ms, 3), "scatter": round(st.scatter_ms / args.steps, 3)}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(rules, hb, R_local, args.cpu_sample)
+
+    if rank == 0:
+        line = {"metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+                "data": "synthetic",
+                "config": {"workload": "config3: 10M resources Zipf(1.1), 60% QPS / 10% THREAD / 15% WarmUp / "
+                                       "15% RateLimiter, acquireCount 1 (90%) or 2-5, RT~Exp(20ms) exits",
+                           "resources": R_total, "events_per_batch_per_gpu": hb.n, "entries_per_batch_per_gpu": n_entry,
+                           "resources_touched": n_seg, "pass_fraction": round(n_pass / max(1, n_entry), 4),
+                           "parallelism": f"resource-sharded x{world}"},
+                "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    for b in batches:
+        b.free()
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(rules, hb, R, sample):
+    """The C restatement (oracle/, test infrastructure) replaying the first
+    ``sample`` events of the same batch on one host core."""
+    try:
+        from oracle import oracle as so
+    except Exception as ex:  # pragma: no cover
+        return {"error": str(ex)}
+    n = min(sample, hb.n)
+    sub = hb.subset(0, n)
+    ora = so.OracleEngine(abi.default_config(max_resources=R, max_batch=n))
+    t = time.perf_counter()
+    ora.load_flow_rules(rules)
+    t_load = time.perf_counter() - t
+    t = time.perf_counter()
+    v = ora.submit(sub)
+    dt = time.perf_counter() - t
+    ent = int(((sub.flags & abi.EV_EXIT) == 0).sum())
+    ora.close()
+    return {"value": round(ent / dt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} events ({ent} entries) of the same config-3 batch, single-threaded C oracle "
+                      f"(rule load {t_load:.1f}s excluded)", "seconds": round(dt, 2)}
+
+
+if __name__ == "__main__":
+    main()

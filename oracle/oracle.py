@@ -422,7 +422,8 @@ class OracleEngine:
     __del__ = close
 
     def load_flow_rules(self, rules):
-        rc = lib().so_load_flow_rules(self.h, abi.rules_array(abi.sf_flow_rule, rules), len(rules))
+        ptr, n = abi.flow_rules_ptr(rules)
+        rc = lib().so_load_flow_rules(self.h, ptr, n)
         assert rc == 0, rc
 
     def load_param_rules(self, rules, items=()):

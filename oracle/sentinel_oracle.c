@@ -586,6 +586,7 @@ static int32_t nd_threads(so_node* n, const so_mock_node* m) { return m ? m->cur
 so_controller* so_ctrl_default(double count, int grade) {
     so_controller* c = calloc(1, sizeof *c);
     c->type = CT_DEFAULT; c->count = count; c->grade = grade;
+    c->latest_passed_time = -1;        /* unused by this controller; reads like the RateLimiter initial */
     return c;
 }
 static void warm_up_construct(so_controller* c, double count, int period, int cold_factor) { /* WarmUpController.java:113-139 */
@@ -600,6 +601,7 @@ so_controller* so_ctrl_warm_up(double count, int period_sec, int cold_factor) {
     if (cold_factor <= 1) return NULL;                              /* :114-116 IllegalArgumentException */
     so_controller* c = calloc(1, sizeof *c);
     c->type = CT_WARM_UP; warm_up_construct(c, count, period_sec, cold_factor);
+    c->latest_passed_time = -1;        /* unused by this controller */
     return c;
 }
 so_controller* so_ctrl_rate_limiter(int timeout_ms, double count) {

@@ -313,3 +313,33 @@ def rules_array(cls, rules):
     for i, r in enumerate(rules):
         arr[i] = r
     return arr
+
+
+# numpy views of the rule structs, for loading millions of rules without
+# building Python objects (layouts pinned by tests/test_abi.py).
+FLOW_RULE_DTYPE = np.dtype({
+    "names": ["resource", "grade", "count", "strategy", "control_behavior", "warm_up_period_sec",
+              "max_queueing_time_ms", "cluster_mode", "ref_resource"],
+    "formats": [np.uint32, np.int32, np.float64, np.int32, np.int32, np.int32, np.int32, np.int32, np.uint32],
+    "offsets": [f[1].offset for f in [(n, getattr(sf_flow_rule, n)) for n, _ in sf_flow_rule._fields_]],
+    "itemsize": C.sizeof(sf_flow_rule)})
+
+
+def flow_rules_np(resource, grade, count, behavior, warm_up=10, max_queue=500) -> np.ndarray:
+    n = len(resource)
+    a = np.zeros(n, FLOW_RULE_DTYPE)
+    a["resource"] = resource
+    a["grade"] = grade
+    a["count"] = count
+    a["control_behavior"] = behavior
+    a["warm_up_period_sec"] = warm_up
+    a["max_queueing_time_ms"] = max_queue
+    return a
+
+
+def flow_rules_ptr(rules):
+    """(pointer, n) for a list of sf_flow_rule or a FLOW_RULE_DTYPE array."""
+    if isinstance(rules, np.ndarray):
+        assert rules.dtype == FLOW_RULE_DTYPE
+        return C.cast(rules.ctypes.data, C.POINTER(sf_flow_rule)), rules.shape[0]
+    return rules_array(sf_flow_rule, list(rules)), len(rules)

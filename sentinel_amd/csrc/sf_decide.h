@@ -1,0 +1,651 @@
+// sf_decide.h — the per-resource decision interpreter (product code).
+//
+// One lane owns one resource segment of a time-sorted batch and replays the
+// reference semantics event by event against that resource's ClusterNode
+// state, which it keeps in registers for the length of the segment:
+//   second window (OccupiableBucketLeapArray + borrow FutureBucketLeapArray),
+//   the current minute bucket (cached; others read on demand), curThreadNum,
+//   the controller states of its flow rules.
+// Every TimeUtil.currentTimeMillis() of the reference reads the event time.
+//
+// Reference citations (CORE = sentinel-core/src/main/java/com/alibaba/csp/sentinel,
+// PF = sentinel-extension/sentinel-parameter-flow-control/src/main/java/com/alibaba/csp/sentinel):
+//   LeapArray.currentWindow            CORE/slots/statistic/base/LeapArray.java:128-225
+//   OccupiableBucketLeapArray          CORE/slots/statistic/metric/occupy/OccupiableBucketLeapArray.java:40-83
+//   FutureBucketLeapArray              .../occupy/FutureBucketLeapArray.java:36-52
+//   ArrayMetric                        CORE/slots/statistic/metric/ArrayMetric.java:117-330
+//   StatisticNode                      CORE/node/StatisticNode.java:205-346
+//   StatisticSlot.entry/exit           CORE/slots/statistic/StatisticSlot.java:55-178
+//   FlowRuleChecker.checkFlow          CORE/slots/block/flow/FlowRuleChecker.java:44-59
+//   Default/WarmUp/RateLimiter/WarmUpRateLimiter controllers  CORE/slots/block/flow/controller/
+//   ParamFlowSlot.checkFlow            PF/slots/block/flow/param/ParamFlowSlot.java:56-104
+//   ParamFlowChecker                   PF/slots/block/flow/param/ParamFlowChecker.java:48-273
+//   ParameterMetric thread counts      PF/slots/block/flow/param/ParameterMetric.java:125-250
+//
+// This header compiles for the device (the product kernel) and, for the CPU
+// unit tests of the kernel logic only, for the host (tests/hostsim).
+#pragma once
+#include "sf_internal.h"
+
+#ifndef SF_HD
+#define SF_HD __host__ __device__ __forceinline__
+#endif
+
+namespace sf {
+
+// ---------------------------------------------------------------- Java numerics
+SF_HD int64_t d_bits(double x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __double_as_longlong(x);
+#else
+    int64_t b; __builtin_memcpy(&b, &x, 8); return b;
+#endif
+}
+SF_HD double d_from_bits(int64_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __longlong_as_double(b);
+#else
+    double x; __builtin_memcpy(&x, &b, 8); return x;
+#endif
+}
+SF_HD int32_t j_d2i(double a) {                        // (int) double, JLS 5.1.3
+    if (a != a) return 0;
+    if (a >= 2147483647.0) return INT32_MAX;
+    if (a <= -2147483648.0) return INT32_MIN;
+    return (int32_t)a;
+}
+SF_HD int64_t j_d2l(double a) {                        // (long) double
+    if (a != a) return 0;
+    if (a >= 9223372036854775807.0) return INT64_MAX;
+    if (a <= -9223372036854775807.0 - 1.0) return INT64_MIN;
+    return (int64_t)a;
+}
+SF_HD int64_t j_round(double a) {                      // Math.round(double), exact half-up
+    int64_t bits = d_bits(a);
+    int64_t be = (bits & 0x7ff0000000000000LL) >> 52;
+    int64_t shift = (52 - 1 + 1023) - be;
+    if ((shift & -64) == 0) {
+        int64_t r = (bits & 0x000fffffffffffffLL) | (0x000fffffffffffffLL + 1);
+        if (bits < 0) r = -r;
+        return ((r >> shift) + 1) >> 1;
+    }
+    return j_d2l(a);
+}
+SF_HD double j_next_up(double x) {                     // Math.nextUp(double)
+    if (x != x || x == __builtin_inf()) return x;
+    if (x == 0.0) return d_from_bits(1);
+    int64_t b = d_bits(x);
+    return d_from_bits(x > 0 ? b + 1 : b - 1);
+}
+SF_HD int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+SF_HD int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+SF_HD int64_t wmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+SF_HD int64_t jdiv(int64_t a, int64_t b) { return (a == INT64_MIN && b == -1) ? INT64_MIN : a / b; }
+
+SF_HD uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33; return x;
+}
+
+SF_HD Bucket fresh_bucket(int64_t ws, int64_t max_rt) {  // new/reset MetricBucket (MetricBucket.java:37-70)
+    Bucket b; b.ws = ws; b.pass = b.block = b.exc = b.succ = b.rt = b.occ = 0; b.min_rt = max_rt; return b;
+}
+
+// ============================================================ node state
+// MAXS: compile-time capacity of the second window.  With MAXS == 2 every
+// bucket access is a branch on a constant index, so the window lives in VGPRs.
+template <int MAXS>
+struct NodeWin {
+    Bucket sec[MAXS];
+    Borrow bor[MAXS];
+    Bucket scratch;        // LeapArray.java:220-223 throwaway windows
+    Borrow bscratch;
+    int64_t threads;
+    // minute window: row in HBM + one cached bucket
+    Bucket* gmin;
+    Bucket mb; int32_t mi; int32_t mdirty;
+    Bucket mscratch;
+    int32_t S, wl, interval;
+    int64_t max_rt;
+    double interval_sec;
+
+    template <class F> SF_HD void visit(int idx, F f) {
+        if constexpr (MAXS == 1) { f(sec[0]); }
+        else if constexpr (MAXS == 2) { if (idx == 0) f(sec[0]); else f(sec[1]); }
+        else { f(sec[idx]); }
+    }
+    template <class F> SF_HD void visit_bor(int idx, F f) {
+        if constexpr (MAXS == 1) { f(bor[0]); }
+        else if constexpr (MAXS == 2) { if (idx == 0) f(bor[0]); else f(bor[1]); }
+        else { f(bor[idx]); }
+    }
+
+    // ---- FutureBucketLeapArray (borrowArray) ----
+    // getWindowValue(t) -> pass of the bucket containing t, or -1 when null (LeapArray.java:268-281)
+    SF_HD int64_t borrow_value(int64_t t) {
+        int idx = (int)((t / wl) % S);
+        int64_t v = -1;
+        visit_bor(idx, [&](Borrow& b) { if (b.ws <= t && t < b.ws + wl) v = b.pass; });
+        return v;
+    }
+    // currentWindow(t): returns idx, or -1 for a throwaway window (bscratch)
+    SF_HD int borrow_current(int64_t t) {
+        int idx = (int)((t / wl) % S);
+        int64_t ws = t - t % wl;
+        int r = idx;
+        visit_bor(idx, [&](Borrow& b) {
+            if (b.ws == ws) return;
+            if (ws > b.ws) { b.ws = ws; b.pass = 0; return; }          // FutureBucketLeapArray.resetWindowTo :41-46
+            r = -1;
+        });
+        if (r < 0) { bscratch.ws = ws; bscratch.pass = 0; }
+        return r;
+    }
+    // OccupiableBucketLeapArray.currentWaiting (:67-76)
+    SF_HD int64_t current_waiting(int64_t now) {
+        borrow_current(now);
+        int64_t w = 0;
+        for (int i = 0; i < S; i++)
+            visit_bor(i, [&](Borrow& b) { if (!(now >= b.ws)) w = wadd(w, b.pass); });   // Future deprecation :49-52
+        return w;
+    }
+    SF_HD void add_waiting(int64_t t, int32_t c) {                       // :79-83
+        int i = borrow_current(t);
+        if (i < 0) { bscratch.pass = wadd(bscratch.pass, c); return; }
+        visit_bor(i, [&](Borrow& b) { b.pass = wadd(b.pass, c); });
+    }
+
+    // ---- OccupiableBucketLeapArray main window ----
+    // currentWindow(t): returns idx or -1 (throwaway in `scratch`)
+    SF_HD int sec_current(int64_t t) {
+        int idx = (int)((t / wl) % S);
+        int64_t ws = t - t % wl;
+        int r = idx;
+        bool reset = false, throwaway = false;
+        visit(idx, [&](Bucket& b) {
+            if (b.ws == ws) return;
+            if (ws > b.ws) { reset = true; return; }
+            throwaway = true;
+        });
+        if (reset || throwaway) {
+            int64_t bp = borrow_value(reset ? ws : t);
+            Bucket nb = fresh_bucket(ws, max_rt);
+            if (bp >= 0) nb.pass = reset ? (int64_t)(int32_t)bp : bp;   // resetWindowTo :52-64 / newEmptyBucket :40-49
+            if (reset) visit(idx, [&](Bucket& b) { b = nb; });
+            else { scratch = nb; r = -1; }
+        }
+        return r;
+    }
+    template <class F> SF_HD void sec_apply(int64_t t, F f) {
+        int i = sec_current(t);
+        if (i < 0) f(scratch); else visit(i, f);
+    }
+    SF_HD int64_t sec_sum_pass(int64_t now) {            // ArrayMetric.pass() :117-126
+        sec_current(now);
+        int64_t s = 0;
+        for (int i = 0; i < S; i++)
+            visit(i, [&](Bucket& b) { if (!(wsub(now, b.ws) > interval)) s = wadd(s, b.pass); });
+        return s;
+    }
+    SF_HD int64_t sec_window_pass(int64_t t) {            // ArrayMetric.getWindowPass :324-330
+        int idx = (int)((t / wl) % S);
+        int64_t v = 0;
+        visit(idx, [&](Bucket& b) { if (b.ws <= t && t < b.ws + wl) v = b.pass; });
+        return v;
+    }
+
+    // ---- BucketLeapArray(60, 60000): minute window ----
+    SF_HD void min_flush() {
+        if (mdirty) { gmin[mi] = mb; mdirty = 0; }
+    }
+    // currentWindow(t) -> pointer to the live bucket (cached) or the throwaway
+    SF_HD Bucket* min_current(int64_t t) {
+        int idx = (int)((t / 1000) % MINUTE);
+        int64_t ws = t - t % 1000;
+        if (idx != mi) { min_flush(); mb = gmin[idx]; mi = idx; }
+        if (mb.ws == ws) { mdirty = 1; return &mb; }
+        if (ws > mb.ws) { mb = fresh_bucket(ws, max_rt); mdirty = 1; return &mb; }
+        mscratch = fresh_bucket(ws, max_rt);
+        return &mscratch;
+    }
+    // ArrayMetric.previousWindowPass (:279-286) -> getPreviousWindow (LeapArray.java:234-251)
+    SF_HD int64_t min_previous_pass(int64_t now) {
+        min_current(now);
+        int64_t tp = now - 1000;
+        int idx = (int)((tp / 1000) % MINUTE);
+        Bucket b = (idx == mi) ? mb : gmin[idx];
+        if (wsub(now, b.ws) > 60000) return 0;           // isWindowDeprecated (TimeUtil now)
+        if (b.ws + 1000 < tp) return 0;
+        return b.pass;
+    }
+
+    // ---- StatisticNode ----
+    SF_HD double pass_qps(int64_t now) { return (double)sec_sum_pass(now) / interval_sec; }   // :205-208
+    SF_HD double previous_pass_qps(int64_t now) { return (double)min_previous_pass(now); }   // :179-181
+    SF_HD void add_pass(int64_t now, int32_t c) {                                            // :253-256
+        sec_apply(now, [&](Bucket& b) { b.pass = wadd(b.pass, c); });
+        Bucket* m = min_current(now); m->pass = wadd(m->pass, c);
+    }
+    SF_HD void add_block(int64_t now, int32_t c) {                                           // :268-271
+        sec_apply(now, [&](Bucket& b) { b.block = wadd(b.block, c); });
+        Bucket* m = min_current(now); m->block = wadd(m->block, c);
+    }
+    SF_HD void add_exception(int64_t now, int32_t c) {                                       // :274-277
+        sec_apply(now, [&](Bucket& b) { b.exc = wadd(b.exc, c); });
+        Bucket* m = min_current(now); m->exc = wadd(m->exc, c);
+    }
+    SF_HD void add_rt_success(int64_t now, int64_t rt, int32_t c) {                          // :259-265
+        sec_apply(now, [&](Bucket& b) {
+            b.succ = wadd(b.succ, c); b.rt = wadd(b.rt, rt); if (rt < b.min_rt) b.min_rt = rt;   // MetricBucket.addRT :129-136
+        });
+        Bucket* m = min_current(now);
+        m->succ = wadd(m->succ, c); m->rt = wadd(m->rt, rt); if (rt < m->min_rt) m->min_rt = rt;
+    }
+    SF_HD void add_occupied_pass(int64_t now, int32_t c) {                                   // :343-346
+        Bucket* m = min_current(now); m->occ = wadd(m->occ, c);
+        m = min_current(now); m->pass = wadd(m->pass, c);
+    }
+    // tryOccupyNext :295-330 (IntervalProperty / SampleCountProperty statics)
+    SF_HD int64_t try_occupy_next(int64_t now, int32_t c, double threshold, int32_t occupy_timeout) {
+        double max_count = threshold * interval / 1000;
+        int64_t current_borrow = current_waiting(now);
+        if ((double)current_borrow >= max_count) return occupy_timeout;
+        int32_t window_length = interval / S;
+        int64_t earliest = now - now % window_length + window_length - interval;
+        int idx = 0;
+        int64_t current_pass = sec_sum_pass(now);
+        while (earliest < now) {
+            int64_t wait = (int64_t)(idx * window_length + window_length) - now % window_length;
+            if (wait >= occupy_timeout) break;
+            int64_t window_pass = sec_window_pass(earliest);
+            if ((double)(current_pass + current_borrow + c - window_pass) <= max_count) return wait;
+            earliest += window_length;
+            current_pass -= window_pass;
+            idx++;
+        }
+        return occupy_timeout;
+    }
+};
+
+// ============================================================ controllers
+// WarmUpController.syncToken :178-197 + coolDownTokens :217-232
+SF_HD void warm_sync(const DevRule& r, DevRuleState& s, int64_t now, int64_t pass_qps) {
+    int64_t current_time = now - now % 1000;
+    if (current_time <= s.last_filled) return;
+    int64_t old_value = s.stored_tokens, new_value = old_value;
+    if (old_value < r.warning_token) {
+        new_value = j_d2l((double)old_value + (double)(current_time - s.last_filled) * r.count / 1000);
+    } else if (old_value > r.warning_token) {
+        if (pass_qps < j_d2i(r.count) / r.cold_factor)
+            new_value = j_d2l((double)old_value + (double)(current_time - s.last_filled) * r.count / 1000);
+    }
+    if (new_value > r.max_token) new_value = r.max_token;
+    s.stored_tokens = wsub(new_value, pass_qps);
+    if (s.stored_tokens < 0) s.stored_tokens = 0;
+    s.last_filled = current_time;
+}
+
+// canPass: returns 1 pass / 0 block; *prio_wait set on PriorityWaitException.
+template <int MAXS>
+SF_HD int can_pass(const DevRule& r, DevRuleState& s, NodeWin<MAXS>& nd, int64_t now, int32_t acq,
+                   bool prio, int32_t occupy_timeout, int64_t* wait, bool* prio_wait) {
+    switch (r.kind) {
+    case CT_DEFAULT: {                                             // DefaultController.java:50-89
+        int32_t cur = r.grade == SF_GRADE_THREAD ? (int32_t)nd.threads : j_d2i(nd.pass_qps(now));
+        if ((double)(int32_t)((uint32_t)cur + (uint32_t)acq) > r.count) {
+            if (prio && r.grade == SF_GRADE_QPS) {
+                int64_t w = nd.try_occupy_next(now, acq, r.count, occupy_timeout);
+                if (w < occupy_timeout) {
+                    nd.add_waiting(now + w, acq);
+                    nd.add_occupied_pass(now, acq);
+                    *wait = w; *prio_wait = true;
+                    return 1;
+                }
+            }
+            return 0;
+        }
+        return 1;
+    }
+    case CT_WARM_UP: {                                             // WarmUpController.java:147-175
+        int64_t pass_qps = j_d2l(nd.pass_qps(now));
+        int64_t previous_qps = j_d2l(nd.previous_pass_qps(now));
+        warm_sync(r, s, now, previous_qps);
+        int64_t rest = s.stored_tokens;
+        if (rest >= r.warning_token) {
+            int64_t above = rest - r.warning_token;
+            double warning_qps = j_next_up(1.0 / ((double)above * r.slope + 1.0 / r.count));
+            return (double)(pass_qps + acq) <= warning_qps;
+        }
+        return (double)(pass_qps + acq) <= r.count;
+    }
+    case CT_RATE_LIMITER:                                          // RateLimiterController.java:48-102
+    case CT_WARM_UP_RATE_LIMITER: {                                // WarmUpRateLimiterController.java:43-87
+        int64_t cost;
+        if (r.kind == CT_RATE_LIMITER) {
+            if (acq <= 0) return 1;
+            if (r.count <= 0) return 0;
+            cost = j_round(1.0 * acq / r.count * 1000);
+        } else {
+            int64_t previous_qps = j_d2l(nd.previous_pass_qps(now));
+            warm_sync(r, s, now, previous_qps);
+            int64_t rest = s.stored_tokens;
+            if (rest >= r.warning_token) {
+                int64_t above = rest - r.warning_token;
+                double warming_qps = j_next_up(1.0 / ((double)above * r.slope + 1.0 / r.count));
+                cost = j_round(1.0 * acq / warming_qps * 1000);
+            } else {
+                cost = j_round(1.0 * acq / r.count * 1000);
+            }
+        }
+        int64_t expected = cost + s.latest_passed;
+        if (expected <= now) { s.latest_passed = now; return 1; }
+        int64_t w = cost + s.latest_passed - now;
+        if (w > r.max_queue_ms) return 0;
+        s.latest_passed += cost;
+        w = s.latest_passed - now;
+        if (w > r.max_queue_ms) { s.latest_passed -= cost; return 0; }
+        if (w > 0) *wait = w;
+        return 1;
+    }
+    }
+    return 1;
+}
+
+// ============================================================ param table
+struct ParamTable {
+    ParamSlot* slots; uint64_t mask; int32_t* err;
+    SF_HD static uint64_t hash(uint64_t hi, uint64_t lo) { return mix64(hi ^ mix64(lo + 0x9e3779b97f4a7c15ULL)); }
+    // find slot of key; returns nullptr if absent
+    SF_HD ParamSlot* find(uint64_t hi, uint64_t lo) const {
+        uint64_t i = hash(hi, lo) & mask;
+        for (uint64_t probe = 0; probe <= mask; probe++) {
+#ifdef __HIP_DEVICE_COMPILE__
+            uint64_t h = __hip_atomic_load(&slots[i].hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+            uint64_t h = slots[i].hi;
+#endif
+            if (h == 0) return nullptr;
+            if (h == hi && slots[i].lo == lo) return &slots[i];
+            i = (i + 1) & mask;
+        }
+        return nullptr;
+    }
+    // insert a key known to be absent (only the owning lane ever inserts a given key)
+    SF_HD ParamSlot* insert(uint64_t hi, uint64_t lo) const {
+        uint64_t i = hash(hi, lo) & mask;
+        for (uint64_t probe = 0; probe <= mask; probe++) {
+#ifdef __HIP_DEVICE_COMPILE__
+            unsigned long long expected = 0;
+            if (__hip_atomic_compare_exchange_strong((unsigned long long*)&slots[i].hi, &expected,
+                    (unsigned long long)hi, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                slots[i].lo = lo; slots[i].a = 0; slots[i].b = 0;
+                return &slots[i];
+            }
+#else
+            if (slots[i].hi == 0) { slots[i].hi = hi; slots[i].lo = lo; slots[i].a = 0; slots[i].b = 0; return &slots[i]; }
+#endif
+            i = (i + 1) & mask;
+        }
+        *err = SF_ERR_CAPACITY;
+        return nullptr;
+    }
+};
+SF_HD uint64_t pkey_hi(uint32_t res, uint64_t kind, uint32_t idx, uint32_t tag) {
+    return ((uint64_t)(res + 1u) << 32) | (kind << 24) | ((uint64_t)(idx & 0xffff) << 8) | (tag & 0xff);
+}
+
+// ParameterMetric.addThreadCount / decreaseThreadCount for one value (:184-239, :125-181)
+SF_HD void pm_thread_add(const ParamTable& pt, uint32_t res, int idx, uint32_t tag, uint64_t bits, int delta) {
+    if (tag == SF_TAG_NULL) return;
+    uint64_t hi = pkey_hi(res, PK_THREAD, (uint32_t)idx, tag);
+    ParamSlot* s = pt.find(hi, bits);
+    if (delta > 0) {
+        if (!s) { s = pt.insert(hi, bits); if (s) s->a = 1; }
+        else s->a = (int32_t)((uint32_t)s->a + 1u);
+    } else {
+        if (!s) { pt.insert(hi, bits); return; }              // putIfAbsent(new AtomicInteger())
+        int32_t cur = (int32_t)((uint32_t)s->a - 1u);
+        s->a = cur <= 0 ? 0 : cur;                            // remove at <= 0 == reads as 0
+    }
+}
+SF_HD int64_t pm_thread_get(const ParamTable& pt, uint32_t res, int idx, uint32_t tag, uint64_t bits) {
+    ParamSlot* s = pt.find(pkey_hi(res, PK_THREAD, (uint32_t)idx, tag), bits);
+    return s ? s->a : 0;
+}
+
+// ParamFlowChecker.passSingleValueCheck :114-137 (+ default :139-219, throttle :222-273)
+SF_HD int param_pass_single(const ParamTable& pt, uint32_t res, int rule_k, const DevParamRule& r,
+                            const DevHotItem* items, int64_t now, int32_t acq, uint32_t tag, uint64_t bits,
+                            int64_t* wait) {
+    int64_t token_count = j_d2l(r.count);
+    bool hot = false; int32_t hot_count = 0;
+    for (int k = 0; k < r.item_cnt; k++) {
+        const DevHotItem& it = items[r.item_off + k];
+        if (it.tag == tag && it.bits == bits) { hot = true; hot_count = it.count; break; }
+    }
+    if (r.grade == SF_GRADE_QPS) {
+        if (hot) token_count = hot_count;
+        if (token_count == 0) return 0;
+        uint64_t hi = pkey_hi(res, PK_RULE, (uint32_t)rule_k, tag);
+        if (r.behavior == SF_BEHAVIOR_RATE_LIMITER) {
+            int64_t cost = j_round(1.0 * 1000 * acq * (double)r.duration_sec / (double)token_count);
+            ParamSlot* s = pt.find(hi, bits);
+            if (!s) { s = pt.insert(hi, bits); if (s) s->a = now; return 1; }
+            int64_t last = s->a, expected = last + cost;
+            if (expected <= now || expected - now < r.max_queue_ms) {
+                s->a = now;
+                int64_t w = expected - now;
+                if (w > 0) { s->a = expected; *wait = w; }
+                return 1;
+            }
+            return 0;
+        }
+        int64_t max_count = wadd(token_count, r.burst);
+        if (acq > max_count) return 0;
+        ParamSlot* s = pt.find(hi, bits);
+        if (!s) {                                          // first sight :165-169
+            s = pt.insert(hi, bits);
+            if (s) { s->a = now; s->b = max_count - acq; }
+            return 1;
+        }
+        int64_t pass_time = now - s->a;
+        if (pass_time > wmul(r.duration_sec, 1000)) {      // refill :173-195
+            int64_t rest = s->b;
+            int64_t to_add = jdiv(wmul(pass_time, token_count), wmul(r.duration_sec, 1000));
+            int64_t new_qps = wadd(to_add, rest) > max_count ? (max_count - acq) : wsub(wadd(rest, to_add), acq);
+            if (new_qps < 0) return 0;
+            s->b = new_qps; s->a = now;
+            return 1;
+        }
+        if (s->b - acq >= 0) { s->b -= acq; return 1; }    // :196-215
+        return 0;
+    } else if (r.grade == SF_GRADE_THREAD) {
+        int64_t thread_count = pm_thread_get(pt, res, r.param_idx, tag, bits);
+        if (hot) return ++thread_count <= hot_count;
+        return ++thread_count <= token_count;
+    }
+    return 1;
+}
+
+// ============================================================ the segment
+struct SegIO {          // sorted-order batch arrays
+    const int64_t* ts; const int32_t* cnt; const uint8_t* flags;
+    const int64_t* eref; const int64_t* cts;
+    uint32_t arg_slots; const uint8_t* nargs; const uint8_t* atag; const uint64_t* abits; uint32_t n;
+    uint8_t* v_status; int32_t* v_wait; uint16_t* v_rule;
+};
+
+SF_HD bool v_blocked(uint8_t v) { return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM; }
+
+template <int MAXS>
+SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi) {
+    NodeWin<MAXS> nd;
+    nd.S = st.S; nd.wl = st.wl; nd.interval = st.interval; nd.max_rt = st.max_rt;
+    nd.interval_sec = st.interval / 1000.0;
+    for (int i = 0; i < MAXS; i++) {
+        if (i < st.S) { nd.sec[i] = st.second[(size_t)res * st.S + i]; nd.bor[i] = st.borrow[(size_t)res * st.S + i]; }
+        else { nd.sec[i] = fresh_bucket(WS_NONE, st.max_rt); nd.bor[i].ws = WS_NONE; nd.bor[i].pass = 0; }
+    }
+    nd.threads = st.threads[res];
+    nd.gmin = st.minute + (size_t)res * MINUTE;
+    nd.mi = -1; nd.mdirty = 0;
+    nd.mb = fresh_bucket(WS_NONE, st.max_rt);
+
+    const uint32_t r0 = st.rule_off[res], r1 = st.rule_off[res + 1];
+    const int nrules = (int)(r1 - r0);
+    DevRuleState rs[MAX_RULES];
+    for (int k = 0; k < MAX_RULES; k++) if (k < nrules) rs[k] = st.rstate[r0 + k];
+    const uint32_t p0 = st.prule_off[res], p1 = st.prule_off[res + 1];
+    const int nprules = (int)(p1 - p0);
+    uint8_t pm_init = nprules ? st.pm_init[res] : 0;
+    bool pm_exists = pm_init != 0;
+    ParamTable pt{st.ptab, st.pcap_mask, st.err};
+
+    for (uint32_t j = lo; j < hi; j++) {
+        const int64_t now = io.ts[j];
+        const int32_t c = io.cnt[j];
+        const uint8_t fl = io.flags[j];
+        const uint32_t na = io.arg_slots ? (io.nargs ? io.nargs[j] : io.arg_slots) : 0;
+        uint8_t status; int64_t wait = 0; int rule_idx = 0;
+
+        if (fl & SF_EV_EXIT) {                                  // StatisticSlot.exit :134-165
+            int64_t ref = io.eref ? io.eref[j] : -1;
+            bool blocked; int64_t create_ts;
+            if (ref >= 0) {
+                if (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT)) {   // entry of another resource / order
+                    *st.err = SF_ERR_INVALID;
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(SF_HOST_DEBUG)
+                    printf("bad ref j=%u ref=%lld lo=%u flags=%d\n", j, (long long)ref, lo, ref>=0? io.flags[ref]:-1);
+#endif
+                    ref = j;   // treat as this exit's own slot: reads as not blocked below
+                }
+                blocked = ref == (int64_t)j ? true : v_blocked(io.v_status[ref]);
+                create_ts = io.ts[ref];
+            }
+            else { blocked = false; create_ts = io.cts ? io.cts[j] : now; }
+            if (!blocked) {
+                int64_t rt = now - create_ts;
+                nd.add_rt_success(now, rt, c);                  // recordCompleteFor :167-178
+                nd.threads--;
+                if (fl & SF_EV_ERROR) nd.add_exception(now, c);
+                if (pm_exists)                                  // ParamFlowStatisticExitCallback
+                    for (uint32_t a = 0; a < na; a++)
+                        if (a < 8 && (pm_init >> a) & 1)
+                            pm_thread_add(pt, res, (int)a, io.atag[(size_t)a * io.n + j], io.abits[(size_t)a * io.n + j], -1);
+                status = SF_V_EXIT;
+            } else {
+                status = SF_V_EXIT_IGNORED;
+            }
+            io.v_status[j] = status;
+            if (io.v_wait) io.v_wait[j] = 0;
+            if (io.v_rule) io.v_rule[j] = 0;
+            continue;
+        }
+
+        bool blocked = false, prio_wait = false;
+        status = SF_V_PASS;
+        // ParamFlowSlot.checkFlow :82-103
+        if (nprules) {
+            pm_exists = true;
+            for (int k = 0; k < nprules && !blocked; k++) {
+                DevParamRule& pr = st.prules[p0 + k];
+                if (pr.param_idx < 0) {                          // applyRealParamIdx :56-66
+                    if (-pr.param_idx <= (int)na) pr.param_idx = (int)na + pr.param_idx;
+                    else pr.param_idx = -pr.param_idx;
+                }
+                if (pr.param_idx < 8) pm_init |= (uint8_t)(1u << pr.param_idx);   // initParamMetricsFor
+                if ((int)na <= pr.param_idx) continue;             // passCheck :53-56
+                uint32_t tg = io.atag[(size_t)pr.param_idx * io.n + j];
+                uint64_t bt = io.abits[(size_t)pr.param_idx * io.n + j];
+                if (tg == SF_TAG_NULL) continue;
+                int64_t w = 0;
+                if (!param_pass_single(pt, res, k, pr, st.items, now, c, tg, bt, &w)) {
+                    blocked = true; status = SF_V_BLOCK_PARAM; rule_idx = k;
+                } else if (w > 0) {
+                    wait += w;
+                }
+            }
+        }
+        // FlowSlot -> FlowRuleChecker.checkFlow :44-59
+        if (!blocked) {
+            for (int k = 0; k < nrules; k++) {
+                int64_t w = 0; bool pw = false;
+                int ok = can_pass<MAXS>(st.rules[r0 + k], rs[k], nd, now, c, (fl & SF_EV_PRIO) != 0,
+                                        st.occupy_timeout, &w, &pw);
+                if (pw) { prio_wait = true; wait += w; rule_idx = k; break; }
+                if (!ok) { blocked = true; status = SF_V_BLOCK_FLOW; rule_idx = k; break; }
+                wait += w;
+            }
+        }
+        // StatisticSlot.entry accounting :64-123
+        if (blocked) {
+            nd.add_block(now, c);
+        } else {
+            nd.threads++;
+            if (prio_wait) status = SF_V_PRIORITY_WAIT;
+            else { nd.add_pass(now, c); status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS; }
+            if (pm_exists)
+                for (uint32_t a = 0; a < na; a++)
+                    if (a < 8 && (pm_init >> a) & 1)
+                        pm_thread_add(pt, res, (int)a, io.atag[(size_t)a * io.n + j], io.abits[(size_t)a * io.n + j], +1);
+        }
+        io.v_status[j] = status;
+        if (io.v_wait) io.v_wait[j] = (int32_t)wait;
+        if (io.v_rule) io.v_rule[j] = (uint16_t)rule_idx;
+    }
+
+    // write back
+    for (int i = 0; i < MAXS; i++)
+        if (i < st.S) { st.second[(size_t)res * st.S + i] = nd.sec[i]; st.borrow[(size_t)res * st.S + i] = nd.bor[i]; }
+    nd.min_flush();
+    st.threads[res] = nd.threads;
+    for (int k = 0; k < MAX_RULES; k++) if (k < nrules) st.rstate[r0 + k] = rs[k];
+    if (nprules) st.pm_init[res] = pm_init;
+}
+
+// ============================================================ rule tables (host side)
+// FlowRuleUtil.isValidRule (FlowRuleUtil.java:170-185) + checkControlBehaviorField (:233-246)
+inline bool valid_flow_rule(const sf_flow_rule& r) {
+    if (!(r.count >= 0) || r.grade < 0 || r.strategy < 0 || r.control_behavior < 0) return false;
+    if (r.grade == SF_GRADE_QPS) {
+        switch (r.control_behavior) {
+        case SF_BEHAVIOR_WARM_UP: return r.warm_up_period_sec > 0;
+        case SF_BEHAVIOR_RATE_LIMITER: return r.max_queueing_time_ms > 0;
+        case SF_BEHAVIOR_WARM_UP_RATE_LIMITER: return r.warm_up_period_sec > 0 && r.max_queueing_time_ms > 0;
+        default: return true;
+        }
+    }
+    return r.grade == SF_GRADE_THREAD;
+}
+// FlowRuleUtil.generateRater (:132-152) + WarmUpController.construct (WarmUpController.java:113-139)
+inline DevRule make_dev_rule(const sf_flow_rule& r, int cold_factor, int host_index) {
+    DevRule d{};
+    d.grade = r.grade; d.count = r.count; d.max_queue_ms = r.max_queueing_time_ms;
+    d.cold_factor = cold_factor; d.host_index = host_index;
+    d.kind = CT_DEFAULT;
+    if (r.grade == SF_GRADE_QPS) {
+        if (r.control_behavior == SF_BEHAVIOR_WARM_UP) d.kind = CT_WARM_UP;
+        else if (r.control_behavior == SF_BEHAVIOR_RATE_LIMITER) d.kind = CT_RATE_LIMITER;
+        else if (r.control_behavior == SF_BEHAVIOR_WARM_UP_RATE_LIMITER) d.kind = CT_WARM_UP_RATE_LIMITER;
+    }
+    if (d.kind == CT_WARM_UP || d.kind == CT_WARM_UP_RATE_LIMITER) {
+        int period = r.warm_up_period_sec;
+        d.warning_token = j_d2i(period * r.count) / (cold_factor - 1);
+        d.max_token = d.warning_token + j_d2i(2 * period * r.count / (1.0 + cold_factor));
+        d.slope = (cold_factor - 1.0) / r.count / (double)(d.max_token - d.warning_token);
+    }
+    return d;
+}
+inline DevRuleState fresh_rule_state() {     // AtomicLong(0), AtomicLong(0), AtomicLong(-1)
+    DevRuleState s{}; s.stored_tokens = 0; s.last_filled = 0; s.latest_passed = -1; return s;
+}
+inline DevParamRule make_dev_param_rule(const sf_param_rule& r, int host_index) {
+    DevParamRule d{};
+    d.grade = r.grade; d.param_idx = r.param_idx; d.behavior = r.control_behavior;
+    d.max_queue_ms = r.max_queueing_time_ms; d.count = r.count; d.duration_sec = r.duration_in_sec;
+    d.burst = r.burst_count; d.item_off = (int32_t)r.item_offset; d.item_cnt = (int32_t)r.item_count;
+    d.host_index = host_index;
+    return d;
+}
+
+}  // namespace sf

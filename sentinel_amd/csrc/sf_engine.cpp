@@ -1,0 +1,464 @@
+// sf_engine.cpp — host runtime behind the C-ABI (include/sentinel_flow.h).
+//
+// Owns one GPU's shard of resource state in HBM, the rule tables, the batch
+// working buffers and one HIP stream.  sf_submit is serialised by a mutex
+// (the Java shim batches from many threads into one flusher).
+// There is no CPU fallback: without a usable gfx950 device sf_create fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sf_decide.h"
+
+using namespace sf;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t _e = (expr);                                                         \
+        if (_e != hipSuccess)                                                           \
+            return fail(_e == hipErrorOutOfMemory ? SF_ERR_NOMEM : SF_ERR_DEVICE,       \
+                        std::string(#expr ": ") + hipGetErrorString(_e));               \
+    } while (0)
+
+struct sf_engine {
+    sf_config cfg{};
+    hipStream_t stream = nullptr;
+    uint32_t R = 0, key_bits = 1;
+    DevState st{};
+    Work w{};
+    // rules
+    std::vector<uint32_t> flow_pos;        // loaded valid rule index -> CSR position
+    uint32_t n_flow = 0, n_prule = 0;
+    // staging for host-memory batches
+    void* stage_in = nullptr; size_t stage_in_bytes = 0;
+    void* stage_out = nullptr; size_t stage_out_bytes = 0;
+    hipEvent_t ev[5]{};
+    bool timing = false;
+    sf_stats stats{};
+    std::vector<void*> user_allocs;
+    std::mutex mu;
+};
+
+extern "C" {
+
+int sf_abi_version(void) { return SF_ABI_VERSION; }
+const char* sf_last_error(void) { return g_err.c_str(); }
+
+void sf_config_default(sf_config* c) {
+    std::memset(c, 0, sizeof *c);
+    c->sample_count = 2; c->interval_ms = 1000; c->occupy_timeout_ms = 500; c->cold_factor = 3;
+    c->statistic_max_rt = 5000; c->max_resources = 1024; c->max_batch = 1u << 20;
+    c->param_capacity = 1u << 16; c->shard_count = 1; c->shard_index = 0; c->device = 0;
+    c->cluster_sample_count = 10; c->cluster_interval_ms = 1000; c->exceed_count = 1.0;
+    c->max_occupy_ratio = 1.0; c->max_flow_ids = 1024;
+}
+
+static int dalloc(void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return fail(SF_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return SF_OK;
+}
+#define DALLOC(ptr, bytes)                                               \
+    do {                                                                 \
+        int _rc = dalloc((void**)&(ptr), (bytes));                       \
+        if (_rc) { sf_destroy(e); return _rc; }                          \
+    } while (0)
+
+void sf_destroy(sf_engine* e) {
+    if (!e) return;
+    if (e->stream) hipStreamSynchronize(e->stream);
+    void* ptrs[] = {e->st.second, e->st.borrow, e->st.minute, e->st.threads, (void*)e->st.rule_off,
+                    (void*)e->st.rules, e->st.rstate, (void*)e->st.prule_off, e->st.prules, (void*)e->st.items,
+                    e->st.pm_init, e->st.ptab, e->st.err,
+                    e->w.keys_in, e->w.keys_out, e->w.vals_in, e->w.perm, e->w.head, e->w.head_scan,
+                    e->w.seg_start, e->w.seg_res, e->w.n_seg, e->w.s_ts, e->w.s_cnt, e->w.s_flags, e->w.s_eref,
+                    e->w.s_cts, e->w.s_nargs, e->w.s_atag, e->w.s_abits, e->w.inv, e->w.v_status, e->w.v_wait,
+                    e->w.v_rule, e->w.sort_tmp, e->w.scan_tmp, e->stage_in, e->stage_out};
+    for (void* p : ptrs) if (p) hipFree(p);
+    for (void* p : e->user_allocs) hipFree(p);
+    for (auto& x : e->ev) if (x) hipEventDestroy(x);
+    if (e->stream) hipStreamDestroy(e->stream);
+    delete e;
+}
+
+int sf_create(const sf_config* cfg, sf_engine** out) {
+    if (!cfg || !out) return fail(SF_ERR_INVALID, "null argument");
+    *out = nullptr;
+    const sf_config& c = *cfg;
+    if (c.sample_count <= 0 || c.sample_count > SF_MAX_SAMPLE_COUNT || c.interval_ms <= 0 ||
+        c.interval_ms % c.sample_count != 0)
+        return fail(SF_ERR_INVALID, "sample_count/interval_ms invalid (LeapArray.java:70-87)");
+    if (c.max_resources == 0 || c.max_batch == 0) return fail(SF_ERR_INVALID, "max_resources/max_batch must be > 0");
+    if (c.shard_count == 0 || c.shard_index >= c.shard_count) return fail(SF_ERR_INVALID, "bad shard");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(SF_ERR_DEVICE, "no HIP device visible: the engine has no CPU fallback");
+    if (c.device < 0 || c.device >= ndev) return fail(SF_ERR_DEVICE, "device ordinal out of range");
+    HIP_TRY(hipSetDevice(c.device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, c.device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SF_ERR_DEVICE, std::string("engine is built for gfx950, device is ") + prop.gcnArchName);
+
+    sf_engine* e = new sf_engine();
+    e->cfg = c;
+    e->R = c.max_resources;
+    while ((1ull << e->key_bits) < e->R) e->key_bits++;
+    HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    for (auto& x : e->ev) HIP_TRY(hipEventCreate(&x));
+
+    DevState& st = e->st;
+    st.S = c.sample_count; st.wl = c.interval_ms / c.sample_count; st.interval = c.interval_ms;
+    st.occupy_timeout = c.occupy_timeout_ms; st.max_rt = c.statistic_max_rt; st.R = e->R;
+    const size_t R = e->R, S = c.sample_count;
+    DALLOC(st.second, R * S * sizeof(Bucket));
+    DALLOC(st.borrow, R * S * sizeof(Borrow));
+    DALLOC(st.minute, R * MINUTE * sizeof(Bucket));
+    DALLOC(st.threads, R * sizeof(int64_t));
+    DALLOC(st.rule_off, (R + 1) * sizeof(uint32_t));
+    DALLOC(st.prule_off, (R + 1) * sizeof(uint32_t));
+    DALLOC(st.pm_init, R);
+    DALLOC(st.err, sizeof(int32_t));
+    uint64_t pcap = 16;
+    while (pcap < (uint64_t)c.param_capacity) pcap <<= 1;
+    DALLOC(st.ptab, pcap * sizeof(ParamSlot));
+    st.pcap_mask = pcap - 1;
+    HIP_TRY(hipMemsetAsync((void*)st.rule_off, 0, (R + 1) * sizeof(uint32_t), e->stream));
+    HIP_TRY(hipMemsetAsync((void*)st.prule_off, 0, (R + 1) * sizeof(uint32_t), e->stream));
+    HIP_TRY(hipMemsetAsync(st.pm_init, 0, R, e->stream));
+    HIP_TRY(hipMemsetAsync(st.ptab, 0, pcap * sizeof(ParamSlot), e->stream));
+    HIP_TRY(hipMemsetAsync(st.err, 0, sizeof(int32_t), e->stream));
+    HIP_TRY(launch_init_state(st, e->stream));
+
+    Work& w = e->w;
+    const size_t N = c.max_batch;
+    DALLOC(w.keys_in, N * 4); DALLOC(w.keys_out, N * 4); DALLOC(w.vals_in, N * 4); DALLOC(w.perm, N * 4);
+    DALLOC(w.head, N * 4); DALLOC(w.head_scan, N * 4);
+    DALLOC(w.seg_start, (N + 1) * 4); DALLOC(w.seg_res, N * 4); DALLOC(w.n_seg, 4);
+    DALLOC(w.s_ts, N * 8); DALLOC(w.s_cnt, N * 4); DALLOC(w.s_flags, N);
+    DALLOC(w.s_eref, N * 8); DALLOC(w.s_cts, N * 8); DALLOC(w.inv, N * 4);
+    DALLOC(w.s_nargs, N); DALLOC(w.s_atag, N * SF_MAX_ARGS); DALLOC(w.s_abits, N * SF_MAX_ARGS * 8);
+    DALLOC(w.v_status, N); DALLOC(w.v_wait, N * 4); DALLOC(w.v_rule, N * 2);
+    HIP_TRY(query_temp_bytes((uint32_t)N, e->key_bits, &w.sort_tmp_bytes, &w.scan_tmp_bytes));
+    DALLOC(w.sort_tmp, w.sort_tmp_bytes);
+    DALLOC(w.scan_tmp, w.scan_tmp_bytes);
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    *out = e;
+    return SF_OK;
+}
+
+static int local_of(const sf_engine* e, uint32_t res, uint32_t* l) {
+    if (res % e->cfg.shard_count != e->cfg.shard_index) return 0;
+    *l = res / e->cfg.shard_count;
+    return *l < e->R;
+}
+
+int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
+    if (!e || (n && !rules)) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    std::vector<uint32_t> counts(e->R + 1, 0);
+    std::vector<const sf_flow_rule*> valid;
+    std::vector<uint32_t> valid_local;
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t l;
+        if (!local_of(e, rules[i].resource, &l)) return fail(SF_ERR_INVALID, "rule resource outside this shard");
+        if (!valid_flow_rule(rules[i])) continue;
+        if (rules[i].strategy != SF_STRATEGY_DIRECT || rules[i].cluster_mode)
+            return fail(SF_ERR_UNSUPPORTED, "only DIRECT, non-cluster flow rules run in the engine");
+        if (rules[i].control_behavior != SF_BEHAVIOR_DEFAULT && rules[i].grade == SF_GRADE_QPS &&
+            e->cfg.cold_factor <= 1 &&
+            (rules[i].control_behavior == SF_BEHAVIOR_WARM_UP || rules[i].control_behavior == SF_BEHAVIOR_WARM_UP_RATE_LIMITER))
+            return fail(SF_ERR_INVALID, "Cold factor should be larger than 1 (WarmUpController.java:114-116)");
+        if (++counts[l] > SF_MAX_RULES_PER_RESOURCE)
+            return fail(SF_ERR_UNSUPPORTED, "more than SF_MAX_RULES_PER_RESOURCE rules on one resource");
+        valid.push_back(&rules[i]);
+        valid_local.push_back(l);
+    }
+    std::vector<uint32_t> off(e->R + 1, 0);
+    for (uint32_t r = 0; r < e->R; r++) off[r + 1] = off[r] + counts[r];
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    std::vector<DevRule> dr(valid.size());
+    std::vector<DevRuleState> ds(valid.size());
+    e->flow_pos.assign(valid.size(), 0);
+    for (size_t k = 0; k < valid.size(); k++) {
+        const sf_flow_rule& r = *valid[k];
+        uint32_t pos = fill[valid_local[k]]++;
+        e->flow_pos[k] = pos;
+        DevRule d = make_dev_rule(r, e->cfg.cold_factor, (int32_t)k);
+        dr[pos] = d;
+        ds[pos] = fresh_rule_state();
+    }
+    e->n_flow = (uint32_t)valid.size();
+    if (e->st.rules) { hipFree((void*)e->st.rules); e->st.rules = nullptr; }
+    if (e->st.rstate) { hipFree(e->st.rstate); e->st.rstate = nullptr; }
+    HIP_TRY(hipMalloc((void**)&e->st.rules, std::max<size_t>(1, dr.size()) * sizeof(DevRule)));
+    HIP_TRY(hipMalloc((void**)&e->st.rstate, std::max<size_t>(1, ds.size()) * sizeof(DevRuleState)));
+    if (!dr.empty()) {
+        HIP_TRY(hipMemcpyAsync((void*)e->st.rules, dr.data(), dr.size() * sizeof(DevRule), hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(hipMemcpyAsync(e->st.rstate, ds.data(), ds.size() * sizeof(DevRuleState), hipMemcpyHostToDevice, e->stream));
+    }
+    HIP_TRY(hipMemcpyAsync((void*)e->st.rule_off, off.data(), off.size() * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return SF_OK;
+}
+
+int sf_load_param_rules(sf_engine* e, const sf_param_rule* rules, uint32_t n, const sf_hot_item* items,
+                        uint32_t n_items) {
+    if (!e || (n && !rules) || (n_items && !items)) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    std::vector<uint32_t> counts(e->R + 1, 0), loc(n);
+    for (uint32_t i = 0; i < n; i++) {
+        if (!local_of(e, rules[i].resource, &loc[i])) return fail(SF_ERR_INVALID, "rule resource outside this shard");
+        if ((uint64_t)rules[i].item_offset + rules[i].item_count > n_items) return fail(SF_ERR_INVALID, "hot item range");
+        if (++counts[loc[i]] > SF_MAX_RULES_PER_RESOURCE)
+            return fail(SF_ERR_UNSUPPORTED, "more than SF_MAX_RULES_PER_RESOURCE param rules on one resource");
+    }
+    std::vector<uint32_t> off(e->R + 1, 0);
+    for (uint32_t r = 0; r < e->R; r++) off[r + 1] = off[r] + counts[r];
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    std::vector<DevParamRule> dp(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const sf_param_rule& r = rules[i];
+        DevParamRule d = make_dev_param_rule(r, (int32_t)i);
+        dp[fill[loc[i]]++] = d;
+    }
+    std::vector<DevHotItem> di(n_items);
+    for (uint32_t i = 0; i < n_items; i++) { di[i].bits = items[i].bits; di[i].count = items[i].count; di[i].tag = items[i].tag; }
+    e->n_prule = n;
+    if (e->st.prules) { hipFree(e->st.prules); e->st.prules = nullptr; }
+    if (e->st.items) { hipFree((void*)e->st.items); e->st.items = nullptr; }
+    HIP_TRY(hipMalloc((void**)&e->st.prules, std::max<size_t>(1, dp.size()) * sizeof(DevParamRule)));
+    HIP_TRY(hipMalloc((void**)&e->st.items, std::max<size_t>(1, di.size()) * sizeof(DevHotItem)));
+    if (n) HIP_TRY(hipMemcpyAsync(e->st.prules, dp.data(), dp.size() * sizeof(DevParamRule), hipMemcpyHostToDevice, e->stream));
+    if (n_items) HIP_TRY(hipMemcpyAsync((void*)e->st.items, di.data(), di.size() * sizeof(DevHotItem), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync((void*)e->st.prule_off, off.data(), off.size() * 4, hipMemcpyHostToDevice, e->stream));
+    // a rule reload drops all ParameterMetric state (new ParameterMetric per resource)
+    HIP_TRY(hipMemsetAsync(e->st.pm_init, 0, e->R, e->stream));
+    HIP_TRY(hipMemsetAsync(e->st.ptab, 0, (e->st.pcap_mask + 1) * sizeof(ParamSlot), e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return SF_OK;
+}
+
+int sf_load_system_rules(sf_engine* e, const sf_system_rule* rules, uint32_t n) {
+    if (!e) return fail(SF_ERR_INVALID, "null engine");
+    (void)rules;
+    if (n) return fail(SF_ERR_UNSUPPORTED, "SystemRule (global ENTRY_NODE coupling) is not on the GPU path yet");
+    return SF_OK;
+}
+int sf_set_system_status(sf_engine* e, double, double) { return e ? SF_OK : SF_ERR_INVALID; }
+
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
+    if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
+    if (in->n == 0) return SF_OK;
+    if (!in->res_id || !in->ts_ms || !in->count || !in->flags) return fail(SF_ERR_INVALID, "missing event array");
+    if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
+    if (in->arg_slots > SF_MAX_ARGS || (in->arg_slots && (!in->arg_tag || !in->arg_bits)))
+        return fail(SF_ERR_INVALID, "bad arg arrays");
+    std::lock_guard<std::mutex> lk(e->mu);
+    const uint32_t n = in->n;
+    DevBatch b{};
+    b.n = n; b.arg_slots = in->arg_slots;
+    hipStream_t s = e->stream;
+    if (in->mem == SF_MEM_HOST) {
+        size_t need = 0;
+        size_t o_res = need; need += align_up((size_t)n * 4);
+        size_t o_ts = need; need += align_up((size_t)n * 8);
+        size_t o_cnt = need; need += align_up((size_t)n * 4);
+        size_t o_fl = need; need += align_up((size_t)n);
+        size_t o_er = need; need += in->entry_ref ? align_up((size_t)n * 8) : 0;
+        size_t o_ct = need; need += (in->entry_ref && in->create_ts) ? align_up((size_t)n * 8) : 0;
+        size_t o_na = need; need += in->n_args ? align_up((size_t)n) : 0;
+        size_t o_at = need; need += align_up((size_t)n * in->arg_slots);
+        size_t o_ab = need; need += align_up((size_t)n * in->arg_slots * 8);
+        if (need > e->stage_in_bytes) {
+            if (e->stage_in) hipFree(e->stage_in);
+            e->stage_in = nullptr;
+            HIP_TRY(hipMalloc(&e->stage_in, need));
+            e->stage_in_bytes = need;
+        }
+        char* base = (char*)e->stage_in;
+        auto up = [&](size_t off, const void* src, size_t bytes) -> const void* {
+            if (!src || !bytes) return nullptr;
+            hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, s);
+            return base + off;
+        };
+        b.res = (const uint32_t*)up(o_res, in->res_id, (size_t)n * 4);
+        b.ts = (const int64_t*)up(o_ts, in->ts_ms, (size_t)n * 8);
+        b.cnt = (const int32_t*)up(o_cnt, in->count, (size_t)n * 4);
+        b.flags = (const uint8_t*)up(o_fl, in->flags, n);
+        b.eref = (const int64_t*)up(o_er, in->entry_ref, in->entry_ref ? (size_t)n * 8 : 0);
+        b.cts = (const int64_t*)up(o_ct, in->entry_ref ? in->create_ts : nullptr, (size_t)n * 8);
+        b.nargs = (const uint8_t*)up(o_na, in->n_args, n);
+        b.atag = (const uint8_t*)up(o_at, in->arg_tag, (size_t)n * in->arg_slots);
+        b.abits = (const uint64_t*)up(o_ab, in->arg_bits, (size_t)n * in->arg_slots * 8);
+    } else {
+        b.res = in->res_id; b.ts = in->ts_ms; b.cnt = in->count; b.flags = in->flags;
+        b.eref = in->entry_ref; b.cts = in->entry_ref ? in->create_ts : nullptr;
+        b.nargs = in->n_args; b.atag = in->arg_tag; b.abits = in->arg_bits;
+    }
+    DevVerdicts dv{};
+    if (out->mem == SF_MEM_HOST) {
+        size_t need = align_up((size_t)n) + align_up((size_t)n * 4) + align_up((size_t)n * 2);
+        if (need > e->stage_out_bytes) {
+            if (e->stage_out) hipFree(e->stage_out);
+            e->stage_out = nullptr;
+            HIP_TRY(hipMalloc(&e->stage_out, need));
+            e->stage_out_bytes = need;
+        }
+        char* base = (char*)e->stage_out;
+        dv.status = (uint8_t*)base;
+        dv.wait = out->wait_ms ? (int32_t*)(base + align_up(n)) : nullptr;
+        dv.rule = out->rule_idx ? (uint16_t*)(base + align_up(n) + align_up((size_t)n * 4)) : nullptr;
+    } else {
+        dv.status = out->status; dv.wait = out->wait_ms; dv.rule = out->rule_idx;
+    }
+    HIP_TRY(hipMemsetAsync(e->st.err, 0, sizeof(int32_t), s));
+    hipError_t le = launch_pipeline(e->st, e->w, b, dv, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s,
+                                    e->timing ? e->ev : nullptr);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
+    if (out->mem == SF_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, s));
+        if (dv.wait) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        if (dv.rule) HIP_TRY(hipMemcpyAsync(out->rule_idx, dv.rule, (size_t)n * 2, hipMemcpyDeviceToHost, s));
+    }
+    int32_t err = 0;
+    uint32_t nseg = 0;
+    HIP_TRY(hipMemcpyAsync(&err, e->st.err, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&nseg, e->w.n_seg, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    e->stats.n_events = n;
+    e->stats.n_segments = nseg;
+    e->stats.n_launches++;
+    if (e->timing) {
+        float a = 0, b2 = 0, c = 0, d = 0;
+        hipEventElapsedTime(&a, e->ev[0], e->ev[1]);
+        hipEventElapsedTime(&b2, e->ev[1], e->ev[2]);
+        hipEventElapsedTime(&c, e->ev[2], e->ev[3]);
+        hipEventElapsedTime(&d, e->ev[3], e->ev[4]);
+        e->stats.sort_ms += a + b2;
+        e->stats.decide_ms += c;
+        e->stats.scatter_ms += d;
+        e->stats.total_ms += a + b2 + c + d;
+    }
+    if (err) return fail(err, err == SF_ERR_CAPACITY ? "param table capacity exceeded"
+                                                     : "invalid batch (resource outside shard or bad entry_ref)");
+    return SF_OK;
+}
+
+static void to_abi_bucket(const Bucket& d, sf_bucket* o) {
+    o->window_start = d.ws == WS_NONE ? SF_WS_ABSENT : d.ws;
+    o->pass = d.pass; o->block = d.block; o->exception = d.exc; o->success = d.succ; o->rt = d.rt;
+    o->occupied_pass = d.occ; o->min_rt = d.min_rt;
+    if (d.ws == WS_NONE) { o->pass = o->block = o->exception = o->success = o->rt = o->occupied_pass = o->min_rt = 0; }
+}
+
+int sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    uint32_t l;
+    if (!local_of(e, resource, &l)) return fail(SF_ERR_INVALID, "resource outside this shard");
+    std::lock_guard<std::mutex> lk(e->mu);
+    const int S = e->cfg.sample_count;
+    std::vector<Bucket> sec(S), mins(MINUTE);
+    std::vector<Borrow> bor(S);
+    int64_t th = 0;
+    HIP_TRY(hipMemcpyAsync(sec.data(), e->st.second + (size_t)l * S, S * sizeof(Bucket), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(bor.data(), e->st.borrow + (size_t)l * S, S * sizeof(Borrow), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(mins.data(), e->st.minute + (size_t)l * MINUTE, MINUTE * sizeof(Bucket), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(&th, e->st.threads + l, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    std::memset(out, 0, sizeof *out);
+    for (int i = 0; i < SF_MAX_SAMPLE_COUNT; i++) { out->second[i].window_start = SF_WS_ABSENT; out->borrow_ws[i] = SF_WS_ABSENT; }
+    for (int i = 0; i < S; i++) {
+        to_abi_bucket(sec[i], &out->second[i]);
+        out->borrow_ws[i] = bor[i].ws == WS_NONE ? SF_WS_ABSENT : bor[i].ws;
+        out->borrow_pass[i] = bor[i].ws == WS_NONE ? 0 : bor[i].pass;
+    }
+    for (int i = 0; i < MINUTE; i++) to_abi_bucket(mins[i], &out->minute[i]);
+    out->cur_thread_num = th;
+    return SF_OK;
+}
+
+int sf_read_entry_node(sf_engine* e, sf_node_state*) {
+    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "ENTRY_NODE aggregate not on the GPU path yet");
+}
+
+int sf_read_rule_state(sf_engine* e, uint32_t idx, sf_rule_state* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    if (idx >= e->n_flow) return fail(SF_ERR_INVALID, "rule index");
+    std::lock_guard<std::mutex> lk(e->mu);
+    DevRuleState s{};
+    HIP_TRY(hipMemcpy(&s, e->st.rstate + e->flow_pos[idx], sizeof s, hipMemcpyDeviceToHost));
+    out->stored_tokens = s.stored_tokens; out->last_filled_time = s.last_filled; out->latest_passed_time = s.latest_passed;
+    return SF_OK;
+}
+
+int sf_snapshot(sf_engine* e, int64_t, sf_metric_row*, uint32_t, uint32_t* n_out) {
+    if (n_out) *n_out = 0;
+    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "metric snapshot not on the GPU path yet");
+}
+int sf_load_namespaces(sf_engine* e, const sf_namespace*, uint32_t) {
+    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "token server not on the GPU path yet");
+}
+int sf_load_cluster_rules(sf_engine* e, const sf_cluster_flow_rule*, uint32_t, const sf_cluster_param_rule*,
+                          uint32_t, const sf_hot_item*, uint32_t) {
+    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "token server not on the GPU path yet");
+}
+int sf_request_tokens(sf_engine* e, const sf_token_batch*, sf_token_results*) {
+    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "token server not on the GPU path yet");
+}
+
+int sf_device_alloc(sf_engine* e, size_t bytes, void** ptr) {
+    if (!e || !ptr) return fail(SF_ERR_INVALID, "null argument");
+    HIP_TRY(hipMalloc(ptr, bytes ? bytes : 16));
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->user_allocs.push_back(*ptr);
+    return SF_OK;
+}
+int sf_device_free(sf_engine* e, void* ptr) {
+    if (!e) return fail(SF_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto it = std::find(e->user_allocs.begin(), e->user_allocs.end(), ptr);
+    if (it == e->user_allocs.end()) return fail(SF_ERR_INVALID, "pointer not from sf_device_alloc");
+    e->user_allocs.erase(it);
+    HIP_TRY(hipFree(ptr));
+    return SF_OK;
+}
+int sf_memcpy(sf_engine* e, void* dst, const void* src, size_t bytes, int kind) {
+    if (!e) return fail(SF_ERR_INVALID, "null engine");
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return SF_OK;
+}
+int sf_sync(sf_engine* e) {
+    if (!e) return fail(SF_ERR_INVALID, "null engine");
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return SF_OK;
+}
+int sf_get_stats(sf_engine* e, sf_stats* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    *out = e->stats;
+    return SF_OK;
+}
+int sf_set_timing(sf_engine* e, int enabled) {
+    if (!e) return fail(SF_ERR_INVALID, "null engine");
+    e->timing = enabled != 0;
+    std::memset(&e->stats, 0, sizeof e->stats);
+    return SF_OK;
+}
+
+}  // extern "C"

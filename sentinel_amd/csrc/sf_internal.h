@@ -1,0 +1,113 @@
+// sf_internal.h — device state layout and kernel launch interface of the
+// MI355X flow-check engine (product code; never includes oracle/).
+//
+// HBM layout (per engine = one GPU = one resource shard), SURVEY.md §8(d):
+//   second  [R][S]  Bucket (64 B)  OccupiableBucketLeapArray main buckets
+//   borrow  [R][S]  Borrow (16 B)  FutureBucketLeapArray (only PASS is ever used)
+//   minute  [R][60] Bucket (64 B)  BucketLeapArray(60, 60000)
+//   threads [R]     int64          StatisticNode.curThreadNum
+//   rules   CSR     DevRule + DevRuleState (controller state)
+//   param   open-addressed exact table of 32-B slots (ParameterMetric maps)
+// A bucket slot that Java would hold as null has ws == WS_NONE.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sentinel_flow.h"
+
+namespace sf {
+
+constexpr int64_t WS_NONE = -(1LL << 62);   // "null" WindowWrap slot; far below any time
+constexpr int MINUTE = SF_MINUTE_BUCKETS;   // 60 x 1000 ms (StatisticNode.java:105)
+constexpr int MAX_RULES = SF_MAX_RULES_PER_RESOURCE;
+
+struct Bucket {          // WindowWrap<MetricBucket>: windowStart + MetricBucket (MetricBucket.java:28-142)
+    int64_t ws, pass, block, exc, succ, rt, occ, min_rt;
+};
+struct Borrow {          // WindowWrap<MetricBucket> of FutureBucketLeapArray: only PASS is written
+    int64_t ws, pass;
+};
+
+// Controller kinds (FlowRuleUtil.generateRater, FlowRuleUtil.java:132-152)
+enum : int32_t { CT_DEFAULT = 0, CT_WARM_UP = 1, CT_RATE_LIMITER = 2, CT_WARM_UP_RATE_LIMITER = 3 };
+
+struct DevRule {         // 48 B, constants precomputed at load (WarmUpController.construct :113-139)
+    int32_t kind, grade;
+    double count;
+    int32_t warning_token, max_token;
+    double slope;
+    int32_t cold_factor, max_queue_ms;
+    int32_t host_index, pad;
+};
+struct DevRuleState {    // AtomicLong fields of the controllers
+    int64_t stored_tokens, last_filled, latest_passed, pad;
+};
+
+struct DevParamRule {    // ParamFlowRule (ParamFlowRule.java:45-83)
+    int32_t grade, param_idx, behavior, max_queue_ms;
+    double count;
+    int64_t duration_sec;
+    int32_t burst, item_off, item_cnt, host_index;
+};
+struct DevHotItem { uint64_t bits; int32_t count; uint32_t tag; };
+
+struct ParamSlot {       // exact hash slot: key (hi, lo) -> (a, b)
+    uint64_t hi, lo;     // hi == 0: empty
+    int64_t a, b;
+};
+constexpr uint64_t PK_RULE = 1, PK_THREAD = 2;
+
+// Everything a decision kernel needs, passed by value.
+struct DevState {
+    int32_t S, wl, interval, occupy_timeout;
+    int64_t max_rt;
+    uint32_t R;
+    Bucket* second;
+    Borrow* borrow;
+    Bucket* minute;
+    int64_t* threads;
+    const uint32_t* rule_off;      // [R+1]
+    const DevRule* rules;
+    DevRuleState* rstate;
+    const uint32_t* prule_off;     // [R+1]
+    DevParamRule* prules;          // param_idx is mutated (ParamFlowSlot.applyRealParamIdx)
+    const DevHotItem* items;
+    uint8_t* pm_init;              // [R] bitmask: thread maps created per paramIdx (<8)
+    ParamSlot* ptab;
+    uint64_t pcap_mask;
+    int32_t* err;                  // device error word (capacity, invalid input)
+};
+
+// Sorted-order working buffers of one batch.
+struct Work {
+    uint32_t n;
+    uint32_t* keys_in;   uint32_t* keys_out;     // local resource id
+    uint32_t* vals_in;   uint32_t* perm;         // iota -> stable permutation
+    uint32_t* head;      uint32_t* head_scan;    // segment flags and positions
+    uint32_t* seg_start; uint32_t* seg_res; uint32_t* n_seg;
+    int64_t* s_ts; int32_t* s_cnt; uint8_t* s_flags;
+    int64_t* s_eref; int64_t* s_cts;
+    uint8_t* s_nargs; uint8_t* s_atag; uint64_t* s_abits;  // [slot][n]
+    uint32_t* inv;
+    uint8_t* v_status; int32_t* v_wait; uint16_t* v_rule;
+    void* sort_tmp; size_t sort_tmp_bytes;
+    void* scan_tmp; size_t scan_tmp_bytes;
+};
+
+// Device view of a caller batch (pointers already on device).
+struct DevBatch {
+    uint32_t n;
+    const uint32_t* res; const int64_t* ts; const int32_t* cnt; const uint8_t* flags;
+    const int64_t* eref; const int64_t* cts;
+    uint32_t arg_slots; const uint8_t* nargs; const uint8_t* atag; const uint64_t* abits;
+};
+struct DevVerdicts { uint8_t* status; int32_t* wait; uint16_t* rule; };
+
+// ---- launchers (sf_kernels.hip) ----
+hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes);
+hipError_t launch_init_state(const DevState& st, hipStream_t s);
+hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
+                           uint32_t shard_count, uint32_t shard_index, uint32_t key_bits,
+                           hipStream_t s, hipEvent_t* ev /* 5 events or null */);
+
+}  // namespace sf

@@ -1,0 +1,227 @@
+"""Python binding of the HIP engine (``libsentinel_flow.so``) through its C-ABI.
+
+This is the host-side mirror of the reference's operator interfaces for the
+hot path: ``FlowEngine.submit`` plays ``ProcessorSlot.entry/exit`` for a batch
+of events (StatisticSlot + SystemSlot + ParamFlowSlot + FlowSlot), and
+``FlowEngine.request_tokens`` plays ``TokenService.requestToken``.
+
+There is no CPU fallback: importing works without a GPU (the library links
+the HIP runtime lazily), but ``FlowEngine(...)`` raises ``EngineError`` unless
+a gfx950 device is visible.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsentinel_flow.so")
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"sentinel_flow error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+P = C.c_void_p
+
+
+def _declare(L):
+    def f(name, res, *args):
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = list(args)
+    I, U32 = C.c_int, C.c_uint32
+    f("sf_abi_version", I)
+    f("sf_config_default", None, C.POINTER(abi.sf_config))
+    f("sf_create", I, C.POINTER(abi.sf_config), C.POINTER(P))
+    f("sf_destroy", None, P)
+    f("sf_last_error", C.c_char_p)
+    f("sf_load_flow_rules", I, P, C.POINTER(abi.sf_flow_rule), U32)
+    f("sf_load_param_rules", I, P, C.POINTER(abi.sf_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
+    f("sf_load_system_rules", I, P, C.POINTER(abi.sf_system_rule), U32)
+    f("sf_set_system_status", I, P, C.c_double, C.c_double)
+    f("sf_submit", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
+    f("sf_load_namespaces", I, P, C.POINTER(abi.sf_namespace), U32)
+    f("sf_load_cluster_rules", I, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
+      C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
+    f("sf_request_tokens", I, P, C.POINTER(abi.sf_token_batch), C.POINTER(abi.sf_token_results))
+    f("sf_read_node", I, P, U32, C.POINTER(abi.sf_node_state))
+    f("sf_read_entry_node", I, P, C.POINTER(abi.sf_node_state))
+    f("sf_read_rule_state", I, P, U32, C.POINTER(abi.sf_rule_state))
+    f("sf_snapshot", I, P, C.c_int64, C.POINTER(abi.sf_metric_row), U32, C.POINTER(U32))
+    f("sf_device_alloc", I, P, C.c_size_t, C.POINTER(P))
+    f("sf_device_free", I, P, P)
+    f("sf_memcpy", I, P, P, P, C.c_size_t, I)
+    f("sf_sync", I, P)
+    f("sf_get_stats", I, P, C.POINTER(abi.sf_stats))
+    f("sf_set_timing", I, P, I)
+
+
+def _check(rc):
+    if rc != 0:
+        raise EngineError(rc, lib().sf_last_error().decode(errors="replace"))
+
+
+class DeviceArray:
+    """A device (HBM) buffer owned by an engine, filled from a numpy array."""
+
+    def __init__(self, eng: "FlowEngine", host: np.ndarray):
+        self.eng = eng
+        self.dtype = host.dtype
+        self.shape = host.shape
+        self.nbytes = host.nbytes
+        p = P()
+        _check(lib().sf_device_alloc(eng.h, max(16, self.nbytes), C.byref(p)))
+        self.ptr = p.value
+        if self.nbytes:
+            _check(lib().sf_memcpy(eng.h, self.ptr, host.ctypes.data, self.nbytes, 0))
+
+    @classmethod
+    def empty(cls, eng, shape, dtype):
+        return cls(eng, np.zeros(shape, dtype))
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, self.dtype)
+        if self.nbytes:
+            _check(lib().sf_memcpy(self.eng.h, out.ctypes.data, self.ptr, self.nbytes, 1))
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().sf_device_free(self.eng.h, self.ptr)
+            self.ptr = None
+
+
+class DeviceBatch:
+    """An event batch resident in HBM (inputs already on the GPU)."""
+
+    def __init__(self, eng: "FlowEngine", hb: abi.HostBatch):
+        self.n = hb.n
+        self.arrays = {k: DeviceArray(eng, getattr(hb, k)) for k in ("res_id", "ts_ms", "count", "flags")}
+        for k in ("entry_ref", "create_ts", "arg_tag", "arg_bits", "n_args"):
+            a = getattr(hb, k)
+            self.arrays[k] = DeviceArray(eng, a) if a is not None else None
+        self.arg_slots = 0 if hb.arg_tag is None else hb.arg_tag.shape[0]
+
+    def c_struct(self) -> abi.sf_event_batch:
+        b = abi.sf_event_batch()
+        b.n, b.mem = self.n, abi.MEM_DEVICE
+        g = lambda k: None if self.arrays[k] is None else self.arrays[k].ptr  # noqa: E731
+        b.res_id, b.ts_ms, b.count, b.flags = g("res_id"), g("ts_ms"), g("count"), g("flags")
+        b.entry_ref, b.create_ts = g("entry_ref"), g("create_ts")
+        b.arg_slots = self.arg_slots
+        b.arg_tag, b.arg_bits, b.n_args = g("arg_tag"), g("arg_bits"), g("n_args")
+        return b
+
+    def free(self):
+        for a in self.arrays.values():
+            if a is not None:
+                a.free()
+
+
+class DeviceVerdicts:
+    def __init__(self, eng: "FlowEngine", n: int, with_wait=True, with_rule=False):
+        self.status = DeviceArray.empty(eng, n, np.uint8)
+        self.wait_ms = DeviceArray.empty(eng, n, np.int32) if with_wait else None
+        self.rule_idx = DeviceArray.empty(eng, n, np.uint16) if with_rule else None
+
+    def c_struct(self) -> abi.sf_verdicts:
+        v = abi.sf_verdicts()
+        v.mem = abi.MEM_DEVICE
+        v.status = self.status.ptr
+        v.wait_ms = self.wait_ms.ptr if self.wait_ms else None
+        v.rule_idx = self.rule_idx.ptr if self.rule_idx else None
+        return v
+
+    def free(self):
+        for a in (self.status, self.wait_ms, self.rule_idx):
+            if a is not None:
+                a.free()
+
+
+class FlowEngine:
+    """One GPU's flow-check engine (sf_create .. sf_destroy)."""
+
+    def __init__(self, cfg: abi.sf_config):
+        self.cfg = cfg
+        h = P()
+        _check(lib().sf_create(C.byref(cfg), C.byref(h)))
+        self.h = h.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_flow_rules(self, rules):
+        ptr, n = abi.flow_rules_ptr(rules)
+        _check(lib().sf_load_flow_rules(self.h, ptr, n))
+
+    def load_param_rules(self, rules, items=()):
+        _check(lib().sf_load_param_rules(self.h, abi.rules_array(abi.sf_param_rule, rules), len(rules),
+                                         abi.rules_array(abi.sf_hot_item, list(items)), len(items)))
+
+    def load_system_rules(self, rules):
+        _check(lib().sf_load_system_rules(self.h, abi.rules_array(abi.sf_system_rule, rules), len(rules)))
+
+    def set_system_status(self, load, cpu):
+        _check(lib().sf_set_system_status(self.h, load, cpu))
+
+    def submit(self, batch: abi.HostBatch) -> abi.HostVerdicts:
+        out = abi.HostVerdicts(batch.n)
+        b = batch.c_struct()
+        v = out.c_struct()
+        _check(lib().sf_submit(self.h, C.byref(b), C.byref(v)))
+        return out
+
+    def submit_device(self, batch: DeviceBatch, out: DeviceVerdicts):
+        b = batch.c_struct()
+        v = out.c_struct()
+        _check(lib().sf_submit(self.h, C.byref(b), C.byref(v)))
+
+    def read_node(self, res) -> abi.sf_node_state:
+        st = abi.sf_node_state()
+        _check(lib().sf_read_node(self.h, res, C.byref(st)))
+        return st
+
+    def read_rule_state(self, idx) -> abi.sf_rule_state:
+        s = abi.sf_rule_state()
+        _check(lib().sf_read_rule_state(self.h, idx, C.byref(s)))
+        return s
+
+    def set_timing(self, on=True):
+        _check(lib().sf_set_timing(self.h, int(on)))
+
+    def stats(self) -> abi.sf_stats:
+        s = abi.sf_stats()
+        _check(lib().sf_get_stats(self.h, C.byref(s)))
+        return s
+
+    def sync(self):
+        _check(lib().sf_sync(self.h))

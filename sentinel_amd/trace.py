@@ -1,0 +1,222 @@
+"""Seeded synthetic traces for the BASELINE.json configs.
+
+All timestamps are int64 ms starting at ``T0``, non-decreasing; ties keep
+submission order (an EXIT always follows its ENTRY).  Every generator is a
+pure function of its arguments and seed, so parity tests, fixtures and the
+benchmark draw the same events.
+
+Config 1  FlowQpsDemo: one resource, QPS rule count 20, 128 virtual threads
+          (entry, exit, think U[0,50) ms) for ``duration_ms``
+          (sentinel-demo-basic/.../flow/FlowQpsDemo.java:46-166).
+Config 2  uniform resources, QPS DefaultController count U{5..50}, count=1,
+          no exits.
+Config 3  Zipf(1.1) resources scrambled by a bijection; per-resource rule mix
+          60 % QPS default / 10 % THREAD / 15 % WarmUp / 15 % RateLimiter,
+          count U{10..1000}; acquireCount 1 (90 %) or U{2..5}; THREAD
+          resources' entries get an EXIT after RT ~ Exp(20 ms).
+Config 4  hot-parameter limiting: per-resource QPS ParamFlowRule (+10 %
+          throttle rule), keys Zipf(1.1) over a large key space.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import abi
+
+T0 = 1_700_000_000_000
+
+
+def mix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser, vectorised (uint64 in/out)."""
+    x = np.asarray(x, dtype=np.uint64).copy()
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xff51afd7ed558ccd)
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xc4ceb9fe1a85ec53)
+        x ^= x >> np.uint64(33)
+    return x
+
+
+def scramble(rank: np.ndarray, n: int) -> np.ndarray:
+    """Bijection [0, n) -> [0, n): multiplication by a unit mod n."""
+    a = 2654435761
+    while np.gcd(a, n) != 1:
+        a += 2
+    return ((rank.astype(np.uint64) * np.uint64(a)) % np.uint64(n)).astype(np.uint64)
+
+
+def zipf_bounded(rng: np.random.Generator, s: float, n_max: int, size: int) -> np.ndarray:
+    """Exact bounded Zipf(s) samples in [1, n_max] by rejection-inversion
+    (Hörmann & Derflinger 1996), vectorised.  P(k) ∝ k^-s."""
+    def h(x):
+        return np.exp((1.0 - s) * np.log(x)) / (1.0 - s)
+
+    def h_inv(x):
+        return np.exp(np.log((1.0 - s) * x) / (1.0 - s))
+
+    hx0 = h(1.5) - 1.0
+    h_n = h(n_max + 0.5)
+    sh = 2.0 - h_inv(h(2.5) - 2.0 ** (-s))
+    out = np.empty(size, dtype=np.int64)
+    filled = 0
+    while filled < size:
+        m = int((size - filled) * 1.08) + 64
+        u = h_n + rng.random(m) * (hx0 - h_n)
+        x = h_inv(u)
+        k = np.floor(x + 0.5)
+        k = np.clip(k, 1, n_max)
+        accept = (k - x <= sh) | (u >= h(k + 0.5) - np.exp(-s * np.log(k)))
+        k = k[accept].astype(np.int64)
+        take = min(k.size, size - filled)
+        out[filled:filled + take] = k[:take]
+        filled += take
+    return out
+
+
+def _per_ms_times(rng, n, duration_ms):
+    """n sorted timestamps, uniform over [T0, T0+duration)."""
+    counts = rng.multinomial(n, np.full(duration_ms, 1.0 / duration_ms))
+    return T0 + np.repeat(np.arange(duration_ms, dtype=np.int64), counts)
+
+
+# ------------------------------------------------------------------ config 1
+def flow_qps_demo(duration_ms: int = 100_000, threads: int = 128, count: float = 20.0, seed: int = 1):
+    """FlowQpsDemo: rules + batch.  Resource id 0 ("abc")."""
+    rng = np.random.default_rng(seed)
+    per = []
+    for th in range(threads):
+        think = rng.integers(0, 50, size=duration_ms // 10 + 100)
+        t = np.cumsum(think)
+        t = t[t < duration_ms]
+        per.append(t)
+    ts = np.concatenate(per)
+    tid = np.concatenate([np.full(p.size, i) for i, p in enumerate(per)])
+    order = np.lexsort((tid, ts))
+    ts = ts[order] + T0
+    n_entry = ts.size
+    # entry immediately followed by its exit (FlowQpsDemo.java:143-166)
+    res = np.zeros(2 * n_entry, np.uint32)
+    t2 = np.repeat(ts, 2)
+    flags = np.tile(np.array([abi.EV_IN, abi.EV_IN | abi.EV_EXIT], np.uint8), n_entry)
+    eref = np.full(2 * n_entry, -1, np.int64)
+    eref[1::2] = np.arange(0, 2 * n_entry, 2)
+    cnt = np.ones(2 * n_entry, np.int32)
+    rules = [abi.sf_flow_rule(resource=0, grade=abi.GRADE_QPS, count=count, strategy=0, control_behavior=0,
+                              warm_up_period_sec=10, max_queueing_time_ms=500)]
+    return rules, abi.HostBatch(res, t2, cnt, flags, entry_ref=eref)
+
+
+# ------------------------------------------------------------------ config 2
+def uniform_rules(n_res: int, seed: int = 2, lo: int = 5, hi: int = 50):
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(lo, hi + 1, size=n_res)
+    return counts.astype(np.float64)
+
+
+def uniform_qps(n_res: int, n_events: int, duration_ms: int = 4000, seed: int = 2):
+    """Config 2 events (res ~ U[0, n_res), count 1, no exits).  Rules via uniform_rules."""
+    rng = np.random.default_rng(seed + 1)
+    ts = _per_ms_times(rng, n_events, duration_ms)
+    res = rng.integers(0, n_res, size=n_events, dtype=np.uint32)
+    cnt = np.ones(n_events, np.int32)
+    flags = np.full(n_events, abi.EV_IN, np.uint8)
+    return abi.HostBatch(res, ts, cnt, flags)
+
+
+def flow_rules_from_counts(counts, behaviors=None, grades=None, warm_up=10, max_queue=500):
+    rules = []
+    for i, c in enumerate(counts):
+        g = abi.GRADE_QPS if grades is None else int(grades[i])
+        b = 0 if behaviors is None else int(behaviors[i])
+        rules.append(abi.sf_flow_rule(resource=i, grade=g, count=float(c), strategy=0, control_behavior=b,
+                                      warm_up_period_sec=warm_up, max_queueing_time_ms=max_queue))
+    return rules
+
+
+# ------------------------------------------------------------------ config 3
+def mixed_rule_table(n_res: int, seed: int = 3):
+    """Per-resource (grade, behavior, count) for config 3, by resource hash."""
+    h = mix64(np.arange(n_res, dtype=np.uint64) + np.uint64(seed * 0x9E3779B97F4A7C15 & 0xFFFFFFFF))
+    bucket = (h % np.uint64(100)).astype(np.int64)
+    count = (10 + (h >> np.uint64(20)) % np.uint64(991)).astype(np.float64)
+    grade = np.where((bucket >= 60) & (bucket < 70), abi.GRADE_THREAD, abi.GRADE_QPS).astype(np.int32)
+    beh = np.zeros(n_res, np.int32)
+    beh[(bucket >= 70) & (bucket < 85)] = abi.BEHAVIOR_WARM_UP
+    beh[bucket >= 85] = abi.BEHAVIOR_RATE_LIMITER
+    return grade, beh, count
+
+
+def mixed_zipf(n_res: int, n_events: int, duration_ms: int = 4000, seed: int = 3, s: float = 1.1,
+               rt_mean_ms: float = 20.0):
+    """Config 3 batch: ``n_events`` total events (entries + exits)."""
+    rng = np.random.default_rng(seed + 7)
+    grade, _, _ = mixed_rule_table(n_res, seed)
+    # draw entries iid; THREAD-grade entries bring one EXIT each.  Take the
+    # shortest prefix whose entries + exits reach n_events exactly (the last
+    # exit is dropped when the prefix overshoots by one).
+    rank = zipf_bounded(rng, s, n_res, n_events) - 1
+    res = scramble(rank, n_res).astype(np.uint32)
+    is_thr = grade[res] == abi.GRADE_THREAD
+    cum = np.cumsum(1 + is_thr.astype(np.int64))
+    n_entry = int(np.searchsorted(cum, n_events, side="left")) + 1
+    res, is_thr = res[:n_entry], is_thr[:n_entry].copy()
+    if int(cum[n_entry - 1]) == n_events + 1:
+        is_thr[n_entry - 1] = False
+    ts = _per_ms_times(rng, n_entry, duration_ms)
+    acq = np.ones(n_entry, np.int32)
+    multi = rng.random(n_entry) < 0.10
+    acq[multi] = rng.integers(2, 6, size=int(multi.sum()))
+    t_end = T0 + duration_ms - 1
+    thr_idx = np.nonzero(is_thr)[0]
+    rt = np.floor(rng.exponential(rt_mean_ms, size=thr_idx.size)).astype(np.int64)
+    exit_ts = np.minimum(ts[thr_idx] + rt, t_end)
+    # merge: key = (ms offset, is_exit) -> stable uint16/uint32 radix sort
+    all_ts = np.concatenate([ts, exit_ts])
+    is_exit = np.concatenate([np.zeros(n_entry, bool), np.ones(thr_idx.size, bool)])
+    key = (all_ts - T0) * 2 + is_exit
+    key = key.astype(np.uint16 if key.max() < 65536 else np.uint32)   # uint16: numpy's O(n) radix sort
+    order = np.argsort(key, kind="stable")
+    pos = np.empty(order.size, np.int64)
+    pos[order] = np.arange(order.size)
+    src_entry = np.concatenate([np.arange(n_entry), thr_idx])
+    res_all = res[src_entry][order]
+    cnt_all = acq[src_entry][order]
+    flags = np.full(order.size, abi.EV_IN, np.uint8)
+    flags[is_exit[order]] = abi.EV_IN | abi.EV_EXIT
+    eref = np.full(order.size, -1, np.int64)
+    exit_pos = pos[n_entry:]
+    eref[exit_pos] = pos[thr_idx]
+    return abi.HostBatch(res_all, all_ts[order], cnt_all, flags, entry_ref=eref)
+
+
+def mixed_rules(n_res: int, seed: int = 3):
+    grade, beh, count = mixed_rule_table(n_res, seed)
+    return flow_rules_from_counts(count, behaviors=beh, grades=grade)
+
+
+# ------------------------------------------------------------------ config 4
+def param_zipf(n_res: int, n_events: int, n_keys: int, duration_ms: int = 4000, seed: int = 4, s: float = 1.1,
+               throttle_frac: float = 0.10):
+    """Config 4: (flow rules none) param rules + batch with one LONG arg per event."""
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(1, 101, size=n_res)
+    rules = []
+    for r in range(n_res):
+        rules.append(abi.sf_param_rule(resource=r, grade=abi.GRADE_QPS, param_idx=0, control_behavior=0,
+                                       count=float(counts[r]), max_queueing_time_ms=0, burst_count=0,
+                                       duration_in_sec=1, item_offset=0, item_count=0))
+    thr = np.nonzero(rng.random(n_res) < throttle_frac)[0]
+    for r in thr:
+        rules.append(abi.sf_param_rule(resource=int(r), grade=abi.GRADE_QPS, param_idx=0,
+                                       control_behavior=abi.BEHAVIOR_RATE_LIMITER,
+                                       count=float(rng.integers(1, 101)), max_queueing_time_ms=500,
+                                       burst_count=0, duration_in_sec=1, item_offset=0, item_count=0))
+    ts = _per_ms_times(rng, n_events, duration_ms)
+    res = rng.integers(0, n_res, size=n_events, dtype=np.uint32)
+    rank = zipf_bounded(rng, s, n_keys, n_events) - 1
+    key = mix64(rank.astype(np.uint64))
+    tag = np.full((1, n_events), abi.TAG_LONG, np.uint8)
+    batch = abi.HostBatch(res, ts, np.ones(n_events, np.int32), np.full(n_events, abi.EV_IN, np.uint8),
+                          arg_tag=tag, arg_bits=key.reshape(1, -1))
+    return rules, batch

@@ -1,0 +1,184 @@
+// TEST-ONLY host build of the engine's decision interpreter (sf_decide.h).
+//
+// Runs the exact per-resource kernel body on the CPU so the device logic can be
+// checked against the oracle in the CPU test suite (no GPU in the build
+// container).  It is never loaded by the product: libsentinel_flow.so has no
+// path to it, and sf_create fails without a gfx950 device.
+#include <cstdio>
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "../../sentinel_amd/csrc/sf_decide.h"
+
+using namespace sf;
+
+struct hs_engine {
+    sf_config cfg;
+    DevState st{};
+    std::vector<Bucket> second, minute;
+    std::vector<Borrow> borrow;
+    std::vector<int64_t> threads;
+    std::vector<uint32_t> rule_off, prule_off;
+    std::vector<DevRule> rules;
+    std::vector<DevRuleState> rstate;
+    std::vector<uint32_t> flow_pos;
+    std::vector<DevParamRule> prules;
+    std::vector<DevHotItem> items;
+    std::vector<uint8_t> pm_init;
+    std::vector<ParamSlot> ptab;
+    int32_t err = 0;
+    uint32_t R;
+    void refresh() {
+        st.second = second.data(); st.borrow = borrow.data(); st.minute = minute.data();
+        st.threads = threads.data(); st.rule_off = rule_off.data(); st.rules = rules.data();
+        st.rstate = rstate.data(); st.prule_off = prule_off.data(); st.prules = prules.data();
+        st.items = items.data(); st.pm_init = pm_init.data(); st.ptab = ptab.data();
+        st.pcap_mask = ptab.size() - 1; st.err = &err;
+    }
+};
+
+extern "C" {
+
+hs_engine* hs_create(const sf_config* c) {
+    hs_engine* e = new hs_engine();
+    e->cfg = *c;
+    e->R = c->max_resources;
+    size_t R = e->R, S = c->sample_count;
+    e->second.assign(R * S, fresh_bucket(WS_NONE, c->statistic_max_rt));
+    e->borrow.assign(R * S, Borrow{WS_NONE, 0});
+    e->minute.assign(R * MINUTE, fresh_bucket(WS_NONE, c->statistic_max_rt));
+    e->threads.assign(R, 0);
+    e->rule_off.assign(R + 1, 0); e->prule_off.assign(R + 1, 0);
+    e->rules.resize(1); e->rstate.resize(1); e->prules.resize(1); e->items.resize(1);
+    e->pm_init.assign(R, 0);
+    size_t pcap = 16; while (pcap < c->param_capacity) pcap <<= 1;
+    e->ptab.assign(pcap, ParamSlot{0, 0, 0, 0});
+    DevState& st = e->st;
+    st.S = c->sample_count; st.wl = c->interval_ms / c->sample_count; st.interval = c->interval_ms;
+    st.occupy_timeout = c->occupy_timeout_ms; st.max_rt = c->statistic_max_rt; st.R = e->R;
+    e->refresh();
+    return e;
+}
+void hs_destroy(hs_engine* e) { delete e; }
+
+static bool local_of(hs_engine* e, uint32_t res, uint32_t* l) {
+    if (res % e->cfg.shard_count != e->cfg.shard_index) return false;
+    *l = res / e->cfg.shard_count; return *l < e->R;
+}
+
+int hs_load_flow_rules(hs_engine* e, const sf_flow_rule* rules, uint32_t n) {
+    std::vector<uint32_t> counts(e->R + 1, 0), loc;
+    std::vector<const sf_flow_rule*> valid;
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t l; if (!local_of(e, rules[i].resource, &l)) return SF_ERR_INVALID;
+        if (!valid_flow_rule(rules[i])) continue;
+        if (++counts[l] > SF_MAX_RULES_PER_RESOURCE) return SF_ERR_UNSUPPORTED;
+        valid.push_back(&rules[i]); loc.push_back(l);
+    }
+    for (uint32_t r = 0; r < e->R; r++) e->rule_off[r + 1] = e->rule_off[r] + counts[r];
+    std::vector<uint32_t> fill(e->rule_off.begin(), e->rule_off.end() - 1);
+    e->rules.assign(std::max<size_t>(1, valid.size()), DevRule{});
+    e->rstate.assign(std::max<size_t>(1, valid.size()), fresh_rule_state());
+    e->flow_pos.assign(valid.size(), 0);
+    for (size_t k = 0; k < valid.size(); k++) {
+        uint32_t pos = fill[loc[k]]++;
+        e->flow_pos[k] = pos;
+        e->rules[pos] = make_dev_rule(*valid[k], e->cfg.cold_factor, (int)k);
+    }
+    e->refresh();
+    return SF_OK;
+}
+
+int hs_load_param_rules(hs_engine* e, const sf_param_rule* rules, uint32_t n, const sf_hot_item* items, uint32_t ni) {
+    std::vector<uint32_t> counts(e->R + 1, 0), loc(n);
+    for (uint32_t i = 0; i < n; i++) { if (!local_of(e, rules[i].resource, &loc[i])) return SF_ERR_INVALID; counts[loc[i]]++; }
+    for (uint32_t r = 0; r < e->R; r++) e->prule_off[r + 1] = e->prule_off[r] + counts[r];
+    std::vector<uint32_t> fill(e->prule_off.begin(), e->prule_off.end() - 1);
+    e->prules.assign(std::max<uint32_t>(1, n), DevParamRule{});
+    for (uint32_t i = 0; i < n; i++) e->prules[fill[loc[i]]++] = make_dev_param_rule(rules[i], (int)i);
+    e->items.assign(std::max<uint32_t>(1, ni), DevHotItem{});
+    for (uint32_t i = 0; i < ni; i++) { e->items[i].bits = items[i].bits; e->items[i].count = items[i].count; e->items[i].tag = items[i].tag; }
+    std::fill(e->pm_init.begin(), e->pm_init.end(), 0);
+    std::fill(e->ptab.begin(), e->ptab.end(), ParamSlot{0, 0, 0, 0});
+    e->refresh();
+    return SF_OK;
+}
+
+int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
+    const uint32_t n = in->n;
+    e->err = 0;
+    std::vector<uint32_t> key(n), perm(n), inv(n);
+    for (uint32_t i = 0; i < n; i++) if (!local_of(e, in->res_id[i], &key[i])) return SF_ERR_INVALID;
+    std::iota(perm.begin(), perm.end(), 0u);
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+    std::vector<int64_t> ts(n), eref(n, -1), cts(n, 0);
+    std::vector<int32_t> cnt(n);
+    std::vector<uint8_t> fl(n), nargs(n), atag((size_t)n * in->arg_slots), vs(n);
+    std::vector<uint64_t> abits((size_t)n * in->arg_slots);
+    std::vector<int32_t> vw(n); std::vector<uint16_t> vr(n);
+    for (uint32_t j = 0; j < n; j++) {
+        uint32_t i = perm[j]; inv[i] = j;
+        ts[j] = in->ts_ms[i]; cnt[j] = in->count[i]; fl[j] = in->flags[i];
+        if (in->n_args) nargs[j] = in->n_args[i];
+        for (uint32_t a = 0; a < in->arg_slots; a++) {
+            atag[(size_t)a * n + j] = in->arg_tag[(size_t)a * n + i];
+            abits[(size_t)a * n + j] = in->arg_bits[(size_t)a * n + i];
+        }
+    }
+    if (in->entry_ref)
+        for (uint32_t j = 0; j < n; j++) {
+            int64_t r = in->entry_ref[perm[j]];
+            eref[j] = r >= 0 ? (int64_t)inv[r] : (int64_t)-1;
+            cts[j] = in->create_ts ? in->create_ts[perm[j]] : 0;
+        }
+    SegIO io{ts.data(), cnt.data(), fl.data(), in->entry_ref ? eref.data() : nullptr,
+             in->entry_ref ? cts.data() : nullptr, in->arg_slots, in->n_args ? nargs.data() : nullptr,
+             atag.data(), abits.data(), n, vs.data(), vw.data(), vr.data()};
+    uint32_t lo = 0;
+    while (lo < n) {
+        uint32_t hi = lo;
+        while (hi < n && key[perm[hi]] == key[perm[lo]]) hi++;
+        if (e->st.S <= 2) decide_segment<2>(e->st, io, key[perm[lo]], lo, hi);
+        else decide_segment<SF_MAX_SAMPLE_COUNT>(e->st, io, key[perm[lo]], lo, hi);
+        lo = hi;
+    }
+    for (uint32_t j = 0; j < n; j++) {
+        uint32_t i = perm[j];
+        ((uint8_t*)out->status)[i] = vs[j];
+        if (out->wait_ms) out->wait_ms[i] = vw[j];
+        if (out->rule_idx) out->rule_idx[i] = vr[j];
+    }
+    return e->err;
+}
+
+int hs_read_node(hs_engine* e, uint32_t res, sf_node_state* out) {
+    uint32_t l; if (!local_of(e, res, &l)) return SF_ERR_INVALID;
+    std::memset(out, 0, sizeof *out);
+    for (int i = 0; i < SF_MAX_SAMPLE_COUNT; i++) { out->second[i].window_start = SF_WS_ABSENT; out->borrow_ws[i] = SF_WS_ABSENT; }
+    auto conv = [](const Bucket& d, sf_bucket* o) {
+        if (d.ws == WS_NONE) { std::memset(o, 0, sizeof *o); o->window_start = SF_WS_ABSENT; return; }
+        o->window_start = d.ws; o->pass = d.pass; o->block = d.block; o->exception = d.exc; o->success = d.succ;
+        o->rt = d.rt; o->occupied_pass = d.occ; o->min_rt = d.min_rt;
+    };
+    int S = e->cfg.sample_count;
+    for (int i = 0; i < S; i++) {
+        conv(e->second[(size_t)l * S + i], &out->second[i]);
+        const Borrow& b = e->borrow[(size_t)l * S + i];
+        out->borrow_ws[i] = b.ws == WS_NONE ? SF_WS_ABSENT : b.ws;
+        out->borrow_pass[i] = b.ws == WS_NONE ? 0 : b.pass;
+    }
+    for (int i = 0; i < MINUTE; i++) conv(e->minute[(size_t)l * MINUTE + i], &out->minute[i]);
+    out->cur_thread_num = e->threads[l];
+    return SF_OK;
+}
+
+int hs_read_rule_state(hs_engine* e, uint32_t idx, sf_rule_state* out) {
+    if (idx >= e->flow_pos.size()) return SF_ERR_INVALID;
+    const DevRuleState& s = e->rstate[e->flow_pos[idx]];
+    out->stored_tokens = s.stored_tokens; out->last_filled_time = s.last_filled; out->latest_passed_time = s.latest_passed;
+    return SF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,47 @@
+"""Shared parity helpers: run one workload through an engine and the oracle and
+compare verdicts, waits, rule indices, per-resource node state and controller
+state bit for bit."""
+import numpy as np
+
+from sentinel_amd import abi
+
+
+def compare_verdicts(a: abi.HostVerdicts, b: abi.HostVerdicts, what=""):
+    bad = np.nonzero((a.status != b.status) | (a.wait_ms != b.wait_ms) | (a.rule_idx != b.rule_idx))[0]
+    if bad.size:
+        i = bad[0]
+        raise AssertionError(f"{what}: {bad.size} verdicts differ; first at {i}: "
+                             f"engine=({a.status[i]},{a.wait_ms[i]},{a.rule_idx[i]}) "
+                             f"oracle=({b.status[i]},{b.wait_ms[i]},{b.rule_idx[i]})")
+
+
+def compare_nodes(eng, ora, resources, sample_count=2, what=""):
+    for r in resources:
+        x = abi.node_state_to_dict(eng.read_node(int(r)), sample_count)
+        y = abi.node_state_to_dict(ora.read_node(int(r)), sample_count)
+        if x != y:
+            for k in x:
+                if x[k] != y[k]:
+                    raise AssertionError(f"{what}: node {r} field {k} differs:\n engine={x[k]}\n oracle={y[k]}")
+
+
+def compare_rule_states(eng, ora, n_rules, what=""):
+    for k in range(n_rules):
+        a, b = eng.read_rule_state(k), ora.read_rule_state(k)
+        ta = (a.stored_tokens, a.last_filled_time, a.latest_passed_time)
+        tb = (b.stored_tokens, b.last_filled_time, b.latest_passed_time)
+        assert ta == tb, f"{what}: rule {k} state engine={ta} oracle={tb}"
+
+
+def run_both(make_engine, make_oracle, cfg, flow_rules=(), param_rules=(), items=(), batches=()):
+    eng, ora = make_engine(cfg), make_oracle(cfg)
+    if flow_rules:
+        eng.load_flow_rules(list(flow_rules))
+        ora.load_flow_rules(list(flow_rules))
+    if param_rules:
+        eng.load_param_rules(list(param_rules), list(items))
+        ora.load_param_rules(list(param_rules), list(items))
+    outs = []
+    for b in batches:
+        outs.append((eng.submit(b), ora.submit(b)))
+    return eng, ora, outs

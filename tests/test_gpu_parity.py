@@ -1,0 +1,77 @@
+"""GPU parity: libsentinel_flow.so (HIP, gfx950) against the oracle, bit for
+bit (verdicts, waits, rule indices, node windows, controller state), on every
+seeded workload, through the C-ABI.  Run with -m gpu on an MI355X."""
+import numpy as np
+import pytest
+
+from sentinel_amd import abi, trace
+from tests import parity, workloads
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng_mod():
+    from sentinel_amd import engine
+    engine.lib()
+    return engine
+
+
+@pytest.mark.parametrize("name", list(workloads.ALL))
+def test_workload(eng_mod, so, name):
+    workloads.run(eng_mod.FlowEngine, so.OracleEngine, workloads.ALL[name]())
+
+
+def test_config3_many_batches(eng_mod, so):
+    workloads.run(eng_mod.FlowEngine, so.OracleEngine, workloads.config3(R=20_000, n=600_000, seed=17, split=5))
+
+
+def test_device_resident_batch(eng_mod, so):
+    """Inputs already in HBM (the bench path): same verdicts as the host path."""
+    w = workloads.config3(R=5000, n=200_000, seed=5, split=1)
+    e = eng_mod.FlowEngine(w["cfg"])
+    e.load_flow_rules(w["flow"])
+    ora = so.OracleEngine(w["cfg"])
+    ora.load_flow_rules(w["flow"])
+    hb = w["batches"][0]
+    db = eng_mod.DeviceBatch(e, hb)
+    dv = eng_mod.DeviceVerdicts(e, hb.n, with_wait=True, with_rule=True)
+    e.submit_device(db, dv)
+    got = abi.HostVerdicts(hb.n)
+    got.status, got.wait_ms, got.rule_idx = dv.status.numpy(), dv.wait_ms.numpy(), dv.rule_idx.numpy()
+    parity.compare_verdicts(got, ora.submit(hb), "device batch")
+    parity.compare_nodes(e, ora, w["nodes"])
+
+
+def test_config2_large_properties(eng_mod, so):
+    """1M-event uniform batch: oracle parity plus the window invariant
+    passes(hw) + passes(hw-1) <= count for every resource."""
+    R, n = 50_000, 1_000_000
+    counts = trace.uniform_rules(R, seed=31)
+    rules = trace.flow_rules_from_counts(counts)
+    b = trace.uniform_qps(R, n, seed=31)
+    cfg = abi.default_config(max_resources=R, max_batch=n)
+    e = eng_mod.FlowEngine(cfg)
+    e.load_flow_rules(rules)
+    v = e.submit(b)
+    ora = so.OracleEngine(cfg)
+    ora.load_flow_rules(rules)
+    parity.compare_verdicts(v, ora.submit(b), "config2 1M")
+    passed = v.status == abi.V_PASS
+    hw = (b.ts_ms - trace.T0) // 500
+    nh = int(hw.max()) + 1
+    grid = np.zeros((R, nh), np.int64)
+    np.add.at(grid, (b.res_id[passed], hw[passed]), 1)
+    assert ((grid[:, 1:] + grid[:, :-1]) <= counts[:, None]).all()
+
+
+def test_invalid_batches_rejected(eng_mod):
+    cfg = abi.default_config(max_resources=8, max_batch=16)
+    e = eng_mod.FlowEngine(cfg)
+    b = abi.HostBatch([9], [trace.T0], [1], [0])           # resource outside the shard
+    with pytest.raises(eng_mod.EngineError):
+        e.submit(b)
+    b = abi.HostBatch(np.zeros(17, np.uint32), np.full(17, trace.T0), np.ones(17), np.zeros(17))
+    with pytest.raises(eng_mod.EngineError):
+        e.submit(b)
+    e.submit(abi.HostBatch([1], [trace.T0], [1], [0]))    # still usable

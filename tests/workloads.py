@@ -1,0 +1,153 @@
+"""Seeded parity workloads shared by the CPU (hostsim) and GPU parity suites.
+
+Each builder returns a dict: cfg, flow (rules), param (rules), items, batches,
+nodes (resources whose full node state is compared) and n_flow.
+"""
+import numpy as np
+
+from sentinel_amd import abi, trace
+
+
+def config1(duration_ms=20_000):
+    rules, batch = trace.flow_qps_demo(duration_ms=duration_ms)
+    return dict(cfg=abi.default_config(max_resources=4, max_batch=batch.n), flow=rules, batches=[batch],
+                nodes=[0])
+
+
+def config2(R=500, n=60_000, seed=2):
+    rules = trace.flow_rules_from_counts(trace.uniform_rules(R, seed=seed))
+    batch = trace.uniform_qps(R, n, seed=seed)
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=batch.n), flow=rules, batches=[batch],
+                nodes=list(range(0, R, 7)))
+
+
+def config3(R=2000, n=80_000, seed=3, split=2, duration_ms=6000):
+    rules = trace.mixed_rules(R, seed=seed)
+    full = trace.mixed_zipf(R, n, duration_ms=duration_ms, seed=seed)
+    cuts = np.linspace(0, full.n, split + 1).astype(int)
+    batches = [full.subset(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
+    hot = np.argsort(-np.bincount(full.res_id, minlength=R))[:50]
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=full.n), flow=rules, batches=batches,
+                nodes=sorted(set(int(x) for x in hot) | set(range(0, R, 37))), n_flow=len(rules))
+
+
+def config4(R=40, n=50_000, keys=5000, seed=4):
+    rules, batch = trace.param_zipf(R, n, keys, seed=seed)
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=batch.n, param_capacity=1 << 17),
+                param=rules, batches=[batch], nodes=list(range(R)))
+
+
+def prioritized(seed=9, R=20, n=20000):
+    rng = np.random.default_rng(seed)
+    rules = trace.flow_rules_from_counts(rng.integers(2, 8, R))
+    ts = np.sort(rng.integers(0, 5000, n)) + trace.T0
+    res = rng.integers(0, R, n).astype(np.uint32)
+    flags = np.where(rng.random(n) < 0.5, abi.EV_PRIO, 0).astype(np.uint8) | abi.EV_IN
+    cnt = rng.integers(1, 3, n).astype(np.int32)
+    ent = np.arange(0, n, 3)
+    ex_ts = ts[ent] + rng.integers(0, 30, ent.size)
+    all_ts = np.concatenate([ts, ex_ts])
+    key = np.lexsort((np.concatenate([np.zeros(n), np.ones(ent.size)]), all_ts))
+    pos = np.empty(key.size, np.int64)
+    pos[key] = np.arange(key.size)
+    src = np.concatenate([np.arange(n), ent])
+    err = np.where(rng.random(ent.size) < 0.2, abi.EV_ERROR, 0)
+    fl = np.concatenate([flags, (abi.EV_EXIT | abi.EV_IN | err).astype(np.uint8)])
+    eref = np.full(key.size, -1, np.int64)
+    eref[pos[n:]] = pos[ent]
+    b = abi.HostBatch(res[src][key], all_ts[key], cnt[src][key], fl[key], entry_ref=eref)
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=b.n), flow=rules, batches=[b],
+                nodes=list(range(R)))
+
+
+def multi_rule(seed=12, R=30, n=30000):
+    rng = np.random.default_rng(seed)
+    rules = []
+    for r in range(R):
+        for _ in range(int(rng.integers(1, 4))):
+            beh = int(rng.integers(0, 4))
+            grade = abi.GRADE_THREAD if (beh == 0 and rng.random() < 0.3) else abi.GRADE_QPS
+            rules.append(abi.sf_flow_rule(resource=r, grade=grade, count=float(rng.integers(1, 40)), strategy=0,
+                                          control_behavior=beh if grade == abi.GRADE_QPS else 0,
+                                          warm_up_period_sec=int(rng.integers(1, 6)),
+                                          max_queueing_time_ms=int(rng.integers(1, 800))))
+    ts = np.sort(rng.integers(0, 8000, n)) + trace.T0
+    res = rng.integers(0, R, n).astype(np.uint32)
+    b = abi.HostBatch(res, ts, rng.integers(1, 4, n).astype(np.int32), np.full(n, abi.EV_IN, np.uint8))
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=n), flow=rules, batches=[b],
+                nodes=list(range(R)), n_flow=len(rules))
+
+
+def geometry(sample_count, interval, R=50, n=20_000):
+    rules = trace.flow_rules_from_counts(trace.uniform_rules(R, seed=7))
+    batch = trace.uniform_qps(R, n, seed=7)
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=batch.n, sample_count=sample_count,
+                                       interval_ms=interval), flow=rules, batches=[batch], nodes=list(range(R)))
+
+
+def param_mixed(seed=21, R=12, n=30000):
+    """Param rules: QPS default with burst/duration/hot items, throttle, THREAD grade
+    with exits, several args, negative paramIdx, null values."""
+    rng = np.random.default_rng(seed)
+    items, prules = [], []
+    for r in range(R):
+        kinds = rng.choice(4, size=int(rng.integers(1, 3)), replace=False)
+        for k in kinds:
+            off = len(items)
+            for v in rng.choice(50, size=2, replace=False):
+                items.append(abi.sf_hot_item(tag=abi.TAG_LONG, count=int(rng.integers(0, 6)), bits=int(v)))
+            pidx = int(rng.choice([0, 1, -1]))
+            if k == 0:
+                prules.append(abi.sf_param_rule(resource=r, grade=abi.GRADE_QPS, param_idx=pidx, control_behavior=0,
+                                                count=float(rng.integers(1, 10)), burst_count=int(rng.integers(0, 4)),
+                                                duration_in_sec=int(rng.integers(1, 3)), item_offset=off, item_count=2))
+            elif k == 1:
+                prules.append(abi.sf_param_rule(resource=r, grade=abi.GRADE_QPS, param_idx=pidx, control_behavior=2,
+                                                count=float(rng.integers(1, 20)), max_queueing_time_ms=int(rng.integers(0, 300)),
+                                                duration_in_sec=1, item_offset=off, item_count=2))
+            else:
+                prules.append(abi.sf_param_rule(resource=r, grade=abi.GRADE_THREAD, param_idx=pidx, control_behavior=0,
+                                                count=float(rng.integers(1, 5)), duration_in_sec=1,
+                                                item_offset=off, item_count=2))
+    flow = [abi.sf_flow_rule(resource=r, grade=abi.GRADE_QPS, count=float(rng.integers(3, 30)), strategy=0,
+                             control_behavior=0, warm_up_period_sec=10, max_queueing_time_ms=500) for r in range(0, R, 2)]
+    ts = np.sort(rng.integers(0, 6000, n)) + trace.T0
+    res = rng.integers(0, R, n).astype(np.uint32)
+    tag = np.full((2, n), abi.TAG_LONG, np.uint8)
+    tag[rng.random((2, n)) < 0.05] = abi.TAG_NULL
+    bits = rng.integers(0, 50, (2, n)).astype(np.uint64)
+    nargs = rng.integers(0, 3, n).astype(np.uint8)
+    ent = np.arange(0, n, 2)
+    ex_ts = ts[ent] + rng.integers(0, 100, ent.size)
+    all_ts = np.concatenate([ts, ex_ts])
+    key = np.lexsort((np.concatenate([np.zeros(n), np.ones(ent.size)]), all_ts))
+    pos = np.empty(key.size, np.int64)
+    pos[key] = np.arange(key.size)
+    src = np.concatenate([np.arange(n), ent])
+    fl = np.concatenate([np.full(n, abi.EV_IN, np.uint8), np.full(ent.size, abi.EV_EXIT | abi.EV_IN, np.uint8)])
+    eref = np.full(key.size, -1, np.int64)
+    eref[pos[n:]] = pos[ent]
+    b = abi.HostBatch(res[src][key], all_ts[key], np.ones(key.size, np.int32), fl[key], entry_ref=eref,
+                      arg_tag=tag[:, src][:, key], arg_bits=bits[:, src][:, key], n_args=nargs[src][key])
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=b.n, param_capacity=1 << 14), flow=flow,
+                param=prules, items=items, batches=[b], nodes=list(range(R)), n_flow=len(flow))
+
+
+ALL = {
+    "config1": config1, "config2": config2, "config3": config3, "config4": config4,
+    "prioritized": prioritized, "multi_rule": multi_rule, "param_mixed": param_mixed,
+    "geom_S1": lambda: geometry(1, 1000), "geom_S4": lambda: geometry(4, 1000), "geom_S10": lambda: geometry(10, 2000),
+}
+
+
+def run(make_engine, make_oracle, w):
+    from tests import parity
+    eng, ora, outs = parity.run_both(make_engine, make_oracle, w["cfg"], flow_rules=w.get("flow", ()),
+                                     param_rules=w.get("param", ()), items=w.get("items", ()),
+                                     batches=w["batches"])
+    for k, (a, b) in enumerate(outs):
+        parity.compare_verdicts(a, b, f"batch{k}")
+    parity.compare_nodes(eng, ora, w["nodes"], sample_count=w["cfg"].sample_count)
+    if w.get("n_flow"):
+        parity.compare_rule_states(eng, ora, w["n_flow"])
+    return eng, ora, outs
