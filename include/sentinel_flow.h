@@ -88,7 +88,8 @@ typedef struct sf_config {
     double   exceed_count;        /* 1.0 */
     double   max_occupy_ratio;    /* 1.0 */
     uint32_t max_flow_ids;        /* capacity of the flowId table              */
-    uint32_t reserved;
+    uint32_t heavy_min_events;    /* resource segments longer than this use the
+                                     window/skip algorithms (0 = engine default) */
 } sf_config;
 
 /* Fill *cfg with the reference defaults listed above. */

@@ -55,7 +55,7 @@ class sf_config(C.Structure):
         ("shard_index", C.c_uint32), ("device", C.c_int32),
         ("cluster_sample_count", C.c_int32), ("cluster_interval_ms", C.c_int32),
         ("exceed_count", C.c_double), ("max_occupy_ratio", C.c_double),
-        ("max_flow_ids", C.c_uint32), ("reserved", C.c_uint32),
+        ("max_flow_ids", C.c_uint32), ("heavy_min_events", C.c_uint32),
     ]
 
 
@@ -65,7 +65,7 @@ def default_config(**kw) -> sf_config:
                     statistic_max_rt=5000, max_resources=1024, max_batch=1 << 20,
                     param_capacity=1 << 16, shard_count=1, shard_index=0, device=0,
                     cluster_sample_count=10, cluster_interval_ms=1000, exceed_count=1.0,
-                    max_occupy_ratio=1.0, max_flow_ids=1024, reserved=0)
+                    max_occupy_ratio=1.0, max_flow_ids=1024, heavy_min_events=0)
     for k, v in kw.items():
         setattr(cfg, k, v)
     return cfg

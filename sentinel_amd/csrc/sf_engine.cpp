@@ -33,7 +33,7 @@ static int fail(int code, const std::string& msg) {
 
 struct sf_engine {
     sf_config cfg{};
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr;
     uint32_t R = 0, key_bits = 1;
     DevState st{};
     Work w{};
@@ -43,7 +43,7 @@ struct sf_engine {
     // staging for host-memory batches
     void* stage_in = nullptr; size_t stage_in_bytes = 0;
     void* stage_out = nullptr; size_t stage_out_bytes = 0;
-    hipEvent_t ev[5]{};
+    hipEvent_t ev[7]{};
     bool timing = false;
     sf_stats stats{};
     std::vector<void*> user_allocs;
@@ -85,11 +85,16 @@ void sf_destroy(sf_engine* e) {
                     e->w.keys_in, e->w.keys_out, e->w.vals_in, e->w.perm, e->w.head, e->w.head_scan,
                     e->w.seg_start, e->w.seg_res, e->w.n_seg, e->w.s_ts, e->w.s_cnt, e->w.s_flags, e->w.s_eref,
                     e->w.s_cts, e->w.s_nargs, e->w.s_atag, e->w.s_abits, e->w.inv, e->w.v_status, e->w.v_wait,
-                    e->w.v_rule, e->w.sort_tmp, e->w.scan_tmp, e->stage_in, e->stage_out};
+                    e->w.v_rule, e->w.sort_tmp, e->w.scan_tmp, e->stage_in, e->stage_out,
+                    e->w.segflag, e->w.seg_mode, e->w.light_list, e->w.heavy_list, e->w.counters, e->w.pcg,
+                    e->w.pscan_tmp, e->w.item_lo, e->w.item_hi, e->w.item_wait, e->w.n_items, e->w.acc_hw,
+                    e->w.acc_sec, e->w.acc_hw_base, e->w.acc_sec_base, e->w.seg_hw0, e->w.seg_sec0,
+                    e->w.seg_nhw, e->w.seg_nsec};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     for (auto& x : e->ev) if (x) hipEventDestroy(x);
     if (e->stream) hipStreamDestroy(e->stream);
+    if (e->stream2) hipStreamDestroy(e->stream2);
     delete e;
 }
 
@@ -117,6 +122,7 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     e->R = c.max_resources;
     while ((1ull << e->key_bits) < e->R) e->key_bits++;
     HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
     for (auto& x : e->ev) HIP_TRY(hipEventCreate(&x));
 
     DevState& st = e->st;
@@ -151,9 +157,21 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     DALLOC(w.s_eref, N * 8); DALLOC(w.s_cts, N * 8); DALLOC(w.inv, N * 4);
     DALLOC(w.s_nargs, N); DALLOC(w.s_atag, N * SF_MAX_ARGS); DALLOC(w.s_abits, N * SF_MAX_ARGS * 8);
     DALLOC(w.v_status, N); DALLOC(w.v_wait, N * 4); DALLOC(w.v_rule, N * 2);
-    HIP_TRY(query_temp_bytes((uint32_t)N, e->key_bits, &w.sort_tmp_bytes, &w.scan_tmp_bytes));
+    HIP_TRY(query_temp_bytes((uint32_t)N, e->key_bits, &w.sort_tmp_bytes, &w.scan_tmp_bytes, &w.pscan_tmp_bytes));
     DALLOC(w.sort_tmp, w.sort_tmp_bytes);
     DALLOC(w.scan_tmp, w.scan_tmp_bytes);
+    DALLOC(w.pscan_tmp, w.pscan_tmp_bytes);
+    // heavy / light split
+    w.heavy_min = c.heavy_min_events ? c.heavy_min_events : 512;
+    const size_t SC = std::min<size_t>(N, R) + 1;
+    w.seg_cap = (uint32_t)SC;
+    DALLOC(w.segflag, SC * 4); DALLOC(w.seg_mode, SC); DALLOC(w.light_list, SC * 4); DALLOC(w.heavy_list, SC * 4);
+    DALLOC(w.counters, 16 * 4); DALLOC(w.pcg, N * 8);
+    DALLOC(w.item_lo, N * 4); DALLOC(w.item_hi, N * 4); DALLOC(w.item_wait, N * 4); DALLOC(w.n_items, SC * 4);
+    w.acc_cap = (uint32_t)std::min<size_t>(std::max<size_t>(N / w.heavy_min * 64, 1 << 16), 1u << 24);
+    DALLOC(w.acc_hw, (size_t)w.acc_cap * ACC_BYTES); DALLOC(w.acc_sec, (size_t)w.acc_cap * ACC_BYTES);
+    DALLOC(w.acc_hw_base, SC * 4); DALLOC(w.acc_sec_base, SC * 4); DALLOC(w.seg_hw0, SC * 8);
+    DALLOC(w.seg_sec0, SC * 8); DALLOC(w.seg_nhw, SC * 4); DALLOC(w.seg_nsec, SC * 4);
     HIP_TRY(hipStreamSynchronize(e->stream));
     *out = e;
     return SF_OK;
@@ -328,7 +346,7 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     }
     HIP_TRY(hipMemsetAsync(e->st.err, 0, sizeof(int32_t), s));
     hipError_t le = launch_pipeline(e->st, e->w, b, dv, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s,
-                                    e->timing ? e->ev : nullptr);
+                                    e->stream2, e->ev, e->timing);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
     if (out->mem == SF_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, s));

@@ -1,0 +1,334 @@
+// sf_heavy.h — decision algorithms for heavy resource segments (product code).
+//
+// A Zipf(1.1) batch puts ~12 % of all events on one resource; replaying such
+// a segment event by event in one lane is a latency-bound serial chain.  For
+// the common single-rule classes the reference semantics admit a description
+// whose size is proportional to the number of WINDOWS and PASSES, not events:
+//
+//  QPS DefaultController / WarmUpController (no prioritized entries):
+//    inside one bucket window (LeapArray hw of length interval/sampleCount)
+//    the threshold and passQps of the other buckets are constant, so the pass
+//    set is the greedy prefix of the entries' acquireCount prefix sums plus at
+//    most a few tail passes (DefaultController.java:50-89,
+//    WarmUpController.java:147-175; WarmUp syncToken runs once per second).
+//  RateLimiterController: an entry passes iff t >= latestPassedTime +
+//    cost(c) - maxQueueingTimeMs (RateLimiterController.java:48-102), so the
+//    next pass is found by a search over the time-sorted segment.
+//
+// One workgroup (a "team") runs the decision chain for one segment and emits
+// a sorted list of pass ITEMS (entry intervals and singleton passes with a
+// wait).  Device-wide kernels then write every verdict from the items, reduce
+// the per-window counters, and apply them to the LeapArray state in time
+// order (bucket reset semantics of LeapArray.currentWindow).
+#pragma once
+#include "sf_decide.h"
+
+namespace sf {
+
+// segment modes (seg_mode[s])
+enum : uint8_t { SM_LIGHT = 0, SM_GENERIC = 1, SM_QPS = 2, SM_WARM = 3, SM_RL = 4, SM_NORULE = 5 };
+constexpr uint32_t SEGF_PRIO = 1u, SEGF_NONPOS = 2u;
+
+struct Acc {            // per (segment, window) counter deltas
+    unsigned long long pass, block, succ, rt, exc, n_pass, n_exit, n_touch;
+    long long min_rt;
+};
+
+static_assert(sizeof(Acc) == ACC_BYTES, "Acc layout must match the engine allocation");
+
+// Segment routing (k_classify): the window/skip algorithms cover single-rule
+// QPS / WarmUp / RateLimiter resources (and resources without rules) when no
+// entry is prioritized or has acquireCount <= 0 and IntervalProperty is 1 s.
+SF_HD uint8_t heavy_mode(const DevState& st, uint32_t res, uint32_t segflags, int64_t first_ts) {
+    // a borrowed (prioritized) pass waiting for a window of this batch would be
+    // copied into that window when it is created: keep such resources exact
+    // on the generic path (OccupiableBucketLeapArray.java:40-64)
+    const int64_t ws_first = first_ts - first_ts % st.wl;
+    for (int i = 0; i < st.S; i++)
+        if (st.borrow[(size_t)res * st.S + i].ws >= ws_first) return SM_GENERIC;
+    const uint32_t nr = st.rule_off[res + 1] - st.rule_off[res];
+    const uint32_t np = st.prule_off[res + 1] - st.prule_off[res];
+    if (np != 0 || (segflags & SEGF_NONPOS) || st.interval != 1000) return SM_GENERIC;
+    if (nr == 0) return SM_NORULE;
+    if (nr != 1 || (segflags & SEGF_PRIO)) return SM_GENERIC;
+    const DevRule& r = st.rules[st.rule_off[res]];
+    if (r.kind == CT_DEFAULT && r.grade == SF_GRADE_QPS) return SM_QPS;
+    if (r.kind == CT_WARM_UP) return SM_WARM;
+    if (r.kind == CT_RATE_LIMITER) return SM_RL;
+    return SM_GENERIC;
+}
+
+struct HeavyCtx {
+    const uint32_t* seg_start; const uint32_t* seg_res; const uint8_t* seg_mode;
+    const uint32_t* heavy_list; const uint32_t* n_heavy;
+    const int64_t* pcg;                // inclusive prefix of entry acquireCount over the sorted batch
+    uint32_t* item_lo; uint32_t* item_hi; int32_t* item_wait; uint32_t* n_items;
+    Acc* acc_hw; Acc* acc_sec; const uint32_t* acc_hw_base; const uint32_t* acc_sec_base;
+    const int64_t* seg_hw0; const int64_t* seg_sec0;    // first window index of the segment
+};
+
+// ------------------------------------------------------------------ team
+#if defined(__HIP_DEVICE_COMPILE__)
+struct Team {
+    int rank, size;
+    long long* red;     // LDS, >= 16 slots
+    __device__ void sync() { __syncthreads(); }
+    __device__ long long min(long long v) {
+        for (int o = 32; o > 0; o >>= 1) { long long w = __shfl_xor(v, o); v = w < v ? w : v; }
+        __syncthreads();
+        if ((rank & 63) == 0) red[rank >> 6] = v;
+        __syncthreads();
+        long long r = red[0];
+        for (int i = 1; i < (size >> 6); i++) r = red[i] < r ? red[i] : r;
+        return r;
+    }
+    __device__ bool leader() const { return rank == 0; }
+};
+#else
+struct Team {
+    int rank = 0, size = 1;
+    long long* red = nullptr;
+    void sync() {}
+    long long min(long long v) { return v; }
+    bool leader() const { return true; }
+};
+#endif
+
+// First j in [lo, hi) with pred(j) true (pred monotone false..true); hi if none.
+template <class P>
+SF_HD uint32_t team_first_true(Team& tm, uint32_t lo, uint32_t hi, P pred) {
+    if (tm.size == 1) {                                   // host build / tiny teams: binary search
+        uint32_t a = lo, b = hi;
+        while (a < b) { uint32_t m = a + (b - a) / 2; if (pred(m)) b = m; else a = m + 1; }
+        return a;
+    }
+    while (lo < hi) {
+        uint64_t n = hi - lo;
+        if (n <= (uint64_t)tm.size) {
+            long long cand = (tm.rank < (int)n && pred(lo + tm.rank)) ? (long long)tm.rank : (long long)n;
+            long long r = tm.min(cand);
+            return lo + (uint32_t)r;
+        }
+        uint64_t step = (n + tm.size - 1) / tm.size;
+        uint64_t last = (uint64_t)(tm.rank + 1) * step;
+        if (last > n) last = n;
+        long long cand = (tm.rank * step < n && pred(lo + (uint32_t)(last - 1))) ? (long long)tm.rank : (long long)tm.size;
+        long long c = tm.min(cand);
+        if (c >= tm.size) return hi;
+        uint64_t nlo = c * step, nhi = (c + 1) * step;
+        if (nhi > n) nhi = n;
+        hi = lo + (uint32_t)nhi;
+        lo = lo + (uint32_t)nlo;
+    }
+    return lo;
+}
+
+SF_HD bool is_entry(uint8_t f) { return (f & SF_EV_EXIT) == 0; }
+
+// Σ acquireCount of entries in [a, b] inclusive (a <= b), from the global prefix
+SF_HD int64_t csum(const int64_t* pcg, uint32_t a, uint32_t b) { return pcg[b] - (a ? pcg[a - 1] : 0); }
+
+struct ItemWriter {
+    uint32_t* lo; uint32_t* hi; int32_t* wait; uint32_t base; uint32_t n;
+    SF_HD void push(bool leader, uint32_t a, uint32_t b, int32_t w) {
+        if (leader) { lo[base + n] = a; hi[base + n] = b; wait[base + n] = w; }
+        n++;
+    }
+};
+
+// ---------------------------------------------------------- QPS / WarmUp
+// Runs uniformly on every lane of the team; only the leader writes.
+SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t s,
+                     uint32_t res, uint32_t lo, uint32_t hi, bool warm) {
+    const int S = st.S, wl = st.wl;
+    Bucket sec[SF_MAX_SAMPLE_COUNT];
+    Borrow bor[SF_MAX_SAMPLE_COUNT];
+    for (int i = 0; i < S; i++) { sec[i] = st.second[(size_t)res * S + i]; bor[i] = st.borrow[(size_t)res * S + i]; }
+    const uint32_t r0 = st.rule_off[res];
+    const DevRule rule = st.rules[r0];
+    DevRuleState rs = st.rstate[r0];
+    const Bucket* gmin = st.minute + (size_t)res * MINUTE;
+    ItemWriter iw{hc.item_lo, hc.item_hi, hc.item_wait, lo, 0};
+    // per-second pass totals of the minute window (for previousPassQps)
+    int64_t cur_sec = INT64_MIN, cur_sec_pass = 0, prev_sec_pass_known = INT64_MIN, prev_sec_pass = 0;
+    int64_t last_sync_sec = INT64_MIN;
+
+    uint32_t p = lo;
+    while (p < hi) {
+        const int64_t t0 = io.ts[p];
+        const int64_t h = t0 / wl, ws = h * wl, hw_end = ws + wl;
+        const uint32_t b = team_first_true(tm, p, hi, [&](uint32_t j) { return io.ts[j] >= hw_end; });
+        // second-window roll at t0 (OccupiableBucketLeapArray.currentWindow)
+        const int idx = (int)(h % S);
+        if (sec[idx].ws != ws) {
+            Bucket nb = fresh_bucket(ws, st.max_rt);
+            const Borrow& bw = bor[(int)((ws / wl) % S)];
+            if (bw.ws <= ws && ws < bw.ws + wl) nb.pass = (int64_t)(int32_t)bw.pass;
+            sec[idx] = nb;
+        }
+        int64_t p_prev = 0;
+        for (int i = 0; i < S; i++)
+            if (i != idx && !(wsub(t0, sec[i].ws) > st.interval)) p_prev = wadd(p_prev, sec[i].pass);
+        const int64_t base = p_prev + sec[idx].pass;
+        // minute-window bookkeeping for this hw's second
+        const int64_t sn = t0 / 1000;
+        if (sn != cur_sec) {
+            // pass of the minute bucket for second sn before this batch's passes
+            const Bucket& mb = gmin[(int)(sn % MINUTE)];
+            int64_t init = (mb.ws == sn * 1000) ? mb.pass : 0;
+            if (cur_sec != INT64_MIN) { prev_sec_pass_known = cur_sec; prev_sec_pass = cur_sec_pass; }
+            cur_sec = sn; cur_sec_pass = init;
+        }
+        // entries of [p, b)
+        const bool has_entry = csum(hc.pcg, p, b - 1) > 0;
+        double thr = rule.count;
+        if (warm && has_entry) {
+            if (sn > last_sync_sec) {
+                int64_t prev_qps;                 // previousPassQps: minute bucket (sn-1)
+                if (prev_sec_pass_known == sn - 1) prev_qps = prev_sec_pass;
+                else {
+                    const Bucket& pb = gmin[(int)((sn - 1) % MINUTE)];
+                    prev_qps = (pb.ws == (sn - 1) * 1000) ? pb.pass : 0;
+                }
+                warm_sync(rule, rs, t0, prev_qps);
+                last_sync_sec = sn;
+            }
+            int64_t rest = rs.stored_tokens;
+            if (rest >= rule.warning_token) {
+                int64_t above = rest - rule.warning_token;
+                thr = j_next_up(1.0 / ((double)above * rule.slope + 1.0 / rule.count));
+            }
+        }
+        int64_t passed = 0;
+        if (has_entry) {
+            const int64_t* pcg = hc.pcg;
+            const int64_t pc0 = p ? pcg[p - 1] : 0;
+            // first failing entry: (double)(base + Σc[p..j]) > thr  (DefaultController: (int)passQps + c > count)
+            const uint32_t f = team_first_true(tm, p, b, [&](uint32_t j) {
+                return (double)(base + (pcg[j] - pc0)) > thr;
+            });
+            if (f > p) { passed = (f ? pcg[f - 1] : 0) - pc0; iw.push(tm.leader(), p, f, 0); }
+            // tail: remaining entries with small acquireCount may still fit
+            for (uint32_t j = f + 1; j < b; j++) {
+                if (!((double)(base + passed + 1) <= thr)) break;       // no c >= 1 can pass any more
+                if (!is_entry(io.flags[j])) continue;
+                int32_t c = io.cnt[j];
+                if ((double)(base + passed + c) <= thr) { passed += c; iw.push(tm.leader(), j, j + 1, 0); }
+            }
+        }
+        sec[idx].pass = wadd(sec[idx].pass, passed);
+        cur_sec_pass = wadd(cur_sec_pass, passed);
+        p = b;
+    }
+    if (tm.leader()) {
+        hc.n_items[s] = iw.n;
+        st.rstate[r0] = rs;
+    }
+}
+
+// ---------------------------------------------------------- RateLimiter
+SF_HD void heavy_rl(Team& tm, const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t s,
+                    uint32_t res, uint32_t lo, uint32_t hi) {
+    const uint32_t r0 = st.rule_off[res];
+    const DevRule rule = st.rules[r0];
+    DevRuleState rs = st.rstate[r0];
+    ItemWriter iw{hc.item_lo, hc.item_hi, hc.item_wait, lo, 0};
+    if (rule.count > 0) {
+        const int64_t cost1 = j_round(1.0 * 1 / rule.count * 1000);
+        int64_t L = rs.latest_passed;
+        uint32_t p = lo;
+        while (p < hi) {
+            const int64_t thr = L + cost1 - rule.max_queue_ms;
+            uint32_t j = team_first_true(tm, p, hi, [&](uint32_t k) { return io.ts[k] >= thr; });
+            int64_t cost = cost1;
+            for (; j < hi; j++) {
+                if (!is_entry(io.flags[j])) continue;
+                int32_t c = io.cnt[j];
+                cost = c == 1 ? cost1 : j_round(1.0 * c / rule.count * 1000);
+                if (io.ts[j] >= L + cost - rule.max_queue_ms) break;
+            }
+            if (j >= hi) break;
+            const int64_t t = io.ts[j];
+            int32_t wait = 0;
+            if (L + cost <= t) L = t;
+            else { L += cost; wait = (int32_t)(L - t); }
+            iw.push(tm.leader(), j, j + 1, wait);
+            p = j + 1;
+        }
+        rs.latest_passed = L;
+    }
+    if (tm.leader()) { hc.n_items[s] = iw.n; st.rstate[r0] = rs; }
+}
+
+// entry verdict from a segment's sorted item list (binary search)
+SF_HD bool item_lookup(const HeavyCtx& hc, uint32_t lo, uint32_t n, uint32_t j, int32_t* wait) {
+    uint32_t a = 0, b = n;                       // last item with item_lo <= j
+    while (a < b) { uint32_t m = (a + b) / 2; if (hc.item_lo[lo + m] <= j) a = m + 1; else b = m; }
+    if (a == 0) return false;
+    uint32_t k = lo + a - 1;
+    if (j < hc.item_hi[k]) { *wait = hc.item_wait[k]; return true; }
+    return false;
+}
+
+// Apply the per-window deltas of one heavy segment to its node state in
+// time order (LeapArray.currentWindow reset semantics; MetricBucket adds).
+SF_HD void heavy_apply(const DevState& st, const HeavyCtx& hc, uint32_t s, uint32_t res, uint32_t n_hw,
+                       uint32_t n_sec) {
+    const int S = st.S, wl = st.wl;
+    const int64_t h0 = hc.seg_hw0[s], s0 = hc.seg_sec0[s];
+    int64_t threads = st.threads[res];
+    for (uint32_t k = 0; k < n_hw; k++) {
+        const Acc& a = hc.acc_hw[hc.acc_hw_base[s] + k];
+        if (!a.n_touch) continue;
+        const int64_t h = h0 + k, ws = h * wl;
+        Bucket& b = st.second[(size_t)res * S + (int)(h % S)];
+        if (b.ws != ws) {
+            Bucket nb = fresh_bucket(ws, st.max_rt);
+            const Borrow& bw = st.borrow[(size_t)res * S + (int)(h % S)];
+            if (bw.ws <= ws && ws < bw.ws + wl) nb.pass = (int64_t)(int32_t)bw.pass;
+            b = nb;
+        }
+        b.pass = wadd(b.pass, (int64_t)a.pass); b.block = wadd(b.block, (int64_t)a.block);
+        b.succ = wadd(b.succ, (int64_t)a.succ); b.rt = wadd(b.rt, (int64_t)a.rt); b.exc = wadd(b.exc, (int64_t)a.exc);
+        if (a.min_rt < b.min_rt) b.min_rt = a.min_rt;
+        threads += (int64_t)a.n_pass - (int64_t)a.n_exit;
+    }
+    for (uint32_t k = 0; k < n_sec; k++) {
+        const Acc& a = hc.acc_sec[hc.acc_sec_base[s] + k];
+        if (!a.n_touch) continue;
+        const int64_t sn = s0 + k, ws = sn * 1000;
+        Bucket& b = st.minute[(size_t)res * MINUTE + (int)(sn % MINUTE)];
+        if (b.ws != ws) b = fresh_bucket(ws, st.max_rt);
+        b.pass = wadd(b.pass, (int64_t)a.pass); b.block = wadd(b.block, (int64_t)a.block);
+        b.succ = wadd(b.succ, (int64_t)a.succ); b.rt = wadd(b.rt, (int64_t)a.rt); b.exc = wadd(b.exc, (int64_t)a.exc);
+        if (a.min_rt < b.min_rt) b.min_rt = a.min_rt;
+    }
+    st.threads[res] = threads;
+}
+
+// verdict + accounting contribution of event j of a heavy item segment
+struct EvContrib { uint8_t status; int32_t wait; bool touch, passed, live_exit; int64_t c, rt; bool err; };
+SF_HD EvContrib heavy_event(const HeavyCtx& hc, const SegIO& io, uint32_t lo, uint32_t nitems, uint32_t j) {
+    EvContrib r{};
+    const uint8_t f = io.flags[j];
+    r.c = io.cnt[j];
+    if (is_entry(f)) {
+        int32_t w = 0;
+        r.passed = item_lookup(hc, lo, nitems, j, &w);
+        r.status = r.passed ? (w > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : SF_V_BLOCK_FLOW;
+        r.wait = r.passed ? w : 0;
+        r.touch = true;
+    } else {
+        int64_t ref = io.eref ? io.eref[j] : -1;
+        bool live; int64_t cts;
+        if (ref >= 0) { int32_t w; live = item_lookup(hc, lo, nitems, (uint32_t)ref, &w); cts = io.ts[ref]; }
+        else { live = true; cts = io.cts ? io.cts[j] : io.ts[j]; }
+        r.status = live ? SF_V_EXIT : SF_V_EXIT_IGNORED;
+        r.live_exit = live; r.touch = live;
+        r.rt = io.ts[j] - cts;
+        r.err = (f & SF_EV_ERROR) != 0;
+    }
+    return r;
+}
+
+}  // namespace sf

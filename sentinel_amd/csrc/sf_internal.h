@@ -92,6 +92,16 @@ struct Work {
     uint8_t* v_status; int32_t* v_wait; uint16_t* v_rule;
     void* sort_tmp; size_t sort_tmp_bytes;
     void* scan_tmp; size_t scan_tmp_bytes;
+    // heavy / light split (sf_heavy.h)
+    uint32_t seg_cap;                                   // min(max_batch, R)
+    uint32_t* segflag; uint8_t* seg_mode;
+    uint32_t* light_list; uint32_t* heavy_list; uint32_t* counters;   // [0] n_light [1] n_heavy [2] hw slots [3] sec slots
+    int64_t* pcg; void* pscan_tmp; size_t pscan_tmp_bytes;
+    uint32_t* item_lo; uint32_t* item_hi; int32_t* item_wait; uint32_t* n_items;
+    void* acc_hw; void* acc_sec; uint32_t acc_cap;
+    uint32_t* acc_hw_base; uint32_t* acc_sec_base; int64_t* seg_hw0; int64_t* seg_sec0;
+    uint32_t* seg_nhw; uint32_t* seg_nsec;
+    uint32_t heavy_min;                                 // segments longer than this go heavy
 };
 
 // Device view of a caller batch (pointers already on device).
@@ -104,10 +114,12 @@ struct DevBatch {
 struct DevVerdicts { uint8_t* status; int32_t* wait; uint16_t* rule; };
 
 // ---- launchers (sf_kernels.hip) ----
-hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes);
+hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes,
+                            size_t* pscan_bytes);
 hipError_t launch_init_state(const DevState& st, hipStream_t s);
 hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                            uint32_t shard_count, uint32_t shard_index, uint32_t key_bits,
-                           hipStream_t s, hipEvent_t* ev /* 5 events or null */);
+                           hipStream_t s, hipStream_t s2, hipEvent_t* ev /* 7 events */, bool timing);
+constexpr size_t ACC_BYTES = 72;                         // sizeof(Acc)
 
 }  // namespace sf

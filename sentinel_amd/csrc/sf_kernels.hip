@@ -1,17 +1,22 @@
 // sf_kernels.hip — gfx950 kernels of one sf_submit (product code).
 //
-// Pipeline (one HIP stream, no host round trip inside):
+// Pipeline (two HIP streams, no host round trip inside):
 //   k_keys      validate + map resource ids to shard-local keys, iota values
 //   radix sort  stable (key, index) sort by resource: per-resource time order
 //               is the input order (LeapArray semantics need it)
 //   k_heads + exclusive scan + k_segments   segment table of touched resources
-//   k_gather    events into sorted order (SoA), inverse permutation for EXIT refs
-//   k_decide    one lane per resource segment: the exact interpreter (sf_decide.h)
+//   k_gather    events into sorted order (SoA), inverse permutation, per-segment flags
+//   pc scan     inclusive prefix of entry acquireCount (heavy window budgets)
+//   k_classify  light segments -> lane interpreter; heavy -> window/skip algorithms
+//   stream A:   k_decide_light  one lane per light segment (sf_decide.h)
+//   stream B:   k_heavy_decide  one workgroup per heavy segment (sf_heavy.h)
+//               k_heavy_fill    verdicts + per-window counter deltas, device-wide
+//               k_heavy_apply   deltas applied to the LeapArray state in time order
 //   k_scatter   verdicts back to submission order
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
-#include "sf_decide.h"
+#include "sf_heavy.h"
 
 namespace sf {
 
@@ -44,22 +49,28 @@ __global__ void k_heads(const uint32_t* keys, uint32_t n, uint32_t* head) {
 }
 
 __global__ void k_segments(const uint32_t* keys, const uint32_t* head, const uint32_t* pos, uint32_t n,
-                           uint32_t* seg_start, uint32_t* seg_res, uint32_t* n_seg) {
+                           uint32_t* seg_start, uint32_t* seg_res, uint32_t* n_seg, uint32_t* segflag) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
-    if (head[j]) { seg_start[pos[j]] = j; seg_res[pos[j]] = keys[j]; }
+    if (head[j]) { seg_start[pos[j]] = j; seg_res[pos[j]] = keys[j]; segflag[pos[j]] = 0; }
     if (j == n - 1) { uint32_t ns = pos[j] + head[j]; *n_seg = ns; seg_start[ns] = n; }
 }
 
 __global__ void k_gather(DevBatch b, const uint32_t* perm, int64_t* s_ts, int32_t* s_cnt, uint8_t* s_flags,
-                         uint32_t* inv, uint8_t* s_nargs, uint8_t* s_atag, uint64_t* s_abits) {
+                         uint32_t* inv, uint8_t* s_nargs, uint8_t* s_atag, uint64_t* s_abits,
+                         const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
     uint32_t i = perm[j];
-    s_ts[j] = b.ts[i];
-    s_cnt[j] = b.cnt[i];
-    s_flags[j] = b.flags[i];
+    int64_t t = b.ts[i];
+    int32_t c = b.cnt[i];
+    uint8_t f = b.flags[i];
+    s_ts[j] = t; s_cnt[j] = c; s_flags[j] = f;
     if (inv) inv[i] = j;
+    if (!(f & SF_EV_EXIT) && ((f & SF_EV_PRIO) || c <= 0)) {
+        uint32_t s = head_scan[j] + head[j] - 1;
+        atomicOr(&segflag[s], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u));
+    }
     if (b.arg_slots) {
         if (b.nargs) s_nargs[j] = b.nargs[i];
         for (uint32_t a = 0; a < b.arg_slots; a++) {
@@ -80,12 +91,175 @@ __global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint32_t* 
     s_cts[j] = b.cts ? b.cts[i] : 0;
 }
 
-template <int MAXS>
-__global__ void __launch_bounds__(128) k_decide(DevState st, SegIO io, const uint32_t* seg_start,
-                                                const uint32_t* seg_res, const uint32_t* n_seg) {
+struct EntryCount {     // acquireCount of entries, 0 for exits (input of the pc scan)
+    const int32_t* cnt; const uint8_t* flags;
+    __device__ int64_t operator()(uint32_t j) const { return (flags[j] & SF_EV_EXIT) ? 0 : (int64_t)cnt[j]; }
+};
+
+// Route each segment: light lane interpreter, heavy window algorithms, or the
+// heavy generic interpreter (one lane of a workgroup).
+__global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= *n_seg) return;
+    if (s >= *w.n_seg) return;
+    const uint32_t lo = w.seg_start[s], hi = w.seg_start[s + 1], res = w.seg_res[s];
+    if (hi - lo <= w.heavy_min) {
+        w.seg_mode[s] = SM_LIGHT;
+        w.light_list[atomicAdd(&w.counters[0], 1u)] = s;
+        return;
+    }
+    uint8_t mode = heavy_mode(st, res, w.segflag[s], s_ts[lo]);
+    if (mode != SM_GENERIC) {
+        const int64_t h0 = s_ts[lo] / st.wl, h1 = s_ts[hi - 1] / st.wl;
+        const int64_t s0 = s_ts[lo] / 1000, s1 = s_ts[hi - 1] / 1000;
+        const int64_t nh = h1 - h0 + 1, ns = s1 - s0 + 1;
+        if (nh > 65536 || ns > 65536) mode = SM_GENERIC;
+        else {
+            uint32_t bh = atomicAdd(&w.counters[2], (uint32_t)nh);
+            uint32_t bs = atomicAdd(&w.counters[3], (uint32_t)ns);
+            if ((uint64_t)bh + nh > w.acc_cap || (uint64_t)bs + ns > w.acc_cap) mode = SM_GENERIC;
+            else {
+                w.acc_hw_base[s] = bh; w.acc_sec_base[s] = bs;
+                w.seg_hw0[s] = h0; w.seg_sec0[s] = s0; w.seg_nhw[s] = (uint32_t)nh; w.seg_nsec[s] = (uint32_t)ns;
+                Acc z{}; z.min_rt = INT64_MAX;
+                Acc* ah = (Acc*)w.acc_hw; Acc* as = (Acc*)w.acc_sec;
+                for (int64_t k = 0; k < nh; k++) ah[bh + k] = z;
+                for (int64_t k = 0; k < ns; k++) as[bs + k] = z;
+            }
+        }
+    }
+    w.seg_mode[s] = mode;
+    w.heavy_list[atomicAdd(&w.counters[1], 1u)] = s;
+}
+
+template <int MAXS>
+__global__ void __launch_bounds__(128) k_decide_light(DevState st, SegIO io, const uint32_t* seg_start,
+                                                      const uint32_t* seg_res, const uint32_t* list,
+                                                      const uint32_t* count) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= *count) return;
+    uint32_t s = list[t];
     decide_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
+}
+
+static HeavyCtx heavy_ctx(const Work& w) {
+    HeavyCtx hc;
+    hc.seg_start = w.seg_start; hc.seg_res = w.seg_res; hc.seg_mode = w.seg_mode;
+    hc.heavy_list = w.heavy_list; hc.n_heavy = w.counters + 1; hc.pcg = w.pcg;
+    hc.item_lo = w.item_lo; hc.item_hi = w.item_hi; hc.item_wait = w.item_wait; hc.n_items = w.n_items;
+    hc.acc_hw = (Acc*)w.acc_hw; hc.acc_sec = (Acc*)w.acc_sec;
+    hc.acc_hw_base = w.acc_hw_base; hc.acc_sec_base = w.acc_sec_base;
+    hc.seg_hw0 = w.seg_hw0; hc.seg_sec0 = w.seg_sec0;
+    return hc;
+}
+
+template <int MAXS>
+__global__ void __launch_bounds__(256) k_heavy_decide(DevState st, SegIO io, HeavyCtx hc) {
+    __shared__ long long red[16];
+    if (blockIdx.x >= *hc.n_heavy) return;
+    const uint32_t s = hc.heavy_list[blockIdx.x];
+    const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1], res = hc.seg_res[s];
+    Team tm{(int)threadIdx.x, (int)blockDim.x, red};
+    switch (hc.seg_mode[s]) {
+    case SM_QPS: heavy_qps(tm, st, io, hc, s, res, lo, hi, false); break;
+    case SM_WARM: heavy_qps(tm, st, io, hc, s, res, lo, hi, true); break;
+    case SM_RL: heavy_rl(tm, st, io, hc, s, res, lo, hi); break;
+    case SM_NORULE:
+        if (tm.leader()) { hc.item_lo[lo] = lo; hc.item_hi[lo] = hi; hc.item_wait[lo] = 0; hc.n_items[s] = 1; }
+        break;
+    default:
+        if (tm.leader()) decide_segment<MAXS>(st, io, res, lo, hi);
+        break;
+    }
+}
+
+struct PAcc {            // per-thread partial of one accumulator slot
+    unsigned long long pass, block, succ, rt, exc, n_pass, n_exit, n_touch;
+    long long min_rt;
+    __device__ void clear() { pass = block = succ = rt = exc = n_pass = n_exit = n_touch = 0; min_rt = INT64_MAX; }
+    __device__ void add(const EvContrib& e) {
+        n_touch++;
+        if (e.live_exit) {
+            succ += (unsigned long long)e.c; rt += (unsigned long long)e.rt; n_exit++;
+            if (e.err) exc += (unsigned long long)e.c;
+            if (e.rt < min_rt) min_rt = e.rt;
+        } else if (e.passed) { pass += (unsigned long long)e.c; n_pass++; }
+        else block += (unsigned long long)e.c;
+    }
+    __device__ void flush(Acc* table, uint32_t key) const {
+        if (!n_touch) return;
+        Acc* a = table + key;
+        atomicAdd(&a->pass, pass); atomicAdd(&a->block, block); atomicAdd(&a->succ, succ);
+        atomicAdd(&a->rt, rt); atomicAdd(&a->exc, exc); atomicAdd(&a->n_pass, n_pass);
+        atomicAdd(&a->n_exit, n_exit); atomicAdd(&a->n_touch, n_touch);
+        if (min_rt != INT64_MAX) atomicMin(&a->min_rt, min_rt);
+    }
+};
+
+__device__ unsigned long long wave_sum(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ long long wave_min(long long v) {
+    for (int o = 32; o > 0; o >>= 1) { long long u = __shfl_xor(v, o); v = u < v ? u : v; }
+    return v;
+}
+// flush at wave level: one set of atomics per wave when all active lanes share a key
+__device__ void wave_flush(PAcc& p, uint32_t key, Acc* table) {
+    const uint32_t NONE = 0xffffffffu;
+    bool act = key != NONE && p.n_touch;
+    unsigned long long m = __ballot(act);
+    if (!m) return;
+    int l0 = __ffsll((long long)m) - 1;
+    uint32_t k0 = __shfl(key, l0);
+    bool differ = __ballot(act && key != k0) != 0;
+    if (differ) { if (act) p.flush(table, key); return; }
+    if (!act) p.clear();
+    PAcc r;
+    r.pass = wave_sum(p.pass); r.block = wave_sum(p.block); r.succ = wave_sum(p.succ); r.rt = wave_sum(p.rt);
+    r.exc = wave_sum(p.exc); r.n_pass = wave_sum(p.n_pass); r.n_exit = wave_sum(p.n_exit);
+    r.n_touch = wave_sum(p.n_touch); r.min_rt = wave_min(p.min_rt);
+    if ((int)(threadIdx.x & 63) == l0) r.flush(table, k0);
+}
+
+constexpr int FILL_ITERS = 16;
+__global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, HeavyCtx hc, const uint32_t* head,
+                                                    const uint32_t* head_scan) {
+    const uint32_t NONE = 0xffffffffu;
+    const uint32_t base = blockIdx.x * (256 * FILL_ITERS);
+    PAcc ph, ps; ph.clear(); ps.clear();
+    uint32_t kh = NONE, ks = NONE;
+    for (int it = 0; it < FILL_ITERS; it++) {
+        const uint32_t j = base + it * 256 + threadIdx.x;
+        if (j >= io.n) break;
+        const uint32_t s = head_scan[j] + head[j] - 1;
+        const uint8_t mode = hc.seg_mode[s];
+        if (mode < SM_QPS) continue;
+        const uint32_t lo = hc.seg_start[s];
+        if (io.eref && !is_entry(io.flags[j])) {
+            int64_t r = io.eref[j];
+            if (r >= 0 && (r < (int64_t)lo || r >= (int64_t)j || !is_entry(io.flags[r]))) { *st.err = SF_ERR_INVALID; }
+        }
+        EvContrib e = heavy_event(hc, io, lo, hc.n_items[s], j);
+        io.v_status[j] = e.status;
+        if (io.v_wait) io.v_wait[j] = e.wait;
+        if (io.v_rule) io.v_rule[j] = 0;
+        if (!e.touch) continue;
+        const uint32_t key_h = hc.acc_hw_base[s] + (uint32_t)(io.ts[j] / st.wl - hc.seg_hw0[s]);
+        const uint32_t key_s = hc.acc_sec_base[s] + (uint32_t)(io.ts[j] / 1000 - hc.seg_sec0[s]);
+        if (key_h != kh) { if (kh != NONE) ph.flush(hc.acc_hw, kh); ph.clear(); kh = key_h; }
+        if (key_s != ks) { if (ks != NONE) ps.flush(hc.acc_sec, ks); ps.clear(); ks = key_s; }
+        ph.add(e); ps.add(e);
+    }
+    wave_flush(ph, kh, hc.acc_hw);
+    wave_flush(ps, ks, hc.acc_sec);
+}
+
+__global__ void k_heavy_apply(DevState st, HeavyCtx hc, const uint32_t* seg_nhw, const uint32_t* seg_nsec) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= *hc.n_heavy) return;
+    const uint32_t s = hc.heavy_list[t];
+    if (hc.seg_mode[s] < SM_QPS) return;
+    heavy_apply(st, hc, s, hc.seg_res[s], seg_nhw[s], seg_nsec[s]);
 }
 
 __global__ void k_scatter(const uint32_t* perm, uint32_t n, const uint8_t* vs, const int32_t* vw,
@@ -100,12 +274,19 @@ __global__ void k_scatter(const uint32_t* perm, uint32_t n, const uint8_t* vs, c
 
 static inline unsigned blocks(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes) {
+using PcIter = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, EntryCount, int64_t>;
+
+hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes,
+                            size_t* pscan_bytes) {
     hipError_t e = rocprim::radix_sort_pairs(nullptr, *sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                              (uint32_t*)nullptr, (uint32_t*)nullptr, max_n, 0u, key_bits);
     if (e != hipSuccess) return e;
-    return rocprim::exclusive_scan(nullptr, *scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
-                                   (size_t)max_n, rocprim::plus<uint32_t>());
+    e = rocprim::exclusive_scan(nullptr, *scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
+                                (size_t)max_n, rocprim::plus<uint32_t>());
+    if (e != hipSuccess) return e;
+    PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{nullptr, nullptr});
+    return rocprim::inclusive_scan(nullptr, *pscan_bytes, it, (int64_t*)nullptr, (size_t)max_n,
+                                   rocprim::plus<int64_t>());
 }
 
 hipError_t launch_init_state(const DevState& st, hipStream_t s) {
@@ -116,11 +297,11 @@ hipError_t launch_init_state(const DevState& st, hipStream_t s) {
 
 hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                            uint32_t shard_count, uint32_t shard_index, uint32_t key_bits,
-                           hipStream_t s, hipEvent_t* ev) {
+                           hipStream_t s, hipStream_t s2, hipEvent_t* ev, bool timing) {
     const uint32_t n = b.n;
     if (n == 0) return hipSuccess;
     const unsigned T = 256;
-    if (ev) hipEventRecord(ev[0], s);
+    if (timing) hipEventRecord(ev[0], s);
     hipLaunchKernelGGL(k_keys, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.vals_in, shard_count,
                        shard_index, st.R, st.err);
     hipError_t e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.vals_in,
@@ -131,32 +312,54 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
                                 rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_segments, dim3(blocks(n, T)), dim3(T), 0, s, w.keys_out, w.head, w.head_scan, n,
-                       w.seg_start, w.seg_res, w.n_seg);
-    if (ev) hipEventRecord(ev[1], s);
+                       w.seg_start, w.seg_res, w.n_seg, w.segflag);
+    if (timing) hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_gather, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_ts, w.s_cnt, w.s_flags,
-                       b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits);
+                       b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag);
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.inv, w.s_eref,
                            w.s_cts, st.err);
-    if (ev) hipEventRecord(ev[2], s);
+    PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
+    e = rocprim::inclusive_scan(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n, rocprim::plus<int64_t>(), s);
+    if (e != hipSuccess) return e;
+    hipMemsetAsync(w.counters, 0, 4 * sizeof(uint32_t), s);
+    const uint32_t max_seg = n < st.R ? n : st.R;
+    hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, T)), dim3(T), 0, s, st, w, w.s_ts);
+    if (timing) hipEventRecord(ev[2], s);
+
     SegIO io;
     io.ts = w.s_ts; io.cnt = w.s_cnt; io.flags = w.s_flags;
     io.eref = b.eref ? w.s_eref : nullptr; io.cts = b.eref ? w.s_cts : nullptr;
     io.arg_slots = b.arg_slots; io.nargs = (b.arg_slots && b.nargs) ? w.s_nargs : nullptr;
     io.atag = w.s_atag; io.abits = w.s_abits; io.n = n;
     io.v_status = w.v_status; io.v_wait = w.v_wait; io.v_rule = w.v_rule;
-    uint32_t max_seg = n < st.R ? n : st.R;
+    HeavyCtx hc = heavy_ctx(w);
+
+    // heavy segments on the second stream, overlapping the light lanes
+    hipEventRecord(ev[5], s);                      // fork
+    hipStreamWaitEvent(s2, ev[5], 0);
+    const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
+    if (st.S <= 2)
+        hipLaunchKernelGGL(k_heavy_decide<2>, dim3(max_heavy), dim3(256), 0, s2, st, io, hc);
+    else
+        hipLaunchKernelGGL(k_heavy_decide<SF_MAX_SAMPLE_COUNT>, dim3(max_heavy), dim3(256), 0, s2, st, io, hc);
+    hipLaunchKernelGGL(k_heavy_fill, dim3(blocks(n, 256 * FILL_ITERS)), dim3(256), 0, s2, st, io, hc, w.head,
+                       w.head_scan);
+    hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, w.seg_nhw, w.seg_nsec);
+
     const unsigned TD = 128;
     if (st.S <= 2)
-        hipLaunchKernelGGL(k_decide<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s, st, io, w.seg_start,
-                           w.seg_res, w.n_seg);
+        hipLaunchKernelGGL(k_decide_light<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s, st, io, w.seg_start,
+                           w.seg_res, w.light_list, w.counters);
     else
-        hipLaunchKernelGGL(k_decide<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s, st, io,
-                           w.seg_start, w.seg_res, w.n_seg);
-    if (ev) hipEventRecord(ev[3], s);
+        hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s, st, io,
+                           w.seg_start, w.seg_res, w.light_list, w.counters);
+    hipEventRecord(ev[6], s2);                     // join
+    hipStreamWaitEvent(s, ev[6], 0);
+    if (timing) hipEventRecord(ev[3], s);
     hipLaunchKernelGGL(k_scatter, dim3(blocks(n, T)), dim3(T), 0, s, w.perm, n, w.v_status, w.v_wait,
                        w.v_rule, out);
-    if (ev) hipEventRecord(ev[4], s);
+    if (timing) hipEventRecord(ev[4], s);
     return hipGetLastError();
 }
 

@@ -1,16 +1,16 @@
-// TEST-ONLY host build of the engine's decision interpreter (sf_decide.h).
+// TEST-ONLY host build of the engine's decision code (sf_decide.h, sf_heavy.h).
 //
-// Runs the exact per-resource kernel body on the CPU so the device logic can be
-// checked against the oracle in the CPU test suite (no GPU in the build
-// container).  It is never loaded by the product: libsentinel_flow.so has no
-// path to it, and sf_create fails without a gfx950 device.
+// Runs the exact device algorithms on the CPU (heavy teams of size 1) with the
+// same routing as the HIP pipeline, so the CPU suite can check the kernel
+// logic against the oracle.  Never loaded by the product: libsentinel_flow.so
+// has no path to it, and sf_create fails without a gfx950 device.
 #include <cstdio>
 #include <algorithm>
 #include <cstring>
 #include <numeric>
 #include <vector>
 
-#include "../../sentinel_amd/csrc/sf_decide.h"
+#include "../../sentinel_amd/csrc/sf_heavy.h"
 
 using namespace sf;
 
@@ -30,6 +30,8 @@ struct hs_engine {
     std::vector<ParamSlot> ptab;
     int32_t err = 0;
     uint32_t R;
+    uint32_t heavy_min;
+    uint64_t n_heavy_segments = 0, n_heavy_item_segments = 0;
     void refresh() {
         st.second = second.data(); st.borrow = borrow.data(); st.minute = minute.data();
         st.threads = threads.data(); st.rule_off = rule_off.data(); st.rules = rules.data();
@@ -45,6 +47,7 @@ hs_engine* hs_create(const sf_config* c) {
     hs_engine* e = new hs_engine();
     e->cfg = *c;
     e->R = c->max_resources;
+    e->heavy_min = c->heavy_min_events ? c->heavy_min_events : 512;
     size_t R = e->R, S = c->sample_count;
     e->second.assign(R * S, fresh_bucket(WS_NONE, c->statistic_max_rt));
     e->borrow.assign(R * S, Borrow{WS_NONE, 0});
@@ -113,7 +116,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     for (uint32_t i = 0; i < n; i++) if (!local_of(e, in->res_id[i], &key[i])) return SF_ERR_INVALID;
     std::iota(perm.begin(), perm.end(), 0u);
     std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
-    std::vector<int64_t> ts(n), eref(n, -1), cts(n, 0);
+    std::vector<int64_t> ts(n), eref(n, -1), cts(n, 0), pcg(n);
     std::vector<int32_t> cnt(n);
     std::vector<uint8_t> fl(n), nargs(n), atag((size_t)n * in->arg_slots), vs(n);
     std::vector<uint64_t> abits((size_t)n * in->arg_slots);
@@ -126,6 +129,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
             atag[(size_t)a * n + j] = in->arg_tag[(size_t)a * n + i];
             abits[(size_t)a * n + j] = in->arg_bits[(size_t)a * n + i];
         }
+        pcg[j] = (j ? pcg[j - 1] : 0) + ((fl[j] & SF_EV_EXIT) ? 0 : (int64_t)cnt[j]);
     }
     if (in->entry_ref)
         for (uint32_t j = 0; j < n; j++) {
@@ -136,14 +140,70 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     SegIO io{ts.data(), cnt.data(), fl.data(), in->entry_ref ? eref.data() : nullptr,
              in->entry_ref ? cts.data() : nullptr, in->arg_slots, in->n_args ? nargs.data() : nullptr,
              atag.data(), abits.data(), n, vs.data(), vw.data(), vr.data()};
-    uint32_t lo = 0;
-    while (lo < n) {
-        uint32_t hi = lo;
-        while (hi < n && key[perm[hi]] == key[perm[lo]]) hi++;
-        if (e->st.S <= 2) decide_segment<2>(e->st, io, key[perm[lo]], lo, hi);
-        else decide_segment<SF_MAX_SAMPLE_COUNT>(e->st, io, key[perm[lo]], lo, hi);
-        lo = hi;
+    // segments + routing (k_segments / k_classify)
+    std::vector<uint32_t> seg_start, seg_res, segflag;
+    for (uint32_t j = 0; j < n; j++) {
+        if (j == 0 || key[perm[j]] != key[perm[j - 1]]) { seg_start.push_back(j); seg_res.push_back(key[perm[j]]); segflag.push_back(0); }
+        if (!(fl[j] & SF_EV_EXIT) && ((fl[j] & SF_EV_PRIO) || cnt[j] <= 0))
+            segflag.back() |= ((fl[j] & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (cnt[j] <= 0 ? SEGF_NONPOS : 0u);
     }
+    const uint32_t ns = (uint32_t)seg_start.size();
+    seg_start.push_back(n);
+    std::vector<uint8_t> mode(ns);
+    std::vector<uint32_t> ilo(n), ihi(n), nitems(ns), hwb(ns), secb(ns), nhw(ns), nsec(ns);
+    std::vector<int32_t> iwait(n);
+    std::vector<int64_t> hw0(ns), sec0(ns);
+    std::vector<Acc> acc_hw, acc_sec;
+    for (uint32_t s = 0; s < ns; s++) {
+        uint32_t lo = seg_start[s], hi = seg_start[s + 1];
+        if (hi - lo <= e->heavy_min) { mode[s] = SM_LIGHT; continue; }
+        e->n_heavy_segments++;
+        mode[s] = heavy_mode(e->st, seg_res[s], segflag[s], ts[lo]);
+        if (mode[s] != SM_GENERIC) {
+            e->n_heavy_item_segments++;
+            hw0[s] = ts[lo] / e->st.wl; sec0[s] = ts[lo] / 1000;
+            nhw[s] = (uint32_t)(ts[hi - 1] / e->st.wl - hw0[s] + 1); nsec[s] = (uint32_t)(ts[hi - 1] / 1000 - sec0[s] + 1);
+            hwb[s] = (uint32_t)acc_hw.size(); secb[s] = (uint32_t)acc_sec.size();
+            Acc z{}; z.min_rt = INT64_MAX;
+            acc_hw.resize(acc_hw.size() + nhw[s], z); acc_sec.resize(acc_sec.size() + nsec[s], z);
+        }
+    }
+    HeavyCtx hc{seg_start.data(), seg_res.data(), mode.data(), nullptr, nullptr, pcg.data(), ilo.data(), ihi.data(),
+                iwait.data(), nitems.data(), acc_hw.data(), acc_sec.data(), hwb.data(), secb.data(), hw0.data(), sec0.data()};
+    for (uint32_t s = 0; s < ns; s++) {
+        uint32_t lo = seg_start[s], hi = seg_start[s + 1], res = seg_res[s];
+        Team tm;
+        switch (mode[s]) {
+        case SM_QPS: heavy_qps(tm, e->st, io, hc, s, res, lo, hi, false); break;
+        case SM_WARM: heavy_qps(tm, e->st, io, hc, s, res, lo, hi, true); break;
+        case SM_RL: heavy_rl(tm, e->st, io, hc, s, res, lo, hi); break;
+        case SM_NORULE: ilo[lo] = lo; ihi[lo] = hi; iwait[lo] = 0; nitems[s] = 1; break;
+        default:
+            if (e->st.S <= 2) decide_segment<2>(e->st, io, res, lo, hi);
+            else decide_segment<SF_MAX_SAMPLE_COUNT>(e->st, io, res, lo, hi);
+        }
+    }
+    // k_heavy_fill
+    for (uint32_t s = 0; s < ns; s++) {
+        if (mode[s] < SM_QPS) continue;
+        for (uint32_t j = seg_start[s]; j < seg_start[s + 1]; j++) {
+            EvContrib c = heavy_event(hc, io, seg_start[s], nitems[s], j);
+            vs[j] = c.status; vw[j] = c.wait; vr[j] = 0;
+            if (!c.touch) continue;
+            for (int t = 0; t < 2; t++) {
+                Acc& a = t == 0 ? acc_hw[hwb[s] + (ts[j] / e->st.wl - hw0[s])] : acc_sec[secb[s] + (ts[j] / 1000 - sec0[s])];
+                a.n_touch++;
+                if (c.live_exit) {
+                    a.succ += c.c; a.rt += c.rt; a.n_exit++; if (c.err) a.exc += c.c;
+                    if (c.rt < a.min_rt) a.min_rt = c.rt;
+                } else if (c.passed) { a.pass += c.c; a.n_pass++; }
+                else a.block += c.c;
+            }
+        }
+    }
+    // k_heavy_apply
+    for (uint32_t s = 0; s < ns; s++)
+        if (mode[s] >= SM_QPS) heavy_apply(e->st, hc, s, seg_res[s], nhw[s], nsec[s]);
     for (uint32_t j = 0; j < n; j++) {
         uint32_t i = perm[j];
         ((uint8_t*)out->status)[i] = vs[j];
@@ -152,6 +212,8 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     }
     return e->err;
 }
+
+void hs_heavy_stats(hs_engine* e, uint64_t* heavy, uint64_t* items) { *heavy = e->n_heavy_segments; *items = e->n_heavy_item_segments; }
 
 int hs_read_node(hs_engine* e, uint32_t res, sf_node_state* out) {
     uint32_t l; if (!local_of(e, res, &l)) return SF_ERR_INVALID;

@@ -17,13 +17,28 @@ def eng_mod():
     return engine
 
 
+@pytest.mark.parametrize("heavy_min", [0, 8])
 @pytest.mark.parametrize("name", list(workloads.ALL))
-def test_workload(eng_mod, so, name):
-    workloads.run(eng_mod.FlowEngine, so.OracleEngine, workloads.ALL[name]())
+def test_workload(eng_mod, so, name, heavy_min):
+    w = workloads.ALL[name]()
+    w["cfg"].heavy_min_events = heavy_min
+    workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
 
 
-def test_config3_many_batches(eng_mod, so):
-    workloads.run(eng_mod.FlowEngine, so.OracleEngine, workloads.config3(R=20_000, n=600_000, seed=17, split=5))
+@pytest.mark.parametrize("heavy_min", [0, 64])
+def test_config3_many_batches(eng_mod, so, heavy_min):
+    w = workloads.config3(R=20_000, n=600_000, seed=17, split=5)
+    w["cfg"].heavy_min_events = heavy_min
+    workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_heavy_edge_traces(eng_mod, so, seed):
+    from tests.test_hostsim_parity import test_heavy_edge_traces as body
+    import types
+    # reuse the CPU edge-trace builder with the GPU engine
+    fake_hs = types.SimpleNamespace(HostSimEngine=eng_mod.FlowEngine)
+    body(fake_hs, so, seed)
 
 
 def test_device_resident_batch(eng_mod, so):

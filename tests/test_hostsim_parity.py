@@ -1,6 +1,10 @@
-"""CPU check of the engine's decision interpreter (sf_decide.h, host build)
-against the oracle on every seeded parity workload.  The GPU parity suite
+"""CPU check of the engine's decision code (sf_decide.h + sf_heavy.h, host
+build) against the oracle on every seeded parity workload, both with the
+default light/heavy split and with a tiny heavy threshold so the window/skip
+algorithms run on every non-trivial segment.  The GPU parity suite
 (test_gpu_parity.py) runs the same workloads through libsentinel_flow.so."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -11,14 +15,17 @@ from tests import workloads
 @pytest.fixture(scope="module")
 def hs():
     from tests.hostsim import hostsim
-    hostsim.lib()
+    L = hostsim.lib()
+    L.hs_heavy_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     return hostsim
 
 
+@pytest.mark.parametrize("heavy_min", [0, 8])
 @pytest.mark.parametrize("name", list(workloads.ALL))
-def test_workload(hs, so, name):
+def test_workload(hs, so, name, heavy_min):
     w = workloads.ALL[name]()
-    _, _, outs = workloads.run(hs.HostSimEngine, so.OracleEngine, w)
+    w["cfg"].heavy_min_events = heavy_min
+    eng, _, outs = workloads.run(hs.HostSimEngine, so.OracleEngine, w)
     if name == "config1":
         b = w["batches"][0]
         st = outs[0][1].status
@@ -29,7 +36,51 @@ def test_workload(hs, so, name):
         assert (c[:-1] + c[1:]).max() <= 20     # FlowQpsDemo: <= 20 passes per 1 s window
     if name == "prioritized":
         assert (outs[0][1].status == abi.V_PRIORITY_WAIT).sum() > 0
+    if heavy_min and name in ("config1", "config2", "config3"):
+        h, it = C.c_uint64(), C.c_uint64()
+        hs.lib().hs_heavy_stats(eng.h, C.byref(h), C.byref(it))
+        assert it.value > 0, "window/skip path not exercised"
 
 
-def test_config3_two_seeds(hs, so):
-    workloads.run(hs.HostSimEngine, so.OracleEngine, workloads.config3(seed=11, split=3))
+@pytest.mark.parametrize("heavy_min", [0, 4])
+def test_config3_more_seeds(hs, so, heavy_min):
+    for seed in (11, 23):
+        w = workloads.config3(seed=seed, split=3)
+        w["cfg"].heavy_min_events = heavy_min
+        workloads.run(hs.HostSimEngine, so.OracleEngine, w)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_heavy_edge_traces(hs, so, seed):
+    """Dense single-resource traces with mixed acquireCount, long gaps, second
+    boundaries and exits, through every heavy class at threshold 2."""
+    rng = np.random.default_rng(100 + seed)
+    R = 4
+    rules = [abi.sf_flow_rule(resource=0, grade=abi.GRADE_QPS, count=float(rng.integers(1, 30)), control_behavior=0,
+                              warm_up_period_sec=10, max_queueing_time_ms=500),
+             abi.sf_flow_rule(resource=1, grade=abi.GRADE_QPS, count=float(rng.integers(5, 60)), control_behavior=1,
+                              warm_up_period_sec=int(rng.integers(1, 5)), max_queueing_time_ms=500),
+             abi.sf_flow_rule(resource=2, grade=abi.GRADE_QPS, count=float(rng.integers(1, 200)), control_behavior=2,
+                              warm_up_period_sec=10, max_queueing_time_ms=int(rng.integers(1, 900)))]
+    n = 40000
+    gaps = rng.choice([0, 0, 0, 1, 2, 7, 450, 1700], size=n)
+    ts = 1_700_000_000_000 + np.cumsum(gaps)
+    res = rng.integers(0, R, n).astype(np.uint32)
+    cnt = np.where(rng.random(n) < 0.7, 1, rng.integers(1, 7, n)).astype(np.int32)
+    flags = np.full(n, abi.EV_IN, np.uint8)
+    # exits for a third of the entries, 0..50 ms later
+    ent = np.nonzero(rng.random(n) < 0.33)[0]
+    ex_ts = ts[ent] + rng.integers(0, 50, ent.size)
+    all_ts = np.concatenate([ts, ex_ts])
+    key = np.lexsort((np.concatenate([np.zeros(n), np.ones(ent.size)]), all_ts))
+    pos = np.empty(key.size, np.int64)
+    pos[key] = np.arange(key.size)
+    src = np.concatenate([np.arange(n), ent])
+    fl = np.concatenate([flags, np.full(ent.size, abi.EV_EXIT | abi.EV_IN, np.uint8)])
+    eref = np.full(key.size, -1, np.int64)
+    eref[pos[n:]] = pos[ent]
+    b = abi.HostBatch(res[src][key], all_ts[key], cnt[src][key], fl[key], entry_ref=eref)
+    half = b.n // 2
+    w = dict(cfg=abi.default_config(max_resources=R, max_batch=b.n, heavy_min_events=2), flow=rules,
+             batches=[b.subset(0, half), b.subset(half, b.n)], nodes=list(range(R)), n_flow=3)
+    workloads.run(hs.HostSimEngine, so.OracleEngine, w)
