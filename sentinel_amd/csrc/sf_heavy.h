@@ -26,7 +26,7 @@
 namespace sf {
 
 // segment modes (seg_mode[s])
-enum : uint8_t { SM_LIGHT = 0, SM_GENERIC = 1, SM_QPS = 2, SM_WARM = 3, SM_RL = 4, SM_NORULE = 5 };
+enum : uint8_t { SM_LIGHT = 0, SM_GENERIC = 1, SM_QPS = 2, SM_WARM = 3, SM_RL = 4, SM_NORULE = 5, SM_THREAD = 6 };
 constexpr uint32_t SEGF_PRIO = 1u, SEGF_NONPOS = 2u;
 
 struct Acc {            // per (segment, window) counter deltas
@@ -55,6 +55,7 @@ SF_HD uint8_t heavy_mode(const DevState& st, uint32_t res, uint32_t segflags, in
     if (r.kind == CT_DEFAULT && r.grade == SF_GRADE_QPS) return SM_QPS;
     if (r.kind == CT_WARM_UP) return SM_WARM;
     if (r.kind == CT_RATE_LIMITER) return SM_RL;
+    if (r.kind == CT_DEFAULT && r.grade == SF_GRADE_THREAD && r.count < 2147483647.0) return SM_THREAD;
     return SM_GENERIC;
 }
 
@@ -68,27 +69,20 @@ struct HeavyCtx {
 };
 
 // ------------------------------------------------------------------ team
-#if defined(__HIP_DEVICE_COMPILE__)
-struct Team {
-    int rank, size;
-    long long* red;     // LDS, >= 16 slots
-    __device__ void sync() { __syncthreads(); }
+#if defined(__HIP__)
+struct Team {           // one wavefront: lock-step, reductions by cross-lane shuffles
+    int rank;
+    static constexpr int size = 64;
     __device__ long long min(long long v) {
         for (int o = 32; o > 0; o >>= 1) { long long w = __shfl_xor(v, o); v = w < v ? w : v; }
-        __syncthreads();
-        if ((rank & 63) == 0) red[rank >> 6] = v;
-        __syncthreads();
-        long long r = red[0];
-        for (int i = 1; i < (size >> 6); i++) r = red[i] < r ? red[i] : r;
-        return r;
+        return v;
     }
     __device__ bool leader() const { return rank == 0; }
 };
 #else
 struct Team {
-    int rank = 0, size = 1;
-    long long* red = nullptr;
-    void sync() {}
+    int rank = 0;
+    static constexpr int size = 1;
     long long min(long long v) { return v; }
     bool leader() const { return true; }
 };
@@ -105,7 +99,7 @@ SF_HD uint32_t team_first_true(Team& tm, uint32_t lo, uint32_t hi, P pred) {
     while (lo < hi) {
         uint64_t n = hi - lo;
         if (n <= (uint64_t)tm.size) {
-            long long cand = (tm.rank < (int)n && pred(lo + tm.rank)) ? (long long)tm.rank : (long long)n;
+            long long cand = (tm.rank < (int)n && pred(lo + (uint32_t)tm.rank)) ? (long long)tm.rank : (long long)n;
             long long r = tm.min(cand);
             return lo + (uint32_t)r;
         }
@@ -121,6 +115,19 @@ SF_HD uint32_t team_first_true(Team& tm, uint32_t lo, uint32_t hi, P pred) {
         lo = lo + (uint32_t)nlo;
     }
     return lo;
+}
+
+// First j in [lo, hi) with pred(j) true, pred arbitrary: forward scan, one
+// team-wide chunk per step (cheap when the answer is near lo).
+template <class P>
+SF_HD uint32_t team_next(Team& tm, uint32_t lo, uint32_t hi, P pred) {
+    for (uint32_t q = lo; q < hi; q += (uint32_t)tm.size) {
+        const uint32_t j = q + (uint32_t)tm.rank;
+        const long long cand = (j < hi && pred(j)) ? (long long)j : (long long)hi;
+        const long long r = tm.min(cand);
+        if (r < (long long)hi) return (uint32_t)r;
+    }
+    return hi;
 }
 
 SF_HD bool is_entry(uint8_t f) { return (f & SF_EV_EXIT) == 0; }
@@ -209,11 +216,15 @@ SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyC
             });
             if (f > p) { passed = (f ? pcg[f - 1] : 0) - pc0; iw.push(tm.leader(), p, f, 0); }
             // tail: remaining entries with small acquireCount may still fit
-            for (uint32_t j = f + 1; j < b; j++) {
-                if (!((double)(base + passed + 1) <= thr)) break;       // no c >= 1 can pass any more
-                if (!is_entry(io.flags[j])) continue;
-                int32_t c = io.cnt[j];
-                if ((double)(base + passed + c) <= thr) { passed += c; iw.push(tm.leader(), j, j + 1, 0); }
+            uint32_t j = f + 1;
+            while (j < b && (double)(base + passed + 1) <= thr) {      // else no c >= 1 can pass any more
+                j = team_next(tm, j, b, [&](uint32_t k) {
+                    return is_entry(io.flags[k]) && (double)(base + passed + io.cnt[k]) <= thr;
+                });
+                if (j >= b) break;
+                passed += io.cnt[j];
+                iw.push(tm.leader(), j, j + 1, 0);
+                j++;
             }
         }
         sec[idx].pass = wadd(sec[idx].pass, passed);
@@ -239,15 +250,18 @@ SF_HD void heavy_rl(Team& tm, const DevState& st, const SegIO& io, const HeavyCt
         uint32_t p = lo;
         while (p < hi) {
             const int64_t thr = L + cost1 - rule.max_queue_ms;
-            uint32_t j = team_first_true(tm, p, hi, [&](uint32_t k) { return io.ts[k] >= thr; });
-            int64_t cost = cost1;
-            for (; j < hi; j++) {
-                if (!is_entry(io.flags[j])) continue;
-                int32_t c = io.cnt[j];
-                cost = c == 1 ? cost1 : j_round(1.0 * c / rule.count * 1000);
-                if (io.ts[j] >= L + cost - rule.max_queue_ms) break;
-            }
+            // entries before thr cannot pass (cost >= cost1 for c >= 1); first candidate chunk checked directly
+            uint32_t j = (p < hi && io.ts[p] >= thr) ? p
+                         : team_first_true(tm, p, hi, [&](uint32_t k) { return io.ts[k] >= thr; });
+            j = team_next(tm, j, hi, [&](uint32_t k) {
+                if (!is_entry(io.flags[k])) return false;
+                const int32_t c = io.cnt[k];
+                const int64_t ck = c == 1 ? cost1 : j_round(1.0 * c / rule.count * 1000);
+                return io.ts[k] >= L + ck - rule.max_queue_ms;
+            });
             if (j >= hi) break;
+            const int32_t cj = io.cnt[j];
+            const int64_t cost = cj == 1 ? cost1 : j_round(1.0 * cj / rule.count * 1000);
             const int64_t t = io.ts[j];
             int32_t wait = 0;
             if (L + cost <= t) L = t;
@@ -259,6 +273,113 @@ SF_HD void heavy_rl(Team& tm, const DevState& st, const SegIO& io, const HeavyCt
     }
     if (tm.leader()) { hc.n_items[s] = iw.n; st.rstate[r0] = rs; }
 }
+
+
+// ---------------------------------------------------------- THREAD grade
+// DefaultController, FLOW_GRADE_THREAD (DefaultController.java:50-89): an
+// entry passes iff (int)curThreadNum + c <= count; a pass adds one thread
+// (StatisticSlot.java:64-65), the exit of a passed entry removes it (:157).
+// The exit of an entry decided in this batch is live iff that entry passed.
+// Verdicts are written directly; the fill kernel reduces them per window.
+constexpr uint32_t RING_WORDS = 2048;                  // 128 Ki events of pass bits in LDS (16 KiB)
+constexpr uint32_t RING_BITS = RING_WORDS * 64;
+#if defined(__HIP__)
+__device__ void heavy_thread(Team& tm, const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t s,
+                             uint32_t res, uint32_t lo, uint32_t hi, unsigned long long* ring) {
+    const DevRule rule = st.rules[st.rule_off[res]];
+    const double M = rule.count;
+    const int64_t IM = (int64_t)floor(M);
+    int64_t T = st.threads[res];
+    const int lane = tm.rank;
+    for (uint32_t q = lo; q < hi; q += 64) {
+        const uint32_t j = q + lane;
+        const bool valid = j < hi;
+        const uint8_t f = valid ? io.flags[j] : 0;
+        const int32_t c = valid ? io.cnt[j] : 0;
+        const bool ent = valid && is_entry(f);
+        const bool ex = valid && !is_entry(f);
+        int64_t r = (ex && io.eref) ? io.eref[j] : -1;
+        const bool bad = ex && r >= 0 && (r < (int64_t)lo || r >= (int64_t)j);   // flagged by k_heavy_fill
+        const bool inwin = ex && !bad && r >= (int64_t)q;
+        bool live = ex && r < 0;
+        if (ex && !bad && r >= 0 && r < (int64_t)q) {
+            if (j - (uint32_t)r < RING_BITS - 64) {
+                const uint32_t b = (uint32_t)(r - lo) % RING_BITS;
+                live = (ring[b >> 6] >> (b & 63)) & 1ull;
+            } else {
+                __threadfence();
+                const uint8_t v = __hip_atomic_load(io.v_status + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                live = v == SF_V_PASS;
+            }
+        }
+        unsigned long long pmask = 0;
+        const unsigned long long m_inwin = __ballot(inwin), m_c1 = __ballot(ent && c != 1);
+        const int64_t room0 = IM - T;
+        if (!m_inwin && !m_c1 && room0 >= 0) {
+            // Lindley recursion: room' = max(room + d, 0), d = -1 entry, +1 live exit
+            long long d = ent ? -1 : (live ? 1 : 0);
+            long long S = d, mn = d < 0 ? d : 0;          // inclusive prefix sum and prefix min(0, S)
+            for (int o = 1; o < 64; o <<= 1) {
+                long long Su = __shfl_up(S, o), mu = __shfl_up(mn, o);
+                if (lane >= o) { long long m2 = Su + mn; mn = mu < m2 ? mu : m2; S = Su + S; }
+            }
+            // room before event k = room after k-1
+            long long S_prev = __shfl_up(S, 1), mn_prev = __shfl_up(mn, 1);
+            if (lane == 0) { S_prev = 0; mn_prev = 0; }
+            long long room_before = S_prev + (room0 > -mn_prev ? room0 : -mn_prev);
+            if (ent && room_before >= 1) pmask = 1;       // per-lane flag, collected below
+            pmask = __ballot(pmask != 0);
+            long long S_last = __shfl(S, 63), mn_last = __shfl(mn, 63);
+            long long room_end = S_last + (room0 > -mn_last ? room0 : -mn_last);
+            T = IM - room_end;
+        } else {
+            int cursor = 0;
+            for (;;) {
+                const bool fits = ent && (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)c) <= M;
+                const bool lv = ex && (inwin ? ((pmask >> (uint32_t)(r - q)) & 1ull) != 0 : live);
+                const unsigned long long m = __ballot(lane >= cursor && (fits || lv));
+                if (!m) break;
+                const int k = __ffsll((long long)m) - 1;
+                const bool k_ent = __shfl((int)ent, k) != 0;
+                if (k_ent) { T += 1; pmask |= 1ull << k; } else { T -= 1; }
+                cursor = k + 1;
+            }
+            if (inwin) live = ((pmask >> (uint32_t)(r - q)) & 1ull) != 0;
+        }
+        const bool passed = ent && ((pmask >> lane) & 1ull);
+        if (valid) {
+            io.v_status[j] = ent ? (passed ? SF_V_PASS : SF_V_BLOCK_FLOW) : (live ? SF_V_EXIT : SF_V_EXIT_IGNORED);
+            if (io.v_wait) io.v_wait[j] = 0;
+            if (io.v_rule) io.v_rule[j] = 0;
+        }
+        // window q covers ring word (q - lo) / 64 exactly: bit = lane, set iff an entry passed
+        if (lane == 0) ring[((q - lo) >> 6) % RING_WORDS] = pmask;
+    }
+    (void)s; (void)hc;
+}
+#else
+// host build: the same semantics, one event at a time
+inline void heavy_thread(Team&, const DevState& st, const SegIO& io, const HeavyCtx&, uint32_t, uint32_t res,
+                         uint32_t lo, uint32_t hi, unsigned long long*) {
+    const double M = st.rules[st.rule_off[res]].count;
+    int64_t T = st.threads[res];
+    for (uint32_t j = lo; j < hi; j++) {
+        const uint8_t f = io.flags[j];
+        if (is_entry(f)) {
+            bool ok = (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)io.cnt[j]) <= M;
+            if (ok) T++;
+            io.v_status[j] = ok ? SF_V_PASS : SF_V_BLOCK_FLOW;
+        } else {
+            int64_t r = io.eref ? io.eref[j] : -1;
+            bool live = r < 0 || io.v_status[r] == SF_V_PASS;
+            if (live) T--;
+            io.v_status[j] = live ? SF_V_EXIT : SF_V_EXIT_IGNORED;
+        }
+        if (io.v_wait) io.v_wait[j] = 0;
+        if (io.v_rule) io.v_rule[j] = 0;
+    }
+}
+#endif
 
 // entry verdict from a segment's sorted item list (binary search)
 SF_HD bool item_lookup(const HeavyCtx& hc, uint32_t lo, uint32_t n, uint32_t j, int32_t* wait) {
@@ -308,10 +429,23 @@ SF_HD void heavy_apply(const DevState& st, const HeavyCtx& hc, uint32_t s, uint3
 
 // verdict + accounting contribution of event j of a heavy item segment
 struct EvContrib { uint8_t status; int32_t wait; bool touch, passed, live_exit; int64_t c, rt; bool err; };
-SF_HD EvContrib heavy_event(const HeavyCtx& hc, const SegIO& io, uint32_t lo, uint32_t nitems, uint32_t j) {
+SF_HD EvContrib heavy_event(const HeavyCtx& hc, const SegIO& io, uint32_t lo, uint32_t nitems, uint32_t j,
+                            bool from_verdicts) {
     EvContrib r{};
     const uint8_t f = io.flags[j];
     r.c = io.cnt[j];
+    if (from_verdicts) {                       // SM_THREAD: decide wrote every verdict
+        const uint8_t v = io.v_status[j];
+        r.status = v; r.wait = 0;
+        if (is_entry(f)) { r.passed = v == SF_V_PASS; r.touch = true; }
+        else {
+            r.live_exit = v == SF_V_EXIT; r.touch = r.live_exit;
+            int64_t ref = io.eref ? io.eref[j] : -1;
+            r.rt = io.ts[j] - (ref >= 0 ? io.ts[ref] : (io.cts ? io.cts[j] : io.ts[j]));
+            r.err = (f & SF_EV_ERROR) != 0;
+        }
+        return r;
+    }
     if (is_entry(f)) {
         int32_t w = 0;
         r.passed = item_lookup(hc, lo, nitems, j, &w);

@@ -9,7 +9,7 @@
 //   pc scan     inclusive prefix of entry acquireCount (heavy window budgets)
 //   k_classify  light segments -> lane interpreter; heavy -> window/skip algorithms
 //   stream A:   k_decide_light  one lane per light segment (sf_decide.h)
-//   stream B:   k_heavy_decide  one workgroup per heavy segment (sf_heavy.h)
+//   stream B:   k_heavy_decide  one wavefront per heavy segment (sf_heavy.h)
 //               k_heavy_fill    verdicts + per-window counter deltas, device-wide
 //               k_heavy_apply   deltas applied to the LeapArray state in time order
 //   k_scatter   verdicts back to submission order
@@ -152,17 +152,20 @@ static HeavyCtx heavy_ctx(const Work& w) {
     return hc;
 }
 
+// One wavefront per heavy segment (64-thread workgroups: the team needs no
+// barriers, and up to 10 segments share a CU under the THREAD ring's LDS).
 template <int MAXS>
-__global__ void __launch_bounds__(256) k_heavy_decide(DevState st, SegIO io, HeavyCtx hc) {
-    __shared__ long long red[16];
+__global__ void __launch_bounds__(64) k_heavy_decide(DevState st, SegIO io, HeavyCtx hc) {
+    __shared__ unsigned long long ring[RING_WORDS];
     if (blockIdx.x >= *hc.n_heavy) return;
     const uint32_t s = hc.heavy_list[blockIdx.x];
     const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1], res = hc.seg_res[s];
-    Team tm{(int)threadIdx.x, (int)blockDim.x, red};
+    Team tm{(int)threadIdx.x};
     switch (hc.seg_mode[s]) {
     case SM_QPS: heavy_qps(tm, st, io, hc, s, res, lo, hi, false); break;
     case SM_WARM: heavy_qps(tm, st, io, hc, s, res, lo, hi, true); break;
     case SM_RL: heavy_rl(tm, st, io, hc, s, res, lo, hi); break;
+    case SM_THREAD: heavy_thread(tm, st, io, hc, s, res, lo, hi, ring); break;
     case SM_NORULE:
         if (tm.leader()) { hc.item_lo[lo] = lo; hc.item_hi[lo] = hi; hc.item_wait[lo] = 0; hc.n_items[s] = 1; }
         break;
@@ -239,10 +242,13 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
             int64_t r = io.eref[j];
             if (r >= 0 && (r < (int64_t)lo || r >= (int64_t)j || !is_entry(io.flags[r]))) { *st.err = SF_ERR_INVALID; }
         }
-        EvContrib e = heavy_event(hc, io, lo, hc.n_items[s], j);
-        io.v_status[j] = e.status;
-        if (io.v_wait) io.v_wait[j] = e.wait;
-        if (io.v_rule) io.v_rule[j] = 0;
+        const bool thr = mode == SM_THREAD;
+        EvContrib e = heavy_event(hc, io, lo, thr ? 0u : hc.n_items[s], j, thr);
+        if (!thr) {
+            io.v_status[j] = e.status;
+            if (io.v_wait) io.v_wait[j] = e.wait;
+            if (io.v_rule) io.v_rule[j] = 0;
+        }
         if (!e.touch) continue;
         const uint32_t key_h = hc.acc_hw_base[s] + (uint32_t)(io.ts[j] / st.wl - hc.seg_hw0[s]);
         const uint32_t key_s = hc.acc_sec_base[s] + (uint32_t)(io.ts[j] / 1000 - hc.seg_sec0[s]);
@@ -340,9 +346,9 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     hipStreamWaitEvent(s2, ev[5], 0);
     const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
     if (st.S <= 2)
-        hipLaunchKernelGGL(k_heavy_decide<2>, dim3(max_heavy), dim3(256), 0, s2, st, io, hc);
+        hipLaunchKernelGGL(k_heavy_decide<2>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     else
-        hipLaunchKernelGGL(k_heavy_decide<SF_MAX_SAMPLE_COUNT>, dim3(max_heavy), dim3(256), 0, s2, st, io, hc);
+        hipLaunchKernelGGL(k_heavy_decide<SF_MAX_SAMPLE_COUNT>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     hipLaunchKernelGGL(k_heavy_fill, dim3(blocks(n, 256 * FILL_ITERS)), dim3(256), 0, s2, st, io, hc, w.head,
                        w.head_scan);
     hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, w.seg_nhw, w.seg_nsec);

@@ -31,7 +31,7 @@ struct hs_engine {
     int32_t err = 0;
     uint32_t R;
     uint32_t heavy_min;
-    uint64_t n_heavy_segments = 0, n_heavy_item_segments = 0;
+    uint64_t n_heavy_segments = 0, n_heavy_item_segments = 0, mode_count[8] = {};
     void refresh() {
         st.second = second.data(); st.borrow = borrow.data(); st.minute = minute.data();
         st.threads = threads.data(); st.rule_off = rule_off.data(); st.rules = rules.data();
@@ -159,6 +159,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         if (hi - lo <= e->heavy_min) { mode[s] = SM_LIGHT; continue; }
         e->n_heavy_segments++;
         mode[s] = heavy_mode(e->st, seg_res[s], segflag[s], ts[lo]);
+        e->mode_count[mode[s] & 7]++;
         if (mode[s] != SM_GENERIC) {
             e->n_heavy_item_segments++;
             hw0[s] = ts[lo] / e->st.wl; sec0[s] = ts[lo] / 1000;
@@ -177,6 +178,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         case SM_QPS: heavy_qps(tm, e->st, io, hc, s, res, lo, hi, false); break;
         case SM_WARM: heavy_qps(tm, e->st, io, hc, s, res, lo, hi, true); break;
         case SM_RL: heavy_rl(tm, e->st, io, hc, s, res, lo, hi); break;
+        case SM_THREAD: heavy_thread(tm, e->st, io, hc, s, res, lo, hi, nullptr); break;
         case SM_NORULE: ilo[lo] = lo; ihi[lo] = hi; iwait[lo] = 0; nitems[s] = 1; break;
         default:
             if (e->st.S <= 2) decide_segment<2>(e->st, io, res, lo, hi);
@@ -187,8 +189,9 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     for (uint32_t s = 0; s < ns; s++) {
         if (mode[s] < SM_QPS) continue;
         for (uint32_t j = seg_start[s]; j < seg_start[s + 1]; j++) {
-            EvContrib c = heavy_event(hc, io, seg_start[s], nitems[s], j);
-            vs[j] = c.status; vw[j] = c.wait; vr[j] = 0;
+            const bool thr = mode[s] == SM_THREAD;
+            EvContrib c = heavy_event(hc, io, seg_start[s], nitems[s], j, thr);
+            if (!thr) { vs[j] = c.status; vw[j] = c.wait; vr[j] = 0; }
             if (!c.touch) continue;
             for (int t = 0; t < 2; t++) {
                 Acc& a = t == 0 ? acc_hw[hwb[s] + (ts[j] / e->st.wl - hw0[s])] : acc_sec[secb[s] + (ts[j] / 1000 - sec0[s])];
@@ -214,6 +217,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
 }
 
 void hs_heavy_stats(hs_engine* e, uint64_t* heavy, uint64_t* items) { *heavy = e->n_heavy_segments; *items = e->n_heavy_item_segments; }
+void hs_mode_counts(hs_engine* e, uint64_t* out8) { for (int i = 0; i < 8; i++) out8[i] = e->mode_count[i]; }
 
 int hs_read_node(hs_engine* e, uint32_t res, sf_node_state* out) {
     uint32_t l; if (!local_of(e, res, &l)) return SF_ERR_INVALID;

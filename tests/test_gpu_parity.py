@@ -41,6 +41,23 @@ def test_heavy_edge_traces(eng_mod, so, seed):
     body(fake_hs, so, seed)
 
 
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("heavy_min", [2, 512])
+def test_heavy_thread_traces(eng_mod, so, seed, heavy_min):
+    """THREAD-grade heavy segments: the wave kernel's Lindley fast path, the
+    ballot path (in-window exits, acquireCount > 1) and the LDS pass ring."""
+    from tests.test_hostsim_parity import thread_workload
+    workloads.run(eng_mod.FlowEngine, so.OracleEngine, thread_workload(seed, heavy_min=heavy_min))
+
+
+def test_heavy_thread_long_range(eng_mod, so):
+    """Exits 0..3 s after their entries in a 600k-event single-resource
+    segment: references beyond the 128 Ki-event LDS ring take the HBM path."""
+    from tests.test_hostsim_parity import thread_workload
+    w = thread_workload(7, R=1, n=600_000, max_rt=3000, gaps=(0,) * 99 + (1,), heavy_min=512)
+    workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
+
+
 def test_device_resident_batch(eng_mod, so):
     """Inputs already in HBM (the bench path): same verdicts as the host path."""
     w = workloads.config3(R=5000, n=200_000, seed=5, split=1)

@@ -17,6 +17,7 @@ def hs():
     from tests.hostsim import hostsim
     L = hostsim.lib()
     L.hs_heavy_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.hs_mode_counts.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     return hostsim
 
 
@@ -84,3 +85,47 @@ def test_heavy_edge_traces(hs, so, seed):
     w = dict(cfg=abi.default_config(max_resources=R, max_batch=b.n, heavy_min_events=2), flow=rules,
              batches=[b.subset(0, half), b.subset(half, b.n)], nodes=list(range(R)), n_flow=3)
     workloads.run(hs.HostSimEngine, so.OracleEngine, w)
+
+
+def thread_trace(seed, R=3, n=60000, exit_frac=0.9, max_rt=60, gaps=(0, 0, 0, 0, 1, 1, 3, 40)):
+    """Entry/exit traces for THREAD-grade rules: most entries exit 0..max_rt ms
+    later (many in the same millisecond), mixed acquireCount, rule counts small
+    enough that the thread gate saturates."""
+    rng = np.random.default_rng(300 + seed)
+    ts = 1_700_000_000_000 + np.cumsum(rng.choice(list(gaps), size=n))
+    res = rng.integers(0, R, n).astype(np.uint32)
+    cnt = np.where(rng.random(n) < 0.85, 1, rng.integers(1, 5, n)).astype(np.int32)
+    flags = np.full(n, abi.EV_IN, np.uint8)
+    ent = np.nonzero(rng.random(n) < exit_frac)[0]
+    ex_ts = ts[ent] + np.where(rng.random(ent.size) < 0.3, 0, rng.integers(0, max_rt, ent.size))
+    all_ts = np.concatenate([ts, ex_ts])
+    key = np.lexsort((np.concatenate([np.zeros(n), np.ones(ent.size)]), all_ts))
+    pos = np.empty(key.size, np.int64)
+    pos[key] = np.arange(key.size)
+    src = np.concatenate([np.arange(n), ent])
+    fl = np.concatenate([flags, np.full(ent.size, abi.EV_EXIT | abi.EV_IN, np.uint8)])
+    fl[n:][rng.random(ent.size) < 0.1] |= abi.EV_ERROR
+    eref = np.full(key.size, -1, np.int64)
+    eref[pos[n:]] = pos[ent]
+    return abi.HostBatch(res[src][key], all_ts[key], cnt[src][key], fl[key], entry_ref=eref)
+
+
+def thread_workload(seed, R=3, n=60000, max_rt=60, gaps=(0, 0, 0, 0, 1, 1, 3, 40), heavy_min=2):
+    rng = np.random.default_rng(400 + seed)
+    rules = [abi.sf_flow_rule(resource=r, grade=abi.GRADE_THREAD, count=float(rng.integers(1, 40)) + (0.5 if r == 2 else 0),
+                              control_behavior=0) for r in range(R)]
+    b = thread_trace(seed, R, n=n, max_rt=max_rt, gaps=gaps)
+    k = b.n // 3
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=b.n, heavy_min_events=heavy_min), flow=rules,
+                batches=[b.subset(0, k), b.subset(k, 2 * k), b.subset(2 * k, b.n)], nodes=list(range(R)), n_flow=R)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_heavy_thread_traces(hs, so, seed):
+    """THREAD-grade heavy segments (SM_THREAD) against the oracle, split into
+    three batches so exits reference entries of earlier batches."""
+    w = thread_workload(seed)
+    eng, _, _ = workloads.run(hs.HostSimEngine, so.OracleEngine, w)
+    mc = (C.c_uint64 * 8)()
+    hs.lib().hs_mode_counts(eng.h, mc)
+    assert mc[6] >= 8     # SM_THREAD segments
