@@ -114,15 +114,43 @@ def main():
     wall = times[0]
     value = total_decisions / wall
 
-    # roofline of the dominant kernel (k_decide): SURVEY.md §8(d) byte model
-    decide_ms = st.decide_ms / args.steps
+    # roofline of the dominant decision kernel: SURVEY.md §8(d) byte model,
+    # B = 25 E + 4 E_wait + 12 E_exit + 528 R_touched, restricted to the
+    # segments (resources) that kernel decides.  Resources with more than
+    # heavy_min events in the batch go to k_heavy_decide, the rest to
+    # k_decide_light (sf_kernels.hip: k_classify).
+    heavy_min = 512
+    per_res = np.bincount(hb.res_id // world if world > 1 else hb.res_id, minlength=R_local)
+    is_heavy_res = per_res > heavy_min
+    ev_heavy = is_heavy_res[hb.res_id // world if world > 1 else hb.res_id]
+    is_exit = (hb.flags & abi.EV_EXIT) != 0
+    waited = wait > 0
+
+    def alg_bytes(sel, n_res):
+        return int(25 * sel.sum() + 4 * (waited & sel).sum() + 12 * (is_exit & sel).sum() + 528 * n_res)
+
+    n_heavy_res = int(is_heavy_res.sum())
+    b_light = alg_bytes(~ev_heavy, int(((per_res > 0) & ~is_heavy_res).sum()))
+    b_heavy = alg_bytes(ev_heavy, n_heavy_res)
     b_alg = 25 * hb.n + 4 * e_wait + 12 * n_exit + 528 * n_seg
-    achieved = b_alg / (decide_ms / 1e3) / 1e9
-    roofline = {"bound": "hbm", "kernel": "k_decide", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+    k = args.steps
+    kern = {"k_decide_light": (st.light_ms / k, b_light), "k_heavy_decide": (st.heavy_decide_ms / k, b_heavy)}
+    name = max(kern, key=lambda x: kern[x][0])
+    ms, bytes_k = kern[name]
+    achieved = bytes_k / (ms / 1e3) / 1e9
+    roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "alg_bytes_per_launch": b_alg, "avg_launch_ms": round(decide_ms, 4),
-                "pipeline_ms": {"sort+segments": round(st.sort_ms / args.steps, 3),
-                                "decide": round(decide_ms, 3), "scatter": round(st.scatter_ms / args.steps, 3)}}
+                "alg_bytes_per_launch": bytes_k, "avg_launch_ms": round(ms, 4),
+                "pipeline": {"alg_bytes_per_step": b_alg,
+                             "achieved_GBs": round(b_alg / (wall / k) / 1e9, 2),
+                             "heavy_segments": n_heavy_res},
+                "kernels_ms": {"sort+segments+classify": round(st.sort_ms / k, 3),
+                               "classify": round(st.classify_ms / k, 3),
+                               "decide(join)": round(st.decide_ms / k, 3),
+                               "k_decide_light": round(st.light_ms / k, 3),
+                               "k_heavy_decide": round(st.heavy_decide_ms / k, 3),
+                               "k_heavy_fill": round(st.heavy_fill_ms / k, 3),
+                               "scatter": round(st.scatter_ms / k, 3)}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

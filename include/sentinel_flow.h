@@ -283,15 +283,27 @@ typedef struct sf_metric_row {    /* MetricNode (MetricNode.java:160-229) */
     int64_t  pass_qps, block_qps, success_qps, exception_qps, rt, occupied_pass_qps;
 } sf_metric_row;
 
-typedef struct sf_stats {         /* timings of the last sf_submit (device clock) */
+typedef struct sf_stats {         /* device-clock timings, summed over sf_submit calls while timing is on */
     double   total_ms;
-    double   sort_ms;
-    double   decide_ms;           /* the dominant per-resource decision kernel */
+    double   sort_ms;             /* keys + radix sort + segment heads + gather + classify */
+    double   decide_ms;           /* light and heavy decision kernels (two streams) up to the join */
     double   scatter_ms;
-    uint64_t n_events;
-    uint64_t n_segments;          /* resources touched                         */
+    uint64_t n_events;            /* of the last call */
+    uint64_t n_segments;          /* resources touched by the last call */
     uint64_t n_launches;
+    double   light_ms;            /* k_decide_light alone (stream A) */
+    double   heavy_decide_ms;     /* k_heavy_decide alone (stream B) */
+    double   heavy_fill_ms;       /* k_heavy_fill alone (stream B) */
+    double   classify_ms;         /* k_classify alone */
 } sf_stats;
+
+typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last sf_submit */
+    uint32_t resource;            /* local resource index on this shard        */
+    uint32_t events;              /* events of the resource in the batch       */
+    uint32_t mode;                /* heavy algorithm (DESIGN.md "Kernels")     */
+    uint32_t pad;
+    uint64_t ticks;               /* k_heavy_decide time of the segment, 100 MHz device clock */
+} sf_heavy_profile;
 
 /* ---- API ------------------------------------------------------------- */
 typedef struct sf_engine sf_engine;
@@ -331,6 +343,8 @@ int  sf_memcpy(sf_engine* e, void* dst, const void* src, size_t bytes, int kind 
 int  sf_sync(sf_engine* e);
 int  sf_get_stats(sf_engine* e, sf_stats* out);
 int  sf_set_timing(sf_engine* e, int enabled);
+/* diagnostics: per heavy segment of the last sf_submit (timing must be on) */
+int  sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uint32_t* n_out);
 
 #ifdef __cplusplus
 }

@@ -172,7 +172,13 @@ class sf_metric_row(C.Structure):
 class sf_stats(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("sort_ms", C.c_double), ("decide_ms", C.c_double),
                 ("scatter_ms", C.c_double), ("n_events", C.c_uint64), ("n_segments", C.c_uint64),
-                ("n_launches", C.c_uint64)]
+                ("n_launches", C.c_uint64), ("light_ms", C.c_double), ("heavy_decide_ms", C.c_double),
+                ("heavy_fill_ms", C.c_double), ("classify_ms", C.c_double)]
+
+
+class sf_heavy_profile(C.Structure):
+    _fields_ = [("resource", C.c_uint32), ("events", C.c_uint32), ("mode", C.c_uint32), ("pad", C.c_uint32),
+                ("ticks", C.c_uint64)]
 
 
 STRUCT_SIZES = {name: C.sizeof(cls) for name, cls in [
@@ -180,7 +186,7 @@ STRUCT_SIZES = {name: C.sizeof(cls) for name, cls in [
     ("sf_param_rule", sf_param_rule), ("sf_system_rule", sf_system_rule),
     ("sf_event_batch", sf_event_batch), ("sf_verdicts", sf_verdicts),
     ("sf_cluster_flow_rule", sf_cluster_flow_rule), ("sf_cluster_param_rule", sf_cluster_param_rule),
-    ("sf_namespace", sf_namespace), ("sf_token_batch", sf_token_batch),
+    ("sf_namespace", sf_namespace), ("sf_heavy_profile", sf_heavy_profile), ("sf_token_batch", sf_token_batch),
     ("sf_token_results", sf_token_results), ("sf_bucket", sf_bucket), ("sf_node_state", sf_node_state),
     ("sf_rule_state", sf_rule_state), ("sf_metric_row", sf_metric_row), ("sf_stats", sf_stats)]}
 

@@ -43,7 +43,7 @@ struct sf_engine {
     // staging for host-memory batches
     void* stage_in = nullptr; size_t stage_in_bytes = 0;
     void* stage_out = nullptr; size_t stage_out_bytes = 0;
-    hipEvent_t ev[7]{};
+    hipEvent_t ev[SF_NUM_EVENTS]{};
     bool timing = false;
     sf_stats stats{};
     std::vector<void*> user_allocs;
@@ -89,7 +89,7 @@ void sf_destroy(sf_engine* e) {
                     e->w.segflag, e->w.seg_mode, e->w.light_list, e->w.heavy_list, e->w.counters, e->w.pcg,
                     e->w.pscan_tmp, e->w.item_lo, e->w.item_hi, e->w.item_wait, e->w.n_items, e->w.acc_hw,
                     e->w.acc_sec, e->w.acc_hw_base, e->w.acc_sec_base, e->w.seg_hw0, e->w.seg_sec0,
-                    e->w.seg_nhw, e->w.seg_nsec};
+                    e->w.seg_nhw, e->w.seg_nsec, e->w.hticks, e->w.passbits};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     for (auto& x : e->ev) if (x) hipEventDestroy(x);
@@ -172,6 +172,8 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     DALLOC(w.acc_hw, (size_t)w.acc_cap * ACC_BYTES); DALLOC(w.acc_sec, (size_t)w.acc_cap * ACC_BYTES);
     DALLOC(w.acc_hw_base, SC * 4); DALLOC(w.acc_sec_base, SC * 4); DALLOC(w.seg_hw0, SC * 8);
     DALLOC(w.seg_sec0, SC * 8); DALLOC(w.seg_nhw, SC * 4); DALLOC(w.seg_nsec, SC * 4);
+    DALLOC(w.hticks, (N / (w.heavy_min + 1) + 2) * 8);
+    DALLOC(w.passbits, (N / 64 + 2) * 8);
     HIP_TRY(hipStreamSynchronize(e->stream));
     *out = e;
     return SF_OK;
@@ -367,6 +369,13 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         hipEventElapsedTime(&b2, e->ev[1], e->ev[2]);
         hipEventElapsedTime(&c, e->ev[2], e->ev[3]);
         hipEventElapsedTime(&d, e->ev[3], e->ev[4]);
+        float cl = 0, li = 0, hd = 0, hf = 0;
+        hipEventElapsedTime(&cl, e->ev[10], e->ev[2]);
+        hipEventElapsedTime(&li, e->ev[5], e->ev[9]);
+        hipEventElapsedTime(&hd, e->ev[5], e->ev[7]);
+        hipEventElapsedTime(&hf, e->ev[7], e->ev[8]);
+        e->stats.classify_ms += cl; e->stats.light_ms += li;
+        e->stats.heavy_decide_ms += hd; e->stats.heavy_fill_ms += hf;
         e->stats.sort_ms += a + b2;
         e->stats.decide_ms += c;
         e->stats.scatter_ms += d;
@@ -476,6 +485,35 @@ int sf_set_timing(sf_engine* e, int enabled) {
     if (!e) return fail(SF_ERR_INVALID, "null engine");
     e->timing = enabled != 0;
     std::memset(&e->stats, 0, sizeof e->stats);
+    return SF_OK;
+}
+
+int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uint32_t* n_out) {
+    if (!e || !n_out || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    uint32_t cnt[5] = {0, 0, 0, 0, 0}, nseg = 0;
+    HIP_TRY(hipStreamSynchronize(e->stream2));
+    HIP_TRY(hipMemcpy(cnt, e->w.counters, sizeof cnt, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&nseg, e->w.n_seg, 4, hipMemcpyDeviceToHost));
+    const uint32_t nf = cnt[1], nb = cnt[4];
+    const uint32_t nh = std::min(nf + nb, cap);
+    std::vector<uint32_t> full(e->w.seg_cap), list(nh), start(nseg + 1), res(nseg);
+    std::vector<uint8_t> mode(nseg);
+    std::vector<uint64_t> ticks(nh);
+    if (nh) {
+        HIP_TRY(hipMemcpy(full.data(), e->w.heavy_list, (size_t)e->w.seg_cap * 4, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < nh; i++) list[i] = i < nf ? full[i] : full[e->w.seg_cap - 1 - (i - nf)];
+        HIP_TRY(hipMemcpy(ticks.data(), e->w.hticks, nh * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(start.data(), e->w.seg_start, (nseg + 1) * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(res.data(), e->w.seg_res, nseg * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(mode.data(), e->w.seg_mode, nseg, hipMemcpyDeviceToHost));
+    }
+    for (uint32_t i = 0; i < nh; i++) {
+        const uint32_t sg = list[i];
+        out[i].resource = res[sg]; out[i].events = start[sg + 1] - start[sg];
+        out[i].mode = mode[sg]; out[i].pad = 0; out[i].ticks = e->timing ? ticks[i] : 0;
+    }
+    *n_out = nh;
     return SF_OK;
 }
 

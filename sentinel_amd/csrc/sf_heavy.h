@@ -61,12 +61,17 @@ SF_HD uint8_t heavy_mode(const DevState& st, uint32_t res, uint32_t segflags, in
 
 struct HeavyCtx {
     const uint32_t* seg_start; const uint32_t* seg_res; const uint8_t* seg_mode;
-    const uint32_t* heavy_list; const uint32_t* n_heavy;
+    const uint32_t* heavy_list; const uint32_t* n_heavy;  // n_heavy[0] front count, n_heavy[3] back count
+    uint32_t seg_cap;
     const int64_t* pcg;                // inclusive prefix of entry acquireCount over the sorted batch
     uint32_t* item_lo; uint32_t* item_hi; int32_t* item_wait; uint32_t* n_items;
     Acc* acc_hw; Acc* acc_sec; const uint32_t* acc_hw_base; const uint32_t* acc_sec_base;
     const int64_t* seg_hw0; const int64_t* seg_sec0;    // first window index of the segment
+    uint64_t* hticks;                                   // per heavy-list entry, or null
+    unsigned long long* passbits;                       // [n/64+2] bit j: entry j passed (SM_THREAD)
 };
+
+SF_HD bool pass_bit(const unsigned long long* pb, uint32_t j) { return (pb[j >> 6] >> (j & 63)) & 1ull; }
 
 // ------------------------------------------------------------------ team
 #if defined(__HIP__)
@@ -280,103 +285,148 @@ SF_HD void heavy_rl(Team& tm, const DevState& st, const SegIO& io, const HeavyCt
 // entry passes iff (int)curThreadNum + c <= count; a pass adds one thread
 // (StatisticSlot.java:64-65), the exit of a passed entry removes it (:157).
 // The exit of an entry decided in this batch is live iff that entry passed.
-// Verdicts are written directly; the fill kernel reduces them per window.
+// Output: one bit per passed entry in hc.passbits; k_heavy_fill turns the
+// bits into verdicts and window counters.
 constexpr uint32_t RING_WORDS = 2048;                  // 128 Ki events of pass bits in LDS (16 KiB)
 constexpr uint32_t RING_BITS = RING_WORDS * 64;
 #if defined(__HIP__)
+constexpr int THREAD_KW = 16;         // windows per load batch; the next batch is in flight meanwhile
+// LDS staging of one batch: flags, acquireCount, entry ref of 16 x 64 events
+constexpr uint32_t THREAD_STAGE_WORDS = (THREAD_KW * 64 * (1 + 4 + 8) + 7) / 8;
+
+struct ThreadIn { uint8_t f[THREAD_KW]; int32_t c[THREAD_KW]; int64_t r[THREAD_KW]; };
+
+__device__ __forceinline__ void thread_load(ThreadIn& in, const SegIO& io, uint32_t q0, uint32_t hi, int lane) {
+#pragma unroll
+    for (int k = 0; k < THREAD_KW; k++) {
+        const uint32_t j = q0 + 64 * k + lane;
+        const bool v = j < hi;
+        in.f[k] = v ? io.flags[j] : (uint8_t)0;
+        in.c[k] = v ? io.cnt[j] : 0;
+        in.r[k] = (v && io.eref && (in.f[k] & SF_EV_EXIT)) ? io.eref[j] : -1;
+    }
+}
+__device__ __forceinline__ void thread_stage(const ThreadIn& in, unsigned long long* stage, int lane) {
+    int64_t* sr = (int64_t*)stage;
+    int32_t* sc = (int32_t*)(sr + THREAD_KW * 64);
+    uint8_t* sf = (uint8_t*)(sc + THREAD_KW * 64);
+#pragma unroll
+    for (int k = 0; k < THREAD_KW; k++) { sr[k * 64 + lane] = in.r[k]; sc[k * 64 + lane] = in.c[k]; sf[k * 64 + lane] = in.f[k]; }
+}
+
 __device__ void heavy_thread(Team& tm, const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t s,
-                             uint32_t res, uint32_t lo, uint32_t hi, unsigned long long* ring) {
+                             uint32_t res, uint32_t lo, uint32_t hi, unsigned long long* ring,
+                             unsigned long long* stage) {
     const DevRule rule = st.rules[st.rule_off[res]];
     const double M = rule.count;
     const int64_t IM = (int64_t)floor(M);
     int64_t T = st.threads[res];
     const int lane = tm.rank;
-    for (uint32_t q = lo; q < hi; q += 64) {
-        const uint32_t j = q + lane;
-        const bool valid = j < hi;
-        const uint8_t f = valid ? io.flags[j] : 0;
-        const int32_t c = valid ? io.cnt[j] : 0;
-        const bool ent = valid && is_entry(f);
-        const bool ex = valid && !is_entry(f);
-        int64_t r = (ex && io.eref) ? io.eref[j] : -1;
-        const bool bad = ex && r >= 0 && (r < (int64_t)lo || r >= (int64_t)j);   // flagged by k_heavy_fill
-        const bool inwin = ex && !bad && r >= (int64_t)q;
-        bool live = ex && r < 0;
-        if (ex && !bad && r >= 0 && r < (int64_t)q) {
-            if (j - (uint32_t)r < RING_BITS - 64) {
-                const uint32_t b = (uint32_t)(r - lo) % RING_BITS;
-                live = (ring[b >> 6] >> (b & 63)) & 1ull;
+    unsigned long long* pbits = hc.passbits;
+    const int64_t* sr = (const int64_t*)stage;
+    const int32_t* sc = (const int32_t*)(sr + THREAD_KW * 64);
+    const uint8_t* sf = (const uint8_t*)(sc + THREAD_KW * 64);
+    ThreadIn nxt;
+    thread_load(nxt, io, lo, hi, lane);
+    for (uint32_t q0 = lo; q0 < hi; q0 += 64 * THREAD_KW) {
+        thread_stage(nxt, stage, lane);                  // this batch: registers -> LDS (own lane's slots)
+        if (q0 + 64 * THREAD_KW < hi) thread_load(nxt, io, q0 + 64 * THREAD_KW, hi, lane);
+        const int nk = (int)min((uint32_t)THREAD_KW, (hi - q0 + 63) / 64);
+        for (int k = 0; k < nk; k++) {
+            const uint32_t q = q0 + 64 * k;
+            const uint32_t j = q + lane;
+            const bool valid = j < hi;
+            const uint8_t fl = sf[k * 64 + lane];
+            const int32_t c = sc[k * 64 + lane];
+            const bool ent = valid && !(fl & SF_EV_EXIT);
+            const bool ex = valid && (fl & SF_EV_EXIT);
+            const int64_t r = sr[k * 64 + lane];
+            const bool bad = ex && r >= 0 && (r < (int64_t)lo || r >= (int64_t)j);   // flagged by k_heavy_fill
+            const bool inwin = ex && !bad && r >= (int64_t)q;
+            bool live = ex && r < 0;
+            if (ex && !bad && r >= 0 && r < (int64_t)q) {
+                if (j - (uint32_t)r < RING_BITS - 64) {
+                    const uint32_t b = (uint32_t)(r - lo) % RING_BITS;
+                    live = (ring[b >> 6] >> (b & 63)) & 1ull;
+                } else {
+                    // older than the ring: read this wave's own bits back from L2 (same XCD);
+                    // wait for its atomics to complete, then load past the L1
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                    __builtin_amdgcn_s_waitcnt(0);
+                    const unsigned long long w =
+                        __hip_atomic_load(pbits + (r >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    live = (w >> (r & 63)) & 1ull;
+                }
+            }
+            const unsigned long long m_ent = __ballot(ent), m_inwin = __ballot(inwin);
+            const int n_live = (int)__popcll(__ballot(ex && !inwin && live));
+            const int n_ent = (int)__popcll(m_ent);
+            const int64_t room0 = IM - T;
+            unsigned long long pmask = 0;
+            if (room0 + n_live < 1) {
+                // acquireCount >= 1 (heavy_mode): even with every live exit first, no entry fits;
+                // the exits of this window's entries are then not live either
+                T -= n_live;
+            } else if (n_ent > 0) {
+                bool all = false;
+                if (room0 >= (int64_t)n_ent) {                // the thread count before entry k is <= T + k
+                    int cmax = 1;
+                    if (__ballot(ent && c != 1)) {
+                        cmax = ent ? c : 0;
+#pragma unroll
+                        for (int o = 32; o > 0; o >>= 1) { const int a2 = __shfl_xor(cmax, o); cmax = a2 > cmax ? a2 : cmax; }
+                    }
+                    all = room0 >= (int64_t)(n_ent - 1) + cmax;
+                }
+                if (all) {
+                    pmask = m_ent;
+                    T += (int64_t)n_ent - (int64_t)n_live - (int64_t)__popcll(m_inwin);
+                } else {
+                    // step through the events that change the thread count: the next
+                    // entry that fits or the next live exit, one ballot per step
+                    int cursor = 0;
+                    for (;;) {
+                        const bool fits = ent && (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)c) <= M;
+                        const bool lv = ex && (inwin ? ((pmask >> (uint32_t)(r - q)) & 1ull) != 0 : live);
+                        const unsigned long long m = __ballot(lane >= cursor && (fits || lv));
+                        if (!m) break;
+                        const int kk = __ffsll((long long)m) - 1;
+                        if ((m_ent >> kk) & 1ull) { T += 1; pmask |= 1ull << kk; } else { T -= 1; }
+                        cursor = kk + 1;
+                    }
+                }
             } else {
-                __threadfence();
-                const uint8_t v = __hip_atomic_load(io.v_status + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                live = v == SF_V_PASS;
+                T -= n_live;
+            }
+            if (lane == 0) {
+                // window q covers ring word (q - lo) / 64 exactly: bit = lane
+                ring[((q - lo) >> 6) % RING_WORDS] = pmask;
+                if (pmask) {
+                    const uint32_t sh = q & 63;
+                    atomicOr(pbits + (q >> 6), pmask << sh);
+                    if (sh) atomicOr(pbits + (q >> 6) + 1, pmask >> (64 - sh));
+                }
             }
         }
-        unsigned long long pmask = 0;
-        const unsigned long long m_inwin = __ballot(inwin), m_c1 = __ballot(ent && c != 1);
-        const int64_t room0 = IM - T;
-        if (!m_inwin && !m_c1 && room0 >= 0) {
-            // Lindley recursion: room' = max(room + d, 0), d = -1 entry, +1 live exit
-            long long d = ent ? -1 : (live ? 1 : 0);
-            long long S = d, mn = d < 0 ? d : 0;          // inclusive prefix sum and prefix min(0, S)
-            for (int o = 1; o < 64; o <<= 1) {
-                long long Su = __shfl_up(S, o), mu = __shfl_up(mn, o);
-                if (lane >= o) { long long m2 = Su + mn; mn = mu < m2 ? mu : m2; S = Su + S; }
-            }
-            // room before event k = room after k-1
-            long long S_prev = __shfl_up(S, 1), mn_prev = __shfl_up(mn, 1);
-            if (lane == 0) { S_prev = 0; mn_prev = 0; }
-            long long room_before = S_prev + (room0 > -mn_prev ? room0 : -mn_prev);
-            if (ent && room_before >= 1) pmask = 1;       // per-lane flag, collected below
-            pmask = __ballot(pmask != 0);
-            long long S_last = __shfl(S, 63), mn_last = __shfl(mn, 63);
-            long long room_end = S_last + (room0 > -mn_last ? room0 : -mn_last);
-            T = IM - room_end;
-        } else {
-            int cursor = 0;
-            for (;;) {
-                const bool fits = ent && (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)c) <= M;
-                const bool lv = ex && (inwin ? ((pmask >> (uint32_t)(r - q)) & 1ull) != 0 : live);
-                const unsigned long long m = __ballot(lane >= cursor && (fits || lv));
-                if (!m) break;
-                const int k = __ffsll((long long)m) - 1;
-                const bool k_ent = __shfl((int)ent, k) != 0;
-                if (k_ent) { T += 1; pmask |= 1ull << k; } else { T -= 1; }
-                cursor = k + 1;
-            }
-            if (inwin) live = ((pmask >> (uint32_t)(r - q)) & 1ull) != 0;
-        }
-        const bool passed = ent && ((pmask >> lane) & 1ull);
-        if (valid) {
-            io.v_status[j] = ent ? (passed ? SF_V_PASS : SF_V_BLOCK_FLOW) : (live ? SF_V_EXIT : SF_V_EXIT_IGNORED);
-            if (io.v_wait) io.v_wait[j] = 0;
-            if (io.v_rule) io.v_rule[j] = 0;
-        }
-        // window q covers ring word (q - lo) / 64 exactly: bit = lane, set iff an entry passed
-        if (lane == 0) ring[((q - lo) >> 6) % RING_WORDS] = pmask;
     }
-    (void)s; (void)hc;
+    (void)s;
 }
 #else
 // host build: the same semantics, one event at a time
-inline void heavy_thread(Team&, const DevState& st, const SegIO& io, const HeavyCtx&, uint32_t, uint32_t res,
-                         uint32_t lo, uint32_t hi, unsigned long long*) {
+inline void heavy_thread(Team&, const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t, uint32_t res,
+                         uint32_t lo, uint32_t hi, unsigned long long*, unsigned long long*) {
     const double M = st.rules[st.rule_off[res]].count;
     int64_t T = st.threads[res];
     for (uint32_t j = lo; j < hi; j++) {
-        const uint8_t f = io.flags[j];
-        if (is_entry(f)) {
-            bool ok = (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)io.cnt[j]) <= M;
-            if (ok) T++;
-            io.v_status[j] = ok ? SF_V_PASS : SF_V_BLOCK_FLOW;
+        if (is_entry(io.flags[j])) {
+            if ((double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)io.cnt[j]) <= M) {
+                T++;
+                hc.passbits[j >> 6] |= 1ull << (j & 63);
+            }
         } else {
-            int64_t r = io.eref ? io.eref[j] : -1;
-            bool live = r < 0 || io.v_status[r] == SF_V_PASS;
-            if (live) T--;
-            io.v_status[j] = live ? SF_V_EXIT : SF_V_EXIT_IGNORED;
+            const int64_t r = io.eref ? io.eref[j] : -1;
+            if (r < 0 || (r >= (int64_t)lo && r < (int64_t)j && pass_bit(hc.passbits, (uint32_t)r))) T--;
         }
-        if (io.v_wait) io.v_wait[j] = 0;
-        if (io.v_rule) io.v_rule[j] = 0;
     }
 }
 #endif
@@ -430,17 +480,20 @@ SF_HD void heavy_apply(const DevState& st, const HeavyCtx& hc, uint32_t s, uint3
 // verdict + accounting contribution of event j of a heavy item segment
 struct EvContrib { uint8_t status; int32_t wait; bool touch, passed, live_exit; int64_t c, rt; bool err; };
 SF_HD EvContrib heavy_event(const HeavyCtx& hc, const SegIO& io, uint32_t lo, uint32_t nitems, uint32_t j,
-                            bool from_verdicts) {
+                            bool from_bits) {
     EvContrib r{};
     const uint8_t f = io.flags[j];
     r.c = io.cnt[j];
-    if (from_verdicts) {                       // SM_THREAD: decide wrote every verdict
-        const uint8_t v = io.v_status[j];
-        r.status = v; r.wait = 0;
-        if (is_entry(f)) { r.passed = v == SF_V_PASS; r.touch = true; }
-        else {
-            r.live_exit = v == SF_V_EXIT; r.touch = r.live_exit;
-            int64_t ref = io.eref ? io.eref[j] : -1;
+    if (from_bits) {                           // SM_THREAD: decide set one bit per passed entry
+        if (is_entry(f)) {
+            r.passed = pass_bit(hc.passbits, j);
+            r.status = r.passed ? SF_V_PASS : SF_V_BLOCK_FLOW;
+            r.touch = true;
+        } else {
+            const int64_t ref = io.eref ? io.eref[j] : -1;
+            r.live_exit = ref < 0 || (ref >= (int64_t)lo && ref < (int64_t)j && pass_bit(hc.passbits, (uint32_t)ref));
+            r.status = r.live_exit ? SF_V_EXIT : SF_V_EXIT_IGNORED;
+            r.touch = r.live_exit;
             r.rt = io.ts[j] - (ref >= 0 ? io.ts[ref] : (io.cts ? io.cts[j] : io.ts[j]));
             r.err = (f & SF_EV_ERROR) != 0;
         }

@@ -96,39 +96,70 @@ struct EntryCount {     // acquireCount of entries, 0 for exits (input of the pc
     __device__ int64_t operator()(uint32_t j) const { return (flags[j] & SF_EV_EXIT) ? 0 : (int64_t)cnt[j]; }
 };
 
+// Append to a list with one atomic per wavefront (a single hot counter would
+// otherwise serialise millions of atomics at one L2 channel).
+__device__ uint32_t wave_append(uint32_t* counter, bool take) {
+    const unsigned long long m = __ballot(take);
+    if (!m) return 0;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
 // Route each segment: light lane interpreter, heavy window algorithms, or the
-// heavy generic interpreter (one lane of a workgroup).
+// heavy generic interpreter (one lane of a wavefront).
 __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
-    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= *w.n_seg) return;
-    const uint32_t lo = w.seg_start[s], hi = w.seg_start[s + 1], res = w.seg_res[s];
-    if (hi - lo <= w.heavy_min) {
-        w.seg_mode[s] = SM_LIGHT;
-        w.light_list[atomicAdd(&w.counters[0], 1u)] = s;
-        return;
-    }
-    uint8_t mode = heavy_mode(st, res, w.segflag[s], s_ts[lo]);
-    if (mode != SM_GENERIC) {
-        const int64_t h0 = s_ts[lo] / st.wl, h1 = s_ts[hi - 1] / st.wl;
-        const int64_t s0 = s_ts[lo] / 1000, s1 = s_ts[hi - 1] / 1000;
-        const int64_t nh = h1 - h0 + 1, ns = s1 - s0 + 1;
-        if (nh > 65536 || ns > 65536) mode = SM_GENERIC;
-        else {
-            uint32_t bh = atomicAdd(&w.counters[2], (uint32_t)nh);
-            uint32_t bs = atomicAdd(&w.counters[3], (uint32_t)ns);
-            if ((uint64_t)bh + nh > w.acc_cap || (uint64_t)bs + ns > w.acc_cap) mode = SM_GENERIC;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = s < *w.n_seg;
+    uint32_t lo = 0, hi = 0, res = 0;
+    if (valid) { lo = w.seg_start[s]; hi = w.seg_start[s + 1]; res = w.seg_res[s]; }
+    const bool light = valid && hi - lo <= w.heavy_min;
+    const uint32_t lpos = wave_append(&w.counters[0], light);
+    if (light) { w.seg_mode[s] = SM_LIGHT; w.light_list[lpos] = s; }
+    const bool heavy = valid && !light;
+    if (!__ballot(heavy)) return;
+    uint8_t mode = SM_GENERIC;
+    if (heavy) {
+        mode = heavy_mode(st, res, w.segflag[s], s_ts[lo]);
+        if (mode != SM_GENERIC) {
+            const int64_t h0 = s_ts[lo] / st.wl, h1 = s_ts[hi - 1] / st.wl;
+            const int64_t s0 = s_ts[lo] / 1000, s1 = s_ts[hi - 1] / 1000;
+            const int64_t nh = h1 - h0 + 1, ns = s1 - s0 + 1;
+            if (nh > 65536 || ns > 65536) mode = SM_GENERIC;
             else {
-                w.acc_hw_base[s] = bh; w.acc_sec_base[s] = bs;
-                w.seg_hw0[s] = h0; w.seg_sec0[s] = s0; w.seg_nhw[s] = (uint32_t)nh; w.seg_nsec[s] = (uint32_t)ns;
-                Acc z{}; z.min_rt = INT64_MAX;
-                Acc* ah = (Acc*)w.acc_hw; Acc* as = (Acc*)w.acc_sec;
-                for (int64_t k = 0; k < nh; k++) ah[bh + k] = z;
-                for (int64_t k = 0; k < ns; k++) as[bs + k] = z;
+                uint32_t bh = atomicAdd(&w.counters[2], (uint32_t)nh);
+                uint32_t bs = atomicAdd(&w.counters[3], (uint32_t)ns);
+                if ((uint64_t)bh + nh > w.acc_cap || (uint64_t)bs + ns > w.acc_cap) mode = SM_GENERIC;
+                else {
+                    w.acc_hw_base[s] = bh; w.acc_sec_base[s] = bs;
+                    w.seg_hw0[s] = h0; w.seg_sec0[s] = s0; w.seg_nhw[s] = (uint32_t)nh; w.seg_nsec[s] = (uint32_t)ns;
+                    Acc z{}; z.min_rt = INT64_MAX;
+                    Acc* ah = (Acc*)w.acc_hw; Acc* as = (Acc*)w.acc_sec;
+                    for (int64_t k = 0; k < nh; k++) ah[bh + k] = z;
+                    for (int64_t k = 0; k < ns; k++) as[bs + k] = z;
+                }
             }
         }
+        w.seg_mode[s] = mode;
     }
-    w.seg_mode[s] = mode;
-    w.heavy_list[atomicAdd(&w.counters[1], 1u)] = s;
+    // long-running heavy segments first in the list, so that their wavefronts
+    // start first: [0, counters[1]) front, [seg_cap - counters[4], seg_cap) back
+    const bool slow = heavy && (mode == SM_THREAD || mode == SM_RL || mode == SM_GENERIC || hi - lo > 65536u);
+    const uint32_t fpos = wave_append(&w.counters[1], slow);
+    const uint32_t bpos = wave_append(&w.counters[4], heavy && !slow);
+    if (slow) w.heavy_list[fpos] = s;
+    else if (heavy) w.heavy_list[w.seg_cap - 1 - bpos] = s;
+}
+
+// heavy-list entry of workgroup b: front part, then the back part
+__device__ __forceinline__ bool heavy_at(const HeavyCtx& hc, uint32_t b, uint32_t* s) {
+    const uint32_t nf = hc.n_heavy[0], nb = hc.n_heavy[3];
+    if (b < nf) { *s = hc.heavy_list[b]; return true; }
+    if (b < nf + nb) { *s = hc.heavy_list[hc.seg_cap - 1 - (b - nf)]; return true; }
+    return false;
 }
 
 template <int MAXS>
@@ -144,11 +175,13 @@ __global__ void __launch_bounds__(128) k_decide_light(DevState st, SegIO io, con
 static HeavyCtx heavy_ctx(const Work& w) {
     HeavyCtx hc;
     hc.seg_start = w.seg_start; hc.seg_res = w.seg_res; hc.seg_mode = w.seg_mode;
-    hc.heavy_list = w.heavy_list; hc.n_heavy = w.counters + 1; hc.pcg = w.pcg;
+    hc.heavy_list = w.heavy_list; hc.n_heavy = w.counters + 1; hc.pcg = w.pcg; hc.seg_cap = w.seg_cap;
     hc.item_lo = w.item_lo; hc.item_hi = w.item_hi; hc.item_wait = w.item_wait; hc.n_items = w.n_items;
     hc.acc_hw = (Acc*)w.acc_hw; hc.acc_sec = (Acc*)w.acc_sec;
     hc.acc_hw_base = w.acc_hw_base; hc.acc_sec_base = w.acc_sec_base;
     hc.seg_hw0 = w.seg_hw0; hc.seg_sec0 = w.seg_sec0;
+    hc.hticks = nullptr;
+    hc.passbits = w.passbits;
     return hc;
 }
 
@@ -156,16 +189,17 @@ static HeavyCtx heavy_ctx(const Work& w) {
 // barriers, and up to 10 segments share a CU under the THREAD ring's LDS).
 template <int MAXS>
 __global__ void __launch_bounds__(64) k_heavy_decide(DevState st, SegIO io, HeavyCtx hc) {
-    __shared__ unsigned long long ring[RING_WORDS];
-    if (blockIdx.x >= *hc.n_heavy) return;
-    const uint32_t s = hc.heavy_list[blockIdx.x];
+    __shared__ unsigned long long lds[RING_WORDS + THREAD_STAGE_WORDS];   // THREAD: pass ring + batch stage
+    uint32_t s;
+    if (!heavy_at(hc, blockIdx.x, &s)) return;
     const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1], res = hc.seg_res[s];
     Team tm{(int)threadIdx.x};
+    const uint64_t t_start = hc.hticks ? wall_clock64() : 0;
     switch (hc.seg_mode[s]) {
     case SM_QPS: heavy_qps(tm, st, io, hc, s, res, lo, hi, false); break;
     case SM_WARM: heavy_qps(tm, st, io, hc, s, res, lo, hi, true); break;
     case SM_RL: heavy_rl(tm, st, io, hc, s, res, lo, hi); break;
-    case SM_THREAD: heavy_thread(tm, st, io, hc, s, res, lo, hi, ring); break;
+    case SM_THREAD: heavy_thread(tm, st, io, hc, s, res, lo, hi, lds, lds + RING_WORDS); break;
     case SM_NORULE:
         if (tm.leader()) { hc.item_lo[lo] = lo; hc.item_hi[lo] = hi; hc.item_wait[lo] = 0; hc.n_items[s] = 1; }
         break;
@@ -173,6 +207,7 @@ __global__ void __launch_bounds__(64) k_heavy_decide(DevState st, SegIO io, Heav
         if (tm.leader()) decide_segment<MAXS>(st, io, res, lo, hi);
         break;
     }
+    if (hc.hticks && tm.leader()) hc.hticks[blockIdx.x] = wall_clock64() - t_start;
 }
 
 struct PAcc {            // per-thread partial of one accumulator slot
@@ -244,11 +279,9 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
         }
         const bool thr = mode == SM_THREAD;
         EvContrib e = heavy_event(hc, io, lo, thr ? 0u : hc.n_items[s], j, thr);
-        if (!thr) {
-            io.v_status[j] = e.status;
-            if (io.v_wait) io.v_wait[j] = e.wait;
-            if (io.v_rule) io.v_rule[j] = 0;
-        }
+        io.v_status[j] = e.status;
+        if (io.v_wait) io.v_wait[j] = e.wait;
+        if (io.v_rule) io.v_rule[j] = 0;
         if (!e.touch) continue;
         const uint32_t key_h = hc.acc_hw_base[s] + (uint32_t)(io.ts[j] / st.wl - hc.seg_hw0[s]);
         const uint32_t key_s = hc.acc_sec_base[s] + (uint32_t)(io.ts[j] / 1000 - hc.seg_sec0[s]);
@@ -261,9 +294,8 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
 }
 
 __global__ void k_heavy_apply(DevState st, HeavyCtx hc, const uint32_t* seg_nhw, const uint32_t* seg_nsec) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= *hc.n_heavy) return;
-    const uint32_t s = hc.heavy_list[t];
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, s;
+    if (!heavy_at(hc, t, &s)) return;
     if (hc.seg_mode[s] < SM_QPS) return;
     heavy_apply(st, hc, s, hc.seg_res[s], seg_nhw[s], seg_nsec[s]);
 }
@@ -328,8 +360,9 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
     e = rocprim::inclusive_scan(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n, rocprim::plus<int64_t>(), s);
     if (e != hipSuccess) return e;
-    hipMemsetAsync(w.counters, 0, 4 * sizeof(uint32_t), s);
+    hipMemsetAsync(w.counters, 0, 8 * sizeof(uint32_t), s);
     const uint32_t max_seg = n < st.R ? n : st.R;
+    if (timing) hipEventRecord(ev[10], s);
     hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, T)), dim3(T), 0, s, st, w, w.s_ts);
     if (timing) hipEventRecord(ev[2], s);
 
@@ -340,17 +373,21 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     io.atag = w.s_atag; io.abits = w.s_abits; io.n = n;
     io.v_status = w.v_status; io.v_wait = w.v_wait; io.v_rule = w.v_rule;
     HeavyCtx hc = heavy_ctx(w);
+    if (timing) hc.hticks = w.hticks;
 
     // heavy segments on the second stream, overlapping the light lanes
     hipEventRecord(ev[5], s);                      // fork
     hipStreamWaitEvent(s2, ev[5], 0);
     const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
+    hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s2);
     if (st.S <= 2)
         hipLaunchKernelGGL(k_heavy_decide<2>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     else
         hipLaunchKernelGGL(k_heavy_decide<SF_MAX_SAMPLE_COUNT>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
+    if (timing) hipEventRecord(ev[7], s2);
     hipLaunchKernelGGL(k_heavy_fill, dim3(blocks(n, 256 * FILL_ITERS)), dim3(256), 0, s2, st, io, hc, w.head,
                        w.head_scan);
+    if (timing) hipEventRecord(ev[8], s2);
     hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, w.seg_nhw, w.seg_nsec);
 
     const unsigned TD = 128;
@@ -360,6 +397,7 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     else
         hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s, st, io,
                            w.seg_start, w.seg_res, w.light_list, w.counters);
+    if (timing) hipEventRecord(ev[9], s);
     hipEventRecord(ev[6], s2);                     // join
     hipStreamWaitEvent(s, ev[6], 0);
     if (timing) hipEventRecord(ev[3], s);

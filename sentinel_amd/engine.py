@@ -75,6 +75,7 @@ def _declare(L):
     f("sf_sync", I, P)
     f("sf_get_stats", I, P, C.POINTER(abi.sf_stats))
     f("sf_set_timing", I, P, I)
+    f("sf_heavy_profile_read", I, P, C.POINTER(abi.sf_heavy_profile), U32, C.POINTER(U32))
 
 
 def _check(rc):
@@ -222,6 +223,13 @@ class FlowEngine:
         s = abi.sf_stats()
         _check(lib().sf_get_stats(self.h, C.byref(s)))
         return s
+
+    def heavy_profile(self, cap=1 << 20):
+        """Per heavy segment of the last submit: (resource, events, mode, microseconds)."""
+        buf = (abi.sf_heavy_profile * cap)()
+        n = C.c_uint32()
+        _check(lib().sf_heavy_profile_read(self.h, buf, cap, C.byref(n)))
+        return [(b.resource, b.events, b.mode, b.ticks / 100.0) for b in buf[:n.value]]
 
     def sync(self):
         _check(lib().sf_sync(self.h))

@@ -169,8 +169,10 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
             acc_hw.resize(acc_hw.size() + nhw[s], z); acc_sec.resize(acc_sec.size() + nsec[s], z);
         }
     }
-    HeavyCtx hc{seg_start.data(), seg_res.data(), mode.data(), nullptr, nullptr, pcg.data(), ilo.data(), ihi.data(),
-                iwait.data(), nitems.data(), acc_hw.data(), acc_sec.data(), hwb.data(), secb.data(), hw0.data(), sec0.data()};
+    std::vector<unsigned long long> passbits(n / 64 + 2, 0ull);
+    HeavyCtx hc{seg_start.data(), seg_res.data(), mode.data(), nullptr, nullptr, 0u, pcg.data(), ilo.data(), ihi.data(),
+                iwait.data(), nitems.data(), acc_hw.data(), acc_sec.data(), hwb.data(), secb.data(), hw0.data(), sec0.data(),
+                nullptr, passbits.data()};
     for (uint32_t s = 0; s < ns; s++) {
         uint32_t lo = seg_start[s], hi = seg_start[s + 1], res = seg_res[s];
         Team tm;
@@ -178,7 +180,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         case SM_QPS: heavy_qps(tm, e->st, io, hc, s, res, lo, hi, false); break;
         case SM_WARM: heavy_qps(tm, e->st, io, hc, s, res, lo, hi, true); break;
         case SM_RL: heavy_rl(tm, e->st, io, hc, s, res, lo, hi); break;
-        case SM_THREAD: heavy_thread(tm, e->st, io, hc, s, res, lo, hi, nullptr); break;
+        case SM_THREAD: heavy_thread(tm, e->st, io, hc, s, res, lo, hi, nullptr, nullptr); break;
         case SM_NORULE: ilo[lo] = lo; ihi[lo] = hi; iwait[lo] = 0; nitems[s] = 1; break;
         default:
             if (e->st.S <= 2) decide_segment<2>(e->st, io, res, lo, hi);
@@ -191,7 +193,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         for (uint32_t j = seg_start[s]; j < seg_start[s + 1]; j++) {
             const bool thr = mode[s] == SM_THREAD;
             EvContrib c = heavy_event(hc, io, seg_start[s], nitems[s], j, thr);
-            if (!thr) { vs[j] = c.status; vw[j] = c.wait; vr[j] = 0; }
+            vs[j] = c.status; vw[j] = c.wait; vr[j] = 0;
             if (!c.touch) continue;
             for (int t = 0; t < 2; t++) {
                 Acc& a = t == 0 ? acc_hw[hwb[s] + (ts[j] / e->st.wl - hw0[s])] : acc_sec[secb[s] + (ts[j] / 1000 - sec0[s])];
