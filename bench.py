@@ -119,22 +119,30 @@ def main():
     # segments (resources) that kernel decides.  Resources with more than
     # heavy_min events in the batch go to k_heavy_decide, the rest to
     # k_decide_light (sf_kernels.hip: k_classify).
+    # k_classify routes segments of more than heavy_min events to the heavy
+    # kernels: THREAD-grade and RateLimiter ones to k_heavy_stream, the rest
+    # to k_heavy_decide.
     heavy_min = 512
-    per_res = np.bincount(hb.res_id // world if world > 1 else hb.res_id, minlength=R_local)
+    local = hb.res_id // world if world > 1 else hb.res_id
+    per_res = np.bincount(local, minlength=R_local)
     is_heavy_res = per_res > heavy_min
-    ev_heavy = is_heavy_res[hb.res_id // world if world > 1 else hb.res_id]
+    is_stream_rule = (grade == abi.GRADE_THREAD) | (beh == abi.BEHAVIOR_RATE_LIMITER)
+    res_cls = np.where(~is_heavy_res, 0, np.where(is_stream_rule, 2, 1))
+    ev_cls = res_cls[local]
     is_exit = (hb.flags & abi.EV_EXIT) != 0
     waited = wait > 0
 
-    def alg_bytes(sel, n_res):
+    def alg_bytes(cls):
+        sel = ev_cls == cls
+        n_res = int(((per_res > 0) & (res_cls == cls)).sum())
         return int(25 * sel.sum() + 4 * (waited & sel).sum() + 12 * (is_exit & sel).sum() + 528 * n_res)
 
     n_heavy_res = int(is_heavy_res.sum())
-    b_light = alg_bytes(~ev_heavy, int(((per_res > 0) & ~is_heavy_res).sum()))
-    b_heavy = alg_bytes(ev_heavy, n_heavy_res)
     b_alg = 25 * hb.n + 4 * e_wait + 12 * n_exit + 528 * n_seg
     k = args.steps
-    kern = {"k_decide_light": (st.light_ms / k, b_light), "k_heavy_decide": (st.heavy_decide_ms / k, b_heavy)}
+    kern = {"k_decide_light": (st.light_ms / k, alg_bytes(0)),
+            "k_heavy_decide": (st.heavy_decide_ms / k, alg_bytes(1)),
+            "k_heavy_stream": (st.stream_ms / k, alg_bytes(2))}
     name = max(kern, key=lambda x: kern[x][0])
     ms, bytes_k = kern[name]
     achieved = bytes_k / (ms / 1e3) / 1e9
@@ -149,6 +157,7 @@ def main():
                                "decide(join)": round(st.decide_ms / k, 3),
                                "k_decide_light": round(st.light_ms / k, 3),
                                "k_heavy_decide": round(st.heavy_decide_ms / k, 3),
+                               "k_heavy_stream": round(st.stream_ms / k, 3),
                                "k_heavy_fill": round(st.heavy_fill_ms / k, 3),
                                "scatter": round(st.scatter_ms / k, 3)}}
 

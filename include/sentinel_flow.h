@@ -295,6 +295,7 @@ typedef struct sf_stats {         /* device-clock timings, summed over sf_submit
     double   heavy_decide_ms;     /* k_heavy_decide alone (stream B) */
     double   heavy_fill_ms;       /* k_heavy_fill alone (stream B) */
     double   classify_ms;         /* k_classify alone */
+    double   stream_ms;           /* k_heavy_stream alone (stream C: THREAD-grade and RateLimiter heavy segments) */
 } sf_stats;
 
 typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last sf_submit */

@@ -173,7 +173,8 @@ class sf_stats(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("sort_ms", C.c_double), ("decide_ms", C.c_double),
                 ("scatter_ms", C.c_double), ("n_events", C.c_uint64), ("n_segments", C.c_uint64),
                 ("n_launches", C.c_uint64), ("light_ms", C.c_double), ("heavy_decide_ms", C.c_double),
-                ("heavy_fill_ms", C.c_double), ("classify_ms", C.c_double)]
+                ("heavy_fill_ms", C.c_double), ("classify_ms", C.c_double),
+                ("stream_ms", C.c_double)]
 
 
 class sf_heavy_profile(C.Structure):

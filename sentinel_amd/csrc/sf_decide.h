@@ -98,13 +98,14 @@ template <int MAXS>
 struct NodeWin {
     Bucket sec[MAXS];
     Borrow bor[MAXS];
-    Bucket scratch;        // LeapArray.java:220-223 throwaway windows
-    Borrow bscratch;
+    // LeapArray.java:220-223 hands out a throwaway window for a time older
+    // than the slot's bucket; what is added to it is lost, so the interpreter
+    // drops those writes instead of keeping a scratch bucket (no lane-private
+    // memory: everything stays in VGPRs).
     int64_t threads;
     // minute window: row in HBM + one cached bucket
     Bucket* gmin;
     Bucket mb; int32_t mi; int32_t mdirty;
-    Bucket mscratch;
     int32_t S, wl, interval;
     int64_t max_rt;
     double interval_sec;
@@ -128,7 +129,7 @@ struct NodeWin {
         visit_bor(idx, [&](Borrow& b) { if (b.ws <= t && t < b.ws + wl) v = b.pass; });
         return v;
     }
-    // currentWindow(t): returns idx, or -1 for a throwaway window (bscratch)
+    // currentWindow(t): returns idx, or -1 for a throwaway window
     SF_HD int borrow_current(int64_t t) {
         int idx = (int)((t / wl) % S);
         int64_t ws = t - t % wl;
@@ -138,7 +139,6 @@ struct NodeWin {
             if (ws > b.ws) { b.ws = ws; b.pass = 0; return; }          // FutureBucketLeapArray.resetWindowTo :41-46
             r = -1;
         });
-        if (r < 0) { bscratch.ws = ws; bscratch.pass = 0; }
         return r;
     }
     // OccupiableBucketLeapArray.currentWaiting (:67-76)
@@ -151,34 +151,33 @@ struct NodeWin {
     }
     SF_HD void add_waiting(int64_t t, int32_t c) {                       // :79-83
         int i = borrow_current(t);
-        if (i < 0) { bscratch.pass = wadd(bscratch.pass, c); return; }
+        if (i < 0) return;                                               // throwaway window
         visit_bor(i, [&](Borrow& b) { b.pass = wadd(b.pass, c); });
     }
 
     // ---- OccupiableBucketLeapArray main window ----
-    // currentWindow(t): returns idx or -1 (throwaway in `scratch`)
+    // currentWindow(t): returns idx or -1 (throwaway window, LeapArray.java:220-223)
     SF_HD int sec_current(int64_t t) {
         int idx = (int)((t / wl) % S);
         int64_t ws = t - t % wl;
         int r = idx;
-        bool reset = false, throwaway = false;
+        bool reset = false;
         visit(idx, [&](Bucket& b) {
             if (b.ws == ws) return;
             if (ws > b.ws) { reset = true; return; }
-            throwaway = true;
+            r = -1;
         });
-        if (reset || throwaway) {
-            int64_t bp = borrow_value(reset ? ws : t);
+        if (reset) {
+            int64_t bp = borrow_value(ws);
             Bucket nb = fresh_bucket(ws, max_rt);
-            if (bp >= 0) nb.pass = reset ? (int64_t)(int32_t)bp : bp;   // resetWindowTo :52-64 / newEmptyBucket :40-49
-            if (reset) visit(idx, [&](Bucket& b) { b = nb; });
-            else { scratch = nb; r = -1; }
+            if (bp >= 0) nb.pass = (int64_t)(int32_t)bp;                // resetWindowTo :52-64
+            visit(idx, [&](Bucket& b) { b = nb; });
         }
         return r;
     }
     template <class F> SF_HD void sec_apply(int64_t t, F f) {
         int i = sec_current(t);
-        if (i < 0) f(scratch); else visit(i, f);
+        if (i >= 0) visit(i, f);                                       // throwaway: the add is lost
     }
     SF_HD int64_t sec_sum_pass(int64_t now) {            // ArrayMetric.pass() :117-126
         sec_current(now);
@@ -198,15 +197,18 @@ struct NodeWin {
     SF_HD void min_flush() {
         if (mdirty) { gmin[mi] = mb; mdirty = 0; }
     }
-    // currentWindow(t) -> pointer to the live bucket (cached) or the throwaway
-    SF_HD Bucket* min_current(int64_t t) {
+    // currentWindow(t): true when the cached bucket is the live one, false
+    // for a throwaway window (older than the slot's bucket)
+    SF_HD bool min_current(int64_t t) {
         int idx = (int)((t / 1000) % MINUTE);
         int64_t ws = t - t % 1000;
         if (idx != mi) { min_flush(); mb = gmin[idx]; mi = idx; }
-        if (mb.ws == ws) { mdirty = 1; return &mb; }
-        if (ws > mb.ws) { mb = fresh_bucket(ws, max_rt); mdirty = 1; return &mb; }
-        mscratch = fresh_bucket(ws, max_rt);
-        return &mscratch;
+        if (mb.ws == ws) return true;
+        if (ws > mb.ws) { mb = fresh_bucket(ws, max_rt); mdirty = 1; return true; }
+        return false;
+    }
+    template <class F> SF_HD void min_apply(int64_t t, F f) {
+        if (min_current(t)) { f(mb); mdirty = 1; }
     }
     // ArrayMetric.previousWindowPass (:279-286) -> getPreviousWindow (LeapArray.java:234-251)
     SF_HD int64_t min_previous_pass(int64_t now) {
@@ -224,26 +226,26 @@ struct NodeWin {
     SF_HD double previous_pass_qps(int64_t now) { return (double)min_previous_pass(now); }   // :179-181
     SF_HD void add_pass(int64_t now, int32_t c) {                                            // :253-256
         sec_apply(now, [&](Bucket& b) { b.pass = wadd(b.pass, c); });
-        Bucket* m = min_current(now); m->pass = wadd(m->pass, c);
+        min_apply(now, [&](Bucket& m) { m.pass = wadd(m.pass, c); });
     }
     SF_HD void add_block(int64_t now, int32_t c) {                                           // :268-271
         sec_apply(now, [&](Bucket& b) { b.block = wadd(b.block, c); });
-        Bucket* m = min_current(now); m->block = wadd(m->block, c);
+        min_apply(now, [&](Bucket& m) { m.block = wadd(m.block, c); });
     }
     SF_HD void add_exception(int64_t now, int32_t c) {                                       // :274-277
         sec_apply(now, [&](Bucket& b) { b.exc = wadd(b.exc, c); });
-        Bucket* m = min_current(now); m->exc = wadd(m->exc, c);
+        min_apply(now, [&](Bucket& m) { m.exc = wadd(m.exc, c); });
     }
     SF_HD void add_rt_success(int64_t now, int64_t rt, int32_t c) {                          // :259-265
-        sec_apply(now, [&](Bucket& b) {
-            b.succ = wadd(b.succ, c); b.rt = wadd(b.rt, rt); if (rt < b.min_rt) b.min_rt = rt;   // MetricBucket.addRT :129-136
-        });
-        Bucket* m = min_current(now);
-        m->succ = wadd(m->succ, c); m->rt = wadd(m->rt, rt); if (rt < m->min_rt) m->min_rt = rt;
+        auto f = [&](Bucket& b) {                                                            // MetricBucket.addRT :129-136
+            b.succ = wadd(b.succ, c); b.rt = wadd(b.rt, rt); if (rt < b.min_rt) b.min_rt = rt;
+        };
+        sec_apply(now, f);
+        min_apply(now, f);
     }
     SF_HD void add_occupied_pass(int64_t now, int32_t c) {                                   // :343-346
-        Bucket* m = min_current(now); m->occ = wadd(m->occ, c);
-        m = min_current(now); m->pass = wadd(m->pass, c);
+        min_apply(now, [&](Bucket& m) { m.occ = wadd(m.occ, c); });
+        min_apply(now, [&](Bucket& m) { m.pass = wadd(m.pass, c); });
     }
     // tryOccupyNext :295-330 (IntervalProperty / SampleCountProperty statics)
     SF_HD int64_t try_occupy_next(int64_t now, int32_t c, double threshold, int32_t occupy_timeout) {
@@ -266,6 +268,10 @@ struct NodeWin {
         return occupy_timeout;
     }
 };
+
+SF_HD DevRuleState fresh_rule_state() {     // AtomicLong(0), AtomicLong(0), AtomicLong(-1)
+    DevRuleState s{}; s.stored_tokens = 0; s.last_filled = 0; s.latest_passed = -1; return s;
+}
 
 // ============================================================ controllers
 // WarmUpController.syncToken :178-197 + coolDownTokens :217-232
@@ -493,8 +499,10 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
 
     const uint32_t r0 = st.rule_off[res], r1 = st.rule_off[res + 1];
     const int nrules = (int)(r1 - r0);
-    DevRuleState rs[MAX_RULES];
-    for (int k = 0; k < MAX_RULES; k++) if (k < nrules) rs[k] = st.rstate[r0 + k];
+    // controller state of the first rule stays in registers; further rules of
+    // the resource (rare) are read-modified-written in place in HBM, which
+    // is exact because this lane owns the resource
+    DevRuleState rs0 = nrules ? st.rstate[r0] : fresh_rule_state();
     const uint32_t p0 = st.prule_off[res], p1 = st.prule_off[res + 1];
     const int nprules = (int)(p1 - p0);
     uint8_t pm_init = nprules ? st.pm_init[res] : 0;
@@ -570,8 +578,8 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
         if (!blocked) {
             for (int k = 0; k < nrules; k++) {
                 int64_t w = 0; bool pw = false;
-                int ok = can_pass<MAXS>(st.rules[r0 + k], rs[k], nd, now, c, (fl & SF_EV_PRIO) != 0,
-                                        st.occupy_timeout, &w, &pw);
+                int ok = can_pass<MAXS>(st.rules[r0 + k], k == 0 ? rs0 : st.rstate[r0 + k], nd, now, c,
+                                        (fl & SF_EV_PRIO) != 0, st.occupy_timeout, &w, &pw);
                 if (pw) { prio_wait = true; wait += w; rule_idx = k; break; }
                 if (!ok) { blocked = true; status = SF_V_BLOCK_FLOW; rule_idx = k; break; }
                 wait += w;
@@ -599,7 +607,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
         if (i < st.S) { st.second[(size_t)res * st.S + i] = nd.sec[i]; st.borrow[(size_t)res * st.S + i] = nd.bor[i]; }
     nd.min_flush();
     st.threads[res] = nd.threads;
-    for (int k = 0; k < MAX_RULES; k++) if (k < nrules) st.rstate[r0 + k] = rs[k];
+    if (nrules) st.rstate[r0] = rs0;
     if (nprules) st.pm_init[res] = pm_init;
 }
 
@@ -635,9 +643,6 @@ inline DevRule make_dev_rule(const sf_flow_rule& r, int cold_factor, int host_in
         d.slope = (cold_factor - 1.0) / r.count / (double)(d.max_token - d.warning_token);
     }
     return d;
-}
-inline DevRuleState fresh_rule_state() {     // AtomicLong(0), AtomicLong(0), AtomicLong(-1)
-    DevRuleState s{}; s.stored_tokens = 0; s.last_filled = 0; s.latest_passed = -1; return s;
 }
 inline DevParamRule make_dev_param_rule(const sf_param_rule& r, int host_index) {
     DevParamRule d{};

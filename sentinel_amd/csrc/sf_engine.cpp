@@ -33,7 +33,7 @@ static int fail(int code, const std::string& msg) {
 
 struct sf_engine {
     sf_config cfg{};
-    hipStream_t stream = nullptr, stream2 = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
     uint32_t R = 0, key_bits = 1;
     DevState st{};
     Work w{};
@@ -89,12 +89,13 @@ void sf_destroy(sf_engine* e) {
                     e->w.segflag, e->w.seg_mode, e->w.light_list, e->w.heavy_list, e->w.counters, e->w.pcg,
                     e->w.pscan_tmp, e->w.item_lo, e->w.item_hi, e->w.item_wait, e->w.n_items, e->w.acc_hw,
                     e->w.acc_sec, e->w.acc_hw_base, e->w.acc_sec_base, e->w.seg_hw0, e->w.seg_sec0,
-                    e->w.seg_nhw, e->w.seg_nsec, e->w.hticks, e->w.passbits};
+                    e->w.seg_nhw, e->w.seg_nsec, e->w.hticks, e->w.passbits, e->w.stream_list, e->w.sticks};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     for (auto& x : e->ev) if (x) hipEventDestroy(x);
     if (e->stream) hipStreamDestroy(e->stream);
     if (e->stream2) hipStreamDestroy(e->stream2);
+    if (e->stream3) hipStreamDestroy(e->stream3);
     delete e;
 }
 
@@ -123,6 +124,7 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     while ((1ull << e->key_bits) < e->R) e->key_bits++;
     HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking));
     for (auto& x : e->ev) HIP_TRY(hipEventCreate(&x));
 
     DevState& st = e->st;
@@ -173,6 +175,8 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     DALLOC(w.acc_hw_base, SC * 4); DALLOC(w.acc_sec_base, SC * 4); DALLOC(w.seg_hw0, SC * 8);
     DALLOC(w.seg_sec0, SC * 8); DALLOC(w.seg_nhw, SC * 4); DALLOC(w.seg_nsec, SC * 4);
     DALLOC(w.hticks, (N / (w.heavy_min + 1) + 2) * 8);
+    DALLOC(w.sticks, (N / (w.heavy_min + 1) + 2) * 8);
+    DALLOC(w.stream_list, SC * 4);
     DALLOC(w.passbits, (N / 64 + 2) * 8);
     HIP_TRY(hipStreamSynchronize(e->stream));
     *out = e;
@@ -348,7 +352,7 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     }
     HIP_TRY(hipMemsetAsync(e->st.err, 0, sizeof(int32_t), s));
     hipError_t le = launch_pipeline(e->st, e->w, b, dv, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s,
-                                    e->stream2, e->ev, e->timing);
+                                    e->stream2, e->stream3, e->ev, e->timing);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
     if (out->mem == SF_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, s));
@@ -369,13 +373,14 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         hipEventElapsedTime(&b2, e->ev[1], e->ev[2]);
         hipEventElapsedTime(&c, e->ev[2], e->ev[3]);
         hipEventElapsedTime(&d, e->ev[3], e->ev[4]);
-        float cl = 0, li = 0, hd = 0, hf = 0;
+        float cl = 0, li = 0, hd = 0, hf = 0, hs = 0;
         hipEventElapsedTime(&cl, e->ev[10], e->ev[2]);
         hipEventElapsedTime(&li, e->ev[5], e->ev[9]);
         hipEventElapsedTime(&hd, e->ev[5], e->ev[7]);
-        hipEventElapsedTime(&hf, e->ev[7], e->ev[8]);
+        hipEventElapsedTime(&hf, e->ev[13], e->ev[8]);
+        hipEventElapsedTime(&hs, e->ev[11], e->ev[12]);
         e->stats.classify_ms += cl; e->stats.light_ms += li;
-        e->stats.heavy_decide_ms += hd; e->stats.heavy_fill_ms += hf;
+        e->stats.heavy_decide_ms += hd; e->stats.heavy_fill_ms += hf; e->stats.stream_ms += hs;
         e->stats.sort_ms += a + b2;
         e->stats.decide_ms += c;
         e->stats.scatter_ms += d;
@@ -491,19 +496,31 @@ int sf_set_timing(sf_engine* e, int enabled) {
 int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uint32_t* n_out) {
     if (!e || !n_out || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> g(e->mu);
-    uint32_t cnt[5] = {0, 0, 0, 0, 0}, nseg = 0;
+    uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0}, nseg = 0;
     HIP_TRY(hipStreamSynchronize(e->stream2));
+    HIP_TRY(hipStreamSynchronize(e->stream3));
     HIP_TRY(hipMemcpy(cnt, e->w.counters, sizeof cnt, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&nseg, e->w.n_seg, 4, hipMemcpyDeviceToHost));
-    const uint32_t nf = cnt[1], nb = cnt[4];
-    const uint32_t nh = std::min(nf + nb, cap);
-    std::vector<uint32_t> full(e->w.seg_cap), list(nh), start(nseg + 1), res(nseg);
+    const uint32_t n1 = cnt[1] + cnt[4], n2 = cnt[5] + cnt[6];
+    const uint32_t nh = std::min(n1 + n2, cap);
+    std::vector<uint32_t> full(e->w.seg_cap), full2(e->w.seg_cap), list(nh), start(nseg + 1), res(nseg);
     std::vector<uint8_t> mode(nseg);
-    std::vector<uint64_t> ticks(nh);
+    std::vector<uint64_t> ticks(n1 + 1), ticks2(n2 + 1), tk(nh);
     if (nh) {
         HIP_TRY(hipMemcpy(full.data(), e->w.heavy_list, (size_t)e->w.seg_cap * 4, hipMemcpyDeviceToHost));
-        for (uint32_t i = 0; i < nh; i++) list[i] = i < nf ? full[i] : full[e->w.seg_cap - 1 - (i - nf)];
-        HIP_TRY(hipMemcpy(ticks.data(), e->w.hticks, nh * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(full2.data(), e->w.stream_list, (size_t)e->w.seg_cap * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(ticks.data(), e->w.hticks, n1 * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(ticks2.data(), e->w.sticks, n2 * 8, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < nh; i++) {
+            if (i < n1) {
+                list[i] = i < cnt[1] ? full[i] : full[e->w.seg_cap - 1 - (i - cnt[1])];
+                tk[i] = ticks[i];
+            } else {
+                const uint32_t k = i - n1;
+                list[i] = k < cnt[5] ? full2[k] : full2[e->w.seg_cap - 1 - (k - cnt[5])];
+                tk[i] = ticks2[k];
+            }
+        }
         HIP_TRY(hipMemcpy(start.data(), e->w.seg_start, (nseg + 1) * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(res.data(), e->w.seg_res, nseg * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(mode.data(), e->w.seg_mode, nseg, hipMemcpyDeviceToHost));
@@ -511,7 +528,7 @@ int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uin
     for (uint32_t i = 0; i < nh; i++) {
         const uint32_t sg = list[i];
         out[i].resource = res[sg]; out[i].events = start[sg + 1] - start[sg];
-        out[i].mode = mode[sg]; out[i].pad = 0; out[i].ticks = e->timing ? ticks[i] : 0;
+        out[i].mode = mode[sg]; out[i].pad = 0; out[i].ticks = e->timing ? tk[i] : 0;
     }
     *n_out = nh;
     return SF_OK;

@@ -150,12 +150,21 @@ struct ItemWriter {
 
 // ---------------------------------------------------------- QPS / WarmUp
 // Runs uniformly on every lane of the team; only the leader writes.
+// Only (windowStart, pass) of the second-window buckets matter here (the
+// deltas are applied by heavy_apply); MAXS bounds the sample count at compile
+// time and every bucket access is an unrolled compare-select (no lane memory).
+template <int MAXS>
 SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t s,
                      uint32_t res, uint32_t lo, uint32_t hi, bool warm) {
     const int S = st.S, wl = st.wl;
-    Bucket sec[SF_MAX_SAMPLE_COUNT];
-    Borrow bor[SF_MAX_SAMPLE_COUNT];
-    for (int i = 0; i < S; i++) { sec[i] = st.second[(size_t)res * S + i]; bor[i] = st.borrow[(size_t)res * S + i]; }
+    int64_t sws[MAXS], spass[MAXS], bws[MAXS], bpass[MAXS];
+#pragma unroll
+    for (int i = 0; i < MAXS; i++) {
+        if (i < S) {
+            sws[i] = st.second[(size_t)res * S + i].ws; spass[i] = st.second[(size_t)res * S + i].pass;
+            bws[i] = st.borrow[(size_t)res * S + i].ws; bpass[i] = st.borrow[(size_t)res * S + i].pass;
+        } else { sws[i] = WS_NONE; spass[i] = 0; bws[i] = WS_NONE; bpass[i] = 0; }
+    }
     const uint32_t r0 = st.rule_off[res];
     const DevRule rule = st.rules[r0];
     DevRuleState rs = st.rstate[r0];
@@ -172,16 +181,22 @@ SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyC
         const uint32_t b = team_first_true(tm, p, hi, [&](uint32_t j) { return io.ts[j] >= hw_end; });
         // second-window roll at t0 (OccupiableBucketLeapArray.currentWindow)
         const int idx = (int)(h % S);
-        if (sec[idx].ws != ws) {
-            Bucket nb = fresh_bucket(ws, st.max_rt);
-            const Borrow& bw = bor[(int)((ws / wl) % S)];
-            if (bw.ws <= ws && ws < bw.ws + wl) nb.pass = (int64_t)(int32_t)bw.pass;
-            sec[idx] = nb;
+        int64_t cur_pass = 0, p_prev = 0;
+#pragma unroll
+        for (int i = 0; i < MAXS; i++) {
+            if (i == idx) {
+                if (sws[i] != ws) {                    // roll: reset / create (resetWindowTo :52-64)
+                    const int64_t bw = bws[i], bp = bpass[i];   // borrow slot of ws is the same index
+                    sws[i] = ws;
+                    spass[i] = (bw <= ws && ws < bw + wl) ? (int64_t)(int32_t)bp : 0;
+                }
+                cur_pass = spass[i];
+            }
         }
-        int64_t p_prev = 0;
-        for (int i = 0; i < S; i++)
-            if (i != idx && !(wsub(t0, sec[i].ws) > st.interval)) p_prev = wadd(p_prev, sec[i].pass);
-        const int64_t base = p_prev + sec[idx].pass;
+#pragma unroll
+        for (int i = 0; i < MAXS; i++)
+            if (i < S && i != idx && !(wsub(t0, sws[i]) > st.interval)) p_prev = wadd(p_prev, spass[i]);
+        const int64_t base = p_prev + cur_pass;
         // minute-window bookkeeping for this hw's second
         const int64_t sn = t0 / 1000;
         if (sn != cur_sec) {
@@ -232,7 +247,9 @@ SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyC
                 j++;
             }
         }
-        sec[idx].pass = wadd(sec[idx].pass, passed);
+#pragma unroll
+        for (int i = 0; i < MAXS; i++)
+            if (i == idx) spass[i] = wadd(spass[i], passed);
         cur_sec_pass = wadd(cur_sec_pass, passed);
         p = b;
     }

@@ -96,6 +96,7 @@ struct Work {
     uint32_t seg_cap;                                   // min(max_batch, R)
     uint32_t* segflag; uint8_t* seg_mode;
     uint32_t* light_list; uint32_t* heavy_list; uint32_t* counters;   // [0] n_light [1] n_heavy front [2] hw slots [3] sec slots [4] n_heavy back
+                                                                      // [5] n_stream front [6] n_stream back
     int64_t* pcg; void* pscan_tmp; size_t pscan_tmp_bytes;
     uint32_t* item_lo; uint32_t* item_hi; int32_t* item_wait; uint32_t* n_items;
     void* acc_hw; void* acc_sec; uint32_t acc_cap;
@@ -103,6 +104,8 @@ struct Work {
     uint32_t* seg_nhw; uint32_t* seg_nsec;
     uint32_t heavy_min;                                 // segments longer than this go heavy
     uint64_t* hticks;                                   // [max heavy] k_heavy_decide clock per segment (timing)
+    uint32_t* stream_list;                              // THREAD / RL heavy segments (k_heavy_stream)
+    uint64_t* sticks;                                   // [max heavy] k_heavy_stream clock per segment (timing)
     unsigned long long* passbits;                       // [n/64+2] pass bit per sorted event (SM_THREAD)
 };
 
@@ -121,10 +124,12 @@ hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_byte
 hipError_t launch_init_state(const DevState& st, hipStream_t s);
 hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                            uint32_t shard_count, uint32_t shard_index, uint32_t key_bits,
-                           hipStream_t s, hipStream_t s2, hipEvent_t* ev /* SF_NUM_EVENTS */, bool timing);
+                           hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev /* SF_NUM_EVENTS */,
+                           bool timing);
 constexpr size_t ACC_BYTES = 72;                         // sizeof(Acc)
 // pipeline events: 0 start, 1 segments, 2 classified, 3 joined, 4 scattered,
-// 5 fork, 6 join (stream B), 7 heavy decided, 8 heavy filled, 9 light decided, 10 before classify
-constexpr int SF_NUM_EVENTS = 11;
+// 5 fork, 6 join (stream B), 7 heavy decided, 8 heavy filled, 9 light decided, 10 before classify,
+// 11 stream start (stream C), 12 stream done (stream C), 13 fill start (stream B, after the join with C)
+constexpr int SF_NUM_EVENTS = 14;
 
 }  // namespace sf

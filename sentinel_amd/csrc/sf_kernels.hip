@@ -9,14 +9,15 @@
 //   pc scan     inclusive prefix of entry acquireCount (heavy window budgets)
 //   k_classify  light segments -> lane interpreter; heavy -> window/skip algorithms
 //   stream A:   k_decide_light  one lane per light segment (sf_decide.h)
-//   stream B:   k_heavy_decide  one wavefront per heavy segment (sf_heavy.h)
+//   stream B:   k_heavy_decide  one wavefront per heavy QPS / WarmUp segment (sf_heavy.h)
+//   stream C:   k_heavy_stream  one 256-thread workgroup per heavy THREAD / RL segment (sf_stream.h)
 //               k_heavy_fill    verdicts + per-window counter deltas, device-wide
 //               k_heavy_apply   deltas applied to the LeapArray state in time order
 //   k_scatter   verdicts back to submission order
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
-#include "sf_heavy.h"
+#include "sf_stream.h"
 
 namespace sf {
 
@@ -145,16 +146,24 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
         }
         w.seg_mode[s] = mode;
     }
-    // long-running heavy segments first in the list, so that their wavefronts
-    // start first: [0, counters[1]) front, [seg_cap - counters[4], seg_cap) back
-    const bool slow = heavy && (mode == SM_THREAD || mode == SM_RL || mode == SM_GENERIC || hi - lo > 65536u);
+    // THREAD-grade and RateLimiter segments go to k_heavy_stream, the rest to
+    // k_heavy_decide.  Long-running segments first in each list, so that they
+    // start first: [0, front) and [seg_cap - back, seg_cap)
+    const bool strm = heavy && (mode == SM_THREAD || mode == SM_RL);
+    const bool big = hi - lo > 65536u;
+    const bool slow = heavy && !strm && (mode == SM_GENERIC || big);
     const uint32_t fpos = wave_append(&w.counters[1], slow);
-    const uint32_t bpos = wave_append(&w.counters[4], heavy && !slow);
+    const uint32_t bpos = wave_append(&w.counters[4], heavy && !strm && !slow);
     if (slow) w.heavy_list[fpos] = s;
-    else if (heavy) w.heavy_list[w.seg_cap - 1 - bpos] = s;
+    else if (heavy && !strm) w.heavy_list[w.seg_cap - 1 - bpos] = s;
+    const uint32_t sfp = wave_append(&w.counters[5], strm && big);
+    const uint32_t sbp = wave_append(&w.counters[6], strm && !big);
+    if (strm && big) w.stream_list[sfp] = s;
+    else if (strm) w.stream_list[w.seg_cap - 1 - sbp] = s;
 }
 
 // heavy-list entry of workgroup b: front part, then the back part
+// (k_heavy_apply walks both lists: every heavy item segment is in one of them)
 __device__ __forceinline__ bool heavy_at(const HeavyCtx& hc, uint32_t b, uint32_t* s) {
     const uint32_t nf = hc.n_heavy[0], nb = hc.n_heavy[3];
     if (b < nf) { *s = hc.heavy_list[b]; return true; }
@@ -185,21 +194,19 @@ static HeavyCtx heavy_ctx(const Work& w) {
     return hc;
 }
 
-// One wavefront per heavy segment (64-thread workgroups: the team needs no
-// barriers, and up to 10 segments share a CU under the THREAD ring's LDS).
+// One wavefront per heavy QPS / WarmUp / no-rule / generic segment (64-thread
+// workgroups: the team needs no barriers).  THREAD and RateLimiter segments
+// run in k_heavy_stream (sf_stream.h).
 template <int MAXS>
 __global__ void __launch_bounds__(64) k_heavy_decide(DevState st, SegIO io, HeavyCtx hc) {
-    __shared__ unsigned long long lds[RING_WORDS + THREAD_STAGE_WORDS];   // THREAD: pass ring + batch stage
     uint32_t s;
     if (!heavy_at(hc, blockIdx.x, &s)) return;
     const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1], res = hc.seg_res[s];
     Team tm{(int)threadIdx.x};
     const uint64_t t_start = hc.hticks ? wall_clock64() : 0;
     switch (hc.seg_mode[s]) {
-    case SM_QPS: heavy_qps(tm, st, io, hc, s, res, lo, hi, false); break;
-    case SM_WARM: heavy_qps(tm, st, io, hc, s, res, lo, hi, true); break;
-    case SM_RL: heavy_rl(tm, st, io, hc, s, res, lo, hi); break;
-    case SM_THREAD: heavy_thread(tm, st, io, hc, s, res, lo, hi, lds, lds + RING_WORDS); break;
+    case SM_QPS: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, false); break;
+    case SM_WARM: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, true); break;
     case SM_NORULE:
         if (tm.leader()) { hc.item_lo[lo] = lo; hc.item_hi[lo] = hi; hc.item_wait[lo] = 0; hc.n_items[s] = 1; }
         break;
@@ -293,9 +300,12 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
     wave_flush(ps, ks, hc.acc_sec);
 }
 
-__global__ void k_heavy_apply(DevState st, HeavyCtx hc, const uint32_t* seg_nhw, const uint32_t* seg_nsec) {
+__global__ void k_heavy_apply(DevState st, HeavyCtx hc, StreamCtx sc, const uint32_t* seg_nhw,
+                              const uint32_t* seg_nsec) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, s;
-    if (!heavy_at(hc, t, &s)) return;
+    const uint32_t nh = hc.n_heavy[0] + hc.n_heavy[3];
+    if (t < nh) { if (!heavy_at(hc, t, &s)) return; }
+    else if (!stream_at(sc, t - nh, &s)) return;
     if (hc.seg_mode[s] < SM_QPS) return;
     heavy_apply(st, hc, s, hc.seg_res[s], seg_nhw[s], seg_nsec[s]);
 }
@@ -335,7 +345,7 @@ hipError_t launch_init_state(const DevState& st, hipStream_t s) {
 
 hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                            uint32_t shard_count, uint32_t shard_index, uint32_t key_bits,
-                           hipStream_t s, hipStream_t s2, hipEvent_t* ev, bool timing) {
+                           hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing) {
     const uint32_t n = b.n;
     if (n == 0) return hipSuccess;
     const unsigned T = 256;
@@ -375,20 +385,27 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     HeavyCtx hc = heavy_ctx(w);
     if (timing) hc.hticks = w.hticks;
 
-    // heavy segments on the second stream, overlapping the light lanes
+    // heavy segments on streams B and C, overlapping the light lanes on A
     hipEventRecord(ev[5], s);                      // fork
     hipStreamWaitEvent(s2, ev[5], 0);
+    hipStreamWaitEvent(s3, ev[5], 0);
     const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
-    hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s2);
+    hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s3);
+    hipEventRecord(ev[11], s3);
+    StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, timing ? w.sticks : nullptr};
+    hipLaunchKernelGGL(k_heavy_stream, dim3(max_heavy), dim3(HS_T), 0, s3, st, io, hc, sc);
+    hipEventRecord(ev[12], s3);
     if (st.S <= 2)
         hipLaunchKernelGGL(k_heavy_decide<2>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     else
         hipLaunchKernelGGL(k_heavy_decide<SF_MAX_SAMPLE_COUNT>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     if (timing) hipEventRecord(ev[7], s2);
+    hipStreamWaitEvent(s2, ev[12], 0);             // k_heavy_fill reads the stream kernel's items and pass bits
+    if (timing) hipEventRecord(ev[13], s2);
     hipLaunchKernelGGL(k_heavy_fill, dim3(blocks(n, 256 * FILL_ITERS)), dim3(256), 0, s2, st, io, hc, w.head,
                        w.head_scan);
     if (timing) hipEventRecord(ev[8], s2);
-    hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, w.seg_nhw, w.seg_nsec);
+    hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, sc, w.seg_nhw, w.seg_nsec);
 
     const unsigned TD = 128;
     if (st.S <= 2)

@@ -177,8 +177,11 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         uint32_t lo = seg_start[s], hi = seg_start[s + 1], res = seg_res[s];
         Team tm;
         switch (mode[s]) {
-        case SM_QPS: heavy_qps(tm, e->st, io, hc, s, res, lo, hi, false); break;
-        case SM_WARM: heavy_qps(tm, e->st, io, hc, s, res, lo, hi, true); break;
+        case SM_QPS:
+        case SM_WARM:
+            if (e->st.S <= 2) heavy_qps<2>(tm, e->st, io, hc, s, res, lo, hi, mode[s] == SM_WARM);
+            else heavy_qps<SF_MAX_SAMPLE_COUNT>(tm, e->st, io, hc, s, res, lo, hi, mode[s] == SM_WARM);
+            break;
         case SM_RL: heavy_rl(tm, e->st, io, hc, s, res, lo, hi); break;
         case SM_THREAD: heavy_thread(tm, e->st, io, hc, s, res, lo, hi, nullptr, nullptr); break;
         case SM_NORULE: ilo[lo] = lo; ihi[lo] = hi; iwait[lo] = 0; nitems[s] = 1; break;

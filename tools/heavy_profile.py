@@ -30,7 +30,7 @@ eng.set_timing(True)
 eng.submit_device(b1, out)
 eng.sync()
 st = eng.stats()
-print(f"light {st.light_ms:.2f} ms  heavy_decide {st.heavy_decide_ms:.2f} ms  fill {st.heavy_fill_ms:.2f} ms  "
+print(f"light {st.light_ms:.2f} ms  heavy_decide {st.heavy_decide_ms:.2f} ms  stream {st.stream_ms:.2f} ms  fill {st.heavy_fill_ms:.2f} ms  "
       f"sort {st.sort_ms:.2f} ms  scatter {st.scatter_ms:.2f} ms")
 prof = eng.heavy_profile()
 prof.sort(key=lambda x: -x[3])
