@@ -330,6 +330,11 @@ int  sf_load_cluster_rules(sf_engine* e, const sf_cluster_flow_rule* flow, uint3
                            const sf_cluster_param_rule* param, uint32_t n_param,
                            const sf_hot_item* items, uint32_t n_items);
 int  sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* out);
+/* ClusterMetric.getSum(event) of a cluster flow rule at time now_ms
+ * (ClusterMetric.java:47-55; rolls the current bucket like the reference).
+ * event: ClusterFlowEvent ordinal (PASS 0, BLOCK 1, PASS_REQUEST 2,
+ * BLOCK_REQUEST 3, OCCUPIED_PASS 4, OCCUPIED_BLOCK 5, WAITING 6). */
+int  sf_cluster_sum(sf_engine* e, int64_t flow_id, int event, int64_t now_ms, int64_t* out);
 
 /* State read-back and the per-second metric snapshot (StatisticNode.metrics). */
 int  sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out);

@@ -14,6 +14,8 @@
 #include <vector>
 
 #include "sf_decide.h"
+#include "sf_token.h"
+#include <unordered_map>
 
 using namespace sf;
 
@@ -48,7 +50,25 @@ struct sf_engine {
     sf_stats stats{};
     std::vector<void*> user_allocs;
     std::mutex mu;
+    // cluster token server (sf_token.hip)
+    TokState ts{};
+    TokWork tw{};
+    uint32_t tw_cap = 0;
+    std::vector<sf_namespace> host_ns;
+    std::vector<sf_cluster_flow_rule> host_cflow;
+    std::vector<sf_cluster_param_rule> host_cparam;
+    std::vector<sf_hot_item> host_citems;
+    std::vector<int64_t> cflow_ids;           // flow rule index -> flowId
+    void* tok_stage = nullptr; size_t tok_stage_bytes = 0;
+    int64_t* d_sum = nullptr;
 };
+
+static void free_tok_work(TokWork& w) {
+    void* ptrs[] = {w.nskey_in, w.nskey_out, w.idx_in, w.idx_out, w.key_in, w.key_out, w.rule_of, w.pending,
+                    w.head, w.head_scan, w.seg_start, w.n_seg, w.sort8_tmp, w.sort64_tmp, w.scan_tmp};
+    for (void* p : ptrs) if (p) hipFree(p);
+    w = TokWork{};
+}
 
 extern "C" {
 
@@ -92,6 +112,10 @@ void sf_destroy(sf_engine* e) {
                     e->w.seg_nhw, e->w.seg_nsec, e->w.hticks, e->w.passbits, e->w.stream_list, e->w.sticks};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
+    void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
+                     (void*)e->ts.items, e->tok_stage, e->d_sum};
+    for (void* p : tptrs) if (p) hipFree(p);
+    free_tok_work(e->tw);
     for (auto& x : e->ev) if (x) hipEventDestroy(x);
     if (e->stream) hipStreamDestroy(e->stream);
     if (e->stream2) hipStreamDestroy(e->stream2);
@@ -149,6 +173,10 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     HIP_TRY(hipMemsetAsync(st.ptab, 0, pcap * sizeof(ParamSlot), e->stream));
     HIP_TRY(hipMemsetAsync(st.err, 0, sizeof(int32_t), e->stream));
     HIP_TRY(launch_init_state(st, e->stream));
+    e->ts.err = st.err;
+    e->ts.exceed_count = c.exceed_count;
+    e->ts.max_occupy_ratio = c.max_occupy_ratio;
+    DALLOC(e->d_sum, sizeof(int64_t));
 
     Work& w = e->w;
     const size_t N = c.max_batch;
@@ -442,15 +470,231 @@ int sf_snapshot(sf_engine* e, int64_t, sf_metric_row*, uint32_t, uint32_t* n_out
     if (n_out) *n_out = 0;
     return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "metric snapshot not on the GPU path yet");
 }
-int sf_load_namespaces(sf_engine* e, const sf_namespace*, uint32_t) {
-    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "token server not on the GPU path yet");
+// ---------------------------------------------------------------- cluster token server
+// Rebuild the device rule table, flowId index and namespace table from the
+// host copies (ClusterFlowRuleManager / ClusterParamFlowRuleManager /
+// ClusterServerConfigManager state).  Metric state is reset when
+// `reset_state` (a rule reload creates new ClusterMetric objects:
+// ClusterFlowRuleManager.java:361-362, ClusterParamFlowRuleManager.java:354-355).
+static int tok_rebuild(sf_engine* e, bool reset_state) {
+    TokState& ts = e->ts;
+    const uint32_t nf = (uint32_t)e->host_cflow.size(), np = (uint32_t)e->host_cparam.size();
+    std::unordered_map<uint32_t, int32_t> ns_index;
+    for (size_t i = 0; i < e->host_ns.size(); i++) ns_index.emplace(e->host_ns[i].namespace_id, (int32_t)i);
+    std::vector<ClRule> rules(nf + np);
+    auto fill = [&](ClRule& r, int64_t id, double count, int32_t tt, uint32_t ns, int32_t S, int32_t I) {
+        r.count = count; r.flow_id = id; r.threshold_type = tt;
+        auto it = ns_index.find(ns);
+        r.ns = it == ns_index.end() ? -1 : it->second;
+        r.S = S; r.wl = I / S; r.interval = I;
+    };
+    for (uint32_t i = 0; i < nf; i++) {
+        const sf_cluster_flow_rule& f = e->host_cflow[i];
+        fill(rules[i], f.flow_id, f.count, f.threshold_type, f.namespace_id, f.sample_count, f.window_interval_ms);
+        rules[i].is_param = 0; rules[i].item_off = rules[i].item_cnt = 0;
+    }
+    for (uint32_t i = 0; i < np; i++) {
+        const sf_cluster_param_rule& f = e->host_cparam[i];
+        ClRule& r = rules[nf + i];
+        fill(r, f.flow_id, f.count, f.threshold_type, f.namespace_id, f.sample_count, f.window_interval_ms);
+        r.is_param = 1; r.item_off = f.item_offset; r.item_cnt = f.item_count;
+    }
+    // flowId -> rule index, open addressing; the first rule of an id wins (like the oracle's lookup)
+    uint64_t cap = 16;
+    while (cap < 2ull * (nf + np) + 2) cap <<= 1;
+    std::vector<IdSlot> tab(cap, IdSlot{0, -1, -1});
+    auto put = [&](int64_t id, int32_t idx, bool param) {
+        uint64_t x = (uint64_t)id * 0x9e3779b97f4a7c15ULL;
+        uint64_t i = mix64(x) & (cap - 1);
+        while (tab[i].id != 0 && tab[i].id != id) i = (i + 1) & (cap - 1);
+        tab[i].id = id;
+        int32_t& slot = param ? tab[i].param : tab[i].flow;
+        if (slot < 0) slot = idx;
+    };
+    for (uint32_t i = 0; i < nf; i++) if (rules[i].flow_id > 0) put(rules[i].flow_id, (int32_t)i, false);
+    for (uint32_t i = 0; i < np; i++) if (rules[nf + i].flow_id > 0) put(rules[nf + i].flow_id, (int32_t)(nf + i), true);
+    std::vector<ClNs> ns(e->host_ns.size());
+    for (size_t i = 0; i < ns.size(); i++) {
+        ns[i].connected = e->host_ns[i].connected_count;
+        ns[i].has_limiter = e->host_ns[i].max_allowed_qps >= 0;   // GlobalRequestLimiter.initIfAbsent
+        ns[i].max_qps = e->host_ns[i].max_allowed_qps;
+    }
+    std::vector<DevHotItem> items(e->host_citems.size());
+    for (size_t i = 0; i < items.size(); i++) {
+        items[i].bits = e->host_citems[i].bits; items[i].count = e->host_citems[i].count; items[i].tag = e->host_citems[i].tag;
+    }
+    hipStream_t s = e->stream;
+    auto upload = [&](void** dst, const void* src, size_t bytes) -> int {
+        if (*dst) { hipFree(*dst); *dst = nullptr; }
+        HIP_TRY(hipMalloc(dst, std::max<size_t>(bytes, 16)));
+        if (bytes) HIP_TRY(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, s));
+        return SF_OK;
+    };
+    int rc;
+    if ((rc = upload((void**)&ts.rules, rules.data(), rules.size() * sizeof(ClRule)))) return rc;
+    if ((rc = upload((void**)&ts.idtab, tab.data(), tab.size() * sizeof(IdSlot)))) return rc;
+    if ((rc = upload((void**)&ts.ns, ns.data(), ns.size() * sizeof(ClNs)))) return rc;
+    if ((rc = upload((void**)&ts.items, items.data(), items.size() * sizeof(DevHotItem)))) return rc;
+    ts.id_mask = cap - 1;
+    ts.n_flow = nf; ts.n_rules = nf + np; ts.n_ns = (uint32_t)ns.size();
+    if (reset_state) {
+        if (ts.fstate) { hipFree(ts.fstate); ts.fstate = nullptr; }
+        HIP_TRY(hipMalloc((void**)&ts.fstate, std::max<size_t>(nf, 1) * sizeof(ClFlowState)));
+        HIP_TRY(tok_init_flow_state(ts.fstate, nf, s));
+        if (!ts.cptab) {
+            uint64_t pc = 1024;
+            while (pc < std::max<uint64_t>(e->cfg.param_capacity, 1024)) pc <<= 1;
+            HIP_TRY(hipMalloc((void**)&ts.cptab, pc * sizeof(CpSlot)));
+            ts.cp_mask = pc - 1;
+        }
+        HIP_TRY(hipMemsetAsync(ts.cptab, 0, (ts.cp_mask + 1) * sizeof(CpSlot), s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return SF_OK;
 }
-int sf_load_cluster_rules(sf_engine* e, const sf_cluster_flow_rule*, uint32_t, const sf_cluster_param_rule*,
-                          uint32_t, const sf_hot_item*, uint32_t) {
-    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "token server not on the GPU path yet");
+
+int sf_load_namespaces(sf_engine* e, const sf_namespace* ns, uint32_t n) {
+    if (!e || (n && !ns)) return fail(SF_ERR_INVALID, "null argument");
+    if (n > 255) return fail(SF_ERR_UNSUPPORTED, "at most 255 namespaces");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->host_ns.assign(ns, ns + n);
+    // GlobalRequestLimiter state of the loaded namespaces starts empty
+    LimState z;
+    for (int k = 0; k < LIM_S; k++) { z.ws[k] = WS_NONE; z.v[k] = 0; }
+    std::vector<LimState> lim(std::max<uint32_t>(n, 1), z);
+    if (e->ts.lim) { hipFree(e->ts.lim); e->ts.lim = nullptr; }
+    HIP_TRY(hipMalloc((void**)&e->ts.lim, lim.size() * sizeof(LimState)));
+    HIP_TRY(hipMemcpyAsync(e->ts.lim, lim.data(), lim.size() * sizeof(LimState), hipMemcpyHostToDevice, e->stream));
+    return tok_rebuild(e, false);
 }
-int sf_request_tokens(sf_engine* e, const sf_token_batch*, sf_token_results*) {
-    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "token server not on the GPU path yet");
+
+int sf_load_cluster_rules(sf_engine* e, const sf_cluster_flow_rule* flow, uint32_t n_flow,
+                          const sf_cluster_param_rule* param, uint32_t n_param, const sf_hot_item* items,
+                          uint32_t n_items) {
+    if (!e || (n_flow && !flow) || (n_param && !param) || (n_items && !items)) return fail(SF_ERR_INVALID, "null argument");
+    auto check = [&](int32_t S, int32_t I) {
+        return S > 0 && S <= CL_MAXS && I > 0 && I % S == 0;   // LeapArray.java:70-87
+    };
+    for (uint32_t i = 0; i < n_flow; i++)
+        if (!check(flow[i].sample_count, flow[i].window_interval_ms))
+            return fail(SF_ERR_UNSUPPORTED, "cluster flow rule: sample_count must be 1..16 and divide window_interval_ms");
+    for (uint32_t i = 0; i < n_param; i++) {
+        if (!check(param[i].sample_count, param[i].window_interval_ms))
+            return fail(SF_ERR_UNSUPPORTED, "cluster param rule: sample_count must be 1..16 and divide window_interval_ms");
+        if ((uint64_t)param[i].item_offset + param[i].item_count > n_items) return fail(SF_ERR_INVALID, "hot item range");
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->host_cflow.assign(flow, flow + n_flow);
+    e->host_cparam.assign(param, param + n_param);
+    e->host_citems.assign(items, items + n_items);
+    return tok_rebuild(e, true);
+}
+
+static int tok_work_ensure(sf_engine* e, uint32_t n) {
+    if (n <= e->tw_cap) return SF_OK;
+    free_tok_work(e->tw);
+    TokWork& w = e->tw;
+    const size_t N = std::max<uint32_t>(n, e->cfg.max_batch);
+    auto A = [&](void** p, size_t bytes) -> int { HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 16))); return SF_OK; };
+    int rc = 0;
+    rc |= A((void**)&w.nskey_in, N); rc |= A((void**)&w.nskey_out, N);
+    rc |= A((void**)&w.idx_in, N * 4); rc |= A((void**)&w.idx_out, N * 4);
+    rc |= A((void**)&w.key_in, N * 8); rc |= A((void**)&w.key_out, N * 8);
+    rc |= A((void**)&w.rule_of, N * 4); rc |= A((void**)&w.pending, N);
+    rc |= A((void**)&w.head, std::max<size_t>(N, 512) * 4); rc |= A((void**)&w.head_scan, N * 4);
+    rc |= A((void**)&w.seg_start, (N + 1) * 4); rc |= A((void**)&w.n_seg, 4);
+    if (rc) return SF_ERR_NOMEM;
+    HIP_TRY(tok_query_temp((uint32_t)N, &w.sort8_bytes, &w.sort64_bytes, &w.scan_bytes));
+    rc |= A(&w.sort8_tmp, w.sort8_bytes); rc |= A(&w.sort64_tmp, w.sort64_bytes); rc |= A(&w.scan_tmp, w.scan_bytes);
+    if (rc) return SF_ERR_NOMEM;
+    e->tw_cap = (uint32_t)N;
+    return SF_OK;
+}
+
+int sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* out) {
+    if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
+    if (in->n == 0) return SF_OK;
+    if (!in->flow_id || !in->count || !in->flags || !in->ts_ms) return fail(SF_ERR_INVALID, "missing request array");
+    if ((in->param_tag == nullptr) != (in->param_bits == nullptr)) return fail(SF_ERR_INVALID, "param_tag/param_bits");
+    std::lock_guard<std::mutex> lk(e->mu);
+    const uint32_t n = in->n;
+    int rc = tok_work_ensure(e, n);
+    if (rc) return fail(rc, "token work buffers");
+    if (!e->ts.rules) { int r2 = tok_rebuild(e, true); if (r2) return r2; }
+    if (!e->ts.lim) {
+        LimState z; for (int k = 0; k < LIM_S; k++) { z.ws[k] = WS_NONE; z.v[k] = 0; }
+        HIP_TRY(hipMalloc((void**)&e->ts.lim, sizeof(LimState)));
+        HIP_TRY(hipMemcpy(e->ts.lim, &z, sizeof z, hipMemcpyHostToDevice));
+    }
+    hipStream_t s = e->stream;
+    TokBatch b{};
+    b.n = n;
+    const bool has_param = in->param_tag != nullptr;
+    // staging: inputs then outputs, 256-B aligned
+    size_t off_fid = 0, off_cnt = align_up(off_fid + (size_t)n * 8), off_fl = align_up(off_cnt + (size_t)n * 4),
+           off_ts = align_up(off_fl + n), off_tag = align_up(off_ts + (size_t)n * 8),
+           off_bits = align_up(off_tag + (has_param ? n : 0)), off_st = align_up(off_bits + (has_param ? (size_t)n * 8 : 0)),
+           off_rem = align_up(off_st + n), off_wt = align_up(off_rem + (size_t)n * 4), need = align_up(off_wt + (size_t)n * 4);
+    if (need > e->tok_stage_bytes) {
+        if (e->tok_stage) hipFree(e->tok_stage);
+        e->tok_stage = nullptr;
+        HIP_TRY(hipMalloc(&e->tok_stage, need));
+        e->tok_stage_bytes = need;
+    }
+    char* base = (char*)e->tok_stage;
+    if (in->mem == SF_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(base + off_fid, in->flow_id, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(base + off_cnt, in->count, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(base + off_fl, in->flags, n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(base + off_ts, in->ts_ms, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        if (has_param) {
+            HIP_TRY(hipMemcpyAsync(base + off_tag, in->param_tag, n, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(base + off_bits, in->param_bits, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        }
+        b.flow_id = (const int64_t*)(base + off_fid); b.count = (const int32_t*)(base + off_cnt);
+        b.flags = (const uint8_t*)(base + off_fl); b.ts = (const int64_t*)(base + off_ts);
+        b.ptag = has_param ? (const uint8_t*)(base + off_tag) : nullptr;
+        b.pbits = has_param ? (const uint64_t*)(base + off_bits) : nullptr;
+    } else {
+        b.flow_id = in->flow_id; b.count = in->count; b.flags = in->flags; b.ts = in->ts_ms;
+        b.ptag = in->param_tag; b.pbits = in->param_bits;
+    }
+    TokOut o{};
+    const bool host_out = out->mem == SF_MEM_HOST;
+    if (host_out) {
+        o.status = (int8_t*)(base + off_st); o.remaining = (int32_t*)(base + off_rem); o.wait = (int32_t*)(base + off_wt);
+    } else {
+        if (!out->remaining || !out->wait_ms) return fail(SF_ERR_INVALID, "device results need remaining and wait_ms");
+        o.status = out->status; o.remaining = out->remaining; o.wait = out->wait_ms;
+    }
+    HIP_TRY(hipMemsetAsync(e->st.err, 0, sizeof(int32_t), s));
+    hipError_t le = tok_launch(e->ts, e->tw, b, o, s);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("token launch: ") + hipGetErrorString(le));
+    if (host_out) {
+        HIP_TRY(hipMemcpyAsync(out->status, o.status, n, hipMemcpyDeviceToHost, s));
+        if (out->remaining) HIP_TRY(hipMemcpyAsync(out->remaining, o.remaining, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        if (out->wait_ms) HIP_TRY(hipMemcpyAsync(out->wait_ms, o.wait, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    }
+    int32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, e->st.err, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (err) return fail(err, err == SF_ERR_CAPACITY ? "cluster param table capacity exceeded" : "invalid token batch");
+    return SF_OK;
+}
+
+int sf_cluster_sum(sf_engine* e, int64_t flow_id, int event, int64_t now_ms, int64_t* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    if (event < 0 || event >= CE_COUNT) return fail(SF_ERR_INVALID, "event");
+    std::lock_guard<std::mutex> lk(e->mu);
+    *out = 0;
+    for (size_t i = 0; i < e->host_cflow.size(); i++) {
+        if (e->host_cflow[i].flow_id != flow_id) continue;
+        HIP_TRY(tok_cluster_sum(e->ts, (uint32_t)i, event, now_ms, e->d_sum, e->stream));
+        HIP_TRY(hipMemcpyAsync(out, e->d_sum, 8, hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        return SF_OK;
+    }
+    return SF_OK;
 }
 
 int sf_device_alloc(sf_engine* e, size_t bytes, void** ptr) {

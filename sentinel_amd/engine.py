@@ -65,6 +65,7 @@ def _declare(L):
     f("sf_load_cluster_rules", I, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
     f("sf_request_tokens", I, P, C.POINTER(abi.sf_token_batch), C.POINTER(abi.sf_token_results))
+    f("sf_cluster_sum", I, P, C.c_int64, I, C.c_int64, C.POINTER(C.c_int64))
     f("sf_read_node", I, P, U32, C.POINTER(abi.sf_node_state))
     f("sf_read_entry_node", I, P, C.POINTER(abi.sf_node_state))
     f("sf_read_rule_state", I, P, U32, C.POINTER(abi.sf_rule_state))
@@ -230,6 +231,27 @@ class FlowEngine:
         n = C.c_uint32()
         _check(lib().sf_heavy_profile_read(self.h, buf, cap, C.byref(n)))
         return [(b.resource, b.events, b.mode, b.ticks / 100.0) for b in buf[:n.value]]
+
+    # ---- cluster token server (TokenService.requestToken / requestParamToken)
+    def load_namespaces(self, ns):
+        _check(lib().sf_load_namespaces(self.h, abi.rules_array(abi.sf_namespace, list(ns)), len(ns)))
+
+    def load_cluster_rules(self, flow=(), param=(), items=()):
+        _check(lib().sf_load_cluster_rules(self.h, abi.rules_array(abi.sf_cluster_flow_rule, list(flow)), len(flow),
+                                           abi.rules_array(abi.sf_cluster_param_rule, list(param)), len(param),
+                                           abi.rules_array(abi.sf_hot_item, list(items)), len(items)))
+
+    def request_tokens(self, batch: abi.HostTokenBatch) -> abi.HostTokenResults:
+        out = abi.HostTokenResults(batch.n)
+        b = batch.c_struct()
+        r = out.c_struct()
+        _check(lib().sf_request_tokens(self.h, C.byref(b), C.byref(r)))
+        return out
+
+    def cluster_sum(self, flow_id, event, now):
+        v = C.c_int64()
+        _check(lib().sf_cluster_sum(self.h, flow_id, event, now, C.byref(v)))
+        return v.value
 
     def sync(self):
         _check(lib().sf_sync(self.h))

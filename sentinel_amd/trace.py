@@ -220,3 +220,54 @@ def param_zipf(n_res: int, n_events: int, n_keys: int, duration_ms: int = 4000, 
     batch = abi.HostBatch(res, ts, np.ones(n_events, np.int32), np.full(n_events, abi.EV_IN, np.uint8),
                           arg_tag=tag, arg_bits=key.reshape(1, -1))
     return rules, batch
+
+
+def token_workload(n_req: int, n_flow: int = 200, n_param: int = 40, n_values: int = 2000, duration_ms: int = 4000,
+                   connected: int = 3, max_qps: float = -1.0, seed: int = 5, prio_frac: float = 0.1,
+                   param_frac: float = 0.3, bad_frac: float = 0.01):
+    """Config 5 shape: batched requestToken / requestParamToken from many
+    clients of one namespace (id 1), time-interleaved.  Flow ids 1..n_flow
+    (mostly AVG_LOCAL x connected, some GLOBAL; a few with non-default
+    sampleCount / interval), param ids n_flow+1.. with LONG values drawn
+    Zipf(1.1) over ``n_values`` (hot items on some).  A small fraction of
+    requests is invalid (id <= 0, count 0) or names no rule.  Namespace 2 has
+    no limiter.  Returns (namespaces, flow_rules, param_rules, items, batch)."""
+    rng = np.random.default_rng(seed)
+    ns = [abi.sf_namespace(namespace_id=1, connected_count=connected, max_allowed_qps=max_qps),
+          abi.sf_namespace(namespace_id=2, connected_count=connected + 2, max_allowed_qps=-1.0)]
+    geoms = [(10, 1000)] * 8 + [(4, 1000), (2, 500), (5, 2000), (1, 1000)]
+    flow = []
+    for k in range(n_flow):
+        s_c, ival = geoms[int(rng.integers(0, len(geoms)))]
+        flow.append(abi.sf_cluster_flow_rule(
+            flow_id=k + 1, count=float(rng.integers(1, 21)) + (0.5 if k % 7 == 3 else 0.0),
+            threshold_type=abi.THRESHOLD_GLOBAL if k % 5 == 0 else abi.THRESHOLD_AVG_LOCAL,
+            namespace_id=1 if k % 9 else 2, sample_count=s_c, window_interval_ms=ival))
+    items, param = [], []
+    for k in range(n_param):
+        off = len(items)
+        if k % 3 == 0:                      # hot items on the most frequent values
+            for v in range(3):
+                items.append(abi.sf_hot_item(tag=abi.TAG_LONG, count=int(rng.integers(0, 40)), bits=int(scramble(np.array([v]), n_values)[0])))
+        param.append(abi.sf_cluster_param_rule(
+            flow_id=n_flow + k + 1, count=float(rng.integers(1, 30)),
+            threshold_type=abi.THRESHOLD_GLOBAL if k % 4 == 0 else abi.THRESHOLD_AVG_LOCAL,
+            namespace_id=1 if k % 5 else 2, sample_count=10 if k % 6 else 4, window_interval_ms=1000,
+            item_offset=off, item_count=len(items) - off))
+    ts = T0 + np.sort(rng.integers(0, duration_ms, n_req)).astype(np.int64)
+    is_param = rng.random(n_req) < param_frac
+    fid = np.where(is_param, n_flow + 1 + rng.integers(0, max(1, n_param), n_req),
+                   1 + rng.integers(0, max(1, n_flow), n_req)).astype(np.int64)
+    cnt = rng.integers(1, 4, n_req).astype(np.int32)
+    flags = np.where(rng.random(n_req) < prio_frac, abi.TOK_PRIORITIZED, 0).astype(np.uint8)
+    flags = flags | np.where(is_param, abi.TOK_PARAM, 0).astype(np.uint8)
+    vals = scramble(zipf_bounded(rng, 1.1, n_values, n_req) - 1, n_values).astype(np.uint64)
+    tag = np.where(rng.random(n_req) < 0.01, abi.TAG_NULL, abi.TAG_LONG).astype(np.uint8)
+    bad = rng.random(n_req) < bad_frac
+    kind = rng.integers(0, 4, n_req)
+    fid = np.where(bad & (kind == 0), 0, fid)
+    fid = np.where(bad & (kind == 1), -5, fid)
+    cnt = np.where(bad & (kind == 2), 0, cnt).astype(np.int32)
+    fid = np.where(bad & (kind == 3), 10 ** 9, fid)          # no such rule
+    batch = abi.HostTokenBatch(fid, cnt, flags, ts, param_tag=tag, param_bits=vals)
+    return ns, flow, param, items, batch

@@ -1,0 +1,70 @@
+"""GPU parity of the batched cluster token server (sf_request_tokens) against
+the oracle's DefaultTokenService replay: TokenResult status, remaining and
+waitInMs per request, and every ClusterMetric counter afterwards, bit for bit.
+Run with -m gpu on an MI355X."""
+import numpy as np
+import pytest
+
+from sentinel_amd import abi, trace
+
+pytestmark = pytest.mark.gpu
+
+EVENTS = range(7)   # ClusterFlowEvent ordinals
+
+
+@pytest.fixture(scope="module")
+def eng_mod():
+    from sentinel_amd import engine
+    engine.lib()
+    return engine
+
+
+def compare_tokens(got, want, what=""):
+    bad = np.nonzero((got.status != want.status) | (got.remaining != want.remaining) | (got.wait_ms != want.wait_ms))[0]
+    if bad.size:
+        i = bad[0]
+        raise AssertionError(f"{what}: {bad.size} token results differ; first at {i}: engine=({got.status[i]},"
+                             f"{got.remaining[i]},{got.wait_ms[i]}) oracle=({want.status[i]},{want.remaining[i]},"
+                             f"{want.wait_ms[i]})")
+
+
+def run_tokens(eng_mod, so, n_req, split=1, seed=5, max_qps=-1.0, check_sums=True, **kw):
+    ns, flow, param, items, b = trace.token_workload(n_req, seed=seed, max_qps=max_qps, **kw)
+    cfg = abi.default_config(max_resources=4, max_batch=b.n, param_capacity=1 << 16)
+    e = eng_mod.FlowEngine(cfg)
+    o = so.OracleEngine(cfg)
+    for x in (e, o):
+        x.load_namespaces(ns)
+        x.load_cluster_rules(flow, param, items)
+    cuts = np.linspace(0, b.n, split + 1).astype(int)
+    for k, (lo, hi) in enumerate(zip(cuts[:-1], cuts[1:])):
+        sub = abi.HostTokenBatch(b.flow_id[lo:hi], b.count[lo:hi], b.flags[lo:hi], b.ts_ms[lo:hi],
+                                 param_tag=b.param_tag[lo:hi], param_bits=b.param_bits[lo:hi])
+        compare_tokens(e.request_tokens(sub), o.request_tokens(sub), f"batch {k}")
+    if check_sums:
+        now = int(b.ts_ms[-1])
+        for f in flow:
+            for ev in EVENTS:
+                a, w = e.cluster_sum(f.flow_id, ev, now), o.cluster_sum(f.flow_id, ev, now)
+                assert a == w, f"flowId {f.flow_id} event {ev}: engine {a} oracle {w}"
+    return e, o
+
+
+@pytest.mark.parametrize("split", [1, 4])
+def test_token_server_parity(eng_mod, so, split):
+    run_tokens(eng_mod, so, 60_000, split=split)
+
+
+@pytest.mark.parametrize("max_qps", [0.0, 500.0, 3000.0])
+def test_token_server_namespace_limiter(eng_mod, so, max_qps):
+    """GlobalRequestLimiter at and around the offered rate (TOO_MANY_REQUEST)."""
+    run_tokens(eng_mod, so, 40_000, split=3, seed=7, max_qps=max_qps)
+
+
+def test_token_server_heavy_values(eng_mod, so):
+    """Few values, many requests each (long per-value chains) and all prioritized."""
+    run_tokens(eng_mod, so, 50_000, split=2, seed=11, n_values=5, n_flow=5, n_param=3, prio_frac=1.0)
+
+
+def test_token_server_bad_requests(eng_mod, so):
+    run_tokens(eng_mod, so, 5_000, seed=13, bad_frac=0.5)
