@@ -61,6 +61,12 @@ struct sf_engine {
     std::vector<int64_t> cflow_ids;           // flow rule index -> flowId
     void* tok_stage = nullptr; size_t tok_stage_bytes = 0;
     int64_t* d_sum = nullptr;
+    // ENTRY_NODE and the metric snapshot (sf_entry.hip)
+    EntryNode* en = nullptr;
+    EntryAcc* en_acc = nullptr;
+    uint32_t* snap_counts = nullptr; uint32_t* snap_offsets = nullptr; uint32_t* snap_total = nullptr;
+    sf_metric_row* snap_rows = nullptr; uint32_t snap_cap = 0;
+    void* snap_scan = nullptr; size_t snap_scan_bytes = 0;
 };
 
 static void free_tok_work(TokWork& w) {
@@ -113,7 +119,8 @@ void sf_destroy(sf_engine* e) {
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
-                     (void*)e->ts.items, e->tok_stage, e->d_sum};
+                     (void*)e->ts.items, e->tok_stage, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
+                     e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch};
     for (void* p : tptrs) if (p) hipFree(p);
     free_tok_work(e->tw);
     for (auto& x : e->ev) if (x) hipEventDestroy(x);
@@ -177,6 +184,11 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     e->ts.exceed_count = c.exceed_count;
     e->ts.max_occupy_ratio = c.max_occupy_ratio;
     DALLOC(e->d_sum, sizeof(int64_t));
+    DALLOC(st.last_fetch, R * sizeof(int64_t));
+    HIP_TRY(hipMemsetAsync(st.last_fetch, 0xff, R * sizeof(int64_t), e->stream));   // lastFetchTime = -1
+    DALLOC(e->en, sizeof(EntryNode));
+    DALLOC(e->en_acc, sizeof(EntryAcc));
+    HIP_TRY(launch_entry_init(e->en, st.max_rt, e->stream));
 
     Work& w = e->w;
     const size_t N = c.max_batch;
@@ -382,6 +394,9 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     hipError_t le = launch_pipeline(e->st, e->w, b, dv, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s,
                                     e->stream2, e->stream3, e->ev, e->timing);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
+    // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream order)
+    le = launch_entry_node(e->st, b, dv.status, e->en, e->en_acc, s);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
     if (out->mem == SF_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, s));
         if (dv.wait) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait, (size_t)n * 4, hipMemcpyDeviceToHost, s));
@@ -452,8 +467,18 @@ int sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out) {
     return SF_OK;
 }
 
-int sf_read_entry_node(sf_engine* e, sf_node_state*) {
-    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "ENTRY_NODE aggregate not on the GPU path yet");
+int sf_read_entry_node(sf_engine* e, sf_node_state* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    EntryNode en;
+    HIP_TRY(hipMemcpyAsync(&en, e->en, sizeof en, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    std::memset(out, 0, sizeof *out);
+    for (int i = 0; i < SF_MAX_SAMPLE_COUNT; i++) { out->second[i].window_start = SF_WS_ABSENT; out->borrow_ws[i] = SF_WS_ABSENT; }
+    for (int i = 0; i < e->cfg.sample_count; i++) to_abi_bucket(en.second[i], &out->second[i]);
+    for (int i = 0; i < MINUTE; i++) to_abi_bucket(en.minute[i], &out->minute[i]);
+    out->cur_thread_num = en.threads;
+    return SF_OK;
 }
 
 int sf_read_rule_state(sf_engine* e, uint32_t idx, sf_rule_state* out) {
@@ -466,9 +491,33 @@ int sf_read_rule_state(sf_engine* e, uint32_t idx, sf_rule_state* out) {
     return SF_OK;
 }
 
-int sf_snapshot(sf_engine* e, int64_t, sf_metric_row*, uint32_t, uint32_t* n_out) {
-    if (n_out) *n_out = 0;
-    return fail(e ? SF_ERR_UNSUPPORTED : SF_ERR_INVALID, "metric snapshot not on the GPU path yet");
+int sf_snapshot(sf_engine* e, int64_t now_ms, sf_metric_row* out, uint32_t cap, uint32_t* n_out) {
+    if (!e || !n_out || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    *n_out = 0;
+    hipStream_t s = e->stream;
+    if (!e->snap_counts) {
+        HIP_TRY(hipMalloc((void**)&e->snap_counts, (size_t)e->R * 4));
+        HIP_TRY(hipMalloc((void**)&e->snap_offsets, (size_t)e->R * 4));
+        HIP_TRY(hipMalloc((void**)&e->snap_total, 4));
+        HIP_TRY(rocprim_scan_bytes(e->R, &e->snap_scan_bytes));
+        HIP_TRY(hipMalloc(&e->snap_scan, std::max<size_t>(e->snap_scan_bytes, 16)));
+    }
+    if (cap > e->snap_cap) {
+        if (e->snap_rows) hipFree(e->snap_rows);
+        e->snap_rows = nullptr;
+        HIP_TRY(hipMalloc((void**)&e->snap_rows, (size_t)cap * sizeof(sf_metric_row)));
+        e->snap_cap = cap;
+    }
+    HIP_TRY(launch_snapshot(e->st, now_ms, e->cfg.shard_count, e->cfg.shard_index, e->snap_counts, e->snap_offsets,
+                            e->snap_rows, cap, e->snap_total, e->snap_scan, e->snap_scan_bytes, s));
+    uint32_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, e->snap_total, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t k = std::min(total, cap);
+    if (k) HIP_TRY(hipMemcpy(out, e->snap_rows, (size_t)k * sizeof(sf_metric_row), hipMemcpyDeviceToHost));
+    *n_out = total;
+    return total <= cap ? SF_OK : fail(SF_ERR_CAPACITY, "snapshot rows exceed cap");
 }
 // ---------------------------------------------------------------- cluster token server
 // Rebuild the device rule table, flowId index and namespace table from the

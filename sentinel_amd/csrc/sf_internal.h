@@ -76,6 +76,26 @@ struct DevState {
     ParamSlot* ptab;
     uint64_t pcap_mask;
     int32_t* err;                  // device error word (capacity, invalid input)
+    int64_t* last_fetch;           // [R] StatisticNode.lastFetchTime (metric snapshot)
+};
+
+// Constants.ENTRY_NODE (Constants.java:66): the ClusterNode of all inbound
+// traffic, updated by StatisticSlot for EntryType.IN (StatisticSlot.java:64-178)
+struct EntryNode {
+    Bucket second[SF_MAX_SAMPLE_COUNT];
+    Bucket minute[SF_MINUTE_BUCKETS];
+    int64_t threads;
+};
+// per-submit reduction of the IN events into the ENTRY_NODE windows: one row
+// per window of the batch (relative to the window of its first event)
+constexpr uint32_t EN_TBL = 4096;
+struct EntryAcc {
+    unsigned long long sec[EN_TBL][6];     // pass, block, succ, rt, exc, touched
+    unsigned long long min[EN_TBL][6];
+    long long minrt_sec[EN_TBL], minrt_min[EN_TBL];
+    long long threads;
+    unsigned int overflow;                 // a window beyond EN_TBL rows: slow exact path
+    unsigned int pad;
 };
 
 // Sorted-order working buffers of one batch.
@@ -122,6 +142,13 @@ struct DevVerdicts { uint8_t* status; int32_t* wait; uint16_t* rule; };
 hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes,
                             size_t* pscan_bytes);
 hipError_t launch_init_state(const DevState& st, hipStream_t s);
+hipError_t launch_entry_node(const DevState& st, const DevBatch& b, const uint8_t* vstatus, EntryNode* en,
+                             EntryAcc* acc, hipStream_t s);
+hipError_t launch_entry_init(EntryNode* en, int64_t max_rt, hipStream_t s);
+hipError_t rocprim_scan_bytes(uint32_t n, size_t* bytes);
+hipError_t launch_snapshot(const DevState& st, int64_t now, uint32_t shard_count, uint32_t shard_index,
+                           uint32_t* counts, uint32_t* offsets, sf_metric_row* out, uint32_t cap, uint32_t* total,
+                           void* scan_tmp, size_t scan_bytes, hipStream_t s);
 hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                            uint32_t shard_count, uint32_t shard_index, uint32_t key_bits,
                            hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev /* SF_NUM_EVENTS */,

@@ -337,6 +337,11 @@ hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_byte
                                    rocprim::plus<int64_t>());
 }
 
+hipError_t rocprim_scan_bytes(uint32_t n, size_t* bytes) {
+    return rocprim::exclusive_scan(nullptr, *bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
+                                   rocprim::plus<uint32_t>());
+}
+
 hipError_t launch_init_state(const DevState& st, hipStream_t s) {
     size_t n_sec = (size_t)st.R * st.S, n_min = (size_t)st.R * MINUTE;
     hipLaunchKernelGGL(k_init_state, dim3(2048), dim3(256), 0, s, st, n_sec, n_min);

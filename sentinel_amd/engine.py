@@ -212,6 +212,20 @@ class FlowEngine:
         _check(lib().sf_read_node(self.h, res, C.byref(st)))
         return st
 
+    has_entry_node = True
+
+    def read_entry_node(self) -> abi.sf_node_state:
+        st = abi.sf_node_state()
+        _check(lib().sf_read_entry_node(self.h, C.byref(st)))
+        return st
+
+    def snapshot(self, now, cap=1 << 20):
+        """StatisticNode.metrics() of every node (MetricTimerListener): MetricNode rows."""
+        rows = (abi.sf_metric_row * cap)()
+        n = C.c_uint32()
+        _check(lib().sf_snapshot(self.h, now, rows, cap, C.byref(n)))
+        return [rows[i] for i in range(n.value)]
+
     def read_rule_state(self, idx) -> abi.sf_rule_state:
         s = abi.sf_rule_state()
         _check(lib().sf_read_rule_state(self.h, idx, C.byref(s)))

@@ -45,3 +45,16 @@ def run_both(make_engine, make_oracle, cfg, flow_rules=(), param_rules=(), items
     for b in batches:
         outs.append((eng.submit(b), ora.submit(b)))
     return eng, ora, outs
+
+
+def compare_entry_node(eng, ora, sample_count=2, what=""):
+    x = abi.node_state_to_dict(eng.read_entry_node(), sample_count)
+    y = abi.node_state_to_dict(ora.read_entry_node(), sample_count)
+    for k in x:
+        if x[k] != y[k]:
+            raise AssertionError(f"{what}: ENTRY_NODE field {k} differs:\n engine={x[k]}\n oracle={y[k]}")
+
+
+def metric_rows(rows):
+    return sorted((r.resource, r.timestamp, r.pass_qps, r.block_qps, r.success_qps, r.exception_qps, r.rt,
+                   r.occupied_pass_qps) for r in rows)

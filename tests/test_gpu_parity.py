@@ -107,3 +107,20 @@ def test_invalid_batches_rejected(eng_mod):
     with pytest.raises(eng_mod.EngineError):
         e.submit(b)
     e.submit(abi.HostBatch([1], [trace.T0], [1], [0]))    # still usable
+
+
+def test_entry_node_and_snapshot(eng_mod, so):
+    """ENTRY_NODE (all IN traffic) and the per-second MetricNode snapshot
+    (StatisticNode.metrics via MetricTimerListener), twice across batches so
+    lastFetchTime and the currentWindow(now) side effect are exercised."""
+    w = workloads.config3(R=3000, n=120_000, seed=23, split=3, duration_ms=9000)
+    e, o = eng_mod.FlowEngine(w["cfg"]), so.OracleEngine(w["cfg"])
+    for x in (e, o):
+        x.load_flow_rules(w["flow"])
+    for k, b in enumerate(w["batches"]):
+        parity.compare_verdicts(e.submit(b), o.submit(b), f"batch {k}")
+        parity.compare_entry_node(e, o, what=f"batch {k}")
+        now = int(b.ts_ms[-1]) + 1
+        got, want = parity.metric_rows(e.snapshot(now)), parity.metric_rows(o.snapshot(now))
+        assert got == want, f"snapshot after batch {k}: {len(got)} vs {len(want)} rows"
+    parity.compare_nodes(e, o, w["nodes"])

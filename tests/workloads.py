@@ -148,6 +148,8 @@ def run(make_engine, make_oracle, w):
     for k, (a, b) in enumerate(outs):
         parity.compare_verdicts(a, b, f"batch{k}")
     parity.compare_nodes(eng, ora, w["nodes"], sample_count=w["cfg"].sample_count)
+    if getattr(eng, "has_entry_node", False):
+        parity.compare_entry_node(eng, ora, sample_count=w["cfg"].sample_count)
     if w.get("n_flow"):
         parity.compare_rule_states(eng, ora, w["n_flow"])
     return eng, ora, outs
