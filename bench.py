@@ -161,6 +161,31 @@ def main():
                                "k_heavy_fill": round(st.heavy_fill_ms / k, 3),
                                "scatter": round(st.scatter_ms / k, 3)}}
 
+    # node-wide ENTRY_NODE over the shards: RCCL all-reduce (off the decision
+    # path, after the timed region)
+    aggregate = None
+    try:
+        from sentinel_amd import dist as sdist
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)              # RCCL prints a version banner on stdout: keep stdout to the one JSON line
+        try:
+            if dist:
+                sdist.rccl_join(eng)
+            else:
+                eng.comm_init(1, 0, engine.comm_unique_id())
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+        eng.sync()
+        t_ag = time.perf_counter()
+        node = eng.entry_node_allreduce()
+        aggregate = {"what": "ENTRY_NODE all-reduce (MAX window, SUM counters, MIN minRt)", "backend": "rccl",
+                     "ranks": world, "ms": round((time.perf_counter() - t_ag) * 1e3, 3),
+                     "node_threads": int(node.cur_thread_num)}
+    except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
+        aggregate = {"error": str(ex)[:200]}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(rules, hb, R_local, args.cpu_sample)
@@ -175,7 +200,7 @@ def main():
                            "resources": R_total, "events_per_batch_per_gpu": hb.n, "entries_per_batch_per_gpu": n_entry,
                            "resources_touched": n_seg, "pass_fraction": round(n_pass / max(1, n_entry), 4),
                            "parallelism": f"resource-sharded x{world}"},
-                "roofline": roofline, "cpu_baseline": cpu}
+                "roofline": roofline, "cpu_baseline": cpu, "aggregate": aggregate}
         print(json.dumps(line), flush=True)
     for b in batches:
         b.free()

@@ -342,6 +342,15 @@ int  sf_read_entry_node(sf_engine* e, sf_node_state* out);
 int  sf_read_rule_state(sf_engine* e, uint32_t rule_index, sf_rule_state* out);
 int  sf_snapshot(sf_engine* e, int64_t now_ms, sf_metric_row* out, uint32_t cap, uint32_t* n_out);
 
+/* Node-wide Constants.ENTRY_NODE over the resource shards of a node: one
+ * engine per GPU, joined by RCCL (xGMI).  Rank 0 creates the id, the host
+ * distributes it (any channel), every rank calls sf_comm_init.  The merge is
+ * exact: per bucket slot the node-wide latest window (all-reduce MAX), then
+ * SUM of its counters, MIN of minRt, SUM of curThreadNum (sentinel_amd/dist.py). */
+int  sf_comm_unique_id(uint8_t* out, size_t len /* >= 128 */);
+int  sf_comm_init(sf_engine* e, int nranks, int rank, const uint8_t* id, size_t len);
+int  sf_entry_node_allreduce(sf_engine* e, sf_node_state* out);
+
 /* Device helpers so hosts without a GPU framework can stage HBM inputs. */
 int  sf_device_alloc(sf_engine* e, size_t bytes, void** ptr);
 int  sf_device_free(sf_engine* e, void* ptr);

@@ -27,6 +27,7 @@ THRESHOLD_AVG_LOCAL, THRESHOLD_GLOBAL = 0, 1
 
 SF_MAX_SAMPLE_COUNT = 16
 SF_MINUTE_BUCKETS = 60
+SF_WS_ABSENT = -(2 ** 63)
 SF_MAX_RULES_PER_RESOURCE = 8
 SF_MAX_ARGS = 4
 
@@ -236,6 +237,22 @@ class HostBatch:
         self.arg_bits = arg_bits
         self.n_args = None if n_args is None else np.ascontiguousarray(n_args, dtype=np.uint8)
         self.n = n
+
+    def shard(self, world: int, rank: int) -> "HostBatch":
+        """The events of the resources ``res % world == rank`` (hash sharding),
+        time order kept; entry_ref indices are remapped into the shard."""
+        sel = np.nonzero(self.res_id % world == rank)[0]
+        er = ct = None
+        if self.entry_ref is not None:
+            pos = np.full(self.n, -1, np.int64)
+            pos[sel] = np.arange(sel.size)
+            er = self.entry_ref[sel].copy()
+            er[er >= 0] = pos[er[er >= 0]]
+            ct = None if self.create_ts is None else self.create_ts[sel].copy()
+        at = None if self.arg_tag is None else self.arg_tag[:, sel].copy()
+        ab = None if self.arg_bits is None else self.arg_bits[:, sel].copy()
+        na = None if self.n_args is None else self.n_args[sel]
+        return HostBatch(self.res_id[sel], self.ts_ms[sel], self.count[sel], self.flags[sel], er, ct, at, ab, na)
 
     def subset(self, lo: int, hi: int) -> "HostBatch":
         """Contiguous slice [lo, hi); entry_ref indices are rebased (refs before lo become -1)."""

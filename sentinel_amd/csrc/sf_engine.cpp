@@ -15,6 +15,7 @@
 
 #include "sf_decide.h"
 #include "sf_token.h"
+#include <rccl/rccl.h>
 #include <unordered_map>
 
 using namespace sf;
@@ -67,6 +68,9 @@ struct sf_engine {
     uint32_t* snap_counts = nullptr; uint32_t* snap_offsets = nullptr; uint32_t* snap_total = nullptr;
     sf_metric_row* snap_rows = nullptr; uint32_t snap_cap = 0;
     void* snap_scan = nullptr; size_t snap_scan_bytes = 0;
+    // node-wide aggregate over the ranks of a node (RCCL over xGMI)
+    ncclComm_t comm = nullptr;
+    int64_t* agg = nullptr;               // [ws (S+60) | gws (S+60) | vals ((S+60)*6+1) | minrt (S+60)]
 };
 
 static void free_tok_work(TokWork& w) {
@@ -122,6 +126,8 @@ void sf_destroy(sf_engine* e) {
                      (void*)e->ts.items, e->tok_stage, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
                      e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch};
     for (void* p : tptrs) if (p) hipFree(p);
+    if (e->agg) hipFree(e->agg);
+    if (e->comm) ncclCommDestroy(e->comm);
     free_tok_work(e->tw);
     for (auto& x : e->ev) if (x) hipEventDestroy(x);
     if (e->stream) hipStreamDestroy(e->stream);
@@ -743,6 +749,66 @@ int sf_cluster_sum(sf_engine* e, int64_t flow_id, int event, int64_t now_ms, int
         HIP_TRY(hipStreamSynchronize(e->stream));
         return SF_OK;
     }
+    return SF_OK;
+}
+
+// ---------------------------------------------------------------- node-wide aggregate (RCCL)
+int sf_comm_unique_id(uint8_t* out, size_t len) {
+    if (!out || len < NCCL_UNIQUE_ID_BYTES) return fail(SF_ERR_INVALID, "unique id buffer");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(SF_ERR_DEVICE, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return SF_OK;
+}
+
+int sf_comm_init(sf_engine* e, int nranks, int rank, const uint8_t* id, size_t len) {
+    if (!e || !id || len < NCCL_UNIQUE_ID_BYTES || nranks <= 0 || rank < 0 || rank >= nranks)
+        return fail(SF_ERR_INVALID, "sf_comm_init arguments");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->comm) { ncclCommDestroy(e->comm); e->comm = nullptr; }
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclResult_t r = ncclCommInitRank(&e->comm, nranks, uid, rank);
+    if (r != ncclSuccess) { e->comm = nullptr; return fail(SF_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)); }
+    if (!e->agg) HIP_TRY(hipMalloc((void**)&e->agg, 4096 * sizeof(int64_t)));
+    return SF_OK;
+}
+
+int sf_entry_node_allreduce(sf_engine* e, sf_node_state* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->comm) return fail(SF_ERR_INVALID, "sf_comm_init first");
+    const int S = e->cfg.sample_count, nb = S + MINUTE;
+    hipStream_t s = e->stream;
+    int64_t *ws = e->agg, *gws = ws + nb, *vals = gws + nb, *minrt = vals + nb * 6 + 1;
+    HIP_TRY(launch_en_pack_ws(e->en, S, ws, s));
+    auto nc = [&](ncclResult_t r, const char* what) -> int {
+        return r == ncclSuccess ? SF_OK : fail(SF_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+    };
+    int rc;
+    if ((rc = nc(ncclAllReduce(ws, gws, nb, ncclInt64, ncclMax, e->comm, s), "allreduce max"))) return rc;
+    HIP_TRY(launch_en_pack_vals(e->en, S, gws, vals, minrt, s));
+    if ((rc = nc(ncclAllReduce(vals, vals, (size_t)nb * 6 + 1, ncclInt64, ncclSum, e->comm, s), "allreduce sum"))) return rc;
+    if ((rc = nc(ncclAllReduce(minrt, minrt, nb, ncclInt64, ncclMin, e->comm, s), "allreduce min"))) return rc;
+    std::vector<int64_t> h_ws(nb), h_vals((size_t)nb * 6 + 1), h_min(nb);
+    HIP_TRY(hipMemcpyAsync(h_ws.data(), gws, nb * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_vals.data(), vals, h_vals.size() * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_min.data(), minrt, nb * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::memset(out, 0, sizeof *out);
+    for (int i = 0; i < SF_MAX_SAMPLE_COUNT; i++) { out->second[i].window_start = SF_WS_ABSENT; out->borrow_ws[i] = SF_WS_ABSENT; }
+    for (int i = 0; i < MINUTE; i++) out->minute[i].window_start = SF_WS_ABSENT;
+    for (int i = 0; i < nb; i++) {
+        sf_bucket& b = i < S ? out->second[i] : out->minute[i - S];
+        if (h_ws[i] == INT64_MIN) continue;
+        b.window_start = h_ws[i];
+        const int64_t* v = &h_vals[(size_t)i * 6];
+        b.pass = v[0]; b.block = v[1]; b.exception = v[2]; b.success = v[3]; b.rt = v[4]; b.occupied_pass = v[5];
+        b.min_rt = h_min[i] == INT64_MAX ? e->cfg.statistic_max_rt : h_min[i];
+    }
+    out->cur_thread_num = h_vals[(size_t)nb * 6];
     return SF_OK;
 }
 

@@ -236,6 +236,37 @@ hipError_t launch_entry_node(const DevState& st, const DevBatch& b, const uint8_
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ node-wide merge (RCCL)
+// pack: window start per slot (absent: INT64_MIN) for an all-reduce MAX
+__global__ void k_en_pack_ws(const EntryNode* en, int S, int64_t* ws) {
+    const int i = threadIdx.x;
+    if (i < S) ws[i] = en->second[i].ws == WS_NONE ? INT64_MIN : en->second[i].ws;
+    if (i < MINUTE) ws[S + i] = en->minute[i].ws == WS_NONE ? INT64_MIN : en->minute[i].ws;
+}
+// after the MAX: counters of slots that hold the node-wide latest window (others 0),
+// minRt (others INT64_MAX), thread count last
+__global__ void k_en_pack_vals(const EntryNode* en, int S, const int64_t* gws, int64_t* vals, int64_t* minrt) {
+    const int i = threadIdx.x;
+    const int nb = S + MINUTE;
+    if (i < nb) {
+        const Bucket& b = i < S ? en->second[i] : en->minute[i - S];
+        const bool keep = b.ws != WS_NONE && b.ws == gws[i];
+        const int64_t v[6] = {b.pass, b.block, b.exc, b.succ, b.rt, b.occ};
+        for (int k = 0; k < 6; k++) vals[i * 6 + k] = keep ? v[k] : 0;
+        minrt[i] = keep ? b.min_rt : INT64_MAX;
+    }
+    if (i == 0) vals[nb * 6] = en->threads;
+}
+hipError_t launch_en_pack_ws(const EntryNode* en, int S, int64_t* ws, hipStream_t s) {
+    hipLaunchKernelGGL(k_en_pack_ws, dim3(1), dim3(64), 0, s, en, S, ws);
+    return hipGetLastError();
+}
+hipError_t launch_en_pack_vals(const EntryNode* en, int S, const int64_t* gws, int64_t* vals, int64_t* minrt,
+                               hipStream_t s) {
+    hipLaunchKernelGGL(k_en_pack_vals, dim3(1), dim3(128), 0, s, en, S, gws, vals, minrt);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ snapshot
 // one thread per resource; pass 0 counts rows, pass 1 (after an exclusive scan) writes them
 __device__ __forceinline__ bool snap_row(const Bucket& b, int64_t now, int64_t last, int64_t cur_sec, sf_metric_row* r) {

@@ -146,6 +146,9 @@ hipError_t launch_entry_node(const DevState& st, const DevBatch& b, const uint8_
                              EntryAcc* acc, hipStream_t s);
 hipError_t launch_entry_init(EntryNode* en, int64_t max_rt, hipStream_t s);
 hipError_t rocprim_scan_bytes(uint32_t n, size_t* bytes);
+hipError_t launch_en_pack_ws(const EntryNode* en, int S, int64_t* ws, hipStream_t s);
+hipError_t launch_en_pack_vals(const EntryNode* en, int S, const int64_t* gws, int64_t* vals, int64_t* minrt,
+                               hipStream_t s);
 hipError_t launch_snapshot(const DevState& st, int64_t now, uint32_t shard_count, uint32_t shard_index,
                            uint32_t* counts, uint32_t* offsets, sf_metric_row* out, uint32_t cap, uint32_t* total,
                            void* scan_tmp, size_t scan_bytes, hipStream_t s);

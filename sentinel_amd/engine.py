@@ -66,6 +66,9 @@ def _declare(L):
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
     f("sf_request_tokens", I, P, C.POINTER(abi.sf_token_batch), C.POINTER(abi.sf_token_results))
     f("sf_cluster_sum", I, P, C.c_int64, I, C.c_int64, C.POINTER(C.c_int64))
+    f("sf_comm_unique_id", I, C.c_char_p, C.c_size_t)
+    f("sf_comm_init", I, P, I, I, C.c_char_p, C.c_size_t)
+    f("sf_entry_node_allreduce", I, P, C.POINTER(abi.sf_node_state))
     f("sf_read_node", I, P, U32, C.POINTER(abi.sf_node_state))
     f("sf_read_entry_node", I, P, C.POINTER(abi.sf_node_state))
     f("sf_read_rule_state", I, P, U32, C.POINTER(abi.sf_rule_state))
@@ -77,6 +80,13 @@ def _declare(L):
     f("sf_get_stats", I, P, C.POINTER(abi.sf_stats))
     f("sf_set_timing", I, P, I)
     f("sf_heavy_profile_read", I, P, C.POINTER(abi.sf_heavy_profile), U32, C.POINTER(U32))
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (rank 0), to be distributed to every rank."""
+    buf = C.create_string_buffer(128)
+    _check(lib().sf_comm_unique_id(buf, 128))
+    return buf.raw
 
 
 def _check(rc):
@@ -217,6 +227,16 @@ class FlowEngine:
     def read_entry_node(self) -> abi.sf_node_state:
         st = abi.sf_node_state()
         _check(lib().sf_read_entry_node(self.h, C.byref(st)))
+        return st
+
+    def comm_init(self, nranks: int, rank: int, unique_id: bytes):
+        """Join the node's RCCL communicator (one engine per GPU)."""
+        _check(lib().sf_comm_init(self.h, nranks, rank, unique_id, len(unique_id)))
+
+    def entry_node_allreduce(self) -> abi.sf_node_state:
+        """Node-wide ENTRY_NODE merged over all ranks with RCCL (exact; see sentinel_amd/dist.py)."""
+        st = abi.sf_node_state()
+        _check(lib().sf_entry_node_allreduce(self.h, C.byref(st)))
         return st
 
     def snapshot(self, now, cap=1 << 20):

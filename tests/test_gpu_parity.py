@@ -124,3 +124,16 @@ def test_entry_node_and_snapshot(eng_mod, so):
         got, want = parity.metric_rows(e.snapshot(now)), parity.metric_rows(o.snapshot(now))
         assert got == want, f"snapshot after batch {k}: {len(got)} vs {len(want)} rows"
     parity.compare_nodes(e, o, w["nodes"])
+
+
+def test_entry_node_rccl_single_rank(eng_mod, so):
+    """The RCCL node-wide merge on a one-rank communicator is the identity."""
+    w = workloads.config3(R=2000, n=60_000, seed=29, split=2)
+    e = eng_mod.FlowEngine(w["cfg"])
+    e.load_flow_rules(w["flow"])
+    for b in w["batches"]:
+        e.submit(b)
+    e.comm_init(1, 0, eng_mod.comm_unique_id())
+    got = abi.node_state_to_dict(e.entry_node_allreduce())
+    want = abi.node_state_to_dict(e.read_entry_node())
+    assert got == want
