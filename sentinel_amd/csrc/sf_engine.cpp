@@ -426,7 +426,7 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         hipEventElapsedTime(&cl, e->ev[10], e->ev[2]);
         hipEventElapsedTime(&li, e->ev[5], e->ev[9]);
         hipEventElapsedTime(&hd, e->ev[5], e->ev[7]);
-        hipEventElapsedTime(&hf, e->ev[13], e->ev[8]);
+        hipEventElapsedTime(&hf, e->ev[7], e->ev[8]);
         hipEventElapsedTime(&hs, e->ev[11], e->ev[12]);
         e->stats.classify_ms += cl; e->stats.light_ms += li;
         e->stats.heavy_decide_ms += hd; e->stats.heavy_fill_ms += hf; e->stats.stream_ms += hs;

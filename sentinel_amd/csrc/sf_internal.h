@@ -159,7 +159,7 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
 constexpr size_t ACC_BYTES = 72;                         // sizeof(Acc)
 // pipeline events: 0 start, 1 segments, 2 classified, 3 joined, 4 scattered,
 // 5 fork, 6 join (stream B), 7 heavy decided, 8 heavy filled, 9 light decided, 10 before classify,
-// 11 stream start (stream C), 12 stream done (stream C), 13 fill start (stream B, after the join with C)
+// 11 stream start (stream C), 12 stream done (stream C), 13 stream fill + apply done (stream C)
 constexpr int SF_NUM_EVENTS = 14;
 
 }  // namespace sf

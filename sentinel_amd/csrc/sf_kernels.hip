@@ -267,8 +267,9 @@ __device__ void wave_flush(PAcc& p, uint32_t key, Acc* table) {
 }
 
 constexpr int FILL_ITERS = 16;
+// cls 0: segments of k_heavy_decide (QPS / WarmUp / no rule); cls 1: of k_heavy_stream (THREAD / RL)
 __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, HeavyCtx hc, const uint32_t* head,
-                                                    const uint32_t* head_scan) {
+                                                    const uint32_t* head_scan, int cls) {
     const uint32_t NONE = 0xffffffffu;
     const uint32_t base = blockIdx.x * (256 * FILL_ITERS);
     PAcc ph, ps; ph.clear(); ps.clear();
@@ -279,6 +280,7 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
         const uint32_t s = head_scan[j] + head[j] - 1;
         const uint8_t mode = hc.seg_mode[s];
         if (mode < SM_QPS) continue;
+        if ((int)(mode == SM_THREAD || mode == SM_RL) != cls) continue;
         const uint32_t lo = hc.seg_start[s];
         if (io.eref && !is_entry(io.flags[j])) {
             int64_t r = io.eref[j];
@@ -301,11 +303,10 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
 }
 
 __global__ void k_heavy_apply(DevState st, HeavyCtx hc, StreamCtx sc, const uint32_t* seg_nhw,
-                              const uint32_t* seg_nsec) {
+                              const uint32_t* seg_nsec, int cls) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, s;
-    const uint32_t nh = hc.n_heavy[0] + hc.n_heavy[3];
-    if (t < nh) { if (!heavy_at(hc, t, &s)) return; }
-    else if (!stream_at(sc, t - nh, &s)) return;
+    if (cls == 0) { if (!heavy_at(hc, t, &s)) return; }
+    else if (!stream_at(sc, t, &s)) return;
     if (hc.seg_mode[s] < SM_QPS) return;
     heavy_apply(st, hc, s, hc.seg_res[s], seg_nhw[s], seg_nsec[s]);
 }
@@ -405,12 +406,15 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     else
         hipLaunchKernelGGL(k_heavy_decide<SF_MAX_SAMPLE_COUNT>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     if (timing) hipEventRecord(ev[7], s2);
-    hipStreamWaitEvent(s2, ev[12], 0);             // k_heavy_fill reads the stream kernel's items and pass bits
-    if (timing) hipEventRecord(ev[13], s2);
+    // verdicts + window deltas of each heavy class as soon as its decisions are done
     hipLaunchKernelGGL(k_heavy_fill, dim3(blocks(n, 256 * FILL_ITERS)), dim3(256), 0, s2, st, io, hc, w.head,
-                       w.head_scan);
+                       w.head_scan, 0);
     if (timing) hipEventRecord(ev[8], s2);
-    hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, sc, w.seg_nhw, w.seg_nsec);
+    hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, sc, w.seg_nhw, w.seg_nsec, 0);
+    hipLaunchKernelGGL(k_heavy_fill, dim3(blocks(n, 256 * FILL_ITERS)), dim3(256), 0, s3, st, io, hc, w.head,
+                       w.head_scan, 1);
+    hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s3, st, hc, sc, w.seg_nhw, w.seg_nsec, 1);
+    hipEventRecord(ev[13], s3);
 
     const unsigned TD = 128;
     if (st.S <= 2)
@@ -420,8 +424,9 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
         hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s, st, io,
                            w.seg_start, w.seg_res, w.light_list, w.counters);
     if (timing) hipEventRecord(ev[9], s);
-    hipEventRecord(ev[6], s2);                     // join
+    hipEventRecord(ev[6], s2);                     // join B and C
     hipStreamWaitEvent(s, ev[6], 0);
+    hipStreamWaitEvent(s, ev[13], 0);
     if (timing) hipEventRecord(ev[3], s);
     hipLaunchKernelGGL(k_scatter, dim3(blocks(n, T)), dim3(T), 0, s, w.perm, n, w.v_status, w.v_wait,
                        w.v_rule, out);

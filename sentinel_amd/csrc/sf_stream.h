@@ -94,11 +94,12 @@ __device__ __forceinline__ void thr_store(const ThrRegs& r, uint32_t* buf) {
 // before the current.  0 when not needed.
 __device__ __forceinline__ unsigned long long thr_ring_word(const unsigned long long* ring, uint32_t code, int lane,
                                                             uint32_t q, uint32_t lo) {
-    if (!(code & CODE_EXIT)) return 0;
+    // branch-free: always one LDS read (clamped address), the word kept only when needed
     const uint32_t d = code & ~CODE_EXIT;
-    if (d == 0 || d == CODE_DEAD || d <= (uint32_t)lane + 64 || d >= RING_BITS - 64) return 0;
-    const uint32_t b = (q + (uint32_t)lane - d - lo) % RING_BITS;
-    return ring[b >> 6];
+    const bool need = (code & CODE_EXIT) && d != 0 && d != CODE_DEAD && d > (uint32_t)lane + 64 && d < RING_BITS - 64;
+    const uint32_t b = (q + (uint32_t)lane - (need ? d : 0u) - lo) % RING_BITS;
+    const unsigned long long wd = ring[b >> 6];
+    return need ? wd : 0ull;
 }
 
 __device__ __forceinline__ int64_t uniform64(int64_t v) {
@@ -147,17 +148,21 @@ __device__ __forceinline__ void thr_decide_chunk(const uint32_t* buf, unsigned l
         const bool ent = valid && !(code & CODE_EXIT);
         const uint32_t d = code & ~CODE_EXIT;
         const int32_t c = (int32_t)code;
-        bool inwin = false, live = false;
-        if (ex && d != CODE_DEAD) {
-            if (d == 0) live = true;                                     // entry of an earlier batch
-            else if (d <= (uint32_t)lane) inwin = true;                  // entry in this window
-            else if (d <= (uint32_t)lane + 64) live = (prev >> ((uint32_t)(lane - (int)d) & 63u)) & 1ull;
-            else if (d < RING_BITS - 64) live = (rw_c >> ((uint32_t)(lane - (int)d) & 63u)) & 1ull;
-            else {
-                // older than the ring: this wave's own bits, back from L2
+        // exit liveness without branches: entry of an earlier batch (d == 0), this
+        // window (in-window: decided below), the previous window, the LDS ring
+        const bool exr = ex && d != CODE_DEAD && d != 0;
+        const uint32_t sh = (uint32_t)(lane - (int)d) & 63u;
+        const bool inwin = exr && d <= (uint32_t)lane;
+        const bool in_prev = exr && d > (uint32_t)lane && d <= (uint32_t)lane + 64;
+        const bool in_ring = exr && d > (uint32_t)lane + 64 && d < RING_BITS - 64;
+        bool live = (ex && d == 0) || (in_prev && ((prev >> sh) & 1ull)) || (in_ring && ((rw_c >> sh) & 1ull));
+        const bool in_hbm = exr && d >= RING_BITS - 64;
+        if (__builtin_expect(__ballot(in_hbm) != 0, 0)) {
+            // older than the ring: this wave's own bits, back from L2
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __builtin_amdgcn_s_waitcnt(0);
+            if (in_hbm) {
                 const uint32_t r = q + (uint32_t)lane - d;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                __builtin_amdgcn_s_waitcnt(0);
                 const unsigned long long wd =
                     __hip_atomic_load(pbits + (r >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 live = (wd >> (r & 63)) & 1ull;
@@ -334,14 +339,35 @@ __global__ void __launch_bounds__(HS_T) k_heavy_stream(DevState st, SegIO io, He
         thr_load(r, io, lo, lo, hi);
         thr_store(r, codes);
         __syncthreads();
+#ifdef SF_STREAM_PROF
+        uint64_t t_dec = 0, t_wait = 0, t_ld = 0;
+#endif
         for (uint32_t k = 0; k < nch; k++) {
             const uint32_t q0 = lo + k * HS_CH;
             const bool more = k + 1 < nch;
+#ifdef SF_STREAM_PROF
+            const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
             if (more) thr_load(r, io, q0 + HS_CH, lo, hi);
+#ifdef SF_STREAM_PROF
+            const uint64_t c1 = __builtin_amdgcn_s_memtime();
+#endif
             if (wave0) thr_decide_chunk(codes + (k & 1) * HS_CH, ring, q0, lo, hi, M, IM, T, prev, hc.passbits);
+#ifdef SF_STREAM_PROF
+            const uint64_t c2 = __builtin_amdgcn_s_memtime();
+#endif
             if (more) thr_store(r, codes + ((k + 1) & 1) * HS_CH);
             __syncthreads();
+#ifdef SF_STREAM_PROF
+            const uint64_t c3 = __builtin_amdgcn_s_memtime();
+            t_ld += c1 - c0; t_dec += c2 - c1; t_wait += c3 - c2;
+#endif
         }
+#ifdef SF_STREAM_PROF
+        if (threadIdx.x == 0)
+            printf("SF_STREAM_PROF seg %u events %u chunks %u: issue %lu decide %lu store+barrier %lu cycles\n", s,
+                   hi - lo, nch, (unsigned long)t_ld, (unsigned long)t_dec, (unsigned long)t_wait);
+#endif
     } else {                                                     // SM_RL
         int64_t* tsb = (int64_t*)smem;                           // [2][HS_CH]
         int32_t* cb = (int32_t*)(smem + 2 * HS_CH);              // [2][HS_CH]

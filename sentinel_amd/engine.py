@@ -19,7 +19,8 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsentinel_flow.so")
+# SENTINEL_FLOW_LIB selects a diagnostics build (e.g. libsentinel_flow_prof.so); default: the product library
+LIB_PATH = os.environ.get("SENTINEL_FLOW_LIB") or os.path.join(_HERE, "libsentinel_flow.so")
 
 
 class EngineError(RuntimeError):

@@ -1,0 +1,99 @@
+"""Committed golden vectors (tests/golden/, written by make_golden.py): the
+oracle must keep reproducing them (CPU), and the HIP engine must match them
+bit for bit (GPU).  Inputs and outputs only; no reference source."""
+import os
+
+import numpy as np
+import pytest
+
+from sentinel_amd import abi
+from tests import parity
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FLOW_CASES = ["flowqps_demo", "mixed_1k", "param_40", "param_mixed"]
+
+
+def _struct(cls, arr):
+    return cls.from_buffer_copy(arr.tobytes())
+
+
+def _rules(cls, arr):
+    n = arr.size // C_sizeof(cls)
+    return [cls.from_buffer_copy(arr[i * C_sizeof(cls):(i + 1) * C_sizeof(cls)].tobytes()) for i in range(n)]
+
+
+def C_sizeof(cls):
+    import ctypes
+    return ctypes.sizeof(cls)
+
+
+def load_flow_case(name):
+    z = np.load(os.path.join(HERE, f"{name}.npz"))
+    case = {"cfg": _struct(abi.sf_config, z["cfg"]), "flow": _rules(abi.sf_flow_rule, z["flow"]),
+            "param": _rules(abi.sf_param_rule, z["param"]), "items": _rules(abi.sf_hot_item, z["items"]),
+            "batches": [], "want": [], "nodes": z["nodes"], "node_states": z["node_states"],
+            "entry_node": z["entry_node"]}
+    for k in range(int(z["n_batches"])):
+        g = lambda key: z[f"b{k}_{key}"] if f"b{k}_{key}" in z else None  # noqa: E731
+        case["batches"].append(abi.HostBatch(g("res"), g("ts"), g("cnt"), g("flags"), entry_ref=g("eref"),
+                                             create_ts=g("cts"), arg_tag=g("atag"), arg_bits=g("abits"),
+                                             n_args=g("nargs")))
+        v = abi.HostVerdicts(g("res").size)
+        v.status, v.wait_ms, v.rule_idx = g("status"), g("wait"), g("rule")
+        case["want"].append(v)
+    return case
+
+
+def check_flow_case(make_engine, name, entry_node=True):
+    c = load_flow_case(name)
+    e = make_engine(c["cfg"])
+    if c["flow"]:
+        e.load_flow_rules(c["flow"])
+    if c["param"]:
+        e.load_param_rules(c["param"], c["items"])
+    for k, (b, want) in enumerate(zip(c["batches"], c["want"])):
+        parity.compare_verdicts(e.submit(b), want, f"{name} batch {k}")
+    for r, st in zip(c["nodes"], c["node_states"]):
+        got = abi.node_state_to_dict(e.read_node(int(r)), c["cfg"].sample_count)
+        want = abi.node_state_to_dict(_struct(abi.sf_node_state, st), c["cfg"].sample_count)
+        assert got == want, f"{name}: node {r} differs"
+    if entry_node:
+        got = abi.node_state_to_dict(e.read_entry_node(), c["cfg"].sample_count)
+        want = abi.node_state_to_dict(_struct(abi.sf_node_state, c["entry_node"]), c["cfg"].sample_count)
+        assert got == want, f"{name}: ENTRY_NODE differs"
+
+
+def check_token_case(make_engine, name="token_5k"):
+    z = np.load(os.path.join(HERE, f"{name}.npz"))
+    e = make_engine(_struct(abi.sf_config, z["cfg"]))
+    e.load_namespaces(_rules(abi.sf_namespace, z["ns"]))
+    flow = _rules(abi.sf_cluster_flow_rule, z["cflow"])
+    e.load_cluster_rules(flow, _rules(abi.sf_cluster_param_rule, z["cparam"]), _rules(abi.sf_hot_item, z["citems"]))
+    b = abi.HostTokenBatch(z["flow_id"], z["count"], z["flags"], z["ts"], param_tag=z["ptag"], param_bits=z["pbits"])
+    r = e.request_tokens(b)
+    assert (r.status == z["status"]).all() and (r.remaining == z["remaining"]).all() and (r.wait_ms == z["wait"]).all()
+    now = int(z["ts"][-1])
+    sums = np.array([[e.cluster_sum(f.flow_id, ev, now) for ev in range(7)] for f in flow], np.int64)
+    assert (sums == z["sums"]).all()
+
+
+@pytest.mark.parametrize("name", FLOW_CASES)
+def test_oracle_reproduces_golden(so, name):
+    check_flow_case(so.OracleEngine, name)
+
+
+def test_oracle_reproduces_golden_tokens(so):
+    check_token_case(so.OracleEngine)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FLOW_CASES)
+def test_engine_matches_golden(name):
+    from sentinel_amd import engine
+    check_flow_case(engine.FlowEngine, name)
+
+
+@pytest.mark.gpu
+def test_engine_matches_golden_tokens():
+    from sentinel_amd import engine
+    check_token_case(engine.FlowEngine)
