@@ -119,7 +119,8 @@ void sf_destroy(sf_engine* e) {
                     e->w.segflag, e->w.seg_mode, e->w.light_list, e->w.heavy_list, e->w.counters, e->w.pcg,
                     e->w.pscan_tmp, e->w.item_lo, e->w.item_hi, e->w.item_wait, e->w.n_items, e->w.acc_hw,
                     e->w.acc_sec, e->w.acc_hw_base, e->w.acc_sec_base, e->w.seg_hw0, e->w.seg_sec0,
-                    e->w.seg_nhw, e->w.seg_nsec, e->w.hticks, e->w.passbits, e->w.stream_list, e->w.sticks};
+                    e->w.seg_nhw, e->w.seg_nsec, e->w.hticks, e->w.passbits, e->w.stream_list, e->w.sticks,
+                    e->w.exit_of, e->w.lxfar};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
@@ -224,6 +225,8 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     DALLOC(w.sticks, (N / (w.heavy_min + 1) + 2) * 8);
     DALLOC(w.stream_list, SC * 4);
     DALLOC(w.passbits, (N / 64 + 2) * 8);
+    DALLOC(w.exit_of, N * 4);
+    DALLOC(w.lxfar, (N / 64 + 2) * 8);
     HIP_TRY(hipStreamSynchronize(e->stream));
     *out = e;
     return SF_OK;

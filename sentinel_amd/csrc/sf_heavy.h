@@ -69,6 +69,8 @@ struct HeavyCtx {
     const int64_t* seg_hw0; const int64_t* seg_sec0;    // first window index of the segment
     uint64_t* hticks;                                   // per heavy-list entry, or null
     unsigned long long* passbits;                       // [n/64+2] bit j: entry j passed (SM_THREAD)
+    const uint32_t* exit_of;                            // [n] sorted index of an entry's exit (or ~0)
+    unsigned long long* lxfar;                          // [n/64+2] live exits beyond the LDS ring (SM_THREAD)
 };
 
 SF_HD bool pass_bit(const unsigned long long* pb, uint32_t j) { return (pb[j >> 6] >> (j & 63)) & 1ull; }

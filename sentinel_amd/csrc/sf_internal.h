@@ -127,6 +127,8 @@ struct Work {
     uint32_t* stream_list;                              // THREAD / RL heavy segments (k_heavy_stream)
     uint64_t* sticks;                                   // [max heavy] k_heavy_stream clock per segment (timing)
     unsigned long long* passbits;                       // [n/64+2] pass bit per sorted event (SM_THREAD)
+    uint32_t* exit_of;                                  // [n] sorted index of each entry's exit, ~0 if none
+    unsigned long long* lxfar;                          // [n/64+2] far live exits (SM_THREAD)
 };
 
 // Device view of a caller batch (pointers already on device).

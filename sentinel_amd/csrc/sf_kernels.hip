@@ -82,14 +82,16 @@ __global__ void k_gather(DevBatch b, const uint32_t* perm, int64_t* s_ts, int32_
 }
 
 __global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint32_t* inv, int64_t* s_eref,
-                              int64_t* s_cts, int32_t* err) {
+                              int64_t* s_cts, uint32_t* exit_of, int32_t* err) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
     uint32_t i = perm[j];
     int64_t r = b.eref[i];
     if (r >= (int64_t)b.n) { *err = SF_ERR_INVALID; r = -1; }
-    s_eref[j] = (r >= 0) ? (int64_t)inv[r] : -1;
+    const int64_t rs = (r >= 0) ? (int64_t)inv[r] : -1;
+    s_eref[j] = rs;
     s_cts[j] = b.cts ? b.cts[i] : 0;
+    if (rs >= 0 && (b.flags[i] & SF_EV_EXIT)) exit_of[rs] = j;   // forward map (THREAD-grade liveness)
 }
 
 struct EntryCount {     // acquireCount of entries, 0 for exits (input of the pc scan)
@@ -191,6 +193,8 @@ static HeavyCtx heavy_ctx(const Work& w) {
     hc.seg_hw0 = w.seg_hw0; hc.seg_sec0 = w.seg_sec0;
     hc.hticks = nullptr;
     hc.passbits = w.passbits;
+    hc.exit_of = w.exit_of;
+    hc.lxfar = w.lxfar;
     return hc;
 }
 
@@ -370,9 +374,10 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     if (timing) hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_gather, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_ts, w.s_cnt, w.s_flags,
                        b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag);
+    hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.inv, w.s_eref,
-                           w.s_cts, st.err);
+                           w.s_cts, w.exit_of, st.err);
     PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
     e = rocprim::inclusive_scan(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n, rocprim::plus<int64_t>(), s);
     if (e != hipSuccess) return e;
@@ -397,6 +402,7 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     hipStreamWaitEvent(s3, ev[5], 0);
     const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
     hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s3);
+    hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s3);
     hipEventRecord(ev[11], s3);
     StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, timing ? w.sticks : nullptr};
     hipLaunchKernelGGL(k_heavy_stream, dim3(max_heavy), dim3(HS_T), 0, s3, st, io, hc, sc);

@@ -47,200 +47,230 @@ __device__ __forceinline__ bool stream_at(const StreamCtx& sc, uint32_t b, uint3
 }
 
 // ------------------------------------------------------------------ THREAD
-struct ThrRegs { uint32_t code[HS_PL]; };
+// DefaultController, FLOW_GRADE_THREAD (DefaultController.java:50-89,
+// StatisticSlot.java:64-65,157): an entry passes iff (int)(curThreadNum +
+// acquireCount) <= count; a pass adds one thread, the exit of a passed entry
+// removes one.  An exit's liveness is settled when its entry passes: the pass
+// sets the exit's bit in a live-exit bitmap, an LDS ring over the next
+// LX_WORDS * 64 events (farther exits go to a bitmap in HBM that the chunk
+// loader folds back in).  Exits of entries of earlier batches are always live
+// and enter the ring when their chunk is prepared.
+//
+// Waves 1-3 prepare chunk k+1 (THR_WPC windows of 64 events) while wave 0
+// decides chunk k.  Per window they precompute the entry mask, cumulative
+// masks of entries with acquireCount <= m (m = 1..7), the in-window exits of
+// the window's own entries, max over entries of (rank + acquireCount), and
+// every entry's exit position (exit_of, written by k_gather_exit).  Wave 0
+// then needs one LDS word of live exits per window:
+//   - no room even with every live exit first: every entry blocks;
+//   - every entry fits even at T + rank: all pass, their exits marked live;
+//   - else a scalar walk over the events that change the thread count (the
+//     next live exit, or the next entry that fits at the current room).
+// Work is proportional to windows plus passes, not to events.
+constexpr uint32_t LX_WORDS = 2048;               // live-exit ring: 128 Ki events ahead (16 KiB)
+constexpr int THR_WPC = 24;                       // windows per chunk (8 per helper wave)
+constexpr uint32_t THR_CH = THR_WPC * 64;          // events per chunk
+constexpr uint32_t XO_NONE = 0xffffffffu;
+constexpr int32_t THR_CSMALL = 8;                  // scalar walk for acquireCount <= 8
+constexpr int32_t THR_CBIG = 1 << 20;              // integer compares exact below this (no int wrap)
 
-__device__ __forceinline__ void thr_load(ThrRegs& r, const SegIO& io, uint32_t q0, uint32_t lo, uint32_t hi) {
-    // every load of the chunk issued before any is used (one memory round trip):
-    // indices are clamped into the segment instead of branching around loads
-    uint8_t f[HS_PL]; int32_t cn[HS_PL]; int64_t rf[HS_PL];
-#pragma unroll
-    for (int i = 0; i < HS_PL; i++) {
-        const uint32_t j = min(q0 + (uint32_t)(i * HS_T) + threadIdx.x, hi - 1);
-        f[i] = io.flags[j];
-        cn[i] = io.cnt[j];
-    }
-    if (io.eref) {
-#pragma unroll
-        for (int i = 0; i < HS_PL; i++) rf[i] = io.eref[min(q0 + (uint32_t)(i * HS_T) + threadIdx.x, hi - 1)];
-    } else {
-#pragma unroll
-        for (int i = 0; i < HS_PL; i++) rf[i] = -1;
-    }
-#pragma unroll
-    for (int i = 0; i < HS_PL; i++) {
-        const uint32_t j = q0 + (uint32_t)(i * HS_T) + threadIdx.x;
-        uint32_t c = 0;
-        if (f[i] & SF_EV_EXIT) {
-            const int64_t ref = rf[i];
-            uint32_t d;
-            if (ref < 0) d = 0;                                                  // entry of an earlier batch: live
-            else if (ref < (int64_t)lo || ref >= (int64_t)j) d = CODE_DEAD;     // bad ref (k_heavy_fill flags it)
-            else d = (uint32_t)((int64_t)j - ref);
-            c = CODE_EXIT | d;
-        } else {
-            c = (uint32_t)cn[i];                                                 // >= 1 (heavy_mode)
-        }
-        r.code[i] = j < hi ? c : 0u;
-    }
-}
-__device__ __forceinline__ void thr_store(const ThrRegs& r, uint32_t* buf) {
-#pragma unroll
-    for (int i = 0; i < HS_PL; i++) buf[i * HS_T + threadIdx.x] = r.code[i];
-}
+struct ThrWin {                                    // 24 B per window
+    unsigned long long ent;                        // entries
+    unsigned long long inw;                        // exits whose entry is in this window
+    int32_t maxrc;                                 // bound of max over entries of rank + acquireCount
+    uint32_t flags;                                // bit 0: an acquireCount > 8, bit 1: > THR_CBIG
+};
 
-// Ring word a lane needs for its exit when the exit's entry lies two or more
-// windows back (windows are 64-event blocks counted from the segment start
-// lo): read ahead of time, since the ring holds every window up to the one
-// before the current.  0 when not needed.
-__device__ __forceinline__ unsigned long long thr_ring_word(const unsigned long long* ring, uint32_t code, int lane,
-                                                            uint32_t q, uint32_t lo) {
-    // branch-free: always one LDS read (clamped address), the word kept only when needed
-    const uint32_t d = code & ~CODE_EXIT;
-    const bool need = (code & CODE_EXIT) && d != 0 && d != CODE_DEAD && d > (uint32_t)lane + 64 && d < RING_BITS - 64;
-    const uint32_t b = (q + (uint32_t)lane - (need ? d : 0u) - lo) % RING_BITS;
-    const unsigned long long wd = ring[b >> 6];
-    return need ? wd : 0ull;
-}
+struct ThrLds {
+    unsigned long long lx[LX_WORDS];               // live exits of window (pos - lo) / 64 at word % LX_WORDS
+    ThrWin win[2][THR_WPC];
+    uint32_t xo[2][THR_CH];                        // exit position (sorted index) of each entry, or XO_NONE
+    int32_t cn[2][THR_CH];                         // acquireCount (exact path)
+};
+static_assert(sizeof(ThrLds) <= HS_LDS_WORDS * 8, "THREAD LDS layout exceeds the stream kernel's LDS");
 
 __device__ __forceinline__ int64_t uniform64(int64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-__device__ __forceinline__ unsigned long long lane_mask64(const uint32_t vlo, const uint32_t vhi, int lane) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)vlo, lane);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)vhi, lane);
-    return ((unsigned long long)hi << 32) | lo;
+__device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
+    return (unsigned long long)uniform64((int64_t)v);
 }
 
-// Wave 0: decide the 64-event windows of one chunk.  T = curThreadNum
-// (wave-uniform, kept in SGPRs); prev = pass mask of the window before.
-// Software-pipelined: the code of window w+2 and the ring words of window
-// w+1 are read from LDS while window w is decided; liveness of an exit whose
-// entry is in window w-1 comes from `prev`, in window w from the mask being
-// built, further back from the ring, beyond the ring from the pass bits in HBM.
-//
-// Per window: all-block and all-pass are decided from a few ballots.  Else a
-// scalar walk visits only the events that change the thread count; the
-// entries that fit at a given room IM - T are precomputed as cumulative
-// ballots by acquireCount (lane m of cum holds the mask of entries with c <= m).
-constexpr int32_t THR_CSMALL = 8;            // scalar walk for acquireCount <= 8
-constexpr int32_t THR_CBIG = 1 << 20;        // integer compares exact below this (no int wrap)
-
-__device__ __forceinline__ void thr_decide_chunk(const uint32_t* buf, unsigned long long* ring, uint32_t q0,
-                                                 uint32_t lo, uint32_t hi, double M, int64_t IM, int64_t& T,
-                                                 unsigned long long& prev, unsigned long long* pbits) {
+// Helper wave h (1..3): prepare windows h-1, h+2, ... of the chunk starting at q0.
+// Every load of the wave's windows is issued before any is used (one memory
+// round trip per chunk; indices clamped into the segment instead of branches).
+constexpr int THR_WPW = THR_WPC / 3;              // windows per helper wave
+__device__ void thr_prepare(ThrLds& L, int buf, const SegIO& io, const uint32_t* exit_of,
+                            const unsigned long long* lxfar, uint32_t q0, uint32_t lo, uint32_t hi, int h) {
     const int lane = (int)(threadIdx.x & 63);
-    const uint32_t nwin = (min(hi - q0, (uint32_t)HS_CH) + 63) / 64;
-    uint32_t code_c = buf[lane];
-    uint32_t code_n = nwin > 1 ? buf[64 + lane] : 0u;
-    unsigned long long rw_c = thr_ring_word(ring, code_c, lane, q0, lo);
-    T = uniform64(T);
-    for (uint32_t w = 0; w < nwin; w++) {
-        const uint32_t q = q0 + 64 * w;
-        // read ahead (LDS ops of one wave complete in order)
-        const uint32_t code_nn = w + 2 < nwin ? buf[64 * (w + 2) + lane] : 0u;
-        const unsigned long long rw_n = w + 1 < nwin ? thr_ring_word(ring, code_n, lane, q + 64, lo) : 0ull;
-
-        const uint32_t code = code_c;
-        const bool valid = q + (uint32_t)lane < hi;
-        const bool ex = valid && (code & CODE_EXIT);
-        const bool ent = valid && !(code & CODE_EXIT);
-        const uint32_t d = code & ~CODE_EXIT;
-        const int32_t c = (int32_t)code;
-        // exit liveness without branches: entry of an earlier batch (d == 0), this
-        // window (in-window: decided below), the previous window, the LDS ring
-        const bool exr = ex && d != CODE_DEAD && d != 0;
-        const uint32_t sh = (uint32_t)(lane - (int)d) & 63u;
-        const bool inwin = exr && d <= (uint32_t)lane;
-        const bool in_prev = exr && d > (uint32_t)lane && d <= (uint32_t)lane + 64;
-        const bool in_ring = exr && d > (uint32_t)lane + 64 && d < RING_BITS - 64;
-        bool live = (ex && d == 0) || (in_prev && ((prev >> sh) & 1ull)) || (in_ring && ((rw_c >> sh) & 1ull));
-        const bool in_hbm = exr && d >= RING_BITS - 64;
-        if (__builtin_expect(__ballot(in_hbm) != 0, 0)) {
-            // older than the ring: this wave's own bits, back from L2
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-            __builtin_amdgcn_s_waitcnt(0);
-            if (in_hbm) {
-                const uint32_t r = q + (uint32_t)lane - d;
-                const unsigned long long wd =
-                    __hip_atomic_load(pbits + (r >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                live = (wd >> (r & 63)) & 1ull;
-            }
-        }
-        const unsigned long long m_ent = __ballot(ent);
-        unsigned long long m_live = __ballot(live);
-        const unsigned long long m_inwin = __ballot(inwin);
-        const int n_live = (int)__popcll(m_live);
-        const int n_ent = (int)__popcll(m_ent);
-        unsigned long long pmask = 0;
-        const int64_t room0 = IM - T;
-        // integer compares are exact while (int)(T + c) of the reference cannot wrap
-        const bool small_t = T >= (int64_t)INT32_MIN + 64 && T + (int64_t)THR_CBIG + 64 <= (int64_t)INT32_MAX;
-        const bool nowrap = small_t && !__ballot(ent && c > THR_CBIG);
-        if (n_ent == 0) {
-            T -= n_live;
-        } else if (nowrap && room0 + n_live < 1) {
-            // even with every earlier-window live exit first, no entry fits (c >= 1);
-            // then this window's own entries all block and their exits are dead
-            T -= n_live;
-        } else if (nowrap && !__ballot(ent && (int64_t)c + (int64_t)__builtin_amdgcn_mbcnt_hi(
-                                                  (uint32_t)(m_ent >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m_ent, 0u))
-                                                  > room0)) {
-            // the thread count before an entry is <= T + (entries before it in the
-            // window): every entry fits
-            pmask = m_ent;
-            T += (int64_t)n_ent - (int64_t)n_live - (int64_t)__popcll(m_inwin);
-        } else if (nowrap && !__ballot(ent && c > THR_CSMALL)) {
-            // scalar walk over the events that change the thread count
-            uint32_t cum_lo = 0, cum_hi = 0;                 // lane m: entries with c <= m
+    uint8_t fa[THR_WPW]; int32_t ca[THR_WPW]; int64_t ra[THR_WPW]; uint32_t xa[THR_WPW];
+    unsigned long long f0a[THR_WPW], f1a[THR_WPW];
 #pragma unroll
-            for (int m = 1; m < THR_CSMALL; m++) {
-                const unsigned long long mm = __ballot(ent && c <= m);
-                if (lane == m) { cum_lo = (uint32_t)mm; cum_hi = (uint32_t)(mm >> 32); }
-            }
+    for (int k = 0; k < THR_WPW; k++) {
+        const uint32_t q = q0 + 64u * (uint32_t)(h - 1 + 3 * k);
+        const uint32_t jc = min(q + (uint32_t)lane, hi - 1);
+        fa[k] = io.flags[jc];
+        ca[k] = io.cnt[jc];
+        ra[k] = io.eref ? io.eref[jc] : -1;
+        xa[k] = exit_of[jc];
+        const uint32_t g = min(q, hi - 1) >> 6;
+        f0a[k] = __hip_atomic_load(lxfar + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        f1a[k] = __hip_atomic_load(lxfar + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int k = 0; k < THR_WPW; k++) {
+        const int wl = h - 1 + 3 * k;
+        const uint32_t q = q0 + 64u * (uint32_t)wl;
+        if (q >= hi) break;
+        const uint32_t j = q + (uint32_t)lane;
+        const bool valid = j < hi;
+        const uint8_t f = fa[k];
+        const int32_t c = ca[k];
+        const int64_t ref = ra[k];
+        const bool ent = valid && !(f & SF_EV_EXIT);
+        const bool ex = valid && (f & SF_EV_EXIT);
+        ThrWin wn;
+        wn.ent = __ballot(ent);
+        wn.inw = __ballot(ex && ref >= (int64_t)q && ref < (int64_t)j);
+        const bool gt1 = __ballot(ent && c > 1) != 0ull, gt8 = __ballot(ent && c > THR_CSMALL) != 0ull;
+        wn.flags = (gt8 ? 1u : 0u) | (__ballot(ent && c > THR_CBIG) ? 2u : 0u);
+        // bound of max(rank + acquireCount): (entries - 1) + (1, or 8 when some count is 2..8)
+        wn.maxrc = gt8 ? INT32_MAX : (int32_t)__popcll(wn.ent) - 1 + (gt1 ? THR_CSMALL : 1);
+        L.xo[buf][64 * wl + lane] = ent ? xa[k] : XO_NONE;
+        L.cn[buf][64 * wl + lane] = c;
+        const unsigned long long mo = __ballot(ex && ref < 0);        // entry of an earlier batch: live
+        if (lane == 0) {
+            L.win[buf][wl] = wn;
+            // live exits of far-away entries (written into HBM when those entries passed)
+            const uint32_t sh = q & 63;
+            const unsigned long long far = sh ? (f0a[k] >> sh) | (f1a[k] << (64 - sh)) : f0a[k];
+            const unsigned long long add = (mo | far) & (q + 64 <= hi ? ~0ull : ((1ull << (hi - q)) - 1ull));
+            if (add) atomicOr(&L.lx[((q - lo) >> 6) % LX_WORDS], add);
+        }
+    }
+}
+
+// mark the exit at sorted position x live (its entry just passed); q = current window
+__device__ __forceinline__ bool thr_mark_exit(ThrLds& L, unsigned long long* lxfar, uint32_t x, uint32_t q,
+                                              uint32_t lo) {
+    if (x - q < (LX_WORDS - 1) * 64u) { atomicOr(&L.lx[((x - lo) >> 6) % LX_WORDS], 1ull << ((x - lo) & 63)); return false; }
+    atomicOr(lxfar + (x >> 6), 1ull << (x & 63));
+    return true;
+}
+
+// Wave 0: decide the windows of one prepared chunk.  The window summaries of
+// the chunk are read into registers once (lane w <-> window w) and used with
+// readlane.  The live-exit word of a window is read from the LDS ring after
+// the previous window's exits were marked (one LDS op per window, in order).
+// While saturated (no room) a run of windows without live exits blocks
+// entirely: one vector read of their ring words finds the next one.  Inside a
+// window, only events that change the thread count are visited; the exits of
+// the window's passed entries are marked in one vector step after it.
+__device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) {
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((unsigned long long)b << 32) | a;
+}
+
+__device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32_t q0, uint32_t lo, uint32_t hi,
+                           double M, int64_t IM, int64_t& T, unsigned long long* pbits) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t nwin = min((hi - q0 + 63) / 64, (uint32_t)THR_WPC);
+    bool far_marked = false;
+    T = uniform64(T);
+    const int wl = lane < THR_WPC ? lane : 0;
+    const unsigned long long r_ent = L.win[buf][wl].ent;
+    const int32_t r_maxrc = L.win[buf][wl].maxrc;
+    const uint32_t r_flags = L.win[buf][wl].flags;
+    const uint32_t slot0 = (q0 - lo) >> 6;
+    uint32_t w = 0;
+    while (w < nwin) {
+        const uint32_t q = q0 + 64 * w;
+        const uint32_t slot = (slot0 + w) % LX_WORDS;
+        const unsigned long long me = rl64(r_ent, (int)w);
+        const uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)r_flags, (int)w);
+        const int64_t room0 = IM - T;
+        const bool tsmall = T >= (int64_t)INT32_MIN + 64 && T + (int64_t)THR_CBIG + 64 <= (int64_t)INT32_MAX;
+        if (room0 <= 0 && tsmall) {
+            // saturated: skip the windows with no live exit (all their entries block)
+            const uint32_t wn_ = w + (uint32_t)lane;
+            const bool inr = wn_ < nwin;
+            const unsigned long long v = inr ? L.lx[(slot0 + wn_) % LX_WORDS] : 0ull;
+            const uint32_t fl = (uint32_t)__shfl((int)r_flags, inr ? (int)wn_ : 0);
+            const unsigned long long stop = __ballot(inr && (v != 0ull || (fl & 2u)));
+            if (!stop) { w = nwin; break; }
+            const uint32_t k = (uint32_t)(__ffsll((long long)stop) - 1);
+            if (k > 0) { w += k; continue; }
+        }
+        unsigned long long ml = uniform_u64(L.lx[slot]);     // live exits of this window
+        const int32_t maxrc = __builtin_amdgcn_readlane(r_maxrc, (int)w);
+        unsigned long long pmask = 0;
+        const bool nowrap = !(flags & 2u) && tsmall;
+        if (me == 0) {
+            T -= __popcll(ml);
+        } else if (nowrap && room0 + (int64_t)__popcll(ml) < 1) {
+            // even with every live exit first, no entry fits (acquireCount >= 1):
+            // all entries block, so no exit of this window's entries turns live
+            T -= __popcll(ml);
+        } else if (nowrap && room0 >= (int64_t)maxrc) {
+            // the thread count before an entry is <= T + (entries before it): all fit
+            pmask = me;
+            ml |= uniform_u64(L.win[buf][w].inw);        // exits of this window's entries, inside it
+            T += (int64_t)__popcll(me) - (int64_t)__popcll(ml);
+        } else {
+            const uint32_t xo = L.xo[buf][64 * w + lane];
+            const int32_t c = L.cn[buf][64 * w + lane];
+            const bool small = nowrap && !(flags & 1u);
+            // in-window exit of each entry lane: bit position, or 64
+            const uint32_t inpos = (xo != XO_NONE && xo - q < 64u && xo > q + (uint32_t)lane) ? xo - q : 64u;
+            const bool ent = (me >> lane) & 1ull;
             int cursor = 0;
             while (cursor < 64) {
-                const int64_t room = IM - T;
-                const unsigned long long fm = room <= 0 ? 0ull
-                                            : room >= THR_CSMALL ? m_ent
-                                            : lane_mask64(cum_lo, cum_hi, (int)room);
-                const unsigned long long cand = (fm | m_live) & (~0ull << cursor);
+                unsigned long long fm = 0;
+                if (small) {
+                    // without int wrap (int)(T + c) <= count  <=>  c <= floor(count) - T
+                    const int64_t room = IM - T;
+                    if (room >= THR_CSMALL) fm = me;
+                    else if (room > 0) fm = __ballot(ent && (int64_t)c <= room);
+                } else {
+                    fm = __ballot(ent && (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)c) <= M);
+                }
+                const unsigned long long cand = (fm | ml) & (~0ull << cursor);
                 if (!cand) break;
                 const int kk = __ffsll((long long)cand) - 1;
                 const unsigned long long bit = 1ull << kk;
-                if (m_ent & bit) {
+                if (me & bit) {
                     T += 1; pmask |= bit;
-                    if (m_inwin) m_live |= __ballot(inwin && lane - (int)d == kk);   // its exit is now live
+                    const uint32_t ip = (uint32_t)__builtin_amdgcn_readlane((int)inpos, kk);
+                    if (ip < 64u) ml |= 1ull << ip;
                 } else {
                     T -= 1;
                 }
                 cursor = kk + 1;
             }
-        } else {
-            // general step loop in exact Java arithmetic (large acquireCount / int wrap)
-            int cursor = 0;
-            for (;;) {
-                const bool fits = ent && (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)c) <= M;
-                const bool lv = inwin ? ((pmask >> ((uint32_t)(lane - (int)d) & 63u)) & 1ull) != 0 : live;
-                const unsigned long long m = __ballot(lane >= cursor && (fits || lv));
-                if (!m) break;
-                const int kk = __ffsll((long long)m) - 1;
-                if ((m_ent >> kk) & 1ull) { T += 1; pmask |= 1ull << kk; } else { T -= 1; }
-                cursor = kk + 1;
-            }
         }
         T = uniform64(T);
-        if (lane == 0) {
-            ring[((q - lo) >> 6) % RING_WORDS] = pmask;                    // window q = ring word (q-lo)/64
-            if (pmask) {
+        if (pmask) {
+            // exits of the passed entries beyond this window turn live (one vector step)
+            const uint32_t xo = L.xo[buf][64 * w + lane];
+            const bool mk = ((pmask >> lane) & 1ull) && xo != XO_NONE && xo < hi && xo >= q + 64;
+            bool fm2 = false;
+            if (mk) fm2 = thr_mark_exit(L, lxfar, xo, q, lo);
+            far_marked |= __ballot(fm2) != 0;
+            if (lane == 0) {
                 const uint32_t sh = q & 63;
                 atomicOr(pbits + (q >> 6), pmask << sh);
                 if (sh) atomicOr(pbits + (q >> 6) + 1, pmask >> (64 - sh));
             }
         }
-        prev = pmask;
-        code_c = code_n; code_n = code_nn; rw_c = rw_n;
+        if (lane == 0) L.lx[slot] = 0ull;                  // consumed: reused LX_WORDS windows later
+        w++;
+    }
+    if (far_marked) {                                      // far exits must be in HBM before a loader reads them
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        __builtin_amdgcn_s_waitcnt(0);
     }
 }
 
@@ -329,44 +359,38 @@ __global__ void __launch_bounds__(HS_T) k_heavy_stream(DevState st, SegIO io, He
     const bool wave0 = threadIdx.x < 64;
     const uint32_t nch = (hi - lo + HS_CH - 1) / HS_CH;
     if (hc.seg_mode[s] == SM_THREAD) {
-        uint32_t* codes = (uint32_t*)smem;                       // [2][HS_CH]
-        unsigned long long* ring = smem + HS_CH;                 // after 16 KiB of codes: RING_WORDS words
+        ThrLds& L = *reinterpret_cast<ThrLds*>(smem);
+        for (uint32_t i = threadIdx.x; i < LX_WORDS; i += HS_T) L.lx[i] = 0ull;
+        __syncthreads();
         const double M = rule.count;
         const int64_t IM = (int64_t)floor(M);
         int64_t T = st.threads[res];
-        unsigned long long prev = 0;
-        ThrRegs r;
-        thr_load(r, io, lo, lo, hi);
-        thr_store(r, codes);
+        const int h = (int)(threadIdx.x >> 6);
+        const uint32_t ntc = (hi - lo + THR_CH - 1) / THR_CH;
+        if (h > 0) thr_prepare(L, 0, io, hc.exit_of, hc.lxfar, lo, lo, hi, h);
         __syncthreads();
 #ifdef SF_STREAM_PROF
-        uint64_t t_dec = 0, t_wait = 0, t_ld = 0;
+        uint64_t t_work = 0, t_bar = 0;
 #endif
-        for (uint32_t k = 0; k < nch; k++) {
-            const uint32_t q0 = lo + k * HS_CH;
-            const bool more = k + 1 < nch;
+        for (uint32_t k = 0; k < ntc; k++) {
+            const uint32_t q0 = lo + k * THR_CH;
 #ifdef SF_STREAM_PROF
             const uint64_t c0 = __builtin_amdgcn_s_memtime();
 #endif
-            if (more) thr_load(r, io, q0 + HS_CH, lo, hi);
+            if (h == 0) thr_decide(L, k & 1, hc.lxfar, q0, lo, hi, M, IM, T, hc.passbits);
+            else if (k + 1 < ntc) thr_prepare(L, (k + 1) & 1, io, hc.exit_of, hc.lxfar, q0 + THR_CH, lo, hi, h);
 #ifdef SF_STREAM_PROF
             const uint64_t c1 = __builtin_amdgcn_s_memtime();
 #endif
-            if (wave0) thr_decide_chunk(codes + (k & 1) * HS_CH, ring, q0, lo, hi, M, IM, T, prev, hc.passbits);
-#ifdef SF_STREAM_PROF
-            const uint64_t c2 = __builtin_amdgcn_s_memtime();
-#endif
-            if (more) thr_store(r, codes + ((k + 1) & 1) * HS_CH);
             __syncthreads();
 #ifdef SF_STREAM_PROF
-            const uint64_t c3 = __builtin_amdgcn_s_memtime();
-            t_ld += c1 - c0; t_dec += c2 - c1; t_wait += c3 - c2;
+            t_work += c1 - c0; t_bar += __builtin_amdgcn_s_memtime() - c1;
 #endif
         }
 #ifdef SF_STREAM_PROF
-        if (threadIdx.x == 0)
-            printf("SF_STREAM_PROF seg %u events %u chunks %u: issue %lu decide %lu store+barrier %lu cycles\n", s,
-                   hi - lo, nch, (unsigned long)t_ld, (unsigned long)t_dec, (unsigned long)t_wait);
+        if ((threadIdx.x & 63) == 0)
+            printf("SF_STREAM_PROF seg %u wave %d events %u chunks %u: work %lu barrier %lu cycles\n", s, h, hi - lo,
+                   ntc, (unsigned long)t_work, (unsigned long)t_bar);
 #endif
     } else {                                                     // SM_RL
         int64_t* tsb = (int64_t*)smem;                           // [2][HS_CH]
