@@ -109,6 +109,8 @@ static int dalloc(void** p, size_t bytes) {
 void sf_destroy(sf_engine* e) {
     if (!e) return;
     if (e->stream) hipStreamSynchronize(e->stream);
+    void* ptrs0[] = {e->w.pv_in, e->w.pv_out};
+    for (void* p : ptrs0) if (p) hipFree(p);
     void* ptrs[] = {e->st.second, e->st.borrow, e->st.minute, e->st.threads, (void*)e->st.rule_off,
                     (void*)e->st.rules, e->st.rstate, (void*)e->st.prule_off, e->st.prules, (void*)e->st.items,
                     e->st.pm_init, e->st.ptab, e->st.err,
@@ -200,6 +202,7 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     Work& w = e->w;
     const size_t N = c.max_batch;
     DALLOC(w.keys_in, N * 4); DALLOC(w.keys_out, N * 4); DALLOC(w.vals_in, N * 4); DALLOC(w.perm, N * 4);
+    DALLOC(w.pv_in, N * sizeof(PackedEv)); DALLOC(w.pv_out, N * sizeof(PackedEv));
     DALLOC(w.head, N * 4); DALLOC(w.head_scan, N * 4);
     DALLOC(w.seg_start, (N + 1) * 4); DALLOC(w.seg_res, N * 4); DALLOC(w.n_seg, 4);
     DALLOC(w.s_ts, N * 8); DALLOC(w.s_cnt, N * 4); DALLOC(w.s_flags, N);
@@ -398,6 +401,14 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         dv.rule = out->rule_idx ? (uint16_t*)(base + align_up(n) + align_up((size_t)n * 4)) : nullptr;
     } else {
         dv.status = out->status; dv.wait = out->wait_ms; dv.rule = out->rule_idx;
+    }
+    {   // time span of the (non-decreasing) batch: packed sort payload when it fits 32 bits
+        int64_t t01[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(&t01[0], b.ts, 8, hipMemcpyDefault, s));
+        HIP_TRY(hipMemcpyAsync(&t01[1], b.ts + (n - 1), 8, hipMemcpyDefault, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        e->w.tmin = t01[0];
+        e->w.packed_ok = t01[1] >= t01[0] && (uint64_t)(t01[1] - t01[0]) < (1ull << 32);
     }
     HIP_TRY(hipMemsetAsync(e->st.err, 0, sizeof(int32_t), s));
     hipError_t le = launch_pipeline(e->st, e->w, b, dv, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s,

@@ -98,11 +98,16 @@ struct EntryAcc {
     unsigned int pad;
 };
 
+// 16-B radix-sort payload of one event (batch time span < 2^32 ms)
+struct alignas(16) PackedEv { uint32_t idx, dts; int32_t cnt; uint32_t flags; };
+
 // Sorted-order working buffers of one batch.
 struct Work {
     uint32_t n;
     uint32_t* keys_in;   uint32_t* keys_out;     // local resource id
     uint32_t* vals_in;   uint32_t* perm;         // iota -> stable permutation
+    PackedEv* pv_in; PackedEv* pv_out;           // packed payload (packed_ok)
+    bool packed_ok; int64_t tmin;                // this batch: span < 2^32 ms, first time
     uint32_t* head;      uint32_t* head_scan;    // segment flags and positions
     uint32_t* seg_start; uint32_t* seg_res; uint32_t* n_seg;
     int64_t* s_ts; int32_t* s_cnt; uint8_t* s_flags;

@@ -43,6 +43,48 @@ __global__ void k_keys(DevBatch b, uint32_t* keys, uint32_t* vals, uint32_t shar
     vals[i] = i;
 }
 
+// Packed payload variant (batch time span < 2^32 ms): the radix sort carries
+// each event's (index, time offset, acquireCount, flags) as a 16-B value, so
+// the sorted order is read back with coalesced loads instead of a random
+// gather from the submission-order arrays.
+__global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t shard_count, uint32_t shard_index,
+                              uint32_t R, int64_t tmin, int32_t* err) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n) return;
+    uint32_t r = b.res[i];
+    uint32_t l = r / shard_count;
+    if (r % shard_count != shard_index || l >= R) { *err = SF_ERR_INVALID; l = 0; }
+    keys[i] = l;
+    PackedEv v;
+    v.idx = i; v.dts = (uint32_t)(b.ts[i] - tmin); v.cnt = b.cnt[i]; v.flags = b.flags[i];
+    pv[i] = v;
+}
+
+__global__ void k_unpack(DevBatch b, const PackedEv* pv, int64_t tmin, uint32_t* perm, int64_t* s_ts, int32_t* s_cnt,
+                         uint8_t* s_flags, uint32_t* inv, uint8_t* s_nargs, uint8_t* s_atag, uint64_t* s_abits,
+                         const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= b.n) return;
+    const PackedEv v = pv[j];
+    const uint32_t i = v.idx;
+    const int32_t c = v.cnt;
+    const uint8_t f = (uint8_t)v.flags;
+    perm[j] = i;
+    s_ts[j] = tmin + (int64_t)v.dts; s_cnt[j] = c; s_flags[j] = f;
+    if (inv) inv[i] = j;
+    if (!(f & SF_EV_EXIT) && ((f & SF_EV_PRIO) || c <= 0)) {
+        uint32_t s = head_scan[j] + head[j] - 1;
+        atomicOr(&segflag[s], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u));
+    }
+    if (b.arg_slots) {
+        if (b.nargs) s_nargs[j] = b.nargs[i];
+        for (uint32_t a = 0; a < b.arg_slots; a++) {
+            s_atag[(size_t)a * b.n + j] = b.atag[(size_t)a * b.n + i];
+            s_abits[(size_t)a * b.n + j] = b.abits[(size_t)a * b.n + i];
+        }
+    }
+}
+
 __global__ void k_heads(const uint32_t* keys, uint32_t n, uint32_t* head) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
@@ -334,6 +376,11 @@ hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_byte
     hipError_t e = rocprim::radix_sort_pairs(nullptr, *sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                              (uint32_t*)nullptr, (uint32_t*)nullptr, max_n, 0u, key_bits);
     if (e != hipSuccess) return e;
+    size_t packed_bytes = 0;
+    e = rocprim::radix_sort_pairs(nullptr, packed_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (PackedEv*)nullptr, (PackedEv*)nullptr, max_n, 0u, key_bits);
+    if (e != hipSuccess) return e;
+    if (packed_bytes > *sort_bytes) *sort_bytes = packed_bytes;
     e = rocprim::exclusive_scan(nullptr, *scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
                                 (size_t)max_n, rocprim::plus<uint32_t>());
     if (e != hipSuccess) return e;
@@ -360,10 +407,19 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     if (n == 0) return hipSuccess;
     const unsigned T = 256;
     if (timing) hipEventRecord(ev[0], s);
-    hipLaunchKernelGGL(k_keys, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.vals_in, shard_count,
-                       shard_index, st.R, st.err);
-    hipError_t e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.vals_in,
-                                             w.perm, n, 0u, key_bits, s);
+    const bool packed = w.packed_ok;
+    hipError_t e;
+    if (packed) {
+        hipLaunchKernelGGL(k_keys_packed, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.pv_in, shard_count,
+                           shard_index, st.R, w.tmin, st.err);
+        e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.pv_in, w.pv_out, n, 0u,
+                                      key_bits, s);
+    } else {
+        hipLaunchKernelGGL(k_keys, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.vals_in, shard_count,
+                           shard_index, st.R, st.err);
+        e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.vals_in, w.perm, n, 0u,
+                                      key_bits, s);
+    }
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_heads, dim3(blocks(n, T)), dim3(T), 0, s, w.keys_out, n, w.head);
     e = rocprim::exclusive_scan(w.scan_tmp, w.scan_tmp_bytes, w.head, w.head_scan, 0u, (size_t)n,
@@ -372,8 +428,13 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     hipLaunchKernelGGL(k_segments, dim3(blocks(n, T)), dim3(T), 0, s, w.keys_out, w.head, w.head_scan, n,
                        w.seg_start, w.seg_res, w.n_seg, w.segflag);
     if (timing) hipEventRecord(ev[1], s);
-    hipLaunchKernelGGL(k_gather, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_ts, w.s_cnt, w.s_flags,
-                       b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag);
+    if (packed)
+        hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.tmin, w.perm, w.s_ts, w.s_cnt,
+                           w.s_flags, b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan,
+                           w.segflag);
+    else
+        hipLaunchKernelGGL(k_gather, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_ts, w.s_cnt, w.s_flags,
+                           b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag);
     hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.inv, w.s_eref,
