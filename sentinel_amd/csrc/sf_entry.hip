@@ -121,15 +121,24 @@ __global__ void __launch_bounds__(EN_T) k_entry_acc(DevState st, DevBatch b, con
     EnPart ps, pm;
     ps.clear(-1); pm.clear(-1);
     long long thr = 0;
-    // lane-contiguous runs: one lane sees few window changes in a time-ordered batch
-    const uint32_t j0 = base + threadIdx.x * EN_PER;
+    // coalesced; a workgroup's 4096 consecutive events span few windows (time order),
+    // so a lane's window key rarely changes.  Window indices by 32-bit division of the
+    // offset from the batch's first window when the batch spans < 2^32 ms.
+    const int64_t base_s = W0s * st.wl, base_m = W0m * 1000;
+    const bool span32 = b.ts[b.n - 1] - base_m < (int64_t)0xffffffffLL;
     for (int k = 0; k < EN_PER; k++) {
-        const uint32_t i = j0 + k;
+        const uint32_t i = base + (uint32_t)(k * EN_T) + threadIdx.x;
         if (i >= b.n) break;
         const EnEvent e = en_event(b, vs, i);
         thr += e.thr;
         if (!e.touch) continue;
-        const long long ks = e.t / st.wl - W0s, km = e.t / 1000 - W0m;
+        long long ks, km;
+        if (span32) {
+            ks = (long long)((uint32_t)(e.t - base_s) / (uint32_t)st.wl);
+            km = (long long)((uint32_t)(e.t - base_m) / 1000u);
+        } else {
+            ks = e.t / st.wl - W0s; km = e.t / 1000 - W0m;
+        }
         if (ks != ps.key) { en_global(acc->sec, acc->minrt_sec, &acc->overflow, ps); ps.clear(ks); }
         if (km != pm.key) { en_global(acc->min, acc->minrt_min, &acc->overflow, pm); pm.clear(km); }
         ps.add(e); pm.add(e);
@@ -189,21 +198,25 @@ __global__ void k_entry_apply_if(DevState st, DevBatch b, EntryNode* en, EntryAc
         }
         return;
     }
+    __shared__ int last_s[SF_MAX_SAMPLE_COUNT], last_m[MINUTE];
     const int i = threadIdx.x;
     const int64_t W0s = b.ts[0] / st.wl, W0m = b.ts[0] / 1000;
-    if (i < st.S) {
-        for (long long r = EN_TBL - 1; r >= 0; r--) {
-            if (!acc->sec[r][5] || (int)((W0s + r) % st.S) != i) continue;
-            en_merge(en->second[i], (W0s + r) * st.wl, acc->sec[r], acc->minrt_sec[r], st.max_rt);
-            break;
-        }
+    if (i < SF_MAX_SAMPLE_COUNT) last_s[i] = -1;
+    if (i < MINUTE) last_m[i] = -1;
+    __syncthreads();
+    // latest touched window row of each slot's residue class
+    for (int r = i; r < (int)EN_TBL; r += blockDim.x) {
+        if (acc->sec[r][5]) atomicMax(&last_s[(int)((W0s + r) % st.S)], r);
+        if (acc->min[r][5]) atomicMax(&last_m[(int)((W0m + r) % MINUTE)], r);
     }
-    if (i < MINUTE) {
-        for (long long r = EN_TBL - 1; r >= 0; r--) {
-            if (!acc->min[r][5] || (int)((W0m + r) % MINUTE) != i) continue;
-            en_merge(en->minute[i], (W0m + r) * 1000, acc->min[r], acc->minrt_min[r], st.max_rt);
-            break;
-        }
+    __syncthreads();
+    if (i < st.S && last_s[i] >= 0) {
+        const int r = last_s[i];
+        en_merge(en->second[i], (W0s + r) * st.wl, acc->sec[r], acc->minrt_sec[r], st.max_rt);
+    }
+    if (i < MINUTE && last_m[i] >= 0) {
+        const int r = last_m[i];
+        en_merge(en->minute[i], (W0m + r) * 1000, acc->min[r], acc->minrt_min[r], st.max_rt);
     }
     if (i == 0) en->threads = wadd(en->threads, (int64_t)acc->threads);
 }
@@ -232,7 +245,7 @@ hipError_t launch_entry_node(const DevState& st, const DevBatch& b, const uint8_
     hipLaunchKernelGGL(k_entry_minrt_init, dim3((EN_TBL + 255) / 256), dim3(256), 0, s, acc);
     const unsigned nb = (unsigned)((b.n + EN_T * EN_PER - 1) / (EN_T * EN_PER));
     hipLaunchKernelGGL(k_entry_acc, dim3(nb), dim3(EN_T), 0, s, st, b, vstatus, acc);
-    hipLaunchKernelGGL(k_entry_apply_if, dim3(1), dim3(64), 0, s, st, b, en, acc, vstatus);
+    hipLaunchKernelGGL(k_entry_apply_if, dim3(1), dim3(256), 0, s, st, b, en, acc, vstatus);
     return hipGetLastError();
 }
 
