@@ -302,8 +302,8 @@ typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last 
     uint32_t resource;            /* local resource index on this shard        */
     uint32_t events;              /* events of the resource in the batch       */
     uint32_t mode;                /* heavy algorithm (DESIGN.md "Kernels")     */
-    uint32_t pad;
-    uint64_t ticks;               /* k_heavy_decide time of the segment, 100 MHz device clock */
+    uint32_t start;               /* k_heavy_stream segments: start after the launch's first segment start (100 MHz ticks) */
+    uint64_t ticks;               /* time of the segment in its kernel, 100 MHz device clock */
 } sf_heavy_profile;
 
 /* ---- API ------------------------------------------------------------- */

@@ -179,7 +179,7 @@ class sf_stats(C.Structure):
 
 
 class sf_heavy_profile(C.Structure):
-    _fields_ = [("resource", C.c_uint32), ("events", C.c_uint32), ("mode", C.c_uint32), ("pad", C.c_uint32),
+    _fields_ = [("resource", C.c_uint32), ("events", C.c_uint32), ("mode", C.c_uint32), ("start", C.c_uint32),
                 ("ticks", C.c_uint64)]
 
 

@@ -37,6 +37,7 @@ static int fail(int code, const std::string& msg) {
 struct sf_engine {
     sf_config cfg{};
     hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
+    bool serial = false;            // diagnostics (SF_SERIAL_STREAMS=1): every kernel on one stream
     uint32_t R = 0, key_bits = 1;
     DevState st{};
     Work w{};
@@ -119,7 +120,7 @@ void sf_destroy(sf_engine* e) {
                     e->w.s_cts, e->w.s_nargs, e->w.s_atag, e->w.s_abits, e->w.inv, e->w.v_status, e->w.v_wait,
                     e->w.v_rule, e->w.sort_tmp, e->w.scan_tmp, e->stage_in, e->stage_out,
                     e->w.segflag, e->w.seg_mode, e->w.light_list, e->w.heavy_list, e->w.counters, e->w.pcg,
-                    e->w.pscan_tmp, e->w.item_lo, e->w.item_hi, e->w.item_wait, e->w.n_items, e->w.acc_hw,
+                    e->w.pscan_tmp, e->w.fill_tiles, e->w.fill_ntiles, e->w.acc_hw,
                     e->w.acc_sec, e->w.acc_hw_base, e->w.acc_sec_base, e->w.seg_hw0, e->w.seg_sec0,
                     e->w.seg_nhw, e->w.seg_nsec, e->w.hticks, e->w.passbits, e->w.stream_list, e->w.sticks,
                     e->w.exit_of, e->w.lxfar};
@@ -164,7 +165,13 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     while ((1ull << e->key_bits) < e->R) e->key_bits++;
     HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&e->stream3, hipStreamNonBlocking));
+    {   // stream C carries k_heavy_stream (the serial chains): its workgroups are
+        // dispatched ahead of the light lanes' when CU slots free up
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&e->stream3, hipStreamNonBlocking, greatest));
+    }
+    if (const char* v = getenv("SF_SERIAL_STREAMS")) e->serial = v[0] == '1';
     for (auto& x : e->ev) HIP_TRY(hipEventCreate(&x));
 
     DevState& st = e->st;
@@ -215,11 +222,19 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     DALLOC(w.pscan_tmp, w.pscan_tmp_bytes);
     // heavy / light split
     w.heavy_min = c.heavy_min_events ? c.heavy_min_events : 512;
+    {
+        int dev = 0, ncu = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        w.stream_grid = 2u * (uint32_t)(ncu > 0 ? ncu : 256);
+        w.fill_grid = 8u * (uint32_t)(ncu > 0 ? ncu : 256);
+    }
     const size_t SC = std::min<size_t>(N, R) + 1;
     w.seg_cap = (uint32_t)SC;
     DALLOC(w.segflag, SC * 4); DALLOC(w.seg_mode, SC); DALLOC(w.light_list, SC * 4); DALLOC(w.heavy_list, SC * 4);
     DALLOC(w.counters, 16 * 4); DALLOC(w.pcg, N * 8);
-    DALLOC(w.item_lo, N * 4); DALLOC(w.item_hi, N * 4); DALLOC(w.item_wait, N * 4); DALLOC(w.n_items, SC * 4);
+    w.fill_tile_cap = (uint32_t)(N / FILL_TILE + N / (w.heavy_min + 1) + 2);
+    DALLOC(w.fill_tiles, (size_t)2 * w.fill_tile_cap * sizeof(uint2)); DALLOC(w.fill_ntiles, 2 * 4);
     w.acc_cap = (uint32_t)std::min<size_t>(std::max<size_t>(N / w.heavy_min * 64, 1 << 16), 1u << 24);
     DALLOC(w.acc_hw, (size_t)w.acc_cap * ACC_BYTES); DALLOC(w.acc_sec, (size_t)w.acc_cap * ACC_BYTES);
     DALLOC(w.acc_hw_base, SC * 4); DALLOC(w.acc_sec_base, SC * 4); DALLOC(w.seg_hw0, SC * 8);
@@ -412,7 +427,8 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     }
     HIP_TRY(hipMemsetAsync(e->st.err, 0, sizeof(int32_t), s));
     hipError_t le = launch_pipeline(e->st, e->w, b, dv, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s,
-                                    e->stream2, e->stream3, e->ev, e->timing);
+                                    e->serial ? e->stream : e->stream2, e->serial ? e->stream : e->stream3,
+                                    e->ev, e->timing);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
     // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream order)
     le = launch_entry_node(e->st, b, dv.status, e->en, e->en_acc, s);
@@ -898,10 +914,16 @@ int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uin
         HIP_TRY(hipMemcpy(res.data(), e->w.seg_res, nseg * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(mode.data(), e->w.seg_mode, nseg, hipMemcpyDeviceToHost));
     }
+    uint64_t t0 = ~0ull;
+    for (uint32_t i = n1; i < nh; i++) t0 = std::min(t0, tk[i] >> 24);
     for (uint32_t i = 0; i < nh; i++) {
         const uint32_t sg = list[i];
         out[i].resource = res[sg]; out[i].events = start[sg + 1] - start[sg];
-        out[i].mode = mode[sg]; out[i].pad = 0; out[i].ticks = e->timing ? tk[i] : 0;
+        out[i].mode = mode[sg]; out[i].start = 0; out[i].ticks = e->timing ? tk[i] : 0;
+        if (i >= n1 && e->timing) {          // stream segments: (start & 2^40-1) << 24 | duration
+            out[i].ticks = tk[i] & 0xffffffull;
+            out[i].start = (uint32_t)((tk[i] >> 24) - t0);
+        }
     }
     *n_out = nh;
     return SF_OK;

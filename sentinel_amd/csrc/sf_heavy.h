@@ -15,11 +15,12 @@
 //    cost(c) - maxQueueingTimeMs (RateLimiterController.java:48-102), so the
 //    next pass is found by a search over the time-sorted segment.
 //
-// One workgroup (a "team") runs the decision chain for one segment and emits
-// a sorted list of pass ITEMS (entry intervals and singleton passes with a
-// wait).  Device-wide kernels then write every verdict from the items, reduce
-// the per-window counters, and apply them to the LeapArray state in time
-// order (bucket reset semantics of LeapArray.currentWindow).
+// One wavefront (a "team", QPS / WarmUp) or workgroup (k_heavy_stream: RL,
+// THREAD) runs the decision chain for one segment and sets one PASS BIT per
+// passed entry (RateLimiter waits go straight into v_wait).  Device-wide
+// kernels then write every verdict from the bits, reduce the per-window
+// counters, and apply them to the LeapArray state in time order (bucket reset
+// semantics of LeapArray.currentWindow).
 #pragma once
 #include "sf_decide.h"
 
@@ -64,11 +65,10 @@ struct HeavyCtx {
     const uint32_t* heavy_list; const uint32_t* n_heavy;  // n_heavy[0] front count, n_heavy[3] back count
     uint32_t seg_cap;
     const int64_t* pcg;                // inclusive prefix of entry acquireCount over the sorted batch
-    uint32_t* item_lo; uint32_t* item_hi; int32_t* item_wait; uint32_t* n_items;
     Acc* acc_hw; Acc* acc_sec; const uint32_t* acc_hw_base; const uint32_t* acc_sec_base;
     const int64_t* seg_hw0; const int64_t* seg_sec0;    // first window index of the segment
     uint64_t* hticks;                                   // per heavy-list entry, or null
-    unsigned long long* passbits;                       // [n/64+2] bit j: entry j passed (SM_THREAD)
+    unsigned long long* passbits;                       // [n/64+2] bit j: entry j passed (QPS/WarmUp/RL/THREAD)
     const uint32_t* exit_of;                            // [n] sorted index of an entry's exit (or ~0)
     unsigned long long* lxfar;                          // [n/64+2] live exits beyond the LDS ring (SM_THREAD)
 };
@@ -142,13 +142,26 @@ SF_HD bool is_entry(uint8_t f) { return (f & SF_EV_EXIT) == 0; }
 // Σ acquireCount of entries in [a, b] inclusive (a <= b), from the global prefix
 SF_HD int64_t csum(const int64_t* pcg, uint32_t a, uint32_t b) { return pcg[b] - (a ? pcg[a - 1] : 0); }
 
-struct ItemWriter {
-    uint32_t* lo; uint32_t* hi; int32_t* wait; uint32_t base; uint32_t n;
-    SF_HD void push(bool leader, uint32_t a, uint32_t b, int32_t w) {
-        if (leader) { lo[base + n] = a; hi[base + n] = b; wait[base + n] = w; }
-        n++;
+// pass bits: decided entries are one bit each in hc.passbits (k_heavy_fill
+// turns them into verdicts); words at segment edges are shared, hence atomic
+SF_HD void or_bits(unsigned long long* w, unsigned long long m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicOr(w, m);
+#else
+    *w |= m;
+#endif
+}
+// entries [a, b) passed: the team sets the words in parallel
+SF_HD void set_pass_range(Team& tm, unsigned long long* pb, uint32_t a, uint32_t b) {
+    if (a >= b) return;
+    const uint32_t w0 = a >> 6, w1 = (b - 1) >> 6;
+    for (uint32_t w = w0 + (uint32_t)tm.rank; w <= w1; w += (uint32_t)Team::size) {
+        unsigned long long m = ~0ull;
+        if (w == w0) m &= ~0ull << (a & 63);
+        if (w == w1) m &= ~0ull >> (63 - ((b - 1) & 63));
+        or_bits(pb + w, m);
     }
-};
+}
 
 // ---------------------------------------------------------- QPS / WarmUp
 // Runs uniformly on every lane of the team; only the leader writes.
@@ -171,7 +184,6 @@ SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyC
     const DevRule rule = st.rules[r0];
     DevRuleState rs = st.rstate[r0];
     const Bucket* gmin = st.minute + (size_t)res * MINUTE;
-    ItemWriter iw{hc.item_lo, hc.item_hi, hc.item_wait, lo, 0};
     // per-second pass totals of the minute window (for previousPassQps)
     int64_t cur_sec = INT64_MIN, cur_sec_pass = 0, prev_sec_pass_known = INT64_MIN, prev_sec_pass = 0;
     int64_t last_sync_sec = INT64_MIN;
@@ -236,7 +248,7 @@ SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyC
             const uint32_t f = team_first_true(tm, p, b, [&](uint32_t j) {
                 return (double)(base + (pcg[j] - pc0)) > thr;
             });
-            if (f > p) { passed = (f ? pcg[f - 1] : 0) - pc0; iw.push(tm.leader(), p, f, 0); }
+            if (f > p) { passed = (f ? pcg[f - 1] : 0) - pc0; set_pass_range(tm, hc.passbits, p, f); }
             // tail: remaining entries with small acquireCount may still fit
             uint32_t j = f + 1;
             while (j < b && (double)(base + passed + 1) <= thr) {      // else no c >= 1 can pass any more
@@ -245,7 +257,7 @@ SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyC
                 });
                 if (j >= b) break;
                 passed += io.cnt[j];
-                iw.push(tm.leader(), j, j + 1, 0);
+                if (tm.leader()) or_bits(hc.passbits + (j >> 6), 1ull << (j & 63));
                 j++;
             }
         }
@@ -255,10 +267,8 @@ SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyC
         cur_sec_pass = wadd(cur_sec_pass, passed);
         p = b;
     }
-    if (tm.leader()) {
-        hc.n_items[s] = iw.n;
-        st.rstate[r0] = rs;
-    }
+    if (tm.leader()) st.rstate[r0] = rs;
+    (void)s;
 }
 
 // ---------------------------------------------------------- RateLimiter
@@ -267,7 +277,6 @@ SF_HD void heavy_rl(Team& tm, const DevState& st, const SegIO& io, const HeavyCt
     const uint32_t r0 = st.rule_off[res];
     const DevRule rule = st.rules[r0];
     DevRuleState rs = st.rstate[r0];
-    ItemWriter iw{hc.item_lo, hc.item_hi, hc.item_wait, lo, 0};
     if (rule.count > 0) {
         const int64_t cost1 = j_round(1.0 * 1 / rule.count * 1000);
         int64_t L = rs.latest_passed;
@@ -290,12 +299,16 @@ SF_HD void heavy_rl(Team& tm, const DevState& st, const SegIO& io, const HeavyCt
             int32_t wait = 0;
             if (L + cost <= t) L = t;
             else { L += cost; wait = (int32_t)(L - t); }
-            iw.push(tm.leader(), j, j + 1, wait);
+            if (tm.leader()) {
+                or_bits(hc.passbits + (j >> 6), 1ull << (j & 63));
+                if (io.v_wait) io.v_wait[j] = wait;
+            }
             p = j + 1;
         }
         rs.latest_passed = L;
     }
-    if (tm.leader()) { hc.n_items[s] = iw.n; st.rstate[r0] = rs; }
+    if (tm.leader()) st.rstate[r0] = rs;
+    (void)s;
 }
 
 
@@ -306,132 +319,8 @@ SF_HD void heavy_rl(Team& tm, const DevState& st, const SegIO& io, const HeavyCt
 // The exit of an entry decided in this batch is live iff that entry passed.
 // Output: one bit per passed entry in hc.passbits; k_heavy_fill turns the
 // bits into verdicts and window counters.
-constexpr uint32_t RING_WORDS = 2048;                  // 128 Ki events of pass bits in LDS (16 KiB)
-constexpr uint32_t RING_BITS = RING_WORDS * 64;
-#if defined(__HIP__)
-constexpr int THREAD_KW = 16;         // windows per load batch; the next batch is in flight meanwhile
-// LDS staging of one batch: flags, acquireCount, entry ref of 16 x 64 events
-constexpr uint32_t THREAD_STAGE_WORDS = (THREAD_KW * 64 * (1 + 4 + 8) + 7) / 8;
-
-struct ThreadIn { uint8_t f[THREAD_KW]; int32_t c[THREAD_KW]; int64_t r[THREAD_KW]; };
-
-__device__ __forceinline__ void thread_load(ThreadIn& in, const SegIO& io, uint32_t q0, uint32_t hi, int lane) {
-#pragma unroll
-    for (int k = 0; k < THREAD_KW; k++) {
-        const uint32_t j = q0 + 64 * k + lane;
-        const bool v = j < hi;
-        in.f[k] = v ? io.flags[j] : (uint8_t)0;
-        in.c[k] = v ? io.cnt[j] : 0;
-        in.r[k] = (v && io.eref && (in.f[k] & SF_EV_EXIT)) ? io.eref[j] : -1;
-    }
-}
-__device__ __forceinline__ void thread_stage(const ThreadIn& in, unsigned long long* stage, int lane) {
-    int64_t* sr = (int64_t*)stage;
-    int32_t* sc = (int32_t*)(sr + THREAD_KW * 64);
-    uint8_t* sf = (uint8_t*)(sc + THREAD_KW * 64);
-#pragma unroll
-    for (int k = 0; k < THREAD_KW; k++) { sr[k * 64 + lane] = in.r[k]; sc[k * 64 + lane] = in.c[k]; sf[k * 64 + lane] = in.f[k]; }
-}
-
-__device__ void heavy_thread(Team& tm, const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t s,
-                             uint32_t res, uint32_t lo, uint32_t hi, unsigned long long* ring,
-                             unsigned long long* stage) {
-    const DevRule rule = st.rules[st.rule_off[res]];
-    const double M = rule.count;
-    const int64_t IM = (int64_t)floor(M);
-    int64_t T = st.threads[res];
-    const int lane = tm.rank;
-    unsigned long long* pbits = hc.passbits;
-    const int64_t* sr = (const int64_t*)stage;
-    const int32_t* sc = (const int32_t*)(sr + THREAD_KW * 64);
-    const uint8_t* sf = (const uint8_t*)(sc + THREAD_KW * 64);
-    ThreadIn nxt;
-    thread_load(nxt, io, lo, hi, lane);
-    for (uint32_t q0 = lo; q0 < hi; q0 += 64 * THREAD_KW) {
-        thread_stage(nxt, stage, lane);                  // this batch: registers -> LDS (own lane's slots)
-        if (q0 + 64 * THREAD_KW < hi) thread_load(nxt, io, q0 + 64 * THREAD_KW, hi, lane);
-        const int nk = (int)min((uint32_t)THREAD_KW, (hi - q0 + 63) / 64);
-        for (int k = 0; k < nk; k++) {
-            const uint32_t q = q0 + 64 * k;
-            const uint32_t j = q + lane;
-            const bool valid = j < hi;
-            const uint8_t fl = sf[k * 64 + lane];
-            const int32_t c = sc[k * 64 + lane];
-            const bool ent = valid && !(fl & SF_EV_EXIT);
-            const bool ex = valid && (fl & SF_EV_EXIT);
-            const int64_t r = sr[k * 64 + lane];
-            const bool bad = ex && r >= 0 && (r < (int64_t)lo || r >= (int64_t)j);   // flagged by k_heavy_fill
-            const bool inwin = ex && !bad && r >= (int64_t)q;
-            bool live = ex && r < 0;
-            if (ex && !bad && r >= 0 && r < (int64_t)q) {
-                if (j - (uint32_t)r < RING_BITS - 64) {
-                    const uint32_t b = (uint32_t)(r - lo) % RING_BITS;
-                    live = (ring[b >> 6] >> (b & 63)) & 1ull;
-                } else {
-                    // older than the ring: read this wave's own bits back from L2 (same XCD);
-                    // wait for its atomics to complete, then load past the L1
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                    __builtin_amdgcn_s_waitcnt(0);
-                    const unsigned long long w =
-                        __hip_atomic_load(pbits + (r >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    live = (w >> (r & 63)) & 1ull;
-                }
-            }
-            const unsigned long long m_ent = __ballot(ent), m_inwin = __ballot(inwin);
-            const int n_live = (int)__popcll(__ballot(ex && !inwin && live));
-            const int n_ent = (int)__popcll(m_ent);
-            const int64_t room0 = IM - T;
-            unsigned long long pmask = 0;
-            if (room0 + n_live < 1) {
-                // acquireCount >= 1 (heavy_mode): even with every live exit first, no entry fits;
-                // the exits of this window's entries are then not live either
-                T -= n_live;
-            } else if (n_ent > 0) {
-                bool all = false;
-                if (room0 >= (int64_t)n_ent) {                // the thread count before entry k is <= T + k
-                    int cmax = 1;
-                    if (__ballot(ent && c != 1)) {
-                        cmax = ent ? c : 0;
-#pragma unroll
-                        for (int o = 32; o > 0; o >>= 1) { const int a2 = __shfl_xor(cmax, o); cmax = a2 > cmax ? a2 : cmax; }
-                    }
-                    all = room0 >= (int64_t)(n_ent - 1) + cmax;
-                }
-                if (all) {
-                    pmask = m_ent;
-                    T += (int64_t)n_ent - (int64_t)n_live - (int64_t)__popcll(m_inwin);
-                } else {
-                    // step through the events that change the thread count: the next
-                    // entry that fits or the next live exit, one ballot per step
-                    int cursor = 0;
-                    for (;;) {
-                        const bool fits = ent && (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)c) <= M;
-                        const bool lv = ex && (inwin ? ((pmask >> (uint32_t)(r - q)) & 1ull) != 0 : live);
-                        const unsigned long long m = __ballot(lane >= cursor && (fits || lv));
-                        if (!m) break;
-                        const int kk = __ffsll((long long)m) - 1;
-                        if ((m_ent >> kk) & 1ull) { T += 1; pmask |= 1ull << kk; } else { T -= 1; }
-                        cursor = kk + 1;
-                    }
-                }
-            } else {
-                T -= n_live;
-            }
-            if (lane == 0) {
-                // window q covers ring word (q - lo) / 64 exactly: bit = lane
-                ring[((q - lo) >> 6) % RING_WORDS] = pmask;
-                if (pmask) {
-                    const uint32_t sh = q & 63;
-                    atomicOr(pbits + (q >> 6), pmask << sh);
-                    if (sh) atomicOr(pbits + (q >> 6) + 1, pmask >> (64 - sh));
-                }
-            }
-        }
-    }
-    (void)s;
-}
-#else
-// host build: the same semantics, one event at a time
+#if !defined(__HIP__)
+// host build (tests/hostsim): one event at a time; the GPU runs k_heavy_stream
 inline void heavy_thread(Team&, const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t, uint32_t res,
                          uint32_t lo, uint32_t hi, unsigned long long*, unsigned long long*) {
     const double M = st.rules[st.rule_off[res]].count;
@@ -449,16 +338,6 @@ inline void heavy_thread(Team&, const DevState& st, const SegIO& io, const Heavy
     }
 }
 #endif
-
-// entry verdict from a segment's sorted item list (binary search)
-SF_HD bool item_lookup(const HeavyCtx& hc, uint32_t lo, uint32_t n, uint32_t j, int32_t* wait) {
-    uint32_t a = 0, b = n;                       // last item with item_lo <= j
-    while (a < b) { uint32_t m = (a + b) / 2; if (hc.item_lo[lo + m] <= j) a = m + 1; else b = m; }
-    if (a == 0) return false;
-    uint32_t k = lo + a - 1;
-    if (j < hc.item_hi[k]) { *wait = hc.item_wait[k]; return true; }
-    return false;
-}
 
 // Apply the per-window deltas of one heavy segment to its node state in
 // time order (LeapArray.currentWindow reset semantics; MetricBucket adds).
@@ -496,42 +375,26 @@ SF_HD void heavy_apply(const DevState& st, const HeavyCtx& hc, uint32_t s, uint3
     st.threads[res] = threads;
 }
 
-// verdict + accounting contribution of event j of a heavy item segment
+// verdict + accounting contribution of event j of a heavy segment decided
+// into pass bits (QPS / WarmUp / RL / THREAD; no-rule segments pass every
+// entry).  RateLimiter waits were written into v_wait when the entry passed.
 struct EvContrib { uint8_t status; int32_t wait; bool touch, passed, live_exit; int64_t c, rt; bool err; };
-SF_HD EvContrib heavy_event(const HeavyCtx& hc, const SegIO& io, uint32_t lo, uint32_t nitems, uint32_t j,
-                            bool from_bits) {
+SF_HD EvContrib heavy_event(const HeavyCtx& hc, const SegIO& io, uint32_t lo, uint8_t mode, uint32_t j) {
     EvContrib r{};
     const uint8_t f = io.flags[j];
     r.c = io.cnt[j];
-    if (from_bits) {                           // SM_THREAD: decide set one bit per passed entry
-        if (is_entry(f)) {
-            r.passed = pass_bit(hc.passbits, j);
-            r.status = r.passed ? SF_V_PASS : SF_V_BLOCK_FLOW;
-            r.touch = true;
-        } else {
-            const int64_t ref = io.eref ? io.eref[j] : -1;
-            r.live_exit = ref < 0 || (ref >= (int64_t)lo && ref < (int64_t)j && pass_bit(hc.passbits, (uint32_t)ref));
-            r.status = r.live_exit ? SF_V_EXIT : SF_V_EXIT_IGNORED;
-            r.touch = r.live_exit;
-            r.rt = io.ts[j] - (ref >= 0 ? io.ts[ref] : (io.cts ? io.cts[j] : io.ts[j]));
-            r.err = (f & SF_EV_ERROR) != 0;
-        }
-        return r;
-    }
+    const bool all = mode == SM_NORULE;
     if (is_entry(f)) {
-        int32_t w = 0;
-        r.passed = item_lookup(hc, lo, nitems, j, &w);
-        r.status = r.passed ? (w > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : SF_V_BLOCK_FLOW;
-        r.wait = r.passed ? w : 0;
+        r.passed = all || pass_bit(hc.passbits, j);
+        r.wait = (mode == SM_RL && r.passed && io.v_wait) ? io.v_wait[j] : 0;
+        r.status = r.passed ? (r.wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : SF_V_BLOCK_FLOW;
         r.touch = true;
     } else {
-        int64_t ref = io.eref ? io.eref[j] : -1;
-        bool live; int64_t cts;
-        if (ref >= 0) { int32_t w; live = item_lookup(hc, lo, nitems, (uint32_t)ref, &w); cts = io.ts[ref]; }
-        else { live = true; cts = io.cts ? io.cts[j] : io.ts[j]; }
-        r.status = live ? SF_V_EXIT : SF_V_EXIT_IGNORED;
-        r.live_exit = live; r.touch = live;
-        r.rt = io.ts[j] - cts;
+        const int64_t ref = io.eref ? io.eref[j] : -1;
+        r.live_exit = ref < 0 || (ref >= (int64_t)lo && ref < (int64_t)j && (all || pass_bit(hc.passbits, (uint32_t)ref)));
+        r.status = r.live_exit ? SF_V_EXIT : SF_V_EXIT_IGNORED;
+        r.touch = r.live_exit;
+        r.rt = io.ts[j] - (ref >= 0 ? io.ts[ref] : (io.cts ? io.cts[j] : io.ts[j]));
         r.err = (f & SF_EV_ERROR) != 0;
     }
     return r;

@@ -101,6 +101,8 @@ struct EntryAcc {
 // 16-B radix-sort payload of one event (batch time span < 2^32 ms)
 struct alignas(16) PackedEv { uint32_t idx, dts; int32_t cnt; uint32_t flags; };
 
+constexpr uint32_t FILL_TILE = 4096;             // events per k_heavy_fill tile (256 threads x 16)
+
 // Sorted-order working buffers of one batch.
 struct Work {
     uint32_t n;
@@ -123,15 +125,18 @@ struct Work {
     uint32_t* light_list; uint32_t* heavy_list; uint32_t* counters;   // [0] n_light [1] n_heavy front [2] hw slots [3] sec slots [4] n_heavy back
                                                                       // [5] n_stream front [6] n_stream back
     int64_t* pcg; void* pscan_tmp; size_t pscan_tmp_bytes;
-    uint32_t* item_lo; uint32_t* item_hi; int32_t* item_wait; uint32_t* n_items;
+    uint2* fill_tiles; uint32_t fill_tile_cap;         // [2][cap] (segment, tile) of each class for k_heavy_fill
+    uint32_t* fill_ntiles;                              // [2] tiles per class
+    uint32_t fill_grid;                                 // persistent k_heavy_fill workgroups (8 per CU)
     void* acc_hw; void* acc_sec; uint32_t acc_cap;
     uint32_t* acc_hw_base; uint32_t* acc_sec_base; int64_t* seg_hw0; int64_t* seg_sec0;
     uint32_t* seg_nhw; uint32_t* seg_nsec;
     uint32_t heavy_min;                                 // segments longer than this go heavy
+    uint32_t stream_grid;                               // persistent k_heavy_stream workgroups (2 per CU)
     uint64_t* hticks;                                   // [max heavy] k_heavy_decide clock per segment (timing)
     uint32_t* stream_list;                              // THREAD / RL heavy segments (k_heavy_stream)
     uint64_t* sticks;                                   // [max heavy] k_heavy_stream clock per segment (timing)
-    unsigned long long* passbits;                       // [n/64+2] pass bit per sorted event (SM_THREAD)
+    unsigned long long* passbits;                       // [n/64+2] pass bit per sorted entry (heavy segments)
     uint32_t* exit_of;                                  // [n] sorted index of each entry's exit, ~0 if none
     unsigned long long* lxfar;                          // [n/64+2] far live exits (SM_THREAD)
 };

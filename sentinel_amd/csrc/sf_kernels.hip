@@ -229,7 +229,6 @@ static HeavyCtx heavy_ctx(const Work& w) {
     HeavyCtx hc;
     hc.seg_start = w.seg_start; hc.seg_res = w.seg_res; hc.seg_mode = w.seg_mode;
     hc.heavy_list = w.heavy_list; hc.n_heavy = w.counters + 1; hc.pcg = w.pcg; hc.seg_cap = w.seg_cap;
-    hc.item_lo = w.item_lo; hc.item_hi = w.item_hi; hc.item_wait = w.item_wait; hc.n_items = w.n_items;
     hc.acc_hw = (Acc*)w.acc_hw; hc.acc_sec = (Acc*)w.acc_sec;
     hc.acc_hw_base = w.acc_hw_base; hc.acc_sec_base = w.acc_sec_base;
     hc.seg_hw0 = w.seg_hw0; hc.seg_sec0 = w.seg_sec0;
@@ -253,9 +252,7 @@ __global__ void __launch_bounds__(64) k_heavy_decide(DevState st, SegIO io, Heav
     switch (hc.seg_mode[s]) {
     case SM_QPS: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, false); break;
     case SM_WARM: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, true); break;
-    case SM_NORULE:
-        if (tm.leader()) { hc.item_lo[lo] = lo; hc.item_hi[lo] = hi; hc.item_wait[lo] = 0; hc.n_items[s] = 1; }
-        break;
+    case SM_NORULE: break;                          // every entry passes (k_heavy_fill)
     default:
         if (tm.leader()) decide_segment<MAXS>(st, io, res, lo, hi);
         break;
@@ -312,40 +309,93 @@ __device__ void wave_flush(PAcc& p, uint32_t key, Acc* table) {
     if ((int)(threadIdx.x & 63) == l0) r.flush(table, k0);
 }
 
-constexpr int FILL_ITERS = 16;
-// cls 0: segments of k_heavy_decide (QPS / WarmUp / no rule); cls 1: of k_heavy_stream (THREAD / RL)
-__global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, HeavyCtx hc, const uint32_t* head,
-                                                    const uint32_t* head_scan, int cls) {
-    const uint32_t NONE = 0xffffffffu;
-    const uint32_t base = blockIdx.x * (256 * FILL_ITERS);
-    PAcc ph, ps; ph.clear(); ps.clear();
-    uint32_t kh = NONE, ks = NONE;
-    for (int it = 0; it < FILL_ITERS; it++) {
-        const uint32_t j = base + it * 256 + threadIdx.x;
-        if (j >= io.n) break;
-        const uint32_t s = head_scan[j] + head[j] - 1;
-        const uint8_t mode = hc.seg_mode[s];
-        if (mode < SM_QPS) continue;
-        if ((int)(mode == SM_THREAD || mode == SM_RL) != cls) continue;
-        const uint32_t lo = hc.seg_start[s];
-        if (io.eref && !is_entry(io.flags[j])) {
-            int64_t r = io.eref[j];
-            if (r >= 0 && (r < (int64_t)lo || r >= (int64_t)j || !is_entry(io.flags[r]))) { *st.err = SF_ERR_INVALID; }
+constexpr int FILL_ITERS = FILL_TILE / 256;
+static_assert(FILL_ITERS * 256 == (int)FILL_TILE, "a fill tile is 256 threads x FILL_ITERS events");
+
+// Tiles of FILL_TILE events over the heavy segments of each class (block c:
+// class c): cls 0 = k_heavy_decide's list (QPS / WarmUp / no rule; generic
+// segments wrote their verdicts themselves), cls 1 = k_heavy_stream's list
+// (THREAD / RL).  k_heavy_fill then reads only the events of its class.
+__global__ void __launch_bounds__(1024) k_fill_tiles(HeavyCtx hc, StreamCtx sc, uint2* tiles, uint32_t cap,
+                                                     uint32_t* ntiles) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const int c = (int)blockIdx.x;
+    uint2* out = tiles + (size_t)c * cap;
+    const uint32_t nl = c == 0 ? hc.n_heavy[0] + hc.n_heavy[3] : sc.n_list[0] + sc.n_list[1];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < nl; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        uint32_t s = 0, nt = 0;
+        if (i < nl) {
+            const bool ok = c == 0 ? heavy_at(hc, i, &s) : stream_at(sc, i, &s);
+            if (ok && hc.seg_mode[s] >= SM_QPS) nt = (hc.seg_start[s + 1] - hc.seg_start[s] + FILL_TILE - 1) / FILL_TILE;
         }
-        const bool thr = mode == SM_THREAD;
-        EvContrib e = heavy_event(hc, io, lo, thr ? 0u : hc.n_items[s], j, thr);
-        io.v_status[j] = e.status;
-        if (io.v_wait) io.v_wait[j] = e.wait;
-        if (io.v_rule) io.v_rule[j] = 0;
-        if (!e.touch) continue;
-        const uint32_t key_h = hc.acc_hw_base[s] + (uint32_t)(io.ts[j] / st.wl - hc.seg_hw0[s]);
-        const uint32_t key_s = hc.acc_sec_base[s] + (uint32_t)(io.ts[j] / 1000 - hc.seg_sec0[s]);
-        if (key_h != kh) { if (kh != NONE) ph.flush(hc.acc_hw, kh); ph.clear(); kh = key_h; }
-        if (key_s != ks) { if (ks != NONE) ps.flush(hc.acc_sec, ks); ps.clear(); ks = key_s; }
-        ph.add(e); ps.add(e);
+        const uint32_t incl = (uint32_t)wave_scan_add((int)nt);
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t before = carry;
+        for (int k = 0; k < wv; k++) before += wsum[k];
+        const uint32_t base = before + incl - nt;
+        for (uint32_t k = 0; k < nt && base + k < cap; k++) out[base + k] = make_uint2(s, k);
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = before + incl;
+        __syncthreads();
     }
-    wave_flush(ph, kh, hc.acc_hw);
-    wave_flush(ps, ks, hc.acc_sec);
+    if (threadIdx.x == 0) ntiles[c] = min(carry, cap);
+}
+
+// Verdicts and per-window counter deltas of the heavy segments of one class,
+// one FILL_TILE-event tile of one segment at a time (persistent grid): the
+// segment's parameters are uniform per tile, every event is one pass-bit
+// lookup (its entry's bit for an exit).
+__global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, HeavyCtx hc, const uint2* tiles,
+                                                    const uint32_t* ntiles, int cls) {
+    const uint32_t NONE = 0xffffffffu;
+    const uint32_t nt = ntiles[cls];
+    const uint32_t wl = (uint32_t)st.wl;
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const uint2 tl = tiles[t];
+        const uint32_t s = tl.x;
+        const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1];
+        const uint8_t mode = hc.seg_mode[s];
+        const uint32_t j0 = lo + tl.y * FILL_TILE, j1 = min(j0 + FILL_TILE, hi);
+        const uint32_t hwb = hc.acc_hw_base[s], secb = hc.acc_sec_base[s];
+        const int64_t hw0 = hc.seg_hw0[s], sec0 = hc.seg_sec0[s];
+        const int64_t bh = hw0 * st.wl, bs = sec0 * 1000;
+        const bool rel32 = io.ts[hi - 1] - bs < (int64_t)0xffffffffLL;   // window keys by 32-bit division
+        PAcc ph, ps; ph.clear(); ps.clear();
+        uint32_t kh = NONE, ks = NONE;
+        for (int it = 0; it < FILL_ITERS; it++) {
+            const uint32_t j = j0 + (uint32_t)(it * 256) + threadIdx.x;
+            if (j >= j1) break;
+            if (io.eref && !is_entry(io.flags[j])) {
+                const int64_t r = io.eref[j];
+                if (r >= 0 && (r < (int64_t)lo || r >= (int64_t)j || !is_entry(io.flags[r]))) *st.err = SF_ERR_INVALID;
+            }
+            const EvContrib e = heavy_event(hc, io, lo, mode, j);
+            io.v_status[j] = e.status;
+            if (io.v_wait) io.v_wait[j] = e.wait;
+            if (io.v_rule) io.v_rule[j] = 0;
+            if (!e.touch) continue;
+            const int64_t tj = io.ts[j];
+            uint32_t key_h, key_s;
+            if (rel32) {
+                key_h = hwb + (uint32_t)(tj - bh) / wl;
+                key_s = secb + (uint32_t)(tj - bs) / 1000u;
+            } else {
+                key_h = hwb + (uint32_t)(tj / st.wl - hw0);
+                key_s = secb + (uint32_t)(tj / 1000 - sec0);
+            }
+            if (key_h != kh) { if (kh != NONE) ph.flush(hc.acc_hw, kh); ph.clear(); kh = key_h; }
+            if (key_s != ks) { if (ks != NONE) ps.flush(hc.acc_sec, ks); ps.clear(); ks = key_s; }
+            ph.add(e); ps.add(e);
+        }
+        wave_flush(ph, kh, hc.acc_hw);
+        wave_flush(ps, ks, hc.acc_sec);
+    }
 }
 
 __global__ void k_heavy_apply(DevState st, HeavyCtx hc, StreamCtx sc, const uint32_t* seg_nhw,
@@ -443,6 +493,8 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     e = rocprim::inclusive_scan(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n, rocprim::plus<int64_t>(), s);
     if (e != hipSuccess) return e;
     hipMemsetAsync(w.counters, 0, 8 * sizeof(uint32_t), s);
+    hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
+    hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
     const uint32_t max_seg = n < st.R ? n : st.R;
     if (timing) hipEventRecord(ev[10], s);
     hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, T)), dim3(T), 0, s, st, w, w.s_ts);
@@ -457,43 +509,42 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     HeavyCtx hc = heavy_ctx(w);
     if (timing) hc.hticks = w.hticks;
 
-    // heavy segments on streams B and C, overlapping the light lanes on A
+    // The serial chains (k_heavy_stream) start first, on A, straight after
+    // classify; QPS/WarmUp heavy segments on B, the light lanes on C.
+    const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
+    StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, timing ? w.sticks : nullptr, w.counters + 7};
+    hipLaunchKernelGGL(k_fill_tiles, dim3(2), dim3(1024), 0, s, hc, sc, w.fill_tiles, w.fill_tile_cap, w.fill_ntiles);
     hipEventRecord(ev[5], s);                      // fork
+    hipEventRecord(ev[11], s);
+    hipLaunchKernelGGL(k_heavy_stream, dim3(std::min(max_heavy, w.stream_grid)), dim3(HS_T), 0, s, st, io, hc, sc);
+    hipEventRecord(ev[12], s);
     hipStreamWaitEvent(s2, ev[5], 0);
     hipStreamWaitEvent(s3, ev[5], 0);
-    const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
-    hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s3);
-    hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s3);
-    hipEventRecord(ev[11], s3);
-    StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, timing ? w.sticks : nullptr};
-    hipLaunchKernelGGL(k_heavy_stream, dim3(max_heavy), dim3(HS_T), 0, s3, st, io, hc, sc);
-    hipEventRecord(ev[12], s3);
     if (st.S <= 2)
         hipLaunchKernelGGL(k_heavy_decide<2>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     else
         hipLaunchKernelGGL(k_heavy_decide<SF_MAX_SAMPLE_COUNT>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     if (timing) hipEventRecord(ev[7], s2);
     // verdicts + window deltas of each heavy class as soon as its decisions are done
-    hipLaunchKernelGGL(k_heavy_fill, dim3(blocks(n, 256 * FILL_ITERS)), dim3(256), 0, s2, st, io, hc, w.head,
-                       w.head_scan, 0);
+    hipLaunchKernelGGL(k_heavy_fill, dim3(w.fill_grid), dim3(256), 0, s2, st, io, hc, w.fill_tiles, w.fill_ntiles, 0);
     if (timing) hipEventRecord(ev[8], s2);
     hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, sc, w.seg_nhw, w.seg_nsec, 0);
-    hipLaunchKernelGGL(k_heavy_fill, dim3(blocks(n, 256 * FILL_ITERS)), dim3(256), 0, s3, st, io, hc, w.head,
-                       w.head_scan, 1);
-    hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s3, st, hc, sc, w.seg_nhw, w.seg_nsec, 1);
-    hipEventRecord(ev[13], s3);
+    hipLaunchKernelGGL(k_heavy_fill, dim3(w.fill_grid), dim3(256), 0, s, st, io, hc,
+                       w.fill_tiles + w.fill_tile_cap, w.fill_ntiles, 1);
+    hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s, st, hc, sc, w.seg_nhw, w.seg_nsec, 1);
 
     const unsigned TD = 128;
     if (st.S <= 2)
-        hipLaunchKernelGGL(k_decide_light<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s, st, io, w.seg_start,
+        hipLaunchKernelGGL(k_decide_light<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
                            w.seg_res, w.light_list, w.counters);
     else
-        hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s, st, io,
+        hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, w.light_list, w.counters);
-    if (timing) hipEventRecord(ev[9], s);
+    hipEventRecord(ev[9], s3);                     // light done (also the join of C)
     hipEventRecord(ev[6], s2);                     // join B and C
     hipStreamWaitEvent(s, ev[6], 0);
-    hipStreamWaitEvent(s, ev[13], 0);
+    hipStreamWaitEvent(s, ev[9], 0);
+    hipEventRecord(ev[13], s);
     if (timing) hipEventRecord(ev[3], s);
     hipLaunchKernelGGL(k_scatter, dim3(blocks(n, T)), dim3(T), 0, s, w.perm, n, w.v_status, w.v_wait,
                        w.v_rule, out);

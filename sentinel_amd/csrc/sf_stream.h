@@ -37,6 +37,7 @@ struct StreamCtx {
     const uint32_t* list; const uint32_t* n_list;   // n_list[0] front count, n_list[1] back count
     uint32_t seg_cap;
     uint64_t* sticks;
+    uint32_t* next;                                 // work queue head (k_heavy_stream)
 };
 
 __device__ __forceinline__ bool stream_at(const StreamCtx& sc, uint32_t b, uint32_t* s) {
@@ -78,7 +79,7 @@ struct ThrWin {                                    // 24 B per window
     unsigned long long ent;                        // entries
     unsigned long long inw;                        // exits whose entry is in this window
     int32_t maxrc;                                 // bound of max over entries of rank + acquireCount
-    uint32_t flags;                                // bit 0: an acquireCount > 8, bit 1: > THR_CBIG
+    uint32_t flags;                                // bit 0: an acquireCount > 8, bit 1: > THR_CBIG, bit 2: > 1
 };
 
 struct ThrLds {
@@ -86,12 +87,18 @@ struct ThrLds {
     ThrWin win[2][THR_WPC];
     uint32_t xo[2][THR_CH];                        // exit position (sorted index) of each entry, or XO_NONE
     int32_t cn[2][THR_CH];                         // acquireCount (exact path)
+    uint8_t el[2][THR_CH];                         // exit whose entry is in its window: the entry's lane, else 255
 };
 static_assert(sizeof(ThrLds) <= HS_LDS_WORDS * 8, "THREAD LDS layout exceeds the stream kernel's LDS");
 
 __device__ __forceinline__ int64_t uniform64(int64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int64_t uniform64_at(int64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
@@ -135,11 +142,12 @@ __device__ void thr_prepare(ThrLds& L, int buf, const SegIO& io, const uint32_t*
         wn.ent = __ballot(ent);
         wn.inw = __ballot(ex && ref >= (int64_t)q && ref < (int64_t)j);
         const bool gt1 = __ballot(ent && c > 1) != 0ull, gt8 = __ballot(ent && c > THR_CSMALL) != 0ull;
-        wn.flags = (gt8 ? 1u : 0u) | (__ballot(ent && c > THR_CBIG) ? 2u : 0u);
+        wn.flags = (gt8 ? 1u : 0u) | (__ballot(ent && c > THR_CBIG) ? 2u : 0u) | (gt1 ? 4u : 0u);
         // bound of max(rank + acquireCount): (entries - 1) + (1, or 8 when some count is 2..8)
         wn.maxrc = gt8 ? INT32_MAX : (int32_t)__popcll(wn.ent) - 1 + (gt1 ? THR_CSMALL : 1);
         L.xo[buf][64 * wl + lane] = ent ? xa[k] : XO_NONE;
         L.cn[buf][64 * wl + lane] = c;
+        L.el[buf][64 * wl + lane] = (ex && ref >= (int64_t)q && ref < (int64_t)j) ? (uint8_t)(ref - (int64_t)q) : (uint8_t)255;
         const unsigned long long mo = __ballot(ex && ref < 0);        // entry of an earlier batch: live
         if (lane == 0) {
             L.win[buf][wl] = wn;
@@ -168,6 +176,69 @@ __device__ __forceinline__ bool thr_mark_exit(ThrLds& L, unsigned long long* lxf
 // entirely: one vector read of their ring words finds the next one.  Inside a
 // window, only events that change the thread count are visited; the exits of
 // the window's passed entries are marked in one vector step after it.
+// inclusive scans over the 64 lanes of a wavefront (DPP: row shifts, then row broadcasts)
+__device__ __forceinline__ int wave_scan_add(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);     // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);     // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);     // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);     // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);     // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);     // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ int wave_scan_max(int v) {
+    constexpr int ID = INT32_MIN;
+    v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(ID, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
+// One window of a THREAD segment with every acquireCount in 1..8, no int
+// wrap and room0 = floor(count) - T >= 0, decided in wavefront steps instead
+// of a walk.  With entries of acquireCount 1 taken as attempted +1 steps and
+// live exits as -1 steps, the thread count is the walk reflected at the cap
+// (a blocked entry is an absorbed step): with V the prefix sum of the steps,
+// the room before event k is  max(room0, max_{j<k} V_j (and 0)) - V_{k-1}.
+// Entries with acquireCount > 1 are taken as blocked unless known to pass
+// ("forced"), and exits of this window's own entries as dead unless known
+// live.  A round is exact up to the first event where either guess is
+// refuted: the first non-forced entry that has room for its acquireCount
+// (it passes: forced), or the first exit whose entry passed (live).  Each
+// refutation is a fact, so the rounds converge, to the serial outcome (every
+// fixed point agrees with the serial decisions event by event).
+__device__ __forceinline__ unsigned long long thr_window_solve(int room0, unsigned long long me,
+                                                               unsigned long long& ml, int32_t c, int eln) {
+    const int lane = (int)(threadIdx.x & 63);
+    const bool ent = (me >> lane) & 1ull;
+    const bool one = ent && c == 1, multi = ent && c > 1;
+    const bool inx = eln < 64;
+    const int el6 = eln & 63;
+    unsigned long long forced = 0, pm = 0;
+    while (true) {
+        const bool live = (ml >> lane) & 1ull;
+        const bool fo = (forced >> lane) & 1ull;
+        const int x = (one || fo) ? 1 : (live ? -1 : 0);
+        const int v = wave_scan_add(x);
+        const int vex = v - x;
+        const int room = max(room0, wave_scan_max(vex)) - vex;     // room before this event
+        pm = __ballot((one && room >= 1) || fo);
+        const unsigned long long mis = __ballot(multi && !fo && room >= c);
+        const int j1 = mis ? __ffsll((long long)mis) - 1 : 64;
+        const bool nx = inx && !live && ((pm >> el6) & 1ull);      // exit of a (guessed) passed entry
+        const unsigned long long nw = __ballot(nx && eln < j1);
+        const int ne = nw ? __ffsll((long long)nw) - 1 : 64;
+        if (j1 == 64 && ne == 64) break;
+        const int F = min(j1, ne);                                  // events before F are exact
+        ml |= __ballot(nx && eln < F);
+        if (j1 < ne) forced |= 1ull << j1;
+    }
+    return pm;
+}
+
 __device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) {
     const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
     const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
@@ -179,6 +250,7 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
     const int lane = (int)(threadIdx.x & 63);
     const uint32_t nwin = min((hi - q0 + 63) / 64, (uint32_t)THR_WPC);
     bool far_marked = false;
+    unsigned long long pst = 0;
     T = uniform64(T);
     const int wl = lane < THR_WPC ? lane : 0;
     const unsigned long long r_ent = L.win[buf][wl].ent;
@@ -219,17 +291,25 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
             pmask = me;
             ml |= uniform_u64(L.win[buf][w].inw);        // exits of this window's entries, inside it
             T += (int64_t)__popcll(me) - (int64_t)__popcll(ml);
+        } else if (nowrap && !(flags & 1u) && room0 >= 0) {
+            const int32_t c = L.cn[buf][64 * w + lane];
+            const int eln = L.el[buf][64 * w + lane];
+            pmask = thr_window_solve((int)room0, me, ml, c, eln);
+            T += (int64_t)__popcll(pmask) - (int64_t)__popcll(ml);
         } else {
             const uint32_t xo = L.xo[buf][64 * w + lane];
             const int32_t c = L.cn[buf][64 * w + lane];
             const bool small = nowrap && !(flags & 1u);
+            const bool ones = nowrap && !(flags & 4u);      // every acquireCount is 1: scalar candidates
             // in-window exit of each entry lane: bit position, or 64
             const uint32_t inpos = (xo != XO_NONE && xo - q < 64u && xo > q + (uint32_t)lane) ? xo - q : 64u;
             const bool ent = (me >> lane) & 1ull;
             int cursor = 0;
             while (cursor < 64) {
                 unsigned long long fm = 0;
-                if (small) {
+                if (ones) {
+                    fm = IM - T > 0 ? me : 0ull;
+                } else if (small) {
                     // without int wrap (int)(T + c) <= count  <=>  c <= floor(count) - T
                     const int64_t room = IM - T;
                     if (room >= THR_CSMALL) fm = me;
@@ -259,14 +339,15 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
             bool fm2 = false;
             if (mk) fm2 = thr_mark_exit(L, lxfar, xo, q, lo);
             far_marked |= __ballot(fm2) != 0;
-            if (lane == 0) {
-                const uint32_t sh = q & 63;
-                atomicOr(pbits + (q >> 6), pmask << sh);
-                if (sh) atomicOr(pbits + (q >> 6) + 1, pmask >> (64 - sh));
-            }
+            if ((uint32_t)lane == w) pst = pmask;          // pass bits staged: lane w <-> window w
         }
         if (lane == 0) L.lx[slot] = 0ull;                  // consumed: reused LX_WORDS windows later
         w++;
+    }
+    if (pst) {                                             // the chunk's pass bits: one vector step
+        const uint32_t q = q0 + 64u * (uint32_t)lane, sh = q & 63;
+        atomicOr(pbits + (q >> 6), pst << sh);
+        if (sh) atomicOr(pbits + (q >> 6) + 1, pst >> (64 - sh));
     }
     if (far_marked) {                                      // far exits must be in HBM before a loader reads them
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
@@ -316,8 +397,29 @@ __device__ __forceinline__ uint32_t lds_first_ge(const int64_t* tsb, uint32_t a,
     return m ? a + (uint32_t)(__ffsll((long long)m) - 1) : n;
 }
 
+// Passes of the deciding wave, staged one per lane and written 64 at a time:
+// one vector atomic into the pass bits and one scattered store of the waits
+// (instead of single-lane memory ops on the serial chain).
+struct PassStage {
+    unsigned long long* pbits; int32_t* wait; uint32_t n;
+    uint32_t spos; int32_t sw;
+    __device__ __forceinline__ void flush() {
+        const uint32_t k = n & 63u;
+        if ((threadIdx.x & 63u) < (k ? k : 64u)) {
+            atomicOr(pbits + (spos >> 6), 1ull << (spos & 63));
+            wait[spos] = sw;
+        }
+    }
+    __device__ __forceinline__ void push(uint32_t pos, int32_t w) {
+        if ((threadIdx.x & 63u) == (n & 63u)) { spos = pos; sw = w; }
+        n++;
+        if ((n & 63u) == 0) flush();
+    }
+    __device__ __forceinline__ void finish() { if (n & 63u) flush(); }
+};
+
 __device__ __forceinline__ void rl_decide_chunk(const int64_t* tsb, const int32_t* cb, uint32_t q0, uint32_t hi,
-                                                const DevRule& rule, int64_t cost1, int64_t& L, ItemWriter& iw) {
+                                                const DevRule& rule, int64_t cost1, int64_t& L, PassStage& iw) {
     const int lane = (int)(threadIdx.x & 63);
     const uint32_t n = min(hi - q0, (uint32_t)HS_CH);
     uint32_t p = 0;
@@ -325,39 +427,39 @@ __device__ __forceinline__ void rl_decide_chunk(const int64_t* tsb, const int32_
         // cost(c) >= cost(1) for c >= 1: nothing before this time can pass
         p = lds_first_ge(tsb, p, n, L + cost1 - rule.max_queue_ms);
         if (p >= n) break;
+        // 64 events into registers; L only grows, so an event that is not a
+        // candidate now never becomes one: the window is settled in one visit
         const uint32_t k = p + (uint32_t)lane;
-        bool cand = false;
-        if (k < n) {
-            const int32_t c = cb[k];
-            if (c > 0) {
-                const int64_t cost = c == 1 ? cost1 : j_round(1.0 * c / rule.count * 1000);
-                cand = tsb[k] >= L + cost - rule.max_queue_ms;
-            }
+        const int32_t c = k < n ? cb[k] : 0;
+        const int64_t t = k < n ? tsb[k] : 0;
+        const int64_t cost = c == 1 ? cost1 : (c > 0 ? j_round(1.0 * c / rule.count * 1000) : 0);
+        int from = 0;
+        while (true) {
+            const unsigned long long m = __ballot(c > 0 && lane >= from && t >= L + cost - rule.max_queue_ms);
+            if (!m) break;
+            const int jj = __ffsll((long long)m) - 1;
+            const int64_t cj = uniform64_at(cost, jj), tj = uniform64_at(t, jj);
+            int32_t wait = 0;
+            if (L + cj <= tj) L = tj;                           // expectedTime <= currentTime
+            else { L += cj; wait = (int32_t)(L - tj); }         // queued: sleep(wait), then pass
+            iw.push(q0 + p + (uint32_t)jj, wait);
+            from = jj + 1;
         }
-        const unsigned long long m = __ballot(cand);
-        if (!m) { p += 64; continue; }
-        const uint32_t jj = p + (uint32_t)(__ffsll((long long)m) - 1);
-        const int32_t cj = cb[jj];
-        const int64_t cost = cj == 1 ? cost1 : j_round(1.0 * cj / rule.count * 1000);
-        const int64_t t = tsb[jj];
-        int32_t wait = 0;
-        if (L + cost <= t) L = t;                           // expectedTime <= currentTime
-        else { L += cost; wait = (int32_t)(L - t); }        // queued: sleep(wait), then pass
-        iw.push(lane == 0, q0 + jj, q0 + jj + 1, wait);
-        p = jj + 1;
+        p += 64;
     }
 }
 
-__global__ void __launch_bounds__(HS_T) k_heavy_stream(DevState st, SegIO io, HeavyCtx hc, StreamCtx sc) {
-    __shared__ unsigned long long smem[HS_LDS_WORDS];
-    uint32_t s;
-    if (!stream_at(sc, blockIdx.x, &s)) return;
+__device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyCtx& hc, const StreamCtx& sc,
+                               uint32_t s, uint32_t b, unsigned long long* smem) {
     const uint64_t t_start = sc.sticks ? wall_clock64() : 0;
     const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1], res = hc.seg_res[s];
     const uint32_t r0 = st.rule_off[res];
     const DevRule rule = st.rules[r0];
     const bool wave0 = threadIdx.x < 64;
     const uint32_t nch = (hi - lo + HS_CH - 1) / HS_CH;
+    // the deciding wave is the serial chain: it wins issue arbitration on its
+    // SIMD against the memory-bound waves of the concurrent kernels
+    if (wave0) __builtin_amdgcn_s_setprio(3);
     if (hc.seg_mode[s] == SM_THREAD) {
         ThrLds& L = *reinterpret_cast<ThrLds*>(smem);
         for (uint32_t i = threadIdx.x; i < LX_WORDS; i += HS_T) L.lx[i] = 0ull;
@@ -396,7 +498,7 @@ __global__ void __launch_bounds__(HS_T) k_heavy_stream(DevState st, SegIO io, He
         int64_t* tsb = (int64_t*)smem;                           // [2][HS_CH]
         int32_t* cb = (int32_t*)(smem + 2 * HS_CH);              // [2][HS_CH]
         DevRuleState rs = st.rstate[r0];
-        ItemWriter iw{hc.item_lo, hc.item_hi, hc.item_wait, lo, 0};
+        PassStage iw{hc.passbits, io.v_wait, 0, 0, 0};
         if (rule.count > 0) {
             const int64_t cost1 = j_round(1.0 * 1 / rule.count * 1000);
             int64_t L = rs.latest_passed;
@@ -412,11 +514,36 @@ __global__ void __launch_bounds__(HS_T) k_heavy_stream(DevState st, SegIO io, He
                 if (more) rl_store(r, tsb + ((k + 1) & 1) * HS_CH, cb + ((k + 1) & 1) * HS_CH);
                 __syncthreads();
             }
+            if (wave0) iw.finish();
             rs.latest_passed = L;
         }
-        if (threadIdx.x == 0) { hc.n_items[s] = iw.n; st.rstate[r0] = rs; }
+        if (threadIdx.x == 0) st.rstate[r0] = rs;
     }
-    if (sc.sticks && threadIdx.x == 0) sc.sticks[blockIdx.x] = wall_clock64() - t_start;
+    if (sc.sticks && threadIdx.x == 0) {       // diagnostics: start (40 bits) and duration (24 bits)
+        const uint64_t d = wall_clock64() - t_start;
+        sc.sticks[b] = ((t_start & 0xffffffffffull) << 24) | (d < 0xffffffull ? d : 0xffffffull);
+    }
+    if (wave0) __builtin_amdgcn_s_setprio(0);
+}
+
+// Persistent: a grid sized to the chip takes the segments from a queue in
+// list order (longest first).  Launched ahead of the light lanes, its
+// workgroups hold their CU slots for the whole list instead of competing for
+// them one segment at a time.  Every workgroup leaves when the queue is
+// exhausted.
+__global__ void __launch_bounds__(HS_T) k_heavy_stream(DevState st, SegIO io, HeavyCtx hc, StreamCtx sc) {
+    __shared__ unsigned long long smem[HS_LDS_WORDS];
+    __shared__ uint32_t slot;
+    while (true) {
+        if (threadIdx.x == 0) slot = atomicAdd(sc.next, 1u);
+        __syncthreads();
+        const uint32_t b = slot;
+        __syncthreads();
+        uint32_t s;
+        if (!stream_at(sc, b, &s)) break;
+        stream_segment(st, io, hc, sc, s, b, smem);
+        __syncthreads();                            // LDS is reused by the next segment
+    }
 }
 
 }  // namespace sf

@@ -261,11 +261,12 @@ class FlowEngine:
         return s
 
     def heavy_profile(self, cap=1 << 20):
-        """Per heavy segment of the last submit: (resource, events, mode, microseconds)."""
+        """Per heavy segment of the last submit: (resource, events, mode, microseconds, start microseconds);
+        start is relative to the first k_heavy_stream segment (0 for k_heavy_decide segments)."""
         buf = (abi.sf_heavy_profile * cap)()
         n = C.c_uint32()
         _check(lib().sf_heavy_profile_read(self.h, buf, cap, C.byref(n)))
-        return [(b.resource, b.events, b.mode, b.ticks / 100.0) for b in buf[:n.value]]
+        return [(b.resource, b.events, b.mode, b.ticks / 100.0, b.start / 100.0) for b in buf[:n.value]]
 
     # ---- cluster token server (TokenService.requestToken / requestParamToken)
     def load_namespaces(self, ns):

@@ -150,8 +150,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     const uint32_t ns = (uint32_t)seg_start.size();
     seg_start.push_back(n);
     std::vector<uint8_t> mode(ns);
-    std::vector<uint32_t> ilo(n), ihi(n), nitems(ns), hwb(ns), secb(ns), nhw(ns), nsec(ns);
-    std::vector<int32_t> iwait(n);
+    std::vector<uint32_t> hwb(ns), secb(ns), nhw(ns), nsec(ns);
     std::vector<int64_t> hw0(ns), sec0(ns);
     std::vector<Acc> acc_hw, acc_sec;
     for (uint32_t s = 0; s < ns; s++) {
@@ -170,8 +169,8 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         }
     }
     std::vector<unsigned long long> passbits(n / 64 + 2, 0ull);
-    HeavyCtx hc{seg_start.data(), seg_res.data(), mode.data(), nullptr, nullptr, 0u, pcg.data(), ilo.data(), ihi.data(),
-                iwait.data(), nitems.data(), acc_hw.data(), acc_sec.data(), hwb.data(), secb.data(), hw0.data(), sec0.data(),
+    HeavyCtx hc{seg_start.data(), seg_res.data(), mode.data(), nullptr, nullptr, 0u, pcg.data(),
+                acc_hw.data(), acc_sec.data(), hwb.data(), secb.data(), hw0.data(), sec0.data(),
                 nullptr, passbits.data()};
     for (uint32_t s = 0; s < ns; s++) {
         uint32_t lo = seg_start[s], hi = seg_start[s + 1], res = seg_res[s];
@@ -184,7 +183,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
             break;
         case SM_RL: heavy_rl(tm, e->st, io, hc, s, res, lo, hi); break;
         case SM_THREAD: heavy_thread(tm, e->st, io, hc, s, res, lo, hi, nullptr, nullptr); break;
-        case SM_NORULE: ilo[lo] = lo; ihi[lo] = hi; iwait[lo] = 0; nitems[s] = 1; break;
+        case SM_NORULE: break;                    // every entry passes (fill)
         default:
             if (e->st.S <= 2) decide_segment<2>(e->st, io, res, lo, hi);
             else decide_segment<SF_MAX_SAMPLE_COUNT>(e->st, io, res, lo, hi);
@@ -194,8 +193,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     for (uint32_t s = 0; s < ns; s++) {
         if (mode[s] < SM_QPS) continue;
         for (uint32_t j = seg_start[s]; j < seg_start[s + 1]; j++) {
-            const bool thr = mode[s] == SM_THREAD;
-            EvContrib c = heavy_event(hc, io, seg_start[s], nitems[s], j, thr);
+            EvContrib c = heavy_event(hc, io, seg_start[s], mode[s], j);
             vs[j] = c.status; vw[j] = c.wait; vr[j] = 0;
             if (!c.touch) continue;
             for (int t = 0; t < 2; t++) {
