@@ -233,7 +233,7 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     w.seg_cap = (uint32_t)SC;
     DALLOC(w.segflag, SC * 4); DALLOC(w.seg_mode, SC); DALLOC(w.light_list, SC * 4); DALLOC(w.heavy_list, SC * 4);
     DALLOC(w.counters, 16 * 4); DALLOC(w.pcg, N * 8);
-    w.fill_tile_cap = (uint32_t)(N / FILL_TILE + N / (w.heavy_min + 1) + 2);
+    w.fill_tile_cap = (uint32_t)(N / FILL_TILE + 2 * (N / (w.heavy_min + 1)) + 2);   // <= len/TILE + 2 per segment
     DALLOC(w.fill_tiles, (size_t)2 * w.fill_tile_cap * sizeof(uint2)); DALLOC(w.fill_ntiles, 2 * 4);
     w.acc_cap = (uint32_t)std::min<size_t>(std::max<size_t>(N / w.heavy_min * 64, 1 << 16), 1u << 24);
     DALLOC(w.acc_hw, (size_t)w.acc_cap * ACC_BYTES); DALLOC(w.acc_sec, (size_t)w.acc_cap * ACC_BYTES);

@@ -101,7 +101,7 @@ struct EntryAcc {
 // 16-B radix-sort payload of one event (batch time span < 2^32 ms)
 struct alignas(16) PackedEv { uint32_t idx, dts; int32_t cnt; uint32_t flags; };
 
-constexpr uint32_t FILL_TILE = 4096;             // events per k_heavy_fill tile (256 threads x 16)
+constexpr uint32_t FILL_TILE = 2048;             // events per k_heavy_fill tile (256 threads x 8)
 
 // Sorted-order working buffers of one batch.
 struct Work {

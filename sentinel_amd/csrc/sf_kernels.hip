@@ -273,6 +273,11 @@ struct PAcc {            // per-thread partial of one accumulator slot
         } else if (e.passed) { pass += (unsigned long long)e.c; n_pass++; }
         else block += (unsigned long long)e.c;
     }
+    __device__ void merge(const PAcc& o) {
+        pass += o.pass; block += o.block; succ += o.succ; rt += o.rt; exc += o.exc;
+        n_pass += o.n_pass; n_exit += o.n_exit; n_touch += o.n_touch;
+        if (o.min_rt < min_rt) min_rt = o.min_rt;
+    }
     __device__ void flush(Acc* table, uint32_t key) const {
         if (!n_touch) return;
         Acc* a = table + key;
@@ -309,8 +314,49 @@ __device__ void wave_flush(PAcc& p, uint32_t key, Acc* table) {
     if ((int)(threadIdx.x & 63) == l0) r.flush(table, k0);
 }
 
-constexpr int FILL_ITERS = FILL_TILE / 256;
-static_assert(FILL_ITERS * 256 == (int)FILL_TILE, "a fill tile is 256 threads x FILL_ITERS events");
+// workgroup flush: the waves' partials of one key are merged in LDS first,
+// so a hot window row takes one set of atomics per workgroup
+struct PAccSlot { PAcc p; uint32_t key; };
+__device__ void block_flush(PAcc& p, uint32_t key, Acc* table, PAccSlot* lds) {
+    const uint32_t NONE = 0xffffffffu;
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6), nw = (int)(blockDim.x >> 6);
+    bool act = key != NONE && p.n_touch;
+    const unsigned long long m = __ballot(act);
+    uint32_t k0 = NONE;
+    bool uni = false;
+    if (m) {
+        const int l0 = __ffsll((long long)m) - 1;
+        k0 = __shfl(key, l0);
+        uni = __ballot(act && key != k0) == 0;
+    }
+    if (m && !uni) { if (act) p.flush(table, key); }      // mixed keys: lane atomics
+    PAcc r; r.clear();
+    if (m && uni) {
+        if (!act) p.clear();
+        r.pass = wave_sum(p.pass); r.block = wave_sum(p.block); r.succ = wave_sum(p.succ); r.rt = wave_sum(p.rt);
+        r.exc = wave_sum(p.exc); r.n_pass = wave_sum(p.n_pass); r.n_exit = wave_sum(p.n_exit);
+        r.n_touch = wave_sum(p.n_touch); r.min_rt = wave_min(p.min_rt);
+    }
+    if (lane == 0) { lds[wv].p = r; lds[wv].key = (m && uni) ? k0 : NONE; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int a = 0; a < nw; a++) {
+            if (lds[a].key == NONE) continue;
+            PAcc acc = lds[a].p;
+            for (int b = a + 1; b < nw; b++) {
+                if (lds[b].key != lds[a].key) continue;
+                const PAcc& o = lds[b].p;
+                acc.pass += o.pass; acc.block += o.block; acc.succ += o.succ; acc.rt += o.rt; acc.exc += o.exc;
+                acc.n_pass += o.n_pass; acc.n_exit += o.n_exit; acc.n_touch += o.n_touch;
+                if (o.min_rt < acc.min_rt) acc.min_rt = o.min_rt;
+                lds[b].key = NONE;
+            }
+            acc.flush(table, lds[a].key);
+        }
+    }
+    __syncthreads();
+}
+
 
 // Tiles of FILL_TILE events over the heavy segments of each class (block c:
 // class c): cls 0 = k_heavy_decide's list (QPS / WarmUp / no rule; generic
@@ -331,7 +377,8 @@ __global__ void __launch_bounds__(1024) k_fill_tiles(HeavyCtx hc, StreamCtx sc, 
         uint32_t s = 0, nt = 0;
         if (i < nl) {
             const bool ok = c == 0 ? heavy_at(hc, i, &s) : stream_at(sc, i, &s);
-            if (ok && hc.seg_mode[s] >= SM_QPS) nt = (hc.seg_start[s + 1] - hc.seg_start[s] + FILL_TILE - 1) / FILL_TILE;
+            if (ok && hc.seg_mode[s] >= SM_QPS)                 // aligned FILL_TILE blocks the segment overlaps
+                nt = (hc.seg_start[s + 1] - 1) / FILL_TILE - hc.seg_start[s] / FILL_TILE + 1;
         }
         const uint32_t incl = (uint32_t)wave_scan_add((int)nt);
         if (lane == 63) wsum[wv] = incl;
@@ -339,7 +386,8 @@ __global__ void __launch_bounds__(1024) k_fill_tiles(HeavyCtx hc, StreamCtx sc, 
         uint32_t before = carry;
         for (int k = 0; k < wv; k++) before += wsum[k];
         const uint32_t base = before + incl - nt;
-        for (uint32_t k = 0; k < nt && base + k < cap; k++) out[base + k] = make_uint2(s, k);
+        const uint32_t g0 = nt ? hc.seg_start[s] / FILL_TILE : 0;
+        for (uint32_t k = 0; k < nt && base + k < cap; k++) out[base + k] = make_uint2(s, g0 + k);
         __syncthreads();
         if (threadIdx.x == 1023) carry = before + incl;
         __syncthreads();
@@ -347,55 +395,191 @@ __global__ void __launch_bounds__(1024) k_fill_tiles(HeavyCtx hc, StreamCtx sc, 
     if (threadIdx.x == 0) ntiles[c] = min(carry, cap);
 }
 
-// Verdicts and per-window counter deltas of the heavy segments of one class,
-// one FILL_TILE-event tile of one segment at a time (persistent grid): the
-// segment's parameters are uniform per tile, every event is one pass-bit
-// lookup (its entry's bit for an exit).
+// Verdicts and per-window counter deltas of the heavy segments of one class.
+// A tile is one segment's part of an aligned FILL_TILE-event block of the
+// sorted batch; lane t owns the aligned group of 16 events at block + 16 t, so
+// every array is read and written with 16-byte vector accesses (groups cut by
+// a segment edge fall back to per-event accesses) and all of a lane's loads
+// are in flight together.  Each event is one pass-bit lookup (its entry's bit
+// for an exit).  Persistent grid, each workgroup a contiguous run of tiles; a
+// thread's partial sums carry across the run while the window row repeats.
+constexpr int FG = (int)FILL_TILE / 256;         // events per lane
+struct FillGrp { uint8_t f[FG]; int32_t c[FG]; int64_t t[FG]; };
+
+// vector copy of an aligned group: 16-byte accesses (8-byte for an 8-byte group)
+__device__ __forceinline__ void load16(void* dst, const void* src, int bytes) {
+    if (bytes == 8) { *(uint2*)dst = *(const uint2*)src; return; }
+    uint4* d = (uint4*)dst; const uint4* q = (const uint4*)src;
+#pragma unroll
+    for (int k = 0; k < bytes / 16; k++) d[k] = q[k];
+}
+__device__ __forceinline__ void store16(void* dst, const void* src, int bytes) {
+    if (bytes == 8) { *(uint2*)dst = *(const uint2*)src; return; }
+    uint4* d = (uint4*)dst; const uint4* q = (const uint4*)src;
+#pragma unroll
+    for (int k = 0; k < bytes / 16; k++) d[k] = q[k];
+}
+
 __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, HeavyCtx hc, const uint2* tiles,
                                                     const uint32_t* ntiles, int cls) {
+    __shared__ PAccSlot lds_h[4], lds_s[4];
     const uint32_t NONE = 0xffffffffu;
     const uint32_t nt = ntiles[cls];
     const uint32_t wl = (uint32_t)st.wl;
-    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const uint32_t tb = (uint32_t)((uint64_t)nt * blockIdx.x / gridDim.x);
+    const uint32_t te = (uint32_t)((uint64_t)nt * (blockIdx.x + 1) / gridDim.x);
+    PAcc ph, ps; ph.clear(); ps.clear();
+    uint32_t kh = NONE, ks = NONE;
+    for (uint32_t t = tb; t < te; t++) {
         const uint2 tl = tiles[t];
         const uint32_t s = tl.x;
         const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1];
         const uint8_t mode = hc.seg_mode[s];
-        const uint32_t j0 = lo + tl.y * FILL_TILE, j1 = min(j0 + FILL_TILE, hi);
+        const bool all = mode == SM_NORULE, rl = mode == SM_RL;
         const uint32_t hwb = hc.acc_hw_base[s], secb = hc.acc_sec_base[s];
         const int64_t hw0 = hc.seg_hw0[s], sec0 = hc.seg_sec0[s];
         const int64_t bh = hw0 * st.wl, bs = sec0 * 1000;
         const bool rel32 = io.ts[hi - 1] - bs < (int64_t)0xffffffffLL;   // window keys by 32-bit division
-        PAcc ph, ps; ph.clear(); ps.clear();
-        uint32_t kh = NONE, ks = NONE;
-        for (int it = 0; it < FILL_ITERS; it++) {
-            const uint32_t j = j0 + (uint32_t)(it * 256) + threadIdx.x;
-            if (j >= j1) break;
-            if (io.eref && !is_entry(io.flags[j])) {
-                const int64_t r = io.eref[j];
-                if (r >= 0 && (r < (int64_t)lo || r >= (int64_t)j || !is_entry(io.flags[r]))) *st.err = SF_ERR_INVALID;
+        const uint32_t base = tl.y * FILL_TILE + (uint32_t)FG * threadIdx.x;
+        const uint32_t a = max(base, lo), b = min(base + (uint32_t)FG, hi);
+        if (a >= b) continue;
+        const bool full = a == base && b == base + (uint32_t)FG;
+        FillGrp g;
+        int32_t wt[FG];
+        if (full) {
+            load16(g.f, io.flags + base, FG); load16(g.c, io.cnt + base, FG * 4); load16(g.t, io.ts + base, FG * 8);
+            if (rl) load16(wt, io.v_wait + base, FG * 4);
+        } else {
+#pragma unroll
+            for (int k = 0; k < FG; k++) {
+                const uint32_t j = base + (uint32_t)k;
+                const bool in = j >= a && j < b;
+                g.f[k] = in ? io.flags[j] : (uint8_t)0;
+                g.c[k] = in ? io.cnt[j] : 0;
+                g.t[k] = in ? io.ts[j] : 0;
+                wt[k] = (in && rl) ? io.v_wait[j] : 0;
             }
-            const EvContrib e = heavy_event(hc, io, lo, mode, j);
-            io.v_status[j] = e.status;
-            if (io.v_wait) io.v_wait[j] = e.wait;
-            if (io.v_rule) io.v_rule[j] = 0;
-            if (!e.touch) continue;
-            const int64_t tj = io.ts[j];
-            uint32_t key_h, key_s;
-            if (rel32) {
-                key_h = hwb + (uint32_t)(tj - bh) / wl;
-                key_s = secb + (uint32_t)(tj - bs) / 1000u;
-            } else {
-                key_h = hwb + (uint32_t)(tj / st.wl - hw0);
-                key_s = secb + (uint32_t)(tj / 1000 - sec0);
-            }
-            if (key_h != kh) { if (kh != NONE) ph.flush(hc.acc_hw, kh); ph.clear(); kh = key_h; }
-            if (key_s != ks) { if (ks != NONE) ps.flush(hc.acc_sec, ks); ps.clear(); ks = key_s; }
-            ph.add(e); ps.add(e);
         }
-        wave_flush(ph, kh, hc.acc_hw);
-        wave_flush(ps, ks, hc.acc_sec);
+        const unsigned long long pw = hc.passbits[base >> 6];
+        const uint32_t bits = all ? 0xffffu : (uint32_t)(pw >> (base & 63)) & ((1u << FG) - 1u);
+        // exits: their entries' bits and times (gathers, all issued together)
+        uint32_t exm = 0;
+#pragma unroll
+        for (int k = 0; k < FG; k++)
+            if (base + (uint32_t)k >= a && base + (uint32_t)k < b && (g.f[k] & SF_EV_EXIT)) exm |= 1u << k;
+        int64_t rf[FG], rts[FG]; uint32_t rlive = 0;
+        if (exm) {
+            if (io.eref) {
+                if (full) load16(rf, io.eref + base, FG * 8);
+                else {
+#pragma unroll
+                    for (int k = 0; k < FG; k++) rf[k] = ((exm >> k) & 1u) ? io.eref[base + k] : -1;
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < FG; k++) rf[k] = -1;
+            }
+            unsigned long long rw[FG]; uint8_t rfl[FG];
+#pragma unroll
+            for (int k = 0; k < FG; k++) {
+                const int64_t r = ((exm >> k) & 1u) ? rf[k] : -1;
+                const uint32_t rc = r >= 0 && r < (int64_t)io.n ? (uint32_t)r : base;
+                rw[k] = hc.passbits[rc >> 6];
+                rts[k] = r >= 0 ? io.ts[rc] : (io.cts ? io.cts[base + k] : g.t[k]);
+                rfl[k] = io.flags[rc];
+            }
+#pragma unroll
+            for (int k = 0; k < FG; k++) {
+                if (!((exm >> k) & 1u)) continue;
+                const int64_t r = rf[k];
+                const uint32_t j = base + (uint32_t)k;
+                if (r >= 0 && (r < (int64_t)lo || r >= (int64_t)j || !is_entry(rfl[k]))) *st.err = SF_ERR_INVALID;
+                const bool live = r < 0 || (r >= (int64_t)lo && r < (int64_t)j &&
+                                            (all || ((rw[k] >> ((uint32_t)r & 63)) & 1ull)));
+                if (live) rlive |= 1u << k;
+            }
+        }
+        // verdicts and the group's contribution
+        uint8_t vs[FG]; int32_t vw[FG]; uint16_t vr[FG];
+        PAcc gp; gp.clear();
+#pragma unroll
+        for (int k = 0; k < FG; k++) {
+            const uint32_t j = base + (uint32_t)k;
+            vr[k] = 0; vw[k] = 0; vs[k] = 0;
+            if (j < a || j >= b) continue;
+            EvContrib e{};
+            e.c = g.c[k];
+            if (!(g.f[k] & SF_EV_EXIT)) {
+                e.passed = (bits >> k) & 1u;
+                e.wait = (rl && e.passed) ? wt[k] : 0;
+                e.status = e.passed ? (e.wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : SF_V_BLOCK_FLOW;
+                e.touch = true;
+            } else {
+                e.live_exit = (rlive >> k) & 1u;
+                e.status = e.live_exit ? SF_V_EXIT : SF_V_EXIT_IGNORED;
+                e.touch = e.live_exit;
+                e.rt = g.t[k] - rts[k];
+                e.err = (g.f[k] & SF_EV_ERROR) != 0;
+            }
+            vs[k] = e.status; vw[k] = e.wait;
+            if (e.touch) gp.add(e);
+        }
+        if (full) {
+            store16(io.v_status + base, vs, FG);
+            if (io.v_wait) store16(io.v_wait + base, vw, FG * 4);
+            if (io.v_rule) store16(io.v_rule + base, vr, FG * 2);
+        } else {
+#pragma unroll
+            for (int k = 0; k < FG; k++) {
+                const uint32_t j = base + (uint32_t)k;
+                if (j < a || j >= b) continue;
+                io.v_status[j] = vs[k];
+                if (io.v_wait) io.v_wait[j] = vw[k];
+                if (io.v_rule) io.v_rule[j] = 0;
+            }
+        }
+        if (!gp.n_touch) continue;
+        // window rows of the group's first and last event (time-sorted): usually one
+        auto key_of = [&](int64_t tj, uint32_t& kh_, uint32_t& ks_) {
+            if (rel32) { kh_ = hwb + (uint32_t)(tj - bh) / wl; ks_ = secb + (uint32_t)(tj - bs) / 1000u; }
+            else { kh_ = hwb + (uint32_t)(tj / st.wl - hw0); ks_ = secb + (uint32_t)(tj / 1000 - sec0); }
+        };
+        int64_t tfirst = 0, tlast = 0;                    // unrolled selects (no dynamic register indexing)
+#pragma unroll
+        for (int k = 0; k < FG; k++) {
+            if (base + (uint32_t)k == a) tfirst = g.t[k];
+            if (base + (uint32_t)k + 1 == b) tlast = g.t[k];
+        }
+        uint32_t h0, s0, h1, s1;
+        key_of(tfirst, h0, s0);
+        key_of(tlast, h1, s1);
+        if (h0 == h1 && s0 == s1) {
+            if (h0 != kh) { if (kh != NONE) ph.flush(hc.acc_hw, kh); ph.clear(); kh = h0; }
+            if (s0 != ks) { if (ks != NONE) ps.flush(hc.acc_sec, ks); ps.clear(); ks = s0; }
+            ph.merge(gp); ps.merge(gp);
+        } else {
+#pragma unroll
+            for (int k = 0; k < FG; k++) {
+                const uint32_t j = base + (uint32_t)k;
+                if (j < a || j >= b) continue;
+                EvContrib e{};
+                e.c = g.c[k];
+                if (!(g.f[k] & SF_EV_EXIT)) { e.passed = (bits >> k) & 1u; e.touch = true; }
+                else {
+                    e.live_exit = (rlive >> k) & 1u; e.touch = e.live_exit;
+                    e.rt = g.t[k] - rts[k]; e.err = (g.f[k] & SF_EV_ERROR) != 0;
+                }
+                if (!e.touch) continue;
+                uint32_t kh_, ks_;
+                key_of(g.t[k], kh_, ks_);
+                if (kh_ != kh) { if (kh != NONE) ph.flush(hc.acc_hw, kh); ph.clear(); kh = kh_; }
+                if (ks_ != ks) { if (ks != NONE) ps.flush(hc.acc_sec, ks); ps.clear(); ks = ks_; }
+                ph.add(e); ps.add(e);
+            }
+        }
     }
+    block_flush(ph, kh, hc.acc_hw, lds_h);
+    block_flush(ps, ks, hc.acc_sec, lds_s);
 }
 
 __global__ void k_heavy_apply(DevState st, HeavyCtx hc, StreamCtx sc, const uint32_t* seg_nhw,
