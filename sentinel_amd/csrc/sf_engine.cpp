@@ -119,7 +119,7 @@ void sf_destroy(sf_engine* e) {
                     e->w.seg_start, e->w.seg_res, e->w.n_seg, e->w.s_ts, e->w.s_cnt, e->w.s_flags, e->w.s_eref,
                     e->w.s_cts, e->w.s_nargs, e->w.s_atag, e->w.s_abits, e->w.inv, e->w.v_status, e->w.v_wait,
                     e->w.v_rule, e->w.sort_tmp, e->w.scan_tmp, e->stage_in, e->stage_out,
-                    e->w.segflag, e->w.seg_mode, e->w.light_list, e->w.heavy_list, e->w.counters, e->w.pcg,
+                    e->w.segflag, e->w.seg_mode, e->w.light_list, e->w.lcounts, e->w.heavy_list, e->w.counters, e->w.pcg,
                     e->w.pscan_tmp, e->w.fill_tiles, e->w.fill_ntiles, e->w.acc_hw,
                     e->w.acc_sec, e->w.acc_hw_base, e->w.acc_sec_base, e->w.seg_hw0, e->w.seg_sec0,
                     e->w.seg_nhw, e->w.seg_nsec, e->w.hticks, e->w.passbits, e->w.stream_list, e->w.sticks,
@@ -231,7 +231,17 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     }
     const size_t SC = std::min<size_t>(N, R) + 1;
     w.seg_cap = (uint32_t)SC;
-    DALLOC(w.segflag, SC * 4); DALLOC(w.seg_mode, SC); DALLOC(w.light_list, SC * 4); DALLOC(w.heavy_list, SC * 4);
+    DALLOC(w.segflag, SC * 4); DALLOC(w.seg_mode, SC); DALLOC(w.lcounts, LCLS * 4);
+    {   // light_list regions per length class: class c holds segments of >= lo_len(c) events
+        size_t off = 0;
+        for (int c = 0; c < LCLS; c++) {
+            const size_t lo_len = c == 0 ? 1 : (c == 1 ? 2 : ((size_t)1 << (c - 1)) + 1);
+            const size_t cap = lo_len > w.heavy_min ? 0 : std::min<size_t>(SC, N / lo_len + 1);
+            w.loff[c] = (uint32_t)off;
+            off += cap;
+        }
+        DALLOC(w.light_list, off * 4);
+    } DALLOC(w.heavy_list, SC * 4);
     DALLOC(w.counters, 16 * 4); DALLOC(w.pcg, N * 8);
     w.fill_tile_cap = (uint32_t)(N / FILL_TILE + 2 * (N / (w.heavy_min + 1)) + 2);   // <= len/TILE + 2 per segment
     DALLOC(w.fill_tiles, (size_t)2 * w.fill_tile_cap * sizeof(uint2)); DALLOC(w.fill_ntiles, 2 * 4);
@@ -886,6 +896,7 @@ int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uin
     if (!e || !n_out || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> g(e->mu);
     uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0}, nseg = 0;
+    HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
     HIP_TRY(hipStreamSynchronize(e->stream3));
     HIP_TRY(hipMemcpy(cnt, e->w.counters, sizeof cnt, hipMemcpyDeviceToHost));

@@ -101,6 +101,14 @@ struct EntryAcc {
 // 16-B radix-sort payload of one event (batch time span < 2^32 ms)
 struct alignas(16) PackedEv { uint32_t idx, dts; int32_t cnt; uint32_t flags; };
 
+// light segments are listed by length class (len 1, 2, 3-4, 5-8, ...) so the
+// lanes of a wavefront interpret segments of similar length
+constexpr int LCLS = 16;
+__host__ __device__ inline int light_class(uint32_t len) {
+    if (len <= 1) return 0;
+    const int c = 32 - __builtin_clz(len - 1);
+    return c < LCLS - 1 ? c : LCLS - 1;
+}
 constexpr uint32_t FILL_TILE = 2048;             // events per k_heavy_fill tile (256 threads x 8)
 
 // Sorted-order working buffers of one batch.
@@ -122,7 +130,9 @@ struct Work {
     // heavy / light split (sf_heavy.h)
     uint32_t seg_cap;                                   // min(max_batch, R)
     uint32_t* segflag; uint8_t* seg_mode;
-    uint32_t* light_list; uint32_t* heavy_list; uint32_t* counters;   // [0] n_light [1] n_heavy front [2] hw slots [3] sec slots [4] n_heavy back
+    uint32_t* light_list; uint32_t* heavy_list; uint32_t* counters;
+    uint32_t* lcounts;                                  // [LCLS] light segments per length class
+    uint32_t loff[LCLS];                                // light_list region of each length class   // [0] n_light [1] n_heavy front [2] hw slots [3] sec slots [4] n_heavy back
                                                                       // [5] n_stream front [6] n_stream back
     int64_t* pcg; void* pscan_tmp; size_t pscan_tmp_bytes;
     uint2* fill_tiles; uint32_t fill_tile_cap;         // [2][cap] (segment, tile) of each class for k_heavy_fill

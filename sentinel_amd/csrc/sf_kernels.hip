@@ -162,8 +162,17 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     uint32_t lo = 0, hi = 0, res = 0;
     if (valid) { lo = w.seg_start[s]; hi = w.seg_start[s + 1]; res = w.seg_res[s]; }
     const bool light = valid && hi - lo <= w.heavy_min;
-    const uint32_t lpos = wave_append(&w.counters[0], light);
-    if (light) { w.seg_mode[s] = SM_LIGHT; w.light_list[lpos] = s; }
+    // light list slot: workgroup histogram of the length classes in LDS, one
+    // global atomic per class and workgroup
+    __shared__ uint32_t hcnt[LCLS], hbase[LCLS];
+    if (threadIdx.x < LCLS) hcnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int lc = light ? light_class(hi - lo) : -1;
+    const uint32_t lrank = lc >= 0 ? atomicAdd(&hcnt[lc], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < LCLS) hbase[threadIdx.x] = hcnt[threadIdx.x] ? atomicAdd(&w.lcounts[threadIdx.x], hcnt[threadIdx.x]) : 0u;
+    __syncthreads();
+    if (light) { w.seg_mode[s] = SM_LIGHT; w.light_list[w.loff[lc] + hbase[lc] + lrank] = s; }
     const bool heavy = valid && !light;
     if (!__ballot(heavy)) return;
     uint8_t mode = SM_GENERIC;
@@ -215,13 +224,23 @@ __device__ __forceinline__ bool heavy_at(const HeavyCtx& hc, uint32_t b, uint32_
     return false;
 }
 
+struct LightLists { const uint32_t* list; const uint32_t* counts; uint32_t off[LCLS]; };
+
+// One lane per light segment; thread t walks the length classes from the
+// longest down, so a wavefront holds segments of one class (similar length)
+// and the long ones are dispatched first.
 template <int MAXS>
 __global__ void __launch_bounds__(128) k_decide_light(DevState st, SegIO io, const uint32_t* seg_start,
-                                                      const uint32_t* seg_res, const uint32_t* list,
-                                                      const uint32_t* count) {
+                                                      const uint32_t* seg_res, LightLists ll) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= *count) return;
-    uint32_t s = list[t];
+    int c = LCLS - 1;
+    for (; c >= 0; c--) {
+        const uint32_t n = ll.counts[c];
+        if (t < n) break;
+        t -= n;
+    }
+    if (c < 0) return;
+    const uint32_t s = ll.list[ll.off[c] + t];
     decide_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
 }
 
@@ -677,11 +696,12 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     e = rocprim::inclusive_scan(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n, rocprim::plus<int64_t>(), s);
     if (e != hipSuccess) return e;
     hipMemsetAsync(w.counters, 0, 8 * sizeof(uint32_t), s);
+    hipMemsetAsync(w.lcounts, 0, LCLS * sizeof(uint32_t), s);
     hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
     hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
     const uint32_t max_seg = n < st.R ? n : st.R;
     if (timing) hipEventRecord(ev[10], s);
-    hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, T)), dim3(T), 0, s, st, w, w.s_ts);
+    hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, 1024)), dim3(1024), 0, s, st, w, w.s_ts);
     if (timing) hipEventRecord(ev[2], s);
 
     SegIO io;
@@ -718,12 +738,14 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s, st, hc, sc, w.seg_nhw, w.seg_nsec, 1);
 
     const unsigned TD = 128;
+    LightLists ll{w.light_list, w.lcounts, {}};
+    for (int c = 0; c < LCLS; c++) ll.off[c] = w.loff[c];
     if (st.S <= 2)
         hipLaunchKernelGGL(k_decide_light<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
-                           w.seg_res, w.light_list, w.counters);
+                           w.seg_res, ll);
     else
         hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
-                           w.seg_start, w.seg_res, w.light_list, w.counters);
+                           w.seg_start, w.seg_res, ll);
     hipEventRecord(ev[9], s3);                     // light done (also the join of C)
     hipEventRecord(ev[6], s2);                     // join B and C
     hipStreamWaitEvent(s, ev[6], 0);
