@@ -47,6 +47,13 @@ __device__ __forceinline__ bool stream_at(const StreamCtx& sc, uint32_t b, uint3
     return false;
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not
+// for its outstanding global stores and atomics (the pass bits are read by
+// later kernels; far live exits are fenced explicitly where they are written).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ------------------------------------------------------------------ THREAD
 // DefaultController, FLOW_GRADE_THREAD (DefaultController.java:50-89,
 // StatisticSlot.java:64-65,157): an entry passes iff (int)(curThreadNum +
@@ -245,6 +252,9 @@ __device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) 
     return ((unsigned long long)b << 32) | a;
 }
 
+#ifdef SF_STREAM_PROF
+__device__ uint64_t thr_prof[3];
+#endif
 __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32_t q0, uint32_t lo, uint32_t hi,
                            double M, int64_t IM, int64_t& T, unsigned long long* pbits) {
     const int lane = (int)(threadIdx.x & 63);
@@ -256,27 +266,39 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
     const unsigned long long r_ent = L.win[buf][wl].ent;
     const int32_t r_maxrc = L.win[buf][wl].maxrc;
     const uint32_t r_flags = L.win[buf][wl].flags;
+    const unsigned long long r_inw = L.win[buf][wl].inw;
+    const unsigned long long bigm = __ballot((uint32_t)lane < nwin && (r_flags & 2u));   // windows needing the exact walk
     const uint32_t slot0 = (q0 - lo) >> 6;
     uint32_t w = 0;
+#ifdef SF_STREAM_PROF
+    uint64_t pa = 0, pb = 0, pc = 0;
+#endif
     while (w < nwin) {
+#ifdef SF_STREAM_PROF
+        const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
         const uint32_t q = q0 + 64 * w;
         const uint32_t slot = (slot0 + w) % LX_WORDS;
+        // every LDS read of the window issued together: the live-exit words of
+        // windows w, w+1, ... (lane k <-> window w+k) and the window's event data
+        const uint32_t wn_ = w + (uint32_t)lane;
+        const bool inr = wn_ < nwin;
+        const unsigned long long v = L.lx[(slot0 + (inr ? wn_ : w)) % LX_WORDS];
+        const uint32_t xo = L.xo[buf][64 * w + lane];
+        const int32_t c = L.cn[buf][64 * w + lane];
+        const int eln = L.el[buf][64 * w + lane];
         const unsigned long long me = rl64(r_ent, (int)w);
         const uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)r_flags, (int)w);
         const int64_t room0 = IM - T;
         const bool tsmall = T >= (int64_t)INT32_MIN + 64 && T + (int64_t)THR_CBIG + 64 <= (int64_t)INT32_MAX;
         if (room0 <= 0 && tsmall) {
             // saturated: skip the windows with no live exit (all their entries block)
-            const uint32_t wn_ = w + (uint32_t)lane;
-            const bool inr = wn_ < nwin;
-            const unsigned long long v = inr ? L.lx[(slot0 + wn_) % LX_WORDS] : 0ull;
-            const uint32_t fl = (uint32_t)__shfl((int)r_flags, inr ? (int)wn_ : 0);
-            const unsigned long long stop = __ballot(inr && (v != 0ull || (fl & 2u)));
+            const unsigned long long stop = __ballot(inr && v != 0ull) | (bigm >> w);
             if (!stop) { w = nwin; break; }
             const uint32_t k = (uint32_t)(__ffsll((long long)stop) - 1);
             if (k > 0) { w += k; continue; }
         }
-        unsigned long long ml = uniform_u64(L.lx[slot]);     // live exits of this window
+        unsigned long long ml = rl64(v, 0);                    // live exits of this window
         const int32_t maxrc = __builtin_amdgcn_readlane(r_maxrc, (int)w);
         unsigned long long pmask = 0;
         const bool nowrap = !(flags & 2u) && tsmall;
@@ -289,16 +311,12 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
         } else if (nowrap && room0 >= (int64_t)maxrc) {
             // the thread count before an entry is <= T + (entries before it): all fit
             pmask = me;
-            ml |= uniform_u64(L.win[buf][w].inw);        // exits of this window's entries, inside it
+            ml |= rl64(r_inw, (int)w);                     // exits of this window's entries, inside it
             T += (int64_t)__popcll(me) - (int64_t)__popcll(ml);
         } else if (nowrap && !(flags & 1u) && room0 >= 0) {
-            const int32_t c = L.cn[buf][64 * w + lane];
-            const int eln = L.el[buf][64 * w + lane];
             pmask = thr_window_solve((int)room0, me, ml, c, eln);
             T += (int64_t)__popcll(pmask) - (int64_t)__popcll(ml);
         } else {
-            const uint32_t xo = L.xo[buf][64 * w + lane];
-            const int32_t c = L.cn[buf][64 * w + lane];
             const bool small = nowrap && !(flags & 1u);
             const bool ones = nowrap && !(flags & 4u);      // every acquireCount is 1: scalar candidates
             // in-window exit of each entry lane: bit position, or 64
@@ -332,9 +350,11 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
             }
         }
         T = uniform64(T);
+#ifdef SF_STREAM_PROF
+        const uint64_t c1 = __builtin_amdgcn_s_memtime();
+#endif
         if (pmask) {
             // exits of the passed entries beyond this window turn live (one vector step)
-            const uint32_t xo = L.xo[buf][64 * w + lane];
             const bool mk = ((pmask >> lane) & 1ull) && xo != XO_NONE && xo < hi && xo >= q + 64;
             bool fm2 = false;
             if (mk) fm2 = thr_mark_exit(L, lxfar, xo, q, lo);
@@ -343,7 +363,14 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
         }
         if (lane == 0) L.lx[slot] = 0ull;                  // consumed: reused LX_WORDS windows later
         w++;
+#ifdef SF_STREAM_PROF
+        const uint64_t c2 = __builtin_amdgcn_s_memtime();
+        pa += c1 - c0; pb += c2 - c1; pc++;
+#endif
     }
+#ifdef SF_STREAM_PROF
+    thr_prof[0] += pa; thr_prof[1] += pb; thr_prof[2] += pc;
+#endif
     if (pst) {                                             // the chunk's pass bits: one vector step
         const uint32_t q = q0 + 64u * (uint32_t)lane, sh = q & 63;
         atomicOr(pbits + (q >> 6), pst << sh);
@@ -484,15 +511,16 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
 #ifdef SF_STREAM_PROF
             const uint64_t c1 = __builtin_amdgcn_s_memtime();
 #endif
-            __syncthreads();
+            lds_barrier();
 #ifdef SF_STREAM_PROF
             t_work += c1 - c0; t_bar += __builtin_amdgcn_s_memtime() - c1;
 #endif
         }
 #ifdef SF_STREAM_PROF
         if ((threadIdx.x & 63) == 0)
-            printf("SF_STREAM_PROF seg %u wave %d events %u chunks %u: work %lu barrier %lu cycles\n", s, h, hi - lo,
-                   ntc, (unsigned long)t_work, (unsigned long)t_bar);
+            printf("SF_STREAM_PROF seg %u wave %d events %u chunks %u: work %lu barrier %lu cycles; decide %lu mark %lu windows %lu\n",
+                   s, h, hi - lo, ntc, (unsigned long)t_work, (unsigned long)t_bar, (unsigned long)thr_prof[0],
+                   (unsigned long)thr_prof[1], (unsigned long)thr_prof[2]);
 #endif
     } else {                                                     // SM_RL
         int64_t* tsb = (int64_t*)smem;                           // [2][HS_CH]
@@ -512,7 +540,7 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
                 if (more) rl_load(r, io, q0 + HS_CH, hi);
                 if (wave0) rl_decide_chunk(tsb + (k & 1) * HS_CH, cb + (k & 1) * HS_CH, q0, hi, rule, cost1, L, iw);
                 if (more) rl_store(r, tsb + ((k + 1) & 1) * HS_CH, cb + ((k + 1) & 1) * HS_CH);
-                __syncthreads();
+                lds_barrier();
             }
             if (wave0) iw.finish();
             rs.latest_passed = L;
