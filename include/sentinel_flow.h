@@ -321,8 +321,16 @@ int  sf_load_system_rules(sf_engine* e, const sf_system_rule* rules, uint32_t n)
 /* JMX load / cpu inputs of SystemRule (fixed inputs in a replay). */
 int  sf_set_system_status(sf_engine* e, double avg_load, double cpu_usage);
 
-/* Decide a time-ordered batch: per-event verdicts, state updated in place. */
+/* Decide a time-ordered batch: per-event verdicts, state updated in place.
+ * Returns when the verdicts are written (and checked). */
 int  sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
+/* Same, enqueued only (batch and verdict arrays in HBM, SF_MEM_DEVICE): the
+ * engine sorts batch k+1 while it decides batch k (two internal Work sets).
+ * Batches are decided in submission order, exactly as by sf_submit; the
+ * arrays must stay valid until sf_sync, which waits for every enqueued batch
+ * and reports the first error any of them raised.  Host-memory batches and
+ * timing mode fall back to sf_submit. */
+int  sf_submit_async(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
 
 /* Cluster token server (DefaultTokenService). */
 int  sf_load_namespaces(sf_engine* e, const sf_namespace* ns, uint32_t n);
@@ -355,7 +363,7 @@ int  sf_entry_node_allreduce(sf_engine* e, sf_node_state* out);
 int  sf_device_alloc(sf_engine* e, size_t bytes, void** ptr);
 int  sf_device_free(sf_engine* e, void* ptr);
 int  sf_memcpy(sf_engine* e, void* dst, const void* src, size_t bytes, int kind /*0 H2D 1 D2H 2 D2D*/);
-int  sf_sync(sf_engine* e);
+int  sf_sync(sf_engine* e);      /* waits for sf_submit_async batches; their first error */
 int  sf_get_stats(sf_engine* e, sf_stats* out);
 int  sf_set_timing(sf_engine* e, int enabled);
 /* diagnostics: per heavy segment of the last sf_submit (timing must be on) */

@@ -37,17 +37,24 @@ static int fail(int code, const std::string& msg) {
 struct sf_engine {
     sf_config cfg{};
     hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
+    hipStream_t sstream = nullptr;  // sort phase of the next batch (overlaps the decide phase on `stream`)
     bool serial = false;            // diagnostics (SF_SERIAL_STREAMS=1): every kernel on one stream
     uint32_t R = 0, key_bits = 1;
     DevState st{};
-    Work w{};
+    Work w[2]{};                    // two Work sets: batch k sorts into w[k % 2] while k-1 is decided
+    bool w_ready[2] = {false, false};
+    int cur = 0, last = 0;          // Work set of the next / last submitted batch
+    unsigned pending = 0;           // Work sets with an asynchronous batch not yet checked by sf_sync
+    bool used[2] = {false, false};
+    hipEvent_t ev_sorted[2]{}, ev_done[2]{};
     // rules
     std::vector<uint32_t> flow_pos;        // loaded valid rule index -> CSR position
     uint32_t n_flow = 0, n_prule = 0;
     // staging for host-memory batches
     void* stage_in = nullptr; size_t stage_in_bytes = 0;
     void* stage_out = nullptr; size_t stage_out_bytes = 0;
-    hipEvent_t ev[SF_NUM_EVENTS]{};
+    hipEvent_t evs[2][SF_NUM_EVENTS]{};   // per Work set: fork/join and timing events of its batch
+    bool timed[2] = {false, false};       // that batch ran with timing on and is not yet in stats
     bool timing = false;
     sf_stats stats{};
     std::vector<void*> user_allocs;
@@ -107,23 +114,28 @@ static int dalloc(void** p, size_t bytes) {
         if (_rc) { sf_destroy(e); return _rc; }                          \
     } while (0)
 
+static void free_work(Work& w) {
+    void* ptrs[] = {w.pv_in, w.pv_out, w.wide, w.err, w.keys_in, w.keys_out, w.perm, w.head, w.head_scan,
+                    w.seg_start, w.seg_res, w.n_seg, w.s_ts, w.s_cnt, w.s_flags, w.s_eref,
+                    w.s_cts, w.s_nargs, w.s_atag, w.s_abits, w.inv, w.v_status, w.v_wait,
+                    w.v_rule, w.sort_tmp, w.scan_tmp,
+                    w.segflag, w.seg_mode, w.light_list, w.lcounts, w.heavy_list, w.counters, w.pcg,
+                    w.pscan_tmp, w.fill_tiles, w.fill_ntiles, w.acc_hw,
+                    w.acc_sec, w.acc_hw_base, w.acc_sec_base, w.seg_hw0, w.seg_sec0,
+                    w.seg_nhw, w.seg_nsec, w.hticks, w.passbits, w.stream_list, w.sticks,
+                    w.exit_of, w.lxfar};
+    for (void* p : ptrs) if (p) hipFree(p);
+    w = Work{};
+}
+
 void sf_destroy(sf_engine* e) {
     if (!e) return;
+    if (e->sstream) hipStreamSynchronize(e->sstream);
     if (e->stream) hipStreamSynchronize(e->stream);
-    void* ptrs0[] = {e->w.pv_in, e->w.pv_out};
-    for (void* p : ptrs0) if (p) hipFree(p);
+    for (Work& w : e->w) free_work(w);
     void* ptrs[] = {e->st.second, e->st.borrow, e->st.minute, e->st.threads, (void*)e->st.rule_off,
                     (void*)e->st.rules, e->st.rstate, (void*)e->st.prule_off, e->st.prules, (void*)e->st.items,
-                    e->st.pm_init, e->st.ptab, e->st.err,
-                    e->w.keys_in, e->w.keys_out, e->w.vals_in, e->w.perm, e->w.head, e->w.head_scan,
-                    e->w.seg_start, e->w.seg_res, e->w.n_seg, e->w.s_ts, e->w.s_cnt, e->w.s_flags, e->w.s_eref,
-                    e->w.s_cts, e->w.s_nargs, e->w.s_atag, e->w.s_abits, e->w.inv, e->w.v_status, e->w.v_wait,
-                    e->w.v_rule, e->w.sort_tmp, e->w.scan_tmp, e->stage_in, e->stage_out,
-                    e->w.segflag, e->w.seg_mode, e->w.light_list, e->w.lcounts, e->w.heavy_list, e->w.counters, e->w.pcg,
-                    e->w.pscan_tmp, e->w.fill_tiles, e->w.fill_ntiles, e->w.acc_hw,
-                    e->w.acc_sec, e->w.acc_hw_base, e->w.acc_sec_base, e->w.seg_hw0, e->w.seg_sec0,
-                    e->w.seg_nhw, e->w.seg_nsec, e->w.hticks, e->w.passbits, e->w.stream_list, e->w.sticks,
-                    e->w.exit_of, e->w.lxfar};
+                    e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
@@ -133,11 +145,82 @@ void sf_destroy(sf_engine* e) {
     if (e->agg) hipFree(e->agg);
     if (e->comm) ncclCommDestroy(e->comm);
     free_tok_work(e->tw);
-    for (auto& x : e->ev) if (x) hipEventDestroy(x);
+    for (auto& a : e->evs) for (auto& x : a) if (x) hipEventDestroy(x);
+    for (int k = 0; k < 2; k++) {
+        if (e->ev_sorted[k]) hipEventDestroy(e->ev_sorted[k]);
+        if (e->ev_done[k]) hipEventDestroy(e->ev_done[k]);
+    }
     if (e->stream) hipStreamDestroy(e->stream);
     if (e->stream2) hipStreamDestroy(e->stream2);
     if (e->stream3) hipStreamDestroy(e->stream3);
+    if (e->sstream) hipStreamDestroy(e->sstream);
     delete e;
+}
+
+#define WALLOC(ptr, bytes)                                               \
+    do {                                                                 \
+        int _rc = dalloc((void**)&(ptr), (bytes));                       \
+        if (_rc) { free_work(w); return _rc; }                           \
+    } while (0)
+
+// One Work set: every sorted-order buffer of one batch (sf_internal.h).
+static int alloc_work(sf_engine* e, Work& w) {
+    const sf_config& c = e->cfg;
+    const size_t N = c.max_batch, R = e->R;
+    WALLOC(w.keys_in, N * 4); WALLOC(w.keys_out, N * 4); WALLOC(w.perm, N * 4);
+    WALLOC(w.pv_in, N * sizeof(PackedEv)); WALLOC(w.pv_out, N * sizeof(PackedEv));
+    WALLOC(w.wide, 4); WALLOC(w.err, 4);
+    WALLOC(w.head, N * 4); WALLOC(w.head_scan, N * 4);
+    WALLOC(w.seg_start, (N + 1) * 4); WALLOC(w.seg_res, N * 4); WALLOC(w.n_seg, 4);
+    WALLOC(w.s_ts, N * 8); WALLOC(w.s_cnt, N * 4); WALLOC(w.s_flags, N);
+    WALLOC(w.s_eref, N * 8); WALLOC(w.s_cts, N * 8); WALLOC(w.inv, N * 4);
+    WALLOC(w.s_nargs, N); WALLOC(w.s_atag, N * SF_MAX_ARGS); WALLOC(w.s_abits, N * SF_MAX_ARGS * 8);
+    WALLOC(w.v_status, N); WALLOC(w.v_wait, N * 4); WALLOC(w.v_rule, N * 2);
+    {
+        hipError_t he = query_temp_bytes((uint32_t)N, e->key_bits, &w.sort_tmp_bytes, &w.scan_tmp_bytes,
+                                         &w.pscan_tmp_bytes);
+        if (he != hipSuccess) { free_work(w); return fail(SF_ERR_DEVICE, "rocprim temp size query"); }
+    }
+    WALLOC(w.sort_tmp, w.sort_tmp_bytes);
+    WALLOC(w.scan_tmp, w.scan_tmp_bytes);
+    WALLOC(w.pscan_tmp, w.pscan_tmp_bytes);
+    // heavy / light split
+    w.heavy_min = c.heavy_min_events ? c.heavy_min_events : 512;
+    {
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+        w.stream_grid = 2u * (uint32_t)(ncu > 0 ? ncu : 256);
+        w.fill_grid = 8u * (uint32_t)(ncu > 0 ? ncu : 256);
+    }
+    const size_t SC = std::min<size_t>(N, R) + 1;
+    w.seg_cap = (uint32_t)SC;
+    WALLOC(w.segflag, SC * 4); WALLOC(w.seg_mode, SC); WALLOC(w.lcounts, LCLS * 4);
+    {   // light_list regions per length class: class c holds segments of >= lo_len(c) events
+        size_t off = 0;
+        for (int k = 0; k < LCLS; k++) {
+            const size_t lo_len = k == 0 ? 1 : (k == 1 ? 2 : ((size_t)1 << (k - 1)) + 1);
+            const size_t cap = lo_len > w.heavy_min ? 0 : std::min<size_t>(SC, N / lo_len + 1);
+            w.loff[k] = (uint32_t)off;
+            off += cap;
+        }
+        WALLOC(w.light_list, off * 4);
+    }
+    WALLOC(w.heavy_list, SC * 4);
+    WALLOC(w.counters, 16 * 4); WALLOC(w.pcg, N * 8);
+    w.fill_tile_cap = (uint32_t)(N / FILL_TILE + 2 * (N / (w.heavy_min + 1)) + 2);   // <= len/TILE + 2 per segment
+    WALLOC(w.fill_tiles, (size_t)2 * w.fill_tile_cap * sizeof(uint2)); WALLOC(w.fill_ntiles, 2 * 4);
+    w.acc_cap = (uint32_t)std::min<size_t>(std::max<size_t>(N / w.heavy_min * 64, 1 << 16), 1u << 24);
+    WALLOC(w.acc_hw, (size_t)w.acc_cap * ACC_BYTES); WALLOC(w.acc_sec, (size_t)w.acc_cap * ACC_BYTES);
+    WALLOC(w.acc_hw_base, SC * 4); WALLOC(w.acc_sec_base, SC * 4); WALLOC(w.seg_hw0, SC * 8);
+    WALLOC(w.seg_sec0, SC * 8); WALLOC(w.seg_nhw, SC * 4); WALLOC(w.seg_nsec, SC * 4);
+    WALLOC(w.hticks, (N / (w.heavy_min + 1) + 2) * 8);
+    WALLOC(w.sticks, (N / (w.heavy_min + 1) + 2) * 8);
+    WALLOC(w.stream_list, SC * 4);
+    WALLOC(w.passbits, (N / 64 + 2) * 8);
+    WALLOC(w.exit_of, N * 4);
+    WALLOC(w.lxfar, (N / 64 + 2) * 8);
+    return SF_OK;
 }
 
 int sf_create(const sf_config* cfg, sf_engine** out) {
@@ -171,8 +254,13 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
         HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIP_TRY(hipStreamCreateWithPriority(&e->stream3, hipStreamNonBlocking, greatest));
     }
+    HIP_TRY(hipStreamCreateWithFlags(&e->sstream, hipStreamNonBlocking));
     if (const char* v = getenv("SF_SERIAL_STREAMS")) e->serial = v[0] == '1';
-    for (auto& x : e->ev) HIP_TRY(hipEventCreate(&x));
+    for (auto& a : e->evs) for (auto& x : a) HIP_TRY(hipEventCreate(&x));
+    for (int k = 0; k < 2; k++) {
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_sorted[k], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_done[k], hipEventDisableTiming));
+    }
 
     DevState& st = e->st;
     st.S = c.sample_count; st.wl = c.interval_ms / c.sample_count; st.interval = c.interval_ms;
@@ -206,55 +294,11 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     DALLOC(e->en_acc, sizeof(EntryAcc));
     HIP_TRY(launch_entry_init(e->en, st.max_rt, e->stream));
 
-    Work& w = e->w;
-    const size_t N = c.max_batch;
-    DALLOC(w.keys_in, N * 4); DALLOC(w.keys_out, N * 4); DALLOC(w.vals_in, N * 4); DALLOC(w.perm, N * 4);
-    DALLOC(w.pv_in, N * sizeof(PackedEv)); DALLOC(w.pv_out, N * sizeof(PackedEv));
-    DALLOC(w.head, N * 4); DALLOC(w.head_scan, N * 4);
-    DALLOC(w.seg_start, (N + 1) * 4); DALLOC(w.seg_res, N * 4); DALLOC(w.n_seg, 4);
-    DALLOC(w.s_ts, N * 8); DALLOC(w.s_cnt, N * 4); DALLOC(w.s_flags, N);
-    DALLOC(w.s_eref, N * 8); DALLOC(w.s_cts, N * 8); DALLOC(w.inv, N * 4);
-    DALLOC(w.s_nargs, N); DALLOC(w.s_atag, N * SF_MAX_ARGS); DALLOC(w.s_abits, N * SF_MAX_ARGS * 8);
-    DALLOC(w.v_status, N); DALLOC(w.v_wait, N * 4); DALLOC(w.v_rule, N * 2);
-    HIP_TRY(query_temp_bytes((uint32_t)N, e->key_bits, &w.sort_tmp_bytes, &w.scan_tmp_bytes, &w.pscan_tmp_bytes));
-    DALLOC(w.sort_tmp, w.sort_tmp_bytes);
-    DALLOC(w.scan_tmp, w.scan_tmp_bytes);
-    DALLOC(w.pscan_tmp, w.pscan_tmp_bytes);
-    // heavy / light split
-    w.heavy_min = c.heavy_min_events ? c.heavy_min_events : 512;
     {
-        int dev = 0, ncu = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-        w.stream_grid = 2u * (uint32_t)(ncu > 0 ? ncu : 256);
-        w.fill_grid = 8u * (uint32_t)(ncu > 0 ? ncu : 256);
+        const int rc = alloc_work(e, e->w[0]);
+        if (rc) { sf_destroy(e); return rc; }
+        e->w_ready[0] = true;
     }
-    const size_t SC = std::min<size_t>(N, R) + 1;
-    w.seg_cap = (uint32_t)SC;
-    DALLOC(w.segflag, SC * 4); DALLOC(w.seg_mode, SC); DALLOC(w.lcounts, LCLS * 4);
-    {   // light_list regions per length class: class c holds segments of >= lo_len(c) events
-        size_t off = 0;
-        for (int c = 0; c < LCLS; c++) {
-            const size_t lo_len = c == 0 ? 1 : (c == 1 ? 2 : ((size_t)1 << (c - 1)) + 1);
-            const size_t cap = lo_len > w.heavy_min ? 0 : std::min<size_t>(SC, N / lo_len + 1);
-            w.loff[c] = (uint32_t)off;
-            off += cap;
-        }
-        DALLOC(w.light_list, off * 4);
-    } DALLOC(w.heavy_list, SC * 4);
-    DALLOC(w.counters, 16 * 4); DALLOC(w.pcg, N * 8);
-    w.fill_tile_cap = (uint32_t)(N / FILL_TILE + 2 * (N / (w.heavy_min + 1)) + 2);   // <= len/TILE + 2 per segment
-    DALLOC(w.fill_tiles, (size_t)2 * w.fill_tile_cap * sizeof(uint2)); DALLOC(w.fill_ntiles, 2 * 4);
-    w.acc_cap = (uint32_t)std::min<size_t>(std::max<size_t>(N / w.heavy_min * 64, 1 << 16), 1u << 24);
-    DALLOC(w.acc_hw, (size_t)w.acc_cap * ACC_BYTES); DALLOC(w.acc_sec, (size_t)w.acc_cap * ACC_BYTES);
-    DALLOC(w.acc_hw_base, SC * 4); DALLOC(w.acc_sec_base, SC * 4); DALLOC(w.seg_hw0, SC * 8);
-    DALLOC(w.seg_sec0, SC * 8); DALLOC(w.seg_nhw, SC * 4); DALLOC(w.seg_nsec, SC * 4);
-    DALLOC(w.hticks, (N / (w.heavy_min + 1) + 2) * 8);
-    DALLOC(w.sticks, (N / (w.heavy_min + 1) + 2) * 8);
-    DALLOC(w.stream_list, SC * 4);
-    DALLOC(w.passbits, (N / 64 + 2) * 8);
-    DALLOC(w.exit_of, N * 4);
-    DALLOC(w.lxfar, (N / 64 + 2) * 8);
     HIP_TRY(hipStreamSynchronize(e->stream));
     *out = e;
     return SF_OK;
@@ -266,9 +310,60 @@ static int local_of(const sf_engine* e, uint32_t res, uint32_t* l) {
     return *l < e->R;
 }
 
+// Per-kernel device times of the batch last run in Work set `slot` (its
+// events), added to the stats once, after that batch has completed.
+static void acc_timing(sf_engine* e, int slot) {
+    if (!e->timed[slot]) return;
+    e->timed[slot] = false;
+    hipEvent_t* ev = e->evs[slot];
+    float a = 0, b2 = 0, c = 0, d = 0;
+    hipEventElapsedTime(&a, ev[0], ev[1]);
+    hipEventElapsedTime(&b2, ev[1], ev[2]);
+    hipEventElapsedTime(&c, ev[2], ev[3]);
+    hipEventElapsedTime(&d, ev[3], ev[4]);
+    float cl = 0, li = 0, hd = 0, hf = 0, hs = 0;
+    hipEventElapsedTime(&cl, ev[10], ev[2]);
+    hipEventElapsedTime(&li, ev[5], ev[9]);
+    hipEventElapsedTime(&hd, ev[5], ev[7]);
+    hipEventElapsedTime(&hf, ev[7], ev[8]);
+    hipEventElapsedTime(&hs, ev[11], ev[12]);
+    e->stats.classify_ms += cl; e->stats.light_ms += li;
+    e->stats.heavy_decide_ms += hd; e->stats.heavy_fill_ms += hf; e->stats.stream_ms += hs;
+    e->stats.sort_ms += a + b2;
+    e->stats.decide_ms += c;
+    e->stats.scatter_ms += d;
+    e->stats.total_ms += a + b2 + c + d;
+}
+
+// Drain asynchronously submitted batches: wait for both streams, then report
+// the first error flag raised by any of them.
+static int drain(sf_engine* e) {
+    if (!e->pending) return SF_OK;
+    HIP_TRY(hipStreamSynchronize(e->sstream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    int first = 0;
+    for (int k = 0; k < 2; k++) {
+        if (!(e->pending & (1u << k))) continue;
+        int32_t err = 0;
+        HIP_TRY(hipMemcpy(&err, e->w[k].err, 4, hipMemcpyDeviceToHost));
+        if (err && !first) first = err;
+    }
+    e->pending = 0;
+    for (int k = 0; k < 2; k++) acc_timing(e, k);
+    {
+        uint32_t nseg = 0;
+        HIP_TRY(hipMemcpy(&nseg, e->w[e->last].n_seg, 4, hipMemcpyDeviceToHost));
+        e->stats.n_segments = nseg;
+    }
+    if (first) return fail(first, first == SF_ERR_CAPACITY ? "param table capacity exceeded"
+                                                           : "invalid batch (resource outside shard or bad entry_ref)");
+    return SF_OK;
+}
+
 int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
     if (!e || (n && !rules)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }   // pending batches were sorted under the old rules
     std::vector<uint32_t> counts(e->R + 1, 0);
     std::vector<const sf_flow_rule*> valid;
     std::vector<uint32_t> valid_local;
@@ -319,6 +414,7 @@ int sf_load_param_rules(sf_engine* e, const sf_param_rule* rules, uint32_t n, co
                         uint32_t n_items) {
     if (!e || (n && !rules) || (n_items && !items)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }   // pending batches were sorted under the old rules
     std::vector<uint32_t> counts(e->R + 1, 0), loc(n);
     for (uint32_t i = 0; i < n; i++) {
         if (!local_of(e, rules[i].resource, &loc[i])) return fail(SF_ERR_INVALID, "rule resource outside this shard");
@@ -362,18 +458,34 @@ int sf_set_system_status(sf_engine* e, double, double) { return e ? SF_OK : SF_E
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
-int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
+static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out, bool async) {
     if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
     if (in->n == 0) return SF_OK;
     if (!in->res_id || !in->ts_ms || !in->count || !in->flags) return fail(SF_ERR_INVALID, "missing event array");
     if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
     if (in->arg_slots > SF_MAX_ARGS || (in->arg_slots && (!in->arg_tag || !in->arg_bits)))
         return fail(SF_ERR_INVALID, "bad arg arrays");
-    std::lock_guard<std::mutex> lk(e->mu);
     const uint32_t n = in->n;
     DevBatch b{};
     b.n = n; b.arg_slots = in->arg_slots;
-    hipStream_t s = e->stream;
+    hipStream_t s = e->stream, ss = e->serial ? e->stream : e->sstream;
+    // asynchronous only for HBM-resident batches and verdicts
+    async = async && in->mem != SF_MEM_HOST && out->mem != SF_MEM_HOST;
+    if (!async) { const int rc = drain(e); if (rc) return rc; }
+    if (async && !e->w_ready[1]) {                 // second Work set on first asynchronous use
+        HIP_TRY(hipStreamSynchronize(s));
+        const int rc = alloc_work(e, e->w[1]);
+        if (rc) return rc;
+        e->w_ready[1] = true;
+    }
+    const int slot = e->cur;
+    Work& w = e->w[slot];
+    if (e->used[slot]) {
+        // the batch that last used this Work set (two submits ago) must be done:
+        // its events and buffers are reused (sort(k) still overlaps decide(k-1))
+        HIP_TRY(hipEventSynchronize(e->ev_done[slot]));
+        acc_timing(e, slot);
+    }
     if (in->mem == SF_MEM_HOST) {
         size_t need = 0;
         size_t o_res = need; need += align_up((size_t)n * 4);
@@ -394,7 +506,7 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         char* base = (char*)e->stage_in;
         auto up = [&](size_t off, const void* src, size_t bytes) -> const void* {
             if (!src || !bytes) return nullptr;
-            hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, s);
+            hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, ss);
             return base + off;
         };
         b.res = (const uint32_t*)up(o_res, in->res_id, (size_t)n * 4);
@@ -427,22 +539,33 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     } else {
         dv.status = out->status; dv.wait = out->wait_ms; dv.rule = out->rule_idx;
     }
-    {   // time span of the (non-decreasing) batch: packed sort payload when it fits 32 bits
-        int64_t t01[2] = {0, 0};
-        HIP_TRY(hipMemcpyAsync(&t01[0], b.ts, 8, hipMemcpyDefault, s));
-        HIP_TRY(hipMemcpyAsync(&t01[1], b.ts + (n - 1), 8, hipMemcpyDefault, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        e->w.tmin = t01[0];
-        e->w.packed_ok = t01[1] >= t01[0] && (uint64_t)(t01[1] - t01[0]) < (1ull << 32);
-    }
-    HIP_TRY(hipMemsetAsync(e->st.err, 0, sizeof(int32_t), s));
-    hipError_t le = launch_pipeline(e->st, e->w, b, dv, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s,
-                                    e->serial ? e->stream : e->stream2, e->serial ? e->stream : e->stream3,
-                                    e->ev, e->timing);
+    // sort phase on the sort stream, into this batch's Work set (after the
+    // decide phase of the batch that used it last)
+    if (e->used[slot]) HIP_TRY(hipStreamWaitEvent(ss, e->ev_done[slot], 0));
+    HIP_TRY(hipMemsetAsync(w.err, 0, sizeof(int32_t), ss));
+    DevState stl = e->st;
+    stl.err = w.err;
+    hipError_t le = launch_sort(stl, w, b, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, ss, e->evs[slot], e->timing);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
+    HIP_TRY(hipEventRecord(e->ev_sorted[slot], ss));
+    // decide phase in batch order on the main streams
+    HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
+    le = launch_decide(stl, w, b, dv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3, e->evs[slot], e->timing);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
     // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream order)
-    le = launch_entry_node(e->st, b, dv.status, e->en, e->en_acc, s);
+    le = launch_entry_node(stl, b, dv.status, e->en, e->en_acc, s);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
+    HIP_TRY(hipEventRecord(e->ev_done[slot], s));
+    e->used[slot] = true;
+    e->timed[slot] = e->timing;
+    e->last = slot;
+    e->stats.n_events = n;
+    e->stats.n_launches++;
+    if (async) {
+        e->pending |= 1u << slot;
+        e->cur ^= 1;
+        return SF_OK;
+    }
     if (out->mem == SF_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, s));
         if (dv.wait) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait, (size_t)n * 4, hipMemcpyDeviceToHost, s));
@@ -450,34 +573,26 @@ int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     }
     int32_t err = 0;
     uint32_t nseg = 0;
-    HIP_TRY(hipMemcpyAsync(&err, e->st.err, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&nseg, e->w.n_seg, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&err, w.err, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&nseg, w.n_seg, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    e->stats.n_events = n;
     e->stats.n_segments = nseg;
-    e->stats.n_launches++;
-    if (e->timing) {
-        float a = 0, b2 = 0, c = 0, d = 0;
-        hipEventElapsedTime(&a, e->ev[0], e->ev[1]);
-        hipEventElapsedTime(&b2, e->ev[1], e->ev[2]);
-        hipEventElapsedTime(&c, e->ev[2], e->ev[3]);
-        hipEventElapsedTime(&d, e->ev[3], e->ev[4]);
-        float cl = 0, li = 0, hd = 0, hf = 0, hs = 0;
-        hipEventElapsedTime(&cl, e->ev[10], e->ev[2]);
-        hipEventElapsedTime(&li, e->ev[5], e->ev[9]);
-        hipEventElapsedTime(&hd, e->ev[5], e->ev[7]);
-        hipEventElapsedTime(&hf, e->ev[7], e->ev[8]);
-        hipEventElapsedTime(&hs, e->ev[11], e->ev[12]);
-        e->stats.classify_ms += cl; e->stats.light_ms += li;
-        e->stats.heavy_decide_ms += hd; e->stats.heavy_fill_ms += hf; e->stats.stream_ms += hs;
-        e->stats.sort_ms += a + b2;
-        e->stats.decide_ms += c;
-        e->stats.scatter_ms += d;
-        e->stats.total_ms += a + b2 + c + d;
-    }
+    acc_timing(e, slot);
     if (err) return fail(err, err == SF_ERR_CAPACITY ? "param table capacity exceeded"
                                                      : "invalid batch (resource outside shard or bad entry_ref)");
     return SF_OK;
+}
+
+int sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
+    if (!e) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return submit_core(e, in, out, false);
+}
+
+int sf_submit_async(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
+    if (!e) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return submit_core(e, in, out, true);
 }
 
 static void to_abi_bucket(const Bucket& d, sf_bucket* o) {
@@ -877,8 +992,10 @@ int sf_memcpy(sf_engine* e, void* dst, const void* src, size_t bytes, int kind) 
 }
 int sf_sync(sf_engine* e) {
     if (!e) return fail(SF_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipStreamSynchronize(e->sstream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    return SF_OK;
+    return drain(e);
 }
 int sf_get_stats(sf_engine* e, sf_stats* out) {
     if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
@@ -896,34 +1013,36 @@ int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uin
     if (!e || !n_out || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> g(e->mu);
     uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0}, nseg = 0;
+    { const int rc = drain(e); if (rc) return rc; }
+    const Work& lw = e->w[e->last];
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
     HIP_TRY(hipStreamSynchronize(e->stream3));
-    HIP_TRY(hipMemcpy(cnt, e->w.counters, sizeof cnt, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(&nseg, e->w.n_seg, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cnt, lw.counters, sizeof cnt, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&nseg, lw.n_seg, 4, hipMemcpyDeviceToHost));
     const uint32_t n1 = cnt[1] + cnt[4], n2 = cnt[5] + cnt[6];
     const uint32_t nh = std::min(n1 + n2, cap);
-    std::vector<uint32_t> full(e->w.seg_cap), full2(e->w.seg_cap), list(nh), start(nseg + 1), res(nseg);
+    std::vector<uint32_t> full(lw.seg_cap), full2(lw.seg_cap), list(nh), start(nseg + 1), res(nseg);
     std::vector<uint8_t> mode(nseg);
     std::vector<uint64_t> ticks(n1 + 1), ticks2(n2 + 1), tk(nh);
     if (nh) {
-        HIP_TRY(hipMemcpy(full.data(), e->w.heavy_list, (size_t)e->w.seg_cap * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(full2.data(), e->w.stream_list, (size_t)e->w.seg_cap * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(ticks.data(), e->w.hticks, n1 * 8, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(ticks2.data(), e->w.sticks, n2 * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(full.data(), lw.heavy_list, (size_t)lw.seg_cap * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(full2.data(), lw.stream_list, (size_t)lw.seg_cap * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(ticks.data(), lw.hticks, n1 * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(ticks2.data(), lw.sticks, n2 * 8, hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < nh; i++) {
             if (i < n1) {
-                list[i] = i < cnt[1] ? full[i] : full[e->w.seg_cap - 1 - (i - cnt[1])];
+                list[i] = i < cnt[1] ? full[i] : full[lw.seg_cap - 1 - (i - cnt[1])];
                 tk[i] = ticks[i];
             } else {
                 const uint32_t k = i - n1;
-                list[i] = k < cnt[5] ? full2[k] : full2[e->w.seg_cap - 1 - (k - cnt[5])];
+                list[i] = k < cnt[5] ? full2[k] : full2[lw.seg_cap - 1 - (k - cnt[5])];
                 tk[i] = ticks2[k];
             }
         }
-        HIP_TRY(hipMemcpy(start.data(), e->w.seg_start, (nseg + 1) * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(res.data(), e->w.seg_res, nseg * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(mode.data(), e->w.seg_mode, nseg, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(start.data(), lw.seg_start, (nseg + 1) * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(res.data(), lw.seg_res, nseg * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(mode.data(), lw.seg_mode, nseg, hipMemcpyDeviceToHost));
     }
     uint64_t t0 = ~0ull;
     for (uint32_t i = n1; i < nh; i++) t0 = std::min(t0, tk[i] >> 24);

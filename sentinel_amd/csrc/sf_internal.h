@@ -115,9 +115,10 @@ constexpr uint32_t FILL_TILE = 2048;             // events per k_heavy_fill tile
 struct Work {
     uint32_t n;
     uint32_t* keys_in;   uint32_t* keys_out;     // local resource id
-    uint32_t* vals_in;   uint32_t* perm;         // iota -> stable permutation
-    PackedEv* pv_in; PackedEv* pv_out;           // packed payload (packed_ok)
-    bool packed_ok; int64_t tmin;                // this batch: span < 2^32 ms, first time
+    uint32_t* perm;                              // sorted position -> submission index
+    PackedEv* pv_in; PackedEv* pv_out;           // sort payload
+    uint32_t* wide;                              // batch times exceed 32-bit offsets (k_unpack reads the batch)
+    int32_t* err;                                // batch error flag (this Work set's batch)
     uint32_t* head;      uint32_t* head_scan;    // segment flags and positions
     uint32_t* seg_start; uint32_t* seg_res; uint32_t* n_seg;
     int64_t* s_ts; int32_t* s_cnt; uint8_t* s_flags;
@@ -174,10 +175,10 @@ hipError_t launch_en_pack_vals(const EntryNode* en, int S, const int64_t* gws, i
 hipError_t launch_snapshot(const DevState& st, int64_t now, uint32_t shard_count, uint32_t shard_index,
                            uint32_t* counts, uint32_t* offsets, sf_metric_row* out, uint32_t cap, uint32_t* total,
                            void* scan_tmp, size_t scan_bytes, hipStream_t s);
-hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
-                           uint32_t shard_count, uint32_t shard_index, uint32_t key_bits,
-                           hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev /* SF_NUM_EVENTS */,
-                           bool timing);
+hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,
+                       uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing);
+hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
+                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing);
 constexpr size_t ACC_BYTES = 72;                         // sizeof(Acc)
 // pipeline events: 0 start, 1 segments, 2 classified, 3 joined, 4 scattered,
 // 5 fork, 6 join (stream B), 7 heavy decided, 8 heavy filled, 9 light decided, 10 before classify,

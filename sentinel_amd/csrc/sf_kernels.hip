@@ -1,18 +1,23 @@
 // sf_kernels.hip — gfx950 kernels of one sf_submit (product code).
 //
-// Pipeline (two HIP streams, no host round trip inside):
-//   k_keys      validate + map resource ids to shard-local keys, iota values
-//   radix sort  stable (key, index) sort by resource: per-resource time order
-//               is the input order (LeapArray semantics need it)
+// Sort phase (sort stream, one of two Work sets; overlaps the previous
+// batch's decide phase):
+//   k_keys_packed  validate + map resource ids to shard-local keys, 16-B payload
+//   radix sort     stable (key, payload) sort by resource: per-resource time order
+//                  is the input order (LeapArray semantics need it)
 //   k_heads + exclusive scan + k_segments   segment table of touched resources
-//   k_gather    events into sorted order (SoA), inverse permutation, per-segment flags
-//   pc scan     inclusive prefix of entry acquireCount (heavy window budgets)
-//   k_classify  light segments -> lane interpreter; heavy -> window/skip algorithms
-//   stream A:   k_decide_light  one lane per light segment (sf_decide.h)
+//   k_unpack       events into sorted order (SoA), inverse permutation, per-segment flags
+//   k_gather_exit  sorted position of each entry's exit
+//   pc scan        inclusive prefix of entry acquireCount (heavy window budgets)
+//   k_classify     light segments (by length class) -> lane interpreter; heavy -> window/skip algorithms
+//   k_fill_tiles   fill tiles of the heavy segments of each class
+// Decide phase (stateful, in batch order):
+//   stream A:   k_heavy_stream  persistent; one 256-thread workgroup per heavy THREAD / RL segment (sf_stream.h)
+//               k_heavy_fill / k_heavy_apply of its class
 //   stream B:   k_heavy_decide  one wavefront per heavy QPS / WarmUp segment (sf_heavy.h)
-//   stream C:   k_heavy_stream  one 256-thread workgroup per heavy THREAD / RL segment (sf_stream.h)
-//               k_heavy_fill    verdicts + per-window counter deltas, device-wide
+//               k_heavy_fill    verdicts + per-window counter deltas from the pass bits
 //               k_heavy_apply   deltas applied to the LeapArray state in time order
+//   stream C:   k_decide_light  one lane per light segment (sf_decide.h)
 //   k_scatter   verdicts back to submission order
 #include <cstring>
 #include <rocprim/rocprim.hpp>
@@ -32,37 +37,30 @@ __global__ void k_init_state(DevState st, size_t n_sec, size_t n_min) {
     for (size_t k = i; k < st.R; k += stride) st.threads[k] = 0;
 }
 
-__global__ void k_keys(DevBatch b, uint32_t* keys, uint32_t* vals, uint32_t shard_count,
-                       uint32_t shard_index, uint32_t R, int32_t* err) {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= b.n) return;
-    uint32_t r = b.res[i];
-    uint32_t l = r / shard_count;
-    if (r % shard_count != shard_index || l >= R) { *err = SF_ERR_INVALID; l = 0; }
-    keys[i] = l;
-    vals[i] = i;
-}
-
-// Packed payload variant (batch time span < 2^32 ms): the radix sort carries
-// each event's (index, time offset, acquireCount, flags) as a 16-B value, so
-// the sorted order is read back with coalesced loads instead of a random
-// gather from the submission-order arrays.
+// Sort payload: the radix sort carries each event's (index, time offset from
+// the batch's first event, acquireCount, flags) as a 16-B value, so the sorted
+// order is read back with coalesced loads instead of a random gather from the
+// submission-order arrays.  A batch whose times do not fit 32-bit offsets from
+// its first event (never for a time-ordered batch shorter than 49 days) sets
+// *wide and k_unpack reads those times from the batch instead.
 __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t shard_count, uint32_t shard_index,
-                              uint32_t R, int64_t tmin, int32_t* err) {
+                              uint32_t R, int32_t* err, uint32_t* wide) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;
     uint32_t r = b.res[i];
     uint32_t l = r / shard_count;
     if (r % shard_count != shard_index || l >= R) { *err = SF_ERR_INVALID; l = 0; }
     keys[i] = l;
+    const int64_t d = b.ts[i] - b.ts[0];
+    if (d < 0 || d > (int64_t)0xffffffffLL) *wide = 1u;
     PackedEv v;
-    v.idx = i; v.dts = (uint32_t)(b.ts[i] - tmin); v.cnt = b.cnt[i]; v.flags = b.flags[i];
+    v.idx = i; v.dts = (uint32_t)d; v.cnt = b.cnt[i]; v.flags = b.flags[i];
     pv[i] = v;
 }
 
-__global__ void k_unpack(DevBatch b, const PackedEv* pv, int64_t tmin, uint32_t* perm, int64_t* s_ts, int32_t* s_cnt,
-                         uint8_t* s_flags, uint32_t* inv, uint8_t* s_nargs, uint8_t* s_atag, uint64_t* s_abits,
-                         const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag) {
+__global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* wide, uint32_t* perm, int64_t* s_ts,
+                         int32_t* s_cnt, uint8_t* s_flags, uint32_t* inv, uint8_t* s_nargs, uint8_t* s_atag,
+                         uint64_t* s_abits, const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
     const PackedEv v = pv[j];
@@ -70,7 +68,7 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, int64_t tmin, uint32_t*
     const int32_t c = v.cnt;
     const uint8_t f = (uint8_t)v.flags;
     perm[j] = i;
-    s_ts[j] = tmin + (int64_t)v.dts; s_cnt[j] = c; s_flags[j] = f;
+    s_ts[j] = *wide ? b.ts[i] : b.ts[0] + (int64_t)v.dts; s_cnt[j] = c; s_flags[j] = f;
     if (inv) inv[i] = j;
     if (!(f & SF_EV_EXIT) && ((f & SF_EV_PRIO) || c <= 0)) {
         uint32_t s = head_scan[j] + head[j] - 1;
@@ -97,30 +95,6 @@ __global__ void k_segments(const uint32_t* keys, const uint32_t* head, const uin
     if (j >= n) return;
     if (head[j]) { seg_start[pos[j]] = j; seg_res[pos[j]] = keys[j]; segflag[pos[j]] = 0; }
     if (j == n - 1) { uint32_t ns = pos[j] + head[j]; *n_seg = ns; seg_start[ns] = n; }
-}
-
-__global__ void k_gather(DevBatch b, const uint32_t* perm, int64_t* s_ts, int32_t* s_cnt, uint8_t* s_flags,
-                         uint32_t* inv, uint8_t* s_nargs, uint8_t* s_atag, uint64_t* s_abits,
-                         const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag) {
-    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= b.n) return;
-    uint32_t i = perm[j];
-    int64_t t = b.ts[i];
-    int32_t c = b.cnt[i];
-    uint8_t f = b.flags[i];
-    s_ts[j] = t; s_cnt[j] = c; s_flags[j] = f;
-    if (inv) inv[i] = j;
-    if (!(f & SF_EV_EXIT) && ((f & SF_EV_PRIO) || c <= 0)) {
-        uint32_t s = head_scan[j] + head[j] - 1;
-        atomicOr(&segflag[s], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u));
-    }
-    if (b.arg_slots) {
-        if (b.nargs) s_nargs[j] = b.nargs[i];
-        for (uint32_t a = 0; a < b.arg_slots; a++) {
-            s_atag[(size_t)a * b.n + j] = b.atag[(size_t)a * b.n + i];
-            s_abits[(size_t)a * b.n + j] = b.abits[(size_t)a * b.n + i];
-        }
-    }
 }
 
 __global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint32_t* inv, int64_t* s_eref,
@@ -653,26 +627,22 @@ hipError_t launch_init_state(const DevState& st, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
-                           uint32_t shard_count, uint32_t shard_index, uint32_t key_bits,
-                           hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing) {
+// Sort phase of a batch (state-independent): keys, radix sort, segments,
+// sorted SoA, exit map, acquireCount prefix, classification and fill tiles.
+// Runs on its own stream into one of the engine's two Work sets, so the next
+// batch is sorted while the current one is decided.
+hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,
+                       uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing) {
     const uint32_t n = b.n;
     if (n == 0) return hipSuccess;
     const unsigned T = 256;
     if (timing) hipEventRecord(ev[0], s);
-    const bool packed = w.packed_ok;
     hipError_t e;
-    if (packed) {
-        hipLaunchKernelGGL(k_keys_packed, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.pv_in, shard_count,
-                           shard_index, st.R, w.tmin, st.err);
-        e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.pv_in, w.pv_out, n, 0u,
-                                      key_bits, s);
-    } else {
-        hipLaunchKernelGGL(k_keys, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.vals_in, shard_count,
-                           shard_index, st.R, st.err);
-        e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.vals_in, w.perm, n, 0u,
-                                      key_bits, s);
-    }
+    hipMemsetAsync(w.wide, 0, 4, s);
+    hipLaunchKernelGGL(k_keys_packed, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.pv_in, shard_count,
+                       shard_index, st.R, st.err, w.wide);
+    e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.pv_in, w.pv_out, n, 0u,
+                                  key_bits, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_heads, dim3(blocks(n, T)), dim3(T), 0, s, w.keys_out, n, w.head);
     e = rocprim::exclusive_scan(w.scan_tmp, w.scan_tmp_bytes, w.head, w.head_scan, 0u, (size_t)n,
@@ -681,13 +651,9 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     hipLaunchKernelGGL(k_segments, dim3(blocks(n, T)), dim3(T), 0, s, w.keys_out, w.head, w.head_scan, n,
                        w.seg_start, w.seg_res, w.n_seg, w.segflag);
     if (timing) hipEventRecord(ev[1], s);
-    if (packed)
-        hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.tmin, w.perm, w.s_ts, w.s_cnt,
-                           w.s_flags, b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan,
-                           w.segflag);
-    else
-        hipLaunchKernelGGL(k_gather, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_ts, w.s_cnt, w.s_flags,
-                           b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag);
+    hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.wide, w.perm, w.s_ts, w.s_cnt,
+                       w.s_flags, b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan,
+                       w.segflag);
     hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.inv, w.s_eref,
@@ -702,8 +668,21 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     const uint32_t max_seg = n < st.R ? n : st.R;
     if (timing) hipEventRecord(ev[10], s);
     hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, 1024)), dim3(1024), 0, s, st, w, w.s_ts);
+    HeavyCtx hc = heavy_ctx(w);
+    StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, nullptr, w.counters + 7};
+    hipLaunchKernelGGL(k_fill_tiles, dim3(2), dim3(1024), 0, s, hc, sc, w.fill_tiles, w.fill_tile_cap, w.fill_ntiles);
     if (timing) hipEventRecord(ev[2], s);
+    return hipGetLastError();
+}
 
+// Decide phase (stateful, batch order): the serial chains (k_heavy_stream)
+// start first, on A; QPS/WarmUp heavy segments on B, the light lanes on C;
+// then the verdicts are scattered back to submission order.
+hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
+                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing) {
+    const uint32_t n = b.n;
+    if (n == 0) return hipSuccess;
+    const unsigned T = 256;
     SegIO io;
     io.ts = w.s_ts; io.cnt = w.s_cnt; io.flags = w.s_flags;
     io.eref = b.eref ? w.s_eref : nullptr; io.cts = b.eref ? w.s_cts : nullptr;
@@ -712,12 +691,9 @@ hipError_t launch_pipeline(const DevState& st, Work& w, const DevBatch& b, const
     io.v_status = w.v_status; io.v_wait = w.v_wait; io.v_rule = w.v_rule;
     HeavyCtx hc = heavy_ctx(w);
     if (timing) hc.hticks = w.hticks;
-
-    // The serial chains (k_heavy_stream) start first, on A, straight after
-    // classify; QPS/WarmUp heavy segments on B, the light lanes on C.
+    const uint32_t max_seg = n < st.R ? n : st.R;
     const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
     StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, timing ? w.sticks : nullptr, w.counters + 7};
-    hipLaunchKernelGGL(k_fill_tiles, dim3(2), dim3(1024), 0, s, hc, sc, w.fill_tiles, w.fill_tile_cap, w.fill_ntiles);
     hipEventRecord(ev[5], s);                      // fork
     hipEventRecord(ev[11], s);
     hipLaunchKernelGGL(k_heavy_stream, dim3(std::min(max_heavy, w.stream_grid)), dim3(HS_T), 0, s, st, io, hc, sc);

@@ -62,6 +62,7 @@ def _declare(L):
     f("sf_load_system_rules", I, P, C.POINTER(abi.sf_system_rule), U32)
     f("sf_set_system_status", I, P, C.c_double, C.c_double)
     f("sf_submit", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
+    f("sf_submit_async", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
     f("sf_load_namespaces", I, P, C.POINTER(abi.sf_namespace), U32)
     f("sf_load_cluster_rules", I, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
@@ -217,6 +218,13 @@ class FlowEngine:
         b = batch.c_struct()
         v = out.c_struct()
         _check(lib().sf_submit(self.h, C.byref(b), C.byref(v)))
+
+    def submit_device_async(self, batch: DeviceBatch, out: DeviceVerdicts):
+        """Enqueue a batch (HBM arrays; keep them alive until sync()): batch k+1 is
+        sorted while batch k is decided; sync() waits and reports errors."""
+        b = batch.c_struct()
+        v = out.c_struct()
+        _check(lib().sf_submit_async(self.h, C.byref(b), C.byref(v)))
 
     def read_node(self, res) -> abi.sf_node_state:
         st = abi.sf_node_state()

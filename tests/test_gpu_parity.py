@@ -75,6 +75,44 @@ def test_device_resident_batch(eng_mod, so):
     parity.compare_nodes(e, ora, w["nodes"])
 
 
+@pytest.mark.parametrize("split", [2, 5])
+def test_async_pipelined_batches(eng_mod, so, split):
+    """sf_submit_async: batch k+1 is sorted while batch k is decided (two Work
+    sets); every batch's verdicts, the node state and ENTRY_NODE equal the
+    oracle's sequential replay."""
+    w = workloads.config3(R=3000, n=240_000, seed=8, split=split)
+    e = eng_mod.FlowEngine(w["cfg"])
+    e.load_flow_rules(w["flow"])
+    ora = so.OracleEngine(w["cfg"])
+    ora.load_flow_rules(w["flow"])
+    dbs = [eng_mod.DeviceBatch(e, hb) for hb in w["batches"]]
+    dvs = [eng_mod.DeviceVerdicts(e, hb.n, with_wait=True, with_rule=True) for hb in w["batches"]]
+    for db, dv in zip(dbs, dvs):
+        e.submit_device_async(db, dv)
+    e.sync()
+    for k, (hb, dv) in enumerate(zip(w["batches"], dvs)):
+        got = abi.HostVerdicts(hb.n)
+        got.status, got.wait_ms, got.rule_idx = dv.status.numpy(), dv.wait_ms.numpy(), dv.rule_idx.numpy()
+        parity.compare_verdicts(got, ora.submit(hb), f"async batch {k}")
+    parity.compare_nodes(e, ora, w["nodes"])
+    parity.compare_entry_node(e, ora)
+    # a synchronous submit after the asynchronous ones continues the same state
+    extra = workloads.config3(R=3000, n=20_000, seed=9, split=1, duration_ms=500)["batches"][0]
+    shifted = abi.HostBatch(extra.res_id, extra.ts_ms + 6000, extra.count, extra.flags, entry_ref=extra.entry_ref)
+    parity.compare_verdicts(e.submit(shifted), ora.submit(shifted), "sync after async")
+
+
+def test_async_error_reported_at_sync(eng_mod):
+    cfg = abi.default_config(max_resources=8, max_batch=16)
+    e = eng_mod.FlowEngine(cfg)
+    db = eng_mod.DeviceBatch(e, abi.HostBatch([9], [trace.T0], [1], [0]))   # resource outside the shard
+    dv = eng_mod.DeviceVerdicts(e, 1)
+    e.submit_device_async(db, dv)
+    with pytest.raises(eng_mod.EngineError):
+        e.sync()
+    e.submit(abi.HostBatch([1], [trace.T0], [1], [0]))    # still usable
+
+
 def test_config2_large_properties(eng_mod, so):
     """1M-event uniform batch: oracle parity plus the window invariant
     passes(hw) + passes(hw-1) <= count for every resource."""
