@@ -478,8 +478,19 @@ struct SegIO {          // sorted-order batch arrays
     const int64_t* ts; const int32_t* cnt; const uint8_t* flags;
     const int64_t* eref; const int64_t* cts;
     uint32_t arg_slots; const uint8_t* nargs; const uint8_t* atag; const uint64_t* abits; uint32_t n;
-    uint8_t* v_status; int32_t* v_wait; uint16_t* v_rule;
+    uint8_t* v_status; int32_t* v_wait; uint16_t* v_rule;     // sorted order (read back by exits)
+    const uint32_t* perm;                                       // sorted -> submission index, or null
+    uint8_t* o_status; int32_t* o_wait; uint16_t* o_rule;       // the caller's verdicts (submission order)
 };
+
+// final verdict of sorted event j, straight into the caller's arrays
+SF_HD void emit_verdict(const SegIO& io, uint32_t j, uint8_t status, int32_t wait, uint16_t rule) {
+    if (!io.perm) return;
+    const uint32_t i = io.perm[j];
+    io.o_status[i] = status;
+    if (io.o_wait) io.o_wait[i] = wait;
+    if (io.o_rule) io.o_rule[i] = rule;
+}
 
 SF_HD bool v_blocked(uint8_t v) { return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM; }
 
@@ -547,6 +558,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
             io.v_status[j] = status;
             if (io.v_wait) io.v_wait[j] = 0;
             if (io.v_rule) io.v_rule[j] = 0;
+            emit_verdict(io, j, status, 0, 0);
             continue;
         }
 
@@ -600,6 +612,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
         io.v_status[j] = status;
         if (io.v_wait) io.v_wait[j] = (int32_t)wait;
         if (io.v_rule) io.v_rule[j] = (uint16_t)rule_idx;
+        emit_verdict(io, j, status, (int32_t)wait, (uint16_t)rule_idx);
     }
 
     // write back

@@ -117,7 +117,7 @@ static int dalloc(void** p, size_t bytes) {
 static void free_work(Work& w) {
     void* ptrs[] = {w.pv_in, w.pv_out, w.wide, w.err, w.keys_in, w.keys_out, w.perm, w.head, w.head_scan,
                     w.seg_start, w.seg_res, w.n_seg, w.s_ts, w.s_cnt, w.s_flags, w.s_eref,
-                    w.s_cts, w.s_nargs, w.s_atag, w.s_abits, w.inv, w.v_status, w.v_wait,
+                    w.s_cts, w.s_nargs, w.s_atag, w.s_abits, w.v_status, w.v_wait,
                     w.v_rule, w.sort_tmp, w.scan_tmp,
                     w.segflag, w.seg_mode, w.light_list, w.lcounts, w.heavy_list, w.counters, w.pcg,
                     w.pscan_tmp, w.fill_tiles, w.fill_ntiles, w.acc_hw,
@@ -173,7 +173,7 @@ static int alloc_work(sf_engine* e, Work& w) {
     WALLOC(w.head, N * 4); WALLOC(w.head_scan, N * 4);
     WALLOC(w.seg_start, (N + 1) * 4); WALLOC(w.seg_res, N * 4); WALLOC(w.n_seg, 4);
     WALLOC(w.s_ts, N * 8); WALLOC(w.s_cnt, N * 4); WALLOC(w.s_flags, N);
-    WALLOC(w.s_eref, N * 8); WALLOC(w.s_cts, N * 8); WALLOC(w.inv, N * 4);
+    WALLOC(w.s_eref, N * 8); WALLOC(w.s_cts, N * 8);
     WALLOC(w.s_nargs, N); WALLOC(w.s_atag, N * SF_MAX_ARGS); WALLOC(w.s_abits, N * SF_MAX_ARGS * 8);
     WALLOC(w.v_status, N); WALLOC(w.v_wait, N * 4); WALLOC(w.v_rule, N * 2);
     {

@@ -124,7 +124,6 @@ struct Work {
     int64_t* s_ts; int32_t* s_cnt; uint8_t* s_flags;
     int64_t* s_eref; int64_t* s_cts;
     uint8_t* s_nargs; uint8_t* s_atag; uint64_t* s_abits;  // [slot][n]
-    uint32_t* inv;
     uint8_t* v_status; int32_t* v_wait; uint16_t* v_rule;
     void* sort_tmp; size_t sort_tmp_bytes;
     void* scan_tmp; size_t scan_tmp_bytes;

@@ -6,8 +6,8 @@
 //   radix sort     stable (key, payload) sort by resource: per-resource time order
 //                  is the input order (LeapArray semantics need it)
 //   k_heads + exclusive scan + k_segments   segment table of touched resources
-//   k_unpack       events into sorted order (SoA), inverse permutation, per-segment flags
-//   k_gather_exit  sorted position of each entry's exit
+//   k_unpack       events into sorted order (SoA), per-segment flags
+//   k_gather_exit  exits: sorted position of the entry (binary search in its segment), exit_of map
 //   pc scan        inclusive prefix of entry acquireCount (heavy window budgets)
 //   k_classify     light segments (by length class) -> lane interpreter; heavy -> window/skip algorithms
 //   k_fill_tiles   fill tiles of the heavy segments of each class
@@ -18,7 +18,8 @@
 //               k_heavy_fill    verdicts + per-window counter deltas from the pass bits
 //               k_heavy_apply   deltas applied to the LeapArray state in time order
 //   stream C:   k_decide_light  one lane per light segment (sf_decide.h)
-//   k_scatter   verdicts back to submission order
+// Every kernel writes its verdicts straight into the caller's arrays
+// (submission order, through the sort permutation).
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -59,7 +60,7 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t
 }
 
 __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* wide, uint32_t* perm, int64_t* s_ts,
-                         int32_t* s_cnt, uint8_t* s_flags, uint32_t* inv, uint8_t* s_nargs, uint8_t* s_atag,
+                         int32_t* s_cnt, uint8_t* s_flags, uint8_t* s_nargs, uint8_t* s_atag,
                          uint64_t* s_abits, const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
@@ -69,7 +70,6 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* wide, u
     const uint8_t f = (uint8_t)v.flags;
     perm[j] = i;
     s_ts[j] = *wide ? b.ts[i] : b.ts[0] + (int64_t)v.dts; s_cnt[j] = c; s_flags[j] = f;
-    if (inv) inv[i] = j;
     if (!(f & SF_EV_EXIT) && ((f & SF_EV_PRIO) || c <= 0)) {
         uint32_t s = head_scan[j] + head[j] - 1;
         atomicOr(&segflag[s], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u));
@@ -97,17 +97,25 @@ __global__ void k_segments(const uint32_t* keys, const uint32_t* head, const uin
     if (j == n - 1) { uint32_t ns = pos[j] + head[j]; *n_seg = ns; seg_start[ns] = n; }
 }
 
-__global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint32_t* inv, int64_t* s_eref,
+// Exits only: the sorted position of each exit's entry.  The sort is stable
+// and the segment holds one resource's events in submission order, so the
+// entry is found by a binary search of the segment's submission indices (no
+// inverse permutation scattered over the whole batch).  Forward map exit_of
+// for THREAD-grade liveness; s_cts for entries of earlier batches.
+__global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint8_t* s_flags, const uint32_t* head,
+                              const uint32_t* head_scan, const uint32_t* seg_start, int64_t* s_eref,
                               int64_t* s_cts, uint32_t* exit_of, int32_t* err) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= b.n) return;
-    uint32_t i = perm[j];
-    int64_t r = b.eref[i];
-    if (r >= (int64_t)b.n) { *err = SF_ERR_INVALID; r = -1; }
-    const int64_t rs = (r >= 0) ? (int64_t)inv[r] : -1;
-    s_eref[j] = rs;
-    s_cts[j] = b.cts ? b.cts[i] : 0;
-    if (rs >= 0 && (b.flags[i] & SF_EV_EXIT)) exit_of[rs] = j;   // forward map (THREAD-grade liveness)
+    if (j >= b.n || !(s_flags[j] & SF_EV_EXIT)) return;
+    const uint32_t i = perm[j];
+    const int64_t r = b.eref[i];
+    if (r < 0) { s_eref[j] = -1; s_cts[j] = b.cts ? b.cts[i] : 0; return; }
+    uint32_t a = seg_start[head_scan[j] + head[j] - 1], e = j;          // entry in [segment start, j)
+    if (r >= (int64_t)i) { *err = SF_ERR_INVALID; s_eref[j] = -1; s_cts[j] = 0; return; }
+    while (a < e) { const uint32_t m = (a + e) >> 1; if ((int64_t)perm[m] < r) a = m + 1; else e = m; }
+    if (a >= j || (int64_t)perm[a] != r) { *err = SF_ERR_INVALID; s_eref[j] = -1; s_cts[j] = 0; return; }
+    s_eref[j] = a;
+    exit_of[a] = j;
 }
 
 struct EntryCount {     // acquireCount of entries, 0 for exits (input of the pc scan)
@@ -517,19 +525,20 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
             vs[k] = e.status; vw[k] = e.wait;
             if (e.touch) gp.add(e);
         }
-        if (full) {
-            store16(io.v_status + base, vs, FG);
-            if (io.v_wait) store16(io.v_wait + base, vw, FG * 4);
-            if (io.v_rule) store16(io.v_rule + base, vr, FG * 2);
-        } else {
+        // verdicts straight to the caller's arrays (submission order)
+        uint32_t pm[FG];
+        if (full) load16(pm, io.perm + base, FG * 4);
+        else {
 #pragma unroll
-            for (int k = 0; k < FG; k++) {
-                const uint32_t j = base + (uint32_t)k;
-                if (j < a || j >= b) continue;
-                io.v_status[j] = vs[k];
-                if (io.v_wait) io.v_wait[j] = vw[k];
-                if (io.v_rule) io.v_rule[j] = 0;
-            }
+            for (int k = 0; k < FG; k++) pm[k] = (base + (uint32_t)k >= a && base + (uint32_t)k < b) ? io.perm[base + k] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < FG; k++) {
+            const uint32_t j = base + (uint32_t)k;
+            if (j < a || j >= b) continue;
+            io.o_status[pm[k]] = vs[k];
+            if (io.o_wait) io.o_wait[pm[k]] = vw[k];
+            if (io.o_rule) io.o_rule[pm[k]] = vr[k];
         }
         if (!gp.n_touch) continue;
         // window rows of the group's first and last event (time-sorted): usually one
@@ -582,16 +591,6 @@ __global__ void k_heavy_apply(DevState st, HeavyCtx hc, StreamCtx sc, const uint
     else if (!stream_at(sc, t, &s)) return;
     if (hc.seg_mode[s] < SM_QPS) return;
     heavy_apply(st, hc, s, hc.seg_res[s], seg_nhw[s], seg_nsec[s]);
-}
-
-__global__ void k_scatter(const uint32_t* perm, uint32_t n, const uint8_t* vs, const int32_t* vw,
-                          const uint16_t* vr, DevVerdicts out) {
-    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    uint32_t i = perm[j];
-    out.status[i] = vs[j];
-    if (out.wait) out.wait[i] = vw[j];
-    if (out.rule) out.rule[i] = vr[j];
 }
 
 static inline unsigned blocks(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
@@ -652,12 +651,11 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
                        w.seg_start, w.seg_res, w.n_seg, w.segflag);
     if (timing) hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.wide, w.perm, w.s_ts, w.s_cnt,
-                       w.s_flags, b.eref ? w.inv : nullptr, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan,
-                       w.segflag);
+                       w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag);
     hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
     if (b.eref)
-        hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.inv, w.s_eref,
-                           w.s_cts, w.exit_of, st.err);
+        hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags, w.head,
+                           w.head_scan, w.seg_start, w.s_eref, w.s_cts, w.exit_of, st.err);
     PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
     e = rocprim::inclusive_scan(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n, rocprim::plus<int64_t>(), s);
     if (e != hipSuccess) return e;
@@ -682,13 +680,13 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
                          hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing) {
     const uint32_t n = b.n;
     if (n == 0) return hipSuccess;
-    const unsigned T = 256;
     SegIO io;
     io.ts = w.s_ts; io.cnt = w.s_cnt; io.flags = w.s_flags;
     io.eref = b.eref ? w.s_eref : nullptr; io.cts = b.eref ? w.s_cts : nullptr;
     io.arg_slots = b.arg_slots; io.nargs = (b.arg_slots && b.nargs) ? w.s_nargs : nullptr;
     io.atag = w.s_atag; io.abits = w.s_abits; io.n = n;
     io.v_status = w.v_status; io.v_wait = w.v_wait; io.v_rule = w.v_rule;
+    io.perm = w.perm; io.o_status = out.status; io.o_wait = out.wait; io.o_rule = out.rule;
     HeavyCtx hc = heavy_ctx(w);
     if (timing) hc.hticks = w.hticks;
     const uint32_t max_seg = n < st.R ? n : st.R;
@@ -727,10 +725,8 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     hipStreamWaitEvent(s, ev[6], 0);
     hipStreamWaitEvent(s, ev[9], 0);
     hipEventRecord(ev[13], s);
-    if (timing) hipEventRecord(ev[3], s);
-    hipLaunchKernelGGL(k_scatter, dim3(blocks(n, T)), dim3(T), 0, s, w.perm, n, w.v_status, w.v_wait,
-                       w.v_rule, out);
-    if (timing) hipEventRecord(ev[4], s);
+    // every kernel wrote its verdicts straight into submission order (no scatter pass)
+    if (timing) { hipEventRecord(ev[3], s); hipEventRecord(ev[4], s); }
     return hipGetLastError();
 }
 
