@@ -252,11 +252,15 @@ __device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) 
     return ((unsigned long long)b << 32) | a;
 }
 
-#ifdef SF_STREAM_PROF
-__device__ uint64_t thr_prof[3];
-#endif
 __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32_t q0, uint32_t lo, uint32_t hi,
-                           double M, int64_t IM, int64_t& T, unsigned long long* pbits) {
+                           double M, int64_t IM, int64_t& T, unsigned long long* pbits
+#ifdef SF_STREAM_PROF
+                           , uint64_t* prof
+#endif
+                           ) {
+#ifdef SF_STREAM_PROF
+    const uint64_t ta = __builtin_amdgcn_s_memtime();
+#endif
     const int lane = (int)(threadIdx.x & 63);
     const uint32_t nwin = min((hi - q0 + 63) / 64, (uint32_t)THR_WPC);
     bool far_marked = false;
@@ -269,21 +273,17 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
     const unsigned long long r_inw = L.win[buf][wl].inw;
     const unsigned long long bigm = __ballot((uint32_t)lane < nwin && (r_flags & 2u));   // windows needing the exact walk
     const uint32_t slot0 = (q0 - lo) >> 6;
+    // live-exit words of the chunk's windows in registers (lane w <-> window w);
+    // only this chunk's own passes can add to them (exits inside the chunk)
+    unsigned long long r_lx = (uint32_t)lane < nwin ? L.lx[(slot0 + lane) % LX_WORDS] : 0ull;
+    const uint32_t qend = q0 + 64u * nwin;
     uint32_t w = 0;
 #ifdef SF_STREAM_PROF
-    uint64_t pa = 0, pb = 0, pc = 0;
+    const uint64_t tb = __builtin_amdgcn_s_memtime();
 #endif
     while (w < nwin) {
-#ifdef SF_STREAM_PROF
-        const uint64_t c0 = __builtin_amdgcn_s_memtime();
-#endif
         const uint32_t q = q0 + 64 * w;
         const uint32_t slot = (slot0 + w) % LX_WORDS;
-        // every LDS read of the window issued together: the live-exit words of
-        // windows w, w+1, ... (lane k <-> window w+k) and the window's event data
-        const uint32_t wn_ = w + (uint32_t)lane;
-        const bool inr = wn_ < nwin;
-        const unsigned long long v = L.lx[(slot0 + (inr ? wn_ : w)) % LX_WORDS];
         const uint32_t xo = L.xo[buf][64 * w + lane];
         const int32_t c = L.cn[buf][64 * w + lane];
         const int eln = L.el[buf][64 * w + lane];
@@ -293,12 +293,12 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
         const bool tsmall = T >= (int64_t)INT32_MIN + 64 && T + (int64_t)THR_CBIG + 64 <= (int64_t)INT32_MAX;
         if (room0 <= 0 && tsmall) {
             // saturated: skip the windows with no live exit (all their entries block)
-            const unsigned long long stop = __ballot(inr && v != 0ull) | (bigm >> w);
+            const unsigned long long stop = (__ballot((uint32_t)lane < nwin && r_lx != 0ull) | bigm) >> w;
             if (!stop) { w = nwin; break; }
             const uint32_t k = (uint32_t)(__ffsll((long long)stop) - 1);
             if (k > 0) { w += k; continue; }
         }
-        unsigned long long ml = rl64(v, 0);                    // live exits of this window
+        unsigned long long ml = rl64(r_lx, (int)w);            // live exits of this window
         const int32_t maxrc = __builtin_amdgcn_readlane(r_maxrc, (int)w);
         unsigned long long pmask = 0;
         const bool nowrap = !(flags & 2u) && tsmall;
@@ -350,9 +350,6 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
             }
         }
         T = uniform64(T);
-#ifdef SF_STREAM_PROF
-        const uint64_t c1 = __builtin_amdgcn_s_memtime();
-#endif
         if (pmask) {
             // exits of the passed entries beyond this window turn live (one vector step)
             const bool mk = ((pmask >> lane) & 1ull) && xo != XO_NONE && xo < hi && xo >= q + 64;
@@ -360,16 +357,17 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
             if (mk) fm2 = thr_mark_exit(L, lxfar, xo, q, lo);
             far_marked |= __ballot(fm2) != 0;
             if ((uint32_t)lane == w) pst = pmask;          // pass bits staged: lane w <-> window w
+            if (__ballot(mk && xo < qend))                 // exits inside this chunk: refresh its words
+                r_lx |= ((uint32_t)lane > w && (uint32_t)lane < nwin) ? L.lx[(slot0 + lane) % LX_WORDS] : 0ull;
         }
         if (lane == 0) L.lx[slot] = 0ull;                  // consumed: reused LX_WORDS windows later
         w++;
 #ifdef SF_STREAM_PROF
-        const uint64_t c2 = __builtin_amdgcn_s_memtime();
-        pa += c1 - c0; pb += c2 - c1; pc++;
+        prof[3]++;
 #endif
     }
 #ifdef SF_STREAM_PROF
-    thr_prof[0] += pa; thr_prof[1] += pb; thr_prof[2] += pc;
+    const uint64_t tc = __builtin_amdgcn_s_memtime();
 #endif
     if (pst) {                                             // the chunk's pass bits: one vector step
         const uint32_t q = q0 + 64u * (uint32_t)lane, sh = q & 63;
@@ -380,6 +378,10 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
         __builtin_amdgcn_s_waitcnt(0);
     }
+#ifdef SF_STREAM_PROF
+    const uint64_t td = __builtin_amdgcn_s_memtime();
+    prof[0] += tb - ta; prof[1] += tc - tb; prof[2] += td - tc;
+#endif
 }
 
 // ------------------------------------------------------------------ RateLimiter
@@ -499,14 +501,18 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
         if (h > 0) thr_prepare(L, 0, io, hc.exit_of, hc.lxfar, lo, lo, hi, h);
         __syncthreads();
 #ifdef SF_STREAM_PROF
-        uint64_t t_work = 0, t_bar = 0;
+        uint64_t t_work = 0, t_bar = 0, tprof[4] = {0, 0, 0, 0};
 #endif
         for (uint32_t k = 0; k < ntc; k++) {
             const uint32_t q0 = lo + k * THR_CH;
 #ifdef SF_STREAM_PROF
             const uint64_t c0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef SF_STREAM_PROF
+            if (h == 0) thr_decide(L, k & 1, hc.lxfar, q0, lo, hi, M, IM, T, hc.passbits, tprof);
+#else
             if (h == 0) thr_decide(L, k & 1, hc.lxfar, q0, lo, hi, M, IM, T, hc.passbits);
+#endif
             else if (k + 1 < ntc) thr_prepare(L, (k + 1) & 1, io, hc.exit_of, hc.lxfar, q0 + THR_CH, lo, hi, h);
 #ifdef SF_STREAM_PROF
             const uint64_t c1 = __builtin_amdgcn_s_memtime();
@@ -518,9 +524,9 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
         }
 #ifdef SF_STREAM_PROF
         if ((threadIdx.x & 63) == 0)
-            printf("SF_STREAM_PROF seg %u wave %d events %u chunks %u: work %lu barrier %lu cycles; decide %lu mark %lu windows %lu\n",
-                   s, h, hi - lo, ntc, (unsigned long)t_work, (unsigned long)t_bar, (unsigned long)thr_prof[0],
-                   (unsigned long)thr_prof[1], (unsigned long)thr_prof[2]);
+            printf("SF_STREAM_PROF seg %u wave %d events %u chunks %u: work %lu barrier %lu cycles; prologue %lu loop %lu epilogue %lu windows %lu\n",
+                   s, h, hi - lo, ntc, (unsigned long)t_work, (unsigned long)t_bar, (unsigned long)tprof[0],
+                   (unsigned long)tprof[1], (unsigned long)tprof[2], (unsigned long)tprof[3]);
 #endif
     } else {                                                     // SM_RL
         int64_t* tsb = (int64_t*)smem;                           // [2][HS_CH]
