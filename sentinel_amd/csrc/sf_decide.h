@@ -186,6 +186,28 @@ struct NodeWin {
             visit(i, [&](Bucket& b) { if (!(wsub(now, b.ws) > interval)) s = wadd(s, b.pass); });
         return s;
     }
+    // ArrayMetric sums / extremes over the valid buckets, after the roll (ArrayMetric.java:68-162)
+    template <class G> SF_HD int64_t sec_sum(int64_t now, G get) {
+        sec_current(now);
+        int64_t s = 0;
+        for (int i = 0; i < S; i++)
+            visit(i, [&](Bucket& b) { if (!(wsub(now, b.ws) > interval)) s = wadd(s, get(b)); });
+        return s;
+    }
+    SF_HD int64_t sec_min_rt(int64_t now) {              // ArrayMetric.minRt :151-162
+        sec_current(now);
+        int64_t rt = max_rt;
+        for (int i = 0; i < S; i++)
+            visit(i, [&](Bucket& b) { if (!(wsub(now, b.ws) > interval) && b.min_rt < rt) rt = b.min_rt; });
+        return rt > 1 ? rt : 1;
+    }
+    SF_HD int64_t sec_max_success(int64_t now) {         // ArrayMetric.maxSuccess :81-92
+        sec_current(now);
+        int64_t m = 0;
+        for (int i = 0; i < S; i++)
+            visit(i, [&](Bucket& b) { if (!(wsub(now, b.ws) > interval) && b.succ > m) m = b.succ; });
+        return m > 1 ? m : 1;
+    }
     SF_HD int64_t sec_window_pass(int64_t t) {            // ArrayMetric.getWindowPass :324-330
         int idx = (int)((t / wl) % S);
         int64_t v = 0;
@@ -494,8 +516,37 @@ SF_HD void emit_verdict(const SegIO& io, uint32_t j, uint8_t status, int32_t wai
 
 SF_HD bool v_blocked(uint8_t v) { return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM; }
 
+template <int MAXS> struct SysCtx { SysRule r; NodeWin<MAXS>* en; };   // en: Constants.ENTRY_NODE
+
+// SystemRuleManager.checkSystem :291-340 and checkBbr :342-348: -1 pass, else
+// the reason (0 qps, 1 thread, 2 rt, 3 load, 4 cpu).  Every read rolls the
+// ENTRY_NODE second window at `now`, like the reference's.
 template <int MAXS>
-SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi) {
+SF_HD int sys_check(SysCtx<MAXS>& sc, int64_t now, int32_t count) {
+    if (!sc.r.check) return -1;
+    NodeWin<MAXS>& n = *sc.en;
+    const double qps = (double)n.sec_sum_pass(now) / n.interval_sec;                 // StatisticNode.passQps
+    if (qps + count > sc.r.qps) return 0;
+    const int32_t th = (int32_t)n.threads;                                           // curThreadNum
+    if (th > sc.r.max_thread) return 1;
+    const int64_t succ = n.sec_sum(now, [](const Bucket& b) { return b.succ; });
+    const double rt = succ == 0 ? 0.0
+                                : (double)n.sec_sum(now, [](const Bucket& b) { return b.rt; }) * 1.0 / (double)succ;
+    if (rt > (double)sc.r.max_rt) return 2;
+    if (sc.r.load_set && sc.r.cur_load > sc.r.highest_load) {
+        const double max_succ_qps = (double)n.sec_max_success(now) * n.S / n.interval_sec;
+        if (th > 1 && th > max_succ_qps * (double)n.sec_min_rt(now) / 1000) return 3;
+    }
+    if (sc.r.cpu_set && sc.r.cur_cpu > sc.r.highest_cpu) return 4;
+    return -1;
+}
+
+// SYS: time-ordered replay with SystemRules (the caller passes one event at a
+// time in submission order, validates exit references, and owns the global
+// ENTRY_NODE in sys->en).
+template <int MAXS, bool SYS = false>
+SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi,
+                          SysCtx<MAXS>* sys = nullptr) {
     NodeWin<MAXS> nd;
     nd.S = st.S; nd.wl = st.wl; nd.interval = st.interval; nd.max_rt = st.max_rt;
     nd.interval_sec = st.interval / 1000.0;
@@ -531,7 +582,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
             int64_t ref = io.eref ? io.eref[j] : -1;
             bool blocked; int64_t create_ts;
             if (ref >= 0) {
-                if (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT)) {   // entry of another resource / order
+                if (!SYS && (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT))) {   // entry of another resource / order
                     *st.err = SF_ERR_INVALID;
 #if !defined(__HIP_DEVICE_COMPILE__) && defined(SF_HOST_DEBUG)
                     printf("bad ref j=%u ref=%lld lo=%u flags=%d\n", j, (long long)ref, lo, ref>=0? io.flags[ref]:-1);
@@ -547,6 +598,11 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
                 nd.add_rt_success(now, rt, c);                  // recordCompleteFor :167-178
                 nd.threads--;
                 if (fl & SF_EV_ERROR) nd.add_exception(now, c);
+                if (SYS && (fl & SF_EV_IN)) {                   // Constants.ENTRY_NODE
+                    sys->en->add_rt_success(now, rt, c);
+                    sys->en->threads--;
+                    if (fl & SF_EV_ERROR) sys->en->add_exception(now, c);
+                }
                 if (pm_exists)                                  // ParamFlowStatisticExitCallback
                     for (uint32_t a = 0; a < na; a++)
                         if (a < 8 && (pm_init >> a) & 1)
@@ -564,8 +620,12 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
 
         bool blocked = false, prio_wait = false;
         status = SF_V_PASS;
+        if (SYS && (fl & SF_EV_IN)) {                           // SystemSlot -> SystemRuleManager.checkSystem
+            const int reason = sys_check(*sys, now, c);
+            if (reason >= 0) { blocked = true; status = SF_V_BLOCK_SYSTEM; rule_idx = reason; }
+        }
         // ParamFlowSlot.checkFlow :82-103
-        if (nprules) {
+        if (!blocked && nprules) {
             pm_exists = true;
             for (int k = 0; k < nprules && !blocked; k++) {
                 DevParamRule& pr = st.prules[p0 + k];
@@ -600,10 +660,15 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
         // StatisticSlot.entry accounting :64-123
         if (blocked) {
             nd.add_block(now, c);
+            if (SYS && (fl & SF_EV_IN)) sys->en->add_block(now, c);
         } else {
             nd.threads++;
+            if (SYS && (fl & SF_EV_IN)) sys->en->threads++;
             if (prio_wait) status = SF_V_PRIORITY_WAIT;
-            else { nd.add_pass(now, c); status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS; }
+            else {
+                nd.add_pass(now, c); status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS;
+                if (SYS && (fl & SF_EV_IN)) sys->en->add_pass(now, c);
+            }
             if (pm_exists)
                 for (uint32_t a = 0; a < na; a++)
                     if (a < 8 && (pm_init >> a) & 1)

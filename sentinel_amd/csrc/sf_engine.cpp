@@ -47,6 +47,7 @@ struct sf_engine {
     unsigned pending = 0;           // Work sets with an asynchronous batch not yet checked by sf_sync
     bool used[2] = {false, false};
     hipEvent_t ev_sorted[2]{}, ev_done[2]{};
+    SysRule sys{};                  // SystemRuleManager statics; sys.check: batches replay in order
     // rules
     std::vector<uint32_t> flow_pos;        // loaded valid rule index -> CSR position
     uint32_t n_flow = 0, n_prule = 0;
@@ -448,13 +449,39 @@ int sf_load_param_rules(sf_engine* e, const sf_param_rule* rules, uint32_t n, co
     return SF_OK;
 }
 
+// SystemRuleManager.loadSystemConf (SystemRuleManager.java:267-289) through
+// SystemPropertyListener.configUpdate (:173-196): the minimum of every set
+// threshold; checkSystemStatus follows the last rule, as in the reference.
 int sf_load_system_rules(sf_engine* e, const sf_system_rule* rules, uint32_t n) {
-    if (!e) return fail(SF_ERR_INVALID, "null engine");
-    (void)rules;
-    if (n) return fail(SF_ERR_UNSUPPORTED, "SystemRule (global ENTRY_NODE coupling) is not on the GPU path yet");
+    if (!e || (n && !rules)) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }
+    SysRule r{};
+    r.qps = r.highest_load = r.highest_cpu = 1.7976931348623157e308;
+    r.max_rt = r.max_thread = INT64_MAX;
+    r.cur_load = e->sys.cur_load; r.cur_cpu = e->sys.cur_cpu;
+    for (uint32_t i = 0; i < n; i++) {
+        const sf_system_rule& x = rules[i];
+        int check = 0;
+        if (x.highest_system_load >= 0) { r.highest_load = std::fmin(r.highest_load, x.highest_system_load); r.load_set = 1; check = 1; }
+        if (x.highest_cpu_usage >= 0 && x.highest_cpu_usage <= 1) {
+            r.highest_cpu = std::fmin(r.highest_cpu, x.highest_cpu_usage); r.cpu_set = 1; check = 1;
+        }
+        if (x.avg_rt >= 0) { if (x.avg_rt < r.max_rt) r.max_rt = x.avg_rt; check = 1; }
+        if (x.max_thread >= 0) { if (x.max_thread < r.max_thread) r.max_thread = x.max_thread; check = 1; }
+        if (x.qps >= 0) { r.qps = std::fmin(r.qps, x.qps); check = 1; }
+        r.check = check;
+    }
+    e->sys = r;
     return SF_OK;
 }
-int sf_set_system_status(sf_engine* e, double, double) { return e ? SF_OK : SF_ERR_INVALID; }
+// SystemStatusListener readings (system load average, cpu usage): fixed inputs of a replay
+int sf_set_system_status(sf_engine* e, double avg_load, double cpu_usage) {
+    if (!e) return fail(SF_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->sys.cur_load = avg_load; e->sys.cur_cpu = cpu_usage;
+    return SF_OK;
+}
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -469,8 +496,8 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     DevBatch b{};
     b.n = n; b.arg_slots = in->arg_slots;
     hipStream_t s = e->stream, ss = e->serial ? e->stream : e->sstream;
-    // asynchronous only for HBM-resident batches and verdicts
-    async = async && in->mem != SF_MEM_HOST && out->mem != SF_MEM_HOST;
+    // asynchronous only for HBM-resident batches and verdicts, without SystemRules
+    async = async && in->mem != SF_MEM_HOST && out->mem != SF_MEM_HOST && !e->sys.check;
     if (!async) { const int rc = drain(e); if (rc) return rc; }
     if (async && !e->w_ready[1]) {                 // second Work set on first asynchronous use
         HIP_TRY(hipStreamSynchronize(s));
@@ -538,6 +565,33 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         dv.rule = out->rule_idx ? (uint16_t*)(base + align_up(n) + align_up((size_t)n * 4)) : nullptr;
     } else {
         dv.status = out->status; dv.wait = out->wait_ms; dv.rule = out->rule_idx;
+    }
+    if (e->sys.check) {
+        // SystemRules couple every IN entry to the global ENTRY_NODE: exact
+        // replay in submission order on the main stream (k_replay)
+        HIP_TRY(hipMemsetAsync(w.err, 0, sizeof(int32_t), ss));
+        HIP_TRY(hipEventRecord(e->ev_sorted[slot], ss));
+        HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
+        DevState stl = e->st;
+        stl.err = w.err;
+        hipError_t le = launch_replay(stl, b, dv, e->cfg.shard_count, e->cfg.shard_index, e->sys, e->en, s);
+        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("replay: ") + hipGetErrorString(le));
+        HIP_TRY(hipEventRecord(e->ev_done[slot], s));
+        e->used[slot] = true;
+        e->last = slot;
+        e->stats.n_events = n;
+        e->stats.n_launches++;
+        if (out->mem == SF_MEM_HOST) {
+            HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, s));
+            if (dv.wait) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+            if (dv.rule) HIP_TRY(hipMemcpyAsync(out->rule_idx, dv.rule, (size_t)n * 2, hipMemcpyDeviceToHost, s));
+        }
+        int32_t err = 0;
+        HIP_TRY(hipMemcpyAsync(&err, w.err, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (err) return fail(err, err == SF_ERR_CAPACITY ? "param table capacity exceeded"
+                                                         : "invalid batch (resource outside shard or bad entry_ref)");
+        return SF_OK;
     }
     // sort phase on the sort stream, into this batch's Work set (after the
     // decide phase of the batch that used it last)

@@ -81,6 +81,14 @@ struct DevState {
 
 // Constants.ENTRY_NODE (Constants.java:66): the ClusterNode of all inbound
 // traffic, updated by StatisticSlot for EntryType.IN (StatisticSlot.java:64-178)
+// SystemRuleManager statics (SystemRuleManager.java:68-101), as loadSystemConf
+// leaves them (:267-289), and the SystemStatusListener readings.
+struct SysRule {
+    int32_t check, load_set, cpu_set;
+    double qps, highest_load, highest_cpu, cur_load, cur_cpu;
+    int64_t max_rt, max_thread;
+};
+
 struct EntryNode {
     Bucket second[SF_MAX_SAMPLE_COUNT];
     Bucket minute[SF_MINUTE_BUCKETS];
@@ -174,6 +182,8 @@ hipError_t launch_en_pack_vals(const EntryNode* en, int S, const int64_t* gws, i
 hipError_t launch_snapshot(const DevState& st, int64_t now, uint32_t shard_count, uint32_t shard_index,
                            uint32_t* counts, uint32_t* offsets, sf_metric_row* out, uint32_t cap, uint32_t* total,
                            void* scan_tmp, size_t scan_bytes, hipStream_t s);
+hipError_t launch_replay(const DevState& st, const DevBatch& b, const DevVerdicts& out, uint32_t shard_count,
+                         uint32_t shard_index, const SysRule& sr, EntryNode* en, hipStream_t s);
 hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,
                        uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing);
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,

@@ -593,6 +593,57 @@ __global__ void k_heavy_apply(DevState st, HeavyCtx hc, StreamCtx sc, const uint
     heavy_apply(st, hc, s, hc.seg_res[s], seg_nhw[s], seg_nsec[s]);
 }
 
+// SystemRules loaded: every IN entry's check reads the global ENTRY_NODE,
+// which every earlier IN event updates, so the batch is replayed in
+// submission order by one lane (SystemRuleManager.checkSystem before
+// ParamFlowSlot and FlowSlot, ENTRY_NODE accounted inline; exact, serial).
+template <int MAXS>
+__global__ void __launch_bounds__(64) k_replay(DevState st, SegIO io, DevBatch b, uint32_t shard_count,
+                                               uint32_t shard_index, SysRule sr, EntryNode* en) {
+    if (threadIdx.x != 0) return;
+    NodeWin<MAXS> e;
+    e.S = st.S; e.wl = st.wl; e.interval = st.interval; e.max_rt = st.max_rt;
+    e.interval_sec = st.interval / 1000.0;
+    for (int i = 0; i < MAXS; i++) {
+        e.sec[i] = i < st.S ? en->second[i] : fresh_bucket(WS_NONE, st.max_rt);
+        e.bor[i].ws = WS_NONE; e.bor[i].pass = 0;          // ENTRY_NODE never borrows
+    }
+    e.threads = en->threads;
+    e.gmin = en->minute; e.mi = -1; e.mdirty = 0; e.mb = fresh_bucket(WS_NONE, st.max_rt);
+    SysCtx<MAXS> sys{sr, &e};
+    for (uint32_t j = 0; j < b.n; j++) {
+        const uint32_t r = b.res[j], l = r / shard_count;
+        if (r % shard_count != shard_index || l >= st.R) { *st.err = SF_ERR_INVALID; continue; }
+        if ((b.flags[j] & SF_EV_EXIT) && b.eref) {              // the entry: earlier, same resource, an entry
+            const int64_t ref = b.eref[j];
+            if (ref >= 0 && (ref >= (int64_t)j || b.res[ref] != r || (b.flags[ref] & SF_EV_EXIT))) {
+                *st.err = SF_ERR_INVALID;
+                continue;
+            }
+        }
+        decide_segment<MAXS, true>(st, io, l, j, j + 1, &sys);
+    }
+    for (int i = 0; i < MAXS; i++) if (i < st.S) en->second[i] = e.sec[i];
+    e.min_flush();
+    en->threads = e.threads;
+}
+
+hipError_t launch_replay(const DevState& st, const DevBatch& b, const DevVerdicts& out, uint32_t shard_count,
+                         uint32_t shard_index, const SysRule& sr, EntryNode* en, hipStream_t s) {
+    if (b.n == 0) return hipSuccess;
+    SegIO io{};
+    io.ts = b.ts; io.cnt = b.cnt; io.flags = b.flags; io.eref = b.eref; io.cts = b.cts;
+    io.arg_slots = b.arg_slots; io.nargs = b.nargs; io.atag = b.atag; io.abits = b.abits; io.n = b.n;
+    io.v_status = out.status; io.v_wait = out.wait; io.v_rule = out.rule;   // submission order: exits read their entry's verdict
+    io.perm = nullptr;
+    if (st.S <= 2)
+        hipLaunchKernelGGL(k_replay<2>, dim3(1), dim3(64), 0, s, st, io, b, shard_count, shard_index, sr, en);
+    else
+        hipLaunchKernelGGL(k_replay<SF_MAX_SAMPLE_COUNT>, dim3(1), dim3(64), 0, s, st, io, b, shard_count, shard_index,
+                           sr, en);
+    return hipGetLastError();
+}
+
 static inline unsigned blocks(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 using PcIter = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, EntryCount, int64_t>;

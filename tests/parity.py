@@ -33,8 +33,15 @@ def compare_rule_states(eng, ora, n_rules, what=""):
         assert ta == tb, f"{what}: rule {k} state engine={ta} oracle={tb}"
 
 
-def run_both(make_engine, make_oracle, cfg, flow_rules=(), param_rules=(), items=(), batches=()):
+def run_both(make_engine, make_oracle, cfg, flow_rules=(), param_rules=(), items=(), batches=(), system=(),
+             status=None):
     eng, ora = make_engine(cfg), make_oracle(cfg)
+    if status is not None:
+        eng.set_system_status(*status)
+        ora.set_system_status(*status)
+    if system:
+        eng.load_system_rules(list(system))
+        ora.load_system_rules(list(system))
     if flow_rules:
         eng.load_flow_rules(list(flow_rules))
         ora.load_flow_rules(list(flow_rules))

@@ -113,6 +113,17 @@ def test_async_error_reported_at_sync(eng_mod):
     e.submit(abi.HostBatch([1], [trace.T0], [1], [0]))    # still usable
 
 
+@pytest.mark.parametrize("kind", ["qps", "thread", "rt", "load", "cpu"])
+def test_system_rule(eng_mod, so, kind):
+    """SystemRuleManager.checkSystem on the global ENTRY_NODE (k_replay):
+    verdicts (SF_V_BLOCK_SYSTEM with the reason in rule_idx), every node, the
+    ENTRY_NODE and the controller states equal the oracle's."""
+    w = workloads.system(kind)
+    eng, ora, outs = workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
+    blocked = sum(int((o[1].status == abi.V_BLOCK_SYSTEM).sum()) for o in outs)
+    assert blocked > 0, "the SystemRule never fired: the workload does not exercise it"
+
+
 def test_config2_large_properties(eng_mod, so):
     """1M-event uniform batch: oracle parity plus the window invariant
     passes(hw) + passes(hw-1) <= count for every resource."""

@@ -133,6 +133,33 @@ def param_mixed(seed=21, R=12, n=30000):
                 param=prules, items=items, batches=[b], nodes=list(range(R)), n_flow=len(flow))
 
 
+def system(kind, seed=41):
+    """SystemRule over mixed traffic (SystemRuleManager.checkSystem, global
+    ENTRY_NODE): config 4's inbound-QPS rule at 0.8x the offered rate, or the
+    thread / RT / load (BBR) / cpu thresholds over THREAD-grade traffic with
+    exits.  Replayed on the GPU in submission order (k_replay)."""
+    rng = np.random.default_rng(seed)
+    if kind == "qps":
+        rules, batch = trace.param_zipf(30, 40_000, 3000, duration_ms=4000, seed=seed)
+        offered = batch.n / 4.0                             # inbound events per second
+        sysr = [abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=0.8 * offered,
+                                   avg_rt=-1, max_thread=-1)]
+        return dict(cfg=abi.default_config(max_resources=30, max_batch=batch.n, param_capacity=1 << 16),
+                    param=rules, batches=[batch], nodes=list(range(30)), system=sysr, status=(0.0, 0.0))
+    R = 60
+    full = trace.mixed_zipf(R, 30_000, duration_ms=3000, seed=seed)
+    rules = trace.mixed_rules(R, seed=seed)
+    thr = {"thread": (-1.0, -1.0, -1.0, -1, 4000), "rt": (-1.0, -1.0, -1.0, 15, -1),
+           "load": (0.5, -1.0, -1.0, -1, -1), "cpu": (-1.0, 0.6, -1.0, -1, -1)}[kind]
+    status = {"load": (2.0, 0.1), "cpu": (0.3, 0.9)}.get(kind, (0.0, 0.0))
+    sysr = [abi.sf_system_rule(highest_system_load=thr[0], highest_cpu_usage=thr[1], qps=thr[2],
+                               avg_rt=thr[3], max_thread=thr[4])]
+    cuts = np.linspace(0, full.n, 3).astype(int)
+    batches = [full.subset(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=full.n), flow=rules, batches=batches,
+                nodes=list(range(R)), n_flow=len(rules), system=sysr, status=status)
+
+
 ALL = {
     "config1": config1, "config2": config2, "config3": config3, "config4": config4,
     "prioritized": prioritized, "multi_rule": multi_rule, "param_mixed": param_mixed,
@@ -144,7 +171,8 @@ def run(make_engine, make_oracle, w):
     from tests import parity
     eng, ora, outs = parity.run_both(make_engine, make_oracle, w["cfg"], flow_rules=w.get("flow", ()),
                                      param_rules=w.get("param", ()), items=w.get("items", ()),
-                                     batches=w["batches"])
+                                     batches=w["batches"], system=w.get("system", ()),
+                                     status=w.get("status"))
     for k, (a, b) in enumerate(outs):
         parity.compare_verdicts(a, b, f"batch{k}")
     parity.compare_nodes(eng, ora, w["nodes"], sample_count=w["cfg"].sample_count)
