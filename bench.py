@@ -148,8 +148,18 @@ def main():
     name = max(kern, key=lambda x: kern[x][0])
     ms, bytes_k = kern[name]
     achieved = bytes_k / (ms / 1e3) / 1e9
+    # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
+    # passes of this same command (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)
+    traffic, traffic_src = None, None
+    prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_config3_summary.json")
+    if os.path.exists(prof):
+        with open(prof) as fh:
+            for k in json.load(fh).get("kernels", []):
+                if k["kernel"].split("<")[0] == name and k.get("hbm_bytes_per_launch") is not None:
+                    traffic, traffic_src = int(k["hbm_bytes_per_launch"]), "profiles/r01_config3_summary.json"
     roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": bytes_k, "avg_launch_ms": round(ms, 4),
                 "pipeline": {"alg_bytes_per_step": b_alg,
                              "achieved_GBs": round(b_alg / (wall / k) / 1e9, 2),
