@@ -154,9 +154,9 @@ def main():
     prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_config3_summary.json")
     if os.path.exists(prof):
         with open(prof) as fh:
-            for k in json.load(fh).get("kernels", []):
-                if k["kernel"].split("<")[0] == name and k.get("hbm_bytes_per_launch") is not None:
-                    traffic, traffic_src = int(k["hbm_bytes_per_launch"]), "profiles/r01_config3_summary.json"
+            for kr in json.load(fh).get("kernels", []):
+                if kr["kernel"].split("<")[0] == name and kr.get("hbm_bytes_per_launch") is not None:
+                    traffic, traffic_src = int(kr["hbm_bytes_per_launch"]), "profiles/r01_config3_summary.json"
     roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "traffic_source": traffic_src,
