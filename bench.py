@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--resources", type=int, default=10_000_000)
     ap.add_argument("--events", type=int, default=1 << 27)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 24, help="events replayed by the CPU oracle")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 26, help="events replayed by the CPU oracle (about 15 s on one core)")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
