@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--events", type=int, default=1 << 27)
     ap.add_argument("--cpu-sample", type=int, default=1 << 26, help="events replayed by the CPU oracle (about 15 s on one core)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-metric-log", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,6 +199,16 @@ def main():
     except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
         aggregate = {"error": str(ex)[:200]}
 
+    # metrics.log leg (off the decision path): one MetricTimerListener.run
+    # over this shard, after a drain fetch, so it covers one second of rows as
+    # the reference's 1 s timer does (sf_metric_log)
+    metric_log = None
+    if not args.no_metric_log:
+        try:
+            metric_log = metric_log_leg(eng, hb, R_total, R_local, world, rank, steps)
+        except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
+            metric_log = {"error": str(ex)[:200]}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(rules, hb, R_local, args.cpu_sample)
@@ -212,12 +223,47 @@ def main():
                            "resources": R_total, "events_per_batch_per_gpu": hb.n, "entries_per_batch_per_gpu": n_entry,
                            "resources_touched": n_seg, "pass_fraction": round(n_pass / max(1, n_entry), 4),
                            "parallelism": f"resource-sharded x{world}"},
-                "roofline": roofline, "cpu_baseline": cpu, "aggregate": aggregate}
+                "roofline": roofline, "cpu_baseline": cpu, "aggregate": aggregate,
+                "metric_log": metric_log}
         print(json.dumps(line), flush=True)
     for b in batches:
         b.free()
     if dist:
         dist.destroy_process_group()
+
+
+def metric_log_leg(eng, hb, R_total, R_local, world, rank, steps):
+    """Resource names "/r/NNNNNNNN" (global id) and types; a drain fetch at
+    T_last + 2 s (cap 0: rows counted, lastFetchTime advanced, nothing
+    copied), then the timed fetch at T_last + 3 s: the second [T_last + 2 s,
+    T_last + 3 s) of every node (and ENTRY_NODE), formatted as metrics.log."""
+    ids = np.arange(R_total, dtype=np.int64)
+    digits = ((ids[:, None] // (10 ** np.arange(7, -1, -1))) % 10 + 48).astype(np.uint8)
+    names = np.concatenate([np.frombuffer(b"/r/" * R_total, np.uint8).reshape(R_total, 3), digits], axis=1)
+    off = np.arange(R_total + 1, dtype=np.uint64) * 11
+    eng.load_resource_names_raw(names.tobytes(), off, (ids % 3).astype(np.int32))
+    t_last = int(hb.ts_ms[0]) + (steps - 1) * DURATION_MS
+    try:
+        eng.metric_log(t_last + 2000, entry_node=(rank == 0), cap=0)
+    except engine.EngineError as ex:
+        if ex.code != abi.SF_ERR_CAPACITY:
+            raise
+    import ctypes
+    buf = ctypes.create_string_buffer(1 << 30)
+    t = time.perf_counter()
+    data = eng.metric_log(t_last + 3000, entry_node=(rank == 0), cap=1 << 30, buf=buf)
+    wall_ms = (time.perf_counter() - t) * 1e3
+    st = eng.stats()
+    nodes = R_local + (1 if rank == 0 else 0)
+    scan_bytes = 3840 * nodes                       # the 60 x 64 B minute row metrics() walks per node
+    ach = scan_bytes / (st.metric_scan_ms / 1e3) / 1e9
+    return {"what": "MetricTimerListener.run -> metrics.log lines (one second)", "nodes": nodes,
+            "lines": data.count(b"\n"), "log_bytes": len(data), "device_ms": round(st.metric_log_ms, 3),
+            "wall_ms_incl_d2h": round(wall_ms, 3),
+            "scan": {"kernel": "k_mlog_count", "ms": round(st.metric_scan_ms, 3), "alg_bytes": scan_bytes,
+                     "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4)},
+            "sample_line": data[:data.find(b"\n")].decode(errors="replace") if data else ""}
 
 
 def cpu_baseline(rules, hb, R, sample):

@@ -277,8 +277,8 @@ typedef struct sf_rule_state {    /* controller state (WarmUp / RateLimiter) */
 } sf_rule_state;
 
 typedef struct sf_metric_row {    /* MetricNode (MetricNode.java:160-229) */
-    uint32_t resource;
-    uint32_t pad;
+    uint32_t resource;            /* global resource id, or SF_RES_ENTRY_NODE  */
+    int32_t  concurrency;         /* MetricNode.concurrency: metrics() never sets it (ArrayMetric.fromBucket :199-214), so 0 in snapshots */
     int64_t  timestamp;
     int64_t  pass_qps, block_qps, success_qps, exception_qps, rt, occupied_pass_qps;
 } sf_metric_row;
@@ -296,6 +296,8 @@ typedef struct sf_stats {         /* device-clock timings, summed over sf_submit
     double   heavy_fill_ms;       /* k_heavy_fill alone (stream B) */
     double   classify_ms;         /* k_classify alone */
     double   stream_ms;           /* k_heavy_stream alone (stream C: THREAD-grade and RateLimiter heavy segments) */
+    double   metric_scan_ms;      /* last sf_metric_log: k_mlog_count alone (every node's minute row) */
+    double   metric_log_ms;       /* last sf_metric_log: all its kernels, before the copy to the host */
 } sf_stats;
 
 typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last sf_submit */
@@ -349,6 +351,28 @@ int  sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out);
 int  sf_read_entry_node(sf_engine* e, sf_node_state* out);
 int  sf_read_rule_state(sf_engine* e, uint32_t rule_index, sf_rule_state* out);
 int  sf_snapshot(sf_engine* e, int64_t now_ms, sf_metric_row* out, uint32_t cap, uint32_t* n_out);
+
+/* metrics.log (MetricTimerListener -> MetricWriter) ------------------------
+ * Resource names and types (ResourceWrapper.getName / getResourceType) for
+ * the log lines: name of resource id i = bytes[offsets[i], offsets[i+1]),
+ * types[i] (ResourceTypeConstants, or NULL = COMMON 0); copied to HBM.
+ * A resource without a loaded name is written as its decimal id. */
+#define SF_RES_ENTRY_NODE 0xFFFFFFFFu   /* Constants.ENTRY_NODE, "__total_inbound_traffic__" */
+int  sf_load_resource_names(sf_engine* e, const char* bytes, const uint64_t* offsets, const int32_t* types,
+                            uint32_t n);
+/* One MetricTimerListener.run (MetricTimerListener.java:40-69) over this
+ * shard at now_ms: StatisticNode.metrics() of every ClusterNode (resource id
+ * order) and, if include_entry_node, of ENTRY_NODE (last within a second),
+ * grouped by second ascending (the TreeMap), each row written as
+ * MetricNode.toFatString (MetricNode.java:213-229) the way MetricWriter.write
+ * appends it (MetricWriter.java:120-170); the date in a fixed zone of
+ * tz_offset_ms.  Updates every node's lastFetchTime, like the reference.
+ * *len_out = bytes needed; SF_ERR_CAPACITY if > cap (state still advanced). */
+int  sf_metric_log(sf_engine* e, int64_t now_ms, int64_t tz_offset_ms, int include_entry_node, char* out,
+                   uint64_t cap, uint64_t* len_out, uint32_t* n_lines);
+/* MetricNode.toFatString of caller rows (formatting alone, on the GPU). */
+int  sf_format_metric_rows(sf_engine* e, const sf_metric_row* rows, uint32_t n, int64_t tz_offset_ms, char* out,
+                           uint64_t cap, uint64_t* len_out);
 
 /* Node-wide Constants.ENTRY_NODE over the resource shards of a node: one
  * engine per GPU, joined by RCCL (xGMI).  Rank 0 creates the id, the host

@@ -147,11 +147,50 @@ def _declare(L):
     f("so_read_param", C.c_int, P, U32, U8, U64, C.POINTER(I64), C.POINTER(I64), C.POINTER(C.c_int))
     f("so_param_thread", I64, P, U32, C.c_int, U8, U64)
     f("so_snapshot", C.c_int, P, I64, C.POINTER(abi.sf_metric_row), U32, C.POINTER(U32))
+    f("so_format_fat", C.c_int, C.POINTER(SoNames), C.POINTER(abi.sf_metric_row), U32, I64, C.c_char_p, U64,
+      C.POINTER(U64))
+    f("so_metric_log", C.c_int, P, C.POINTER(SoNames), I64, I64, C.c_int, C.c_char_p, U64, C.POINTER(U64),
+      C.POINTER(U32))
     f("so_load_namespaces", C.c_int, P, C.POINTER(abi.sf_namespace), U32)
     f("so_load_cluster_rules", C.c_int, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
     f("so_request_tokens", C.c_int, P, C.POINTER(abi.sf_token_batch), C.POINTER(abi.sf_token_results))
     f("so_cluster_sum", I64, P, I64, C.c_int, I64)
+
+
+class SoNames(C.Structure):
+    _fields_ = [("bytes", C.c_char_p), ("offsets", C.POINTER(C.c_uint64)), ("types", C.POINTER(C.c_int32)),
+                ("n", C.c_uint32)]
+
+
+def names_struct(names, types=None):
+    """(SoNames, keep-alive) of a list of resource names (str) and types."""
+    data = b"".join(n.encode() for n in names)
+    off = [0]
+    for n in names:
+        off.append(off[-1] + len(n.encode()))
+    offs = (C.c_uint64 * len(off))(*off)
+    ty = (C.c_int32 * len(names))(*types) if types is not None else None
+    st = SoNames(data, offs, ty, len(names))
+    return st, (data, offs, ty)
+
+
+def format_fat(rows, names=None, types=None, tz_offset_ms=0):
+    """MetricNode.toFatString of rows (sf_metric_row or dict) -> bytes."""
+    arr = (abi.sf_metric_row * max(1, len(rows)))()
+    for i, r in enumerate(rows):
+        if isinstance(r, dict):
+            for k, v in r.items():
+                setattr(arr[i], k, v)
+        else:
+            arr[i] = r
+    nt, keep = names_struct(names or [], types) if names is not None else (None, None)
+    cap = 256 * max(1, len(rows)) + sum(len(n) for n in (names or []))
+    buf = C.create_string_buffer(cap)
+    n = U64(0)
+    rc = lib().so_format_fat(C.byref(nt) if nt else None, arr, len(rows), tz_offset_ms, buf, cap, C.byref(n))
+    assert rc == 0, rc
+    return buf.raw[:n.value]
 
 
 class MockNode(C.Structure):
@@ -478,6 +517,15 @@ class OracleEngine:
         rc = lib().so_snapshot(self.h, now, rows, cap, C.byref(n))
         assert rc == 0, rc
         return [rows[i] for i in range(n.value)]
+
+    def metric_log(self, now, names=None, types=None, tz_offset_ms=0, entry_node=True, cap=1 << 22):
+        nt, keep = names_struct(names, types) if names is not None else (None, None)
+        buf = C.create_string_buffer(cap)
+        n, k = U64(0), U32(0)
+        rc = lib().so_metric_log(self.h, C.byref(nt) if nt else None, now, tz_offset_ms, int(entry_node), buf, cap,
+                                 C.byref(n), C.byref(k))
+        assert rc == 0, rc
+        return buf.raw[:n.value]
 
     def load_namespaces(self, ns):
         lib().so_load_namespaces(self.h, abi.rules_array(abi.sf_namespace, ns), len(ns))

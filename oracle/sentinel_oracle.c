@@ -23,6 +23,7 @@
 #include "sentinel_oracle.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1370,33 +1371,124 @@ int64_t so_param_thread(so_engine* e, uint32_t res, int idx, uint8_t tag, uint64
     if (!local_id(e, res, &l) || !e->res[l].pm) return 0;
     return so_pm_thread_count(e->res[l].pm, idx, tag, bits);
 }
+/* StatisticNode.metrics() :120-137 of one node: rows appended at out[*k] */
+static void node_metrics(so_node* n, int64_t now, uint32_t resource, sf_metric_row* out, uint32_t cap, uint32_t* k) {
+    int64_t current_time = now - now % 1000;
+    sf_metric_row rows[64];
+    int nr = so_am_details(n->minute, 0, 0, rows, 64);
+    int64_t new_last = n->last_fetch_time;
+    for (int j = 0; j < nr && j < 64; j++) {
+        sf_metric_row* r = &rows[j];
+        int in_time = r->timestamp > n->last_fetch_time && r->timestamp < current_time;     /* isNodeInTime :144-146 */
+        int valid = r->pass_qps > 0 || r->block_qps > 0 || r->success_qps > 0 || r->exception_qps > 0
+                    || r->rt > 0 || r->occupied_pass_qps > 0;                                /* isValidMetricNode :148-151 */
+        if (in_time && valid) {
+            r->resource = resource;
+            if (*k < cap) out[*k] = *r;
+            (*k)++;
+            if (r->timestamp > new_last) new_last = r->timestamp;
+        }
+    }
+    n->last_fetch_time = new_last;
+}
+
 /* StatisticNode.metrics() per ClusterNode :120-137 (MetricTimerListener.java:40-69) */
 int so_snapshot(so_engine* e, int64_t now, sf_metric_row* out, uint32_t cap, uint32_t* n_out) {
     uint32_t k = 0;
     g_now = now;
-    for (uint32_t l = 0; l < e->n_res; l++) {
-        so_node* n = e->res[l].node;
-        if (!n) continue;
-        int64_t current_time = now - now % 1000;
-        sf_metric_row rows[64];
-        int nr = so_am_details(n->minute, 0, 0, rows, 64);
-        int64_t new_last = n->last_fetch_time;
-        for (int j = 0; j < nr && j < 64; j++) {
-            sf_metric_row* r = &rows[j];
-            int in_time = r->timestamp > n->last_fetch_time && r->timestamp < current_time;
-            int valid = r->pass_qps > 0 || r->block_qps > 0 || r->success_qps > 0 || r->exception_qps > 0
-                        || r->rt > 0 || r->occupied_pass_qps > 0;
-            if (in_time && valid) {
-                r->resource = l * e->cfg.shard_count + e->cfg.shard_index;
-                if (k < cap) out[k] = *r;
-                k++;
-                if (r->timestamp > new_last) new_last = r->timestamp;
-            }
-        }
-        n->last_fetch_time = new_last;
-    }
+    for (uint32_t l = 0; l < e->n_res; l++)
+        if (e->res[l].node) node_metrics(e->res[l].node, now, l * e->cfg.shard_count + e->cfg.shard_index, out, cap, &k);
     *n_out = k;
     return k <= cap ? SF_OK : SF_ERR_CAPACITY;
+}
+
+/* ---- metrics.log lines ------------------------------------------------
+ * MetricNode.toFatString (CORE/node/metric/MetricNode.java:213-229):
+ * timestamp|yyyy-MM-dd HH:mm:ss|name('|'->'_')|pass|block|success|exception|rt|occupiedPass|concurrency|classification\n
+ * SimpleDateFormat in a fixed zone of tz_offset_ms (no DST). */
+static const char* const ENTRY_NAME = "__total_inbound_traffic__";   /* Constants.java:45 */
+
+static size_t fat_line(const sf_metric_row* r, const char* name, size_t name_len, int32_t cls, int64_t tz,
+                       char* buf, size_t cap) {
+    int64_t t = r->timestamp + tz;
+    int64_t days = t / 86400000, msd = t % 86400000;
+    if (msd < 0) { msd += 86400000; days--; }
+    /* civil date of a day count (proleptic Gregorian, as java.util.GregorianCalendar after 1582) */
+    int64_t z = days + 719468, era = (z >= 0 ? z : z - 146096) / 146097;
+    int64_t doe = z - era * 146097, yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    int64_t y = yoe + era * 400, doy = doe - (365 * yoe + yoe / 4 - yoe / 100), mp = (5 * doy + 2) / 153;
+    int64_t d = doy - (153 * mp + 2) / 5 + 1, m = mp < 10 ? mp + 3 : mp - 9;
+    if (m <= 2) y++;
+    char nm[4096];
+    size_t nl = name_len < sizeof nm - 1 ? name_len : sizeof nm - 1;
+    for (size_t i = 0; i < nl; i++) nm[i] = name[i] == '|' ? '_' : name[i];
+    nm[nl] = 0;
+    int w = snprintf(buf, cap, "%lld|%04lld-%02lld-%02lld %02lld:%02lld:%02lld|%s|%lld|%lld|%lld|%lld|%lld|%lld|%d|%d\n",
+                     (long long)r->timestamp, (long long)y, (long long)m, (long long)d, (long long)(msd / 3600000),
+                     (long long)(msd / 60000 % 60), (long long)(msd / 1000 % 60), nm, (long long)r->pass_qps,
+                     (long long)r->block_qps, (long long)r->success_qps, (long long)r->exception_qps,
+                     (long long)r->rt, (long long)r->occupied_pass_qps, (int)r->concurrency, (int)cls);
+    return w < 0 ? 0 : (size_t)w;
+}
+
+static void row_name(const so_names* nt, uint32_t res, const char** name, size_t* len, int32_t* cls, char* tmp) {
+    *cls = 0;
+    if (res == SF_RES_ENTRY_NODE) { *name = ENTRY_NAME; *len = strlen(ENTRY_NAME); return; }
+    if (nt && res < nt->n) {
+        *name = nt->bytes + nt->offsets[res]; *len = (size_t)(nt->offsets[res + 1] - nt->offsets[res]);
+        if (nt->types) *cls = nt->types[res];
+        return;
+    }
+    *len = (size_t)sprintf(tmp, "%u", res); *name = tmp;    /* no name loaded: the resource id */
+}
+
+int so_format_fat(const so_names* nt, const sf_metric_row* rows, uint32_t n, int64_t tz_offset_ms, char* out,
+                  uint64_t cap, uint64_t* len_out) {
+    uint64_t o = 0;
+    char line[8192], tmp[16];
+    for (uint32_t i = 0; i < n; i++) {
+        const char* nm; size_t nl; int32_t cls;
+        row_name(nt, rows[i].resource, &nm, &nl, &cls, tmp);
+        size_t w = fat_line(&rows[i], nm, nl, cls, tz_offset_ms, line, sizeof line);
+        if (o + w <= cap) memcpy(out + o, line, w);
+        o += w;
+    }
+    *len_out = o;
+    return o <= cap ? SF_OK : SF_ERR_CAPACITY;
+}
+
+/* MetricTimerListener.run (CORE/node/metric/MetricTimerListener.java:40-69):
+ * every ClusterNode's metrics() (resources in id order: the reference walks a
+ * HashMap, whose order is not reproducible), then ENTRY_NODE's, grouped by
+ * second in a TreeMap; MetricWriter.write(time, nodes) (MetricWriter.java:120-170)
+ * appends each node's toFatString in list order. */
+typedef struct { int64_t ts; uint32_t pos; } ts_pos;
+static int cmp_ts(const void* a, const void* b) {
+    const ts_pos *x = a, *y = b;
+    if (x->ts != y->ts) return x->ts < y->ts ? -1 : 1;
+    return x->pos < y->pos ? -1 : x->pos > y->pos;    /* list position: stable */
+}
+int so_metric_log(so_engine* e, const so_names* nt, int64_t now, int64_t tz_offset_ms, int include_entry_node,
+                  char* out, uint64_t cap, uint64_t* len_out, uint32_t* n_lines) {
+    uint32_t k = 0, cap_rows = 1024;
+    sf_metric_row* rows = malloc(cap_rows * sizeof *rows);
+    g_now = now;
+    for (uint32_t l = 0; l <= e->n_res; l++) {
+        so_node* n = l < e->n_res ? e->res[l].node : (include_entry_node ? e->entry_node : NULL);
+        if (!n) continue;
+        if (k + 64 > cap_rows) { cap_rows = 2 * (k + 64); rows = realloc(rows, cap_rows * sizeof *rows); }
+        node_metrics(n, now, l < e->n_res ? l * e->cfg.shard_count + e->cfg.shard_index : SF_RES_ENTRY_NODE,
+                     rows, cap_rows, &k);
+    }
+    ts_pos* order = malloc((k ? k : 1) * sizeof *order);
+    sf_metric_row* sorted = malloc((k ? k : 1) * sizeof *sorted);
+    for (uint32_t i = 0; i < k; i++) { order[i].ts = rows[i].timestamp; order[i].pos = i; }
+    qsort(order, k, sizeof *order, cmp_ts);
+    for (uint32_t i = 0; i < k; i++) sorted[i] = rows[order[i].pos];
+    int rc = so_format_fat(nt, sorted, k, tz_offset_ms, out, cap, len_out);
+    free(rows); free(order); free(sorted);
+    *n_lines = k;
+    return rc;
 }
 
 /* ---- cluster token server: DefaultTokenService / ClusterFlowChecker ---- */

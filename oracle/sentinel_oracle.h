@@ -198,6 +198,12 @@ int  so_read_param(so_engine* e, uint32_t param_rule_index, uint8_t tag, uint64_
 int32_t so_param_rule_idx(so_engine* e, uint32_t param_rule_index);
 int64_t so_param_thread(so_engine* e, uint32_t res, int param_idx, uint8_t tag, uint64_t bits);
 int  so_snapshot(so_engine* e, int64_t now, sf_metric_row* out, uint32_t cap, uint32_t* n_out);
+/* metrics.log lines (MetricTimerListener / MetricWriter / MetricNode.toFatString) */
+typedef struct so_names { const char* bytes; const uint64_t* offsets; const int32_t* types; uint32_t n; } so_names;
+int  so_format_fat(const so_names* nt, const sf_metric_row* rows, uint32_t n, int64_t tz_offset_ms, char* out,
+                   uint64_t cap, uint64_t* len_out);
+int  so_metric_log(so_engine* e, const so_names* nt, int64_t now, int64_t tz_offset_ms, int include_entry_node,
+                   char* out, uint64_t cap, uint64_t* len_out, uint32_t* n_lines);
 int  so_load_namespaces(so_engine* e, const sf_namespace* ns, uint32_t n);
 int  so_load_cluster_rules(so_engine* e, const sf_cluster_flow_rule* flow, uint32_t n_flow,
                            const sf_cluster_param_rule* param, uint32_t n_param,

@@ -28,6 +28,7 @@ THRESHOLD_AVG_LOCAL, THRESHOLD_GLOBAL = 0, 1
 SF_MAX_SAMPLE_COUNT = 16
 SF_MINUTE_BUCKETS = 60
 SF_WS_ABSENT = -(2 ** 63)
+RES_ENTRY_NODE = 0xFFFFFFFF      # sf_metric_row.resource of Constants.ENTRY_NODE
 SF_MAX_RULES_PER_RESOURCE = 8
 SF_MAX_ARGS = 4
 
@@ -165,7 +166,7 @@ class sf_rule_state(C.Structure):
 
 
 class sf_metric_row(C.Structure):
-    _fields_ = [("resource", C.c_uint32), ("pad", C.c_uint32), ("timestamp", C.c_int64),
+    _fields_ = [("resource", C.c_uint32), ("concurrency", C.c_int32), ("timestamp", C.c_int64),
                 ("pass_qps", C.c_int64), ("block_qps", C.c_int64), ("success_qps", C.c_int64),
                 ("exception_qps", C.c_int64), ("rt", C.c_int64), ("occupied_pass_qps", C.c_int64)]
 
@@ -175,7 +176,7 @@ class sf_stats(C.Structure):
                 ("scatter_ms", C.c_double), ("n_events", C.c_uint64), ("n_segments", C.c_uint64),
                 ("n_launches", C.c_uint64), ("light_ms", C.c_double), ("heavy_decide_ms", C.c_double),
                 ("heavy_fill_ms", C.c_double), ("classify_ms", C.c_double),
-                ("stream_ms", C.c_double)]
+                ("stream_ms", C.c_double), ("metric_scan_ms", C.c_double), ("metric_log_ms", C.c_double)]
 
 
 class sf_heavy_profile(C.Structure):

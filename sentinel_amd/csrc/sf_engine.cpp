@@ -77,6 +77,15 @@ struct sf_engine {
     uint32_t* snap_counts = nullptr; uint32_t* snap_offsets = nullptr; uint32_t* snap_total = nullptr;
     sf_metric_row* snap_rows = nullptr; uint32_t snap_cap = 0;
     void* snap_scan = nullptr; size_t snap_scan_bytes = 0;
+    // metrics.log (sf_metric.hip)
+    char* nm_bytes = nullptr; uint64_t* nm_off = nullptr; int32_t* nm_types = nullptr; uint32_t n_names = 0;
+    unsigned long long* ml_mask = nullptr; uint32_t* ml_counts = nullptr; uint32_t* ml_offsets = nullptr;
+    uint32_t* ml_total = nullptr;
+    sf_metric_row* ml_rows = nullptr; uint8_t* ml_keys = nullptr; uint32_t* ml_order = nullptr; uint32_t ml_row_cap = 0;
+    uint64_t* ml_len = nullptr; uint64_t* ml_off = nullptr; uint64_t* ml_bytes = nullptr;
+    char* ml_out = nullptr; uint64_t ml_out_cap = 0;
+    void* ml_tmp = nullptr; size_t ml_tmp_bytes = 0;
+    hipEvent_t ml_ev[3]{};
     // node-wide aggregate over the ranks of a node (RCCL over xGMI)
     ncclComm_t comm = nullptr;
     int64_t* agg = nullptr;               // [ws (S+60) | gws (S+60) | vals ((S+60)*6+1) | minrt (S+60)]
@@ -141,12 +150,15 @@ void sf_destroy(sf_engine* e) {
     for (void* p : e->user_allocs) hipFree(p);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
                      (void*)e->ts.items, e->tok_stage, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
-                     e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch};
+                     e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch, e->nm_bytes, e->nm_off,
+                     e->nm_types, e->ml_mask, e->ml_counts, e->ml_offsets, e->ml_total, e->ml_rows, e->ml_keys,
+                     e->ml_order, e->ml_len, e->ml_off, e->ml_bytes, e->ml_out, e->ml_tmp};
     for (void* p : tptrs) if (p) hipFree(p);
     if (e->agg) hipFree(e->agg);
     if (e->comm) ncclCommDestroy(e->comm);
     free_tok_work(e->tw);
     for (auto& a : e->evs) for (auto& x : a) if (x) hipEventDestroy(x);
+    for (auto& x : e->ml_ev) if (x) hipEventDestroy(x);
     for (int k = 0; k < 2; k++) {
         if (e->ev_sorted[k]) hipEventDestroy(e->ev_sorted[k]);
         if (e->ev_done[k]) hipEventDestroy(e->ev_done[k]);
@@ -733,6 +745,137 @@ int sf_snapshot(sf_engine* e, int64_t now_ms, sf_metric_row* out, uint32_t cap, 
     if (k) HIP_TRY(hipMemcpy(out, e->snap_rows, (size_t)k * sizeof(sf_metric_row), hipMemcpyDeviceToHost));
     *n_out = total;
     return total <= cap ? SF_OK : fail(SF_ERR_CAPACITY, "snapshot rows exceed cap");
+}
+// ---------------------------------------------------------------- metrics.log
+int sf_load_resource_names(sf_engine* e, const char* bytes, const uint64_t* offsets, const int32_t* types,
+                           uint32_t n) {
+    if (!e || (n && (!offsets || (!bytes && offsets[n])))) return fail(SF_ERR_INVALID, "null argument");
+    for (uint32_t i = 0; i < n; i++)
+        if (offsets[i + 1] < offsets[i]) return fail(SF_ERR_INVALID, "name offsets must be non-decreasing");
+    std::lock_guard<std::mutex> lk(e->mu);
+    void* old[] = {e->nm_bytes, e->nm_off, e->nm_types};
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (void* p : old) if (p) hipFree(p);
+    e->nm_bytes = nullptr; e->nm_off = nullptr; e->nm_types = nullptr; e->n_names = 0;
+    const uint64_t nb = n ? offsets[n] - offsets[0] : 0;
+    HIP_TRY(hipMalloc((void**)&e->nm_bytes, std::max<uint64_t>(nb, 16)));
+    HIP_TRY(hipMalloc((void**)&e->nm_off, ((size_t)n + 1) * 8));
+    if (nb) HIP_TRY(hipMemcpy(e->nm_bytes, bytes + offsets[0], nb, hipMemcpyHostToDevice));
+    std::vector<uint64_t> off(offsets, offsets + n + 1);
+    for (auto& o : off) o -= offsets[0];
+    HIP_TRY(hipMemcpy(e->nm_off, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+    if (types) {
+        HIP_TRY(hipMalloc((void**)&e->nm_types, std::max<size_t>((size_t)n * 4, 16)));
+        if (n) HIP_TRY(hipMemcpy(e->nm_types, types, (size_t)n * 4, hipMemcpyHostToDevice));
+    }
+    e->n_names = n;
+    return SF_OK;
+}
+
+static int ml_reserve(sf_engine* e, uint32_t rows) {
+    const uint32_t nodes = e->R + 1;
+    if (!e->ml_mask) {
+        HIP_TRY(hipMalloc((void**)&e->ml_mask, (size_t)nodes * 8));
+        HIP_TRY(hipMalloc((void**)&e->ml_counts, (size_t)nodes * 4));
+        HIP_TRY(hipMalloc((void**)&e->ml_offsets, (size_t)nodes * 4));
+        HIP_TRY(hipMalloc((void**)&e->ml_total, 4));
+        HIP_TRY(hipMalloc((void**)&e->ml_bytes, 8));
+        for (auto& x : e->ml_ev) HIP_TRY(hipEventCreate(&x));
+    }
+    if (rows > e->ml_row_cap || !e->ml_rows) {
+        const uint32_t cap = std::max<uint32_t>(rows, 1024);
+        void* old[] = {e->ml_rows, e->ml_keys, e->ml_order, e->ml_len, e->ml_off};
+        for (void* p : old) if (p) hipFree(p);
+        e->ml_rows = nullptr; e->ml_keys = nullptr; e->ml_order = nullptr; e->ml_len = nullptr; e->ml_off = nullptr;
+        e->ml_row_cap = 0;
+        HIP_TRY(hipMalloc((void**)&e->ml_rows, (size_t)cap * sizeof(sf_metric_row)));
+        HIP_TRY(hipMalloc((void**)&e->ml_keys, (size_t)cap * 2));
+        HIP_TRY(hipMalloc((void**)&e->ml_order, (size_t)cap * 8));
+        HIP_TRY(hipMalloc((void**)&e->ml_len, (size_t)cap * 8));
+        HIP_TRY(hipMalloc((void**)&e->ml_off, (size_t)cap * 8));
+        e->ml_row_cap = cap;
+    }
+    size_t tb = 0;
+    HIP_TRY(mlog_temp_bytes(nodes, e->ml_row_cap, &tb));
+    if (tb > e->ml_tmp_bytes) {
+        if (e->ml_tmp) hipFree(e->ml_tmp);
+        e->ml_tmp = nullptr; e->ml_tmp_bytes = 0;
+        HIP_TRY(hipMalloc(&e->ml_tmp, tb));
+        e->ml_tmp_bytes = tb;
+    }
+    return SF_OK;
+}
+
+// line lengths -> offsets -> lines, copied to the caller's host buffer
+static int ml_format(sf_engine* e, const uint32_t* order, uint32_t n, int64_t tz, char* out, uint64_t cap,
+                     uint64_t* len_out) {
+    hipStream_t s = e->stream;
+    HIP_TRY(launch_fmt_len(e->ml_rows, order, n, e->nm_bytes, e->nm_off, e->nm_types, e->n_names, tz, e->ml_len,
+                           e->ml_off, e->ml_bytes, e->ml_tmp, e->ml_tmp_bytes, s));
+    uint64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, e->ml_bytes, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *len_out = total;
+    if (total > cap) return fail(SF_ERR_CAPACITY, "metric log bytes exceed cap");
+    if (total > e->ml_out_cap) {
+        if (e->ml_out) hipFree(e->ml_out);
+        e->ml_out = nullptr; e->ml_out_cap = 0;
+        HIP_TRY(hipMalloc((void**)&e->ml_out, total));
+        e->ml_out_cap = total;
+    }
+    HIP_TRY(launch_fmt_write(e->ml_rows, order, n, e->nm_bytes, e->nm_off, e->nm_types, e->n_names, tz, e->ml_off,
+                             e->ml_out, s));
+    HIP_TRY(hipEventRecord(e->ml_ev[2], s));
+    if (total) HIP_TRY(hipMemcpyAsync(out, e->ml_out, total, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SF_OK;
+}
+
+int sf_metric_log(sf_engine* e, int64_t now_ms, int64_t tz_offset_ms, int include_entry_node, char* out,
+                  uint64_t cap, uint64_t* len_out, uint32_t* n_lines) {
+    if (!e || !len_out || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    *len_out = 0;
+    if (n_lines) *n_lines = 0;
+    int rc = ml_reserve(e, 0);
+    if (rc) return rc;
+    hipStream_t s = e->stream;
+    const bool with_en = include_entry_node != 0;
+    const uint32_t nodes = e->R + (with_en ? 1u : 0u);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const unsigned grid = (unsigned)std::min<uint64_t>(((uint64_t)nodes + 3) / 4, (uint64_t)cus * 16);
+    HIP_TRY(hipEventRecord(e->ml_ev[0], s));
+    HIP_TRY(launch_mlog_count(e->st, e->en, with_en, e->cfg.shard_count, e->cfg.shard_index, now_ms, e->ml_mask,
+                              e->ml_counts, e->ml_offsets, e->ml_total, e->ml_tmp, e->ml_tmp_bytes, grid, e->ml_ev[1], s));
+    uint32_t rows = 0;
+    HIP_TRY(hipMemcpyAsync(&rows, e->ml_total, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    rc = ml_reserve(e, rows);
+    if (rc) return rc;
+    uint32_t* ord = e->ml_order;
+    HIP_TRY(launch_mlog_rows(e->st, e->en, with_en, e->cfg.shard_count, e->cfg.shard_index, now_ms, e->ml_mask,
+                             e->ml_offsets, rows, e->ml_rows, e->ml_keys, e->ml_keys + e->ml_row_cap, ord,
+                             ord + e->ml_row_cap, e->ml_tmp, e->ml_tmp_bytes, grid, s));
+    if (n_lines) *n_lines = rows;
+    rc = ml_format(e, ord + e->ml_row_cap, rows, tz_offset_ms, out, cap, len_out);
+    if (rc) return rc;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e->ml_ev[0], e->ml_ev[1]) == hipSuccess) e->stats.metric_scan_ms = ms;
+    if (hipEventElapsedTime(&ms, e->ml_ev[0], e->ml_ev[2]) == hipSuccess) e->stats.metric_log_ms = ms;
+    return SF_OK;
+}
+
+int sf_format_metric_rows(sf_engine* e, const sf_metric_row* rows, uint32_t n, int64_t tz_offset_ms, char* out,
+                          uint64_t cap, uint64_t* len_out) {
+    if (!e || !len_out || (n && !rows) || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    *len_out = 0;
+    int rc = ml_reserve(e, n);
+    if (rc) return rc;
+    if (n) HIP_TRY(hipMemcpyAsync(e->ml_rows, rows, (size_t)n * sizeof(sf_metric_row), hipMemcpyHostToDevice,
+                                  e->stream));
+    return ml_format(e, nullptr, n, tz_offset_ms, out, cap, len_out);
 }
 // ---------------------------------------------------------------- cluster token server
 // Rebuild the device rule table, flowId index and namespace table from the

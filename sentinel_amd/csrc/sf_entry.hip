@@ -230,7 +230,7 @@ __global__ void k_entry_init(EntryNode* en, int64_t max_rt) {
     const int i = threadIdx.x;
     if (i < SF_MAX_SAMPLE_COUNT) en->second[i] = fresh_bucket(WS_NONE, max_rt);
     if (i < MINUTE) en->minute[i] = fresh_bucket(WS_NONE, max_rt);
-    if (i == 0) en->threads = 0;
+    if (i == 0) { en->threads = 0; en->last_fetch = -1; }
 }
 
 hipError_t launch_entry_init(EntryNode* en, int64_t max_rt, hipStream_t s) {
@@ -288,7 +288,7 @@ __device__ __forceinline__ bool snap_row(const Bucket& b, int64_t now, int64_t l
     if (!(b.ws > last && b.ws < cur_sec)) return false;                    // isNodeInTime
     if (!(b.pass > 0 || b.block > 0 || b.succ > 0 || b.exc > 0 || rt > 0 || b.occ > 0)) return false;   // isValidMetricNode
     if (r) {
-        r->pad = 0; r->timestamp = b.ws;
+        r->concurrency = 0; r->timestamp = b.ws;
         r->pass_qps = b.pass; r->block_qps = b.block; r->success_qps = b.succ; r->exception_qps = b.exc;
         r->rt = rt; r->occupied_pass_qps = b.occ;
     }

@@ -93,6 +93,7 @@ struct EntryNode {
     Bucket second[SF_MAX_SAMPLE_COUNT];
     Bucket minute[SF_MINUTE_BUCKETS];
     int64_t threads;
+    int64_t last_fetch;                    // StatisticNode.lastFetchTime (metrics.log)
 };
 // per-submit reduction of the IN events into the ENTRY_NODE windows: one row
 // per window of the batch (relative to the window of its first event)
@@ -182,6 +183,23 @@ hipError_t launch_en_pack_vals(const EntryNode* en, int S, const int64_t* gws, i
 hipError_t launch_snapshot(const DevState& st, int64_t now, uint32_t shard_count, uint32_t shard_index,
                            uint32_t* counts, uint32_t* offsets, sf_metric_row* out, uint32_t cap, uint32_t* total,
                            void* scan_tmp, size_t scan_bytes, hipStream_t s);
+// metrics.log (sf_metric.hip)
+hipError_t mlog_temp_bytes(uint32_t nodes, uint32_t rows, size_t* bytes);
+hipError_t launch_mlog_count(const DevState& st, EntryNode* en, bool with_entry, uint32_t shard_count,
+                             uint32_t shard_index, int64_t now, unsigned long long* mask, uint32_t* counts,
+                             uint32_t* offsets, uint32_t* total, void* tmp, size_t tmp_bytes, unsigned grid,
+                             hipEvent_t after_count, hipStream_t s);
+hipError_t launch_mlog_rows(const DevState& st, EntryNode* en, bool with_entry, uint32_t shard_count,
+                            uint32_t shard_index, int64_t now, const unsigned long long* mask, const uint32_t* offsets,
+                            uint32_t n_rows, sf_metric_row* rows, uint8_t* keys, uint8_t* keys_out, uint32_t* order,
+                            uint32_t* order_out, void* tmp, size_t tmp_bytes, unsigned grid, hipStream_t s);
+hipError_t launch_fmt_len(const sf_metric_row* rows, const uint32_t* order, uint32_t n, const char* names,
+                          const uint64_t* name_off, const int32_t* types, uint32_t n_names, int64_t tz,
+                          uint64_t* line_len, uint64_t* line_off, uint64_t* total, void* tmp, size_t tmp_bytes,
+                          hipStream_t s);
+hipError_t launch_fmt_write(const sf_metric_row* rows, const uint32_t* order, uint32_t n, const char* names,
+                            const uint64_t* name_off, const int32_t* types, uint32_t n_names, int64_t tz,
+                            const uint64_t* line_off, char* out, hipStream_t s);
 hipError_t launch_replay(const DevState& st, const DevBatch& b, const DevVerdicts& out, uint32_t shard_count,
                          uint32_t shard_index, const SysRule& sr, EntryNode* en, hipStream_t s);
 hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,

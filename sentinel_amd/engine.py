@@ -75,6 +75,11 @@ def _declare(L):
     f("sf_read_entry_node", I, P, C.POINTER(abi.sf_node_state))
     f("sf_read_rule_state", I, P, U32, C.POINTER(abi.sf_rule_state))
     f("sf_snapshot", I, P, C.c_int64, C.POINTER(abi.sf_metric_row), U32, C.POINTER(U32))
+    f("sf_load_resource_names", I, P, C.c_char_p, C.POINTER(C.c_uint64), C.POINTER(C.c_int32), U32)
+    f("sf_metric_log", I, P, C.c_int64, C.c_int64, I, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64),
+      C.POINTER(U32))
+    f("sf_format_metric_rows", I, P, C.POINTER(abi.sf_metric_row), U32, C.c_int64, C.c_char_p, C.c_uint64,
+      C.POINTER(C.c_uint64))
     f("sf_device_alloc", I, P, C.c_size_t, C.POINTER(P))
     f("sf_device_free", I, P, P)
     f("sf_memcpy", I, P, P, P, C.c_size_t, I)
@@ -254,6 +259,43 @@ class FlowEngine:
         n = C.c_uint32()
         _check(lib().sf_snapshot(self.h, now, rows, cap, C.byref(n)))
         return [rows[i] for i in range(n.value)]
+
+    def load_resource_names(self, names, types=None):
+        """ResourceWrapper names (and ResourceTypeConstants) by global resource id, for metrics.log."""
+        enc = [n.encode() if isinstance(n, str) else bytes(n) for n in names]
+        off = np.zeros(len(enc) + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in enc], dtype=np.uint64)
+        data = b"".join(enc)
+        ty = None if types is None else np.ascontiguousarray(types, dtype=np.int32)
+        _check(lib().sf_load_resource_names(self.h, data, off.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                            None if ty is None else ty.ctypes.data_as(C.POINTER(C.c_int32)),
+                                            len(enc)))
+
+    def load_resource_names_raw(self, data: bytes, offsets, types=None):
+        """Names as one byte string and n+1 offsets (uint64)."""
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ty = None if types is None else np.ascontiguousarray(types, dtype=np.int32)
+        _check(lib().sf_load_resource_names(self.h, data, off.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                            None if ty is None else ty.ctypes.data_as(C.POINTER(C.c_int32)),
+                                            off.shape[0] - 1))
+
+    def metric_log(self, now, tz_offset_ms=0, entry_node=True, cap=1 << 24, buf=None) -> bytes:
+        """One MetricTimerListener.run at ``now``: the metrics.log bytes MetricWriter appends
+        (``buf``: a reusable ctypes char buffer of at least ``cap`` bytes)."""
+        if buf is None or len(buf) < cap:
+            buf = C.create_string_buffer(max(1, cap))
+        n, k = C.c_uint64(), C.c_uint32()
+        _check(lib().sf_metric_log(self.h, now, tz_offset_ms, int(entry_node), buf, cap, C.byref(n), C.byref(k)))
+        return buf.raw[:n.value]
+
+    def format_metric_rows(self, rows, tz_offset_ms=0) -> bytes:
+        """MetricNode.toFatString of the given rows, formatted on the GPU."""
+        arr = (abi.sf_metric_row * max(1, len(rows)))(*rows)
+        cap = 256 * max(1, len(rows)) + (1 << 16)
+        buf = C.create_string_buffer(cap)
+        n = C.c_uint64()
+        _check(lib().sf_format_metric_rows(self.h, arr, len(rows), tz_offset_ms, buf, cap, C.byref(n)))
+        return buf.raw[:n.value]
 
     def read_rule_state(self, idx) -> abi.sf_rule_state:
         s = abi.sf_rule_state()

@@ -186,3 +186,46 @@ def test_entry_node_rccl_single_rank(eng_mod, so):
     got = abi.node_state_to_dict(e.entry_node_allreduce())
     want = abi.node_state_to_dict(e.read_entry_node())
     assert got == want
+
+
+def test_metric_log_matches_oracle(eng_mod, so):
+    """metrics.log on the GPU (sf_metric_log: MetricTimerListener.run ->
+    MetricWriter.write -> MetricNode.toFatString) byte for byte against the
+    oracle: several fetches across batches (lastFetchTime, the current-second
+    exclusion, ENTRY_NODE last in each second), names with '|', resource types,
+    a resource without a name, UTC+8 dates."""
+    w = workloads.config3(R=3000, n=120_000, seed=31, split=3, duration_ms=9000)
+    e, o = eng_mod.FlowEngine(w["cfg"]), so.OracleEngine(w["cfg"])
+    R = w["cfg"].max_resources
+    names = [f"/svc/{r}|op" if r % 7 == 0 else f"res-{r}" for r in range(R - 5)]   # the last 5 unnamed
+    types = [r % 5 for r in range(R - 5)]
+    e.load_resource_names(names, types)
+    tz = 8 * 3600 * 1000
+    for x in (e, o):
+        x.load_flow_rules(w["flow"])
+    for k, b in enumerate(w["batches"]):
+        parity.compare_verdicts(e.submit(b), o.submit(b), f"batch {k}")
+        for now in (int(b.ts_ms[-1]) + 1, int(b.ts_ms[-1]) + 1700):
+            got = e.metric_log(now, tz_offset_ms=tz)
+            want = o.metric_log(now, names=names, types=types, tz_offset_ms=tz)
+            assert got == want, f"metric log after batch {k} at {now}: {len(got)} vs {len(want)} bytes"
+            assert k > 0 or len(got) > 0
+    assert e.metric_log(int(w["batches"][-1].ts_ms[-1]) + 1700, tz_offset_ms=tz) == b""   # nothing new
+    parity.compare_nodes(e, o, w["nodes"])
+
+
+def test_format_metric_rows_kat(eng_mod, so):
+    """MetricNodeTest.java:29-36 fat line, formatted by the GPU kernel, and
+    the formatter on edge values against the oracle's."""
+    from sentinel_amd import abi as A
+    e = eng_mod.FlowEngine(abi.default_config(max_resources=16))
+    e.load_resource_names(["/foo/*", "a|b"], [1, 2])
+    r = A.sf_metric_row(resource=0, concurrency=2, timestamp=1564382218000, pass_qps=1, success_qps=1)
+    assert e.format_metric_rows([r], tz_offset_ms=8 * 3600 * 1000) == \
+        b"1564382218000|2019-07-29 14:36:58|/foo/*|1|0|1|0|0|0|2|1\n"
+    rows = [A.sf_metric_row(resource=res, timestamp=ts, pass_qps=p, block_qps=-p, rt=(1 << 63) - 1 - p)
+            for res, ts, p in [(1, -1, 0), (0, 951868799999, 7), (A.RES_ENTRY_NODE, 253402300799000, -3),
+                               (12, 0, 1 << 40), (1, -2208988800000, 9)]]
+    got = e.format_metric_rows(rows, tz_offset_ms=-5 * 3600 * 1000)
+    want = so.format_fat(rows, names=["/foo/*", "a|b"], types=[1, 2], tz_offset_ms=-5 * 3600 * 1000)
+    assert got == want

@@ -504,3 +504,54 @@ def test_token_service_bad_request_and_no_rule(so):
     assert list(r.status) == [abi.TOKEN_BAD_REQUEST, abi.TOKEN_NO_RULE_EXISTS, abi.TOKEN_OK,
                               abi.TOKEN_BAD_REQUEST, abi.TOKEN_OK, abi.TOKEN_BLOCKED]
     assert list(r.remaining[[2, 4]]) == [1, 0]
+
+
+# ---------------------------------------------------------------- metrics.log lines
+def test_metric_node_fat_string(so):
+    """CORE_T/node/metric/MetricNodeTest.java:29-36: the fat line
+    "1564382218000|2019-07-29 14:36:58|/foo/*|1|0|1|0|0|0|2|1" (written in
+    UTC+8) is what toFatString (MetricNode.java:213-229) gives for that node."""
+    row = dict(resource=0, concurrency=2, timestamp=1564382218000, pass_qps=1, block_qps=0, success_qps=1,
+               exception_qps=0, rt=0, occupied_pass_qps=0)
+    got = so.format_fat([row], names=["/foo/*"], types=[1], tz_offset_ms=8 * 3600 * 1000)
+    assert got == b"1564382218000|2019-07-29 14:36:58|/foo/*|1|0|1|0|0|0|2|1\n"
+
+
+def test_metric_fat_string_fields(so):
+    """toFatString details: '|' in the name becomes '_' (:220), negative longs,
+    ENTRY_NODE's name (Constants.java:45), dates before 1970 and at leap days
+    (checked against Python's calendar in the same fixed zone)."""
+    import datetime as dt
+    cases = [(0, 0), (-1, 0), (951782400000 + 86399999, 0), (1709164800000, -5 * 3600 * 1000),
+             (-2208988800000, 3600 * 1000), (253402300799000, 0), (1564382218000, 8 * 3600 * 1000)]
+    for ts, tz in cases:
+        row = dict(resource=0, timestamp=ts, pass_qps=-7, block_qps=1 << 62, rt=-(1 << 63))
+        got = so.format_fat([row], names=["a|b||c"], tz_offset_ms=tz).decode()
+        d = dt.datetime(1970, 1, 1) + dt.timedelta(milliseconds=ts + tz)
+        want = f"{ts}|{d:%Y-%m-%d %H:%M:%S}|a_b__c|-7|{1 << 62}|0|0|{-(1 << 63)}|0|0|0\n"
+        assert got == want, (ts, tz, got)
+    got = so.format_fat([dict(resource=abi.RES_ENTRY_NODE, timestamp=1000, pass_qps=3)], names=[])
+    assert got == b"1000|1970-01-01 00:00:01|__total_inbound_traffic__|3|0|0|0|0|0|0|0\n"
+    assert so.format_fat([dict(resource=12, timestamp=1000)], names=["x"]).split(b"|")[2] == b"12"
+
+
+def test_metric_log_oracle(so):
+    """MetricTimerListener.run (:40-69) on the oracle: rows grouped by second,
+    ENTRY_NODE last in each second, lastFetchTime advancing (StatisticNode
+    .metrics :120-137: a second is written once, the current one not yet)."""
+    e = so.OracleEngine(_cfg())
+    e.load_flow_rules([abi.sf_flow_rule(resource=r, grade=abi.GRADE_QPS, count=5, warm_up_period_sec=10,
+                                        max_queueing_time_ms=500) for r in range(3)])
+    t0 = 1_700_000_000_000
+    res, ts = [0, 1, 0, 2, 1, 0], [t0, t0 + 10, t0 + 1100, t0 + 1200, t0 + 2100, t0 + 2200]
+    e.submit(abi.HostBatch(res, ts, [1] * 6, [abi.EV_IN] * 6))
+    names = ["r0", "r|1", "r2"]
+    log = e.metric_log(t0 + 2500, names=names).decode().splitlines()
+    sec = [int(l.split("|")[0]) for l in log]
+    assert sec == sorted(sec) and sec[0] == t0 and sec[-1] == t0 + 1000
+    assert [l.split("|")[2] for l in log] == ["r0", "r_1", "__total_inbound_traffic__",
+                                              "r0", "r2", "__total_inbound_traffic__"]
+    assert [l.split("|")[3] for l in log] == ["1", "1", "2", "1", "1", "2"]
+    assert e.metric_log(t0 + 2600, names=names) == b""          # nothing new in the same second
+    log2 = e.metric_log(t0 + 3000, names=names).decode().splitlines()
+    assert [l.split("|")[2] for l in log2] == ["r0", "r_1", "__total_inbound_traffic__"]
