@@ -121,6 +121,9 @@ typedef struct sf_flow_rule {
 #define SF_TAG_DOUBLE 4
 #define SF_TAG_BOOL   5
 #define SF_TAG_OTHER  6
+#define SF_TAG_BYTE   7   /* java.lang.Byte  (wire PARAM_TYPE_BYTE)  */
+#define SF_TAG_SHORT  8   /* java.lang.Short (wire PARAM_TYPE_SHORT) */
+#define SF_TAG_FLOAT  9   /* java.lang.Float (wire PARAM_TYPE_FLOAT), bits = floatToIntBits */
 
 typedef struct sf_hot_item {      /* ParamFlowItem parsed (ParamFlowRuleUtil.java:188-240) */
     uint8_t  tag;
@@ -298,6 +301,7 @@ typedef struct sf_stats {         /* device-clock timings, summed over sf_submit
     double   stream_ms;           /* k_heavy_stream alone (stream C: THREAD-grade and RateLimiter heavy segments) */
     double   metric_scan_ms;      /* last sf_metric_log: k_mlog_count alone (every node's minute row) */
     double   metric_log_ms;       /* last sf_metric_log: all its kernels, before the copy to the host */
+    double   wire_ms;             /* last sf_serve_frames: device time from framing to encoded responses (host syncs included) */
 } sf_stats;
 
 typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last sf_submit */
@@ -340,6 +344,64 @@ int  sf_load_cluster_rules(sf_engine* e, const sf_cluster_flow_rule* flow, uint3
                            const sf_cluster_param_rule* param, uint32_t n_param,
                            const sf_hot_item* items, uint32_t n_items);
 int  sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* out);
+/* ---- token-server wire path (C1 frames) ------------
+ * Replaces the server pipeline of NettyTransportServer.java:84-101 up to the
+ * TokenService call and back:
+ *   LengthFieldBasedFrameDecoder(1024, 0, 2, 0, 2)  -> NettyRequestDecoder
+ *   -> DefaultRequestEntityDecoder.java:42-63 (xid:int32, type:int8)
+ *   -> FlowRequestDataDecoder.java:37-48 / ParamFlowRequestDataDecoder.java:35-90
+ *   -> TokenServerHandler.channelRead (:61-82) -> Flow/ParamFlowRequestProcessor
+ *   -> DefaultTokenService (sf_request_tokens)
+ *   -> DefaultResponseEntityWriter.java:35-52 + FlowResponseDataWriter.java:30-33
+ *   -> LengthFieldPrepender(2).
+ * The input is the raw inbound bytes of n_streams connections, concatenated
+ * (stream s = in[stream_off[s], stream_off[s+1])); all big-endian, as Netty.
+ * Every request decided in one call is stamped now_ms and decided in (stream,
+ * frame) order.  Per stream the engine handles the longest prefix of frames it
+ * decides exactly like the reference and stops at:
+ *   - an incomplete frame at the end              -> SF_WIRE_PARTIAL
+ *   - a frame the host must run through the reference pipeline -> SF_WIRE_HOST:
+ *     PING (ConnectionManager bookkeeping; its connected count takes effect at
+ *     the next call), a type with no decoder, a PARAM_FLOW with more than one
+ *     parameter, or a frame whose body the decoder does not consume exactly
+ *     (Netty's cumulation would carry the rest into the next frame).
+ * consumed[s] = bytes of stream s handled (the stopping frame starts there).
+ * Frames longer than 1024 bytes are skipped without a response (Netty's
+ * TooLongFrameException); a FLOW / PARAM_FLOW frame with no data gets no
+ * response (the processor's NullPointerException), as in the reference.
+ * Responses of stream s: out[resp_off[s] .. resp_off[s+1]), SF_WIRE_RESP_BYTES
+ * each (2-B length 14, xid, type, status, remaining, waitInMs).
+ * String parameters are keyed by sf_string_key() of their bytes: a rule's
+ * String hot items must be loaded with SF_TAG_STRING bits = sf_string_key(). */
+#define SF_WIRE_DONE    0
+#define SF_WIRE_PARTIAL 1
+#define SF_WIRE_HOST    2
+#define SF_WIRE_RESP_BYTES 16
+#define SF_WIRE_MAX_FRAME 1024      /* LengthFieldBasedFrameDecoder maxFrameLength */
+
+typedef struct sf_wire_batch {
+    int32_t         mem;            /* SF_MEM_HOST / SF_MEM_DEVICE: bytes and stream_off */
+    uint32_t        n_streams;
+    const uint8_t*  bytes;
+    const uint64_t* stream_off;     /* [n_streams + 1], non-decreasing, total < 2^31 */
+    int64_t         now_ms;         /* server clock (TimeUtil) of every request   */
+} sf_wire_batch;
+
+typedef struct sf_wire_out {        /* host memory */
+    uint8_t*  resp;                 /* response bytes                               */
+    uint64_t  cap;                  /* capacity of resp in bytes                    */
+    uint64_t* resp_off;             /* [n_streams + 1] byte offsets into resp       */
+    uint64_t* consumed;             /* [n_streams]                                  */
+    uint8_t*  stop;                 /* [n_streams] SF_WIRE_*                        */
+    uint64_t  n_frames;             /* out: complete frames found                   */
+    uint64_t  n_requests;           /* out: requests decided by the token service   */
+    uint64_t  n_responses;          /* out: responses written                       */
+} sf_wire_out;
+
+/* 64-bit key of a wire String parameter (FNV-1a 64 of its bytes). */
+uint64_t sf_string_key(const uint8_t* bytes, uint32_t len);
+int  sf_serve_frames(sf_engine* e, const sf_wire_batch* in, sf_wire_out* out);
+
 /* ClusterMetric.getSum(event) of a cluster flow rule at time now_ms
  * (ClusterMetric.java:47-55; rolls the current bucket like the reference).
  * event: ClusterFlowEvent ordinal (PASS 0, BLOCK 1, PASS_REQUEST 2,

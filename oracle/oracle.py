@@ -155,6 +155,8 @@ def _declare(L):
     f("so_load_cluster_rules", C.c_int, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
     f("so_request_tokens", C.c_int, P, C.POINTER(abi.sf_token_batch), C.POINTER(abi.sf_token_results))
+    f("so_serve_frames", C.c_int, P, C.POINTER(abi.sf_wire_batch), C.POINTER(abi.sf_wire_out))
+    f("so_string_key", C.c_uint64, C.c_char_p, C.c_uint32)
     f("so_cluster_sum", I64, P, I64, C.c_int, I64)
 
 
@@ -542,6 +544,13 @@ class OracleEngine:
         rc = lib().so_request_tokens(self.h, C.byref(b), C.byref(r))
         assert rc == 0, rc
         return out
+
+    def serve_frames(self, streams, now_ms) -> abi.WireResult:
+        r = abi.WireResult(streams, now_ms)
+        b, o = r.c_structs()
+        rc = lib().so_serve_frames(self.h, C.byref(b), C.byref(o))
+        assert rc == 0, rc
+        return r.finish(o)
 
     def cluster_sum(self, flow_id, event, now):
         return lib().so_cluster_sum(self.h, flow_id, event, now)

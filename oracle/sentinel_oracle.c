@@ -1617,3 +1617,186 @@ int so_request_tokens(so_engine* e, const sf_token_batch* in, sf_token_results* 
     }
     return SF_OK;
 }
+
+/* ======================================================================
+ * Token-server wire path (C1 frames).  Restates, per connection and in
+ * order, the server pipeline of CS/server/NettyTransportServer.java:84-101:
+ *   LengthFieldBasedFrameDecoder(1024, 0, 2, 0, 2)  (netty 4.1: 2-byte
+ *     big-endian length, frameLength = length + 2, frames above 1024 bytes
+ *     discarded with TooLongFrameException, length field stripped)
+ *   NettyRequestDecoder (ByteToMessageDecoder, CS/server/codec/netty/
+ *     NettyRequestDecoder.java:36-49): decodes while bytes remain; bytes a
+ *     decode leaves unread stay in the cumulation for the next frame
+ *   DefaultRequestEntityDecoder.java:42-63, FlowRequestDataDecoder.java:37-48,
+ *   ParamFlowRequestDataDecoder.java:35-90 (ClusterConstants PARAM_TYPE_*)
+ *   TokenServerHandler.channelRead :61-82 -> FlowRequestProcessor :36-52 /
+ *     ParamFlowRequestProcessor :38-54 -> DefaultTokenService :39-64
+ *   DefaultResponseEntityWriter.java:35-52, FlowResponseDataWriter.java:30-33,
+ *     LengthFieldPrepender(2).
+ * The stream stops (SF_WIRE_HOST) at the first frame whose outcome is not a
+ * pure function of the frame and the token state (PING, a type without a
+ * decoder, a body not consumed exactly, more than one parameter): the C-ABI
+ * contract in sentinel_flow.h.
+ * ====================================================================== */
+enum { WF_NONE = 0, WF_REQ = 1, WF_BAD = 2, WF_HOST = 3 };
+
+static uint32_t wbe32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
+static uint64_t wbe64(const uint8_t* p) { return ((uint64_t)wbe32(p) << 32) | wbe32(p + 4); }
+static void wput32(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v; }
+
+uint64_t so_string_key(const uint8_t* b, uint32_t len) {
+    uint64_t h = 0xcbf29ce484222325ULL;
+    for (uint32_t i = 0; i < len; i++) { h ^= b[i]; h *= 0x100000001b3ULL; }
+    return h;
+}
+
+typedef struct {
+    int32_t xid; int8_t type; uint8_t prio;
+    int64_t flow_id; int32_t count;
+    int param; uint8_t tag; uint64_t bits;
+} so_wire_req;
+
+/* One frame body through NettyRequestDecoder + DefaultRequestEntityDecoder +
+ * the request processor.  WF_NONE: no response (empty frame, or the
+ * processor's NullPointerException on null data). */
+static int so_wire_decode(const uint8_t* b, uint32_t L, so_wire_req* r) {
+    memset(r, 0, sizeof *r);
+    if (L == 0) return WF_NONE;                      /* callDecode: nothing readable */
+    if (L < 5) return WF_HOST;                       /* decode() returns null, bytes stay cumulated */
+    r->xid = (int32_t)wbe32(b);
+    r->type = (int8_t)b[4];                          /* int type = source.readByte() */
+    const uint8_t* q = b + 5;
+    const uint32_t rem = L - 5;
+    if (r->type == 1) {                              /* MSG_TYPE_FLOW */
+        if (rem == 0) return WF_NONE;                /* data null -> NPE in FlowRequestProcessor :39 */
+        if (rem < 12 || rem > 13) return WF_HOST;    /* data bytes left unread */
+        r->flow_id = (int64_t)wbe64(q);
+        r->count = (int32_t)wbe32(q + 8);
+        r->prio = rem == 13 ? (q[12] != 0) : 0;      /* readBoolean */
+        return WF_REQ;
+    }
+    if (r->type == 2) {                              /* MSG_TYPE_PARAM_FLOW */
+        if (rem == 0) return WF_NONE;
+        if (rem < 16) return WF_HOST;
+        r->flow_id = (int64_t)wbe64(q);
+        r->count = (int32_t)wbe32(q + 8);
+        const int32_t amount = (int32_t)wbe32(q + 12);
+        uint32_t p = 16;
+        if (amount <= 0) return rem == 16 ? WF_NONE : WF_HOST;   /* decode() returns null */
+        if ((uint32_t)amount > rem - 16) return WF_HOST;          /* every parameter reads >= 1 byte */
+        int n = 0;
+        for (int32_t k = 0; k < amount; k++) {
+            if (p + 1 > rem) return WF_HOST;         /* IndexOutOfBoundsException */
+            const uint8_t ty = q[p++];
+            uint8_t tag = 0; uint64_t bits = 0; int ok = 1;
+            switch (ty) {
+            case 0: if (p + 4 > rem) return WF_HOST; tag = SF_TAG_INT; bits = (uint64_t)(int64_t)(int32_t)wbe32(q + p); p += 4; break;
+            case 7: {                                /* PARAM_TYPE_STRING */
+                if (p + 4 > rem) return WF_HOST;
+                const int32_t len = (int32_t)wbe32(q + p); p += 4;
+                if (len < 0 || (uint32_t)len > rem - p) return WF_HOST;
+                tag = SF_TAG_STRING; bits = so_string_key(q + p, (uint32_t)len); p += (uint32_t)len; break;
+            }
+            case 6: if (p + 1 > rem) return WF_HOST; tag = SF_TAG_BOOL; bits = q[p] != 0; p += 1; break;
+            case 3: {                                /* readDouble; Double.equals: doubleToLongBits */
+                if (p + 8 > rem) return WF_HOST;
+                uint64_t v = wbe64(q + p); p += 8;
+                if ((v & 0x7ff0000000000000ULL) == 0x7ff0000000000000ULL && (v & 0x000fffffffffffffULL)) v = 0x7ff8000000000000ULL;
+                tag = SF_TAG_DOUBLE; bits = v; break;
+            }
+            case 1: if (p + 8 > rem) return WF_HOST; tag = SF_TAG_LONG; bits = wbe64(q + p); p += 8; break;
+            case 4: {                                /* readFloat; Float.equals: floatToIntBits */
+                if (p + 4 > rem) return WF_HOST;
+                uint32_t v = wbe32(q + p); p += 4;
+                if ((v & 0x7f800000u) == 0x7f800000u && (v & 0x007fffffu)) v = 0x7fc00000u;
+                tag = SF_TAG_FLOAT; bits = v; break;
+            }
+            case 2: if (p + 1 > rem) return WF_HOST; tag = SF_TAG_BYTE; bits = (uint64_t)(int64_t)(int8_t)q[p]; p += 1; break;
+            case 5: if (p + 2 > rem) return WF_HOST; tag = SF_TAG_SHORT; bits = (uint64_t)(int64_t)(int16_t)(((uint32_t)q[p] << 8) | q[p + 1]); p += 2; break;
+            default: ok = 0;                         /* decodeParam returns false, nothing added */
+            }
+            if (ok) { if (n == 0) { r->tag = tag; r->bits = bits; } n++; }
+        }
+        if (p != rem) return WF_HOST;                /* bytes left in the cumulation */
+        if (n == 0) return WF_BAD;                   /* requestParamToken: params.isEmpty() -> badRequest */
+        if (n > 1) return WF_HOST;
+        r->param = 1;
+        return WF_REQ;
+    }
+    if (rem == 0 && r->type != 0) return WF_NONE;    /* no decoder: null message, nothing left */
+    return WF_HOST;                                  /* PING, or no decoder with bytes left */
+}
+
+int so_serve_frames(so_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
+    const uint32_t S = in->n_streams;
+    const uint64_t total = in->stream_off[S];
+    so_wire_req* reqs = (so_wire_req*)malloc(sizeof(so_wire_req) * (total / 2 + 1));
+    uint8_t* kind = (uint8_t*)malloc(total / 2 + 1);
+    uint32_t* rstream = (uint32_t*)malloc(sizeof(uint32_t) * (total / 2 + 1));
+    uint64_t nr = 0, nframes = 0;
+    for (uint32_t s = 0; s < S; s++) {
+        uint64_t p = in->stream_off[s];
+        const uint64_t end = in->stream_off[s + 1];
+        uint8_t stop = SF_WIRE_DONE;
+        while (p < end) {
+            if (end - p < 2) { stop = SF_WIRE_PARTIAL; break; }
+            const uint32_t L = ((uint32_t)in->bytes[p] << 8) | in->bytes[p + 1];
+            if (p + 2 + L > end) { stop = SF_WIRE_PARTIAL; break; }
+            if (L + 2 > SF_WIRE_MAX_FRAME) { p += 2 + L; nframes++; continue; }   /* TooLongFrameException */
+            so_wire_req r;
+            const int k = so_wire_decode(in->bytes + p + 2, L, &r);
+            if (k == WF_HOST) { stop = SF_WIRE_HOST; break; }
+            nframes++;
+            if (k != WF_NONE) { reqs[nr] = r; kind[nr] = (uint8_t)k; rstream[nr] = s; nr++; }
+            p += 2 + L;
+        }
+        out->consumed[s] = p - in->stream_off[s];
+        out->stop[s] = stop;
+    }
+    /* the token service, in (stream, frame) order */
+    uint64_t nq = 0;
+    for (uint64_t i = 0; i < nr; i++) nq += kind[i] == WF_REQ;
+    int64_t* fid = (int64_t*)calloc(nq + 1, 8); int32_t* cnt = (int32_t*)calloc(nq + 1, 4);
+    uint8_t* fl = (uint8_t*)calloc(nq + 1, 1); int64_t* ts = (int64_t*)calloc(nq + 1, 8);
+    uint8_t* tg = (uint8_t*)calloc(nq + 1, 1); uint64_t* bt = (uint64_t*)calloc(nq + 1, 8);
+    int8_t* st = (int8_t*)calloc(nq + 1, 1); int32_t* rm = (int32_t*)calloc(nq + 1, 4); int32_t* wt = (int32_t*)calloc(nq + 1, 4);
+    for (uint64_t i = 0, j = 0; i < nr; i++) {
+        if (kind[i] != WF_REQ) continue;
+        fid[j] = reqs[i].flow_id; cnt[j] = reqs[i].count; ts[j] = in->now_ms;
+        fl[j] = (uint8_t)((reqs[i].prio ? SF_TOK_PRIORITIZED : 0) | (reqs[i].param ? SF_TOK_PARAM : 0));
+        tg[j] = reqs[i].tag; bt[j] = reqs[i].bits; j++;
+    }
+    int rc = SF_OK;
+    if (nq) {
+        sf_token_batch b = {(uint32_t)nq, SF_MEM_HOST, fid, cnt, fl, ts, tg, bt};
+        sf_token_results o = {SF_MEM_HOST, st, rm, wt};
+        rc = so_request_tokens(e, &b, &o);
+    }
+    /* responses: LengthFieldPrepender(2) + xid, type, status, FlowTokenResponseData */
+    const uint64_t need = nr * SF_WIRE_RESP_BYTES;
+    uint32_t s_cur = 0;
+    out->resp_off[0] = 0;
+    for (uint64_t i = 0, j = 0; i < nr && rc == SF_OK; i++) {
+        while (s_cur < rstream[i]) out->resp_off[++s_cur] = i * SF_WIRE_RESP_BYTES;
+        if (need > out->cap) continue;
+        uint8_t* o = out->resp + i * SF_WIRE_RESP_BYTES;
+        int8_t status = SF_TOKEN_BAD_REQUEST; int32_t remaining = 0, wait = 0;
+        if (kind[i] == WF_REQ) {
+            status = st[j]; remaining = rm[j];
+            wait = reqs[i].param ? 0 : wt[j];        /* ParamFlowRequestProcessor: setWaitInMs(0) */
+            j++;
+        }
+        o[0] = 0; o[1] = 14;
+        wput32(o + 2, (uint32_t)reqs[i].xid);
+        o[6] = (uint8_t)reqs[i].type;
+        o[7] = (uint8_t)status;
+        wput32(o + 8, (uint32_t)remaining);
+        wput32(o + 12, (uint32_t)wait);
+    }
+    while (s_cur < S) out->resp_off[++s_cur] = nr * SF_WIRE_RESP_BYTES;
+    out->n_frames = nframes; out->n_requests = nq; out->n_responses = nr;
+    free(reqs); free(kind); free(rstream);
+    free(fid); free(cnt); free(fl); free(ts); free(tg); free(bt); free(st); free(rm); free(wt);
+    if (rc == SF_OK && need > out->cap) return SF_ERR_CAPACITY;
+    return rc;
+}

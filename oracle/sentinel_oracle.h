@@ -210,6 +210,9 @@ int  so_load_cluster_rules(so_engine* e, const sf_cluster_flow_rule* flow, uint3
                            const sf_hot_item* items, uint32_t n_items);
 int  so_request_tokens(so_engine* e, const sf_token_batch* in, sf_token_results* out);
 int64_t so_cluster_sum(so_engine* e, int64_t flow_id, int event, int64_t now);
+/* token-server wire path (sf_serve_frames contract, sentinel_flow.h) */
+uint64_t so_string_key(const uint8_t* b, uint32_t len);
+int  so_serve_frames(so_engine* e, const sf_wire_batch* in, sf_wire_out* out);
 
 #ifdef __cplusplus
 }

@@ -32,7 +32,7 @@ RES_ENTRY_NODE = 0xFFFFFFFF      # sf_metric_row.resource of Constants.ENTRY_NOD
 SF_MAX_RULES_PER_RESOURCE = 8
 SF_MAX_ARGS = 4
 
-TAG_NULL, TAG_INT, TAG_LONG, TAG_STRING, TAG_DOUBLE, TAG_BOOL, TAG_OTHER = range(7)
+TAG_NULL, TAG_INT, TAG_LONG, TAG_STRING, TAG_DOUBLE, TAG_BOOL, TAG_OTHER, TAG_BYTE, TAG_SHORT, TAG_FLOAT = range(10)
 
 EV_EXIT, EV_IN, EV_PRIO, EV_ERROR = 0x01, 0x02, 0x04, 0x08
 MEM_HOST, MEM_DEVICE = 0, 1
@@ -176,7 +176,8 @@ class sf_stats(C.Structure):
                 ("scatter_ms", C.c_double), ("n_events", C.c_uint64), ("n_segments", C.c_uint64),
                 ("n_launches", C.c_uint64), ("light_ms", C.c_double), ("heavy_decide_ms", C.c_double),
                 ("heavy_fill_ms", C.c_double), ("classify_ms", C.c_double),
-                ("stream_ms", C.c_double), ("metric_scan_ms", C.c_double), ("metric_log_ms", C.c_double)]
+                ("stream_ms", C.c_double), ("metric_scan_ms", C.c_double), ("metric_log_ms", C.c_double),
+                ("wire_ms", C.c_double)]
 
 
 class sf_heavy_profile(C.Structure):
@@ -368,3 +369,52 @@ def flow_rules_ptr(rules):
         assert rules.dtype == FLOW_RULE_DTYPE
         return C.cast(rules.ctypes.data, C.POINTER(sf_flow_rule)), rules.shape[0]
     return rules_array(sf_flow_rule, list(rules)), len(rules)
+
+
+WIRE_DONE, WIRE_PARTIAL, WIRE_HOST = 0, 1, 2
+WIRE_RESP_BYTES = 16
+
+
+class sf_wire_batch(C.Structure):
+    _fields_ = [("mem", C.c_int32), ("n_streams", C.c_uint32), ("bytes", C.c_void_p), ("stream_off", C.c_void_p),
+                ("now_ms", C.c_int64)]
+
+
+class sf_wire_out(C.Structure):
+    _fields_ = [("resp", C.c_void_p), ("cap", C.c_uint64), ("resp_off", C.c_void_p), ("consumed", C.c_void_p),
+                ("stop", C.c_void_p), ("n_frames", C.c_uint64), ("n_requests", C.c_uint64),
+                ("n_responses", C.c_uint64)]
+
+
+STRUCT_SIZES.update({"sf_wire_batch": C.sizeof(sf_wire_batch), "sf_wire_out": C.sizeof(sf_wire_out)})
+
+
+class WireResult:
+    """Result of one sf_serve_frames / so_serve_frames call over host memory."""
+
+    def __init__(self, streams, now_ms):
+        self.streams = [bytes(x) for x in streams]
+        S = len(self.streams)
+        self.data = np.frombuffer(b"".join(self.streams) + b"\0" * 16, dtype=np.uint8)
+        self.off = np.zeros(S + 1, np.uint64)
+        self.off[1:] = np.cumsum([len(x) for x in self.streams])
+        total = int(self.off[-1])
+        self.resp = np.zeros(max(total // 2 + 1, 1) * WIRE_RESP_BYTES, np.uint8)
+        self.resp_off = np.zeros(S + 1, np.uint64)
+        self.consumed = np.zeros(S, np.uint64)
+        self.stop = np.zeros(S, np.uint8)
+        self.now_ms = now_ms
+
+    def c_structs(self):
+        b = sf_wire_batch(MEM_HOST, len(self.streams), self.data.ctypes.data, self.off.ctypes.data, self.now_ms)
+        o = sf_wire_out(self.resp.ctypes.data, self.resp.size, self.resp_off.ctypes.data, self.consumed.ctypes.data,
+                        self.stop.ctypes.data, 0, 0, 0)
+        return b, o
+
+    def finish(self, o):
+        self.n_frames, self.n_requests, self.n_responses = o.n_frames, o.n_requests, o.n_responses
+        self.resp = self.resp[: int(self.resp_off[-1])]
+        return self
+
+    def responses(self, s):
+        return bytes(self.resp[int(self.resp_off[s]): int(self.resp_off[s + 1])])

@@ -15,6 +15,7 @@
 
 #include "sf_decide.h"
 #include "sf_token.h"
+#include "sf_wire.h"
 #include <rccl/rccl.h>
 #include <unordered_map>
 
@@ -71,6 +72,7 @@ struct sf_engine {
     std::vector<int64_t> cflow_ids;           // flow rule index -> flowId
     void* tok_stage = nullptr; size_t tok_stage_bytes = 0;
     int64_t* d_sum = nullptr;
+    void* wire_arena = nullptr; size_t wire_bytes = 0;   // sf_serve_frames scratch (grow-only)
     // ENTRY_NODE and the metric snapshot (sf_entry.hip)
     EntryNode* en = nullptr;
     EntryAcc* en_acc = nullptr;
@@ -149,7 +151,7 @@ void sf_destroy(sf_engine* e) {
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
-                     (void*)e->ts.items, e->tok_stage, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
+                     (void*)e->ts.items, e->tok_stage, e->wire_arena, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
                      e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch, e->nm_bytes, e->nm_off,
                      e->nm_types, e->ml_mask, e->ml_counts, e->ml_offsets, e->ml_total, e->ml_rows, e->ml_keys,
                      e->ml_order, e->ml_len, e->ml_off, e->ml_bytes, e->ml_out, e->ml_tmp};
@@ -1018,6 +1020,17 @@ static int tok_work_ensure(sf_engine* e, uint32_t n) {
     return SF_OK;
 }
 
+// token state present (rules built, namespace limiter allocated); caller holds e->mu
+static int tok_ready(sf_engine* e) {
+    if (!e->ts.rules) { int r2 = tok_rebuild(e, true); if (r2) return r2; }
+    if (!e->ts.lim) {
+        LimState z; for (int k = 0; k < LIM_S; k++) { z.ws[k] = WS_NONE; z.v[k] = 0; }
+        HIP_TRY(hipMalloc((void**)&e->ts.lim, sizeof(LimState)));
+        HIP_TRY(hipMemcpy(e->ts.lim, &z, sizeof z, hipMemcpyHostToDevice));
+    }
+    return SF_OK;
+}
+
 int sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* out) {
     if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
     if (in->n == 0) return SF_OK;
@@ -1027,12 +1040,7 @@ int sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* 
     const uint32_t n = in->n;
     int rc = tok_work_ensure(e, n);
     if (rc) return fail(rc, "token work buffers");
-    if (!e->ts.rules) { int r2 = tok_rebuild(e, true); if (r2) return r2; }
-    if (!e->ts.lim) {
-        LimState z; for (int k = 0; k < LIM_S; k++) { z.ws[k] = WS_NONE; z.v[k] = 0; }
-        HIP_TRY(hipMalloc((void**)&e->ts.lim, sizeof(LimState)));
-        HIP_TRY(hipMemcpy(e->ts.lim, &z, sizeof z, hipMemcpyHostToDevice));
-    }
+    { int r2 = tok_ready(e); if (r2) return r2; }
     hipStream_t s = e->stream;
     TokBatch b{};
     b.n = n;
@@ -1086,6 +1094,138 @@ int sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* 
     HIP_TRY(hipMemcpyAsync(&err, e->st.err, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (err) return fail(err, err == SF_ERR_CAPACITY ? "cluster param table capacity exceeded" : "invalid token batch");
+    return SF_OK;
+}
+
+uint64_t sf_string_key(const uint8_t* bytes, uint32_t len) {   // FNV-1a 64 (the wire path's String key)
+    uint64_t h = 0xcbf29ce484222325ULL;
+    for (uint32_t i = 0; i < len; i++) { h ^= bytes[i]; h *= 0x100000001b3ULL; }
+    return h;
+}
+
+int sf_serve_frames(sf_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
+    if (!e || !in || !out || !in->stream_off || !out->resp_off || !out->consumed || !out->stop)
+        return fail(SF_ERR_INVALID, "null argument");
+    if (in->n_streams == 0) return fail(SF_ERR_INVALID, "n_streams must be > 0");
+    const uint32_t S = in->n_streams;
+    std::vector<uint64_t> soff(S + 1);
+    if (in->mem == SF_MEM_HOST) std::memcpy(soff.data(), in->stream_off, (S + 1) * sizeof(uint64_t));
+    else HIP_TRY(hipMemcpy(soff.data(), in->stream_off, (S + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (uint32_t s = 0; s < S; s++)
+        if (soff[s + 1] < soff[s]) return fail(SF_ERR_INVALID, "stream_off must be non-decreasing");
+    if (soff[S] >= (1ull << 31)) return fail(SF_ERR_CAPACITY, "wire batch must be < 2^31 bytes");
+    if (soff[S] && !in->bytes) return fail(SF_ERR_INVALID, "null bytes");
+    std::lock_guard<std::mutex> lk(e->mu);
+    out->n_frames = out->n_requests = out->n_responses = 0;
+    const uint32_t n = (uint32_t)soff[S];
+    if (soff[0] == n) {                          // nothing to read: every stream handled, no response
+        for (uint32_t s = 0; s < S; s++) { out->consumed[s] = 0; out->stop[s] = SF_WIRE_DONE; }
+        for (uint32_t s = 0; s <= S; s++) out->resp_off[s] = 0;
+        return SF_OK;
+    }
+    { int r2 = tok_ready(e); if (r2) return r2; }
+    hipStream_t st = e->stream;
+    WireBufs w{};
+    w.n = n; w.S = S;
+    w.n_tiles = (n + WIRE_TILE - 1) / WIRE_TILE;
+    const uint32_t F = n / 2 + 1;                 // frames are >= 2 bytes
+    size_t tmp = 0;
+    { hipError_t qe = wire_query_temp(w.n_tiles, S, F, &tmp);
+      if (qe != hipSuccess) return fail(SF_ERR_DEVICE, std::string("wire temp: ") + hipGetErrorString(qe)); }
+    // one grow-only arena, 256-B aligned pieces
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + std::max<size_t>(bytes, 16)); return o; };
+    const bool host_in = in->mem == SF_MEM_HOST;
+    const size_t o_bytes = host_in ? take(n + 16) : 0, o_soff = host_in ? take((S + 1) * 8) : 0;
+    const size_t o_exit = take((size_t)n * 4), o_tent = take((size_t)w.n_tiles * 4),
+                 o_bm = take((size_t)w.n_tiles * (WIRE_TILE / 32) * 4), o_tc = take(((size_t)w.n_tiles + 1) * 4),
+                 o_tb = take(((size_t)w.n_tiles + 1) * 4), o_cons = take((size_t)S * 4), o_stop = take((size_t)S * 4),
+                 o_rsc = take(((size_t)S + 1) * 4), o_fr = take((size_t)F * 4), o_wf = take((size_t)F * sizeof(WFrame)),
+                 o_fl = take((size_t)F * 8), o_pos = take((size_t)F * 8), o_cnt = take(16),
+                 o_qf = take((size_t)F * 8), o_qc = take((size_t)F * 4), o_qfl = take(F), o_qts = take((size_t)F * 8),
+                 o_qtg = take(F), o_qb = take((size_t)F * 8), o_rs = take(F), o_rr = take((size_t)F * 4),
+                 o_rw = take((size_t)F * 4), o_resp = take((size_t)F * 16), o_sb = take(S),
+                 o_crel = take((size_t)S * 8), o_tmp = take(tmp);
+    if (off > e->wire_bytes) {
+        if (e->wire_arena) hipFree(e->wire_arena);
+        e->wire_arena = nullptr; e->wire_bytes = 0;
+        HIP_TRY(hipMalloc(&e->wire_arena, off));
+        e->wire_bytes = off;
+    }
+    char* A = (char*)e->wire_arena;
+    if (host_in) {
+        HIP_TRY(hipMemcpyAsync(A + o_bytes, in->bytes, n, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(A + o_soff, soff.data(), (S + 1) * 8, hipMemcpyHostToDevice, st));
+        w.bytes = (const uint8_t*)(A + o_bytes); w.soff = (const uint64_t*)(A + o_soff);
+    } else {
+        w.bytes = in->bytes; w.soff = in->stream_off;
+    }
+    w.exitv = (uint32_t*)(A + o_exit); w.tentry = (uint32_t*)(A + o_tent); w.bitmap = (uint32_t*)(A + o_bm);
+    w.tcount = (uint32_t*)(A + o_tc); w.tbase = (uint32_t*)(A + o_tb); w.consumed = (uint32_t*)(A + o_cons);
+    w.stopoff = (uint32_t*)(A + o_stop); w.resp_cnt = nullptr; w.resp_scan = (uint32_t*)(A + o_rsc);
+    w.frames = (uint32_t*)(A + o_fr); w.wf = (WFrame*)(A + o_wf); w.fl = (uint64_t*)(A + o_fl);
+    w.pos = (uint64_t*)(A + o_pos); w.counters = (uint32_t*)(A + o_cnt);
+    w.q_fid = (int64_t*)(A + o_qf); w.q_cnt = (int32_t*)(A + o_qc); w.q_flags = (uint8_t*)(A + o_qfl);
+    w.q_ts = (int64_t*)(A + o_qts); w.q_tag = (uint8_t*)(A + o_qtg); w.q_bits = (uint64_t*)(A + o_qb);
+    w.r_status = (int8_t*)(A + o_rs); w.r_rem = (int32_t*)(A + o_rr); w.r_wait = (int32_t*)(A + o_rw);
+    w.resp = (uint8_t*)(A + o_resp); w.stop = (uint8_t*)(A + o_sb); w.consumed_rel = (uint64_t*)(A + o_crel);
+    w.tmp = A + o_tmp; w.tmp_bytes = tmp;
+
+    if (e->timing) HIP_TRY(hipEventRecord(e->ml_ev[0], st));
+    hipError_t le = wire_frame(w, st);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("wire framing: ") + hipGetErrorString(le));
+    uint32_t nf = 0;
+    HIP_TRY(hipMemcpyAsync(&nf, w.tbase + w.n_tiles, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    uint64_t tot[2] = {0, 0};
+    if (nf) {
+        le = wire_decode(w, nf, in->now_ms, st);
+        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("wire decode: ") + hipGetErrorString(le));
+        HIP_TRY(hipMemcpyAsync(&tot[0], w.pos + nf - 1, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&tot[1], w.fl + nf - 1, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    const uint64_t both = tot[0] + tot[1];
+    const uint32_t n_req = (uint32_t)(both >> 32), n_resp = (uint32_t)both;
+    HIP_TRY(hipMemsetAsync(e->st.err, 0, sizeof(int32_t), st));
+    if (n_req) {
+        int rc = tok_work_ensure(e, n_req);
+        if (rc) return fail(rc, "token work buffers");
+        le = wire_compact(w, nf, in->now_ms, st);
+        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("wire compact: ") + hipGetErrorString(le));
+        TokBatch b{};
+        b.n = n_req; b.flow_id = w.q_fid; b.count = w.q_cnt; b.flags = w.q_flags; b.ts = w.q_ts;
+        b.ptag = w.q_tag; b.pbits = w.q_bits;
+        TokOut o{w.r_status, w.r_rem, w.r_wait};
+        le = tok_launch(e->ts, e->tw, b, o, st);
+        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("token launch: ") + hipGetErrorString(le));
+    }
+    le = wire_encode(w, nf, st);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("wire encode: ") + hipGetErrorString(le));
+    if (e->timing) HIP_TRY(hipEventRecord(e->ml_ev[1], st));
+    const bool fits = (uint64_t)n_resp * SF_WIRE_RESP_BYTES <= out->cap;
+    if (fits && n_resp) {
+        if (!out->resp) return fail(SF_ERR_INVALID, "null resp");
+        HIP_TRY(hipMemcpyAsync(out->resp, w.resp, (size_t)n_resp * SF_WIRE_RESP_BYTES, hipMemcpyDeviceToHost, st));
+    }
+    std::vector<uint32_t> roff(S + 1);
+    uint32_t handled = 0;
+    int32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(roff.data(), w.resp_scan, (S + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->consumed, w.consumed_rel, (size_t)S * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->stop, w.stop, S, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&handled, w.counters, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&err, e->st.err, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (e->timing) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, e->ml_ev[0], e->ml_ev[1]));
+        e->stats.wire_ms = ms;
+    }
+    for (uint32_t s = 0; s <= S; s++) out->resp_off[s] = (uint64_t)roff[s] * SF_WIRE_RESP_BYTES;
+    out->n_frames = handled; out->n_requests = n_req; out->n_responses = n_resp;
+    if (err) return fail(err, err == SF_ERR_CAPACITY ? "cluster param table capacity exceeded" : "invalid token batch");
+    if (!fits) return fail(SF_ERR_CAPACITY, "response buffer too small (n_responses * 16 bytes needed)");
     return SF_OK;
 }
 

@@ -67,6 +67,8 @@ def _declare(L):
     f("sf_load_cluster_rules", I, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
     f("sf_request_tokens", I, P, C.POINTER(abi.sf_token_batch), C.POINTER(abi.sf_token_results))
+    f("sf_serve_frames", I, P, C.POINTER(abi.sf_wire_batch), C.POINTER(abi.sf_wire_out))
+    f("sf_string_key", C.c_uint64, C.c_char_p, C.c_uint32)
     f("sf_cluster_sum", I, P, C.c_int64, I, C.c_int64, C.POINTER(C.c_int64))
     f("sf_comm_unique_id", I, C.c_char_p, C.c_size_t)
     f("sf_comm_init", I, P, I, I, C.c_char_p, C.c_size_t)
@@ -333,6 +335,13 @@ class FlowEngine:
         r = out.c_struct()
         _check(lib().sf_request_tokens(self.h, C.byref(b), C.byref(r)))
         return out
+
+    def serve_frames(self, streams, now_ms) -> abi.WireResult:
+        """Inbound C1 bytes of each connection -> response frames (sf_serve_frames)."""
+        r = abi.WireResult(streams, now_ms)
+        b, o = r.c_structs()
+        _check(lib().sf_serve_frames(self.h, C.byref(b), C.byref(o)))
+        return r.finish(o)
 
     def cluster_sum(self, flow_id, event, now):
         v = C.c_int64()

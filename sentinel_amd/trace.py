@@ -271,3 +271,72 @@ def token_workload(n_req: int, n_flow: int = 200, n_param: int = 40, n_values: i
     fid = np.where(bad & (kind == 3), 10 ** 9, fid)          # no such rule
     batch = abi.HostTokenBatch(fid, cnt, flags, ts, param_tag=tag, param_bits=vals)
     return ns, flow, param, items, batch
+
+
+def wire_workload(n_req: int, n_streams: int = 500, seed: int = 11, edge: bool = False, **kw):
+    """Config 5 over the wire: the token_workload requests written as C1 frames
+    by the reference client codec (sentinel_amd.wire), spread over
+    ``n_streams`` connections (time order kept per connection).  Param values
+    go out as Long (mostly), Integer or String.  ``edge`` mixes in the frames
+    the reference server treats specially: too-long frames (skipped, some
+    spanning many framing tiles), empty frames, FLOW without the priority
+    byte, a type without a decoder, unknown parameter tags, null-only params
+    (amount 0), and near each connection's end PING / multi-value / malformed
+    frames (where the engine hands the rest to the host).
+    Returns (namespaces, flow_rules, param_rules, items, streams)."""
+    import struct
+    from . import wire
+    ns, flow, param, items, b = token_workload(n_req, seed=seed, **kw)
+    rng = np.random.default_rng(seed + 1)
+    streams = [bytearray() for _ in range(n_streams)]
+    xid = np.zeros(n_streams, np.int64)
+    conn = rng.integers(0, n_streams, b.n)
+    kinds = rng.random(b.n)
+    for i in range(b.n):
+        s = int(conn[i])
+        x = int(xid[s]); xid[s] += 1
+        fid, c = int(b.flow_id[i]), int(b.count[i])
+        if b.flags[i] & abi.TOK_PARAM:
+            if b.param_tag[i] == abi.TAG_NULL:
+                params = [None]
+            else:
+                v = int(b.param_bits[i])
+                sv = v - (1 << 64) if v >= 1 << 63 else v
+                params = [("long", sv)] if kinds[i] < 0.8 else ([("int", sv & 0x7fffffff)] if kinds[i] < 0.9
+                                                                 else [("str", "v%d" % v)])
+            streams[s] += wire.param_frame(x, fid, c, params)
+        else:
+            streams[s] += wire.flow_frame(x, fid, c, bool(b.flags[i] & abi.TOK_PRIORITIZED))
+        if edge and rng.random() < 0.03:
+            e = int(rng.integers(0, 7))
+            if e == 0:                                   # too long: skipped without a response
+                L = int(rng.integers(1023, 1100)) if rng.random() < 0.7 else int(rng.integers(20000, 65536))
+                streams[s] += struct.pack(">H", L) + rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+            elif e == 1:
+                streams[s] += wire.frame(b"")
+            elif e == 2:                                 # FLOW without the priority byte
+                streams[s] += wire.frame(struct.pack(">ibqi", x + 100000, 1, fid if fid > 0 else 1, 1))
+            elif e == 3:                                 # no decoder, no data: nothing happens
+                streams[s] += wire.frame(struct.pack(">ib", x + 200000, 9))
+            elif e == 4:                                 # unknown parameter tag skipped, one Long value
+                body = struct.pack(">ibqii", x + 300000, 2, 201 + int(rng.integers(0, 40)), 1, 2) + bytes([99]) + \
+                    wire.encode_param(("long", int(rng.integers(0, 50))))
+                streams[s] += wire.frame(body)
+            elif e == 5:                                 # FLOW / PARAM_FLOW with no data: no response
+                streams[s] += wire.frame(struct.pack(">ib", x + 400000, int(rng.integers(1, 3))))
+            else:                                        # only non-primitive params: empty -> BAD_REQUEST
+                body = struct.pack(">ibqii", x + 500000, 2, 205, 1, 1) + bytes([77])
+                streams[s] += wire.frame(body)
+    if edge:
+        for s in range(n_streams):
+            r = rng.random()
+            if r < 0.1:
+                streams[s] += wire.ping_frame(9999, "default") + wire.flow_frame(1, 1, 1)
+            elif r < 0.15:
+                streams[s] += wire.param_frame(9998, 201, 1, [("long", 1), ("long", 2)]) + wire.flow_frame(2, 1, 1)
+            elif r < 0.2:                               # bytes left after the data: Netty would cumulate them
+                streams[s] += wire.frame(struct.pack(">ibqi?", 9997, 1, 1, 1, False) + b"\x00\x01")
+            elif r < 0.3:                               # incomplete last frame
+                f = wire.flow_frame(9996, 1, 1)
+                streams[s] += f[: int(rng.integers(1, len(f)))]
+    return ns, flow, param, items, [bytes(x) for x in streams]
