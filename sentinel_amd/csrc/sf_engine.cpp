@@ -1171,7 +1171,10 @@ int sf_serve_frames(sf_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
     w.resp = (uint8_t*)(A + o_resp); w.stop = (uint8_t*)(A + o_sb); w.consumed_rel = (uint64_t*)(A + o_crel);
     w.tmp = A + o_tmp; w.tmp_bytes = tmp;
 
-    if (e->timing) HIP_TRY(hipEventRecord(e->ml_ev[0], st));
+    if (e->timing) {
+        for (auto& x : e->ml_ev) if (!x) HIP_TRY(hipEventCreate(&x));
+        HIP_TRY(hipEventRecord(e->ml_ev[0], st));
+    }
     hipError_t le = wire_frame(w, st);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("wire framing: ") + hipGetErrorString(le));
     uint32_t nf = 0;
