@@ -445,6 +445,55 @@ int  sf_comm_unique_id(uint8_t* out, size_t len /* >= 128 */);
 int  sf_comm_init(sf_engine* e, int nranks, int rank, const uint8_t* id, size_t len);
 int  sf_entry_node_allreduce(sf_engine* e, sf_node_state* out);
 
+/* ---- DegradeSlot circuit breakers -----------------
+ * Replaces DegradeSlot.performChecking / exit (DegradeSlot.java:50-94) and
+ * the breakers behind DegradeRuleManager.getCircuitBreakers
+ * (DegradeRuleManager.java:236-265): ResponseTimeCircuitBreaker
+ * (ResponseTimeCircuitBreaker.java:64-130) and ExceptionCircuitBreaker
+ * (ExceptionCircuitBreaker.java:64-119) over AbstractCircuitBreaker's
+ * CLOSED/OPEN/HALF_OPEN machine (AbstractCircuitBreaker.java:67-173).
+ * sf_degrade_submit runs a degrade-only chain: ENTRY -> tryPass of each
+ * breaker of the resource in rule order (first refusal = DegradeException;
+ * a breaker moved OPEN->HALF_OPEN by this entry falls back to OPEN through
+ * the whenTerminate hook, :113-129); EXIT of a passed entry ->
+ * onRequestComplete of every breaker with rt = exit ts - create ts and the
+ * SF_EV_ERROR flag (Tracer error).  Loading rules resets breaker state.   */
+#define SF_DEGRADE_GRADE_RT              0   /* RuleConstant.DEGRADE_GRADE_RT */
+#define SF_DEGRADE_GRADE_EXCEPTION_RATIO 1
+#define SF_DEGRADE_GRADE_EXCEPTION_COUNT 2
+#define SF_V_BLOCK_DEGRADE 8   /* DegradeException (rule_idx = breaker index in the resource's list) */
+#define SF_CB_CLOSED    0
+#define SF_CB_OPEN      1
+#define SF_CB_HALF_OPEN 2
+#define SF_MAX_BREAKERS_PER_RESOURCE 64
+
+typedef struct sf_degrade_rule {   /* DegradeRule (DegradeRule.java) */
+    uint32_t resource;
+    int32_t  grade;                /* SF_DEGRADE_GRADE_* */
+    double   count;                /* RT: max allowed rt (Math.round); ratio / count threshold */
+    int32_t  time_window_s;        /* recovery timeout = time_window_s * 1000 */
+    int32_t  min_request_amount;   /* default 5 */
+    double   slow_ratio_threshold; /* RT grade only, default 1.0 */
+    int32_t  stat_interval_ms;     /* default 1000 */
+    int32_t  pad;
+} sf_degrade_rule;
+
+typedef struct sf_breaker_state {  /* one circuit breaker after the last batch */
+    int32_t  state;                /* SF_CB_* */
+    int32_t  pad;
+    int64_t  next_retry_ms;        /* nextRetryTimestamp */
+    int64_t  window_start;         /* its single stat bucket (LeapArray(1, statIntervalMs)) */
+    int64_t  hit_count;            /* slowCount (RT) / errorCount (exception) */
+    int64_t  total_count;
+} sf_breaker_state;
+
+/* Invalid rules (DegradeRuleManager.isValidRule :183-204) are skipped like
+ * the reference; *n_loaded (may be NULL) = breakers installed, whose
+ * indices (load order of the valid rules) sf_read_breaker takes. */
+int  sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t n, uint32_t* n_loaded);
+int  sf_degrade_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
+int  sf_read_breaker(sf_engine* e, uint32_t breaker_index, sf_breaker_state* out);
+
 /* Device helpers so hosts without a GPU framework can stage HBM inputs. */
 int  sf_device_alloc(sf_engine* e, size_t bytes, void** ptr);
 int  sf_device_free(sf_engine* e, void* ptr);

@@ -418,3 +418,32 @@ class WireResult:
 
     def responses(self, s):
         return bytes(self.resp[int(self.resp_off[s]): int(self.resp_off[s + 1])])
+
+
+# ---- DegradeSlot circuit breakers (include/sentinel_flow.h, sf_degrade_*) ----
+V_BLOCK_DEGRADE = 8
+DEGRADE_GRADE_RT, DEGRADE_GRADE_EXCEPTION_RATIO, DEGRADE_GRADE_EXCEPTION_COUNT = 0, 1, 2
+CB_CLOSED, CB_OPEN, CB_HALF_OPEN = 0, 1, 2
+
+
+class sf_degrade_rule(C.Structure):
+    _fields_ = [("resource", C.c_uint32), ("grade", C.c_int32), ("count", C.c_double),
+                ("time_window_s", C.c_int32), ("min_request_amount", C.c_int32),
+                ("slow_ratio_threshold", C.c_double), ("stat_interval_ms", C.c_int32), ("pad", C.c_int32)]
+
+
+class sf_breaker_state(C.Structure):
+    _fields_ = [("state", C.c_int32), ("pad", C.c_int32), ("next_retry_ms", C.c_int64),
+                ("window_start", C.c_int64), ("hit_count", C.c_int64), ("total_count", C.c_int64)]
+
+
+def degrade_rule(resource, grade, count, time_window_s, min_request_amount=5, slow_ratio_threshold=1.0,
+                 stat_interval_ms=1000) -> dict:
+    """DegradeRule with the reference defaults (DegradeRule.java: minRequestAmount 5,
+    slowRatioThreshold 1.0, statIntervalMs 1000)."""
+    return dict(resource=resource, grade=grade, count=float(count), time_window_s=time_window_s,
+                min_request_amount=min_request_amount, slow_ratio_threshold=float(slow_ratio_threshold),
+                stat_interval_ms=stat_interval_ms)
+
+
+STRUCT_SIZES.update({"sf_degrade_rule": C.sizeof(sf_degrade_rule), "sf_breaker_state": C.sizeof(sf_breaker_state)})

@@ -16,6 +16,7 @@
 #include "sf_decide.h"
 #include "sf_token.h"
 #include "sf_wire.h"
+#include "sf_degrade.h"
 #include <rccl/rccl.h>
 #include <unordered_map>
 
@@ -91,6 +92,11 @@ struct sf_engine {
     // node-wide aggregate over the ranks of a node (RCCL over xGMI)
     ncclComm_t comm = nullptr;
     int64_t* agg = nullptr;               // [ws (S+60) | gws (S+60) | vals ((S+60)*6+1) | minrt (S+60)]
+    // DegradeSlot circuit breakers (sf_degrade.hip)
+    DegradeDev dg{};
+    DegradeWork dgw{};
+    std::vector<uint32_t> dg_pos;         // breaker index (load order) -> CSR position
+    void* dg_stage = nullptr; size_t dg_stage_bytes = 0;
 };
 
 static void free_tok_work(TokWork& w) {
@@ -157,6 +163,10 @@ void sf_destroy(sf_engine* e) {
                      e->ml_order, e->ml_len, e->ml_off, e->ml_bytes, e->ml_out, e->ml_tmp};
     for (void* p : tptrs) if (p) hipFree(p);
     if (e->agg) hipFree(e->agg);
+    void* dptrs[] = {(void*)e->dg.rr_of, (void*)e->dg.off, (void*)e->dg.rules, e->dg.state, e->dgw.keys_in,
+                     e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
+                     e->dgw.err, e->dg_stage};
+    for (void* p : dptrs) if (p) hipFree(p);
     if (e->comm) ncclCommDestroy(e->comm);
     free_tok_work(e->tw);
     for (auto& a : e->evs) for (auto& x : a) if (x) hipEventDestroy(x);
@@ -1396,6 +1406,203 @@ int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uin
         }
     }
     *n_out = nh;
+    return SF_OK;
+}
+
+
+// ---------------------------------------------------------------- DegradeSlot circuit breakers
+// DegradeRuleManager.isValidRule (DegradeRuleManager.java:183-204)
+static bool dg_valid(const sf_degrade_rule& r) {
+    if (!(r.count >= 0) || r.time_window_s <= 0) return false;
+    if (r.min_request_amount <= 0 || r.stat_interval_ms <= 0) return false;
+    switch (r.grade) {
+        case SF_DEGRADE_GRADE_RT: return r.slow_ratio_threshold >= 0 && r.slow_ratio_threshold <= 1;
+        case SF_DEGRADE_GRADE_EXCEPTION_RATIO: return r.count <= 1;
+        case SF_DEGRADE_GRADE_EXCEPTION_COUNT: return true;
+        default: return false;
+    }
+}
+
+int sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t n, uint32_t* n_loaded) {
+    if (!e || (n && !rules)) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    const int rc = drain(e);
+    if (rc) return rc;
+    // buildCircuitBreakers (DegradeRuleManager.java:236-265): valid rules, list order per resource
+    std::vector<uint32_t> loc, valid;
+    for (uint32_t i = 0; i < n; i++) {
+        if (!dg_valid(rules[i])) continue;
+        uint32_t l;
+        if (!local_of(e, rules[i].resource, &l)) return fail(SF_ERR_INVALID, "degrade rule resource outside this shard");
+        valid.push_back(i);
+        loc.push_back(l);
+    }
+    const uint32_t nv = (uint32_t)valid.size();
+    std::vector<uint32_t> order(nv);
+    for (uint32_t i = 0; i < nv; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return loc[a] < loc[b]; });
+    std::vector<uint32_t> rr_of(e->R, 0), off;
+    std::vector<DevBreakerRule> dr(nv);
+    std::vector<sf_breaker_state> st(nv);
+    e->dg_pos.assign(nv, 0);
+    uint32_t n_rres = 0;
+    for (uint32_t p = 0; p < nv; p++) {
+        const uint32_t v = order[p];
+        if (p == 0 || loc[order[p - 1]] != loc[v]) {
+            off.push_back(p);
+            n_rres++;
+        }
+        if (p > 0 && loc[order[p - 1]] == loc[v] && p - off.back() >= SF_MAX_BREAKERS_PER_RESOURCE)
+            return fail(SF_ERR_UNSUPPORTED, "more than SF_MAX_BREAKERS_PER_RESOURCE degrade rules on one resource");
+        const sf_degrade_rule& r = rules[valid[v]];
+        DevBreakerRule& d = dr[p];
+        d.grade = r.grade;
+        d.min_req = r.min_request_amount;
+        d.max_rt = (int64_t)std::floor(r.count + 0.5);           // Math.round (ResponseTimeCircuitBreaker.java:52)
+        d.thr = r.grade == SF_DEGRADE_GRADE_RT ? r.slow_ratio_threshold : r.count;
+        d.recovery = (int64_t)r.time_window_s * 1000;
+        d.interval = r.stat_interval_ms;
+        st[p] = sf_breaker_state{SF_CB_CLOSED, 0, 0, DG_WS_NONE, 0, 0};
+        e->dg_pos[v] = p;
+    }
+    off.push_back(nv);
+    for (auto& x : rr_of) x = n_rres;
+    for (uint32_t k = 0; k < n_rres; k++) rr_of[loc[order[off[k]]]] = k;
+    void* dptrs[] = {(void*)e->dg.rr_of, (void*)e->dg.off, (void*)e->dg.rules, e->dg.state};
+    for (void* p : dptrs) if (p) hipFree(p);
+    e->dg = DegradeDev{};
+    uint32_t *d_rr, *d_off;
+    DevBreakerRule* d_rules;
+    sf_breaker_state* d_st;
+    if (dalloc((void**)&d_rr, (size_t)e->R * 4) || dalloc((void**)&d_off, off.size() * 4) ||
+        dalloc((void**)&d_rules, (size_t)nv * sizeof(DevBreakerRule)) ||
+        dalloc((void**)&d_st, (size_t)nv * sizeof(sf_breaker_state)))
+        return SF_ERR_NOMEM;
+    HIP_TRY(hipMemcpy(d_rr, rr_of.data(), (size_t)e->R * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_off, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+    if (nv) {
+        HIP_TRY(hipMemcpy(d_rules, dr.data(), (size_t)nv * sizeof(DevBreakerRule), hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(d_st, st.data(), (size_t)nv * sizeof(sf_breaker_state), hipMemcpyHostToDevice));
+    }
+    e->dg.rr_of = d_rr; e->dg.off = d_off; e->dg.rules = d_rules; e->dg.state = d_st;
+    e->dg.n_rres = n_rres;
+    uint32_t kb = 1;
+    while ((1ull << kb) <= n_rres) kb++;                        // keys 0..n_rres (n_rres = no breaker)
+    e->dg.key_bits = kb;
+    e->dgw.sort_tmp_bytes = 0;                                  // re-sized for the new key width
+    if (e->dgw.sort_tmp) { hipFree(e->dgw.sort_tmp); e->dgw.sort_tmp = nullptr; }
+    if (n_loaded) *n_loaded = nv;
+    return SF_OK;
+}
+
+static int dg_ensure(sf_engine* e, uint32_t n) {
+    DegradeWork& w = e->dgw;
+    if (n > w.cap) {
+        void* ptrs[] = {w.keys_in, w.keys_out, w.idx_in, w.idx_out};
+        for (void* p : ptrs) if (p) hipFree(p);
+        w.keys_in = w.keys_out = w.idx_in = w.idx_out = nullptr;
+        if (dalloc((void**)&w.keys_in, (size_t)n * 4) || dalloc((void**)&w.keys_out, (size_t)n * 4) ||
+            dalloc((void**)&w.idx_in, (size_t)n * 4) || dalloc((void**)&w.idx_out, (size_t)n * 4))
+            return SF_ERR_NOMEM;
+        w.cap = n;
+        if (w.sort_tmp) { hipFree(w.sort_tmp); w.sort_tmp = nullptr; }
+        w.sort_tmp_bytes = 0;
+    }
+    if (!w.sort_tmp) {
+        size_t bytes = 0;
+        HIP_TRY(dg_sort_bytes(w.cap, e->dg.key_bits, &bytes));
+        if (dalloc(&w.sort_tmp, bytes)) return SF_ERR_NOMEM;
+        w.sort_tmp_bytes = bytes;
+    }
+    if (e->dg.n_rres > w.beg_cap || !w.beg) {
+        if (w.beg) hipFree(w.beg);
+        if (w.end) hipFree(w.end);
+        w.beg = w.end = nullptr;
+        const uint32_t c = std::max<uint32_t>(e->dg.n_rres, 1);
+        if (dalloc((void**)&w.beg, (size_t)c * 4) || dalloc((void**)&w.end, (size_t)c * 4)) return SF_ERR_NOMEM;
+        w.beg_cap = c;
+    }
+    if (!w.err && dalloc((void**)&w.err, 4)) return SF_ERR_NOMEM;
+    return SF_OK;
+}
+
+int sf_degrade_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
+    if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
+    if (in->n == 0) return SF_OK;
+    if (!in->res_id || !in->ts_ms || !in->flags) return fail(SF_ERR_INVALID, "missing event array");
+    if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
+    std::lock_guard<std::mutex> lk(e->mu);
+    int rc = drain(e);
+    if (rc) return rc;
+    const uint32_t n = in->n;
+    rc = dg_ensure(e, n);
+    if (rc) return rc;
+    hipStream_t s = e->stream;
+    DegradeBatch b{};
+    b.n = n; b.shard_count = e->cfg.shard_count; b.shard_index = e->cfg.shard_index; b.R = e->R;
+    uint8_t* status = out->status;
+    uint16_t* rule = out->rule_idx;
+    int32_t* wait = out->wait_ms;
+    const bool host_in = in->mem == SF_MEM_HOST, host_out = out->mem == SF_MEM_HOST;
+    if (host_in || host_out) {
+        size_t need = 0;
+        const size_t o_res = need; need += host_in ? align_up((size_t)n * 4) : 0;
+        const size_t o_ts = need; need += host_in ? align_up((size_t)n * 8) : 0;
+        const size_t o_fl = need; need += host_in ? align_up((size_t)n) : 0;
+        const size_t o_er = need; need += host_in && in->entry_ref ? align_up((size_t)n * 8) : 0;
+        const size_t o_ct = need; need += host_in && in->create_ts ? align_up((size_t)n * 8) : 0;
+        const size_t o_st = need; need += host_out ? align_up((size_t)n) : 0;
+        const size_t o_ru = need; need += host_out && rule ? align_up((size_t)n * 2) : 0;
+        const size_t o_wa = need; need += host_out && wait ? align_up((size_t)n * 4) : 0;
+        if (need > e->dg_stage_bytes) {
+            if (e->dg_stage) hipFree(e->dg_stage);
+            e->dg_stage = nullptr;
+            if (dalloc(&e->dg_stage, need)) return SF_ERR_NOMEM;
+            e->dg_stage_bytes = need;
+        }
+        char* base = (char*)e->dg_stage;
+        auto up = [&](size_t off, const void* src, size_t bytes) -> const void* {
+            if (!src) return nullptr;
+            hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, s);
+            return base + off;
+        };
+        if (host_in) {
+            b.res = (const uint32_t*)up(o_res, in->res_id, (size_t)n * 4);
+            b.ts = (const int64_t*)up(o_ts, in->ts_ms, (size_t)n * 8);
+            b.flags = (const uint8_t*)up(o_fl, in->flags, n);
+            b.eref = (const int64_t*)up(o_er, in->entry_ref, (size_t)n * 8);
+            b.cts = (const int64_t*)up(o_ct, in->create_ts, (size_t)n * 8);
+        }
+        if (host_out) {
+            status = (uint8_t*)(base + o_st);
+            rule = rule ? (uint16_t*)(base + o_ru) : nullptr;
+            wait = wait ? (int32_t*)(base + o_wa) : nullptr;
+        }
+    }
+    if (!host_in) {
+        b.res = in->res_id; b.ts = in->ts_ms; b.flags = in->flags; b.eref = in->entry_ref; b.cts = in->create_ts;
+    }
+    HIP_TRY(hipMemsetAsync(e->dgw.err, 0, 4, s));
+    HIP_TRY(dg_launch(e->dg, e->dgw, b, status, rule, wait, s));
+    int err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, e->dgw.err, 4, hipMemcpyDeviceToHost, s));
+    if (host_out) {
+        HIP_TRY(hipMemcpyAsync(out->status, status, n, hipMemcpyDeviceToHost, s));
+        if (rule) HIP_TRY(hipMemcpyAsync(out->rule_idx, rule, (size_t)n * 2, hipMemcpyDeviceToHost, s));
+        if (wait) HIP_TRY(hipMemcpyAsync(out->wait_ms, wait, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    if (err & 1) return fail(SF_ERR_INVALID, "event resource outside this shard");
+    if (err & 2) return fail(SF_ERR_INVALID, "EXIT without a valid entry_ref or create_ts");
+    return SF_OK;
+}
+
+int sf_read_breaker(sf_engine* e, uint32_t k, sf_breaker_state* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (k >= e->dg_pos.size()) return fail(SF_ERR_INVALID, "breaker index");
+    HIP_TRY(hipMemcpy(out, e->dg.state + e->dg_pos[k], sizeof *out, hipMemcpyDeviceToHost));
+    if (out->window_start == DG_WS_NONE) out->window_start = SF_WS_ABSENT;
     return SF_OK;
 }
 

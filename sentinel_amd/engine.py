@@ -76,6 +76,9 @@ def _declare(L):
     f("sf_read_node", I, P, U32, C.POINTER(abi.sf_node_state))
     f("sf_read_entry_node", I, P, C.POINTER(abi.sf_node_state))
     f("sf_read_rule_state", I, P, U32, C.POINTER(abi.sf_rule_state))
+    f("sf_load_degrade_rules", I, P, C.POINTER(abi.sf_degrade_rule), U32, C.POINTER(U32))
+    f("sf_degrade_submit", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
+    f("sf_read_breaker", I, P, U32, C.POINTER(abi.sf_breaker_state))
     f("sf_snapshot", I, P, C.c_int64, C.POINTER(abi.sf_metric_row), U32, C.POINTER(U32))
     f("sf_load_resource_names", I, P, C.c_char_p, C.POINTER(C.c_uint64), C.POINTER(C.c_int32), U32)
     f("sf_metric_log", I, P, C.c_int64, C.c_int64, I, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64),
@@ -298,6 +301,36 @@ class FlowEngine:
         n = C.c_uint64()
         _check(lib().sf_format_metric_rows(self.h, arr, len(rows), tz_offset_ms, buf, cap, C.byref(n)))
         return buf.raw[:n.value]
+
+    # ---- DegradeSlot circuit breakers (DegradeSlot.java:50-94) ----
+    def load_degrade_rules(self, rules) -> int:
+        """rules: dicts of sf_degrade_rule fields (abi.degrade_rule); returns breakers installed."""
+        arr = (abi.sf_degrade_rule * max(1, len(rules)))()
+        for i, r in enumerate(rules):
+            for k, v in r.items():
+                setattr(arr[i], k, v)
+        n = C.c_uint32(0)
+        _check(lib().sf_load_degrade_rules(self.h, arr, len(rules), C.byref(n)))
+        return n.value
+
+    def degrade_submit(self, batch: abi.HostBatch) -> abi.HostVerdicts:
+        out = abi.HostVerdicts(batch.n)
+        b = batch.c_struct()
+        v = out.c_struct()
+        _check(lib().sf_degrade_submit(self.h, C.byref(b), C.byref(v)))
+        return out
+
+    def degrade_submit_device(self, batch: DeviceBatch, out: DeviceVerdicts):
+        b = batch.c_struct()
+        v = out.c_struct()
+        _check(lib().sf_degrade_submit(self.h, C.byref(b), C.byref(v)))
+
+    def read_breaker(self, idx) -> dict:
+        s = abi.sf_breaker_state()
+        _check(lib().sf_read_breaker(self.h, idx, C.byref(s)))
+        ws = None if s.window_start == abi.SF_WS_ABSENT else s.window_start
+        return dict(state=s.state, next_retry_ms=s.next_retry_ms, window_start=ws, hit_count=s.hit_count,
+                    total_count=s.total_count)
 
     def read_rule_state(self, idx) -> abi.sf_rule_state:
         s = abi.sf_rule_state()

@@ -340,3 +340,56 @@ def wire_workload(n_req: int, n_streams: int = 500, seed: int = 11, edge: bool =
                 f = wire.flow_frame(9996, 1, 1)
                 streams[s] += f[: int(rng.integers(1, len(f)))]
     return ns, flow, param, items, [bytes(x) for x in streams]
+
+
+def degrade_rules(n_res: int, seed: int = 5, frac: float = 0.5, invalid: int = 3):
+    """DegradeRules over ``frac`` of the resources: 1-3 breakers each, mixed
+    grades, thresholds chosen so breakers open and recover within seconds;
+    plus ``invalid`` rules DegradeRuleManager.isValidRule rejects."""
+    rng = np.random.default_rng(seed)
+    rules = []
+    for r in np.nonzero(rng.random(n_res) < frac)[0]:
+        for _ in range(int(rng.integers(1, 4))):
+            g = int(rng.integers(0, 3))
+            kw = dict(min_request_amount=int(rng.integers(1, 6)),
+                      stat_interval_ms=int(rng.choice([200, 500, 1000])))
+            if g == abi.DEGRADE_GRADE_RT:
+                rules.append(abi.degrade_rule(int(r), g, float(rng.integers(5, 40)), int(rng.integers(1, 3)),
+                                              slow_ratio_threshold=float(rng.choice([0.3, 0.5, 1.0])), **kw))
+            elif g == abi.DEGRADE_GRADE_EXCEPTION_RATIO:
+                rules.append(abi.degrade_rule(int(r), g, float(rng.choice([0.1, 0.3, 0.5])),
+                                              int(rng.integers(1, 3)), **kw))
+            else:
+                rules.append(abi.degrade_rule(int(r), g, float(rng.integers(1, 6)), int(rng.integers(1, 3)), **kw))
+    for k in range(invalid):
+        bad = abi.degrade_rule(k % n_res, abi.DEGRADE_GRADE_RT, 10.0, 1)
+        bad.update([dict(count=-1.0), dict(time_window_s=0), dict(min_request_amount=0),
+                    dict(slow_ratio_threshold=1.5), dict(stat_interval_ms=0)][k % 5])
+        rules.insert(int(rng.integers(0, len(rules) + 1)), bad)
+    return rules
+
+
+def degrade_workload(n_res: int, n_entries: int, duration_ms: int = 6000, seed: int = 6, s: float = 1.1,
+                     rt_mean_ms: float = 20.0, err_p: float = 0.15):
+    """Entries on a Zipf(s) resource mix, each followed by its EXIT after an
+    Exp(rt_mean) response time (SF_EV_ERROR with probability err_p); exits past
+    the end of the trace are dropped.  Time ordered, exits after entries of
+    the same millisecond."""
+    rng = np.random.default_rng(seed)
+    res = scramble(zipf_bounded(rng, s, n_res, n_entries) - 1, n_res).astype(np.uint32)
+    ts = _per_ms_times(rng, n_entries, duration_ms)
+    rt = np.floor(rng.exponential(rt_mean_ms, size=n_entries)).astype(np.int64)
+    ex_ts = ts + rt
+    keep = np.nonzero(ex_ts <= T0 + duration_ms - 1)[0]
+    all_ts = np.concatenate([ts, ex_ts[keep]])
+    is_exit = np.concatenate([np.zeros(n_entries, bool), np.ones(keep.size, bool)])
+    order = np.argsort((all_ts - T0) * 2 + is_exit, kind="stable")
+    pos = np.empty(order.size, np.int64)
+    pos[order] = np.arange(order.size)
+    src = np.concatenate([np.arange(n_entries), keep])
+    flags = np.where(is_exit[order], abi.EV_EXIT, 0).astype(np.uint8)
+    err = np.concatenate([np.zeros(n_entries, bool), rng.random(keep.size) < err_p])[order]
+    flags[err] |= abi.EV_ERROR
+    eref = np.full(order.size, -1, np.int64)
+    eref[pos[n_entries:]] = pos[keep]
+    return abi.HostBatch(res[src][order], all_ts[order], np.ones(order.size, np.int32), flags, entry_ref=eref)

@@ -1,0 +1,252 @@
+"""DegradeSlot circuit breakers: the oracle pinned by the
+reference's own known-answer tests, then the HIP path (sf_degrade_submit)
+against the oracle, bit for bit (verdicts, blocking breaker index, every
+breaker's state and counters).
+
+Known-answer scenarios restated from
+sentinel-core/src/test/java/com/alibaba/csp/sentinel/slots/block/degrade/circuitbreaker/
+- ResponseTimeCircuitBreakerTest.testMaxSlowRatioThreshold (:32-57)
+- ExceptionCircuitBreakerTest.testRecordErrorOrSuccess (:47-83)
+driven by AbstractTimeBasedTest's mocked clock (test/AbstractTimeBasedTest.java:40-98):
+entryAndSleepFor = entry, sleep(ms), exit; entryWithErrorIfPresent = entry,
+Tracer error, sleep(5..10 ms; 7 here), exit; a blocked entry neither sleeps nor exits.
+"""
+import numpy as np
+import pytest
+
+from oracle import degrade as od
+from sentinel_amd import abi, trace
+
+RES = 0
+
+
+class Script:
+    """Replays a reference test script against the oracle one event at a time
+    (time advances only through sleeps of passed entries), recording the event
+    trace and each call's return value."""
+
+    def __init__(self, rules):
+        self.o = od.DegradeOracle()
+        self.o.load_rules(rules)
+        self.t = 0
+        self.res, self.ts, self.flags, self.eref = [], [], [], []
+        self.returns = []
+
+    def _event(self, flags, ref=-1, create=0):
+        st, _ = self.o.submit([RES], [self.t], [flags], [-1], [create])
+        self.res.append(RES)
+        self.ts.append(self.t)
+        self.flags.append(flags)
+        self.eref.append(ref)
+        return int(st[0])
+
+    def sleep(self, ms):
+        self.t += ms
+
+    def _call(self, ms, error):
+        t0, idx = self.t, len(self.ts)
+        if self._event(0) == od.V_BLOCK_DEGRADE:
+            self.returns.append(False)
+            return False
+        self.sleep(ms)
+        self._event(od.EV_EXIT | (od.EV_ERROR if error else 0), ref=idx, create=t0)
+        self.returns.append(True)
+        return True
+
+    def entry_and_sleep_for(self, ms):
+        return self._call(ms, False)
+
+    def entry_with_error(self, error=True):
+        return self._call(7, error)
+
+    def batch(self):
+        n = len(self.ts)
+        return abi.HostBatch(np.array(self.res), np.array(self.ts), np.ones(n, np.int32),
+                             np.array(self.flags), entry_ref=np.array(self.eref))
+
+
+def rt_script():
+    rule = abi.degrade_rule(RES, abi.DEGRADE_GRADE_RT, 10, 5, min_request_amount=3, slow_ratio_threshold=1,
+                            stat_interval_ms=5000)
+    s = Script([rule])
+    expect = []
+    for _ in range(3):
+        expect.append((s.entry_and_sleep_for(20), True))
+    expect.append((s.entry_and_sleep_for(20), False))   # 3/3 slow -> open
+    s.sleep(1000)
+    expect.append((s.entry_and_sleep_for(20), False))
+    s.sleep(4000)
+    expect.append((s.entry_and_sleep_for(20), True))    # retry timeout -> half-open probe
+    return [rule], s, expect
+
+
+def exception_script():
+    rule = abi.degrade_rule(RES, abi.DEGRADE_GRADE_EXCEPTION_RATIO, 0.2, 10, min_request_amount=1,
+                            stat_interval_ms=20_000)
+    retry = 10_000
+    s = Script([rule])
+    e = []
+    e.append((s.entry_and_sleep_for(10), True))
+    e.append((s.entry_with_error(), True))              # -> open
+    e.append((s.entry_with_error(), False))
+    e.append((s.entry_and_sleep_for(100), False))
+    s.sleep(retry // 2)
+    e.append((s.entry_and_sleep_for(100), False))
+    s.sleep(retry // 2)
+    e.append((s.entry_with_error(), True))              # -> half -> open
+    e.append((s.entry_and_sleep_for(100), False))
+    e.append((s.entry_and_sleep_for(100), False))
+    s.sleep(retry)
+    e.append((s.entry_and_sleep_for(100), True))        # -> half -> closed
+    for _ in range(6):
+        e.append((s.entry_and_sleep_for(100), True))
+    e.append((s.entry_with_error(), True))
+    e.append((s.entry_and_sleep_for(100), True))
+    return [rule], s, e
+
+
+SCRIPTS = {"rt_max_slow_ratio": rt_script, "exception_record_error_or_success": exception_script}
+
+
+# ---------------------------------------------------------------- oracle (CPU)
+@pytest.mark.parametrize("name", list(SCRIPTS))
+def test_oracle_reference_scripts(name):
+    _, _, expect = SCRIPTS[name]()
+    got = [g for g, _ in expect]
+    want = [w for _, w in expect]
+    assert got == want
+
+
+def test_oracle_state_machine_details():
+    # half-open probe blocked by a later breaker falls back to OPEN with the old retry time
+    # (AbstractCircuitBreaker.java:113-129), so the next entry probes again
+    r0 = abi.degrade_rule(RES, abi.DEGRADE_GRADE_EXCEPTION_COUNT, 0, 1, min_request_amount=1)
+    r1 = abi.degrade_rule(RES, abi.DEGRADE_GRADE_EXCEPTION_COUNT, 0, 3, min_request_amount=1)
+    o = od.DegradeOracle()
+    assert o.load_rules([r0, r1]) == 2
+    st, _ = o.submit([RES, RES], [0, 5], [0, od.EV_EXIT | od.EV_ERROR], [-1, 0], None)
+    assert list(st) == [od.V_PASS, od.V_EXIT]
+    assert o.state(0)["state"] == od.OPEN and o.state(0)["next_retry_ms"] == 1005
+    assert o.state(1)["state"] == od.OPEN and o.state(1)["next_retry_ms"] == 3005
+    st, ri = o.submit([RES, RES], [1005, 1006], [0, 0])
+    assert list(st) == [od.V_BLOCK_DEGRADE] * 2 and list(ri) == [1, 1]
+    assert o.state(0)["state"] == od.OPEN and o.state(0)["next_retry_ms"] == 1005
+    # both retry times reached: the probe passes both, a clean exit closes both and resets the bucket
+    st, _ = o.submit([RES, RES], [3005, 3010], [0, od.EV_EXIT], [-1, 0])
+    assert list(st) == [od.V_PASS, od.V_EXIT]
+    for k in (0, 1):
+        s = o.state(k)
+        assert s["state"] == od.CLOSED and s["hit_count"] == 0 and s["total_count"] == 0
+    # exit of a blocked entry records nothing (DegradeSlot.java:72-77)
+    o.load_rules([r0])
+    o.submit([RES, RES], [0, 1], [0, od.EV_EXIT | od.EV_ERROR], [-1, 0])
+    st, _ = o.submit([RES, RES], [2, 3], [0, od.EV_EXIT | od.EV_ERROR], [-1, 0])
+    assert list(st) == [od.V_BLOCK_DEGRADE, od.V_EXIT_IGNORED]
+    assert o.state(0)["total_count"] == 1
+
+
+def test_oracle_rule_validity():
+    # DegradeRuleManager.isValidRule (:183-204)
+    ok = abi.degrade_rule(1, abi.DEGRADE_GRADE_RT, 10, 1)
+    assert od.is_valid_rule(ok)
+    for bad in (dict(count=-1.0), dict(time_window_s=0), dict(min_request_amount=0), dict(stat_interval_ms=0),
+                dict(slow_ratio_threshold=1.01), dict(slow_ratio_threshold=-0.1), dict(grade=3)):
+        assert not od.is_valid_rule({**ok, **bad}), bad
+    assert not od.is_valid_rule(abi.degrade_rule(1, abi.DEGRADE_GRADE_EXCEPTION_RATIO, 1.5, 1))
+    assert od.is_valid_rule(abi.degrade_rule(1, abi.DEGRADE_GRADE_EXCEPTION_COUNT, 1.5, 1))
+    assert od.java_round(10.5) == 11 and od.java_round(-10.5) == -10 and od.java_round(2.4999) == 2
+
+
+def test_workload_generator_shape():
+    b = trace.degrade_workload(100, 2000, duration_ms=500, seed=1)
+    assert np.all(np.diff(b.ts_ms) >= 0)
+    ex = np.nonzero(b.flags & abi.EV_EXIT)[0]
+    assert np.all(b.entry_ref[ex] >= 0) and np.all(b.entry_ref[ex] < ex)
+    assert np.all(b.res_id[b.entry_ref[ex]] == b.res_id[ex])
+    assert np.all((b.flags[b.entry_ref[ex]] & abi.EV_EXIT) == 0)
+
+
+def oracle_run(rules, batches):
+    o = od.DegradeOracle()
+    n = o.load_rules(rules)
+    outs = [o.submit(b.res_id, b.ts_ms, b.flags, b.entry_ref, b.create_ts) for b in batches]
+    return outs, [o.state(k) for k in range(n)]
+
+
+# ---------------------------------------------------------------- HIP path (GPU)
+def _engine(R, max_batch):
+    from sentinel_amd import engine
+    return engine.FlowEngine(abi.default_config(max_resources=R, max_batch=max_batch))
+
+
+def check_gpu(rules, batches, R, tag):
+    e = _engine(R, max(b.n for b in batches))
+    try:
+        n = e.load_degrade_rules(rules)
+        outs, states = oracle_run(rules, batches)
+        assert n == len(states)
+        for bi, (b, (st, ri)) in enumerate(zip(batches, outs)):
+            v = e.degrade_submit(b)
+            bad = np.nonzero(v.status != st)[0]
+            assert bad.size == 0, f"{tag} batch {bi}: {bad.size} verdicts differ, first at {bad[:5]}"
+            blk = st == od.V_BLOCK_DEGRADE
+            assert np.array_equal(v.rule_idx[blk], ri[blk]), f"{tag} batch {bi}: breaker index"
+            assert np.all(v.wait_ms == 0)
+        for k, want in enumerate(states):
+            assert e.read_breaker(k) == want, f"{tag} breaker {k}"
+        return outs
+    finally:
+        e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(SCRIPTS))
+def test_gpu_reference_scripts(name):
+    rules, s, expect = SCRIPTS[name]()
+    outs = check_gpu(rules, [s.batch()], 4, name)
+    st = outs[0][0]
+    entries = st[(s.batch().flags & abi.EV_EXIT) == 0]
+    assert list(entries != od.V_BLOCK_DEGRADE) == [w for _, w in expect]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_gpu_mixed_breakers(seed):
+    R = 3000
+    rules = trace.degrade_rules(R, seed=seed)
+    full = trace.degrade_workload(R, 60_000, duration_ms=8000, seed=seed, err_p=0.2)
+    cut = [0, full.n // 3, full.n // 2, full.n]                # cross-batch exits via create_ts
+    batches = [full.subset(cut[i], cut[i + 1]) for i in range(3)]
+    outs = check_gpu(rules, batches, R, f"seed {seed}")
+    allst = np.concatenate([o[0] for o in outs])
+    assert (allst == od.V_BLOCK_DEGRADE).sum() > 100              # breakers did open
+    assert (allst == od.V_EXIT_IGNORED).sum() > 0
+
+
+@pytest.mark.gpu
+def test_gpu_no_rules_and_sharding():
+    from sentinel_amd import engine
+    b = trace.degrade_workload(64, 5000, duration_ms=1000, seed=9)
+    e = _engine(64, b.n)
+    try:
+        assert e.load_degrade_rules([]) == 0
+        v = e.degrade_submit(b)
+        want = np.where(b.flags & abi.EV_EXIT, od.V_EXIT, od.V_PASS)
+        assert np.array_equal(v.status, want)
+    finally:
+        e.close()
+    cfg = abi.default_config(max_resources=64, max_batch=b.n)
+    cfg.shard_count, cfg.shard_index = 2, 1
+    e = engine.FlowEngine(cfg)
+    try:
+        with pytest.raises(engine.EngineError):
+            e.degrade_submit(b)                                   # events of the other shard
+        sh = b.shard(2, 1)
+        rules = [r for r in trace.degrade_rules(64, seed=4, invalid=0) if r["resource"] % 2 == 1]
+        o = od.DegradeOracle()
+        o.load_rules(rules)
+        st, _ = o.submit(sh.res_id, sh.ts_ms, sh.flags, sh.entry_ref, sh.create_ts)
+        e.load_degrade_rules(rules)
+        assert np.array_equal(e.degrade_submit(sh).status, st)
+    finally:
+        e.close()
