@@ -446,4 +446,8 @@ def degrade_rule(resource, grade, count, time_window_s, min_request_amount=5, sl
                 stat_interval_ms=stat_interval_ms)
 
 
+DEGRADE_RULE_DTYPE = np.dtype([(n, {C.c_uint32: "<u4", C.c_int32: "<i4", C.c_double: "<f8"}[t])
+                               for n, t in sf_degrade_rule._fields_])
+assert DEGRADE_RULE_DTYPE.itemsize == C.sizeof(sf_degrade_rule)
+
 STRUCT_SIZES.update({"sf_degrade_rule": C.sizeof(sf_degrade_rule), "sf_breaker_state": C.sizeof(sf_breaker_state)})

@@ -43,6 +43,8 @@ struct DegradeWork {
     uint32_t beg_cap = 0;
     void* sort_tmp = nullptr; size_t sort_tmp_bytes = 0;
     int* err = nullptr;                        // events outside the shard / bad refs
+    uint32_t* heavy = nullptr;                 // [n_rres] long segments for the wave walk
+    uint32_t* n_heavy = nullptr;
 };
 
 hipError_t dg_sort_bytes(uint32_t n, uint32_t key_bits, size_t* bytes);

@@ -16,9 +16,11 @@
 #include <rocprim/rocprim.hpp>
 #include "sf_degrade.h"
 
-namespace {
+namespace sf_dg {
 
 constexpr int BLK = 256;
+constexpr uint32_t HEAVY = 512;     // segments longer than this are walked by a whole wave
+constexpr uint32_t MAXC = 4;        // breakers per resource held in registers by the wave walk
 
 __global__ void __launch_bounds__(BLK) k_dg_keys(DegradeDev d, DegradeBatch b, uint32_t* keys, uint32_t* idx,
                                                  uint8_t* status, uint16_t* rule, int32_t* wait, int* err) {
@@ -52,6 +54,8 @@ __global__ void __launch_bounds__(BLK) k_dg_bounds(const uint32_t* keys, uint32_
 
 __device__ __forceinline__ void dg_roll(sf_breaker_state& s, const DevBreakerRule& r, int64_t t) {
     // LeapArray(1, interval).currentWindow(t): create, keep, or reset the single bucket (LeapArray.java:128-225)
+    if (t >= 0 && s.window_start != DG_WS_NONE && t >= s.window_start && t - s.window_start < r.interval)
+        return;                                // same window: no 64-bit modulo on the serial chain
     const int64_t ws = t - t % r.interval;
     if (s.window_start == DG_WS_NONE || ws > s.window_start) {
         s.window_start = ws;
@@ -93,15 +97,154 @@ __device__ __forceinline__ void dg_complete(sf_breaker_state& s, const DevBreake
     }
 }
 
-// One lane walks one breaker resource's events in time order.
+
+__device__ __forceinline__ int64_t rl64(int64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// One wave per long breaker segment (<= MAXC breakers).  Chunks of 64 events:
+// every lane gathers one event (index, ts, flags, entry ref, create ts) and the
+// verdict of an entry decided in an earlier chunk, the next chunk's events are
+// fetched while this one is walked, and the walk itself runs wave-uniform on
+// readlane'd values with the breaker state in registers -- the per-event chain
+// has no memory access.  A reference to an entry of the current chunk is
+// resolved with a ballot over the chunk's indices (the sort is stable, so
+// indices grow with the sorted position).
+__global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, const uint32_t* perm,
+                                                const uint32_t* beg, const uint32_t* end, uint8_t* status,
+                                                uint16_t* rule, int* err, const uint32_t* heavy,
+                                                const uint32_t* n_heavy) {
+    const int lane = threadIdx.x;
+    const uint32_t nh = *n_heavy;
+    for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
+        const uint32_t k = heavy[h];
+        const uint32_t j0 = beg[k], j1 = end[k];
+        const uint32_t c0 = d.off[k];
+        const uint32_t nc = d.off[k + 1] - c0;
+        sf_breaker_state S[MAXC];
+        DevBreakerRule R[MAXC];
+#pragma unroll
+        for (uint32_t c = 0; c < MAXC; c++) {
+            if (c < nc) { S[c] = d.state[c0 + c]; R[c] = d.rules[c0 + c]; }
+        }
+        // gather of chunk [j, j+64): the lane's event, and the verdict of its
+        // entry when that entry is older than `bound` (already stored and fenced)
+        auto fetch = [&](uint32_t j, uint32_t bound, uint32_t& idx, int64_t& t, uint32_t& fl, int64_t& ref,
+                         int64_t& cr, bool& bad, bool& old_blk) {
+            const uint32_t p = j + lane;
+            idx = 0xFFFFFFFFu; t = 0; fl = 0; ref = -1; cr = 0; bad = false; old_blk = false;
+            if (p < j1) {
+                idx = perm[p];
+                t = b.ts[idx];
+                fl = b.flags[idx];
+                if (fl & SF_EV_EXIT) {
+                    ref = b.eref ? b.eref[idx] : -1;
+                    if (ref >= 0) {
+                        if ((uint64_t)ref < b.n) {
+                            cr = b.ts[ref];
+                            if ((uint64_t)ref < bound) old_blk = status[ref] == SF_V_BLOCK_DEGRADE;
+                        } else {
+                            bad = true;
+                        }
+                    } else if (b.cts) {
+                        cr = b.cts[idx];
+                    } else {
+                        bad = true;
+                    }
+                }
+            }
+        };
+        uint32_t idx, fl, nidx = 0, nfl = 0;
+        int64_t t, ref, cr, nt = 0, nref = 0, ncr = 0;
+        bool bad, old_blk, nbad = false, nold = false;
+        const uint32_t first0 = perm[j0];
+        fetch(j0, first0, idx, t, fl, ref, cr, bad, old_blk);
+        uint32_t pidx = 0xFFFFFFFFu, pfirst = first0;   // previous chunk: lane indices, lowest index
+        uint64_t pblk = 0;                              // previous chunk: blocked entries
+        for (uint32_t j = j0; j < j1; j += 64) {
+            const uint32_t cnt = min(64u, j1 - j);
+            const uint32_t first = __builtin_amdgcn_readfirstlane(idx);   // lowest index of the chunk
+            if (bad) atomicOr(err, 2);
+            const uint64_t badm = __ballot(bad), oldm = __ballot(old_blk);
+            // next chunk in flight; its older-entry verdicts are those stored before this chunk
+            if (j + 64 < j1) fetch(j + 64, first, nidx, nt, nfl, nref, ncr, nbad, nold);
+            uint64_t blkm = 0;
+            uint8_t my_st = (fl & SF_EV_EXIT) ? SF_V_EXIT : SF_V_PASS;
+            uint16_t my_rule = 0;
+            for (uint32_t q = 0; q < cnt; q++) {
+                const int64_t tq = rl64(t, q);
+                const uint32_t fq = (uint32_t)__builtin_amdgcn_readlane((int)fl, q);
+                if (!(fq & SF_EV_EXIT)) {
+                    uint32_t moved = 0;
+                    int blocked = -1;
+#pragma unroll
+                    for (uint32_t c = 0; c < MAXC; c++) {
+                        if (c < nc && blocked < 0 && S[c].state != SF_CB_CLOSED) {
+                            if (S[c].state == SF_CB_OPEN && tq >= S[c].next_retry_ms) {
+                                S[c].state = SF_CB_HALF_OPEN;
+                                moved |= 1u << c;
+                            } else {
+                                blocked = (int)c;
+                            }
+                        }
+                    }
+                    if (blocked >= 0) {
+#pragma unroll
+                        for (uint32_t c = 0; c < MAXC; c++)
+                            if (((moved >> c) & 1u) && S[c].state == SF_CB_HALF_OPEN) S[c].state = SF_CB_OPEN;
+                        blkm |= 1ull << q;
+                        if ((uint32_t)lane == q) { my_st = SF_V_BLOCK_DEGRADE; my_rule = (uint16_t)blocked; }
+                    }
+                    continue;
+                }
+                if ((badm >> q) & 1ull) continue;
+                const int64_t rq = rl64(ref, q);
+                bool ign;
+                if (rq < 0) ign = false;
+                else if ((uint64_t)rq >= first) ign = (__ballot(idx == (uint32_t)rq) & blkm) != 0ull;
+                else if ((uint64_t)rq >= pfirst) ign = (__ballot(pidx == (uint32_t)rq) & pblk) != 0ull;
+                else ign = (oldm >> q) & 1ull;
+                if (ign) {
+                    if ((uint32_t)lane == q) my_st = SF_V_EXIT_IGNORED;
+                    continue;
+                }
+                const int64_t rt = tq - rl64(cr, q);
+                const bool error = (fq & SF_EV_ERROR) != 0;
+#pragma unroll
+                for (uint32_t c = 0; c < MAXC; c++)
+                    if (c < nc) dg_complete(S[c], R[c], tq, rt, error);
+            }
+            if ((uint32_t)lane < cnt) {
+                status[idx] = my_st;
+                if (rule) rule[idx] = my_rule;
+            }
+            __threadfence();                     // verdicts visible to the loads issued from the next chunk on
+            pidx = idx; pfirst = first; pblk = blkm;
+            idx = nidx; t = nt; fl = nfl; ref = nref; cr = ncr; bad = nbad; old_blk = nold;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (uint32_t c = 0; c < MAXC; c++)
+                if (c < nc) d.state[c0 + c] = S[c];
+        }
+    }
+}
+
+// One lane walks one breaker resource's events in time order (short segments).
 __global__ void __launch_bounds__(BLK) k_dg_walk(DegradeDev d, DegradeBatch b, const uint32_t* perm,
                                                  const uint32_t* beg, const uint32_t* end, uint8_t* status,
-                                                 uint16_t* rule, int* err) {
+                                                 uint16_t* rule, int* err, uint32_t* heavy, uint32_t* n_heavy) {
     const uint32_t k = blockIdx.x * BLK + threadIdx.x;
     if (k >= d.n_rres) return;
     const uint32_t j0 = beg[k], j1 = end[k];
     if (j0 >= j1) return;
     const uint32_t c0 = d.off[k], c1 = d.off[k + 1];
+    if (j1 - j0 > HEAVY && c1 - c0 <= MAXC) {               // k_dg_wave's segment
+        heavy[atomicAdd(n_heavy, 1u)] = k;
+        return;
+    }
     const DevBreakerRule* R = d.rules;
     sf_breaker_state* S = d.state;
     for (uint32_t j = j0; j < j1; j++) {
@@ -158,7 +301,9 @@ __global__ void __launch_bounds__(BLK) k_dg_walk(DegradeDev d, DegradeBatch b, c
 
 inline uint32_t blocks(uint32_t n) { return (n + BLK - 1) / BLK; }
 
-}  // namespace
+}  // namespace sf_dg
+
+using namespace sf_dg;
 
 hipError_t dg_sort_bytes(uint32_t n, uint32_t key_bits, size_t* bytes) {
     return rocprim::radix_sort_pairs(nullptr, *bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
@@ -178,7 +323,12 @@ hipError_t dg_launch(const DegradeDev& d, DegradeWork& w, const DegradeBatch& b,
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(w.beg, 0, (size_t)d.n_rres * 4, s);
     if (e != hipSuccess) return e;
+    e = hipMemsetAsync(w.n_heavy, 0, 4, s);
+    if (e != hipSuccess) return e;
     k_dg_bounds<<<blocks(b.n), BLK, 0, s>>>(w.keys_out, b.n, d.n_rres, w.beg, w.end);
-    k_dg_walk<<<blocks(d.n_rres), BLK, 0, s>>>(d, b, w.idx_out, w.beg, w.end, status, rule, w.err);
+    k_dg_walk<<<blocks(d.n_rres), BLK, 0, s>>>(d, b, w.idx_out, w.beg, w.end, status, rule, w.err, w.heavy,
+                                               w.n_heavy);
+    const uint32_t waves = min(d.n_rres, 2048u);
+    k_dg_wave<<<waves, 64, 0, s>>>(d, b, w.idx_out, w.beg, w.end, status, rule, w.err, w.heavy, w.n_heavy);
     return hipGetLastError();
 }

@@ -165,7 +165,7 @@ void sf_destroy(sf_engine* e) {
     if (e->agg) hipFree(e->agg);
     void* dptrs[] = {(void*)e->dg.rr_of, (void*)e->dg.off, (void*)e->dg.rules, e->dg.state, e->dgw.keys_in,
                      e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
-                     e->dgw.err, e->dg_stage};
+                     e->dgw.err, e->dg_stage, e->dgw.heavy, e->dgw.n_heavy};
     for (void* p : dptrs) if (p) hipFree(p);
     if (e->comm) ncclCommDestroy(e->comm);
     free_tok_work(e->tw);
@@ -1517,12 +1517,16 @@ static int dg_ensure(sf_engine* e, uint32_t n) {
     if (e->dg.n_rres > w.beg_cap || !w.beg) {
         if (w.beg) hipFree(w.beg);
         if (w.end) hipFree(w.end);
-        w.beg = w.end = nullptr;
+        if (w.heavy) hipFree(w.heavy);
+        w.beg = w.end = w.heavy = nullptr;
         const uint32_t c = std::max<uint32_t>(e->dg.n_rres, 1);
-        if (dalloc((void**)&w.beg, (size_t)c * 4) || dalloc((void**)&w.end, (size_t)c * 4)) return SF_ERR_NOMEM;
+        if (dalloc((void**)&w.beg, (size_t)c * 4) || dalloc((void**)&w.end, (size_t)c * 4) ||
+            dalloc((void**)&w.heavy, (size_t)c * 4))
+            return SF_ERR_NOMEM;
         w.beg_cap = c;
     }
     if (!w.err && dalloc((void**)&w.err, 4)) return SF_ERR_NOMEM;
+    if (!w.n_heavy && dalloc((void**)&w.n_heavy, 4)) return SF_ERR_NOMEM;
     return SF_OK;
 }
 

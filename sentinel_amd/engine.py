@@ -304,11 +304,17 @@ class FlowEngine:
 
     # ---- DegradeSlot circuit breakers (DegradeSlot.java:50-94) ----
     def load_degrade_rules(self, rules) -> int:
-        """rules: dicts of sf_degrade_rule fields (abi.degrade_rule); returns breakers installed."""
-        arr = (abi.sf_degrade_rule * max(1, len(rules)))()
-        for i, r in enumerate(rules):
-            for k, v in r.items():
-                setattr(arr[i], k, v)
+        """rules: dicts of sf_degrade_rule fields (abi.degrade_rule), or a numpy
+        array of abi.DEGRADE_RULE_DTYPE; returns breakers installed."""
+        if isinstance(rules, np.ndarray):
+            assert rules.dtype == abi.DEGRADE_RULE_DTYPE
+            rules = np.ascontiguousarray(rules)
+            arr = C.cast(rules.ctypes.data, C.POINTER(abi.sf_degrade_rule))
+        else:
+            arr = (abi.sf_degrade_rule * max(1, len(rules)))()
+            for i, r in enumerate(rules):
+                for k, v in r.items():
+                    setattr(arr[i], k, v)
         n = C.c_uint32(0)
         _check(lib().sf_load_degrade_rules(self.h, arr, len(rules), C.byref(n)))
         return n.value

@@ -393,3 +393,20 @@ def degrade_workload(n_res: int, n_entries: int, duration_ms: int = 6000, seed: 
     eref = np.full(order.size, -1, np.int64)
     eref[pos[n_entries:]] = pos[keep]
     return abi.HostBatch(res[src][order], all_ts[order], np.ones(order.size, np.int32), flags, entry_ref=eref)
+
+
+def degrade_rules_array(n_res: int, seed: int = 5, frac: float = 0.5):
+    """Vectorised degrade_rules for bench sizes: one breaker on ``frac`` of the
+    resources (grades mixed 1:1:1), as a numpy array of abi.DEGRADE_RULE_DTYPE."""
+    rng = np.random.default_rng(seed)
+    res = np.nonzero(rng.random(n_res) < frac)[0].astype(np.uint32)
+    a = np.zeros(res.size, abi.DEGRADE_RULE_DTYPE)
+    g = rng.integers(0, 3, size=res.size).astype(np.int32)
+    a["resource"], a["grade"] = res, g
+    a["count"] = np.where(g == abi.DEGRADE_GRADE_RT, rng.integers(5, 40, size=res.size),
+                          np.where(g == abi.DEGRADE_GRADE_EXCEPTION_RATIO, 0.3, rng.integers(1, 6, size=res.size)))
+    a["time_window_s"] = rng.integers(1, 3, size=res.size)
+    a["min_request_amount"] = rng.integers(1, 6, size=res.size)
+    a["slow_ratio_threshold"] = rng.choice([0.3, 0.5, 1.0], size=res.size)
+    a["stat_interval_ms"] = rng.choice([200, 500, 1000], size=res.size)
+    return a

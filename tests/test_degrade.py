@@ -250,3 +250,21 @@ def test_gpu_no_rules_and_sharding():
         assert np.array_equal(e.degrade_submit(sh).status, st)
     finally:
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [4, 5])
+def test_gpu_long_segments(seed):
+    """Few resources, thousands of events each: the wave walk (segments > 512
+    events, <= 4 breakers), its chunk boundaries and tail chunks; resource 0
+    carries 5 breakers and stays on the lane walk."""
+    R = 16
+    rules = trace.degrade_rules(R, seed=seed, frac=1.0, invalid=2)
+    extra = [abi.degrade_rule(0, g, c, 1, min_request_amount=2, stat_interval_ms=500)
+             for g, c in [(0, 15.0), (1, 0.4), (2, 3.0), (0, 25.0), (1, 0.2)]]
+    rules = extra + [r for r in rules if r["resource"] != 0]
+    full = trace.degrade_workload(R, 40_000, duration_ms=6000, seed=seed, err_p=0.2, s=0.8)
+    cut = [0, 20_001, full.n]
+    outs = check_gpu(rules, [full.subset(cut[i], cut[i + 1]) for i in range(2)], R, f"long {seed}")
+    allst = np.concatenate([o[0] for o in outs])
+    assert (allst == od.V_BLOCK_DEGRADE).sum() > 100 and (allst == od.V_EXIT_IGNORED).sum() > 0
