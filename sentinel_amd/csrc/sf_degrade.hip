@@ -104,6 +104,24 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int l) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// value of the lane below (lane 0: its own)
+__device__ __forceinline__ int64_t rl64_up(int64_t v) {
+    const int lane = threadIdx.x;
+    const int src = lane == 0 ? 0 : lane - 1;
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)v >> 32), src);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// position of index x in an ascending LDS array of 64 indices (x is present)
+__device__ __forceinline__ uint32_t lds_find(const uint32_t* a, uint32_t x) {
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1)
+        if (a[lo + step - 1] < x) lo += step;
+    return lo;
+}
+
 // One wave per long breaker segment (<= MAXC breakers).  Chunks of 64 events:
 // every lane gathers one event (index, ts, flags, entry ref, create ts) and the
 // verdict of an entry decided in an earlier chunk, the next chunk's events are
@@ -111,13 +129,19 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int l) {
 // readlane'd values with the breaker state in registers -- the per-event chain
 // has no memory access.  A reference to an entry of the current chunk is
 // resolved with a ballot over the chunk's indices (the sort is stable, so
-// indices grow with the sorted position).
+// indices grow with the sorted position).  Before the serial walk, a bulk
+// prefix decides lane-parallel every event up to the first one that can change
+// a breaker's state: entries refused by an OPEN (retry not reached) or
+// HALF_OPEN breaker or passed by CLOSED ones, and exits that only count
+// (window rolls by a segmented ballot count; a CLOSED breaker's trip point is
+// found from each lane's running counts).
 __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, const uint32_t* perm,
                                                 const uint32_t* beg, const uint32_t* end, uint8_t* status,
                                                 uint16_t* rule, int* err, const uint32_t* heavy,
                                                 const uint32_t* n_heavy) {
     const int lane = threadIdx.x;
     const uint32_t nh = *n_heavy;
+    __shared__ uint32_t sidx[128];               // [0,64) previous chunk's indices, [64,128) this chunk's
     for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
         const uint32_t k = heavy[h];
         const uint32_t j0 = beg[k], j1 = end[k];
@@ -170,10 +194,99 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
             const uint64_t badm = __ballot(bad), oldm = __ballot(old_blk);
             // next chunk in flight; its older-entry verdicts are those stored before this chunk
             if (j + 64 < j1) fetch(j + 64, first, nidx, nt, nfl, nref, ncr, nbad, nold);
-            uint64_t blkm = 0;
             uint8_t my_st = (fl & SF_EV_EXIT) ? SF_V_EXIT : SF_V_PASS;
             uint16_t my_rule = 0;
-            for (uint32_t q = 0; q < cnt; q++) {
+            // ---- bulk prefix: the events before the first state change, decided lane-parallel
+            sidx[64 + lane] = idx;
+            __syncthreads();
+            const bool valid = (uint32_t)lane < cnt;
+            const bool is_en = valid && !(fl & SF_EV_EXIT);
+            const bool is_ex = valid && (fl & SF_EV_EXIT) && !bad;
+            // an entry changes nothing while the first non-CLOSED breaker refuses it without a retry
+            int bstar = -1;
+            bool any_half = false;
+#pragma unroll
+            for (uint32_t c = 0; c < MAXC; c++) {
+                if (c < nc) {
+                    any_half |= S[c].state == SF_CB_HALF_OPEN;
+                    if (bstar < 0 && S[c].state != SF_CB_CLOSED) bstar = (int)c;
+                }
+            }
+            bool inv_blk = false, inv = true;
+            if (bstar >= 0) {
+                int64_t retry = 0;
+                int st = 0;
+#pragma unroll
+                for (uint32_t c = 0; c < MAXC; c++)
+                    if ((int)c == bstar) { retry = S[c].next_retry_ms; st = S[c].state; }
+                inv = st == SF_CB_HALF_OPEN || t < retry;
+                inv_blk = inv;
+            }
+            const uint64_t N = __ballot(is_en && !inv), BI = __ballot(is_en && inv_blk);
+            bool ign = false;
+            if (is_ex && ref >= 0) {
+                if ((uint64_t)ref >= first) ign = (BI >> lds_find(sidx + 64, (uint32_t)ref)) & 1ull;
+                else if ((uint64_t)ref >= pfirst) ign = (pblk >> lds_find(sidx, (uint32_t)ref)) & 1ull;
+                else ign = old_blk;
+            }
+            const uint64_t E = __ballot(is_ex && !ign);
+            const uint64_t le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1);
+            uint64_t T = any_half ? E : 0ull;
+            int64_t wsv[MAXC];
+            uint64_t Hm[MAXC];
+#pragma unroll
+            for (uint32_t c = 0; c < MAXC; c++) {
+                wsv[c] = 0; Hm[c] = 0;
+                if (c < nc) {
+                    const int64_t L = R[c].interval;
+                    const int64_t ws = t - t % L;
+                    wsv[c] = ws;
+                    const bool h = R[c].grade == SF_DEGRADE_GRADE_RT ? (t - cr) > R[c].max_rt : (fl & SF_EV_ERROR) != 0;
+                    Hm[c] = __ballot(is_ex && !ign && h);
+                    if (S[c].state == SF_CB_CLOSED) {
+                        const int64_t pws = rl64_up(ws);
+                        const uint64_t B = __ballot(valid && (lane == 0 || ws != pws));
+                        const uint64_t bl = B & le;
+                        const int start = bl ? 63 - __builtin_clzll(bl) : 0;
+                        const uint64_t run = le & ~((1ull << start) - 1);
+                        const bool same = ws == S[c].window_start;
+                        const int64_t tot = __builtin_popcountll(E & run) + (same ? S[c].total_count : 0);
+                        const int64_t hh = __builtin_popcountll(Hm[c] & run) + (same ? S[c].hit_count : 0);
+                        bool cond = false;
+                        if (((E >> lane) & 1ull) && tot >= R[c].min_req) {
+                            const double cur = R[c].grade == SF_DEGRADE_GRADE_EXCEPTION_COUNT
+                                                   ? (double)hh : (double)hh * 1.0 / (double)tot;
+                            cond = cur > R[c].thr ||
+                                   (R[c].grade == SF_DEGRADE_GRADE_RT && cur == R[c].thr && R[c].thr == 1.0);
+                        }
+                        T |= __ballot(cond);
+                    }
+                }
+            }
+            const uint64_t stop = (T | N) & (cnt == 64 ? ~0ull : ((1ull << cnt) - 1));
+            const uint32_t cut = stop ? (uint32_t)__builtin_ctzll(stop) : cnt;
+            const uint64_t below = cut >= 64 ? ~0ull : ((1ull << cut) - 1);
+#pragma unroll
+            for (uint32_t c = 0; c < MAXC; c++) {
+                const uint64_t eb = E & below;
+                if (c < nc && eb) {
+                    const int m = 63 - __builtin_clzll(eb);
+                    const int64_t W = rl64(wsv[c], m);
+                    const uint64_t inW = __ballot(wsv[c] == W) & eb;
+                    const int64_t nW = __builtin_popcountll(inW), hW = __builtin_popcountll(inW & Hm[c]);
+                    if (S[c].window_start == DG_WS_NONE || W > S[c].window_start) {
+                        S[c].window_start = W; S[c].total_count = nW; S[c].hit_count = hW;
+                    } else {
+                        S[c].total_count += nW; S[c].hit_count += hW;
+                    }
+                }
+            }
+            if ((uint32_t)lane < cut) {
+                if (is_en && inv_blk) { my_st = SF_V_BLOCK_DEGRADE; my_rule = (uint16_t)bstar; }
+                else if (is_ex && ign) my_st = SF_V_EXIT_IGNORED;
+            }
+            uint64_t blkm = BI & below;
+            for (uint32_t q = cut; q < cnt; q++) {
                 const int64_t tq = rl64(t, q);
                 const uint32_t fq = (uint32_t)__builtin_amdgcn_readlane((int)fl, q);
                 if (!(fq & SF_EV_EXIT)) {
@@ -222,6 +335,8 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
             }
             __threadfence();                     // verdicts visible to the loads issued from the next chunk on
             pidx = idx; pfirst = first; pblk = blkm;
+            __syncthreads();
+            sidx[lane] = idx;                    // previous chunk's indices for the next bulk prefix
             idx = nidx; t = nt; fl = nfl; ref = nref; cr = ncr; bad = nbad; old_blk = nold;
         }
         if (lane == 0) {

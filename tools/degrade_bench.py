@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-sample", type=int, default=200_000)
+    ap.add_argument("--check", action="store_true", help="compare every verdict with the oracle (slow)")
     a = ap.parse_args()
     R = a.resources
     rules = trace.degrade_rules_array(R, seed=5)
@@ -39,9 +40,9 @@ def main():
     dv = engine.DeviceVerdicts(e, b.n, with_wait=False, with_rule=True)
     for _ in range(a.warmup):
         e.degrade_submit_device(db, dv)
-    e.load_degrade_rules(rules)                      # fresh breaker state for the timed steps
     wall = []
     for _ in range(a.steps):
+        e.load_degrade_rules(rules)                  # every step replays the same trace from fresh breakers
         t = time.perf_counter()
         e.degrade_submit_device(db, dv)
         wall.append(time.perf_counter() - t)
@@ -54,6 +55,16 @@ def main():
            "alg_bytes_per_event": 24}
     if st is not None:
         out["blocked"] = int((st == abi.V_BLOCK_DEGRADE).sum())
+    if a.check:
+        from oracle import degrade as od
+        o = od.DegradeOracle()
+        o.load_rules([{k: (v.item() if hasattr(v, "item") else v) for k, v in zip(rules.dtype.names, r)}
+                      for r in rules])
+        want, want_rule = o.submit(b.res_id, b.ts_ms, b.flags, b.entry_ref, b.create_ts)
+        ri = dv.rule_idx.numpy()
+        blk = want == abi.V_BLOCK_DEGRADE
+        out["parity"] = {"events": int(b.n), "status_mismatches": int((st != want).sum()),
+                         "rule_idx_mismatches": int((ri[blk] != want_rule[blk]).sum())}
     if a.cpu_sample:
         from oracle import degrade as od
         o = od.DegradeOracle()

@@ -1,9 +1,9 @@
 # DegradeSlot bench + rocprofv3 kernel trace (run on the GPU box from the repo root).
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/degrade; mkdir -p $OUT
-timeout -k 10 200 python3 tools/degrade_bench.py ${DG_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAILED; tail $OUT/bench.err; exit 1; }
+timeout -k 10 300 python3 tools/degrade_bench.py ${DG_ARGS:-} --check > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAILED; tail $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-timeout -k 10 200 python3 tools/degrade_bench.py ${DG_ARGS:-} --zipf 0.6 --cpu-sample 0 > $OUT/bench_mild.json 2> $OUT/bench_mild.err || { echo BENCH2_FAILED; tail $OUT/bench_mild.err; exit 1; }
+timeout -k 10 200 python3 tools/degrade_bench.py ${DG_ARGS:-} --zipf 0.6 --cpu-sample 0 --check > $OUT/bench_mild.json 2> $OUT/bench_mild.err || { echo BENCH2_FAILED; tail $OUT/bench_mild.err; exit 1; }
 cat $OUT/bench_mild.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format rocpd -d $OUT/kt -o kt -- python3 tools/degrade_bench.py \
     ${DG_ARGS:-} --steps 3 --warmup 1 --cpu-sample 0 > $OUT/kt_bench.json 2> $OUT/kt.err || { echo KT_FAILED; tail $OUT/kt.err; exit 1; }
