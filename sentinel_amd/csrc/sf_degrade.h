@@ -36,6 +36,11 @@ struct DegradeBatch {
     uint32_t shard_count, shard_index, R;
 };
 
+struct alignas(16) DgEv {                      // sorted event of a breaker resource, 32 B
+    int64_t t, cr, ref;                        // ts, entry create ts (exits), entry_ref
+    uint32_t idx, fl;                          // submission index, flags | bad << 8
+};
+
 struct DegradeWork {
     uint32_t cap = 0;
     uint32_t *keys_in = nullptr, *keys_out = nullptr, *idx_in = nullptr, *idx_out = nullptr;
@@ -45,6 +50,7 @@ struct DegradeWork {
     int* err = nullptr;                        // events outside the shard / bad refs
     uint32_t* heavy = nullptr;                 // [n_rres] long segments for the wave walk
     uint32_t* n_heavy = nullptr;
+    DgEv* sev = nullptr;                       // [cap]
 };
 
 hipError_t dg_sort_bytes(uint32_t n, uint32_t key_bits, size_t* bytes);

@@ -104,6 +104,36 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int l) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// Sorted event payload of every breaker-resource event (keys < none come
+// first after the sort): the wave walk then reads one coalesced 32-B record per
+// lane instead of a chain of dependent gathers.
+__global__ void __launch_bounds__(BLK) k_dg_gather(DegradeBatch b, const uint32_t* keys, const uint32_t* perm,
+                                                   uint32_t none, DgEv* sev) {
+    const uint32_t j = blockIdx.x * BLK + threadIdx.x;
+    if (j >= b.n || keys[j] >= none) return;
+    const uint32_t idx = perm[j];
+    DgEv ev;
+    ev.idx = idx;
+    ev.t = b.ts[idx];
+    uint32_t fl = b.flags[idx], bad = 0;
+    ev.ref = -1;
+    ev.cr = 0;
+    if (fl & SF_EV_EXIT) {
+        const int64_t ref = b.eref ? b.eref[idx] : -1;
+        ev.ref = ref;
+        if (ref >= 0) {
+            if ((uint64_t)ref < b.n) ev.cr = b.ts[ref];
+            else bad = 1;
+        } else if (b.cts) {
+            ev.cr = b.cts[idx];
+        } else {
+            bad = 1;
+        }
+    }
+    ev.fl = fl | (bad << 8);
+    sev[j] = ev;
+}
+
 // value of the lane below (lane 0: its own)
 __device__ __forceinline__ int64_t rl64_up(int64_t v) {
     const int lane = threadIdx.x;
@@ -135,7 +165,7 @@ __device__ __forceinline__ uint32_t lds_find(const uint32_t* a, uint32_t x) {
 // HALF_OPEN breaker or passed by CLOSED ones, and exits that only count
 // (window rolls by a segmented ballot count; a CLOSED breaker's trip point is
 // found from each lane's running counts).
-__global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, const uint32_t* perm,
+__global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, const DgEv* __restrict__ sev,
                                                 const uint32_t* beg, const uint32_t* end, uint8_t* status,
                                                 uint16_t* rule, int* err, const uint32_t* heavy,
                                                 const uint32_t* n_heavy) {
@@ -160,30 +190,17 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
             const uint32_t p = j + lane;
             idx = 0xFFFFFFFFu; t = 0; fl = 0; ref = -1; cr = 0; bad = false; old_blk = false;
             if (p < j1) {
-                idx = perm[p];
-                t = b.ts[idx];
-                fl = b.flags[idx];
-                if (fl & SF_EV_EXIT) {
-                    ref = b.eref ? b.eref[idx] : -1;
-                    if (ref >= 0) {
-                        if ((uint64_t)ref < b.n) {
-                            cr = b.ts[ref];
-                            if ((uint64_t)ref < bound) old_blk = status[ref] == SF_V_BLOCK_DEGRADE;
-                        } else {
-                            bad = true;
-                        }
-                    } else if (b.cts) {
-                        cr = b.cts[idx];
-                    } else {
-                        bad = true;
-                    }
-                }
+                const DgEv ev = sev[p];          // sorted payload (k_dg_gather): one coalesced 32-B load
+                idx = ev.idx; t = ev.t; fl = ev.fl & 0xFFu; ref = ev.ref; cr = ev.cr;
+                bad = (ev.fl >> 8) != 0u;
+                if ((fl & SF_EV_EXIT) && !bad && ref >= 0 && (uint64_t)ref < bound)
+                    old_blk = status[ref] == SF_V_BLOCK_DEGRADE;
             }
         };
         uint32_t idx, fl, nidx = 0, nfl = 0;
         int64_t t, ref, cr, nt = 0, nref = 0, ncr = 0;
         bool bad, old_blk, nbad = false, nold = false;
-        const uint32_t first0 = perm[j0];
+        const uint32_t first0 = sev[j0].idx;
         fetch(j0, first0, idx, t, fl, ref, cr, bad, old_blk);
         uint32_t pidx = 0xFFFFFFFFu, pfirst = first0;   // previous chunk: lane indices, lowest index
         uint64_t pblk = 0;                              // previous chunk: blocked entries
@@ -444,6 +461,7 @@ hipError_t dg_launch(const DegradeDev& d, DegradeWork& w, const DegradeBatch& b,
     k_dg_walk<<<blocks(d.n_rres), BLK, 0, s>>>(d, b, w.idx_out, w.beg, w.end, status, rule, w.err, w.heavy,
                                                w.n_heavy);
     const uint32_t waves = min(d.n_rres, 2048u);
-    k_dg_wave<<<waves, 64, 0, s>>>(d, b, w.idx_out, w.beg, w.end, status, rule, w.err, w.heavy, w.n_heavy);
+    k_dg_gather<<<blocks(b.n), BLK, 0, s>>>(b, w.keys_out, w.idx_out, d.n_rres, w.sev);
+    k_dg_wave<<<waves, 64, 0, s>>>(d, b, w.sev, w.beg, w.end, status, rule, w.err, w.heavy, w.n_heavy);
     return hipGetLastError();
 }
