@@ -255,8 +255,9 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
             for (uint32_t c = 0; c < MAXC; c++) {
                 wsv[c] = 0; Hm[c] = 0;
                 if (c < nc) {
-                    const int64_t L = R[c].interval;
-                    const int64_t ws = t - t % L;
+                    const int64_t L = R[c].interval, ws0 = S[c].window_start;
+                    // the current window needs no 64-bit modulo (lanes past a window boundary take it)
+                    const int64_t ws = (t >= 0 && ws0 != DG_WS_NONE && t >= ws0 && t - ws0 < L) ? ws0 : t - t % L;
                     wsv[c] = ws;
                     const bool h = R[c].grade == SF_DEGRADE_GRADE_RT ? (t - cr) > R[c].max_rt : (fl & SF_EV_ERROR) != 0;
                     Hm[c] = __ballot(is_ex && !ign && h);
@@ -350,7 +351,8 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
                 status[idx] = my_st;
                 if (rule) rule[idx] = my_rule;
             }
-            __threadfence();                     // verdicts visible to the loads issued from the next chunk on
+            // verdicts visible to this wave's loads from the next chunk on (one wave owns the segment)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             pidx = idx; pfirst = first; pblk = blkm;
             __syncthreads();
             sidx[lane] = idx;                    // previous chunk's indices for the next bulk prefix
