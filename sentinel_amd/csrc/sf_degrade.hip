@@ -183,25 +183,30 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
         for (uint32_t c = 0; c < MAXC; c++) {
             if (c < nc) { S[c] = d.state[c0 + c]; R[c] = d.rules[c0 + c]; }
         }
-        // gather of chunk [j, j+64): the lane's event, and the verdict of its
-        // entry when that entry is older than `bound` (already stored and fenced)
-        auto fetch = [&](uint32_t j, uint32_t bound, uint32_t& idx, int64_t& t, uint32_t& fl, int64_t& ref,
-                         int64_t& cr, bool& bad, bool& old_blk) {
+        // the lane's event of chunk [j, j+64) (sorted payload of k_dg_gather: one coalesced 32-B load)
+        auto load_rec = [&](uint32_t j, uint32_t& idx, int64_t& t, uint32_t& fl, int64_t& ref, int64_t& cr,
+                            bool& bad) {
             const uint32_t p = j + lane;
-            idx = 0xFFFFFFFFu; t = 0; fl = 0; ref = -1; cr = 0; bad = false; old_blk = false;
+            idx = 0xFFFFFFFFu; t = 0; fl = 0; ref = -1; cr = 0; bad = false;
             if (p < j1) {
-                const DgEv ev = sev[p];          // sorted payload (k_dg_gather): one coalesced 32-B load
+                const DgEv ev = sev[p];
                 idx = ev.idx; t = ev.t; fl = ev.fl & 0xFFu; ref = ev.ref; cr = ev.cr;
                 bad = (ev.fl >> 8) != 0u;
-                if ((fl & SF_EV_EXIT) && !bad && ref >= 0 && (uint64_t)ref < bound)
-                    old_blk = status[ref] == SF_V_BLOCK_DEGRADE;
             }
         };
-        uint32_t idx, fl, nidx = 0, nfl = 0;
-        int64_t t, ref, cr, nt = 0, nref = 0, ncr = 0;
-        bool bad, old_blk, nbad = false, nold = false;
+        // verdict of the event's entry when that entry is older than `bound` (stored and fenced)
+        auto load_old = [&](uint32_t fl, bool bad, int64_t ref, uint32_t bound) -> bool {
+            return (fl & SF_EV_EXIT) && !bad && ref >= 0 && (uint64_t)ref < bound &&
+                   status[ref] == SF_V_BLOCK_DEGRADE;
+        };
+        // records are fetched two chunks ahead, older-entry verdicts one chunk ahead
+        uint32_t idx, fl, idx1 = 0xFFFFFFFFu, fl1 = 0, idx2 = 0xFFFFFFFFu, fl2 = 0;
+        int64_t t, ref, cr, t1 = 0, ref1 = -1, cr1 = 0, t2 = 0, ref2 = -1, cr2 = 0;
+        bool bad, old_blk, bad1 = false, old1 = false, bad2 = false;
         const uint32_t first0 = sev[j0].idx;
-        fetch(j0, first0, idx, t, fl, ref, cr, bad, old_blk);
+        load_rec(j0, idx, t, fl, ref, cr, bad);
+        old_blk = load_old(fl, bad, ref, first0);
+        if (j0 + 64 < j1) load_rec(j0 + 64, idx1, t1, fl1, ref1, cr1, bad1);
         uint32_t pidx = 0xFFFFFFFFu, pfirst = first0;   // previous chunk: lane indices, lowest index
         uint64_t pblk = 0;                              // previous chunk: blocked entries
         for (uint32_t j = j0; j < j1; j += 64) {
@@ -209,8 +214,9 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
             const uint32_t first = __builtin_amdgcn_readfirstlane(idx);   // lowest index of the chunk
             if (bad) atomicOr(err, 2);
             const uint64_t badm = __ballot(bad), oldm = __ballot(old_blk);
-            // next chunk in flight; its older-entry verdicts are those stored before this chunk
-            if (j + 64 < j1) fetch(j + 64, first, nidx, nt, nfl, nref, ncr, nbad, nold);
+            if (j + 128 < j1) load_rec(j + 128, idx2, t2, fl2, ref2, cr2, bad2);
+            // the next chunk's older-entry verdicts are those stored before this chunk
+            if (j + 64 < j1) old1 = load_old(fl1, bad1, ref1, first);
             uint8_t my_st = (fl & SF_EV_EXIT) ? SF_V_EXIT : SF_V_PASS;
             uint16_t my_rule = 0;
             // ---- bulk prefix: the events before the first state change, decided lane-parallel
@@ -356,7 +362,8 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
             pidx = idx; pfirst = first; pblk = blkm;
             __syncthreads();
             sidx[lane] = idx;                    // previous chunk's indices for the next bulk prefix
-            idx = nidx; t = nt; fl = nfl; ref = nref; cr = ncr; bad = nbad; old_blk = nold;
+            idx = idx1; t = t1; fl = fl1; ref = ref1; cr = cr1; bad = bad1; old_blk = old1;
+            idx1 = idx2; t1 = t2; fl1 = fl2; ref1 = ref2; cr1 = cr2; bad1 = bad2;
         }
         if (lane == 0) {
 #pragma unroll
