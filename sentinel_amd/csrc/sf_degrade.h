@@ -37,8 +37,9 @@ struct DegradeBatch {
 };
 
 struct alignas(16) DgEv {                      // sorted event of a breaker resource, 32 B
-    int64_t t, cr, ref;                        // ts, entry create ts (exits), entry_ref
+    int64_t t, cr;                             // ts, entry create ts (exits)
     uint32_t idx, fl;                          // submission index, flags | bad << 8
+    uint32_t ref, refpos;                      // entry_ref (~0 = none) and its sorted position
 };
 
 struct DegradeWork {
@@ -51,6 +52,7 @@ struct DegradeWork {
     uint32_t* heavy = nullptr;                 // [n_rres] long segments for the wave walk
     uint32_t* n_heavy = nullptr;
     DgEv* sev = nullptr;                       // [cap]
+    uint32_t* inv = nullptr;                   // [cap] submission index -> sorted position
 };
 
 hipError_t dg_sort_bytes(uint32_t n, uint32_t key_bits, size_t* bytes);

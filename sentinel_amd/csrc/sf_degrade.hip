@@ -107,8 +107,14 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int l) {
 // Sorted event payload of every breaker-resource event (keys < none come
 // first after the sort): the wave walk then reads one coalesced 32-B record per
 // lane instead of a chain of dependent gathers.
+__global__ void __launch_bounds__(BLK) k_dg_inv(uint32_t n, const uint32_t* keys, const uint32_t* perm,
+                                                uint32_t none, uint32_t* inv) {
+    const uint32_t j = blockIdx.x * BLK + threadIdx.x;
+    if (j < n && keys[j] < none) inv[perm[j]] = j;
+}
+
 __global__ void __launch_bounds__(BLK) k_dg_gather(DegradeBatch b, const uint32_t* keys, const uint32_t* perm,
-                                                   uint32_t none, DgEv* sev) {
+                                                   uint32_t none, const uint32_t* inv, DgEv* sev) {
     const uint32_t j = blockIdx.x * BLK + threadIdx.x;
     if (j >= b.n || keys[j] >= none) return;
     const uint32_t idx = perm[j];
@@ -116,14 +122,19 @@ __global__ void __launch_bounds__(BLK) k_dg_gather(DegradeBatch b, const uint32_
     ev.idx = idx;
     ev.t = b.ts[idx];
     uint32_t fl = b.flags[idx], bad = 0;
-    ev.ref = -1;
+    ev.ref = 0xFFFFFFFFu;
+    ev.refpos = 0xFFFFFFFFu;
     ev.cr = 0;
     if (fl & SF_EV_EXIT) {
         const int64_t ref = b.eref ? b.eref[idx] : -1;
-        ev.ref = ref;
         if (ref >= 0) {
-            if ((uint64_t)ref < b.n) ev.cr = b.ts[ref];
-            else bad = 1;
+            if ((uint64_t)ref < b.n) {
+                ev.cr = b.ts[ref];
+                ev.ref = (uint32_t)ref;
+                ev.refpos = inv[ref];        // the entry's sorted position (same resource)
+            } else {
+                bad = 1;
+            }
         } else if (b.cts) {
             ev.cr = b.cts[idx];
         } else {
@@ -141,15 +152,6 @@ __device__ __forceinline__ int64_t rl64_up(int64_t v) {
     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
     const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)v >> 32), src);
     return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
-// position of index x in an ascending LDS array of 64 indices (x is present)
-__device__ __forceinline__ uint32_t lds_find(const uint32_t* a, uint32_t x) {
-    uint32_t lo = 0;
-#pragma unroll
-    for (uint32_t step = 32; step; step >>= 1)
-        if (a[lo + step - 1] < x) lo += step;
-    return lo;
 }
 
 // One wave per long breaker segment (<= MAXC breakers).  Chunks of 64 events:
@@ -171,7 +173,6 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
                                                 const uint32_t* n_heavy) {
     const int lane = threadIdx.x;
     const uint32_t nh = *n_heavy;
-    __shared__ uint32_t sidx[128];               // [0,64) previous chunk's indices, [64,128) this chunk's
     for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {
         const uint32_t k = heavy[h];
         const uint32_t j0 = beg[k], j1 = end[k];
@@ -184,44 +185,42 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
             if (c < nc) { S[c] = d.state[c0 + c]; R[c] = d.rules[c0 + c]; }
         }
         // the lane's event of chunk [j, j+64) (sorted payload of k_dg_gather: one coalesced 32-B load)
-        auto load_rec = [&](uint32_t j, uint32_t& idx, int64_t& t, uint32_t& fl, int64_t& ref, int64_t& cr,
-                            bool& bad) {
+        auto load_rec = [&](uint32_t j, uint32_t& idx, int64_t& t, uint32_t& fl, int64_t& ref, uint32_t& rp,
+                            int64_t& cr, bool& bad) {
             const uint32_t p = j + lane;
-            idx = 0xFFFFFFFFu; t = 0; fl = 0; ref = -1; cr = 0; bad = false;
+            idx = 0xFFFFFFFFu; t = 0; fl = 0; ref = -1; rp = 0xFFFFFFFFu; cr = 0; bad = false;
             if (p < j1) {
                 const DgEv ev = sev[p];
-                idx = ev.idx; t = ev.t; fl = ev.fl & 0xFFu; ref = ev.ref; cr = ev.cr;
+                idx = ev.idx; t = ev.t; fl = ev.fl & 0xFFu; cr = ev.cr; rp = ev.refpos;
+                ref = ev.ref == 0xFFFFFFFFu ? -1 : (int64_t)ev.ref;
                 bad = (ev.fl >> 8) != 0u;
             }
         };
-        // verdict of the event's entry when that entry is older than `bound` (stored and fenced)
-        auto load_old = [&](uint32_t fl, bool bad, int64_t ref, uint32_t bound) -> bool {
-            return (fl & SF_EV_EXIT) && !bad && ref >= 0 && (uint64_t)ref < bound &&
-                   status[ref] == SF_V_BLOCK_DEGRADE;
+        // verdict of the event's entry when that entry sits before sorted position `bound`
+        // (stored and fenced by this wave, or outside the segment)
+        auto load_old = [&](uint32_t fl, bool bad, int64_t ref, uint32_t rp, uint32_t bound) -> bool {
+            return (fl & SF_EV_EXIT) && !bad && ref >= 0 && rp < bound && status[ref] == SF_V_BLOCK_DEGRADE;
         };
         // records are fetched two chunks ahead, older-entry verdicts one chunk ahead
-        uint32_t idx, fl, idx1 = 0xFFFFFFFFu, fl1 = 0, idx2 = 0xFFFFFFFFu, fl2 = 0;
+        uint32_t idx, fl, rp, idx1 = 0xFFFFFFFFu, fl1 = 0, rp1 = 0xFFFFFFFFu, idx2 = 0xFFFFFFFFu, fl2 = 0,
+                 rp2 = 0xFFFFFFFFu;
         int64_t t, ref, cr, t1 = 0, ref1 = -1, cr1 = 0, t2 = 0, ref2 = -1, cr2 = 0;
         bool bad, old_blk, bad1 = false, old1 = false, bad2 = false;
-        const uint32_t first0 = sev[j0].idx;
-        load_rec(j0, idx, t, fl, ref, cr, bad);
-        old_blk = load_old(fl, bad, ref, first0);
-        if (j0 + 64 < j1) load_rec(j0 + 64, idx1, t1, fl1, ref1, cr1, bad1);
-        uint32_t pidx = 0xFFFFFFFFu, pfirst = first0;   // previous chunk: lane indices, lowest index
+        load_rec(j0, idx, t, fl, ref, rp, cr, bad);
+        old_blk = load_old(fl, bad, ref, rp, j0);
+        if (j0 + 64 < j1) load_rec(j0 + 64, idx1, t1, fl1, ref1, rp1, cr1, bad1);
         uint64_t pblk = 0;                              // previous chunk: blocked entries
         for (uint32_t j = j0; j < j1; j += 64) {
             const uint32_t cnt = min(64u, j1 - j);
-            const uint32_t first = __builtin_amdgcn_readfirstlane(idx);   // lowest index of the chunk
+            const uint32_t pj = j - 64;                 // previous chunk's start (unused in the first chunk)
             if (bad) atomicOr(err, 2);
             const uint64_t badm = __ballot(bad), oldm = __ballot(old_blk);
-            if (j + 128 < j1) load_rec(j + 128, idx2, t2, fl2, ref2, cr2, bad2);
+            if (j + 128 < j1) load_rec(j + 128, idx2, t2, fl2, ref2, rp2, cr2, bad2);
             // the next chunk's older-entry verdicts are those stored before this chunk
-            if (j + 64 < j1) old1 = load_old(fl1, bad1, ref1, first);
+            if (j + 64 < j1) old1 = load_old(fl1, bad1, ref1, rp1, j);
             uint8_t my_st = (fl & SF_EV_EXIT) ? SF_V_EXIT : SF_V_PASS;
             uint16_t my_rule = 0;
             // ---- bulk prefix: the events before the first state change, decided lane-parallel
-            sidx[64 + lane] = idx;
-            __syncthreads();
             const bool valid = (uint32_t)lane < cnt;
             const bool is_en = valid && !(fl & SF_EV_EXIT);
             const bool is_ex = valid && (fl & SF_EV_EXIT) && !bad;
@@ -248,8 +247,8 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
             const uint64_t N = __ballot(is_en && !inv), BI = __ballot(is_en && inv_blk);
             bool ign = false;
             if (is_ex && ref >= 0) {
-                if ((uint64_t)ref >= first) ign = (BI >> lds_find(sidx + 64, (uint32_t)ref)) & 1ull;
-                else if ((uint64_t)ref >= pfirst) ign = (pblk >> lds_find(sidx, (uint32_t)ref)) & 1ull;
+                if (rp >= j && rp < j + 64) ign = (BI >> (rp - j)) & 1ull;
+                else if (j > j0 && rp >= pj && rp < j) ign = (pblk >> (rp - pj)) & 1ull;
                 else ign = old_blk;
             }
             const uint64_t E = __ballot(is_ex && !ign);
@@ -338,10 +337,11 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
                 }
                 if ((badm >> q) & 1ull) continue;
                 const int64_t rq = rl64(ref, q);
+                const uint32_t rpq = (uint32_t)__builtin_amdgcn_readlane((int)rp, q);
                 bool ign;
                 if (rq < 0) ign = false;
-                else if ((uint64_t)rq >= first) ign = (__ballot(idx == (uint32_t)rq) & blkm) != 0ull;
-                else if ((uint64_t)rq >= pfirst) ign = (__ballot(pidx == (uint32_t)rq) & pblk) != 0ull;
+                else if (rpq >= j && rpq < j + 64) ign = (blkm >> (rpq - j)) & 1ull;
+                else if (j > j0 && rpq >= pj && rpq < j) ign = (pblk >> (rpq - pj)) & 1ull;
                 else ign = (oldm >> q) & 1ull;
                 if (ign) {
                     if ((uint32_t)lane == q) my_st = SF_V_EXIT_IGNORED;
@@ -359,11 +359,9 @@ __global__ void __launch_bounds__(64) k_dg_wave(DegradeDev d, DegradeBatch b, co
             }
             // verdicts visible to this wave's loads from the next chunk on (one wave owns the segment)
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            pidx = idx; pfirst = first; pblk = blkm;
-            __syncthreads();
-            sidx[lane] = idx;                    // previous chunk's indices for the next bulk prefix
-            idx = idx1; t = t1; fl = fl1; ref = ref1; cr = cr1; bad = bad1; old_blk = old1;
-            idx1 = idx2; t1 = t2; fl1 = fl2; ref1 = ref2; cr1 = cr2; bad1 = bad2;
+            pblk = blkm;
+            idx = idx1; t = t1; fl = fl1; ref = ref1; rp = rp1; cr = cr1; bad = bad1; old_blk = old1;
+            idx1 = idx2; t1 = t2; fl1 = fl2; ref1 = ref2; rp1 = rp2; cr1 = cr2; bad1 = bad2;
         }
         if (lane == 0) {
 #pragma unroll
@@ -470,7 +468,8 @@ hipError_t dg_launch(const DegradeDev& d, DegradeWork& w, const DegradeBatch& b,
     k_dg_walk<<<blocks(d.n_rres), BLK, 0, s>>>(d, b, w.idx_out, w.beg, w.end, status, rule, w.err, w.heavy,
                                                w.n_heavy);
     const uint32_t waves = min(d.n_rres, 2048u);
-    k_dg_gather<<<blocks(b.n), BLK, 0, s>>>(b, w.keys_out, w.idx_out, d.n_rres, w.sev);
+    k_dg_inv<<<blocks(b.n), BLK, 0, s>>>(b.n, w.keys_out, w.idx_out, d.n_rres, w.inv);
+    k_dg_gather<<<blocks(b.n), BLK, 0, s>>>(b, w.keys_out, w.idx_out, d.n_rres, w.inv, w.sev);
     k_dg_wave<<<waves, 64, 0, s>>>(d, b, w.sev, w.beg, w.end, status, rule, w.err, w.heavy, w.n_heavy);
     return hipGetLastError();
 }

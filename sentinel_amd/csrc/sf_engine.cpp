@@ -165,7 +165,7 @@ void sf_destroy(sf_engine* e) {
     if (e->agg) hipFree(e->agg);
     void* dptrs[] = {(void*)e->dg.rr_of, (void*)e->dg.off, (void*)e->dg.rules, e->dg.state, e->dgw.keys_in,
                      e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
-                     e->dgw.err, e->dg_stage, e->dgw.heavy, e->dgw.n_heavy, e->dgw.sev};
+                     e->dgw.err, e->dg_stage, e->dgw.heavy, e->dgw.n_heavy, e->dgw.sev, e->dgw.inv};
     for (void* p : dptrs) if (p) hipFree(p);
     if (e->comm) ncclCommDestroy(e->comm);
     free_tok_work(e->tw);
@@ -1498,13 +1498,14 @@ int sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t n
 static int dg_ensure(sf_engine* e, uint32_t n) {
     DegradeWork& w = e->dgw;
     if (n > w.cap) {
-        void* ptrs[] = {w.keys_in, w.keys_out, w.idx_in, w.idx_out, w.sev};
+        void* ptrs[] = {w.keys_in, w.keys_out, w.idx_in, w.idx_out, w.sev, w.inv};
         for (void* p : ptrs) if (p) hipFree(p);
         w.keys_in = w.keys_out = w.idx_in = w.idx_out = nullptr;
         w.sev = nullptr;
+        w.inv = nullptr;
         if (dalloc((void**)&w.keys_in, (size_t)n * 4) || dalloc((void**)&w.keys_out, (size_t)n * 4) ||
             dalloc((void**)&w.idx_in, (size_t)n * 4) || dalloc((void**)&w.idx_out, (size_t)n * 4) ||
-            dalloc((void**)&w.sev, (size_t)n * sizeof(DgEv)))
+            dalloc((void**)&w.sev, (size_t)n * sizeof(DgEv)) || dalloc((void**)&w.inv, (size_t)n * 4))
             return SF_ERR_NOMEM;
         w.cap = n;
         if (w.sort_tmp) { hipFree(w.sort_tmp); w.sort_tmp = nullptr; }
