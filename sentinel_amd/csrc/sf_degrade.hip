@@ -159,9 +159,9 @@ __device__ __forceinline__ int64_t rl64_up(int64_t v) {
 // verdict of an entry decided in an earlier chunk, the next chunk's events are
 // fetched while this one is walked, and the walk itself runs wave-uniform on
 // readlane'd values with the breaker state in registers -- the per-event chain
-// has no memory access.  A reference to an entry of the current chunk is
-// resolved with a ballot over the chunk's indices (the sort is stable, so
-// indices grow with the sorted position).  Before the serial walk, a bulk
+// has no memory access.  A reference to an entry of the current or previous
+// chunk is a bit of that chunk's blocked mask, found from the entry's sorted
+// position (k_dg_inv / k_dg_gather).  Before the serial walk, a bulk
 // prefix decides lane-parallel every event up to the first one that can change
 // a breaker's state: entries refused by an OPEN (retry not reached) or
 // HALF_OPEN breaker or passed by CLOSED ones, and exits that only count
