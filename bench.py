@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1 << 26, help="events replayed by the CPU oracle (about 15 s on one core)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-metric-log", action="store_true")
+    ap.add_argument("--no-degrade", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -209,6 +210,15 @@ def main():
         except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
             metric_log = {"error": str(ex)[:200]}
 
+    # DegradeSlot leg (tools/degrade_bench.py has the full
+    # version with the whole-batch oracle check): its own 1M-resource engine
+    degrade = None
+    if rank == 0 and world == 1 and not args.no_degrade:
+        try:
+            degrade = degrade_leg()
+        except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
+            degrade = {"error": str(ex)[:200]}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(rules, hb, R_local, args.cpu_sample)
@@ -224,12 +234,41 @@ def main():
                            "resources_touched": n_seg, "pass_fraction": round(n_pass / max(1, n_entry), 4),
                            "parallelism": f"resource-sharded x{world}"},
                 "roofline": roofline, "cpu_baseline": cpu, "aggregate": aggregate,
-                "metric_log": metric_log}
+                "metric_log": metric_log, "degrade": degrade}
         print(json.dumps(line), flush=True)
     for b in batches:
         b.free()
     if dist:
         dist.destroy_process_group()
+
+
+def degrade_leg(R=1_000_000, entries=1 << 22, steps=3):
+    """sf_degrade_submit over an HBM-resident batch: one circuit breaker (RT /
+    exception ratio / exception count) on half of 1M resources, Zipf(1.1)
+    entries each followed by its exit; every step replays from fresh breakers."""
+    rules = trace.degrade_rules_array(R, seed=5)
+    b = trace.degrade_workload(R, entries, duration_ms=4000, seed=6, s=1.1)
+    e = engine.FlowEngine(abi.default_config(max_resources=R, max_batch=b.n))
+    try:
+        n_cb = e.load_degrade_rules(rules)
+        db = engine.DeviceBatch(e, b)
+        dv = engine.DeviceVerdicts(e, b.n, with_wait=False, with_rule=True)
+        e.degrade_submit_device(db, dv)
+        wall = []
+        for _ in range(steps):
+            e.load_degrade_rules(rules)
+            t = time.perf_counter()
+            e.degrade_submit_device(db, dv)
+            wall.append(time.perf_counter() - t)
+        ms = float(np.median(wall)) * 1e3
+        st = dv.status.numpy()
+        db.free()
+        return {"what": "DegradeSlot circuit breakers (sf_degrade_submit), Zipf(1.1), fresh breakers per step",
+                "resources": R, "breakers": int(n_cb), "events": int(b.n), "ms_per_batch": round(ms, 3),
+                "events_per_s": round(b.n / (ms / 1e3), 1),
+                "blocked": int((st == abi.V_BLOCK_DEGRADE).sum())}
+    finally:
+        e.close()
 
 
 def metric_log_leg(eng, hb, R_total, R_local, world, rank, steps):
