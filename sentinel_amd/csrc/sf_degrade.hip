@@ -19,7 +19,7 @@
 namespace sf_dg {
 
 constexpr int BLK = 256;
-constexpr uint32_t HEAVY = 512;     // segments longer than this are walked by a whole wave
+constexpr uint32_t HEAVY = 64;      // segments longer than this are walked by a whole wave
 constexpr uint32_t MAXC = 4;        // breakers per resource held in registers by the wave walk
 
 __global__ void __launch_bounds__(BLK) k_dg_keys(DegradeDev d, DegradeBatch b, uint32_t* keys, uint32_t* idx,
