@@ -7,5 +7,15 @@ timeout -k 10 200 python3 tools/degrade_bench.py ${DG_ARGS:-} --zipf 0.6 --cpu-s
 cat $OUT/bench_mild.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format rocpd -d $OUT/kt -o kt -- python3 tools/degrade_bench.py \
     ${DG_ARGS:-} --steps 3 --warmup 1 --cpu-sample 0 > $OUT/kt_bench.json 2> $OUT/kt.err || { echo KT_FAILED; tail $OUT/kt.err; exit 1; }
-python3 tools/prof_summary.py --kt $(find $OUT/kt -name '*.db' | head -1) --out $OUT/summary
+KT=$(find $OUT/kt -name '*.db' | head -1)
+if [ -n "$PMC" ]; then
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format rocpd -d $OUT/fetch -o fetch -- python3 tools/degrade_bench.py \
+        ${DG_ARGS:-} --steps 3 --warmup 1 --cpu-sample 0 > $OUT/fetch.log 2>&1 || { echo FETCH_FAILED; tail $OUT/fetch.log; exit 1; }
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format rocpd -d $OUT/write -o write -- python3 tools/degrade_bench.py \
+        ${DG_ARGS:-} --steps 3 --warmup 1 --cpu-sample 0 > $OUT/write.log 2>&1 || { echo WRITE_FAILED; tail $OUT/write.log; exit 1; }
+    python3 tools/prof_summary.py --kt $KT --fetch $(find $OUT/fetch -name '*.db' | head -1) \
+        --write $(find $OUT/write -name '*.db' | head -1) --out $OUT/summary
+else
+    python3 tools/prof_summary.py --kt $KT --out $OUT/summary
+fi
 cat $OUT/summary_kernels.txt
