@@ -12,6 +12,11 @@ Seeds are fixed; inputs are the shapes of BASELINE.json's configs at test size:
   param_40       config 4 shape: ParamFlow QPS / throttle, Zipf keys
   param_mixed    ParamFlow QPS / throttle / THREAD grade, hot items, null values
   token_5k       config 5 shape: requestToken / requestParamToken, namespace limiter
+  degrade_3k     DegradeSlot: RT / exception-ratio / exception-count breakers on
+                 3k resources, Zipf entries + exits, two batches (cross-batch
+                 exits); verdicts, breaker indices, final breaker states.  Made by
+                 oracle/degrade.py, which the reference's circuit-breaker tests
+                 pin (tests/test_degrade.py)
 """
 import os
 import sys
@@ -82,9 +87,35 @@ def token_case(name, n):
     print(name, b.n, "requests")
 
 
+def degrade_case(name="degrade_3k"):
+    from oracle import degrade as od
+    R = 3000
+    rules = trace.degrade_rules(R, seed=81)
+    arr = np.zeros(len(rules), abi.DEGRADE_RULE_DTYPE)
+    for i, r in enumerate(rules):
+        for k, v in r.items():
+            arr[i][k] = v
+    full = trace.degrade_workload(R, 40_000, duration_ms=6000, seed=81, err_p=0.2)
+    cut = full.n // 2
+    o = od.DegradeOracle()
+    n = o.load_rules(rules)
+    out = {"rules": arr, "R": np.array([R])}
+    for k, b in enumerate((full.subset(0, cut), full.subset(cut, full.n))):
+        st, ri = o.submit(b.res_id, b.ts_ms, b.flags, b.entry_ref, b.create_ts)
+        out.update(batch_arrays(f"b{k}_", b))
+        out[f"b{k}_status"], out[f"b{k}_rule"] = st, ri
+    states = [o.state(i) for i in range(n)]
+    out["breakers"] = np.array([[s["state"], s["next_retry_ms"],
+                                 abi.WS_ABSENT if s["window_start"] is None else s["window_start"],
+                                 s["hit_count"], s["total_count"]] for s in states], np.int64)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(name, full.n, "events,", n, "breakers")
+
+
 if __name__ == "__main__":
     flow_case("flowqps_demo", workloads.config1(duration_ms=10_000))
     flow_case("mixed_1k", workloads.config3(R=1000, n=50_000, seed=77, split=2, duration_ms=5000))
     flow_case("param_40", workloads.config4(R=40, n=30_000, keys=3000, seed=78))
     flow_case("param_mixed", workloads.param_mixed(seed=79, R=10, n=15_000))
     token_case("token_5k", 5000)
+    degrade_case()

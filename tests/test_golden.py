@@ -97,3 +97,49 @@ def test_engine_matches_golden(name):
 def test_engine_matches_golden_tokens():
     from sentinel_amd import engine
     check_token_case(engine.FlowEngine)
+
+
+# ---- DegradeSlot (degrade_3k.npz) ----
+def _degrade_case():
+    z = np.load(os.path.join(HERE, "degrade_3k.npz"))
+    rules = [{k: z["rules"][i][k].item() for k in abi.DEGRADE_RULE_DTYPE.names if k != "pad"}
+             for i in range(z["rules"].size)]
+    batches = []
+    for k in (0, 1):
+        p = f"b{k}_"
+        b = abi.HostBatch(z[p + "res"], z[p + "ts"], z[p + "cnt"], z[p + "flags"], entry_ref=z[p + "eref"],
+                          create_ts=z[p + "cts"] if p + "cts" in z else None)
+        batches.append((b, z[p + "status"], z[p + "rule"]))
+    return int(z["R"][0]), rules, batches, z["breakers"]
+
+
+def _state_row(s):
+    return [s["state"], s["next_retry_ms"], abi.WS_ABSENT if s["window_start"] is None else s["window_start"],
+            s["hit_count"], s["total_count"]]
+
+
+def test_degrade_oracle_reproduces_golden():
+    from oracle import degrade as od
+    _, rules, batches, breakers = _degrade_case()
+    o = od.DegradeOracle()
+    assert o.load_rules(rules) == breakers.shape[0]
+    for b, st, ri in batches:
+        got, gri = o.submit(b.res_id, b.ts_ms, b.flags, b.entry_ref, b.create_ts)
+        assert np.array_equal(got, st) and np.array_equal(gri, ri)
+    assert np.array_equal(np.array([_state_row(o.state(i)) for i in range(breakers.shape[0])]), breakers)
+
+
+@pytest.mark.gpu
+def test_degrade_engine_matches_golden():
+    from sentinel_amd import engine
+    R, rules, batches, breakers = _degrade_case()
+    e = engine.FlowEngine(abi.default_config(max_resources=R, max_batch=max(b.n for b, _, _ in batches)))
+    try:
+        assert e.load_degrade_rules(rules) == breakers.shape[0]
+        for b, st, ri in batches:
+            v = e.degrade_submit(b)
+            blk = st == abi.V_BLOCK_DEGRADE
+            assert np.array_equal(v.status, st) and np.array_equal(v.rule_idx[blk], ri[blk])
+        assert np.array_equal(np.array([_state_row(e.read_breaker(i)) for i in range(breakers.shape[0])]), breakers)
+    finally:
+        e.close()
