@@ -457,7 +457,12 @@ int  sf_entry_node_allreduce(sf_engine* e, sf_node_state* out);
  * a breaker moved OPEN->HALF_OPEN by this entry falls back to OPEN through
  * the whenTerminate hook, :113-129); EXIT of a passed entry ->
  * onRequestComplete of every breaker with rt = exit ts - create ts and the
- * SF_EV_ERROR flag (Tracer error).  Loading rules resets breaker state.   */
+ * SF_EV_ERROR flag (Tracer error).  A reload keeps the breaker (and its
+ * state) of every rule equal to a loaded one on the same resource
+ * (DegradeRuleManager.getExistingSameCbOrNew :151-163; two equal new rules
+ * that would share one breaker are refused with SF_ERR_UNSUPPORTED); a
+ * failed load leaves the loaded rules in place.  Event times must be
+ * non-decreasing within a batch and across batches (SF_ERR_INVALID).      */
 #define SF_DEGRADE_GRADE_RT              0   /* RuleConstant.DEGRADE_GRADE_RT */
 #define SF_DEGRADE_GRADE_EXCEPTION_RATIO 1
 #define SF_DEGRADE_GRADE_EXCEPTION_COUNT 2

@@ -29,8 +29,18 @@ V_PASS, V_EXIT, V_EXIT_IGNORED, V_BLOCK_DEGRADE = 0, 6, 7, 8
 
 
 def java_round(x: float) -> int:
-    """Math.round(double): floor(x + 0.5) as long."""
-    return int(math.floor(x + 0.5))
+    """Math.round(double) (Java 7+): the exact floor(x + 1/2) -- no rounding
+    error in the addition (0.49999999999999994 rounds to 0) -- saturated to
+    the long range, NaN to 0."""
+    x = float(x)
+    if math.isnan(x):
+        return 0
+    if x >= 9223372036854775807.0:
+        return (1 << 63) - 1
+    if x <= -9223372036854775808.0:
+        return -(1 << 63)
+    f = math.floor(x)
+    return int(f) + (1 if x - f >= 0.5 else 0)     # x - floor(x) is exact for a double
 
 
 def is_valid_rule(r) -> bool:
@@ -51,6 +61,8 @@ class Breaker:
     """One CircuitBreaker with its LeapArray(1, statIntervalMs) counter."""
 
     def __init__(self, r):
+        self.rule = {k: r[k] for k in ("resource", "grade", "count", "time_window_s", "min_request_amount",
+                                       "slow_ratio_threshold", "stat_interval_ms")}
         self.grade = r["grade"]
         self.max_rt = java_round(r["count"])             # ResponseTimeCircuitBreaker :52
         self.threshold = float(r["slow_ratio_threshold"] if self.grade == GRADE_RT else r["count"])
@@ -62,6 +74,18 @@ class Breaker:
         self.ws = None                                   # the single bucket (null until first use)
         self.hit = 0
         self.total = 0
+
+    def same_rule(self, r) -> bool:
+        """DegradeRule.equals: the six fields by Double.compare, same resource."""
+        def deq(a, b):
+            a, b = float(a), float(b)
+            return (a != a and b != b) or np.float64(a).tobytes() == np.float64(b).tobytes()
+        o = self.rule
+        return (int(o["resource"]) == int(r["resource"]) and int(o["grade"]) == int(r["grade"])
+                and deq(o["count"], r["count"]) and int(o["time_window_s"]) == int(r["time_window_s"])
+                and int(o["min_request_amount"]) == int(r["min_request_amount"])
+                and deq(o["slow_ratio_threshold"], r["slow_ratio_threshold"])
+                and int(o["stat_interval_ms"]) == int(r["stat_interval_ms"]))
 
     def _current(self, t):
         """LeapArray.currentWindow(t) with one bucket: create / keep / reset (:128-225)."""
@@ -120,12 +144,22 @@ class DegradeOracle:
         self.created = {}         # entries passed in earlier batches are looked up by create_ts
 
     def load_rules(self, rules):
+        """buildCircuitBreakers (:236-265) with getExistingSameCbOrNew (:151-163):
+        a valid rule equal (DegradeRule.equals :153-164) to one of the
+        resource's current breakers keeps that breaker, state included."""
+        old = {}
+        for res, ks in self.by_res.items():
+            old[res] = [self.breakers[k] for k in ks]
         self.breakers, self.by_res = [], {}
         for r in rules:
             if not is_valid_rule(r):
                 continue
-            self.by_res.setdefault(int(r["resource"]), []).append(len(self.breakers))
-            self.breakers.append(Breaker(r))
+            res = int(r["resource"])
+            cb = next((b for b in old.get(res, ()) if b.same_rule(r)), None)
+            if cb is not None and any(b is cb for b in self.breakers):
+                raise ValueError("two equal rules share one breaker (the engine refuses this reload)")
+            self.by_res.setdefault(res, []).append(len(self.breakers))
+            self.breakers.append(cb if cb is not None else Breaker(r))
         return len(self.breakers)
 
     def submit(self, res, ts, flags, entry_ref=None, create_ts=None):

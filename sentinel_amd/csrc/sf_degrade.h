@@ -34,6 +34,7 @@ struct DegradeBatch {
     const uint32_t* res; const int64_t* ts; const uint8_t* flags;
     const int64_t* eref; const int64_t* cts;
     uint32_t shard_count, shard_index, R;
+    int64_t* last_ts;                          // engine clock (non-decreasing across batches)
 };
 
 struct alignas(16) DgEv {                      // sorted event of a breaker resource, 32 B

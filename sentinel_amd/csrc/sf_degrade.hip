@@ -29,6 +29,7 @@ __global__ void __launch_bounds__(BLK) k_dg_keys(DegradeDev d, DegradeBatch b, u
     const uint32_t r = b.res[i];
     const uint8_t f = b.flags[i];
     uint32_t key = d.n_rres;
+    if (b.ts[i] < (i ? b.ts[i - 1] : *b.last_ts)) atomicOr(err, 4);   // the clock never goes back
     if (r % b.shard_count != b.shard_index || r / b.shard_count >= b.R) {
         atomicOr(err, 1);
     } else if (d.n_rres) {               // rr_of exists once degrade rules were loaded
@@ -41,6 +42,8 @@ __global__ void __launch_bounds__(BLK) k_dg_keys(DegradeDev d, DegradeBatch b, u
     if (rule) rule[i] = 0;
     if (wait) wait[i] = 0;
 }
+
+__global__ void k_dg_clock(DegradeBatch b) { *b.last_ts = b.ts[b.n - 1]; }
 
 __global__ void __launch_bounds__(BLK) k_dg_bounds(const uint32_t* keys, uint32_t n, uint32_t none, uint32_t* beg,
                                                    uint32_t* end) {
@@ -128,7 +131,8 @@ __global__ void __launch_bounds__(BLK) k_dg_gather(DegradeBatch b, const uint32_
     if (fl & SF_EV_EXIT) {
         const int64_t ref = b.eref ? b.eref[idx] : -1;
         if (ref >= 0) {
-            if ((uint64_t)ref < b.n) {
+            // the entry: earlier in this batch, same resource, an ENTRY (its sorted position is then valid)
+            if (ref < (int64_t)idx && b.res[ref] == b.res[idx] && !(b.flags[ref] & SF_EV_EXIT)) {
                 ev.cr = b.ts[ref];
                 ev.ref = (uint32_t)ref;
                 ev.refpos = inv[ref];        // the entry's sorted position (same resource)
@@ -421,7 +425,7 @@ __global__ void __launch_bounds__(BLK) k_dg_walk(DegradeDev d, DegradeBatch b, c
         int64_t created;
         const int64_t ref = b.eref ? b.eref[i] : -1;
         if (ref >= 0) {
-            if ((uint64_t)ref >= b.n) { atomicOr(err, 2); continue; }
+            if (ref >= (int64_t)i || b.res[ref] != b.res[i] || (b.flags[ref] & SF_EV_EXIT)) { atomicOr(err, 2); continue; }
             if (status[ref] == SF_V_BLOCK_DEGRADE) { status[i] = SF_V_EXIT_IGNORED; continue; }
             created = b.ts[ref];
         } else {
@@ -453,6 +457,7 @@ hipError_t dg_launch(const DegradeDev& d, DegradeWork& w, const DegradeBatch& b,
                      int32_t* wait, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
     k_dg_keys<<<blocks(b.n), BLK, 0, s>>>(d, b, w.keys_in, w.idx_in, status, rule, wait, w.err);
+    k_dg_clock<<<1, 1, 0, s>>>(b);
     if (d.n_rres == 0) return hipGetLastError();
     size_t bytes = w.sort_tmp_bytes;
     hipError_t e = rocprim::radix_sort_pairs(w.sort_tmp, bytes, w.keys_in, w.keys_out, w.idx_in, w.idx_out, b.n, 0u,

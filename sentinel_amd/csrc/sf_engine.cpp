@@ -96,6 +96,7 @@ struct sf_engine {
     DegradeDev dg{};
     DegradeWork dgw{};
     std::vector<uint32_t> dg_pos;         // breaker index (load order) -> CSR position
+    std::vector<sf_degrade_rule> dg_rules;   // the valid rules of the loaded breakers (load order)
     void* dg_stage = nullptr; size_t dg_stage_bytes = 0;
 };
 
@@ -158,7 +159,7 @@ void sf_destroy(sf_engine* e) {
     for (void* p : e->user_allocs) hipFree(p);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
                      (void*)e->ts.items, e->tok_stage, e->wire_arena, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
-                     e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch, e->nm_bytes, e->nm_off,
+                     e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch, e->st.last_ts, e->nm_bytes, e->nm_off,
                      e->nm_types, e->ml_mask, e->ml_counts, e->ml_offsets, e->ml_total, e->ml_rows, e->ml_keys,
                      e->ml_order, e->ml_len, e->ml_off, e->ml_bytes, e->ml_out, e->ml_tmp};
     for (void* p : tptrs) if (p) hipFree(p);
@@ -314,6 +315,11 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     e->ts.max_occupy_ratio = c.max_occupy_ratio;
     DALLOC(e->d_sum, sizeof(int64_t));
     DALLOC(st.last_fetch, R * sizeof(int64_t));
+    DALLOC(st.last_ts, sizeof(int64_t));
+    {
+        const int64_t t_min = INT64_MIN;
+        HIP_TRY(hipMemcpyAsync(st.last_ts, &t_min, 8, hipMemcpyHostToDevice, e->stream));
+    }
     HIP_TRY(hipMemsetAsync(st.last_fetch, 0xff, R * sizeof(int64_t), e->stream));   // lastFetchTime = -1
     DALLOC(e->en, sizeof(EntryNode));
     DALLOC(e->en_acc, sizeof(EntryAcc));
@@ -480,6 +486,8 @@ int sf_load_system_rules(sf_engine* e, const sf_system_rule* rules, uint32_t n) 
     if (!e || (n && !rules)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     { const int rc = drain(e); if (rc) return rc; }
+    if (n && e->cfg.shard_count > 1)
+        return fail(SF_ERR_UNSUPPORTED, "SystemRule reads the node-wide ENTRY_NODE: not on a sharded engine");
     SysRule r{};
     r.qps = r.highest_load = r.highest_cpu = 1.7976931348623157e308;
     r.max_rt = r.max_thread = INT64_MAX;
@@ -1423,12 +1431,29 @@ static bool dg_valid(const sf_degrade_rule& r) {
     }
 }
 
+// DegradeRule.equals (DegradeRule.java:153-164, AbstractRule.equals :76-93):
+// resource, limitApp (always "default" here) and the six fields, doubles by
+// Double.compare (bit pattern; every NaN equal).
+static bool dg_same_double(double a, double b) {
+    if (a != a && b != b) return true;
+    int64_t x, y;
+    std::memcpy(&x, &a, 8); std::memcpy(&y, &b, 8);
+    return x == y;
+}
+static bool dg_rule_equal(const sf_degrade_rule& a, const sf_degrade_rule& b) {
+    return a.resource == b.resource && a.grade == b.grade && dg_same_double(a.count, b.count) &&
+           a.time_window_s == b.time_window_s && a.min_request_amount == b.min_request_amount &&
+           dg_same_double(a.slow_ratio_threshold, b.slow_ratio_threshold) && a.stat_interval_ms == b.stat_interval_ms;
+}
+
 int sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t n, uint32_t* n_loaded) {
     if (!e || (n && !rules)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     const int rc = drain(e);
     if (rc) return rc;
-    // buildCircuitBreakers (DegradeRuleManager.java:236-265): valid rules, list order per resource
+    // buildCircuitBreakers (DegradeRuleManager.java:236-265): valid rules, list order per resource.
+    // Everything is built in locals first; the engine's tables are swapped only
+    // after every check and allocation succeeded (a failed load keeps the old rules).
     std::vector<uint32_t> loc, valid;
     for (uint32_t i = 0; i < n; i++) {
         if (!dg_valid(rules[i])) continue;
@@ -1444,7 +1469,7 @@ int sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t n
     std::vector<uint32_t> rr_of(e->R, 0), off;
     std::vector<DevBreakerRule> dr(nv);
     std::vector<sf_breaker_state> st(nv);
-    e->dg_pos.assign(nv, 0);
+    std::vector<uint32_t> pos(nv, 0);
     uint32_t n_rres = 0;
     for (uint32_t p = 0; p < nv; p++) {
         const uint32_t v = order[p];
@@ -1452,40 +1477,69 @@ int sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t n
             off.push_back(p);
             n_rres++;
         }
-        if (p > 0 && loc[order[p - 1]] == loc[v] && p - off.back() >= SF_MAX_BREAKERS_PER_RESOURCE)
+        if (p - off.back() >= SF_MAX_BREAKERS_PER_RESOURCE)
             return fail(SF_ERR_UNSUPPORTED, "more than SF_MAX_BREAKERS_PER_RESOURCE degrade rules on one resource");
         const sf_degrade_rule& r = rules[valid[v]];
         DevBreakerRule& d = dr[p];
         d.grade = r.grade;
         d.min_req = r.min_request_amount;
-        d.max_rt = (int64_t)std::floor(r.count + 0.5);           // Math.round (ResponseTimeCircuitBreaker.java:52)
+        d.max_rt = j_round(r.count);                             // Math.round (ResponseTimeCircuitBreaker.java:52)
         d.thr = r.grade == SF_DEGRADE_GRADE_RT ? r.slow_ratio_threshold : r.count;
         d.recovery = (int64_t)r.time_window_s * 1000;
         d.interval = r.stat_interval_ms;
         st[p] = sf_breaker_state{SF_CB_CLOSED, 0, 0, DG_WS_NONE, 0, 0};
-        e->dg_pos[v] = p;
+        pos[v] = p;
     }
     off.push_back(nv);
     for (auto& x : rr_of) x = n_rres;
     for (uint32_t k = 0; k < n_rres; k++) rr_of[loc[order[off[k]]]] = k;
+    // getExistingSameCbOrNew (DegradeRuleManager.java:151-163): a rule equal to
+    // one of the resource's current breakers keeps that breaker and its state.
+    // The reference hands the SAME breaker object to two equal new rules of one
+    // resource; that aliasing is refused rather than approximated.
+    if (nv && !e->dg_rules.empty()) {
+        std::vector<sf_breaker_state> old(e->dg_rules.size());
+        for (size_t k = 0; k < old.size(); k++)
+            HIP_TRY(hipMemcpy(&old[k], e->dg.state + e->dg_pos[k], sizeof(sf_breaker_state), hipMemcpyDeviceToHost));
+        std::vector<uint8_t> taken(old.size(), 0);
+        for (uint32_t v = 0; v < nv; v++) {
+            const sf_degrade_rule& r = rules[valid[v]];
+            for (size_t k = 0; k < old.size(); k++) {
+                if (!dg_rule_equal(r, e->dg_rules[k])) continue;
+                if (taken[k])
+                    return fail(SF_ERR_UNSUPPORTED, "two equal degrade rules would share one existing breaker");
+                taken[k] = 1;
+                st[pos[v]] = old[k];
+                break;
+            }
+        }
+    }
+    uint32_t *d_rr = nullptr, *d_off = nullptr;
+    DevBreakerRule* d_rules = nullptr;
+    sf_breaker_state* d_st = nullptr;
+    auto release = [&]() {
+        void* p[] = {d_rr, d_off, d_rules, d_st};
+        for (void* x : p) if (x) hipFree(x);
+    };
+    if (dalloc((void**)&d_rr, (size_t)e->R * 4) || dalloc((void**)&d_off, off.size() * 4) ||
+        dalloc((void**)&d_rules, (size_t)nv * sizeof(DevBreakerRule)) ||
+        dalloc((void**)&d_st, (size_t)nv * sizeof(sf_breaker_state))) {
+        release();
+        return SF_ERR_NOMEM;
+    }
+    hipError_t he = hipMemcpy(d_rr, rr_of.data(), (size_t)e->R * 4, hipMemcpyHostToDevice);
+    if (he == hipSuccess) he = hipMemcpy(d_off, off.data(), off.size() * 4, hipMemcpyHostToDevice);
+    if (he == hipSuccess && nv) he = hipMemcpy(d_rules, dr.data(), (size_t)nv * sizeof(DevBreakerRule), hipMemcpyHostToDevice);
+    if (he == hipSuccess && nv) he = hipMemcpy(d_st, st.data(), (size_t)nv * sizeof(sf_breaker_state), hipMemcpyHostToDevice);
+    if (he != hipSuccess) { release(); return fail(SF_ERR_DEVICE, std::string("degrade rule upload: ") + hipGetErrorString(he)); }
     void* dptrs[] = {(void*)e->dg.rr_of, (void*)e->dg.off, (void*)e->dg.rules, e->dg.state};
     for (void* p : dptrs) if (p) hipFree(p);
     e->dg = DegradeDev{};
-    uint32_t *d_rr, *d_off;
-    DevBreakerRule* d_rules;
-    sf_breaker_state* d_st;
-    if (dalloc((void**)&d_rr, (size_t)e->R * 4) || dalloc((void**)&d_off, off.size() * 4) ||
-        dalloc((void**)&d_rules, (size_t)nv * sizeof(DevBreakerRule)) ||
-        dalloc((void**)&d_st, (size_t)nv * sizeof(sf_breaker_state)))
-        return SF_ERR_NOMEM;
-    HIP_TRY(hipMemcpy(d_rr, rr_of.data(), (size_t)e->R * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_off, off.data(), off.size() * 4, hipMemcpyHostToDevice));
-    if (nv) {
-        HIP_TRY(hipMemcpy(d_rules, dr.data(), (size_t)nv * sizeof(DevBreakerRule), hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(d_st, st.data(), (size_t)nv * sizeof(sf_breaker_state), hipMemcpyHostToDevice));
-    }
     e->dg.rr_of = d_rr; e->dg.off = d_off; e->dg.rules = d_rules; e->dg.state = d_st;
     e->dg.n_rres = n_rres;
+    e->dg_pos = pos;
+    e->dg_rules.clear();
+    for (uint32_t v = 0; v < nv; v++) e->dg_rules.push_back(rules[valid[v]]);
     uint32_t kb = 1;
     while ((1ull << kb) <= n_rres) kb++;                        // keys 0..n_rres (n_rres = no breaker)
     e->dg.key_bits = kb;
@@ -1547,6 +1601,7 @@ int sf_degrade_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) 
     hipStream_t s = e->stream;
     DegradeBatch b{};
     b.n = n; b.shard_count = e->cfg.shard_count; b.shard_index = e->cfg.shard_index; b.R = e->R;
+    b.last_ts = e->st.last_ts;
     uint8_t* status = out->status;
     uint16_t* rule = out->rule_idx;
     int32_t* wait = out->wait_ms;
@@ -1601,6 +1656,7 @@ int sf_degrade_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) 
     HIP_TRY(hipStreamSynchronize(s));
     if (err & 1) return fail(SF_ERR_INVALID, "event resource outside this shard");
     if (err & 2) return fail(SF_ERR_INVALID, "EXIT without a valid entry_ref or create_ts");
+    if (err & 4) return fail(SF_ERR_INVALID, "event times must be non-decreasing (within and across batches)");
     return SF_OK;
 }
 

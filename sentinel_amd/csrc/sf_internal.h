@@ -77,6 +77,7 @@ struct DevState {
     uint64_t pcap_mask;
     int32_t* err;                  // device error word (capacity, invalid input)
     int64_t* last_fetch;           // [R] StatisticNode.lastFetchTime (metric snapshot)
+    int64_t* last_ts;              // engine clock: last event time of the previous batch (time never goes back)
 };
 
 // Constants.ENTRY_NODE (Constants.java:66): the ClusterNode of all inbound

@@ -45,12 +45,15 @@ __global__ void k_init_state(DevState st, size_t n_sec, size_t n_min) {
 // its first event (never for a time-ordered batch shorter than 49 days) sets
 // *wide and k_unpack reads those times from the batch instead.
 __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t shard_count, uint32_t shard_index,
-                              uint32_t R, int32_t* err, uint32_t* wide) {
+                              uint32_t R, int32_t* err, uint32_t* wide, const int64_t* last_ts) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;
     uint32_t r = b.res[i];
     uint32_t l = r / shard_count;
     if (r % shard_count != shard_index || l >= R) { *err = SF_ERR_INVALID; l = 0; }
+    // the mocked clock never goes back: within the batch and across batches
+    // (LeapArray would hand such an event a throwaway window)
+    if (b.ts[i] < (i ? b.ts[i - 1] : *last_ts)) *err = SF_ERR_INVALID;
     keys[i] = l;
     const int64_t d = b.ts[i] - b.ts[0];
     if (d < 0 || d > (int64_t)0xffffffffLL) *wide = 1u;
@@ -61,9 +64,11 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t
 
 __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* wide, uint32_t* perm, int64_t* s_ts,
                          int32_t* s_cnt, uint8_t* s_flags, uint8_t* s_nargs, uint8_t* s_atag,
-                         uint64_t* s_abits, const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag) {
+                         uint64_t* s_abits, const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag,
+                         int64_t* last_ts) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
+    if (j == 0) *last_ts = b.ts[b.n - 1];        // k_keys_packed of this batch has read the old value
     const PackedEv v = pv[j];
     const uint32_t i = v.idx;
     const int32_t c = v.cnt;
@@ -690,7 +695,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     hipError_t e;
     hipMemsetAsync(w.wide, 0, 4, s);
     hipLaunchKernelGGL(k_keys_packed, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.pv_in, shard_count,
-                       shard_index, st.R, st.err, w.wide);
+                       shard_index, st.R, st.err, w.wide, st.last_ts);
     e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.pv_in, w.pv_out, n, 0u,
                                   key_bits, s);
     if (e != hipSuccess) return e;
@@ -702,7 +707,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
                        w.seg_start, w.seg_res, w.n_seg, w.segflag);
     if (timing) hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.wide, w.perm, w.s_ts, w.s_cnt,
-                       w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag);
+                       w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag, st.last_ts);
     hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags, w.head,

@@ -138,6 +138,7 @@ def test_oracle_state_machine_details():
         s = o.state(k)
         assert s["state"] == od.CLOSED and s["hit_count"] == 0 and s["total_count"] == 0
     # exit of a blocked entry records nothing (DegradeSlot.java:72-77)
+    o = od.DegradeOracle()
     o.load_rules([r0])
     o.submit([RES, RES], [0, 1], [0, od.EV_EXIT | od.EV_ERROR], [-1, 0])
     st, _ = o.submit([RES, RES], [2, 3], [0, od.EV_EXIT | od.EV_ERROR], [-1, 0])
@@ -155,6 +156,49 @@ def test_oracle_rule_validity():
     assert not od.is_valid_rule(abi.degrade_rule(1, abi.DEGRADE_GRADE_EXCEPTION_RATIO, 1.5, 1))
     assert od.is_valid_rule(abi.degrade_rule(1, abi.DEGRADE_GRADE_EXCEPTION_COUNT, 1.5, 1))
     assert od.java_round(10.5) == 11 and od.java_round(-10.5) == -10 and od.java_round(2.4999) == 2
+
+
+def test_java_round_edges():
+    """Math.round(double) is the exact floor(x + 1/2), saturated (JDK 7+):
+    floor(x + 0.5) in double arithmetic gets 0.49999999999999994 wrong."""
+    assert od.java_round(0.49999999999999994) == 0
+    assert od.java_round(-0.5) == 0 and od.java_round(-0.5000000000000001) == -1
+    assert od.java_round(4503599627370497.0) == 4503599627370497        # 2^52 + 1: no +0.5 rounding up
+    assert od.java_round(1e19) == (1 << 63) - 1 and od.java_round(-1e19) == -(1 << 63)
+    assert od.java_round(float("nan")) == 0 and od.java_round(float("inf")) == (1 << 63) - 1
+    # an RT breaker with count 0.49999999999999994 treats rt = 1 as slow (maxAllowedRt 0)
+    r = abi.degrade_rule(RES, abi.DEGRADE_GRADE_RT, 0.49999999999999994, 1, min_request_amount=1)
+    assert od.Breaker(r).max_rt == 0
+
+
+def reload_script():
+    """A rule reload that keeps an unchanged rule keeps its breaker, OPEN state
+    and retry time included (DegradeRuleManager.getExistingSameCbOrNew
+    :151-163); a changed rule starts CLOSED."""
+    r0 = abi.degrade_rule(RES, abi.DEGRADE_GRADE_EXCEPTION_COUNT, 0, 5, min_request_amount=1)
+    r1 = abi.degrade_rule(RES + 1, abi.DEGRADE_GRADE_EXCEPTION_COUNT, 0, 5, min_request_amount=1)
+    b1 = abi.HostBatch(np.array([RES, RES, RES + 1, RES + 1]), np.array([0, 3, 4, 6]), np.ones(4, np.int32),
+                       np.array([0, od.EV_EXIT | od.EV_ERROR, 0, od.EV_EXIT | od.EV_ERROR], np.uint8),
+                       entry_ref=np.array([-1, 0, -1, 2]))
+    r1b = dict(r1, min_request_amount=2)                  # changed: a new breaker
+    b2 = abi.HostBatch(np.array([RES, RES + 1]), np.array([100, 101]), np.ones(2, np.int32),
+                       np.array([0, 0], np.uint8), entry_ref=np.array([-1, -1]))
+    return [r0, r1], b1, [r1b, r0], b2
+
+
+def test_oracle_reload_keeps_unchanged_breaker():
+    rules1, b1, rules2, b2 = reload_script()
+    o = od.DegradeOracle()
+    o.load_rules(rules1)
+    o.submit(b1.res_id, b1.ts_ms, b1.flags, b1.entry_ref)
+    assert o.state(0)["state"] == od.OPEN and o.state(1)["state"] == od.OPEN
+    o.load_rules(rules2)
+    assert o.state(1)["state"] == od.OPEN and o.state(1)["next_retry_ms"] == 5003    # r0, now second
+    assert o.state(0)["state"] == od.CLOSED                                          # r1 changed
+    st, _ = o.submit(b2.res_id, b2.ts_ms, b2.flags, b2.entry_ref)
+    assert list(st) == [od.V_BLOCK_DEGRADE, od.V_PASS]
+    with pytest.raises(ValueError):
+        o.load_rules([rules2[1], dict(rules2[1])])          # equal rules would share one breaker
 
 
 def test_workload_generator_shape():
@@ -253,9 +297,64 @@ def test_gpu_no_rules_and_sharding():
 
 
 @pytest.mark.gpu
+def test_gpu_reload_keeps_unchanged_breaker():
+    from sentinel_amd import engine
+    rules1, b1, rules2, b2 = reload_script()
+    o = od.DegradeOracle()
+    o.load_rules(rules1)
+    e = _engine(4, 16)
+    try:
+        e.load_degrade_rules(rules1)
+        st, _ = o.submit(b1.res_id, b1.ts_ms, b1.flags, b1.entry_ref)
+        assert np.array_equal(e.degrade_submit(b1).status, st)
+        o.load_rules(rules2)
+        e.load_degrade_rules(rules2)
+        for k in range(2):
+            assert e.read_breaker(k) == o.state(k), k
+        st, _ = o.submit(b2.res_id, b2.ts_ms, b2.flags, b2.entry_ref)
+        assert np.array_equal(e.degrade_submit(b2).status, st)
+        with pytest.raises(engine.EngineError):
+            e.load_degrade_rules([rules2[1], dict(rules2[1])])
+        for k in range(2):                                  # the failed load changed nothing
+            assert e.read_breaker(k) == o.state(k), k
+    finally:
+        e.close()
+
+
+@pytest.mark.gpu
+def test_gpu_bad_exit_refs_and_clock():
+    """An EXIT whose entry_ref names another resource's event, an exit, or a
+    later event is refused (SF_ERR_INVALID), as is a clock that goes back
+    (within a batch or against the previous batch)."""
+    from sentinel_amd import engine
+    rules = [abi.degrade_rule(r, abi.DEGRADE_GRADE_EXCEPTION_COUNT, 0, 5, min_request_amount=1) for r in range(2)]
+    ok = abi.HostBatch(np.array([0, 1, 0, 1]), np.array([10, 11, 12, 13]), np.ones(4, np.int32),
+                       np.array([0, 0, od.EV_EXIT, od.EV_EXIT], np.uint8), entry_ref=np.array([-1, -1, 0, 1]))
+    bads = [np.array([-1, -1, 1, 1]), np.array([-1, -1, 3, 1]), np.array([-1, -1, 0, 2])]
+    for eref in bads:
+        e = _engine(4, 16)
+        try:
+            e.load_degrade_rules(rules)
+            with pytest.raises(engine.EngineError):
+                e.degrade_submit(abi.HostBatch(ok.res_id, ok.ts_ms, ok.count, ok.flags, entry_ref=eref))
+        finally:
+            e.close()
+    e = _engine(4, 16)
+    try:
+        e.load_degrade_rules(rules)
+        e.degrade_submit(ok)
+        with pytest.raises(engine.EngineError):                       # earlier than the last batch
+            e.degrade_submit(abi.HostBatch(ok.res_id, ok.ts_ms - 5, ok.count, ok.flags, entry_ref=ok.entry_ref))
+        with pytest.raises(engine.EngineError):                       # backwards inside the batch
+            e.degrade_submit(abi.HostBatch(ok.res_id, ok.ts_ms[::-1] + 100, ok.count, np.zeros(4, np.uint8)))
+    finally:
+        e.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", [4, 5])
 def test_gpu_long_segments(seed):
-    """Few resources, thousands of events each: the wave walk (segments > 512
+    """Few resources, thousands of events each: the wave walk (segments > 64
     events, <= 4 breakers), its chunk boundaries and tail chunks; resource 0
     carries 5 breakers and stays on the lane walk."""
     R = 16
