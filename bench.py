@@ -41,8 +41,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--resources", type=int, default=10_000_000)
     ap.add_argument("--events", type=int, default=1 << 27)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 26, help="events replayed by the CPU oracle (about 15 s on one core)")
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the whole-batch oracle replay (parity + cpu_baseline)")
     ap.add_argument("--no-metric-log", action="store_true")
     ap.add_argument("--no-degrade", action="store_true")
     args = ap.parse_args()
@@ -72,19 +71,19 @@ def main():
     eng = engine.FlowEngine(cfg)
     eng.load_flow_rules(rules)
     steps = args.warmup + args.steps
-    # one device-resident copy of the batch per step, timestamps shifted so
-    # consecutive batches continue the same trace
-    batches = []
-    for k in range(steps):
-        shifted = abi.HostBatch(hb.res_id, hb.ts_ms + k * DURATION_MS, hb.count, hb.flags, entry_ref=hb.entry_ref)
-        batches.append(engine.DeviceBatch(eng, shifted))
+    # the batch resident in HBM once per step: timestamps shifted so that
+    # consecutive batches continue the same trace (every other array shared)
+    base = engine.DeviceBatch(eng, hb)
+    batches = [base] + [engine.DeviceBatch.with_ts(eng, base, hb.ts_ms + k * DURATION_MS) for k in range(1, steps)]
     out = engine.DeviceVerdicts(eng, hb.n, with_wait=True, with_rule=False)
+    out0 = engine.DeviceVerdicts(eng, hb.n, with_wait=True, with_rule=True)
     log(f"[rank {rank}] staged {steps} batches in HBM, t={time.time()-t0:.1f}s")
 
     # batches are enqueued (sf_submit_async): the engine sorts batch k+1 on
-    # its sort stream while it decides batch k; decisions stay in batch order
+    # its sort stream while it decides batch k; decisions stay in batch order.
+    # Batch 0 (fresh engine) keeps its verdicts for the whole-batch parity check.
     for k in range(args.warmup):
-        eng.submit_device_async(batches[k], out)
+        eng.submit_device_async(batches[k], out0 if k == 0 else out)
     eng.sync()
     eng.set_timing(True)
     if dist:
@@ -153,12 +152,14 @@ def main():
     # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
     # passes of this same command (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)
     traffic, traffic_src = None, None
-    prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_config3_summary.json")
-    if os.path.exists(prof):
+    import glob
+    profs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_config3_summary.json")))
+    prof = profs[-1] if profs else ""
+    if prof:
         with open(prof) as fh:
             for kr in json.load(fh).get("kernels", []):
                 if kr["kernel"].split("<")[0] == name and kr.get("hbm_bytes_per_launch") is not None:
-                    traffic, traffic_src = int(kr["hbm_bytes_per_launch"]), "profiles/r01_config3_summary.json"
+                    traffic, traffic_src = int(kr["hbm_bytes_per_launch"]), os.path.relpath(prof, ROOT)
     roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "traffic_source": traffic_src,
@@ -219,9 +220,11 @@ def main():
         except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
             degrade = {"error": str(ex)[:200]}
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(rules, hb, R_local, args.cpu_sample)
+    # whole-batch parity (batch 0 from a fresh engine vs the oracle replaying
+    # the same batch) -- the same replay, timed, is the CPU baseline
+    cpu, parity = None, None
+    if rank == 0 and world == 1 and not args.no_cpu and args.warmup > 0:
+        cpu, parity = oracle_leg(rules, hb, R_local, out0)
 
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
@@ -233,11 +236,12 @@ def main():
                            "resources": R_total, "events_per_batch_per_gpu": hb.n, "entries_per_batch_per_gpu": n_entry,
                            "resources_touched": n_seg, "pass_fraction": round(n_pass / max(1, n_entry), 4),
                            "parallelism": f"resource-sharded x{world}"},
-                "roofline": roofline, "cpu_baseline": cpu, "aggregate": aggregate,
+                "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "aggregate": aggregate,
                 "metric_log": metric_log, "degrade": degrade}
         print(json.dumps(line), flush=True)
-    for b in batches:
+    for b in batches[1:]:
         b.free()
+    base.free()
     if dist:
         dist.destroy_process_group()
 
@@ -252,14 +256,22 @@ def degrade_leg(R=1_000_000, entries=1 << 22, steps=3):
     try:
         n_cb = e.load_degrade_rules(rules)
         db = engine.DeviceBatch(e, b)
+        # every step replays the trace from fresh breakers (an empty load drops
+        # them; an equal rule would keep its breaker), shifted by a multiple of
+        # every stat interval so the clock moves forward and verdicts repeat
+        span = (int(b.ts_ms[-1] - b.ts_ms[0]) // 60_000 + 2) * 60_000
+        dbs = [engine.DeviceBatch.with_ts(e, db, b.ts_ms + k * span) for k in range(1, steps + 1)]
         dv = engine.DeviceVerdicts(e, b.n, with_wait=False, with_rule=True)
         e.degrade_submit_device(db, dv)
         wall = []
-        for _ in range(steps):
+        for k in range(steps):
+            e.load_degrade_rules([])
             e.load_degrade_rules(rules)
             t = time.perf_counter()
-            e.degrade_submit_device(db, dv)
+            e.degrade_submit_device(dbs[k], dv)
             wall.append(time.perf_counter() - t)
+        for x in dbs:
+            x.free()
         ms = float(np.median(wall)) * 1e3
         st = dv.status.numpy()
         db.free()
@@ -305,27 +317,35 @@ def metric_log_leg(eng, hb, R_total, R_local, world, rank, steps):
             "sample_line": data[:data.find(b"\n")].decode(errors="replace") if data else ""}
 
 
-def cpu_baseline(rules, hb, R, sample):
-    """The C restatement (oracle/, test infrastructure) replaying the first
-    ``sample`` events of the same batch on one host core."""
+def oracle_leg(rules, hb, R, out0):
+    """The C restatement (oracle/, test infrastructure) replays the whole
+    batch 0 on one host core from fresh state: its verdicts are compared with
+    the GPU's verdicts of that batch (status, wait, rule index: parity), and
+    its time is the CPU baseline."""
     try:
         from oracle import oracle as so
     except Exception as ex:  # pragma: no cover
-        return {"error": str(ex)}
-    n = min(sample, hb.n)
-    sub = hb.subset(0, n)
-    ora = so.OracleEngine(abi.default_config(max_resources=R, max_batch=n))
+        return {"error": str(ex)}, {"error": str(ex)}
+    ora = so.OracleEngine(abi.default_config(max_resources=R, max_batch=hb.n))
     t = time.perf_counter()
     ora.load_flow_rules(rules)
     t_load = time.perf_counter() - t
     t = time.perf_counter()
-    v = ora.submit(sub)
+    want = ora.submit(hb)
     dt = time.perf_counter() - t
-    ent = int(((sub.flags & abi.EV_EXIT) == 0).sum())
+    ent = int(((hb.flags & abi.EV_EXIT) == 0).sum())
     ora.close()
-    return {"value": round(ent / dt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
-            "sample": f"first {n} events ({ent} entries) of the same config-3 batch, single-threaded C oracle "
-                      f"(rule load {t_load:.1f}s excluded)", "seconds": round(dt, 2)}
+    st, wt, ru = out0.status.numpy(), out0.wait_ms.numpy(), out0.rule_idx.numpy()
+    blk = np.isin(want.status, [abi.V_BLOCK_FLOW, abi.V_BLOCK_PARAM, abi.V_BLOCK_SYSTEM])
+    mism = {"status": int((st != want.status).sum()), "wait_ms": int((wt != want.wait_ms).sum()),
+            "rule_idx_of_blocks": int((ru[blk] != want.rule_idx[blk]).sum())}
+    cpu = {"value": round(ent / dt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+           "sample": f"the whole batch 0 ({hb.n} events, {ent} entries) of the timed workload from fresh state, "
+                     f"single-threaded C oracle (rule load {t_load:.1f}s excluded)", "seconds": round(dt, 2)}
+    parity = {"what": "batch 0 of the timed run (fresh engine) vs the oracle replay of the same batch",
+              "events": int(hb.n), "mismatches": mism,
+              "exact": all(v == 0 for v in mism.values())}
+    return cpu, parity
 
 
 if __name__ == "__main__":

@@ -43,7 +43,8 @@ __global__ void __launch_bounds__(BLK) k_dg_keys(DegradeDev d, DegradeBatch b, u
     if (wait) wait[i] = 0;
 }
 
-__global__ void k_dg_clock(DegradeBatch b) { *b.last_ts = b.ts[b.n - 1]; }
+// a refused batch (bad shard, clock, refs) does not advance the engine clock
+__global__ void k_dg_clock(DegradeBatch b, const int* err) { if (*err == 0) *b.last_ts = b.ts[b.n - 1]; }
 
 __global__ void __launch_bounds__(BLK) k_dg_bounds(const uint32_t* keys, uint32_t n, uint32_t none, uint32_t* beg,
                                                    uint32_t* end) {
@@ -457,7 +458,7 @@ hipError_t dg_launch(const DegradeDev& d, DegradeWork& w, const DegradeBatch& b,
                      int32_t* wait, hipStream_t s) {
     if (b.n == 0) return hipSuccess;
     k_dg_keys<<<blocks(b.n), BLK, 0, s>>>(d, b, w.keys_in, w.idx_in, status, rule, wait, w.err);
-    k_dg_clock<<<1, 1, 0, s>>>(b);
+    k_dg_clock<<<1, 1, 0, s>>>(b, w.err);
     if (d.n_rres == 0) return hipGetLastError();
     size_t bytes = w.sort_tmp_bytes;
     hipError_t e = rocprim::radix_sort_pairs(w.sort_tmp, bytes, w.keys_in, w.keys_out, w.idx_in, w.idx_out, b.n, 0u,

@@ -65,10 +65,10 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t
 __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* wide, uint32_t* perm, int64_t* s_ts,
                          int32_t* s_cnt, uint8_t* s_flags, uint8_t* s_nargs, uint8_t* s_atag,
                          uint64_t* s_abits, const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag,
-                         int64_t* last_ts) {
+                         int64_t* last_ts, const int32_t* err) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
-    if (j == 0) *last_ts = b.ts[b.n - 1];        // k_keys_packed of this batch has read the old value
+    if (j == 0 && *err == 0) *last_ts = b.ts[b.n - 1];   // k_keys_packed of this batch has read the old value
     const PackedEv v = pv[j];
     const uint32_t i = v.idx;
     const int32_t c = v.cnt;
@@ -707,7 +707,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
                        w.seg_start, w.seg_res, w.n_seg, w.segflag);
     if (timing) hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.wide, w.perm, w.s_ts, w.s_cnt,
-                       w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag, st.last_ts);
+                       w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag, st.last_ts, st.err);
     hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags, w.head,

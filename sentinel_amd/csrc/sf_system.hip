@@ -1,0 +1,215 @@
+// sf_system.hip — the SystemRule safe-prefix planner on the GPU (product code).
+//
+// One sys_plan call plans the events from p: it finds the ENTRY_NODE bucket
+// window of event p, bounds the ENTRY_NODE statistics at every IN entry of
+// [p, min(window end, p + SP_CAP)) (sf_system.h), writes the forced system
+// verdict of every entry whose five checks are all certain (mask: reason, or
+// SYS_NONE for a certain pass) and returns q, the first IN entry whose
+// outcome depends on undecided events (or the end of that range).
+//
+// The bounds are prefix sums in submission order: an exit-side prefix
+// (independent of any classification) and an entry-side prefix (entries not
+// certainly blocked, which depends on the exit side only).  Three passes of
+// 4096-event blocks: A sums the exit side per block, B sums the entry side
+// (classifying with A's prefix), C classifies every entry with both.  A
+// block's prefix is the sum of the earlier blocks' totals (at most SP_NB
+// partials, summed by the block itself: no separate scan launch).
+#include "sf_system.h"
+
+namespace sf {
+
+constexpr int SP_T = 256, SP_RUN = 16, SP_BLK = SP_T * SP_RUN;   // 4096 events per block
+constexpr uint32_t SP_NB = 512;                                   // blocks per plan
+constexpr uint32_t SP_CAP = SP_NB * SP_BLK;                       // 2 Mi events per plan
+
+struct SysPlanArgs {
+    const int64_t* ts; const int32_t* cnt; const uint8_t* flags; const int64_t* eref; const int64_t* cts;
+    const uint8_t* vstatus;                 // verdicts of the whole batch (events before p are decided)
+    uint8_t* mask;                          // out: forced reason / SYS_NONE per IN entry of [p, q)
+    uint32_t n, p;
+    SysRule r;
+    int32_t S, wl, interval;
+    int64_t max_rt;                         // statisticMaxRt (empty-window minRt)
+    double interval_sec;
+    SysPlanDev* plan;
+    SysExitQ* pa; SysEntQ* pb;              // [SP_NB] block totals
+};
+
+__global__ void k_sp_init(SysPlanArgs a, const EntryNode* en) {
+    if (threadIdx.x != 0) return;
+    SysPlanDev& pl = *a.plan;
+    const int64_t t = a.ts[a.p];
+    const int64_t end = t - t % a.wl + a.wl;
+    uint32_t lo = a.p, hi = a.n;                 // first index with ts >= end
+    while (lo < hi) { const uint32_t m = lo + (hi - lo) / 2; if (a.ts[m] >= end) hi = m; else lo = m + 1; }
+    pl.wend = lo;
+    pl.lim = min(lo, a.p + SP_CAP);
+    pl.first_unc = pl.lim;
+    pl.base = sys_base(en->second, a.S, a.wl, a.interval, a.max_rt, en->threads, t);
+}
+
+// block-wide inclusive scan of a struct with clear()/add() (Hillis-Steele in LDS)
+template <class Q>
+__device__ Q block_scan_incl(Q v, Q* lds) {
+    const int t = threadIdx.x;
+    lds[t] = v;
+    __syncthreads();
+    for (int d = 1; d < SP_T; d <<= 1) {
+        Q o;
+        o.clear();
+        if (t >= d) o = lds[t - d];
+        __syncthreads();
+        if (t >= d) { v.add(o); lds[t] = v; }
+        __syncthreads();
+    }
+    return v;
+}
+
+// sum of the totals of the blocks before block k
+template <class Q>
+__device__ Q block_prefix(const Q* tot, uint32_t k, Q* lds) {
+    Q v;
+    v.clear();
+    for (uint32_t j = threadIdx.x; j < k; j += SP_T) v.add(tot[j]);
+    v = block_scan_incl(v, lds);
+    __shared__ Q res;
+    if (threadIdx.x == SP_T - 1) res = v;
+    __syncthreads();
+    Q r = res;
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ SysExitQ exit_q(const SysPlanArgs& a, uint32_t i) {
+    return sys_exit_q(a.ts, a.cnt, a.flags, a.eref, a.cts, a.vstatus, a.p, i, a.r.max_rt);
+}
+__device__ __forceinline__ bool in_entry(const SysPlanArgs& a, uint32_t i) {
+    const uint8_t f = a.flags[i];
+    return (f & SF_EV_IN) && !(f & SF_EV_EXIT);
+}
+
+__global__ void __launch_bounds__(SP_T) k_sp_a(SysPlanArgs a) {
+    __shared__ SysExitQ lds[SP_T];
+    const SysPlanDev& pl = *a.plan;
+    const uint32_t b0 = a.p + blockIdx.x * SP_BLK;
+    if (b0 >= pl.lim) return;
+    const uint32_t r0 = b0 + threadIdx.x * SP_RUN, r1 = min(r0 + SP_RUN, pl.lim);
+    SysExitQ v;
+    v.clear();
+    for (uint32_t i = r0; i < r1; i++) v.add(exit_q(a, i));
+    v = block_scan_incl(v, lds);
+    if (threadIdx.x == SP_T - 1) a.pa[blockIdx.x] = v;
+}
+
+// entry-side contribution of IN entry i with exit-side prefix x
+__device__ __forceinline__ SysEntQ ent_q(const SysPlanArgs& a, const SysBase& base, const SysExitQ& x, uint32_t i) {
+    SysEntQ e;
+    e.clear();
+    const int32_t c = a.cnt[i];
+    SysEntQ none;
+    none.clear();
+    bool fire = false;
+    sys_classify(a.r, base, a.S, a.interval_sec, x, none, c, &fire);
+    if (!fire) { e.nb = 1; e.nb_c = c > 0 ? c : 0; e.nb_neg = c < 0 ? 1 : 0; }
+    return e;
+}
+
+__global__ void __launch_bounds__(SP_T) k_sp_b(SysPlanArgs a) {
+    __shared__ SysExitQ ldsx[SP_T];
+    __shared__ SysEntQ ldse[SP_T];
+    const SysPlanDev& pl = *a.plan;
+    const uint32_t b0 = a.p + blockIdx.x * SP_BLK;
+    if (b0 >= pl.lim) return;
+    const SysBase base = pl.base;
+    const uint32_t r0 = b0 + threadIdx.x * SP_RUN, r1 = min(r0 + SP_RUN, pl.lim);
+    SysExitQ x = block_prefix(a.pa, blockIdx.x, ldsx);
+    SysExitQ run;
+    run.clear();
+    for (uint32_t i = r0; i < r1; i++) run.add(exit_q(a, i));
+    SysExitQ incl = block_scan_incl(run, ldsx);
+    // exclusive prefix of this thread's run: block prefix + (inclusive - own)
+    SysExitQ ex;
+    ex.clear();
+    if (threadIdx.x > 0) ex = ldsx[threadIdx.x - 1];
+    __syncthreads();
+    x.add(ex);
+    (void)incl;
+    SysEntQ e;
+    e.clear();
+    for (uint32_t i = r0; i < r1; i++) {
+        if (in_entry(a, i)) e.add(ent_q(a, base, x, i));
+        x.add(exit_q(a, i));
+    }
+    e = block_scan_incl(e, ldse);
+    if (threadIdx.x == SP_T - 1) a.pb[blockIdx.x] = e;
+}
+
+__global__ void __launch_bounds__(SP_T) k_sp_c(SysPlanArgs a) {
+    __shared__ SysExitQ ldsx[SP_T];
+    __shared__ SysEntQ ldse[SP_T];
+    SysPlanDev& pl = *a.plan;
+    const uint32_t b0 = a.p + blockIdx.x * SP_BLK;
+    if (b0 >= pl.lim) return;
+    const SysBase base = pl.base;
+    const uint32_t r0 = b0 + threadIdx.x * SP_RUN, r1 = min(r0 + SP_RUN, pl.lim);
+    SysExitQ x = block_prefix(a.pa, blockIdx.x, ldsx);
+    SysEntQ en = block_prefix(a.pb, blockIdx.x, ldse);
+    SysExitQ run;
+    run.clear();
+    for (uint32_t i = r0; i < r1; i++) run.add(exit_q(a, i));
+    block_scan_incl(run, ldsx);
+    SysExitQ ex;
+    ex.clear();
+    if (threadIdx.x > 0) ex = ldsx[threadIdx.x - 1];
+    __syncthreads();
+    x.add(ex);
+    // entry-side run partial, then its exclusive prefix
+    SysExitQ xw = x;
+    SysEntQ erun;
+    erun.clear();
+    for (uint32_t i = r0; i < r1; i++) {
+        if (in_entry(a, i)) erun.add(ent_q(a, base, xw, i));
+        xw.add(exit_q(a, i));
+    }
+    block_scan_incl(erun, ldse);
+    SysEntQ eex;
+    eex.clear();
+    if (threadIdx.x > 0) eex = ldse[threadIdx.x - 1];
+    __syncthreads();
+    en.add(eex);
+    // classify
+    for (uint32_t i = r0; i < r1; i++) {
+        if (in_entry(a, i)) {
+            const int32_t c = a.cnt[i];
+            bool fire = false;
+            const int res = sys_classify(a.r, base, a.S, a.interval_sec, x, en, c, &fire);
+            if (res == -1) { atomicMin(&pl.first_unc, i); break; }
+            a.mask[i] = res >= 0 ? (uint8_t)res : SYS_NONE;
+            if (!fire) { en.nb++; en.nb_c = wadd(en.nb_c, c > 0 ? c : 0); en.nb_neg += c < 0 ? 1 : 0; }
+        }
+        x.add(exit_q(a, i));
+    }
+}
+
+__global__ void k_sp_done(SysPlanDev* pl) {
+    if (threadIdx.x == 0) pl->q = min(pl->first_unc, pl->lim);
+}
+
+hipError_t sys_plan(const DevState& st, const DevBatch& b, const uint8_t* vstatus, uint8_t* mask, const SysRule& r,
+                    const EntryNode* en, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb, hipStream_t s) {
+    SysPlanArgs a;
+    a.ts = b.ts; a.cnt = b.cnt; a.flags = b.flags; a.eref = b.eref; a.cts = b.cts;
+    a.vstatus = vstatus; a.mask = mask; a.n = b.n; a.p = p; a.r = r;
+    a.S = st.S; a.wl = st.wl; a.interval = st.interval; a.max_rt = st.max_rt;
+    a.interval_sec = st.interval / 1000.0;
+    a.plan = plan; a.pa = pa; a.pb = pb;
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(SP_NB, ((uint64_t)(b.n - p) + SP_BLK - 1) / SP_BLK);
+    hipLaunchKernelGGL(k_sp_init, dim3(1), dim3(64), 0, s, a, en);
+    hipLaunchKernelGGL(k_sp_a, dim3(nb), dim3(SP_T), 0, s, a);
+    hipLaunchKernelGGL(k_sp_b, dim3(nb), dim3(SP_T), 0, s, a);
+    hipLaunchKernelGGL(k_sp_c, dim3(nb), dim3(SP_T), 0, s, a);
+    hipLaunchKernelGGL(k_sp_done, dim3(1), dim3(64), 0, s, plan);
+    return hipGetLastError();
+}
+
+}  // namespace sf

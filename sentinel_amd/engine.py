@@ -147,6 +147,19 @@ class DeviceBatch:
             self.arrays[k] = DeviceArray(eng, a) if a is not None else None
         self.arg_slots = 0 if hb.arg_tag is None else hb.arg_tag.shape[0]
 
+    @classmethod
+    def with_ts(cls, eng: "FlowEngine", base: "DeviceBatch", ts_ms: np.ndarray) -> "DeviceBatch":
+        """The events of ``base`` at other times: only the timestamps are
+        uploaded, every other array is shared with ``base`` (free() frees only
+        the timestamps)."""
+        self = cls.__new__(cls)
+        self.n = base.n
+        self.arg_slots = base.arg_slots
+        self.arrays = dict(base.arrays)
+        self.arrays["ts_ms"] = DeviceArray(eng, np.ascontiguousarray(ts_ms, dtype=np.int64))
+        self._owned = ("ts_ms",)
+        return self
+
     def c_struct(self) -> abi.sf_event_batch:
         b = abi.sf_event_batch()
         b.n, b.mem = self.n, abi.MEM_DEVICE
@@ -158,8 +171,9 @@ class DeviceBatch:
         return b
 
     def free(self):
-        for a in self.arrays.values():
-            if a is not None:
+        owned = getattr(self, "_owned", None)
+        for k, a in self.arrays.items():
+            if a is not None and (owned is None or k in owned):
                 a.free()
 
 

@@ -38,14 +38,18 @@ def main():
     n_cb = e.load_degrade_rules(rules)
     db = engine.DeviceBatch(e, b)
     dv = engine.DeviceVerdicts(e, b.n, with_wait=False, with_rule=True)
-    for _ in range(a.warmup):
-        e.degrade_submit_device(db, dv)
+    # every step replays the same trace from fresh breakers (an empty load drops
+    # them), shifted by a multiple of every stat interval: the clock moves forward
+    span = (int(b.ts_ms[-1] - b.ts_ms[0]) // 60_000 + 2) * 60_000
+    shifted = [engine.DeviceBatch.with_ts(e, db, b.ts_ms + k * span) for k in range(1, a.warmup + a.steps + 1)]
     wall = []
-    for _ in range(a.steps):
-        e.load_degrade_rules(rules)                  # every step replays the same trace from fresh breakers
+    for k, x in enumerate(shifted):
+        e.load_degrade_rules([])
+        e.load_degrade_rules(rules)
         t = time.perf_counter()
-        e.degrade_submit_device(db, dv)
-        wall.append(time.perf_counter() - t)
+        e.degrade_submit_device(x, dv)
+        if k >= a.warmup:
+            wall.append(time.perf_counter() - t)
     st = dv.status.numpy() if hasattr(dv, "status") else None
     ms = 1e3 * float(np.median(wall))
     counts = np.bincount(np.asarray(b.res_id, np.int64), minlength=R)
