@@ -302,6 +302,7 @@ typedef struct sf_stats {         /* device-clock timings, summed over sf_submit
     double   metric_scan_ms;      /* last sf_metric_log: k_mlog_count alone (every node's minute row) */
     double   metric_log_ms;       /* last sf_metric_log: all its kernels, before the copy to the host */
     double   wire_ms;             /* last sf_serve_frames: device time from framing to encoded responses (host syncs included) */
+    uint64_t sys_rounds;          /* SystemRule sub-batches (planner rounds) over the sf_submit calls */
 } sf_stats;
 
 typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last sf_submit */
@@ -506,6 +507,10 @@ int  sf_memcpy(sf_engine* e, void* dst, const void* src, size_t bytes, int kind 
 int  sf_sync(sf_engine* e);      /* waits for sf_submit_async batches; their first error */
 int  sf_get_stats(sf_engine* e, sf_stats* out);
 int  sf_set_timing(sf_engine* e, int enabled);
+/* diagnostics: the exact hot-parameter table (ParameterMetric maps): occupied
+ * slots, capacity, and the longest probe distance from a key's home slot
+ * (at most 4096: an insert that would go farther is SF_ERR_CAPACITY). */
+int  sf_param_table_stats(sf_engine* e, uint64_t* used, uint64_t* capacity, uint32_t* max_probe);
 /* diagnostics: per heavy segment of the last sf_submit (timing must be on) */
 int  sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uint32_t* n_out);
 

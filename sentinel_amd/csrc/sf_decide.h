@@ -380,13 +380,19 @@ SF_HD int can_pass(const DevRule& r, DevRuleState& s, NodeWin<MAXS>& nd, int64_t
 }
 
 // ============================================================ param table
+// Open addressing with linear probing, at most PT_MAX_PROBE slots from a
+// key's home: a key is never placed farther, so a lookup stops there too, and
+// an insert that finds no free slot in reach is SF_ERR_CAPACITY (the table is
+// too full for the configured param_capacity) instead of a scan of the table.
+constexpr uint64_t PT_MAX_PROBE = 4096;
 struct ParamTable {
     ParamSlot* slots; uint64_t mask; int32_t* err;
     SF_HD static uint64_t hash(uint64_t hi, uint64_t lo) { return mix64(hi ^ mix64(lo + 0x9e3779b97f4a7c15ULL)); }
     // find slot of key; returns nullptr if absent
     SF_HD ParamSlot* find(uint64_t hi, uint64_t lo) const {
         uint64_t i = hash(hi, lo) & mask;
-        for (uint64_t probe = 0; probe <= mask; probe++) {
+        const uint64_t reach = mask < PT_MAX_PROBE ? mask : PT_MAX_PROBE;
+        for (uint64_t probe = 0; probe <= reach; probe++) {
 #ifdef __HIP_DEVICE_COMPILE__
             uint64_t h = __hip_atomic_load(&slots[i].hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
@@ -401,7 +407,8 @@ struct ParamTable {
     // insert a key known to be absent (only the owning lane ever inserts a given key)
     SF_HD ParamSlot* insert(uint64_t hi, uint64_t lo) const {
         uint64_t i = hash(hi, lo) & mask;
-        for (uint64_t probe = 0; probe <= mask; probe++) {
+        const uint64_t reach = mask < PT_MAX_PROBE ? mask : PT_MAX_PROBE;
+        for (uint64_t probe = 0; probe <= reach; probe++) {
 #ifdef __HIP_DEVICE_COMPILE__
             unsigned long long expected = 0;
             if (__hip_atomic_compare_exchange_strong((unsigned long long*)&slots[i].hi, &expected,
@@ -516,37 +523,10 @@ SF_HD void emit_verdict(const SegIO& io, uint32_t j, uint8_t status, int32_t wai
 
 SF_HD bool v_blocked(uint8_t v) { return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM; }
 
-template <int MAXS> struct SysCtx { SysRule r; NodeWin<MAXS>* en; };   // en: Constants.ENTRY_NODE
-
-// SystemRuleManager.checkSystem :291-340 and checkBbr :342-348: -1 pass, else
-// the reason (0 qps, 1 thread, 2 rt, 3 load, 4 cpu).  Every read rolls the
-// ENTRY_NODE second window at `now`, like the reference's.
+// SystemRules: a SystemBlockException of an IN entry is decided by the
+// planner (sf_system.h) and arrives as EVF_SYSBLK on the event.
 template <int MAXS>
-SF_HD int sys_check(SysCtx<MAXS>& sc, int64_t now, int32_t count) {
-    if (!sc.r.check) return -1;
-    NodeWin<MAXS>& n = *sc.en;
-    const double qps = (double)n.sec_sum_pass(now) / n.interval_sec;                 // StatisticNode.passQps
-    if (qps + count > sc.r.qps) return 0;
-    const int32_t th = (int32_t)n.threads;                                           // curThreadNum
-    if (th > sc.r.max_thread) return 1;
-    const int64_t succ = n.sec_sum(now, [](const Bucket& b) { return b.succ; });
-    const double rt = succ == 0 ? 0.0
-                                : (double)n.sec_sum(now, [](const Bucket& b) { return b.rt; }) * 1.0 / (double)succ;
-    if (rt > (double)sc.r.max_rt) return 2;
-    if (sc.r.load_set && sc.r.cur_load > sc.r.highest_load) {
-        const double max_succ_qps = (double)n.sec_max_success(now) * n.S / n.interval_sec;
-        if (th > 1 && th > max_succ_qps * (double)n.sec_min_rt(now) / 1000) return 3;
-    }
-    if (sc.r.cpu_set && sc.r.cur_cpu > sc.r.highest_cpu) return 4;
-    return -1;
-}
-
-// SYS: time-ordered replay with SystemRules (the caller passes one event at a
-// time in submission order, validates exit references, and owns the global
-// ENTRY_NODE in sys->en).
-template <int MAXS, bool SYS = false>
-SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi,
-                          SysCtx<MAXS>* sys = nullptr) {
+SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi) {
     NodeWin<MAXS> nd;
     nd.S = st.S; nd.wl = st.wl; nd.interval = st.interval; nd.max_rt = st.max_rt;
     nd.interval_sec = st.interval / 1000.0;
@@ -582,7 +562,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
             int64_t ref = io.eref ? io.eref[j] : -1;
             bool blocked; int64_t create_ts;
             if (ref >= 0) {
-                if (!SYS && (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT))) {   // entry of another resource / order
+                if ((ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT))) {   // entry of another resource / order
                     *st.err = SF_ERR_INVALID;
 #if !defined(__HIP_DEVICE_COMPILE__) && defined(SF_HOST_DEBUG)
                     printf("bad ref j=%u ref=%lld lo=%u flags=%d\n", j, (long long)ref, lo, ref>=0? io.flags[ref]:-1);
@@ -592,17 +572,12 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
                 blocked = ref == (int64_t)j ? true : v_blocked(io.v_status[ref]);
                 create_ts = io.ts[ref];
             }
-            else { blocked = false; create_ts = io.cts ? io.cts[j] : now; }
+            else { blocked = ref == EREF_DEAD; create_ts = io.cts ? io.cts[j] : now; }
             if (!blocked) {
                 int64_t rt = now - create_ts;
                 nd.add_rt_success(now, rt, c);                  // recordCompleteFor :167-178
                 nd.threads--;
                 if (fl & SF_EV_ERROR) nd.add_exception(now, c);
-                if (SYS && (fl & SF_EV_IN)) {                   // Constants.ENTRY_NODE
-                    sys->en->add_rt_success(now, rt, c);
-                    sys->en->threads--;
-                    if (fl & SF_EV_ERROR) sys->en->add_exception(now, c);
-                }
                 if (pm_exists)                                  // ParamFlowStatisticExitCallback
                     for (uint32_t a = 0; a < na; a++)
                         if (a < 8 && (pm_init >> a) & 1)
@@ -620,9 +595,8 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
 
         bool blocked = false, prio_wait = false;
         status = SF_V_PASS;
-        if (SYS && (fl & SF_EV_IN)) {                           // SystemSlot -> SystemRuleManager.checkSystem
-            const int reason = sys_check(*sys, now, c);
-            if (reason >= 0) { blocked = true; status = SF_V_BLOCK_SYSTEM; rule_idx = reason; }
+        if (fl & EVF_SYSBLK) {                                  // SystemBlockException (planned, sf_system.h)
+            blocked = true; status = SF_V_BLOCK_SYSTEM; rule_idx = (fl >> EVF_SYSREASON_SHIFT) & 7;
         }
         // ParamFlowSlot.checkFlow :82-103
         if (!blocked && nprules) {
@@ -660,14 +634,11 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
         // StatisticSlot.entry accounting :64-123
         if (blocked) {
             nd.add_block(now, c);
-            if (SYS && (fl & SF_EV_IN)) sys->en->add_block(now, c);
         } else {
             nd.threads++;
-            if (SYS && (fl & SF_EV_IN)) sys->en->threads++;
             if (prio_wait) status = SF_V_PRIORITY_WAIT;
             else {
                 nd.add_pass(now, c); status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS;
-                if (SYS && (fl & SF_EV_IN)) sys->en->add_pass(now, c);
             }
             if (pm_exists)
                 for (uint32_t a = 0; a < na; a++)

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "sf_decide.h"
+#include "sf_system.h"
 #include "sf_token.h"
 #include "sf_wire.h"
 #include "sf_degrade.h"
@@ -49,7 +50,9 @@ struct sf_engine {
     unsigned pending = 0;           // Work sets with an asynchronous batch not yet checked by sf_sync
     bool used[2] = {false, false};
     hipEvent_t ev_sorted[2]{}, ev_done[2]{};
-    SysRule sys{};                  // SystemRuleManager statics; sys.check: batches replay in order
+    SysRule sys{};                  // SystemRuleManager statics; sys.check: batches go through the planner
+    SysPlanDev* sys_plan = nullptr; SysExitQ* sys_pa = nullptr; SysEntQ* sys_pb = nullptr;
+    uint8_t* sys_mask = nullptr;    // [max_batch] planner verdicts (sf_system.h)
     // rules
     std::vector<uint32_t> flow_pos;        // loaded valid rule index -> CSR position
     uint32_t n_flow = 0, n_prule = 0;
@@ -164,6 +167,8 @@ void sf_destroy(sf_engine* e) {
                      e->ml_order, e->ml_len, e->ml_off, e->ml_bytes, e->ml_out, e->ml_tmp};
     for (void* p : tptrs) if (p) hipFree(p);
     if (e->agg) hipFree(e->agg);
+    void* sptrs[] = {e->sys_plan, e->sys_pa, e->sys_pb, e->sys_mask};
+    for (void* p : sptrs) if (p) hipFree(p);
     void* dptrs[] = {(void*)e->dg.rr_of, (void*)e->dg.off, (void*)e->dg.rules, e->dg.state, e->dgw.keys_in,
                      e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
                      e->dgw.err, e->dg_stage, e->dgw.heavy, e->dgw.n_heavy, e->dgw.sev, e->dgw.inv};
@@ -598,21 +603,55 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     } else {
         dv.status = out->status; dv.wait = out->wait_ms; dv.rule = out->rule_idx;
     }
+    b.arg_stride = n;
     if (e->sys.check) {
-        // SystemRules couple every IN entry to the global ENTRY_NODE: exact
-        // replay in submission order on the main stream (k_replay)
+        // SystemRules couple every IN entry to the global ENTRY_NODE: the batch
+        // is decided as a sequence of safe sub-batches (sf_system.h), each
+        // planned on the exact ENTRY_NODE, then sorted / decided / reduced by
+        // the ordinary pipeline.  One host round trip per sub-batch (its end q).
+        if (!e->sys_plan) {
+            HIP_TRY(hipMalloc((void**)&e->sys_plan, sizeof(SysPlanDev)));
+            HIP_TRY(hipMalloc((void**)&e->sys_pa, SYS_PLAN_BLOCKS * sizeof(SysExitQ)));
+            HIP_TRY(hipMalloc((void**)&e->sys_pb, SYS_PLAN_BLOCKS * sizeof(SysEntQ)));
+            HIP_TRY(hipMalloc((void**)&e->sys_mask, e->cfg.max_batch));
+        }
         HIP_TRY(hipMemsetAsync(w.err, 0, sizeof(int32_t), ss));
         HIP_TRY(hipEventRecord(e->ev_sorted[slot], ss));
         HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
         DevState stl = e->st;
         stl.err = w.err;
-        hipError_t le = launch_replay(stl, b, dv, e->cfg.shard_count, e->cfg.shard_index, e->sys, e->en, s);
-        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("replay: ") + hipGetErrorString(le));
+        uint32_t p = 0, rounds = 0;
+        while (p < n) {
+            hipError_t le = sys_plan(stl, b, dv.status, e->sys_mask, e->sys, e->en, p, e->sys_plan, e->sys_pa,
+                                     e->sys_pb, s);
+            if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("system plan: ") + hipGetErrorString(le));
+            uint32_t q = 0;
+            HIP_TRY(hipMemcpyAsync(&q, &e->sys_plan->q, 4, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (q <= p || q > n) return fail(SF_ERR_DEVICE, "system planner made no progress");
+            DevBatch v = b;                        // the view [p, q)
+            v.n = q - p; v.base = p;
+            v.res = b.res + p; v.ts = b.ts + p; v.cnt = b.cnt + p; v.flags = b.flags + p;
+            v.eref = b.eref ? b.eref + p : nullptr; v.cts = b.cts ? b.cts + p : nullptr;
+            v.nargs = b.nargs ? b.nargs + p : nullptr;
+            v.atag = b.atag ? b.atag + p : nullptr; v.abits = b.abits ? b.abits + p : nullptr;
+            v.sys = e->sys_mask + p; v.vprev = dv.status + p;
+            DevVerdicts dvv{dv.status + p, dv.wait ? dv.wait + p : nullptr, dv.rule ? dv.rule + p : nullptr};
+            le = launch_sort(stl, w, v, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s, e->evs[slot], false);
+            if (le == hipSuccess)
+                le = launch_decide(stl, w, v, dvv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3,
+                                   e->evs[slot], false);
+            if (le == hipSuccess) le = launch_entry_node(stl, v, dvv.status, e->en, e->en_acc, s);
+            if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
+            p = q;
+            rounds++;
+        }
         HIP_TRY(hipEventRecord(e->ev_done[slot], s));
         e->used[slot] = true;
         e->last = slot;
         e->stats.n_events = n;
         e->stats.n_launches++;
+        e->stats.sys_rounds += rounds;
         if (out->mem == SF_MEM_HOST) {
             HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, s));
             if (dv.wait) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait, (size_t)n * 4, hipMemcpyDeviceToHost, s));
@@ -1364,6 +1403,22 @@ int sf_set_timing(sf_engine* e, int enabled) {
     if (!e) return fail(SF_ERR_INVALID, "null engine");
     e->timing = enabled != 0;
     std::memset(&e->stats, 0, sizeof e->stats);
+    return SF_OK;
+}
+
+int sf_param_table_stats(sf_engine* e, uint64_t* used, uint64_t* capacity, uint32_t* max_probe) {
+    if (!e || !used || !capacity || !max_probe) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> g(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, 16));
+    unsigned long long h[2] = {0, 0};
+    hipError_t he = launch_param_stats(e->st, d, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    hipFree(d);
+    if (he != hipSuccess) return fail(SF_ERR_DEVICE, std::string("param stats: ") + hipGetErrorString(he));
+    *used = h[0]; *capacity = e->st.pcap_mask + 1; *max_probe = (uint32_t)h[1];
     return SF_OK;
 }
 

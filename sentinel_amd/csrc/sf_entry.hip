@@ -41,8 +41,8 @@ __device__ __forceinline__ EnEvent en_event(const DevBatch& b, const uint8_t* vs
         e.touch = e.pass || e.block;                                 // PriorityWait: thread only
         e.thr = (e.pass || v == SF_V_PRIORITY_WAIT) ? 1 : 0;
     } else if (v == SF_V_EXIT) {
-        const int64_t ref = b.eref ? b.eref[i] : -1;
-        const int64_t cts = ref >= 0 ? b.ts[ref] : (b.cts ? b.cts[i] : e.t);
+        const int64_t ref = b.eref ? b.eref[i] : -1;              // batch index (view-local: ref - base)
+        const int64_t cts = ref >= 0 ? b.ts[ref - b.base] : (b.cts ? b.cts[i] : e.t);
         e.touch = true; e.rt = e.t - cts; e.err = (f & SF_EV_ERROR) != 0; e.thr = -1;
     }
     return e;

@@ -28,7 +28,7 @@ namespace sf {
 
 // segment modes (seg_mode[s])
 enum : uint8_t { SM_LIGHT = 0, SM_GENERIC = 1, SM_QPS = 2, SM_WARM = 3, SM_RL = 4, SM_NORULE = 5, SM_THREAD = 6 };
-constexpr uint32_t SEGF_PRIO = 1u, SEGF_NONPOS = 2u;
+constexpr uint32_t SEGF_PRIO = 1u, SEGF_NONPOS = 2u, SEGF_SYS = 4u;
 
 struct Acc {            // per (segment, window) counter deltas
     unsigned long long pass, block, succ, rt, exc, n_pass, n_exit, n_touch;
@@ -49,7 +49,7 @@ SF_HD uint8_t heavy_mode(const DevState& st, uint32_t res, uint32_t segflags, in
         if (st.borrow[(size_t)res * st.S + i].ws >= ws_first) return SM_GENERIC;
     const uint32_t nr = st.rule_off[res + 1] - st.rule_off[res];
     const uint32_t np = st.prule_off[res + 1] - st.prule_off[res];
-    if (np != 0 || (segflags & SEGF_NONPOS) || st.interval != 1000) return SM_GENERIC;
+    if (np != 0 || (segflags & (SEGF_NONPOS | SEGF_SYS)) || st.interval != 1000) return SM_GENERIC;
     if (nr == 0) return SM_NORULE;
     if (nr != 1 || (segflags & SEGF_PRIO)) return SM_GENERIC;
     const DevRule& r = st.rules[st.rule_off[res]];
@@ -333,7 +333,7 @@ inline void heavy_thread(Team&, const DevState& st, const SegIO& io, const Heavy
             }
         } else {
             const int64_t r = io.eref ? io.eref[j] : -1;
-            if (r < 0 || (r >= (int64_t)lo && r < (int64_t)j && pass_bit(hc.passbits, (uint32_t)r))) T--;
+            if (r == -1 || (r >= (int64_t)lo && r < (int64_t)j && pass_bit(hc.passbits, (uint32_t)r))) T--;
         }
     }
 }
@@ -391,7 +391,7 @@ SF_HD EvContrib heavy_event(const HeavyCtx& hc, const SegIO& io, uint32_t lo, ui
         r.touch = true;
     } else {
         const int64_t ref = io.eref ? io.eref[j] : -1;
-        r.live_exit = ref < 0 || (ref >= (int64_t)lo && ref < (int64_t)j && (all || pass_bit(hc.passbits, (uint32_t)ref)));
+        r.live_exit = ref == -1 || (ref >= (int64_t)lo && ref < (int64_t)j && (all || pass_bit(hc.passbits, (uint32_t)ref)));
         r.status = r.live_exit ? SF_V_EXIT : SF_V_EXIT_IGNORED;
         r.touch = r.live_exit;
         r.rt = io.ts[j] - (ref >= 0 ? io.ts[ref] : (io.cts ? io.cts[j] : io.ts[j]));

@@ -162,13 +162,30 @@ struct Work {
 };
 
 // Device view of a caller batch (pointers already on device).
+// A sub-batch (SystemRule planner, sf_system.h) is a view of events
+// [base, base + n) of the caller's batch: every pointer is offset by base,
+// entry_ref values stay batch indices (an entry before the view is at a
+// negative local index), args keep the batch's slot stride.
 struct DevBatch {
     uint32_t n;
     const uint32_t* res; const int64_t* ts; const int32_t* cnt; const uint8_t* flags;
     const int64_t* eref; const int64_t* cts;
     uint32_t arg_slots; const uint8_t* nargs; const uint8_t* atag; const uint64_t* abits;
+    uint32_t arg_stride;           // slot stride of atag / abits (the whole batch's n)
+    int64_t base;                  // index of the view's first event in the batch (0: whole batch)
+    const uint8_t* sys;            // planner verdicts of IN entries (SYS_NONE: none), or null
+    const uint8_t* vprev;          // verdicts of the batch (decided before the view), or null
 };
 struct DevVerdicts { uint8_t* status; int32_t* wait; uint16_t* rule; };
+
+// internal event flags (sorted-order s_flags; never set by the caller): a
+// SystemBlockException forced by the SystemRule planner, reason in bits 4-6
+constexpr uint8_t EVF_SYSBLK = 0x80u;
+constexpr uint8_t EVF_SYSREASON_SHIFT = 4;
+constexpr uint8_t SYS_NONE = 0xFFu;      // planner mask: no forced block
+// sorted entry_ref of an exit whose entry was decided in an earlier sub-batch:
+// -1 it passed (the exit is live, like an entry of an earlier batch), -2 blocked
+constexpr int64_t EREF_DEAD = -2;
 
 // ---- launchers (sf_kernels.hip) ----
 hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes,
@@ -201,8 +218,7 @@ hipError_t launch_fmt_len(const sf_metric_row* rows, const uint32_t* order, uint
 hipError_t launch_fmt_write(const sf_metric_row* rows, const uint32_t* order, uint32_t n, const char* names,
                             const uint64_t* name_off, const int32_t* types, uint32_t n_names, int64_t tz,
                             const uint64_t* line_off, char* out, hipStream_t s);
-hipError_t launch_replay(const DevState& st, const DevBatch& b, const DevVerdicts& out, uint32_t shard_count,
-                         uint32_t shard_index, const SysRule& sr, EntryNode* en, hipStream_t s);
+hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipStream_t s);   // out[0] used, out[1] max probe
 hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,
                        uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing);
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,

@@ -24,6 +24,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "sf_stream.h"
+#include "sf_system.h"
 
 namespace sf {
 
@@ -58,7 +59,12 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t
     const int64_t d = b.ts[i] - b.ts[0];
     if (d < 0 || d > (int64_t)0xffffffffLL) *wide = 1u;
     PackedEv v;
-    v.idx = i; v.dts = (uint32_t)d; v.cnt = b.cnt[i]; v.flags = b.flags[i];
+    const uint8_t f = b.flags[i];
+    v.idx = i; v.dts = (uint32_t)d; v.cnt = b.cnt[i]; v.flags = f & 0x0Fu;
+    if (b.sys && (f & SF_EV_IN) && !(f & SF_EV_EXIT)) {          // SystemBlockException forced by the planner
+        const uint8_t r = b.sys[i];
+        if (r != SYS_NONE) v.flags |= EVF_SYSBLK | ((uint32_t)r << EVF_SYSREASON_SHIFT);
+    }
     pv[i] = v;
 }
 
@@ -75,15 +81,16 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* wide, u
     const uint8_t f = (uint8_t)v.flags;
     perm[j] = i;
     s_ts[j] = *wide ? b.ts[i] : b.ts[0] + (int64_t)v.dts; s_cnt[j] = c; s_flags[j] = f;
-    if (!(f & SF_EV_EXIT) && ((f & SF_EV_PRIO) || c <= 0)) {
+    if (!(f & SF_EV_EXIT) && ((f & (SF_EV_PRIO | EVF_SYSBLK)) || c <= 0)) {
         uint32_t s = head_scan[j] + head[j] - 1;
-        atomicOr(&segflag[s], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u));
+        atomicOr(&segflag[s], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) |
+                              ((f & EVF_SYSBLK) ? SEGF_SYS : 0u));
     }
     if (b.arg_slots) {
         if (b.nargs) s_nargs[j] = b.nargs[i];
         for (uint32_t a = 0; a < b.arg_slots; a++) {
-            s_atag[(size_t)a * b.n + j] = b.atag[(size_t)a * b.n + i];
-            s_abits[(size_t)a * b.n + j] = b.abits[(size_t)a * b.n + i];
+            s_atag[(size_t)a * b.n + j] = b.atag[(size_t)a * b.arg_stride + i];
+            s_abits[(size_t)a * b.n + j] = b.abits[(size_t)a * b.arg_stride + i];
         }
     }
 }
@@ -113,8 +120,19 @@ __global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint8_t* s
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n || !(s_flags[j] & SF_EV_EXIT)) return;
     const uint32_t i = perm[j];
-    const int64_t r = b.eref[i];
-    if (r < 0) { s_eref[j] = -1; s_cts[j] = b.cts ? b.cts[i] : 0; return; }
+    const int64_t raw = b.eref[i];
+    if (raw < 0) { s_eref[j] = -1; s_cts[j] = b.cts ? b.cts[i] : 0; return; }
+    const int64_t r = raw - b.base;                                      // view-local index
+    if (r < 0) {
+        // the entry was decided in an earlier sub-batch of this batch: live
+        // (-1, its time as create_ts) unless it was blocked (-2: the exit is ignored)
+        if (!b.vprev || b.res[r] != b.res[i] || (b.flags[r] & SF_EV_EXIT)) {
+            *err = SF_ERR_INVALID; s_eref[j] = -1; s_cts[j] = 0; return;
+        }
+        s_eref[j] = v_blocked_any(b.vprev[r]) ? -2 : -1;
+        s_cts[j] = b.ts[r];
+        return;
+    }
     uint32_t a = seg_start[head_scan[j] + head[j] - 1], e = j;          // entry in [segment start, j)
     if (r >= (int64_t)i) { *err = SF_ERR_INVALID; s_eref[j] = -1; s_cts[j] = 0; return; }
     while (a < e) { const uint32_t m = (a + e) >> 1; if ((int64_t)perm[m] < r) a = m + 1; else e = m; }
@@ -500,7 +518,7 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
                 const int64_t r = rf[k];
                 const uint32_t j = base + (uint32_t)k;
                 if (r >= 0 && (r < (int64_t)lo || r >= (int64_t)j || !is_entry(rfl[k]))) *st.err = SF_ERR_INVALID;
-                const bool live = r < 0 || (r >= (int64_t)lo && r < (int64_t)j &&
+                const bool live = r == -1 || (r >= (int64_t)lo && r < (int64_t)j &&
                                             (all || ((rw[k] >> ((uint32_t)r & 63)) & 1ull)));
                 if (live) rlive |= 1u << k;
             }
@@ -598,54 +616,28 @@ __global__ void k_heavy_apply(DevState st, HeavyCtx hc, StreamCtx sc, const uint
     heavy_apply(st, hc, s, hc.seg_res[s], seg_nhw[s], seg_nsec[s]);
 }
 
-// SystemRules loaded: every IN entry's check reads the global ENTRY_NODE,
-// which every earlier IN event updates, so the batch is replayed in
-// submission order by one lane (SystemRuleManager.checkSystem before
-// ParamFlowSlot and FlowSlot, ENTRY_NODE accounted inline; exact, serial).
-template <int MAXS>
-__global__ void __launch_bounds__(64) k_replay(DevState st, SegIO io, DevBatch b, uint32_t shard_count,
-                                               uint32_t shard_index, SysRule sr, EntryNode* en) {
-    if (threadIdx.x != 0) return;
-    NodeWin<MAXS> e;
-    e.S = st.S; e.wl = st.wl; e.interval = st.interval; e.max_rt = st.max_rt;
-    e.interval_sec = st.interval / 1000.0;
-    for (int i = 0; i < MAXS; i++) {
-        e.sec[i] = i < st.S ? en->second[i] : fresh_bucket(WS_NONE, st.max_rt);
-        e.bor[i].ws = WS_NONE; e.bor[i].pass = 0;          // ENTRY_NODE never borrows
+// occupancy and longest probe distance of the exact param table (diagnostics)
+__global__ void k_param_stats(DevState st, unsigned long long* out) {
+    unsigned long long used = 0, maxp = 0;
+    const uint64_t cap = st.pcap_mask + 1;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
+        const ParamSlot& s = st.ptab[i];
+        if (s.hi == 0) continue;
+        used++;
+        const uint64_t home = ParamTable::hash(s.hi, s.lo) & st.pcap_mask;
+        const unsigned long long d = (i - home) & st.pcap_mask;
+        if (d > maxp) maxp = d;
     }
-    e.threads = en->threads;
-    e.gmin = en->minute; e.mi = -1; e.mdirty = 0; e.mb = fresh_bucket(WS_NONE, st.max_rt);
-    SysCtx<MAXS> sys{sr, &e};
-    for (uint32_t j = 0; j < b.n; j++) {
-        const uint32_t r = b.res[j], l = r / shard_count;
-        if (r % shard_count != shard_index || l >= st.R) { *st.err = SF_ERR_INVALID; continue; }
-        if ((b.flags[j] & SF_EV_EXIT) && b.eref) {              // the entry: earlier, same resource, an entry
-            const int64_t ref = b.eref[j];
-            if (ref >= 0 && (ref >= (int64_t)j || b.res[ref] != r || (b.flags[ref] & SF_EV_EXIT))) {
-                *st.err = SF_ERR_INVALID;
-                continue;
-            }
-        }
-        decide_segment<MAXS, true>(st, io, l, j, j + 1, &sys);
+    for (int o = 32; o > 0; o >>= 1) {
+        used += __shfl_xor(used, o);
+        const unsigned long long m = __shfl_xor(maxp, o);
+        maxp = m > maxp ? m : maxp;
     }
-    for (int i = 0; i < MAXS; i++) if (i < st.S) en->second[i] = e.sec[i];
-    e.min_flush();
-    en->threads = e.threads;
+    if ((threadIdx.x & 63) == 0) { atomicAdd(&out[0], used); atomicMax(&out[1], maxp); }
 }
-
-hipError_t launch_replay(const DevState& st, const DevBatch& b, const DevVerdicts& out, uint32_t shard_count,
-                         uint32_t shard_index, const SysRule& sr, EntryNode* en, hipStream_t s) {
-    if (b.n == 0) return hipSuccess;
-    SegIO io{};
-    io.ts = b.ts; io.cnt = b.cnt; io.flags = b.flags; io.eref = b.eref; io.cts = b.cts;
-    io.arg_slots = b.arg_slots; io.nargs = b.nargs; io.atag = b.atag; io.abits = b.abits; io.n = b.n;
-    io.v_status = out.status; io.v_wait = out.wait; io.v_rule = out.rule;   // submission order: exits read their entry's verdict
-    io.perm = nullptr;
-    if (st.S <= 2)
-        hipLaunchKernelGGL(k_replay<2>, dim3(1), dim3(64), 0, s, st, io, b, shard_count, shard_index, sr, en);
-    else
-        hipLaunchKernelGGL(k_replay<SF_MAX_SAMPLE_COUNT>, dim3(1), dim3(64), 0, s, st, io, b, shard_count, shard_index,
-                           sr, en);
+hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipStream_t s) {
+    hipMemsetAsync(out, 0, 16, s);
+    hipLaunchKernelGGL(k_param_stats, dim3(2048), dim3(256), 0, s, st, out);
     return hipGetLastError();
 }
 

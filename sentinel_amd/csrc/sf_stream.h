@@ -155,7 +155,7 @@ __device__ void thr_prepare(ThrLds& L, int buf, const SegIO& io, const uint32_t*
         L.xo[buf][64 * wl + lane] = ent ? xa[k] : XO_NONE;
         L.cn[buf][64 * wl + lane] = c;
         L.el[buf][64 * wl + lane] = (ex && ref >= (int64_t)q && ref < (int64_t)j) ? (uint8_t)(ref - (int64_t)q) : (uint8_t)255;
-        const unsigned long long mo = __ballot(ex && ref < 0);        // entry of an earlier batch: live
+        const unsigned long long mo = __ballot(ex && ref == -1);       // entry of an earlier batch: live
         if (lane == 0) {
             L.win[buf][wl] = wn;
             // live exits of far-away entries (written into HBM when those entries passed)

@@ -36,12 +36,6 @@
 
 namespace sf {
 
-// internal event flags (sorted-order s_flags; never set by the caller):
-// a SystemBlockException forced by the planner, reason in bits 4-6
-constexpr uint8_t EVF_SYSBLK = 0x80u;
-constexpr uint8_t EVF_SYSREASON_SHIFT = 4;
-constexpr uint8_t SYS_NONE = 0xFFu;      // planner mask: no forced block
-
 // ENTRY_NODE at p, restricted to what the checks read inside the window.
 struct SysBase {
     int64_t W;              // window start of the current bucket
@@ -212,5 +206,17 @@ SF_HD SysExitQ sys_exit_q(const int64_t* ts, const int32_t* cnt, const uint8_t* 
     }
     return q;
 }
+
+// planner state in HBM (one per engine)
+struct SysPlanDev {
+    SysBase base;
+    uint32_t wend, lim, first_unc, q;
+};
+
+// Plan the events from p of batch b (whole batch, base 0): mask[i] for the
+// IN entries of [p, q), plan->q.  vstatus: the batch's verdicts (before p).
+hipError_t sys_plan(const DevState& st, const DevBatch& b, const uint8_t* vstatus, uint8_t* mask, const SysRule& r,
+                    const EntryNode* en, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb, hipStream_t s);
+constexpr uint32_t SYS_PLAN_BLOCKS = 512;       // SP_NB (sf_system.hip): size of pa / pb
 
 }  // namespace sf

@@ -19,7 +19,7 @@
 namespace sf {
 
 constexpr int SP_T = 256, SP_RUN = 16, SP_BLK = SP_T * SP_RUN;   // 4096 events per block
-constexpr uint32_t SP_NB = 512;                                   // blocks per plan
+constexpr uint32_t SP_NB = SYS_PLAN_BLOCKS;                       // blocks per plan
 constexpr uint32_t SP_CAP = SP_NB * SP_BLK;                       // 2 Mi events per plan
 
 struct SysPlanArgs {

@@ -157,7 +157,8 @@ __global__ void __launch_bounds__(64) k_ns_limit(TokState ts, TokBatch b, TokWor
 __device__ uint32_t cp_find_or_insert(const TokState& ts, uint64_t hi, uint64_t lo) {
     uint64_t i = mix64(hi ^ mix64(lo + 0x9e3779b97f4a7c15ULL)) & ts.cp_mask;
     uint64_t probes = 0;
-    while (probes <= ts.cp_mask) {
+    const uint64_t reach = ts.cp_mask < PT_MAX_PROBE ? ts.cp_mask : PT_MAX_PROBE;   // as ParamTable (sf_decide.h)
+    while (probes <= reach) {
         CpSlot& s = ts.cptab[i];
         const uint64_t h = __hip_atomic_load(&s.hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         if (h == 0) {

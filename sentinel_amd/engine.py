@@ -92,6 +92,7 @@ def _declare(L):
     f("sf_get_stats", I, P, C.POINTER(abi.sf_stats))
     f("sf_set_timing", I, P, I)
     f("sf_heavy_profile_read", I, P, C.POINTER(abi.sf_heavy_profile), U32, C.POINTER(U32))
+    f("sf_param_table_stats", I, P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(U32))
 
 
 def comm_unique_id() -> bytes:
@@ -356,6 +357,13 @@ class FlowEngine:
         s = abi.sf_rule_state()
         _check(lib().sf_read_rule_state(self.h, idx, C.byref(s)))
         return s
+
+    def param_table_stats(self) -> dict:
+        """Exact hot-parameter table: occupied slots, capacity, load factor, longest probe."""
+        u, c, m = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        _check(lib().sf_param_table_stats(self.h, C.byref(u), C.byref(c), C.byref(m)))
+        return dict(used=u.value, capacity=c.value, load_factor=round(u.value / max(1, c.value), 4),
+                    max_probe=m.value)
 
     def set_timing(self, on=True):
         _check(lib().sf_set_timing(self.h, int(on)))

@@ -122,6 +122,27 @@ def test_system_rule(eng_mod, so, kind):
     eng, ora, outs = workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
     blocked = sum(int((o[1].status == abi.V_BLOCK_SYSTEM).sum()) for o in outs)
     assert blocked > 0, "the SystemRule never fired: the workload does not exercise it"
+    n = sum(b.n for b in w["batches"])
+    assert 0 < eng.stats().sys_rounds < n // 4, eng.stats().sys_rounds   # planned sub-batches, not a replay
+
+
+@pytest.mark.parametrize("kind", ["param", "mixed"])
+def test_system_rule_large(eng_mod, so, kind):
+    """SystemRules at scale through the planner: config 4's shape (2 Mi
+    events, 1k resources, param rules, inbound QPS at 0.8x the offered rate)
+    and config 3's traffic with QPS + thread + RT system rules over three
+    batches; every verdict, the sampled nodes, ENTRY_NODE and the controller
+    states equal the oracle's."""
+    w = workloads.system_large(kind)
+    eng, ora, outs = workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
+    st = np.concatenate([o[1].status for o in outs])
+    reasons = np.concatenate([o[1].rule_idx[o[1].status == abi.V_BLOCK_SYSTEM] for o in outs])
+    assert (st == abi.V_BLOCK_SYSTEM).sum() > 1000, "the SystemRule barely fired"
+    if kind == "mixed":
+        assert set(np.unique(reasons)) >= {0, 1}, np.unique(reasons)
+    n = sum(b.n for b in w["batches"])
+    print(f"{kind}: {n} events, {eng.stats().sys_rounds} planner rounds, "
+          f"{(st == abi.V_BLOCK_SYSTEM).sum()} system blocks, reasons {np.bincount(reasons)}")
 
 
 def test_config2_large_properties(eng_mod, so):

@@ -137,7 +137,7 @@ def system(kind, seed=41):
     """SystemRule over mixed traffic (SystemRuleManager.checkSystem, global
     ENTRY_NODE): config 4's inbound-QPS rule at 0.8x the offered rate, or the
     thread / RT / load (BBR) / cpu thresholds over THREAD-grade traffic with
-    exits.  Replayed on the GPU in submission order (k_replay)."""
+    exits.  Decided on the GPU as planned safe sub-batches (sf_system.h)."""
     rng = np.random.default_rng(seed)
     if kind == "qps":
         rules, batch = trace.param_zipf(30, 40_000, 3000, duration_ms=4000, seed=seed)
@@ -158,6 +158,33 @@ def system(kind, seed=41):
     batches = [full.subset(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
     return dict(cfg=abi.default_config(max_resources=R, max_batch=full.n), flow=rules, batches=batches,
                 nodes=list(range(R)), n_flow=len(rules), system=sysr, status=status)
+
+
+def system_large(kind, seed=43):
+    """SystemRule at scale: "param" = config 4's shape (uniform resources with
+    QPS / throttle ParamFlowRules, Zipf(1.1) keys) with the inbound-QPS rule at
+    ``frac`` x the offered rate; "mixed" = config 3's traffic (flow rules of all
+    four controllers, THREAD exits, acquireCount 1-5) with an inbound-QPS rule
+    and a thread rule that both fire; three batches."""
+    if kind == "param":
+        R, n = 1000, 1 << 21
+        rules, batch = trace.param_zipf(R, n, 200_000, duration_ms=4000, seed=seed)
+        sysr = [abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=0.8 * n / 4.0,
+                                   avg_rt=-1, max_thread=-1)]
+        return dict(cfg=abi.default_config(max_resources=R, max_batch=batch.n, param_capacity=1 << 22),
+                    param=rules, batches=[batch], nodes=list(range(0, R, 9)), system=sysr, status=(0.0, 0.0))
+    R = 5000
+    full = trace.mixed_zipf(R, 600_000, duration_ms=6000, seed=seed)
+    rules = trace.mixed_rules(R, seed=seed)
+    sysr = [abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=0.35 * full.n / 6.0,
+                               avg_rt=-1, max_thread=60_000),
+            abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=-1, avg_rt=21, max_thread=-1)]
+    cuts = np.linspace(0, full.n, 4).astype(int)
+    batches = [full.subset(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
+    hot = np.argsort(-np.bincount(full.res_id, minlength=R))[:40]
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=full.n), flow=rules, batches=batches,
+                nodes=sorted(set(int(x) for x in hot) | set(range(0, R, 97))), n_flow=len(rules), system=sysr,
+                status=(0.0, 0.0))
 
 
 ALL = {
