@@ -124,6 +124,9 @@ typedef struct sf_flow_rule {
 #define SF_TAG_BYTE   7   /* java.lang.Byte  (wire PARAM_TYPE_BYTE)  */
 #define SF_TAG_SHORT  8   /* java.lang.Short (wire PARAM_TYPE_SHORT) */
 #define SF_TAG_FLOAT  9   /* java.lang.Float (wire PARAM_TYPE_FLOAT), bits = floatToIntBits */
+/* An argument that is a java.util.Collection or an array: its elements are
+ * listed separately (sf_event_batch.arg_elem_off / sf_token_batch.param_off). */
+#define SF_TAG_COLLECTION 0x40
 
 typedef struct sf_hot_item {      /* ParamFlowItem parsed (ParamFlowRuleUtil.java:188-240) */
     uint8_t  tag;
@@ -180,6 +183,20 @@ typedef struct sf_event_batch {
     const uint8_t*  n_args;       /* [n] or NULL (= arg_slots for every event) */
     const uint8_t*  arg_tag;      /* [arg_slots*n]                             */
     const uint64_t* arg_bits;     /* [arg_slots*n]                             */
+    /* Collection / array arguments (ParamFlowChecker.passLocalCheck :84-112,
+     * ParameterMetric.addThreadCount / decreaseThreadCount :125-239): the
+     * argument k = slot*n + i whose arg_tag[k] is SF_TAG_COLLECTION holds the
+     * elements elem_tag / elem_bits[arg_elem_off[k] .. arg_elem_off[k+1]) in
+     * iteration order.  Every element must pass each rule in turn; the tokens
+     * of the elements before a failing one stay consumed.  A null element
+     * (SF_TAG_NULL) ends the loop as the reference's NullPointerException in
+     * the parameter maps does (the value then passes that rule), after the
+     * checks that come first (a zero threshold, acquireCount > max tokens).
+     * NULL arg_elem_off: no argument is a collection.                         */
+    const uint32_t* arg_elem_off; /* [arg_slots*n + 1] or NULL                 */
+    const uint8_t*  elem_tag;     /* [n_elems]                                 */
+    const uint64_t* elem_bits;    /* [n_elems]                                 */
+    uint32_t        n_elems;
 } sf_event_batch;
 
 /* ---- verdicts ---------------------------------------------------------- */
@@ -236,7 +253,7 @@ typedef struct sf_namespace {
 } sf_namespace;
 
 #define SF_TOK_PRIORITIZED 0x01u
-#define SF_TOK_PARAM       0x02u  /* requestParamToken (one param value)       */
+#define SF_TOK_PARAM       0x02u  /* requestParamToken                          */
 
 typedef struct sf_token_batch {
     uint32_t        n;
@@ -245,8 +262,15 @@ typedef struct sf_token_batch {
     const int32_t*  count;        /* [n] acquireCount                          */
     const uint8_t*  flags;        /* [n] SF_TOK_*                              */
     const int64_t*  ts_ms;        /* [n] server clock at request, non-decreasing */
-    const uint8_t*  param_tag;    /* [n] or NULL                               */
-    const uint64_t* param_bits;   /* [n] or NULL                               */
+    const uint8_t*  param_tag;    /* [n] or NULL (param_off: [param_off[n]])   */
+    const uint64_t* param_bits;   /* [n] or NULL (param_off: [param_off[n]])   */
+    /* requestParamToken(Long, int, Collection<Object> params): with param_off,
+     * request i's params are param_tag / param_bits[param_off[i] ..
+     * param_off[i+1]) in iteration order (ClusterParamFlowChecker.java:42-87:
+     * every value must have room before any is added; remaining is -1 for
+     * more than one value; an empty collection is BAD_REQUEST,
+     * DefaultTokenService.java:53-56).  NULL: one value per request.        */
+    const uint32_t* param_off;    /* [n + 1] or NULL                           */
 } sf_token_batch;
 
 typedef struct sf_token_results {
@@ -363,9 +387,10 @@ int  sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results*
  *   - an incomplete frame at the end              -> SF_WIRE_PARTIAL
  *   - a frame the host must run through the reference pipeline -> SF_WIRE_HOST:
  *     PING (ConnectionManager bookkeeping; its connected count takes effect at
- *     the next call), a type with no decoder, a PARAM_FLOW with more than one
- *     parameter, or a frame whose body the decoder does not consume exactly
- *     (Netty's cumulation would carry the rest into the next frame).
+ *     the next call), a type with no decoder, or a frame whose body the
+ *     decoder does not consume exactly (Netty's cumulation would carry the
+ *     rest into the next frame).  The parameters of a PARAM_FLOW frame are
+ *     one Collection (requestParamToken with every decoded value).
  * consumed[s] = bytes of stream s handled (the stopping frame starts there).
  * Frames longer than 1024 bytes are skipped without a response (Netty's
  * TooLongFrameException); a FLOW / PARAM_FLOW frame with no data gets no

@@ -831,11 +831,12 @@ static int pass_default_local(so_param_metric* pm, int key, const sf_param_rule*
     so_map* time_counters = rule_map_get(pm->time_counters, pm->n_time, key);
     if (!token_counters || !time_counters) return 1;
     int64_t token_count = so_java_d2l(rule->count);
-    const sf_hot_item* hi = hot_item(rule, items, tag, bits);
+    const sf_hot_item* hi = tag == SF_TAG_NULL ? NULL : hot_item(rule, items, tag, bits);   /* no null hot item */
     if (hi) token_count = hi->count;
     if (token_count == 0) return 0;
     int64_t max_count = jadd(token_count, rule->burst_count);
     if (acquire > max_count) return 0;
+    if (tag == SF_TAG_NULL) return 2;       /* timeCounters.putIfAbsent(null): NullPointerException */
     for (;;) {
         int64_t current_time = g_now;
         int64_t* last_add = map_find(time_counters, tag, bits);
@@ -880,9 +881,10 @@ static int pass_throttle_local(so_param_metric* pm, int key, const sf_param_rule
     so_map* time_recorder = rule_map_get(pm->time_counters, pm->n_time, key);
     if (!time_recorder) return 1;
     int64_t token_count = so_java_d2l(rule->count);
-    const sf_hot_item* hi = hot_item(rule, items, tag, bits);
+    const sf_hot_item* hi = tag == SF_TAG_NULL ? NULL : hot_item(rule, items, tag, bits);
     if (hi) token_count = hi->count;
     if (token_count == 0) return 0;
+    if (tag == SF_TAG_NULL) return 2;       /* timeRecorderMap.putIfAbsent(null): NullPointerException */
     int64_t cost = so_java_round(1.0 * 1000 * acquire * (double)rule->duration_in_sec / (double)token_count);
     int64_t current_time = g_now;
     int64_t* rec = map_find(time_recorder, tag, bits);
@@ -897,7 +899,10 @@ static int pass_throttle_local(so_param_metric* pm, int key, const sf_param_rule
     }
     return 0;
 }
-/* ParamFlowChecker.passSingleValueCheck — :114-137 */
+/* ParamFlowChecker.passSingleValueCheck — :114-137.  1 pass, 0 block; 2 for a
+ * null element of a collection: the parameter maps throw NullPointerException
+ * (ConcurrentLinkedHashMap takes no null key) after the checks before them,
+ * and passLocalCheck catches it (:108-110): the value passes, its loop ends. */
 int so_param_pass_single(so_param_metric* pm, int key, const sf_param_rule* rule,
                          const sf_hot_item* items, int32_t acquire, uint8_t tag, uint64_t bits,
                          int64_t* wait_ms) {
@@ -907,6 +912,7 @@ int so_param_pass_single(so_param_metric* pm, int key, const sf_param_rule* rule
             return pass_throttle_local(pm, key, rule, items, acquire, tag, bits, wait_ms);
         return pass_default_local(pm, key, rule, items, acquire, tag, bits);
     } else if (rule->grade == SF_GRADE_THREAD) {
+        if (tag == SF_TAG_NULL) return 2;   /* getThreadCount: cacheMap.get(null) */
         int64_t thread_count = so_pm_thread_count(pm, rule->param_idx, tag, bits);
         const sf_hot_item* hi = hot_item(rule, items, tag, bits);
         if (hi) return ++thread_count <= hi->count;
@@ -1211,6 +1217,44 @@ static uint32_t nargs_of(const sf_event_batch* in, uint32_t i) {
     return in->n_args ? in->n_args[i] : in->arg_slots;
 }
 
+/* ParamFlowChecker.passLocalCheck — :84-112: the value, or every element of a
+ * Collection / array in iteration order (earlier elements' tokens stay
+ * consumed when a later one fails); a thrown exception passes the value. */
+static int param_pass_value(so_param_metric* pm, int key, const sf_param_rule* rule, const sf_hot_item* items,
+                            int32_t acquire, const sf_event_batch* in, uint32_t i, uint32_t slot, int64_t* wait_ms) {
+    uint8_t tg; uint64_t bt; arg_of(in, i, slot, &tg, &bt);
+    if (tg != SF_TAG_COLLECTION) return so_param_pass_single(pm, key, rule, items, acquire, tg, bt, wait_ms) != 0;
+    *wait_ms = 0;
+    const uint64_t k = (uint64_t)slot * in->n + i;
+    for (uint32_t e = in->arg_elem_off[k]; e < in->arg_elem_off[k + 1]; e++) {
+        int64_t w = 0;
+        int ok = so_param_pass_single(pm, key, rule, items, acquire, in->elem_tag[e], in->elem_bits[e], &w);
+        if (ok == 0) return 0;
+        if (ok == 2) return 1;
+        *wait_ms += w;
+    }
+    return 1;
+}
+/* ParameterMetric.addThreadCount / decreaseThreadCount — :125-239 over every
+ * arg: null skipped, collections element by element; a null element throws
+ * and ends the whole callback (one try around the loop over the args). */
+static void pm_thread_event(so_param_metric* pm, const sf_event_batch* in, uint32_t i, uint32_t na, int add) {
+    for (uint32_t s = 0; s < na; s++) {
+        uint8_t tg; uint64_t bt; arg_of(in, i, s, &tg, &bt);
+        if (tg != SF_TAG_COLLECTION) {
+            if (add) so_pm_add_thread(pm, (int)s, tg, bt); else so_pm_dec_thread(pm, (int)s, tg, bt);
+            continue;
+        }
+        if (!thread_map_get(pm, (int)s)) continue;
+        const uint64_t k = (uint64_t)s * in->n + i;
+        for (uint32_t e = in->arg_elem_off[k]; e < in->arg_elem_off[k + 1]; e++) {
+            if (in->elem_tag[e] == SF_TAG_NULL) return;
+            if (add) so_pm_add_thread(pm, (int)s, in->elem_tag[e], in->elem_bits[e]);
+            else so_pm_dec_thread(pm, (int)s, in->elem_tag[e], in->elem_bits[e]);
+        }
+    }
+}
+
 int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     apply_statics(&e->cfg);
     if (in->mem != SF_MEM_HOST || out->mem != SF_MEM_HOST) return SF_ERR_INVALID;
@@ -1256,10 +1300,7 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
                     if (err) so_node_increase_exception_qps(e->entry_node, count);
                 }
                 /* ParamFlowStatisticExitCallback.onExit -> decreaseThreadCount(args) */
-                if (rr->pm) for (uint32_t s = 0; s < na; s++) {
-                    uint8_t tg; uint64_t bt; arg_of(in, i, s, &tg, &bt);
-                    so_pm_dec_thread(rr->pm, (int)s, tg, bt);
-                }
+                if (rr->pm) pm_thread_event(rr->pm, in, i, na, 0);
                 status = SF_V_EXIT;
             } else {
                 status = SF_V_EXIT_IGNORED;
@@ -1296,7 +1337,7 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
                 uint8_t tg; uint64_t bt; arg_of(in, i, (uint32_t)pr->param_idx, &tg, &bt);
                 if (tg == SF_TAG_NULL) continue;
                 int64_t w = 0;
-                if (!so_param_pass_single(rr->pm, rr->param_rules[k], pr, e->items, count, tg, bt, &w)) {
+                if (!param_pass_value(rr->pm, rr->param_rules[k], pr, e->items, count, in, i, (uint32_t)pr->param_idx, &w)) {
                     blocked = 1; status = SF_V_BLOCK_PARAM; rule_idx = k;
                 } else if (w > 0) {
                     wait += w;                                  /* throttle sleep inside the slot */
@@ -1322,17 +1363,13 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         } else if (prio_wait) {
             so_node_increase_thread_num(rr->node);
             if (is_in) so_node_increase_thread_num(e->entry_node);
-            if (rr->pm) for (uint32_t s = 0; s < na; s++) {
-                uint8_t tg; uint64_t bt; arg_of(in, i, s, &tg, &bt); so_pm_add_thread(rr->pm, (int)s, tg, bt);
-            }
+            if (rr->pm) pm_thread_event(rr->pm, in, i, na, 1);
             status = SF_V_PRIORITY_WAIT;
         } else {
             so_node_increase_thread_num(rr->node);
             so_node_add_pass_request(rr->node, count);
             if (is_in) { so_node_increase_thread_num(e->entry_node); so_node_add_pass_request(e->entry_node, count); }
-            if (rr->pm) for (uint32_t s = 0; s < na; s++) {
-                uint8_t tg; uint64_t bt; arg_of(in, i, s, &tg, &bt); so_pm_add_thread(rr->pm, (int)s, tg, bt);
-            }
+            if (rr->pm) pm_thread_event(rr->pm, in, i, na, 1);
             status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS;
         }
         e->entry_blocked[i] = (uint8_t)blocked;
@@ -1554,7 +1591,8 @@ int so_request_tokens(so_engine* e, const sf_token_batch* in, sf_token_results* 
         int8_t st; int32_t remaining = 0, wait = 0;
         if (id <= 0 || count <= 0) {                                   /* DefaultTokenService.notValidRequest :70-72 */
             st = SF_TOKEN_BAD_REQUEST;
-        } else if (is_param && (!in->param_tag || !in->param_bits)) {
+        } else if (is_param && (!in->param_tag || !in->param_bits ||
+                                (in->param_off && in->param_off[i + 1] == in->param_off[i]))) {
             st = SF_TOKEN_BAD_REQUEST;                                  /* params == null || isEmpty :52-54 */
         } else {
             cluster_rt* c = find_cl(e, id, is_param);
@@ -1592,19 +1630,28 @@ int so_request_tokens(so_engine* e, const sf_token_batch* in, sf_token_results* 
                         }
                     }
                 } else {
-                    /* ClusterParamFlowChecker.acquireClusterToken :42-87 (one value) */
-                    uint8_t tg = in->param_tag[i]; uint64_t bt = in->param_bits[i];
-                    double latest_qps = so_cpm_avg(c->cpm, tg, bt);
-                    double raw = c->count;
-                    for (uint32_t k = 0; k < c->item_count; k++) {
-                        const sf_hot_item* it = &e->cl_items[c->item_offset + k];
-                        if (it->tag == tg && it->bits == bt) { raw = it->count; break; }
+                    /* ClusterParamFlowChecker.acquireClusterToken :42-87: every value
+                     * must have room (the first without stops the check), then all are added */
+                    const uint32_t v0 = in->param_off ? in->param_off[i] : i;
+                    const uint32_t v1 = in->param_off ? in->param_off[i + 1] : i + 1;
+                    double rem = -1;
+                    int passed = 1;
+                    for (uint32_t v = v0; v < v1; v++) {
+                        uint8_t tg = in->param_tag[v]; uint64_t bt = in->param_bits[v];
+                        double latest_qps = so_cpm_avg(c->cpm, tg, bt);
+                        double raw = c->count;                              /* getRawThreshold :110-117 */
+                        for (uint32_t k = 0; k < c->item_count; k++) {
+                            const sf_hot_item* it = &e->cl_items[c->item_offset + k];
+                            if (it->tag == tg && it->bits == bt) { raw = it->count; break; }
+                        }
+                        double threshold = c->threshold_type == SF_THRESHOLD_GLOBAL ? raw : raw * connected;
+                        rem = threshold - latest_qps - count;
+                        if (rem < 0) { passed = 0; break; }
                     }
-                    double threshold = c->threshold_type == SF_THRESHOLD_GLOBAL ? raw : raw * connected;
-                    double next_remaining = threshold - latest_qps - count;
-                    if (next_remaining >= 0) {
-                        so_cpm_add_value(c->cpm, tg, bt, count);
-                        st = SF_TOKEN_OK; remaining = so_java_d2i(next_remaining);
+                    if (passed) {
+                        for (uint32_t v = v0; v < v1; v++) so_cpm_add_value(c->cpm, in->param_tag[v], in->param_bits[v], count);
+                        if (v1 - v0 > 1) rem = -1;                          /* remaining unsupported for multi-values */
+                        st = SF_TOKEN_OK; remaining = so_java_d2i(rem);
                     } else {
                         st = SF_TOKEN_BLOCKED;
                     }
@@ -1635,8 +1682,9 @@ int so_request_tokens(so_engine* e, const sf_token_batch* in, sf_token_results* 
  *     LengthFieldPrepender(2).
  * The stream stops (SF_WIRE_HOST) at the first frame whose outcome is not a
  * pure function of the frame and the token state (PING, a type without a
- * decoder, a body not consumed exactly, more than one parameter): the C-ABI
- * contract in sentinel_flow.h.
+ * decoder, a body not consumed exactly): the C-ABI contract in
+ * sentinel_flow.h.  A PARAM_FLOW frame's parameters are one Collection
+ * (ParamFlowRequestDataDecoder.java:49-58 builds an ArrayList).
  * ====================================================================== */
 enum { WF_NONE = 0, WF_REQ = 1, WF_BAD = 2, WF_HOST = 3 };
 
@@ -1653,14 +1701,15 @@ uint64_t so_string_key(const uint8_t* b, uint32_t len) {
 typedef struct {
     int32_t xid; int8_t type; uint8_t prio;
     int64_t flow_id; int32_t count;
-    int param; uint8_t tag; uint64_t bits;
+    int param; uint32_t v0, nv;               /* values at vtag/vbits[v0 .. v0 + nv) */
 } so_wire_req;
 
 /* One frame body through NettyRequestDecoder + DefaultRequestEntityDecoder +
  * the request processor.  WF_NONE: no response (empty frame, or the
  * processor's NullPointerException on null data). */
-static int so_wire_decode(const uint8_t* b, uint32_t L, so_wire_req* r) {
+static int so_wire_decode(const uint8_t* b, uint32_t L, so_wire_req* r, uint8_t* vtag, uint64_t* vbits, uint32_t v0) {
     memset(r, 0, sizeof *r);
+    r->v0 = v0;
     if (L == 0) return WF_NONE;                      /* callDecode: nothing readable */
     if (L < 5) return WF_HOST;                       /* decode() returns null, bytes stay cumulated */
     r->xid = (int32_t)wbe32(b);
@@ -1715,11 +1764,11 @@ static int so_wire_decode(const uint8_t* b, uint32_t L, so_wire_req* r) {
             case 5: if (p + 2 > rem) return WF_HOST; tag = SF_TAG_SHORT; bits = (uint64_t)(int64_t)(int16_t)(((uint32_t)q[p] << 8) | q[p + 1]); p += 2; break;
             default: ok = 0;                         /* decodeParam returns false, nothing added */
             }
-            if (ok) { if (n == 0) { r->tag = tag; r->bits = bits; } n++; }
+            if (ok) { vtag[v0 + n] = tag; vbits[v0 + n] = bits; n++; }
         }
         if (p != rem) return WF_HOST;                /* bytes left in the cumulation */
         if (n == 0) return WF_BAD;                   /* requestParamToken: params.isEmpty() -> badRequest */
-        if (n > 1) return WF_HOST;
+        r->nv = (uint32_t)n;
         r->param = 1;
         return WF_REQ;
     }
@@ -1734,6 +1783,9 @@ int so_serve_frames(so_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
     uint8_t* kind = (uint8_t*)malloc(total / 2 + 1);
     uint32_t* rstream = (uint32_t*)malloc(sizeof(uint32_t) * (total / 2 + 1));
     uint64_t nr = 0, nframes = 0;
+    uint8_t* vtag = (uint8_t*)malloc(total + 1);             /* every parameter takes >= 1 byte */
+    uint64_t* vbits = (uint64_t*)malloc(8 * (total + 1));
+    uint32_t nvals = 0;
     for (uint32_t s = 0; s < S; s++) {
         uint64_t p = in->stream_off[s];
         const uint64_t end = in->stream_off[s + 1];
@@ -1744,10 +1796,11 @@ int so_serve_frames(so_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
             if (p + 2 + L > end) { stop = SF_WIRE_PARTIAL; break; }
             if (L + 2 > SF_WIRE_MAX_FRAME) { p += 2 + L; nframes++; continue; }   /* TooLongFrameException */
             so_wire_req r;
-            const int k = so_wire_decode(in->bytes + p + 2, L, &r);
+            const int k = so_wire_decode(in->bytes + p + 2, L, &r, vtag, vbits, nvals);
             if (k == WF_HOST) { stop = SF_WIRE_HOST; break; }
             nframes++;
             if (k != WF_NONE) { reqs[nr] = r; kind[nr] = (uint8_t)k; rstream[nr] = s; nr++; }
+            if (k == WF_REQ) nvals += r.nv;
             p += 2 + L;
         }
         out->consumed[s] = p - in->stream_off[s];
@@ -1758,17 +1811,20 @@ int so_serve_frames(so_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
     for (uint64_t i = 0; i < nr; i++) nq += kind[i] == WF_REQ;
     int64_t* fid = (int64_t*)calloc(nq + 1, 8); int32_t* cnt = (int32_t*)calloc(nq + 1, 4);
     uint8_t* fl = (uint8_t*)calloc(nq + 1, 1); int64_t* ts = (int64_t*)calloc(nq + 1, 8);
-    uint8_t* tg = (uint8_t*)calloc(nq + 1, 1); uint64_t* bt = (uint64_t*)calloc(nq + 1, 8);
+    uint8_t* tg = (uint8_t*)calloc(nvals + nq + 1, 1); uint64_t* bt = (uint64_t*)calloc(nvals + nq + 1, 8);
+    uint32_t* po = (uint32_t*)calloc(nq + 1, 4);
     int8_t* st = (int8_t*)calloc(nq + 1, 1); int32_t* rm = (int32_t*)calloc(nq + 1, 4); int32_t* wt = (int32_t*)calloc(nq + 1, 4);
     for (uint64_t i = 0, j = 0; i < nr; i++) {
         if (kind[i] != WF_REQ) continue;
         fid[j] = reqs[i].flow_id; cnt[j] = reqs[i].count; ts[j] = in->now_ms;
         fl[j] = (uint8_t)((reqs[i].prio ? SF_TOK_PRIORITIZED : 0) | (reqs[i].param ? SF_TOK_PARAM : 0));
-        tg[j] = reqs[i].tag; bt[j] = reqs[i].bits; j++;
+        for (uint32_t v = 0; v < reqs[i].nv; v++) { tg[po[j] + v] = vtag[reqs[i].v0 + v]; bt[po[j] + v] = vbits[reqs[i].v0 + v]; }
+        po[j + 1] = po[j] + reqs[i].nv;
+        j++;
     }
     int rc = SF_OK;
     if (nq) {
-        sf_token_batch b = {(uint32_t)nq, SF_MEM_HOST, fid, cnt, fl, ts, tg, bt};
+        sf_token_batch b = {(uint32_t)nq, SF_MEM_HOST, fid, cnt, fl, ts, tg, bt, po};
         sf_token_results o = {SF_MEM_HOST, st, rm, wt};
         rc = so_request_tokens(e, &b, &o);
     }
@@ -1797,6 +1853,7 @@ int so_serve_frames(so_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
     out->n_frames = nframes; out->n_requests = nq; out->n_responses = nr;
     free(reqs); free(kind); free(rstream);
     free(fid); free(cnt); free(fl); free(ts); free(tg); free(bt); free(st); free(rm); free(wt);
+    free(po); free(vtag); free(vbits);
     if (rc == SF_OK && need > out->cap) return SF_ERR_CAPACITY;
     return rc;
 }

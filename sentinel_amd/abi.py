@@ -33,6 +33,7 @@ SF_MAX_RULES_PER_RESOURCE = 8
 SF_MAX_ARGS = 4
 
 TAG_NULL, TAG_INT, TAG_LONG, TAG_STRING, TAG_DOUBLE, TAG_BOOL, TAG_OTHER, TAG_BYTE, TAG_SHORT, TAG_FLOAT = range(10)
+TAG_COLLECTION = 0x40        # a Collection / array argument: elements listed in the CSR
 
 EV_EXIT, EV_IN, EV_PRIO, EV_ERROR = 0x01, 0x02, 0x04, 0x08
 MEM_HOST, MEM_DEVICE = 0, 1
@@ -109,6 +110,8 @@ class sf_event_batch(C.Structure):
         ("flags", C.c_void_p), ("entry_ref", C.c_void_p), ("create_ts", C.c_void_p),
         ("arg_slots", C.c_uint32), ("n_args", C.c_void_p),
         ("arg_tag", C.c_void_p), ("arg_bits", C.c_void_p),
+        ("arg_elem_off", C.c_void_p), ("elem_tag", C.c_void_p), ("elem_bits", C.c_void_p),
+        ("n_elems", C.c_uint32),
     ]
 
 
@@ -139,6 +142,7 @@ class sf_token_batch(C.Structure):
     _fields_ = [
         ("n", C.c_uint32), ("mem", C.c_int32), ("flow_id", C.c_void_p), ("count", C.c_void_p),
         ("flags", C.c_void_p), ("ts_ms", C.c_void_p), ("param_tag", C.c_void_p), ("param_bits", C.c_void_p),
+        ("param_off", C.c_void_p),
     ]
 
 
@@ -219,7 +223,7 @@ class HostBatch:
     """
 
     def __init__(self, res_id, ts_ms, count, flags, entry_ref=None, create_ts=None,
-                 arg_tag=None, arg_bits=None, n_args=None):
+                 arg_tag=None, arg_bits=None, n_args=None, elem_off=None, elem_tag=None, elem_bits=None):
         self.res_id = np.ascontiguousarray(res_id, dtype=np.uint32)
         self.ts_ms = np.ascontiguousarray(ts_ms, dtype=np.int64)
         self.count = np.ascontiguousarray(count, dtype=np.int32)
@@ -239,6 +243,53 @@ class HostBatch:
         self.arg_bits = arg_bits
         self.n_args = None if n_args is None else np.ascontiguousarray(n_args, dtype=np.uint8)
         self.n = n
+        # collection / array args: elements of arg k = slot*n + i at [elem_off[k], elem_off[k+1])
+        self.elem_off = None if elem_off is None else np.ascontiguousarray(elem_off, dtype=np.uint32)
+        self.elem_tag = None if elem_tag is None else np.ascontiguousarray(elem_tag, dtype=np.uint8)
+        self.elem_bits = None if elem_bits is None else np.ascontiguousarray(elem_bits, dtype=np.uint64)
+        if self.elem_off is not None:
+            assert arg_tag is not None and self.elem_off.shape == (arg_tag.shape[0] * n + 1,)
+            assert self.elem_tag.shape == self.elem_bits.shape == (int(self.elem_off[-1]),)
+
+    @staticmethod
+    def collections(slots, n, values):
+        """(arg_tag, arg_bits, elem_off, elem_tag, elem_bits) from values[slot][i]:
+        None (null), (tag, bits), or a list of (tag, bits) / None elements (a
+        Collection or array)."""
+        at = np.zeros((slots, n), np.uint8)
+        ab = np.zeros((slots, n), np.uint64)
+        off = np.zeros(slots * n + 1, np.uint32)
+        et, eb = [], []
+        for a in range(slots):
+            for i in range(n):
+                v = values[a][i]
+                if isinstance(v, list):
+                    at[a, i] = TAG_COLLECTION
+                    for x in v:
+                        et.append(TAG_NULL if x is None else x[0])
+                        eb.append(0 if x is None else x[1])
+                elif v is not None:
+                    at[a, i], ab[a, i] = v[0], v[1]
+                off[a * n + i + 1] = len(et)
+        return at, ab, off, np.array(et, np.uint8), np.array(eb, np.uint64)
+
+    def _take_args(self, sel):
+        """args of the events sel (ascending), collections re-packed."""
+        at = None if self.arg_tag is None else self.arg_tag[:, sel].copy()
+        ab = None if self.arg_bits is None else self.arg_bits[:, sel].copy()
+        na = None if self.n_args is None else self.n_args[sel]
+        if self.elem_off is None:
+            return at, ab, na, None, None, None
+        slots = self.arg_tag.shape[0]
+        off, et, eb = [0], [], []
+        for a in range(slots):
+            for i in sel:
+                k = a * self.n + int(i)
+                lo, hi = int(self.elem_off[k]), int(self.elem_off[k + 1])
+                et.append(self.elem_tag[lo:hi]); eb.append(self.elem_bits[lo:hi])
+                off.append(off[-1] + hi - lo)
+        cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)  # noqa: E731
+        return at, ab, na, np.array(off, np.uint32), cat(et, np.uint8), cat(eb, np.uint64)
 
     def shard(self, world: int, rank: int) -> "HostBatch":
         """The events of the resources ``res % world == rank`` (hash sharding),
@@ -251,10 +302,9 @@ class HostBatch:
             er = self.entry_ref[sel].copy()
             er[er >= 0] = pos[er[er >= 0]]
             ct = None if self.create_ts is None else self.create_ts[sel].copy()
-        at = None if self.arg_tag is None else self.arg_tag[:, sel].copy()
-        ab = None if self.arg_bits is None else self.arg_bits[:, sel].copy()
-        na = None if self.n_args is None else self.n_args[sel]
-        return HostBatch(self.res_id[sel], self.ts_ms[sel], self.count[sel], self.flags[sel], er, ct, at, ab, na)
+        at, ab, na, eo, et, eb = self._take_args(sel)
+        return HostBatch(self.res_id[sel], self.ts_ms[sel], self.count[sel], self.flags[sel], er, ct, at, ab, na,
+                         eo, et, eb)
 
     def subset(self, lo: int, hi: int) -> "HostBatch":
         """Contiguous slice [lo, hi); entry_ref indices are rebased (refs before lo become -1)."""
@@ -267,11 +317,9 @@ class HostBatch:
             ct[prior] = self.ts_ms[er[prior]]
             er[prior] = -1
             er[er >= lo] -= lo
-        at = None if self.arg_tag is None else self.arg_tag[:, lo:hi].copy()
-        ab = None if self.arg_bits is None else self.arg_bits[:, lo:hi].copy()
-        na = None if self.n_args is None else self.n_args[lo:hi]
+        at, ab, na, eo, et, eb = self._take_args(np.arange(lo, hi))
         return HostBatch(self.res_id[lo:hi], self.ts_ms[lo:hi], self.count[lo:hi], self.flags[lo:hi],
-                         er, ct, at, ab, na)
+                         er, ct, at, ab, na, eo, et, eb)
 
     def c_struct(self) -> sf_event_batch:
         b = sf_event_batch()
@@ -287,6 +335,9 @@ class HostBatch:
         else:
             b.arg_slots = 0
         b.n_args = _ptr(self.n_args)
+        if self.elem_off is not None:
+            b.arg_elem_off, b.elem_tag, b.elem_bits = _ptr(self.elem_off), _ptr(self.elem_tag), _ptr(self.elem_bits)
+            b.n_elems = int(self.elem_off[-1])
         return b
 
 
@@ -304,7 +355,7 @@ class HostVerdicts:
 
 
 class HostTokenBatch:
-    def __init__(self, flow_id, count, flags, ts_ms, param_tag=None, param_bits=None):
+    def __init__(self, flow_id, count, flags, ts_ms, param_tag=None, param_bits=None, param_off=None):
         self.flow_id = np.ascontiguousarray(flow_id, np.int64)
         self.count = np.ascontiguousarray(count, np.int32)
         self.flags = np.ascontiguousarray(flags, np.uint8)
@@ -312,12 +363,17 @@ class HostTokenBatch:
         self.param_tag = None if param_tag is None else np.ascontiguousarray(param_tag, np.uint8)
         self.param_bits = None if param_bits is None else np.ascontiguousarray(param_bits, np.uint64)
         self.n = self.flow_id.shape[0]
+        # Collection<Object> params: request i's values at [param_off[i], param_off[i+1])
+        self.param_off = None if param_off is None else np.ascontiguousarray(param_off, np.uint32)
+        if self.param_off is not None:
+            assert self.param_off.shape == (self.n + 1,) and self.param_tag.shape == (int(self.param_off[-1]),)
 
     def c_struct(self) -> sf_token_batch:
         t = sf_token_batch()
         t.n, t.mem = self.n, MEM_HOST
         t.flow_id, t.count, t.flags, t.ts_ms = (_ptr(self.flow_id), _ptr(self.count), _ptr(self.flags), _ptr(self.ts_ms))
         t.param_tag, t.param_bits = _ptr(self.param_tag), _ptr(self.param_bits)
+        t.param_off = _ptr(self.param_off)
         return t
 
 

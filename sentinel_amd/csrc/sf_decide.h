@@ -448,11 +448,21 @@ SF_HD int64_t pm_thread_get(const ParamTable& pt, uint32_t res, int idx, uint32_
     return s ? s->a : 0;
 }
 
-// ParamFlowChecker.passSingleValueCheck :114-137 (+ default :139-219, throttle :222-273)
+// ParamFlowChecker.passSingleValueCheck :114-137 (+ default :139-219, throttle :222-273).
+// Returns 1 pass, 0 block, 2 for a null element of a collection: the checks
+// before the first map access run, then the map throws NullPointerException,
+// which passLocalCheck catches (:108-110): the value passes, its loop ends.
 SF_HD int param_pass_single(const ParamTable& pt, uint32_t res, int rule_k, const DevParamRule& r,
                             const DevHotItem* items, int64_t now, int32_t acq, uint32_t tag, uint64_t bits,
                             int64_t* wait) {
     int64_t token_count = j_d2l(r.count);
+    if (tag == SF_TAG_NULL) {                                // no hot item is null (ParamFlowRuleUtil.parseHotItems)
+        if (r.grade == SF_GRADE_QPS) {
+            if (token_count == 0) return 0;                  // :156-158 / :236-238
+            if (r.behavior != SF_BEHAVIOR_RATE_LIMITER && acq > wadd(token_count, r.burst)) return 0;   // :160-163
+        }
+        return 2;                                            // putIfAbsent(null) / get(null)
+    }
     bool hot = false; int32_t hot_count = 0;
     for (int k = 0; k < r.item_cnt; k++) {
         const DevHotItem& it = items[r.item_off + k];
@@ -507,6 +517,9 @@ struct SegIO {          // sorted-order batch arrays
     const int64_t* ts; const int32_t* cnt; const uint8_t* flags;
     const int64_t* eref; const int64_t* cts;
     uint32_t arg_slots; const uint8_t* nargs; const uint8_t* atag; const uint64_t* abits; uint32_t n;
+    // collection / array arguments: a sorted arg with tag SF_TAG_COLLECTION has
+    // abits = its index k into the batch's CSR (elements [aoff[k], aoff[k+1]))
+    const uint32_t* aoff; const uint8_t* etag; const uint64_t* ebits;
     uint8_t* v_status; int32_t* v_wait; uint16_t* v_rule;     // sorted order (read back by exits)
     const uint32_t* perm;                                       // sorted -> submission index, or null
     uint8_t* o_status; int32_t* o_wait; uint16_t* o_rule;       // the caller's verdicts (submission order)
@@ -519,6 +532,41 @@ SF_HD void emit_verdict(const SegIO& io, uint32_t j, uint8_t status, int32_t wai
     io.o_status[i] = status;
     if (io.o_wait) io.o_wait[i] = wait;
     if (io.o_rule) io.o_rule[i] = rule;
+}
+
+// ParamFlowChecker.passLocalCheck (:84-112): one value, or every element of a
+// collection / array in order (the tokens of the elements before a failing one
+// stay consumed).  Waits of throttled elements add up (each sleeps).
+SF_HD int param_pass_value(const ParamTable& pt, uint32_t res, int rule_k, const DevParamRule& r,
+                           const DevHotItem* items, int64_t now, int32_t acq, uint32_t tag, uint64_t bits,
+                           const SegIO& io, int64_t* wait) {
+    if (tag != SF_TAG_COLLECTION) return param_pass_single(pt, res, rule_k, r, items, now, acq, tag, bits, wait) != 0;
+    for (uint32_t e = io.aoff[bits], e1 = io.aoff[bits + 1]; e < e1; e++) {
+        int64_t w = 0;
+        const int ok = param_pass_single(pt, res, rule_k, r, items, now, acq, io.etag[e], io.ebits[e], &w);
+        if (ok == 0) return 0;
+        if (ok == 2) return 1;
+        if (w > 0) *wait += w;
+    }
+    return 1;
+}
+
+// ParameterMetric.addThreadCount / decreaseThreadCount (:125-239) over the
+// event's args with a thread map (pm_init): a null arg is skipped, a
+// collection counts each element; a null element throws, which ends the whole
+// callback (the outer try around every index).
+SF_HD void pm_thread_event(const ParamTable& pt, uint32_t res, uint8_t pm_init, const SegIO& io, uint32_t j,
+                           uint32_t na, int delta) {
+    for (uint32_t a = 0; a < na && a < 8; a++) {
+        if (!((pm_init >> a) & 1)) continue;
+        const uint32_t tg = io.atag[(size_t)a * io.n + j];
+        const uint64_t bt = io.abits[(size_t)a * io.n + j];
+        if (tg != SF_TAG_COLLECTION) { pm_thread_add(pt, res, (int)a, tg, bt, delta); continue; }
+        for (uint32_t e = io.aoff[bt], e1 = io.aoff[bt + 1]; e < e1; e++) {
+            if (io.etag[e] == SF_TAG_NULL) return;
+            pm_thread_add(pt, res, (int)a, io.etag[e], io.ebits[e], delta);
+        }
+    }
 }
 
 SF_HD bool v_blocked(uint8_t v) { return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM; }
@@ -578,10 +626,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
                 nd.add_rt_success(now, rt, c);                  // recordCompleteFor :167-178
                 nd.threads--;
                 if (fl & SF_EV_ERROR) nd.add_exception(now, c);
-                if (pm_exists)                                  // ParamFlowStatisticExitCallback
-                    for (uint32_t a = 0; a < na; a++)
-                        if (a < 8 && (pm_init >> a) & 1)
-                            pm_thread_add(pt, res, (int)a, io.atag[(size_t)a * io.n + j], io.abits[(size_t)a * io.n + j], -1);
+                if (pm_exists) pm_thread_event(pt, res, pm_init, io, j, na, -1);   // ParamFlowStatisticExitCallback
                 status = SF_V_EXIT;
             } else {
                 status = SF_V_EXIT_IGNORED;
@@ -613,7 +658,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
                 uint64_t bt = io.abits[(size_t)pr.param_idx * io.n + j];
                 if (tg == SF_TAG_NULL) continue;
                 int64_t w = 0;
-                if (!param_pass_single(pt, res, k, pr, st.items, now, c, tg, bt, &w)) {
+                if (!param_pass_value(pt, res, k, pr, st.items, now, c, tg, bt, io, &w)) {
                     blocked = true; status = SF_V_BLOCK_PARAM; rule_idx = k;
                 } else if (w > 0) {
                     wait += w;
@@ -640,10 +685,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
             else {
                 nd.add_pass(now, c); status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS;
             }
-            if (pm_exists)
-                for (uint32_t a = 0; a < na; a++)
-                    if (a < 8 && (pm_init >> a) & 1)
-                        pm_thread_add(pt, res, (int)a, io.atag[(size_t)a * io.n + j], io.abits[(size_t)a * io.n + j], +1);
+            if (pm_exists) pm_thread_event(pt, res, pm_init, io, j, na, +1);
         }
         io.v_status[j] = status;
         if (io.v_wait) io.v_wait[j] = (int32_t)wait;

@@ -161,7 +161,7 @@ void sf_destroy(sf_engine* e) {
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
-                     (void*)e->ts.items, e->tok_stage, e->wire_arena, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
+                     (void*)e->ts.items, e->ts.rmulti, e->tok_stage, e->wire_arena, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
                      e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch, e->st.last_ts, e->nm_bytes, e->nm_off,
                      e->nm_types, e->ml_mask, e->ml_counts, e->ml_offsets, e->ml_total, e->ml_rows, e->ml_keys,
                      e->ml_order, e->ml_len, e->ml_off, e->ml_bytes, e->ml_out, e->ml_tmp};
@@ -529,6 +529,8 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
     if (in->arg_slots > SF_MAX_ARGS || (in->arg_slots && (!in->arg_tag || !in->arg_bits)))
         return fail(SF_ERR_INVALID, "bad arg arrays");
+    if (in->arg_elem_off && in->n_elems && (!in->elem_tag || !in->elem_bits))
+        return fail(SF_ERR_INVALID, "collection arguments without element arrays");
     const uint32_t n = in->n;
     DevBatch b{};
     b.n = n; b.arg_slots = in->arg_slots;
@@ -561,6 +563,10 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         size_t o_na = need; need += in->n_args ? align_up((size_t)n) : 0;
         size_t o_at = need; need += align_up((size_t)n * in->arg_slots);
         size_t o_ab = need; need += align_up((size_t)n * in->arg_slots * 8);
+        const bool coll = in->arg_elem_off != nullptr;
+        size_t o_eo = need; need += coll ? align_up(((size_t)n * in->arg_slots + 1) * 4) : 0;
+        size_t o_et = need; need += coll ? align_up((size_t)in->n_elems) : 0;
+        size_t o_eb = need; need += coll ? align_up((size_t)in->n_elems * 8) : 0;
         if (need > e->stage_in_bytes) {
             if (e->stage_in) hipFree(e->stage_in);
             e->stage_in = nullptr;
@@ -582,10 +588,16 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         b.nargs = (const uint8_t*)up(o_na, in->n_args, n);
         b.atag = (const uint8_t*)up(o_at, in->arg_tag, (size_t)n * in->arg_slots);
         b.abits = (const uint64_t*)up(o_ab, in->arg_bits, (size_t)n * in->arg_slots * 8);
+        if (coll) {
+            b.aoff = (const uint32_t*)up(o_eo, in->arg_elem_off, ((size_t)n * in->arg_slots + 1) * 4);
+            b.etag = (const uint8_t*)up(o_et, in->elem_tag, in->n_elems);
+            b.ebits = (const uint64_t*)up(o_eb, in->elem_bits, (size_t)in->n_elems * 8);
+        }
     } else {
         b.res = in->res_id; b.ts = in->ts_ms; b.cnt = in->count; b.flags = in->flags;
         b.eref = in->entry_ref; b.cts = in->entry_ref ? in->create_ts : nullptr;
         b.nargs = in->n_args; b.atag = in->arg_tag; b.abits = in->arg_bits;
+        b.aoff = in->arg_elem_off; b.etag = in->elem_tag; b.ebits = in->elem_bits;
     }
     DevVerdicts dv{};
     if (out->mem == SF_MEM_HOST) {
@@ -1001,6 +1013,8 @@ static int tok_rebuild(sf_engine* e, bool reset_state) {
     if ((rc = upload((void**)&ts.idtab, tab.data(), tab.size() * sizeof(IdSlot)))) return rc;
     if ((rc = upload((void**)&ts.ns, ns.data(), ns.size() * sizeof(ClNs)))) return rc;
     if ((rc = upload((void**)&ts.items, items.data(), items.size() * sizeof(DevHotItem)))) return rc;
+    if (ts.rmulti) { hipFree(ts.rmulti); ts.rmulti = nullptr; }
+    HIP_TRY(hipMalloc((void**)&ts.rmulti, std::max<size_t>(rules.size(), 16)));   // per-call multi-value flags
     ts.id_mask = cap - 1;
     ts.n_flow = nf; ts.n_rules = nf + np; ts.n_ns = (uint32_t)ns.size();
     if (reset_state) {
@@ -1102,10 +1116,18 @@ int sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* 
     TokBatch b{};
     b.n = n;
     const bool has_param = in->param_tag != nullptr;
+    // Collection params: the value arrays hold param_off[n] elements
+    uint32_t n_vals = n;
+    if (in->param_off) {
+        if (in->mem == SF_MEM_HOST) n_vals = in->param_off[n];
+        else HIP_TRY(hipMemcpy(&n_vals, in->param_off + n, 4, hipMemcpyDeviceToHost));
+    }
     // staging: inputs then outputs, 256-B aligned
     size_t off_fid = 0, off_cnt = align_up(off_fid + (size_t)n * 8), off_fl = align_up(off_cnt + (size_t)n * 4),
            off_ts = align_up(off_fl + n), off_tag = align_up(off_ts + (size_t)n * 8),
-           off_bits = align_up(off_tag + (has_param ? n : 0)), off_st = align_up(off_bits + (has_param ? (size_t)n * 8 : 0)),
+           off_bits = align_up(off_tag + (has_param ? n_vals : 0)),
+           off_po = align_up(off_bits + (has_param ? (size_t)n_vals * 8 : 0)),
+           off_st = align_up(off_po + (in->param_off ? ((size_t)n + 1) * 4 : 0)),
            off_rem = align_up(off_st + n), off_wt = align_up(off_rem + (size_t)n * 4), need = align_up(off_wt + (size_t)n * 4);
     if (need > e->tok_stage_bytes) {
         if (e->tok_stage) hipFree(e->tok_stage);
@@ -1119,17 +1141,20 @@ int sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* 
         HIP_TRY(hipMemcpyAsync(base + off_cnt, in->count, (size_t)n * 4, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(base + off_fl, in->flags, n, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(base + off_ts, in->ts_ms, (size_t)n * 8, hipMemcpyHostToDevice, s));
-        if (has_param) {
-            HIP_TRY(hipMemcpyAsync(base + off_tag, in->param_tag, n, hipMemcpyHostToDevice, s));
-            HIP_TRY(hipMemcpyAsync(base + off_bits, in->param_bits, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        if (has_param && n_vals) {
+            HIP_TRY(hipMemcpyAsync(base + off_tag, in->param_tag, n_vals, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(base + off_bits, in->param_bits, (size_t)n_vals * 8, hipMemcpyHostToDevice, s));
         }
+        if (in->param_off)
+            HIP_TRY(hipMemcpyAsync(base + off_po, in->param_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s));
         b.flow_id = (const int64_t*)(base + off_fid); b.count = (const int32_t*)(base + off_cnt);
         b.flags = (const uint8_t*)(base + off_fl); b.ts = (const int64_t*)(base + off_ts);
         b.ptag = has_param ? (const uint8_t*)(base + off_tag) : nullptr;
         b.pbits = has_param ? (const uint64_t*)(base + off_bits) : nullptr;
+        b.poff = in->param_off ? (const uint32_t*)(base + off_po) : nullptr;
     } else {
         b.flow_id = in->flow_id; b.count = in->count; b.flags = in->flags; b.ts = in->ts_ms;
-        b.ptag = in->param_tag; b.pbits = in->param_bits;
+        b.ptag = in->param_tag; b.pbits = in->param_bits; b.poff = in->param_off;
     }
     TokOut o{};
     const bool host_out = out->mem == SF_MEM_HOST;
@@ -1200,7 +1225,8 @@ int sf_serve_frames(sf_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
                  o_rsc = take(((size_t)S + 1) * 4), o_fr = take((size_t)F * 4), o_wf = take((size_t)F * sizeof(WFrame)),
                  o_fl = take((size_t)F * 8), o_pos = take((size_t)F * 8), o_cnt = take(16),
                  o_qf = take((size_t)F * 8), o_qc = take((size_t)F * 4), o_qfl = take(F), o_qts = take((size_t)F * 8),
-                 o_qtg = take(F), o_qb = take((size_t)F * 8), o_rs = take(F), o_rr = take((size_t)F * 4),
+                 o_qtg = take(n), o_qb = take((size_t)n * 8), o_rs = take(F), o_rr = take((size_t)F * 4),
+                 o_nv = take((size_t)F * 4), o_qnv = take(((size_t)F + 1) * 4), o_qpo = take(((size_t)F + 1) * 4),
                  o_rw = take((size_t)F * 4), o_resp = take((size_t)F * 16), o_sb = take(S),
                  o_crel = take((size_t)S * 8), o_tmp = take(tmp);
     if (off > e->wire_bytes) {
@@ -1224,6 +1250,7 @@ int sf_serve_frames(sf_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
     w.pos = (uint64_t*)(A + o_pos); w.counters = (uint32_t*)(A + o_cnt);
     w.q_fid = (int64_t*)(A + o_qf); w.q_cnt = (int32_t*)(A + o_qc); w.q_flags = (uint8_t*)(A + o_qfl);
     w.q_ts = (int64_t*)(A + o_qts); w.q_tag = (uint8_t*)(A + o_qtg); w.q_bits = (uint64_t*)(A + o_qb);
+    w.nval = (uint32_t*)(A + o_nv); w.q_nval = (uint32_t*)(A + o_qnv); w.q_poff = (uint32_t*)(A + o_qpo);
     w.r_status = (int8_t*)(A + o_rs); w.r_rem = (int32_t*)(A + o_rr); w.r_wait = (int32_t*)(A + o_rw);
     w.resp = (uint8_t*)(A + o_resp); w.stop = (uint8_t*)(A + o_sb); w.consumed_rel = (uint64_t*)(A + o_crel);
     w.tmp = A + o_tmp; w.tmp_bytes = tmp;
@@ -1251,11 +1278,11 @@ int sf_serve_frames(sf_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
     if (n_req) {
         int rc = tok_work_ensure(e, n_req);
         if (rc) return fail(rc, "token work buffers");
-        le = wire_compact(w, nf, in->now_ms, st);
+        le = wire_compact(w, nf, n_req, in->now_ms, st);
         if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("wire compact: ") + hipGetErrorString(le));
         TokBatch b{};
         b.n = n_req; b.flow_id = w.q_fid; b.count = w.q_cnt; b.flags = w.q_flags; b.ts = w.q_ts;
-        b.ptag = w.q_tag; b.pbits = w.q_bits;
+        b.ptag = w.q_tag; b.pbits = w.q_bits; b.poff = w.q_poff;
         TokOut o{w.r_status, w.r_rem, w.r_wait};
         le = tok_launch(e->ts, e->tw, b, o, st);
         if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("token launch: ") + hipGetErrorString(le));

@@ -172,6 +172,7 @@ struct DevBatch {
     const int64_t* eref; const int64_t* cts;
     uint32_t arg_slots; const uint8_t* nargs; const uint8_t* atag; const uint64_t* abits;
     uint32_t arg_stride;           // slot stride of atag / abits (the whole batch's n)
+    const uint32_t* aoff; const uint8_t* etag; const uint64_t* ebits;   // collection elements (batch-wide CSR)
     int64_t base;                  // index of the view's first event in the batch (0: whole batch)
     const uint8_t* sys;            // planner verdicts of IN entries (SYS_NONE: none), or null
     const uint8_t* vprev;          // verdicts of the batch (decided before the view), or null

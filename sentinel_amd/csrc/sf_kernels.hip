@@ -89,8 +89,11 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* wide, u
     if (b.arg_slots) {
         if (b.nargs) s_nargs[j] = b.nargs[i];
         for (uint32_t a = 0; a < b.arg_slots; a++) {
-            s_atag[(size_t)a * b.n + j] = b.atag[(size_t)a * b.arg_stride + i];
-            s_abits[(size_t)a * b.n + j] = b.abits[(size_t)a * b.arg_stride + i];
+            const uint8_t tg = b.atag[(size_t)a * b.arg_stride + i];
+            s_atag[(size_t)a * b.n + j] = tg;
+            // a collection argument carries its index into the batch's element CSR
+            s_abits[(size_t)a * b.n + j] = tg == SF_TAG_COLLECTION ? (uint64_t)a * b.arg_stride + (uint64_t)b.base + i
+                                                                  : b.abits[(size_t)a * b.arg_stride + i];
         }
     }
 }
@@ -733,6 +736,7 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     io.eref = b.eref ? w.s_eref : nullptr; io.cts = b.eref ? w.s_cts : nullptr;
     io.arg_slots = b.arg_slots; io.nargs = (b.arg_slots && b.nargs) ? w.s_nargs : nullptr;
     io.atag = w.s_atag; io.abits = w.s_abits; io.n = n;
+    io.aoff = b.aoff; io.etag = b.etag; io.ebits = b.ebits;
     io.v_status = w.v_status; io.v_wait = w.v_wait; io.v_rule = w.v_rule;
     io.perm = w.perm; io.o_status = out.status; io.o_wait = out.wait; io.o_rule = out.rule;
     HeavyCtx hc = heavy_ctx(w);

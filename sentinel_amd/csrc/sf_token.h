@@ -63,12 +63,14 @@ struct TokState {
     const DevHotItem* items;
     double exceed_count, max_occupy_ratio;
     int32_t* err;
+    uint8_t* rmulti;             // [n_rules] per call: a param rule with a multi-value request (serial group)
 };
 
 struct TokBatch {
     uint32_t n;
     const int64_t* flow_id; const int32_t* count; const uint8_t* flags; const int64_t* ts;
     const uint8_t* ptag; const uint64_t* pbits;
+    const uint32_t* poff;        // [n+1] Collection<Object> params (values at [poff[i], poff[i+1])), or null
 };
 struct TokOut { int8_t* status; int32_t* remaining; int32_t* wait; };
 

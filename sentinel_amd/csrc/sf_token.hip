@@ -35,6 +35,7 @@ namespace sf {
 constexpr uint8_t NS_NONE = 0xff;
 constexpr uint64_t KEY_NONE = ~0ull;
 constexpr uint64_t KEY_PARAM = 1ull << 63;
+constexpr uint64_t KEY_SERIAL = 1ull << 62;     // every request of one param rule, in time order
 constexpr int8_t TOK_PENDING = 100;
 
 static inline unsigned tblocks(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
@@ -61,13 +62,17 @@ __global__ void k_tok_prep(TokState ts, TokBatch b, TokWork w, TokOut out) {
     const bool param = (b.flags[i] & SF_TOK_PARAM) != 0;
     int8_t st = TOK_PENDING;
     uint8_t nk = NS_NONE;
-    if (id <= 0 || c <= 0 || (param && (!b.ptag || !b.pbits))) {
+    const uint32_t nv = (param && b.poff) ? b.poff[i + 1] - b.poff[i] : 1u;
+    if (id <= 0 || c <= 0 || (param && (!b.ptag || !b.pbits || nv == 0))) {
         st = SF_TOKEN_BAD_REQUEST;                          // notValidRequest / params empty :66-72
     } else {
         const int32_t r = id_lookup(ts, id, param);
         if (r < 0) st = SF_TOKEN_NO_RULE_EXISTS;           // getFlowRuleById == null :45-47
         else {
             w.rule_of[i] = (uint32_t)r;
+            // a request with several values couples them (all must pass before any is
+            // added): that rule's requests are decided by one lane in time order
+            if (nv > 1) ts.rmulti[r] = 1;
             const int32_t ns = ts.rules[r].ns;
             if (ns >= 0 && ts.ns[ns].has_limiter) nk = (uint8_t)ns;   // else GlobalRequestLimiter passes
         }
@@ -188,8 +193,10 @@ __global__ void k_tok_keys(TokState ts, TokBatch b, TokWork w, TokOut out) {
     if (w.pending[i]) {
         const uint32_t r = w.rule_of[i];
         const ClRule& rule = ts.rules[r];
+        const uint32_t v0 = b.poff ? b.poff[i] : i;
         if (!rule.is_param) key = r;
-        else if (b.ptag[i] == SF_TAG_NULL) {
+        else if (ts.rmulti[r]) key = KEY_SERIAL | r;
+        else if (b.ptag[v0] == SF_TAG_NULL) {
             // a null value has no metric: getSum(null) == 0 and addValue(null) adds nothing
             // (ClusterParamMetric.java:52-55,72-75), so the decision needs no state
             const int32_t connected = rule.ns >= 0 ? ts.ns[rule.ns].connected : 0;
@@ -202,8 +209,8 @@ __global__ void k_tok_keys(TokState ts, TokBatch b, TokWork w, TokOut out) {
             out.remaining[i] = next >= 0 ? j_d2i(next) : 0;
             out.wait[i] = 0;
         } else {
-            const uint64_t hi = ((uint64_t)(r + 1) << 32) | b.ptag[i];
-            const uint32_t slot = cp_find_or_insert(ts, hi, b.pbits[i]);
+            const uint64_t hi = ((uint64_t)(r + 1) << 32) | b.ptag[v0];
+            const uint32_t slot = cp_find_or_insert(ts, hi, b.pbits[v0]);
             if (slot != 0xffffffffu) key = KEY_PARAM | slot;
         }
     }
@@ -311,6 +318,81 @@ __device__ void flow_decide(ClMetric& m, const ClRule& r, const TokState& ts, in
     *st = SF_TOKEN_BLOCKED; *rem = 0; *wt = 0;
 }
 
+// one value's column of ClusterParameterLeapArray: getSum(value) at t (:52-66)
+// and addValue(value, c) (:72-84) -- only the value's own adds are counted
+__device__ __forceinline__ int64_t cp_sum(const CpSlot& s, int S, int wl, int I, int64_t t) {
+    const int idx = (int)((t / wl) % S);
+    const int64_t ws = t - t % wl;
+    int64_t sum = 0;
+    for (int k = 0; k < S; k++) {
+        if (k == idx) { if (s.ws[k] == ws) sum = wadd(sum, s.cnt[k]); }
+        else if (s.ws[k] != WS_NONE && !(wsub(t, s.ws[k]) > I)) sum = wadd(sum, s.cnt[k]);
+    }
+    return sum;
+}
+__device__ __forceinline__ void cp_add(CpSlot& s, int S, int wl, int64_t t, int32_t c) {
+    const int idx = (int)((t / wl) % S);
+    const int64_t ws = t - t % wl;
+    if (s.ws[idx] != ws) {
+        if (ws < s.ws[idx]) return;                              // throwaway window
+        s.ws[idx] = ws; s.cnt[idx] = 0;
+    }
+    s.cnt[idx] = wadd(s.cnt[idx], c);
+}
+// getRawThreshold (:110-117) + calcGlobalThreshold (:97-108)
+__device__ __forceinline__ double cp_threshold(const TokState& ts, const ClRule& rule, int32_t connected, uint8_t tag,
+                                               uint64_t bits) {
+    double raw = rule.count;
+    for (uint32_t k = 0; k < rule.item_cnt; k++) {
+        const DevHotItem& it = ts.items[rule.item_off + k];
+        if (it.tag == tag && it.bits == bits) { raw = it.count; break; }
+    }
+    return rule.threshold_type == SF_THRESHOLD_GLOBAL ? raw : raw * connected;
+}
+
+// ClusterParamFlowChecker.acquireClusterToken (:42-87) for every request of one
+// param rule that has multi-value requests in this batch, in time order: each
+// value needs room (the first without stops the check), then every value is
+// added; remaining is -1 for more than one value.  Value columns are found /
+// claimed in the exact table as the single-value path does.
+__device__ void tok_serial_rule(const TokState& ts, const TokBatch& b, const TokWork& w, const TokOut& out, uint32_t r,
+                                uint32_t lo, uint32_t hi) {
+    const ClRule rule = ts.rules[r];
+    const int32_t connected = rule.ns >= 0 ? ts.ns[rule.ns].connected : 0;
+    const double isec = rule.interval / 1000.0;
+    for (uint32_t j = lo; j < hi; j++) {
+        const uint32_t i = w.idx_out[j];
+        const int64_t t = b.ts[i];
+        const int32_t c = b.count[i];
+        const uint32_t v0 = b.poff ? b.poff[i] : i, v1 = b.poff ? b.poff[i + 1] : i + 1;
+        double rem = -1;
+        bool passed = true;
+        for (uint32_t v = v0; v < v1; v++) {
+            const uint8_t tg = b.ptag[v];
+            int64_t sum = 0;
+            if (tg != SF_TAG_NULL) {                             // getSum(null) == 0
+                const uint32_t sl = cp_find_or_insert(ts, ((uint64_t)(r + 1) << 32) | tg, b.pbits[v]);
+                if (sl == 0xffffffffu) { passed = false; break; }
+                sum = cp_sum(ts.cptab[sl], rule.S, rule.wl, rule.interval, t);
+            }
+            rem = cp_threshold(ts, rule, connected, tg, b.pbits[v]) - (double)sum / isec - c;
+            if (rem < 0) { passed = false; break; }
+        }
+        if (passed) {
+            for (uint32_t v = v0; v < v1; v++) {
+                if (b.ptag[v] == SF_TAG_NULL) continue;          // addValue(null) adds nothing
+                const uint32_t sl = cp_find_or_insert(ts, ((uint64_t)(r + 1) << 32) | b.ptag[v], b.pbits[v]);
+                if (sl != 0xffffffffu) cp_add(ts.cptab[sl], rule.S, rule.wl, t, c);
+            }
+            if (v1 - v0 > 1) rem = -1;
+            out.status[i] = SF_TOKEN_OK; out.remaining[i] = j_d2i(rem);
+        } else {
+            out.status[i] = SF_TOKEN_BLOCKED; out.remaining[i] = 0;
+        }
+        out.wait[i] = 0;
+    }
+}
+
 constexpr int TD_T = 64;     // lanes per workgroup of k_tok_decide (LDS: one ClFlowState per lane)
 
 __global__ void __launch_bounds__(TD_T) k_tok_decide(TokState ts, TokBatch b, TokWork w, TokOut out) {
@@ -319,6 +401,7 @@ __global__ void __launch_bounds__(TD_T) k_tok_decide(TokState ts, TokBatch b, To
     if (sg >= *w.n_seg) return;
     const uint32_t lo = w.seg_start[sg], hi = w.seg_start[sg + 1];
     const uint64_t key = w.key_out[lo];
+    if (key & KEY_SERIAL) { tok_serial_rule(ts, b, w, out, (uint32_t)(key & 0xffffffffu), lo, hi); return; }
     if (!(key & KEY_PARAM)) {
         const uint32_t r = (uint32_t)key;
         const ClRule rule = ts.rules[r];
@@ -342,34 +425,16 @@ __global__ void __launch_bounds__(TD_T) k_tok_decide(TokState ts, TokBatch b, To
     const uint64_t bits = slot.lo;
     const ClRule rule = ts.rules[r];
     const int32_t connected = rule.ns >= 0 ? ts.ns[rule.ns].connected : 0;
-    double raw = rule.count;                                     // getRawThreshold :110-117
-    for (uint32_t k = 0; k < rule.item_cnt; k++) {
-        const DevHotItem& it = ts.items[rule.item_off + k];
-        if (it.tag == tag && it.bits == bits) { raw = it.count; break; }
-    }
-    const double thr = rule.threshold_type == SF_THRESHOLD_GLOBAL ? raw : raw * connected;
+    const double thr = cp_threshold(ts, rule, connected, tag, bits);
     const int S = rule.S, wl = rule.wl, I = rule.interval;
     const double isec = rule.interval / 1000.0;
-    int64_t* wsv = slot.ws;
-    int64_t* cnt = slot.cnt;
     for (uint32_t j = lo; j < hi; j++) {
         const uint32_t i = w.idx_out[j];
         const int64_t t = b.ts[i];
         const int32_t c = b.count[i];
-        const int idx = (int)((t / wl) % S);
-        const int64_t ws = t - t % wl;
-        int64_t sum = 0;                                         // ClusterParamMetric.getSum(value)
-        for (int k = 0; k < S; k++) {
-            if (k == idx) { if (wsv[k] == ws) sum = wadd(sum, cnt[k]); }
-            else if (wsv[k] != WS_NONE && !(wsub(t, wsv[k]) > I)) sum = wadd(sum, cnt[k]);
-        }
-        const double next = thr - (double)sum / isec - c;
+        const double next = thr - (double)cp_sum(slot, S, wl, I, t) / isec - c;   // getSum(value)
         if (next >= 0) {
-            if (wsv[idx] != ws) {
-                if (ws > wsv[idx]) { wsv[idx] = ws; cnt[idx] = 0; }
-                else { out.status[i] = SF_TOKEN_OK; out.remaining[i] = j_d2i(next); out.wait[i] = 0; continue; }
-            }
-            cnt[idx] = wadd(cnt[idx], c);                        // addValue :72-84
+            cp_add(slot, S, wl, t, c);                           // addValue :72-84
             out.status[i] = SF_TOKEN_OK; out.remaining[i] = j_d2i(next);
         } else {
             out.status[i] = SF_TOKEN_BLOCKED; out.remaining[i] = 0;
@@ -419,6 +484,7 @@ hipError_t tok_launch(const TokState& ts, TokWork& w, const TokBatch& b, const T
     const uint32_t n = b.n;
     if (!n) return hipSuccess;
     const unsigned T = 256;
+    hipMemsetAsync(ts.rmulti, 0, ts.n_rules ? ts.n_rules : 1, s);
     hipLaunchKernelGGL(k_tok_prep, dim3(tblocks(n, T)), dim3(T), 0, s, ts, b, w, out);
     bool any_limiter = false;   // known on the host through n_ns (the table may have none with a limiter)
     any_limiter = ts.n_ns > 0;

@@ -56,6 +56,10 @@ struct WireBufs {
     uint32_t* counters;         // [0] frames handled
     // token batch built from the frames (capacity = max frames)
     int64_t* q_fid; int32_t* q_cnt; uint8_t* q_flags; int64_t* q_ts; uint8_t* q_tag; uint64_t* q_bits;
+    // parameter Collection of each request: q_poff (exclusive scan of q_nval), values in q_tag / q_bits
+    uint32_t* nval;             // [max frames] decoded parameters of a PARAM_FLOW frame (0 otherwise)
+    uint32_t* q_nval;           // [max frames + 1]
+    uint32_t* q_poff;           // [max frames + 1]
     int8_t* r_status; int32_t* r_rem; int32_t* r_wait;
     uint8_t* resp;              // [max frames * 16]
     uint8_t* stop;              // [S]
@@ -69,8 +73,8 @@ hipError_t wire_query_temp(uint32_t n_tiles, uint32_t S, uint32_t max_frames, si
 hipError_t wire_frame(const WireBufs& w, hipStream_t s);
 // frame list, decode, stop offsets, request/response ranks (pos[nf-1] + fl[nf-1] = totals)
 hipError_t wire_decode(const WireBufs& w, uint32_t nf, int64_t now_ms, hipStream_t s);
-// token batch arrays of the requests
-hipError_t wire_compact(const WireBufs& w, uint32_t nf, int64_t now_ms, hipStream_t s);
+// token batch arrays of the requests (n_req of them), parameters as one CSR
+hipError_t wire_compact(const WireBufs& w, uint32_t nf, uint32_t n_req, int64_t now_ms, hipStream_t s);
 // response frames and per-stream results
 hipError_t wire_encode(const WireBufs& w, uint32_t nf, hipStream_t s);
 

@@ -196,7 +196,56 @@ __global__ void __launch_bounds__(256) k_wire_emit(WireBufs w) {
 // PARAM_TYPE_INTEGER 0, LONG 1, BYTE 2, DOUBLE 3, FLOAT 4, SHORT 5,
 // BOOLEAN 6, STRING 7).  WC_HOST where the reference's outcome depends on
 // more than this frame (sentinel_flow.h).
-__device__ uint8_t wire_decode_body(const uint8_t* b, uint32_t L, WFrame& f) {
+// The parameters of a PARAM_FLOW body (q: the data after xid and type, rem
+// bytes; amount entries from offset 16): values written to tag / bits when
+// given.  Returns how many decodeParam accepted, or -1 where the reference's
+// outcome depends on more than the frame (bytes short or left over).
+__device__ int wire_params(const uint8_t* q, uint32_t rem, int32_t amount, uint8_t* otag, uint64_t* obits) {
+    uint32_t p = 16;
+    int n = 0;
+    for (int32_t k = 0; k < amount; k++) {
+        if (p + 1 > rem) return -1;
+        const uint8_t ty = q[p++];
+        uint8_t tag = 0; uint64_t bits = 0; bool ok = true;
+        switch (ty) {
+        case 0: if (p + 4 > rem) return -1; tag = SF_TAG_INT; bits = (uint64_t)(int64_t)(int32_t)rd32(q + p); p += 4; break;
+        case 1: if (p + 8 > rem) return -1; tag = SF_TAG_LONG; bits = rd64(q + p); p += 8; break;
+        case 2: if (p + 1 > rem) return -1; tag = SF_TAG_BYTE; bits = (uint64_t)(int64_t)(int8_t)q[p]; p += 1; break;
+        case 3: {
+            if (p + 8 > rem) return -1;
+            uint64_t x = rd64(q + p); p += 8;
+            if ((x & 0x7ff0000000000000ULL) == 0x7ff0000000000000ULL && (x & 0x000fffffffffffffULL))
+                x = 0x7ff8000000000000ULL;                   // Double.equals: doubleToLongBits
+            tag = SF_TAG_DOUBLE; bits = x; break;
+        }
+        case 4: {
+            if (p + 4 > rem) return -1;
+            uint32_t x = rd32(q + p); p += 4;
+            if ((x & 0x7f800000u) == 0x7f800000u && (x & 0x007fffffu)) x = 0x7fc00000u;   // floatToIntBits
+            tag = SF_TAG_FLOAT; bits = x; break;
+        }
+        case 5: if (p + 2 > rem) return -1; tag = SF_TAG_SHORT;
+            bits = (uint64_t)(int64_t)(int16_t)(((uint32_t)q[p] << 8) | q[p + 1]); p += 2; break;
+        case 6: if (p + 1 > rem) return -1; tag = SF_TAG_BOOL; bits = q[p] != 0; p += 1; break;
+        case 7: {
+            if (p + 4 > rem) return -1;
+            const int32_t sl = (int32_t)rd32(q + p); p += 4;
+            if (sl < 0 || (uint32_t)sl > rem - p) return -1;
+            uint64_t h = 0xcbf29ce484222325ULL;              // sf_string_key: FNV-1a 64
+            for (int32_t j = 0; j < sl; j++) { h ^= q[p + j]; h *= 0x100000001b3ULL; }
+            tag = SF_TAG_STRING; bits = h; p += (uint32_t)sl; break;
+        }
+        default: ok = false;                                 // decodeParam returns false
+        }
+        if (ok) {
+            if (otag) { otag[n] = tag; obits[n] = bits; }
+            n++;
+        }
+    }
+    return p == rem ? n : -1;
+}
+
+__device__ uint8_t wire_decode_body(const uint8_t* b, uint32_t L, WFrame& f, uint32_t* nval) {
     if (L == 0) return WC_NONE;                              // nothing readable
     if (L < 5) return WC_HOST;                               // decode() null, bytes stay cumulated
     f.xid = (int32_t)rd32(b);
@@ -220,47 +269,10 @@ __device__ uint8_t wire_decode_body(const uint8_t* b, uint32_t L, WFrame& f) {
         const int32_t amount = (int32_t)rd32(q + 12);
         if (amount <= 0) return rem == 16 ? WC_NONE : WC_HOST;
         if ((uint32_t)amount > rem - 16) return WC_HOST;    // each parameter reads >= 1 byte
-        uint32_t p = 16;
-        int n = 0;
-        for (int32_t k = 0; k < amount; k++) {
-            if (p + 1 > rem) return WC_HOST;
-            const uint8_t ty = q[p++];
-            uint8_t tag = 0; uint64_t bits = 0; bool ok = true;
-            switch (ty) {
-            case 0: if (p + 4 > rem) return WC_HOST; tag = SF_TAG_INT; bits = (uint64_t)(int64_t)(int32_t)rd32(q + p); p += 4; break;
-            case 1: if (p + 8 > rem) return WC_HOST; tag = SF_TAG_LONG; bits = rd64(q + p); p += 8; break;
-            case 2: if (p + 1 > rem) return WC_HOST; tag = SF_TAG_BYTE; bits = (uint64_t)(int64_t)(int8_t)q[p]; p += 1; break;
-            case 3: {
-                if (p + 8 > rem) return WC_HOST;
-                uint64_t x = rd64(q + p); p += 8;
-                if ((x & 0x7ff0000000000000ULL) == 0x7ff0000000000000ULL && (x & 0x000fffffffffffffULL))
-                    x = 0x7ff8000000000000ULL;               // Double.equals: doubleToLongBits
-                tag = SF_TAG_DOUBLE; bits = x; break;
-            }
-            case 4: {
-                if (p + 4 > rem) return WC_HOST;
-                uint32_t x = rd32(q + p); p += 4;
-                if ((x & 0x7f800000u) == 0x7f800000u && (x & 0x007fffffu)) x = 0x7fc00000u;   // floatToIntBits
-                tag = SF_TAG_FLOAT; bits = x; break;
-            }
-            case 5: if (p + 2 > rem) return WC_HOST; tag = SF_TAG_SHORT;
-                bits = (uint64_t)(int64_t)(int16_t)(((uint32_t)q[p] << 8) | q[p + 1]); p += 2; break;
-            case 6: if (p + 1 > rem) return WC_HOST; tag = SF_TAG_BOOL; bits = q[p] != 0; p += 1; break;
-            case 7: {
-                if (p + 4 > rem) return WC_HOST;
-                const int32_t sl = (int32_t)rd32(q + p); p += 4;
-                if (sl < 0 || (uint32_t)sl > rem - p) return WC_HOST;
-                uint64_t h = 0xcbf29ce484222325ULL;          // sf_string_key: FNV-1a 64
-                for (int32_t j = 0; j < sl; j++) { h ^= q[p + j]; h *= 0x100000001b3ULL; }
-                tag = SF_TAG_STRING; bits = h; p += (uint32_t)sl; break;
-            }
-            default: ok = false;                             // decodeParam returns false
-            }
-            if (ok) { if (n == 0) { f.tag = tag; f.bits = bits; } n++; }
-        }
-        if (p != rem) return WC_HOST;
+        const int n = wire_params(q, rem, amount, nullptr, nullptr);
+        if (n < 0) return WC_HOST;
         if (n == 0) return WC_BAD;                           // requestParamToken: params.isEmpty()
-        if (n > 1) return WC_HOST;
+        *nval = (uint32_t)n;                                 // one Collection (the decoder's ArrayList)
         f.flags = SF_TOK_PARAM;
         return WC_REQ;
     }
@@ -276,8 +288,10 @@ __global__ void k_wire_class(WireBufs w, uint32_t nf) {
     const uint32_t L = ((uint32_t)w.bytes[p] << 8) | w.bytes[p + 1];
     WFrame x{};
     x.stream = s;
-    x.cls = L + 2 > SF_WIRE_MAX_FRAME ? WC_SKIP : wire_decode_body(w.bytes + p + 2, L, x);
+    uint32_t nv = 0;
+    x.cls = L + 2 > SF_WIRE_MAX_FRAME ? WC_SKIP : wire_decode_body(w.bytes + p + 2, L, x, &nv);
     w.wf[f] = x;
+    w.nval[f] = x.cls == WC_REQ ? nv : 0u;
     if (x.cls == WC_HOST) atomicMin(&w.stopoff[s], p);
 }
 
@@ -297,7 +311,18 @@ __global__ void k_wire_compact(WireBufs w, uint32_t nf, int64_t now_ms) {
     const uint32_t r = (uint32_t)(w.pos[f] >> 32);
     const WFrame x = w.wf[f];
     w.q_fid[r] = x.flow_id; w.q_cnt[r] = x.count; w.q_flags[r] = x.flags; w.q_ts[r] = now_ms;
-    w.q_tag[r] = x.tag; w.q_bits[r] = x.bits;
+    w.q_nval[r] = w.nval[f];
+}
+// parameters of each PARAM_FLOW request at q_poff[r] (decoded again from its frame)
+__global__ void k_wire_values(WireBufs w, uint32_t nf) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nf || !(w.fl[f] >> 32) || !w.nval[f]) return;
+    const uint32_t r = (uint32_t)(w.pos[f] >> 32);
+    const uint32_t p = w.frames[f];
+    const uint32_t L = ((uint32_t)w.bytes[p] << 8) | w.bytes[p + 1];
+    const uint8_t* q = w.bytes + p + 2 + 5;
+    const uint32_t o = w.q_poff[r];
+    wire_params(q, L - 5, (int32_t)rd32(q + 12), w.q_tag + o, w.q_bits + o);
 }
 
 // response frames (LengthFieldPrepender(2) + DefaultResponseEntityWriter + FlowResponseDataWriter)
@@ -353,7 +378,11 @@ hipError_t wire_query_temp(uint32_t n_tiles, uint32_t S, uint32_t max_frames, si
     if (e != hipSuccess) return e;
     e = rocprim::exclusive_scan(nullptr, b, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0,
                                 (size_t)std::max<uint32_t>(max_frames, 1), rocprim::plus<uint64_t>());
-    *bytes = std::max(a, b);
+    if (e != hipSuccess) return e;
+    size_t c = 0;
+    e = rocprim::exclusive_scan(nullptr, c, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)max_frames + 1,
+                                rocprim::plus<uint32_t>());
+    *bytes = std::max(std::max(a, b), c);
     (void)S;
     return e;
 }
@@ -385,9 +414,15 @@ hipError_t wire_decode(const WireBufs& w, uint32_t nf, int64_t now_ms, hipStream
     return hipGetLastError();
 }
 
-hipError_t wire_compact(const WireBufs& w, uint32_t nf, int64_t now_ms, hipStream_t s) {
+hipError_t wire_compact(const WireBufs& w, uint32_t nf, uint32_t n_req, int64_t now_ms, hipStream_t s) {
     if (!nf) return hipSuccess;
+    hipMemsetAsync(w.q_nval + n_req, 0, 4, s);
     hipLaunchKernelGGL(k_wire_compact, dim3(wblocks(nf, 256)), dim3(256), 0, s, w, nf, now_ms);
+    size_t tb = w.tmp_bytes;
+    hipError_t e = rocprim::exclusive_scan(w.tmp, tb, w.q_nval, w.q_poff, 0u, (size_t)n_req + 1,
+                                           rocprim::plus<uint32_t>(), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_wire_values, dim3(wblocks(nf, 256)), dim3(256), 0, s, w, nf);
     return hipGetLastError();
 }
 

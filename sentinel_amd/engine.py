@@ -143,7 +143,7 @@ class DeviceBatch:
     def __init__(self, eng: "FlowEngine", hb: abi.HostBatch):
         self.n = hb.n
         self.arrays = {k: DeviceArray(eng, getattr(hb, k)) for k in ("res_id", "ts_ms", "count", "flags")}
-        for k in ("entry_ref", "create_ts", "arg_tag", "arg_bits", "n_args"):
+        for k in ("entry_ref", "create_ts", "arg_tag", "arg_bits", "n_args", "elem_off", "elem_tag", "elem_bits"):
             a = getattr(hb, k)
             self.arrays[k] = DeviceArray(eng, a) if a is not None else None
         self.arg_slots = 0 if hb.arg_tag is None else hb.arg_tag.shape[0]
@@ -169,6 +169,9 @@ class DeviceBatch:
         b.entry_ref, b.create_ts = g("entry_ref"), g("create_ts")
         b.arg_slots = self.arg_slots
         b.arg_tag, b.arg_bits, b.n_args = g("arg_tag"), g("arg_bits"), g("n_args")
+        if self.arrays.get("elem_off") is not None:
+            b.arg_elem_off, b.elem_tag, b.elem_bits = g("elem_off"), g("elem_tag"), g("elem_bits")
+            b.n_elems = self.arrays["elem_tag"].shape[0]
         return b
 
     def free(self):

@@ -127,7 +127,8 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         if (in->n_args) nargs[j] = in->n_args[i];
         for (uint32_t a = 0; a < in->arg_slots; a++) {
             atag[(size_t)a * n + j] = in->arg_tag[(size_t)a * n + i];
-            abits[(size_t)a * n + j] = in->arg_bits[(size_t)a * n + i];
+            abits[(size_t)a * n + j] = atag[(size_t)a * n + j] == SF_TAG_COLLECTION ? (uint64_t)a * n + i
+                                                                                  : in->arg_bits[(size_t)a * n + i];
         }
         pcg[j] = (j ? pcg[j - 1] : 0) + ((fl[j] & SF_EV_EXIT) ? 0 : (int64_t)cnt[j]);
     }
@@ -139,7 +140,8 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         }
     SegIO io{ts.data(), cnt.data(), fl.data(), in->entry_ref ? eref.data() : nullptr,
              in->entry_ref ? cts.data() : nullptr, in->arg_slots, in->n_args ? nargs.data() : nullptr,
-             atag.data(), abits.data(), n, vs.data(), vw.data(), vr.data()};
+             atag.data(), abits.data(), n, in->arg_elem_off, in->elem_tag, in->elem_bits,
+             vs.data(), vw.data(), vr.data()};
     // segments + routing (k_segments / k_classify)
     std::vector<uint32_t> seg_start, seg_res, segflag;
     for (uint32_t j = 0; j < n; j++) {

@@ -68,3 +68,36 @@ def test_token_server_heavy_values(eng_mod, so):
 
 def test_token_server_bad_requests(eng_mod, so):
     run_tokens(eng_mod, so, 5_000, seed=13, bad_frac=0.5)
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_token_server_collection_params(eng_mod, so, seed):
+    """requestParamToken with Collection params (1-4 values, some null; a few
+    empty -> BAD_REQUEST): rules with multi-value requests are decided per rule
+    in time order (every value must have room before any is added), the rest
+    per value; results and every flow rule's ClusterMetric equal the oracle's."""
+    ns, flow, param, items, b = trace.token_workload(30_000, seed=seed, n_values=60)
+    rng = np.random.default_rng(seed)
+    vals = []
+    for i in range(b.n):
+        if not (b.flags[i] & abi.TOK_PARAM):
+            vals.append([])
+            continue
+        k = int(rng.choice([0, 1, 1, 1, 2, 3, 4])) if rng.random() < 0.6 else 1
+        vals.append([(abi.TAG_NULL, 0) if rng.random() < 0.03 else (abi.TAG_LONG, int(rng.integers(0, 60)))
+                     for _ in range(k)])
+    off = np.concatenate([[0], np.cumsum([len(v) for v in vals])]).astype(np.uint32)
+    tags = np.array([t for v in vals for t, _ in v], np.uint8)
+    bits = np.array([x for v in vals for _, x in v], np.uint64)
+    cfg = abi.default_config(max_resources=4, max_batch=b.n, param_capacity=1 << 16)
+    e, o = eng_mod.FlowEngine(cfg), so.OracleEngine(cfg)
+    for x in (e, o):
+        x.load_namespaces(ns)
+        x.load_cluster_rules(flow, param, items)
+    for lo, hi in ((0, b.n // 2), (b.n // 2, b.n)):
+        po = off[lo:hi + 1] - off[lo]
+        sub = abi.HostTokenBatch(b.flow_id[lo:hi], b.count[lo:hi], b.flags[lo:hi], b.ts_ms[lo:hi],
+                                 param_tag=tags[off[lo]:off[hi]], param_bits=bits[off[lo]:off[hi]], param_off=po)
+        got, want = e.request_tokens(sub), o.request_tokens(sub)
+        compare_tokens(got, want, f"[{lo}, {hi})")
+    assert (want.remaining == -1).sum() > 0

@@ -92,3 +92,24 @@ def test_wire_parity_many_tiny_and_empty_connections(eng_mod):
     now = trace.T0 + 50
     compare(e.serve_frames(streams, now), o.serve_frames(streams, now), "tiny connections")
     compare(e.serve_frames([b""] * 3, now), o.serve_frames([b""] * 3, now), "empty")
+
+
+def test_multi_value_param_frames(eng_mod):
+    """PARAM_FLOW frames with several parameters are one Collection each
+    (decided on the GPU, not handed to the host): byte-exact with the oracle."""
+    ns, flow, param, items, b = trace.token_workload(8000, seed=17, n_values=50)
+    rng = np.random.default_rng(4)
+    streams = [bytearray() for _ in range(20)]
+    for i in range(b.n):
+        s = int(rng.integers(0, 20))
+        if b.flags[i] & abi.TOK_PARAM:
+            k = int(rng.integers(1, 5))
+            vs = [("long", int(x)) if rng.random() < 0.7 else ("str", "v%d" % int(x)) for x in rng.integers(0, 50, k)]
+            streams[s] += wire.param_frame(i, int(b.flow_id[i]), int(b.count[i]), vs)
+        else:
+            streams[s] += wire.flow_frame(i, int(b.flow_id[i]), int(b.count[i]), bool(b.flags[i] & abi.TOK_PRIORITIZED))
+    streams = [bytes(x) for x in streams]
+    e, o = pair(eng_mod, ns, flow, param, items)
+    for k in range(2):
+        now = trace.T0 + 300 * k
+        compare(e.serve_frames(streams, now), o.serve_frames(streams, now), f"call {k}")

@@ -427,6 +427,61 @@ def test_param_slot_second_entry_blocked(so):
     assert list(e.submit(b).status) == [abi.V_PASS, abi.V_BLOCK_PARAM]
 
 
+def _coll_batch(res, times, values, flags=abi.EV_IN):
+    """Entries whose one argument is values[i]: a list = a Collection / array
+    argument (None elements are null), else a scalar (tag, bits) or None."""
+    n = len(times)
+    at, ab, off, et, eb = abi.HostBatch.collections(1, n, [values])
+    return abi.HostBatch([res] * n, times, [1] * n, [flags] * n, arg_tag=at, arg_bits=ab,
+                         elem_off=off, elem_tag=et, elem_bits=eb)
+
+
+def test_param_collection_and_array(so):
+    """PF_T/.../ParamFlowCheckerTest.testPassLocalCheckForCollection (:147-166):
+    QPS count 1, a list of three values passes, the same list again blocks;
+    testPassLocalCheckForArray (:168-187): the same with a throttle rule
+    (maxQueueingTimeMs 0) over an array."""
+    t = 1_700_000_000_000
+    vals = [S("a"), S("B"), S("Cc")]
+    for beh in (0, abi.BEHAVIOR_RATE_LIMITER):
+        e = so.OracleEngine(_cfg())
+        e.load_param_rules([_prule(resource=3, count=1, control_behavior=beh)])
+        v = e.submit(_coll_batch(3, [t, t], [list(vals), list(vals)]))
+        assert list(v.status) == [abi.V_PASS, abi.V_BLOCK_PARAM], beh
+
+
+def test_param_collection_consumes_earlier_elements(so):
+    """passLocalCheck (ParamFlowChecker.java:84-112) stops at the first element
+    that fails; the tokens of the elements before it stay consumed."""
+    t = 1_700_000_000_000
+    e = so.OracleEngine(_cfg())
+    e.load_param_rules([_prule(resource=3, count=1)])
+    v = e.submit(_coll_batch(3, [t, t + 1, t + 2, t + 3], [[S("x")], [S("y"), S("x"), S("z")], [S("y")], [S("z")]]))
+    assert list(v.status) == [abi.V_PASS, abi.V_BLOCK_PARAM, abi.V_BLOCK_PARAM, abi.V_PASS]
+
+
+def test_param_collection_null_element(so):
+    """A null element: the checks before the parameter maps run (a zero
+    threshold blocks), then ConcurrentLinkedHashMap.putIfAbsent(null) throws,
+    passLocalCheck catches it and the value passes; later elements are not
+    checked.  addThreadCount stops at the same element (one try around every
+    argument, ParameterMetric.java:184-239)."""
+    t = 1_700_000_000_000
+    e = so.OracleEngine(_cfg())
+    e.load_param_rules([_prule(resource=3, count=1)])
+    v = e.submit(_coll_batch(3, [t, t + 1, t + 2], [[None, S("x")], [S("x")], [S("x")]]))
+    assert list(v.status) == [abi.V_PASS, abi.V_PASS, abi.V_BLOCK_PARAM]     # x untouched by the first
+    e = so.OracleEngine(_cfg())
+    e.load_param_rules([_prule(resource=3, count=0)])
+    assert e.submit(_coll_batch(3, [t], [[None]])).status[0] == abi.V_BLOCK_PARAM
+    # thread grade: getThreadCount(null) throws -> pass; elements after the null are not counted
+    e = so.OracleEngine(_cfg())
+    e.load_param_rules([_prule(resource=3, count=1, grade=abi.GRADE_THREAD)])
+    v = e.submit(_coll_batch(3, [t, t + 1, t + 2], [[S("p"), None, S("q")], [S("p")], [S("q")]]))
+    assert list(v.status) == [abi.V_PASS, abi.V_BLOCK_PARAM, abi.V_PASS]
+    assert e.param_thread(3, 0, S("p")) == 1 and e.param_thread(3, 0, S("q")) == 1
+
+
 # ------------------------------------------------------ cluster server
 @pytest.mark.parametrize("t0", STARTS)
 def test_cluster_metric_try_occupy_next(so, t0):

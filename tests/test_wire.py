@@ -92,7 +92,7 @@ def test_wire_frame_edge_cases():
         (wire.frame(struct.pack(">ibqii", 5, 2, pp, 1, 0)), 0, abi.WIRE_DONE),      # amount 0: null data
         (wire.frame(struct.pack(">ibqii", 5, 2, pp, 1, 1) + bytes([42])), 1, abi.WIRE_DONE),  # unknown tag: empty -> BAD
         (wire.frame(struct.pack(">ib", 5, 0) + b"\0\0\0\1x"), 0, abi.WIRE_HOST),    # PING
-        (wire.param_frame(5, pp, 1, [("long", 1), ("int", 2)]), 0, abi.WIRE_HOST),  # two values
+        (wire.param_frame(5, pp, 1, [("long", 1), ("int", 2)]), 1, abi.WIRE_DONE),  # two values: one Collection
         (wire.frame(struct.pack(">ibqi", 5, 1, p, 1) + b"\0\0"), 0, abi.WIRE_HOST), # bytes left over
         (wire.frame(b"\0\0\0"), 0, abi.WIRE_HOST),                                  # < 5 bytes
         (wire.flow_frame(5, p, 1)[:7], 0, abi.WIRE_PARTIAL),                        # incomplete
@@ -103,6 +103,58 @@ def test_wire_frame_edge_cases():
         assert int(r.consumed[0]) == (0 if stop != abi.WIRE_DONE else len(fr))
     r = o.serve_frames([wire.frame(struct.pack(">ibqii", 5, 2, pp, 1, 1) + bytes([42]))], now)
     assert wire.decode_responses(r.resp)["status"][0] == abi.TOKEN_BAD_REQUEST
+
+
+def test_cluster_param_collection_semantics():
+    """ClusterParamFlowChecker.acquireClusterToken (:42-87) over a Collection:
+    every value must have room or nothing is added; remaining is -1 for more
+    than one value; a null value counts 0 and is never added; an empty
+    collection is BAD_REQUEST (DefaultTokenService.java:53-56)."""
+    ns = [abi.sf_namespace(namespace_id=1, connected_count=1, max_allowed_qps=-1.0)]
+    param = [abi.sf_cluster_param_rule(flow_id=7, count=2.0, threshold_type=abi.THRESHOLD_GLOBAL, namespace_id=1,
+                                       sample_count=10, window_interval_ms=1000, item_offset=0, item_count=0)]
+    o = _oracle(ns, [], param, [])
+    L = abi.TAG_LONG
+    reqs = [[(L, 1), (L, 2)], [(L, 1)], [(L, 1), (L, 3)], [(L, 3)], [(L, 3)], [(abi.TAG_NULL, 0), (L, 4)], []]
+    off = np.concatenate([[0], np.cumsum([len(r) for r in reqs])]).astype(np.uint32)
+    tags = np.array([t for r in reqs for t, _ in r], np.uint8)
+    bits = np.array([b for r in reqs for _, b in r], np.uint64)
+    n = len(reqs)
+    b = abi.HostTokenBatch(np.full(n, 7), np.ones(n), np.full(n, abi.TOK_PARAM), np.full(n, trace.T0),
+                           param_tag=tags, param_bits=bits, param_off=off)
+    r = o.request_tokens(b)
+    OK, BL, BAD = abi.TOKEN_OK, abi.TOKEN_BLOCKED, abi.TOKEN_BAD_REQUEST
+    assert list(r.status) == [OK, OK, BL, OK, OK, OK, BAD]
+    assert list(r.remaining) == [-1, 0, 0, 1, 0, -1, 0]    # [1,3] blocked at 1: 3 not added (room 1 after)
+
+
+def test_wire_multi_value_frames_match_token_service():
+    """PARAM_FLOW frames with several parameters (one Collection) give the
+    decisions of requestParamToken with those values, in frame order."""
+    ns, flow, param, items, b = trace.token_workload(3000, seed=13)
+    rng = np.random.default_rng(5)
+    now = trace.T0 + 100
+    frames, vals = [], []
+    for i in range(b.n):
+        if b.flags[i] & abi.TOK_PARAM:
+            k = int(rng.integers(1, 4))
+            v = [int(x) for x in rng.integers(0, 40, k)]
+            vals.append(v)
+            frames.append(wire.param_frame(i, int(b.flow_id[i]), int(b.count[i]), [("long", x) for x in v]))
+        else:
+            vals.append([])
+            frames.append(wire.flow_frame(i, int(b.flow_id[i]), int(b.count[i]), bool(b.flags[i] & abi.TOK_PRIORITIZED)))
+    r = _oracle(ns, flow, param, items).serve_frames([b"".join(frames)], now)
+    off = np.concatenate([[0], np.cumsum([len(v) for v in vals])]).astype(np.uint32)
+    allv = np.array([x for v in vals for x in v], np.uint64)
+    want = _oracle(ns, flow, param, items).request_tokens(abi.HostTokenBatch(
+        b.flow_id, b.count, b.flags, np.full(b.n, now, np.int64), param_tag=np.full(allv.size, abi.TAG_LONG, np.uint8),
+        param_bits=allv, param_off=off))
+    a = wire.decode_responses(r.resp)
+    assert r.stop[0] == abi.WIRE_DONE and r.n_responses == b.n
+    assert (a["status"] == want.status).all() and (a["remaining"] == want.remaining).all()
+    multi = np.array([len(v) > 1 for v in vals])
+    assert multi.sum() > 100 and (a["remaining"][multi & (a["status"] == abi.TOKEN_OK)] == -1).all()
 
 
 def test_wire_streams_stop_independently():

@@ -133,6 +133,66 @@ def param_mixed(seed=21, R=12, n=30000):
                 param=prules, items=items, batches=[b], nodes=list(range(R)), n_flow=len(flow))
 
 
+def param_collections(seed=31, R=10, n=20000):
+    """Param rules (QPS default with burst / hot items, throttle, THREAD grade)
+    over arguments that are scalars, nulls, or Collections / arrays of 0-4
+    elements (some null); exits carry their entry's arguments."""
+    rng = np.random.default_rng(seed)
+    items, prules = [], []
+    for r in range(R):
+        for k in rng.choice(3, size=int(rng.integers(1, 3)), replace=False):
+            off = len(items)
+            for v in rng.choice(30, size=2, replace=False):
+                items.append(abi.sf_hot_item(tag=abi.TAG_LONG, count=int(rng.integers(0, 6)), bits=int(v)))
+            pidx = int(rng.choice([0, 1]))
+            if k == 0:
+                prules.append(abi.sf_param_rule(resource=r, grade=abi.GRADE_QPS, param_idx=pidx, control_behavior=0,
+                                                count=float(rng.integers(1, 12)), burst_count=int(rng.integers(0, 3)),
+                                                duration_in_sec=1, item_offset=off, item_count=2))
+            elif k == 1:
+                prules.append(abi.sf_param_rule(resource=r, grade=abi.GRADE_QPS, param_idx=pidx, control_behavior=2,
+                                                count=float(rng.integers(2, 30)),
+                                                max_queueing_time_ms=int(rng.integers(0, 200)),
+                                                duration_in_sec=1, item_offset=off, item_count=2))
+            else:
+                prules.append(abi.sf_param_rule(resource=r, grade=abi.GRADE_THREAD, param_idx=pidx, control_behavior=0,
+                                                count=float(rng.integers(1, 6)), duration_in_sec=1,
+                                                item_offset=off, item_count=2))
+    flow = [abi.sf_flow_rule(resource=r, grade=abi.GRADE_QPS, count=float(rng.integers(20, 60)), strategy=0,
+                             control_behavior=0, warm_up_period_sec=10, max_queueing_time_ms=500) for r in range(0, R, 3)]
+    ts = np.sort(rng.integers(0, 5000, n)) + trace.T0
+    res = rng.integers(0, R, n).astype(np.uint32)
+
+    def value():
+        u = rng.random()
+        if u < 0.05:
+            return None
+        if u < 0.7:
+            return (abi.TAG_LONG, int(rng.integers(0, 30)))
+        return [None if rng.random() < 0.05 else (abi.TAG_LONG, int(rng.integers(0, 30)))
+                for _ in range(int(rng.integers(0, 5)))]
+    vals = [[value() for _ in range(n)] for _ in range(2)]
+    ent = np.arange(0, n, 2)                               # half of the entries exit after 0-80 ms
+    ex_ts = ts[ent] + rng.integers(0, 80, ent.size)
+    all_ts = np.concatenate([ts, ex_ts])
+    key = np.lexsort((np.concatenate([np.zeros(n), np.ones(ent.size)]), all_ts))
+    pos = np.empty(key.size, np.int64)
+    pos[key] = np.arange(key.size)
+    src = np.concatenate([np.arange(n), ent])[key]
+    m = key.size
+    at, ab, off, et, eb = abi.HostBatch.collections(2, m, [[vals[a][int(s)] for s in src] for a in range(2)])
+    fl = np.concatenate([np.full(n, abi.EV_IN, np.uint8), np.full(ent.size, abi.EV_EXIT | abi.EV_IN, np.uint8)])[key]
+    eref = np.full(m, -1, np.int64)
+    eref[pos[n:]] = pos[ent]
+    nargs = rng.integers(1, 3, n).astype(np.uint8)[src]
+    b = abi.HostBatch(res[src], all_ts[key], np.ones(m, np.int32), fl, entry_ref=eref, arg_tag=at, arg_bits=ab,
+                      n_args=nargs, elem_off=off, elem_tag=et, elem_bits=eb)
+    cuts = [0, m // 2, m]
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=m, param_capacity=1 << 14), flow=flow,
+                param=prules, items=items, batches=[b.subset(cuts[0], cuts[1]), b.subset(cuts[1], cuts[2])],
+                nodes=list(range(R)), n_flow=len(flow))
+
+
 def system(kind, seed=41):
     """SystemRule over mixed traffic (SystemRuleManager.checkSystem, global
     ENTRY_NODE): config 4's inbound-QPS rule at 0.8x the offered rate, or the
@@ -190,6 +250,7 @@ def system_large(kind, seed=43):
 ALL = {
     "config1": config1, "config2": config2, "config3": config3, "config4": config4,
     "prioritized": prioritized, "multi_rule": multi_rule, "param_mixed": param_mixed,
+    "param_collections": param_collections,
     "geom_S1": lambda: geometry(1, 1000), "geom_S4": lambda: geometry(4, 1000), "geom_S10": lambda: geometry(10, 2000),
 }
 
