@@ -369,6 +369,21 @@ int  sf_load_cluster_rules(sf_engine* e, const sf_cluster_flow_rule* flow, uint3
                            const sf_cluster_param_rule* param, uint32_t n_param,
                            const sf_hot_item* items, uint32_t n_items);
 int  sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* out);
+/* Token server over the GPUs of a node: one engine per GPU,
+ * each loaded with ALL cluster rules and namespaces, with shard_count /
+ * shard_index of its sf_config; a request is decided by its owner shard only
+ * (another shard's request makes sf_request_tokens fail with SF_ERR_INVALID).
+ * The owner of a flowId is flow_id % shard_count, except that every rule of a
+ * namespace with a GlobalRequestLimiter (max_allowed_qps >= 0) is pinned to
+ * namespace_id % shard_count: the limiter is one sequential gate over the
+ * namespace (GlobalRequestLimiter.java:46-55).  Requests with flow_id <= 0
+ * belong to shard 0.  sf_token_shard computes the owners of a batch from the
+ * rule tables (host only: no engine, no GPU), for the front-end that routes
+ * requests; ClusterMetric state stays on the owner (sf_cluster_sum).
+ * sf_serve_frames needs shard_count == 1 (its front-end routes decoded frames). */
+int  sf_token_shard(const sf_cluster_flow_rule* flow, uint32_t n_flow, const sf_cluster_param_rule* param,
+                    uint32_t n_param, const sf_namespace* ns, uint32_t n_ns, uint32_t shard_count,
+                    const int64_t* flow_id, const uint8_t* flags, uint32_t n, uint32_t* out_shard);
 /* ---- token-server wire path (C1 frames) ------------
  * Replaces the server pipeline of NettyTransportServer.java:84-101 up to the
  * TokenService call and back:

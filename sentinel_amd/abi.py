@@ -376,6 +376,19 @@ class HostTokenBatch:
         t.param_off = _ptr(self.param_off)
         return t
 
+    def take(self, sel) -> "HostTokenBatch":
+        """The requests sel (ascending), values re-packed."""
+        sel = np.asarray(sel, np.int64)
+        if self.param_off is None:
+            pt = None if self.param_tag is None else self.param_tag[sel]
+            pb = None if self.param_bits is None else self.param_bits[sel]
+            return HostTokenBatch(self.flow_id[sel], self.count[sel], self.flags[sel], self.ts_ms[sel], pt, pb)
+        lo, hi = self.param_off[sel], self.param_off[sel + 1]
+        idx = np.concatenate([np.arange(a, b) for a, b in zip(lo, hi)]) if sel.size else np.zeros(0, np.int64)
+        off = np.concatenate([[0], np.cumsum(hi - lo)]).astype(np.uint32)
+        return HostTokenBatch(self.flow_id[sel], self.count[sel], self.flags[sel], self.ts_ms[sel],
+                              self.param_tag[idx], self.param_bits[idx], off)
+
 
 class HostTokenResults:
     def __init__(self, n: int):

@@ -317,6 +317,7 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     HIP_TRY(launch_init_state(st, e->stream));
     e->ts.err = st.err;
     e->ts.exceed_count = c.exceed_count;
+    e->ts.shard_count = c.shard_count; e->ts.shard_index = c.shard_index;
     e->ts.max_occupy_ratio = c.max_occupy_ratio;
     DALLOC(e->d_sum, sizeof(int64_t));
     DALLOC(st.last_fetch, R * sizeof(int64_t));
@@ -949,6 +950,18 @@ int sf_format_metric_rows(sf_engine* e, const sf_metric_row* rows, uint32_t n, i
     return ml_format(e, nullptr, n, tz_offset_ms, out, cap, len_out);
 }
 // ---------------------------------------------------------------- cluster token server
+// Owner shard of a cluster rule's requests (sentinel_flow.h, sf_token_shard):
+// a namespace with a GlobalRequestLimiter is one sequential gate, so all its
+// rules live on namespace_id % N; any other rule on flow_id % N.
+static uint32_t tok_rule_owner(int64_t flow_id, uint32_t ns_id, const std::vector<sf_namespace>& ns, uint32_t N) {
+    for (const sf_namespace& x : ns)
+        if (x.namespace_id == ns_id) {
+            if (x.max_allowed_qps >= 0) return ns_id % N;
+            break;
+        }
+    return flow_id <= 0 ? 0u : (uint32_t)((uint64_t)flow_id % N);
+}
+
 // Rebuild the device rule table, flowId index and namespace table from the
 // host copies (ClusterFlowRuleManager / ClusterParamFlowRuleManager /
 // ClusterServerConfigManager state).  Metric state is reset when
@@ -966,16 +979,19 @@ static int tok_rebuild(sf_engine* e, bool reset_state) {
         r.ns = it == ns_index.end() ? -1 : it->second;
         r.S = S; r.wl = I / S; r.interval = I;
     };
+    const uint32_t N = e->cfg.shard_count;
     for (uint32_t i = 0; i < nf; i++) {
         const sf_cluster_flow_rule& f = e->host_cflow[i];
         fill(rules[i], f.flow_id, f.count, f.threshold_type, f.namespace_id, f.sample_count, f.window_interval_ms);
         rules[i].is_param = 0; rules[i].item_off = rules[i].item_cnt = 0;
+        rules[i].owner = tok_rule_owner(f.flow_id, f.namespace_id, e->host_ns, N);
     }
     for (uint32_t i = 0; i < np; i++) {
         const sf_cluster_param_rule& f = e->host_cparam[i];
         ClRule& r = rules[nf + i];
         fill(r, f.flow_id, f.count, f.threshold_type, f.namespace_id, f.sample_count, f.window_interval_ms);
         r.is_param = 1; r.item_off = f.item_offset; r.item_cnt = f.item_count;
+        r.owner = tok_rule_owner(f.flow_id, f.namespace_id, e->host_ns, N);
     }
     // flowId -> rule index, open addressing; the first rule of an id wins (like the oracle's lookup)
     uint64_t cap = 16;
@@ -1175,7 +1191,30 @@ int sf_request_tokens(sf_engine* e, const sf_token_batch* in, sf_token_results* 
     int32_t err = 0;
     HIP_TRY(hipMemcpyAsync(&err, e->st.err, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (err) return fail(err, err == SF_ERR_CAPACITY ? "cluster param table capacity exceeded" : "invalid token batch");
+    if (err) return fail(err, err == SF_ERR_CAPACITY ? "cluster param table capacity exceeded"
+                                                     : "invalid token batch (a request owned by another shard?)");
+    return SF_OK;
+}
+
+int sf_token_shard(const sf_cluster_flow_rule* flow, uint32_t n_flow, const sf_cluster_param_rule* param,
+                   uint32_t n_param, const sf_namespace* ns, uint32_t n_ns, uint32_t shard_count,
+                   const int64_t* flow_id, const uint8_t* flags, uint32_t n, uint32_t* out_shard) {
+    if ((n_flow && !flow) || (n_param && !param) || (n_ns && !ns) || (n && (!flow_id || !flags || !out_shard)) ||
+        shard_count == 0)
+        return fail(SF_ERR_INVALID, "sf_token_shard arguments");
+    const std::vector<sf_namespace> nsv(ns, ns + n_ns);
+    std::unordered_map<int64_t, uint32_t> fo, po;                  // first rule of an id (tok_rebuild's lookup)
+    for (uint32_t i = 0; i < n_flow; i++)
+        if (flow[i].flow_id > 0) fo.emplace(flow[i].flow_id, tok_rule_owner(flow[i].flow_id, flow[i].namespace_id, nsv, shard_count));
+    for (uint32_t i = 0; i < n_param; i++)
+        if (param[i].flow_id > 0) po.emplace(param[i].flow_id, tok_rule_owner(param[i].flow_id, param[i].namespace_id, nsv, shard_count));
+    for (uint32_t i = 0; i < n; i++) {
+        const int64_t id = flow_id[i];
+        if (id <= 0) { out_shard[i] = 0; continue; }
+        const auto& m = (flags[i] & SF_TOK_PARAM) ? po : fo;
+        const auto it = m.find(id);
+        out_shard[i] = it != m.end() ? it->second : (uint32_t)((uint64_t)id % shard_count);
+    }
     return SF_OK;
 }
 
@@ -1189,6 +1228,8 @@ int sf_serve_frames(sf_engine* e, const sf_wire_batch* in, sf_wire_out* out) {
     if (!e || !in || !out || !in->stream_off || !out->resp_off || !out->consumed || !out->stop)
         return fail(SF_ERR_INVALID, "null argument");
     if (in->n_streams == 0) return fail(SF_ERR_INVALID, "n_streams must be > 0");
+    if (e->cfg.shard_count > 1)
+        return fail(SF_ERR_UNSUPPORTED, "sf_serve_frames on a sharded token server: route decoded requests with sf_token_shard");
     const uint32_t S = in->n_streams;
     std::vector<uint64_t> soff(S + 1);
     if (in->mem == SF_MEM_HOST) std::memcpy(soff.data(), in->stream_off, (S + 1) * sizeof(uint64_t));

@@ -29,13 +29,14 @@ constexpr int CE_PASS = 0, CE_BLOCK = 1, CE_PASS_REQUEST = 2, CE_BLOCK_REQUEST =
               CE_OCCUPIED_BLOCK = 5, CE_WAITING = 6, CE_COUNT = 7;   // ClusterFlowEvent.java ordinals
 constexpr int LIM_S = 10, LIM_WL = 100, LIM_INTERVAL = 1000;        // RequestLimiter: UnaryLeapArray(10, 1000)
 
-struct ClRule {                  // 48 B
+struct ClRule {                  // 56 B
     double count;
     int64_t flow_id;
     int32_t threshold_type, ns;  // ns: namespace index, -1 when the namespace is not loaded
     int32_t S, wl;
     int32_t interval, is_param;
     uint32_t item_off, item_cnt;
+    uint32_t owner, pad;         // shard deciding this rule's requests (sf_token_shard)
 };
 struct ClBucket { int64_t ws; int64_t c[CE_COUNT]; };          // WindowWrap<ClusterMetricBucket>, 64 B
 struct ClFlowState {                                            // ClusterMetricLeapArray, 1056 B
@@ -64,6 +65,7 @@ struct TokState {
     double exceed_count, max_occupy_ratio;
     int32_t* err;
     uint8_t* rmulti;             // [n_rules] per call: a param rule with a multi-value request (serial group)
+    uint32_t shard_count, shard_index;
 };
 
 struct TokBatch {

@@ -60,22 +60,24 @@ __global__ void k_tok_prep(TokState ts, TokBatch b, TokWork w, TokOut out) {
     const int64_t id = b.flow_id[i];
     const int32_t c = b.count[i];
     const bool param = (b.flags[i] & SF_TOK_PARAM) != 0;
+    const int32_t r = id > 0 ? id_lookup(ts, id, param) : -1;
+    // sharded token server: only the owner shard decides (sf_token_shard)
+    const uint32_t owner = id <= 0 ? 0u : (r >= 0 ? ts.rules[r].owner : (uint32_t)((uint64_t)id % ts.shard_count));
+    if (owner != ts.shard_index) *ts.err = SF_ERR_INVALID;
     int8_t st = TOK_PENDING;
     uint8_t nk = NS_NONE;
     const uint32_t nv = (param && b.poff) ? b.poff[i + 1] - b.poff[i] : 1u;
     if (id <= 0 || c <= 0 || (param && (!b.ptag || !b.pbits || nv == 0))) {
         st = SF_TOKEN_BAD_REQUEST;                          // notValidRequest / params empty :66-72
+    } else if (r < 0) {
+        st = SF_TOKEN_NO_RULE_EXISTS;                       // getFlowRuleById == null :45-47
     } else {
-        const int32_t r = id_lookup(ts, id, param);
-        if (r < 0) st = SF_TOKEN_NO_RULE_EXISTS;           // getFlowRuleById == null :45-47
-        else {
-            w.rule_of[i] = (uint32_t)r;
-            // a request with several values couples them (all must pass before any is
-            // added): that rule's requests are decided by one lane in time order
-            if (nv > 1) ts.rmulti[r] = 1;
-            const int32_t ns = ts.rules[r].ns;
-            if (ns >= 0 && ts.ns[ns].has_limiter) nk = (uint8_t)ns;   // else GlobalRequestLimiter passes
-        }
+        w.rule_of[i] = (uint32_t)r;
+        // a request with several values couples them (all must pass before any is
+        // added): that rule's requests are decided by one lane in time order
+        if (nv > 1) ts.rmulti[r] = 1;
+        const int32_t ns = ts.rules[r].ns;
+        if (ns >= 0 && ts.ns[ns].has_limiter) nk = (uint8_t)ns;   // else GlobalRequestLimiter passes
     }
     w.pending[i] = st == TOK_PENDING;
     w.nskey_in[i] = nk;

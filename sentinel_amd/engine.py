@@ -93,6 +93,19 @@ def _declare(L):
     f("sf_set_timing", I, P, I)
     f("sf_heavy_profile_read", I, P, C.POINTER(abi.sf_heavy_profile), U32, C.POINTER(U32))
     f("sf_param_table_stats", I, P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(U32))
+    f("sf_token_shard", I, C.POINTER(abi.sf_cluster_flow_rule), U32, C.POINTER(abi.sf_cluster_param_rule), U32,
+      C.POINTER(abi.sf_namespace), U32, U32, P, P, U32, P)
+
+
+def token_shard(flow, param, namespaces, shard_count: int, batch: abi.HostTokenBatch) -> np.ndarray:
+    """Owner shard of every request of ``batch`` on a token server sharded
+    over ``shard_count`` GPUs (sf_token_shard: host only, no GPU needed)."""
+    out = np.zeros(batch.n, np.uint32)
+    _check(lib().sf_token_shard(abi.rules_array(abi.sf_cluster_flow_rule, list(flow)), len(flow),
+                                abi.rules_array(abi.sf_cluster_param_rule, list(param)), len(param),
+                                abi.rules_array(abi.sf_namespace, list(namespaces)), len(namespaces), shard_count,
+                                batch.flow_id.ctypes.data, batch.flags.ctypes.data, batch.n, out.ctypes.data))
+    return out
 
 
 def comm_unique_id() -> bytes:

@@ -128,3 +128,131 @@ def test_degrade_sharded_two_ranks():
         p.join(timeout=60)
     assert np.array_equal(got, want)
     assert (want == 8).sum() > 0
+
+
+def _token_worker(rank, world, port, q):
+    """Cluster token server sharded by flowId: the library's
+    sf_token_shard routes every request (a namespace with a
+    GlobalRequestLimiter pinned to one shard); each rank decides its requests
+    with the token service of its own engine (the oracle here: the CPU
+    stand-in of the GPU engine, which the GPU suite pins to it); rank 0 gathers
+    the results and compares them with one token server deciding every request."""
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle as so
+    from sentinel_amd import engine
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ns, flow, param, items, b = trace.token_workload(20_000, seed=33, max_qps=1500.0, n_flow=60, n_param=20)
+    owner = engine.token_shard(flow, param, ns, world, b)
+    sel = np.nonzero(owner == rank)[0]
+    cfg = abi.default_config(max_resources=4, max_batch=b.n, param_capacity=1 << 16, shard_count=world,
+                             shard_index=rank)
+    o = so.OracleEngine(cfg)
+    o.load_namespaces(ns)
+    o.load_cluster_rules(flow, param, items)
+    r = o.request_tokens(b.take(sel))
+    n_max = torch.tensor([sel.size])
+    dist.all_reduce(n_max, op=dist.ReduceOp.MAX)
+    pack = torch.full((int(n_max), 3), -99, dtype=torch.int64)
+    pos = torch.full((int(n_max),), -1, dtype=torch.int64)
+    pos[:sel.size] = torch.from_numpy(sel)
+    pack[:sel.size, 0] = torch.from_numpy(r.status.astype(np.int64))
+    pack[:sel.size, 1] = torch.from_numpy(r.remaining.astype(np.int64))
+    pack[:sel.size, 2] = torch.from_numpy(r.wait_ms.astype(np.int64))
+    all_pos = [torch.empty_like(pos) for _ in range(world)]
+    all_pack = [torch.empty_like(pack) for _ in range(world)]
+    dist.all_gather(all_pos, pos)
+    dist.all_gather(all_pack, pack)
+    if rank == 0:
+        got = np.full((b.n, 3), -99, np.int64)
+        for p_, v in zip(all_pos, all_pack):
+            m = p_ >= 0
+            got[p_[m].numpy()] = v[m].numpy()
+        ref = so.OracleEngine(abi.default_config(max_resources=4, max_batch=b.n, param_capacity=1 << 16))
+        ref.load_namespaces(ns)
+        ref.load_cluster_rules(flow, param, items)
+        w = ref.request_tokens(b)
+        want = np.stack([w.status.astype(np.int64), w.remaining.astype(np.int64), w.wait_ms.astype(np.int64)], 1)
+        q.put((got, want, np.bincount(owner, minlength=world)))
+    dist.destroy_process_group()
+
+
+def test_token_server_sharded_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_token_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, want, per_shard = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert (per_shard > 1000).all(), per_shard
+    assert np.array_equal(got, want)
+    assert (want[:, 0] == abi.TOKEN_TOO_MANY_REQUEST).sum() > 0        # the pinned namespace limiter fired
+
+
+def _hostsim_worker(rank, world, port, q):
+    """Resource-sharded flow engine: each rank runs the engine's own decision
+    code (tests/hostsim: sf_decide.h / sf_heavy.h built for the CPU) with
+    shard_count = 2 on its shard of a config-3 batch (two batches, exits
+    crossing them); rank 0 gathers the verdicts and compares them with one
+    oracle replay of the whole batch."""
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle as so
+    from tests.hostsim import hostsim
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    R = 3000
+    rules = trace.mixed_rules(R, seed=35)
+    full = trace.mixed_zipf(R, 120_000, duration_ms=6000, seed=35)
+    sel = np.nonzero(full.res_id % world == rank)[0]
+    sub = full.shard(world, rank)
+    cfg = abi.default_config(max_resources=(R + world - 1) // world, max_batch=max(sub.n, 1), shard_count=world,
+                             shard_index=rank, heavy_min_events=64)
+    h = hostsim.HostSimEngine(cfg)
+    h.load_flow_rules([r for r in rules if r.resource % world == rank])
+    cut = full.n // 2
+    half = int(np.searchsorted(sel, cut))
+    outs = [h.submit(sub.subset(0, half)), h.submit(sub.subset(half, sub.n))]
+    st = np.concatenate([o.status for o in outs]).astype(np.int64)
+    wt = np.concatenate([o.wait_ms for o in outs]).astype(np.int64)
+    n_max = torch.tensor([sel.size])
+    dist.all_reduce(n_max, op=dist.ReduceOp.MAX)
+    pos = torch.full((int(n_max),), -1, dtype=torch.int64)
+    pos[:sel.size] = torch.from_numpy(sel)
+    val = torch.zeros((int(n_max), 2), dtype=torch.int64)
+    val[:sel.size, 0] = torch.from_numpy(st)
+    val[:sel.size, 1] = torch.from_numpy(wt)
+    all_pos = [torch.empty_like(pos) for _ in range(world)]
+    all_val = [torch.empty_like(val) for _ in range(world)]
+    dist.all_gather(all_pos, pos)
+    dist.all_gather(all_val, val)
+    if rank == 0:
+        got = np.full((full.n, 2), -1, np.int64)
+        for p_, v in zip(all_pos, all_val):
+            m = p_ >= 0
+            got[p_[m].numpy()] = v[m].numpy()
+        ref = so.OracleEngine(abi.default_config(max_resources=R, max_batch=full.n))
+        ref.load_flow_rules(rules)
+        ws = [ref.submit(full.subset(0, cut)), ref.submit(full.subset(cut, full.n))]
+        want = np.stack([np.concatenate([w.status for w in ws]), np.concatenate([w.wait_ms for w in ws])], 1)
+        q.put((got, want.astype(np.int64)))
+    dist.destroy_process_group()
+
+
+def test_flow_engine_hostsim_sharded_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hostsim_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, want = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(got, want)

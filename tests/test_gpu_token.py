@@ -101,3 +101,28 @@ def test_token_server_collection_params(eng_mod, so, seed):
         got, want = e.request_tokens(sub), o.request_tokens(sub)
         compare_tokens(got, want, f"[{lo}, {hi})")
     assert (want.remaining == -1).sum() > 0
+
+
+@pytest.mark.parametrize("shard", [0, 1])
+def test_token_server_sharded(eng_mod, so, shard):
+    """A token server sharded over two GPUs (sf_token_shard): this shard's
+    engine decides the requests it owns exactly as one token server deciding
+    every request; a request of the other shard is refused."""
+    ns, flow, param, items, b = trace.token_workload(30_000, seed=34, max_qps=1500.0, n_flow=60, n_param=20)
+    owner = eng_mod.token_shard(flow, param, ns, 2, b)
+    sel = np.nonzero(owner == shard)[0]
+    cfg = abi.default_config(max_resources=4, max_batch=b.n, param_capacity=1 << 16, shard_count=2, shard_index=shard)
+    e = eng_mod.FlowEngine(cfg)
+    e.load_namespaces(ns)
+    e.load_cluster_rules(flow, param, items)
+    ref = so.OracleEngine(abi.default_config(max_resources=4, max_batch=b.n, param_capacity=1 << 16))
+    ref.load_namespaces(ns)
+    ref.load_cluster_rules(flow, param, items)
+    want = ref.request_tokens(b)
+    got = e.request_tokens(b.take(sel))
+    sub = abi.HostTokenResults(sel.size)
+    sub.status, sub.remaining, sub.wait_ms = want.status[sel], want.remaining[sel], want.wait_ms[sel]
+    compare_tokens(got, sub, f"shard {shard}")
+    other = np.nonzero(owner != shard)[0][:5]
+    with pytest.raises(eng_mod.EngineError):
+        e.request_tokens(b.take(other))
