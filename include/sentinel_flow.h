@@ -540,6 +540,38 @@ int  sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t 
 int  sf_degrade_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
 int  sf_read_breaker(sf_engine* e, uint32_t breaker_index, sf_breaker_state* out);
 
+/* ---- rule-list order (host only, no engine) -----------------------------
+ * The order in which the reference's managers hold a resource's rules:
+ * FlowRuleUtil.buildFlowRuleMap (FlowRuleUtil.java:83-130) drops invalid
+ * rules, collapses equal ones in a java.util.HashSet, lists the set in its
+ * (JDK 8 HashMap) iteration order and sorts it stably with FlowRuleComparator
+ * (FlowRuleComparator.java:27-57: cluster-mode rules last, limitApp
+ * "default" after specific origins); ParamFlowRuleUtil.buildParamRuleMap
+ * (ParamFlowRuleUtil.java:138-186) the same without the sort.  Rule order
+ * decides which rule blocks (and which ParamFlow rules consumed tokens), so a
+ * host that loads rules from a Java rule list passes them to sf_load_*_rules
+ * in this order.  The String fields enter through their Java hash codes:    */
+typedef struct sf_rule_key {
+    int32_t  resource_hash;   /* getResource().hashCode()                          */
+    uint32_t limit_app_id;    /* 0 "default" (also a blank limitApp), 1 "other", >1 an origin */
+    int32_t  limit_app_hash;  /* getLimitApp().hashCode() (unused when id is 0)    */
+    int32_t  extra_hash;      /* flow: refResource.hashCode() (0 for null);
+                                 param: paramFlowItemList.hashCode()               */
+    int32_t  cluster_hash;    /* flow: clusterConfig.hashCode() (0 for null, the local
+                                 rule); equal rules must have equal values here      */
+} sf_rule_key;
+/* order[0 .. *n_out): indices of the kept rules, resources in order of first
+ * appearance, each resource's rules in the manager's order.  Validity is
+ * FlowRuleUtil.isValidRule (:170-254) / ParamFlowRuleUtil.isValidRule (:46-52)
+ * on the struct fields; a cluster-mode or RELATE/CHAIN flow rule is taken to
+ * carry a valid clusterConfig / non-blank refResource.
+ * SF_ERR_UNSUPPORTED if a HashMap bin would be treeified (>8 equal-bucket
+ * rules of one resource in a 64-slot table): not modelled.                   */
+int  sf_flow_rule_order(const sf_flow_rule* rules, const sf_rule_key* keys, uint32_t n, uint32_t* order,
+                        uint32_t* n_out);
+int  sf_param_rule_order(const sf_param_rule* rules, const sf_rule_key* keys, uint32_t n, const sf_hot_item* items,
+                         uint32_t n_items, uint32_t* order, uint32_t* n_out);
+
 /* Device helpers so hosts without a GPU framework can stage HBM inputs. */
 int  sf_device_alloc(sf_engine* e, size_t bytes, void** ptr);
 int  sf_device_free(sf_engine* e, void* ptr);

@@ -1,0 +1,221 @@
+"""TEST INFRASTRUCTURE ONLY -- restatement of the rule ordering the reference's
+rule managers produce, the checker for the engine's sf_flow_rule_order /
+sf_param_rule_order (sentinel_amd/csrc/sf_rules.cpp).
+
+FlowRuleUtil.buildFlowRuleMap (sentinel-core/.../flow/FlowRuleUtil.java:83-130):
+valid rules of one resource go into a java.util.HashSet (equal rules collapse
+to the first one added), the set is copied into an ArrayList in HashMap
+iteration order, then Collections.sort with FlowRuleComparator
+(FlowRuleComparator.java:27-57, a stable merge sort).  ParamFlowRuleUtil
+.buildParamRuleMap (ParamFlowRuleUtil.java:138-186) does the same without the
+sort.  HashMap iteration order (JDK 8): buckets 0..capacity-1, each bucket's
+entries in insertion order; bucket = (h ^ h >>> 16) & (capacity - 1) with
+h = hashCode(); the table starts at 16 and doubles when the size passes
+0.75 x capacity (splitting keeps relative order), and a bucket that reaches
+9 entries in a table smaller than 64 doubles it too (treeifyBin).
+Hash codes: String.hashCode, Double.doubleToLongBits, AbstractRule.hashCode
+(AbstractRule.java:111-118), FlowRule.hashCode (FlowRule.java:207-222),
+ParamFlowRule.hashCode (ParamFlowRule.java:211-227).
+
+Rules are the ABI structs (abi.sf_flow_rule / sf_param_rule); the String
+fields arrive as a key per rule: (resource_hash, limit_app_id,
+limit_app_hash, extra_hash, cluster_hash) exactly as sf_rule_key --
+limit_app_id 0 is "default" (a blank limitApp becomes "default" before
+hashing), 1 "other", >1 an origin; extra_hash is refResource.hashCode()
+(flow) or paramFlowItemList.hashCode() (param); cluster_hash is
+clusterConfig.hashCode() (0: null).
+
+Parity pin: the reference's FlowRuleComparatorTest (B, C, D, A, E) and
+String.hashCode known answers; the HashMap model is JDK 8's published
+algorithm (java.util.HashMap.putVal / resize / treeifyBin), pinned by the
+well-known iteration orders in tests/test_rule_order.py.  No Java runs here.
+"""
+import struct
+
+M32 = 0xFFFFFFFF
+
+
+def i32(x: int) -> int:
+    x &= M32
+    return x - (1 << 32) if x & 0x80000000 else x
+
+
+def java_string_hash(s: str) -> int:
+    """String.hashCode over UTF-16 code units."""
+    h = 0
+    data = s.encode("utf-16-be")
+    for k in range(0, len(data), 2):
+        h = (31 * h + ((data[k] << 8) | data[k + 1])) & M32
+    return i32(h)
+
+
+def double_bits(x: float) -> int:
+    """Double.doubleToLongBits (every NaN -> the canonical NaN)."""
+    if x != x:
+        return 0x7ff8000000000000
+    return struct.unpack(">q", struct.pack(">d", x))[0]
+
+
+def _mix_double(h: int, x: float) -> int:
+    t = double_bits(x) & 0xFFFFFFFFFFFFFFFF
+    return i32(31 * h + i32(t ^ (t >> 32)))
+
+
+def abstract_rule_hash(key) -> int:
+    """AbstractRule.hashCode: resource, plus limitApp unless blank / "default"."""
+    h = i32(key[0])
+    if key[1] != 0:
+        h = i32(31 * h + key[2])
+    return h
+
+
+def flow_rule_hash(r, key) -> int:
+    h = abstract_rule_hash(key)
+    h = i32(31 * h + r.grade)
+    h = _mix_double(h, r.count)
+    h = i32(31 * h + r.strategy)
+    h = i32(31 * h + key[3])                       # refResource
+    h = i32(31 * h + r.control_behavior)
+    h = i32(31 * h + r.warm_up_period_sec)
+    h = i32(31 * h + r.max_queueing_time_ms)
+    h = i32(31 * h + (1 if r.cluster_mode else 0))
+    return i32(31 * h + key[4])                    # clusterConfig
+
+
+def param_rule_hash(r, key) -> int:
+    h = abstract_rule_hash(key)
+    h = i32(31 * h + r.grade)
+    h = i32(31 * h + r.param_idx)                  # Integer.hashCode
+    h = _mix_double(h, r.count)
+    h = i32(31 * h + r.control_behavior)
+    h = i32(31 * h + r.max_queueing_time_ms)
+    h = i32(31 * h + r.burst_count)
+    d = r.duration_in_sec & 0xFFFFFFFFFFFFFFFF
+    h = i32(31 * h + i32(d ^ (d >> 32)))
+    h = i32(31 * h + key[3])                       # paramFlowItemList
+    h = i32(31 * h + 0)                            # clusterMode false
+    return i32(31 * h + 0)                         # clusterConfig null
+
+
+def hashset_order(hashes):
+    """Iteration order of a HashSet after adding elements with these hash codes in turn."""
+    cap, size = 16, 0
+    buckets = {}
+    order = []                                     # insertion order of the kept elements
+    for k, h in enumerate(hashes):
+        order.append((k, h))
+        size += 1
+        spread = lambda hh, c: ((hh & M32) ^ ((hh & M32) >> 16)) & (c - 1)  # noqa: E731
+        while True:
+            counts = {}
+            for _, hh in order:
+                b = spread(hh, cap)
+                counts[b] = counts.get(b, 0) + 1
+            b_new = spread(h, cap)
+            if counts[b_new] >= 9 and cap < 64:     # putVal -> treeifyBin -> resize
+                cap *= 2
+                continue
+            if counts[b_new] >= 9:
+                raise NotImplementedError("treeified HashMap bin")
+            break
+        if size > 0.75 * cap:
+            cap *= 2
+    spread = lambda hh, c: ((hh & M32) ^ ((hh & M32) >> 16)) & (c - 1)  # noqa: E731
+    return [k for k, _ in sorted(order, key=lambda kh: (spread(kh[1], cap), kh[0]))]
+
+
+def _flow_equal(a, ka, b, kb):
+    return (a.resource == b.resource and ka[1] == kb[1] and a.grade == b.grade and
+            double_bits(a.count) == double_bits(b.count) and a.strategy == b.strategy and
+            a.control_behavior == b.control_behavior and a.warm_up_period_sec == b.warm_up_period_sec and
+            a.max_queueing_time_ms == b.max_queueing_time_ms and bool(a.cluster_mode) == bool(b.cluster_mode) and
+            a.ref_resource == b.ref_resource and ka[3] == kb[3] and ka[4] == kb[4])
+
+
+def flow_comparator(a, ka, b, kb) -> int:
+    """FlowRuleComparator.compare (:30-55); limit_app_id 0 == "default"."""
+    if a.cluster_mode and not b.cluster_mode:
+        return 1
+    if not a.cluster_mode and b.cluster_mode:
+        return -1
+    if ka[1] == kb[1]:
+        return 0
+    if ka[1] == 0:
+        return 1
+    if kb[1] == 0:
+        return -1
+    return 0
+
+
+def valid_flow_rule(r) -> bool:
+    """FlowRuleUtil.isValidRule (FlowRuleUtil.java:170-185, 236-254)."""
+    if not (r.count >= 0) or r.grade < 0 or r.strategy < 0 or r.control_behavior < 0:
+        return False
+    if r.grade == 1:                               # FLOW_GRADE_QPS
+        cb = r.control_behavior
+        if cb == 1:
+            return r.warm_up_period_sec > 0
+        if cb == 2:
+            return r.max_queueing_time_ms > 0
+        if cb == 3:
+            return r.warm_up_period_sec > 0 and r.max_queueing_time_ms > 0
+        return True
+    return r.grade == 0                            # FLOW_GRADE_THREAD
+
+
+def valid_param_rule(r) -> bool:
+    """ParamFlowRuleUtil.isValidRule (ParamFlowRuleUtil.java:46-52), local rules."""
+    return (r.count >= 0 and r.grade >= 0 and r.burst_count >= 0 and r.control_behavior >= 0 and
+            r.duration_in_sec > 0 and r.max_queueing_time_ms >= 0)
+
+
+def _stable_sort(idx, cmp):
+    import functools
+    return sorted(idx, key=functools.cmp_to_key(cmp))      # Python's sort is stable, like Collections.sort
+
+
+def flow_rule_order(rules, keys, valid=None):
+    """Indices of the kept rules, resource by resource (first appearance), in
+    the order FlowRuleManager's per-resource list holds them."""
+    if valid is None:
+        valid = [valid_flow_rule(r) for r in rules]
+    return _rule_order(rules, keys, valid, flow_rule_hash, _flow_equal, sort=True)
+
+
+def _param_equal(items):
+    def eq(a, ka, b, kb):
+        if not (a.resource == b.resource and ka[1] == kb[1] and a.grade == b.grade and a.param_idx == b.param_idx and
+                double_bits(a.count) == double_bits(b.count) and a.control_behavior == b.control_behavior and
+                a.max_queueing_time_ms == b.max_queueing_time_ms and a.burst_count == b.burst_count and
+                a.duration_in_sec == b.duration_in_sec and a.item_count == b.item_count and ka[3] == kb[3]):
+            return False
+        for t in range(a.item_count):
+            x, y = items[a.item_offset + t], items[b.item_offset + t]
+            if (x.tag, x.bits, x.count) != (y.tag, y.bits, y.count):
+                return False
+        return True
+    return eq
+
+
+def param_rule_order(rules, keys, items, valid=None):
+    if valid is None:
+        valid = [valid_param_rule(r) for r in rules]
+    return _rule_order(rules, keys, valid, param_rule_hash, _param_equal(items), sort=False)
+
+
+def _rule_order(rules, keys, valid, hfun, eq, sort):
+    by_res = {}
+    for i, r in enumerate(rules):
+        if not valid[i]:
+            continue
+        kept = by_res.setdefault(r.resource, [])
+        if any(eq(rules[j], keys[j], r, keys[i]) for j in kept):
+            continue                                # HashSet.add of an equal rule: no change
+        kept.append(i)
+    out = []
+    for res, kept in by_res.items():
+        order = [kept[k] for k in hashset_order([hfun(rules[i], keys[i]) for i in kept])]
+        if sort:
+            order = _stable_sort(order, lambda a, b: flow_comparator(rules[a], keys[a], rules[b], keys[b]))
+        out.extend(order)
+    return out

@@ -96,6 +96,13 @@ class sf_param_rule(C.Structure):
     ]
 
 
+class sf_rule_key(C.Structure):
+    """Java hash codes of a rule's String fields (sentinel_flow.h sf_rule_key)."""
+    _fields_ = [("resource_hash", C.c_int32), ("limit_app_id", C.c_uint32),
+                ("limit_app_hash", C.c_int32), ("extra_hash", C.c_int32),
+                ("cluster_hash", C.c_int32)]
+
+
 class sf_system_rule(C.Structure):
     _fields_ = [
         ("highest_system_load", C.c_double), ("highest_cpu_usage", C.c_double),
@@ -191,7 +198,7 @@ class sf_heavy_profile(C.Structure):
 
 STRUCT_SIZES = {name: C.sizeof(cls) for name, cls in [
     ("sf_config", sf_config), ("sf_flow_rule", sf_flow_rule), ("sf_hot_item", sf_hot_item),
-    ("sf_param_rule", sf_param_rule), ("sf_system_rule", sf_system_rule),
+    ("sf_param_rule", sf_param_rule), ("sf_system_rule", sf_system_rule), ("sf_rule_key", sf_rule_key),
     ("sf_event_batch", sf_event_batch), ("sf_verdicts", sf_verdicts),
     ("sf_cluster_flow_rule", sf_cluster_flow_rule), ("sf_cluster_param_rule", sf_cluster_param_rule),
     ("sf_namespace", sf_namespace), ("sf_heavy_profile", sf_heavy_profile), ("sf_token_batch", sf_token_batch),

@@ -95,6 +95,31 @@ def _declare(L):
     f("sf_param_table_stats", I, P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(U32))
     f("sf_token_shard", I, C.POINTER(abi.sf_cluster_flow_rule), U32, C.POINTER(abi.sf_cluster_param_rule), U32,
       C.POINTER(abi.sf_namespace), U32, U32, P, P, U32, P)
+    f("sf_flow_rule_order", I, C.POINTER(abi.sf_flow_rule), C.POINTER(abi.sf_rule_key), U32, P, C.POINTER(U32))
+    f("sf_param_rule_order", I, C.POINTER(abi.sf_param_rule), C.POINTER(abi.sf_rule_key), U32,
+      C.POINTER(abi.sf_hot_item), U32, P, C.POINTER(U32))
+
+
+def flow_rule_order(rules, keys) -> np.ndarray:
+    """Indices of ``rules`` in the order FlowRuleManager holds them (invalid
+    and duplicate rules dropped; sf_flow_rule_order, host only)."""
+    n = len(rules)
+    out, m = np.zeros(max(n, 1), np.uint32), C.c_uint32(0)
+    _check(lib().sf_flow_rule_order(abi.rules_array(abi.sf_flow_rule, list(rules)),
+                                    abi.rules_array(abi.sf_rule_key, list(keys)), n, out.ctypes.data, C.byref(m)))
+    return out[:m.value].copy()
+
+
+def param_rule_order(rules, keys, items=()) -> np.ndarray:
+    """Indices of ``rules`` in the order ParamFlowRuleManager holds them
+    (sf_param_rule_order, host only)."""
+    n = len(rules)
+    out, m = np.zeros(max(n, 1), np.uint32), C.c_uint32(0)
+    _check(lib().sf_param_rule_order(abi.rules_array(abi.sf_param_rule, list(rules)),
+                                     abi.rules_array(abi.sf_rule_key, list(keys)), n,
+                                     abi.rules_array(abi.sf_hot_item, list(items)), len(items),
+                                     out.ctypes.data, C.byref(m)))
+    return out[:m.value].copy()
 
 
 def token_shard(flow, param, namespaces, shard_count: int, batch: abi.HostTokenBatch) -> np.ndarray:
