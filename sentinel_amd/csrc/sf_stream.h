@@ -94,7 +94,7 @@ struct ThrLds {
     ThrWin win[2][THR_WPC];
     uint32_t xo[2][THR_CH];                        // exit position (sorted index) of each entry, or XO_NONE
     int32_t cn[2][THR_CH];                         // acquireCount (exact path)
-    uint8_t el[2][THR_CH];                         // exit whose entry is in its window: the entry's lane, else 255
+    uint16_t dx[2][THR_CH];                        // exit: distance back to its entry (1..65535), else 0
 };
 static_assert(sizeof(ThrLds) <= HS_LDS_WORDS * 8, "THREAD LDS layout exceeds the stream kernel's LDS");
 
@@ -112,27 +112,36 @@ __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) 
     return (unsigned long long)uniform64((int64_t)v);
 }
 
-// Helper wave h (1..3): prepare windows h-1, h+2, ... of the chunk starting at q0.
-// Every load of the wave's windows is issued before any is used (one memory
-// round trip per chunk; indices clamped into the segment instead of branches).
+// Helper wave h (1..3): prepare windows h-1, h+2, ... of the chunk starting at
+// q0.  Two steps, software-pipelined one chunk ahead: thr_issue puts every
+// global load of the wave's windows in flight (indices clamped into the
+// segment instead of branches), thr_finish (one chunk later, after the loads
+// have landed) builds the window summaries in LDS.  Far live-exit words may be
+// read that early: a far mark lands at least LX_WORDS - 1 windows past the
+// entry that makes it, and the decider fences those before each barrier.
 constexpr int THR_WPW = THR_WPC / 3;              // windows per helper wave
-__device__ void thr_prepare(ThrLds& L, int buf, const SegIO& io, const uint32_t* exit_of,
-                            const unsigned long long* lxfar, uint32_t q0, uint32_t lo, uint32_t hi, int h) {
-    const int lane = (int)(threadIdx.x & 63);
+struct ThrPre {
     uint8_t fa[THR_WPW]; int32_t ca[THR_WPW]; int64_t ra[THR_WPW]; uint32_t xa[THR_WPW];
     unsigned long long f0a[THR_WPW], f1a[THR_WPW];
+};
+__device__ __forceinline__ void thr_issue(ThrPre& P, const SegIO& io, const uint32_t* exit_of,
+                                          const unsigned long long* lxfar, uint32_t q0, uint32_t hi, int h) {
+    const int lane = (int)(threadIdx.x & 63);
 #pragma unroll
     for (int k = 0; k < THR_WPW; k++) {
         const uint32_t q = q0 + 64u * (uint32_t)(h - 1 + 3 * k);
         const uint32_t jc = min(q + (uint32_t)lane, hi - 1);
-        fa[k] = io.flags[jc];
-        ca[k] = io.cnt[jc];
-        ra[k] = io.eref ? io.eref[jc] : -1;
-        xa[k] = exit_of[jc];
+        P.fa[k] = io.flags[jc];
+        P.ca[k] = io.cnt[jc];
+        P.ra[k] = io.eref ? io.eref[jc] : -1;
+        P.xa[k] = exit_of[jc];
         const uint32_t g = min(q, hi - 1) >> 6;
-        f0a[k] = __hip_atomic_load(lxfar + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        f1a[k] = __hip_atomic_load(lxfar + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        P.f0a[k] = __hip_atomic_load(lxfar + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        P.f1a[k] = __hip_atomic_load(lxfar + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+__device__ void thr_finish(ThrLds& L, int buf, const ThrPre& P, uint32_t q0, uint32_t lo, uint32_t hi, int h) {
+    const int lane = (int)(threadIdx.x & 63);
 #pragma unroll
     for (int k = 0; k < THR_WPW; k++) {
         const int wl = h - 1 + 3 * k;
@@ -140,9 +149,9 @@ __device__ void thr_prepare(ThrLds& L, int buf, const SegIO& io, const uint32_t*
         if (q >= hi) break;
         const uint32_t j = q + (uint32_t)lane;
         const bool valid = j < hi;
-        const uint8_t f = fa[k];
-        const int32_t c = ca[k];
-        const int64_t ref = ra[k];
+        const uint8_t f = P.fa[k];
+        const int32_t c = P.ca[k];
+        const int64_t ref = P.ra[k];
         const bool ent = valid && !(f & SF_EV_EXIT);
         const bool ex = valid && (f & SF_EV_EXIT);
         ThrWin wn;
@@ -152,15 +161,15 @@ __device__ void thr_prepare(ThrLds& L, int buf, const SegIO& io, const uint32_t*
         wn.flags = (gt8 ? 1u : 0u) | (__ballot(ent && c > THR_CBIG) ? 2u : 0u) | (gt1 ? 4u : 0u);
         // bound of max(rank + acquireCount): (entries - 1) + (1, or 8 when some count is 2..8)
         wn.maxrc = gt8 ? INT32_MAX : (int32_t)__popcll(wn.ent) - 1 + (gt1 ? THR_CSMALL : 1);
-        L.xo[buf][64 * wl + lane] = ent ? xa[k] : XO_NONE;
+        L.xo[buf][64 * wl + lane] = ent ? P.xa[k] : XO_NONE;
         L.cn[buf][64 * wl + lane] = c;
-        L.el[buf][64 * wl + lane] = (ex && ref >= (int64_t)q && ref < (int64_t)j) ? (uint8_t)(ref - (int64_t)q) : (uint8_t)255;
+        L.dx[buf][64 * wl + lane] = (ex && ref >= 0 && (int64_t)j - ref <= 65535) ? (uint16_t)((int64_t)j - ref) : (uint16_t)0;
         const unsigned long long mo = __ballot(ex && ref == -1);       // entry of an earlier batch: live
         if (lane == 0) {
             L.win[buf][wl] = wn;
             // live exits of far-away entries (written into HBM when those entries passed)
             const uint32_t sh = q & 63;
-            const unsigned long long far = sh ? (f0a[k] >> sh) | (f1a[k] << (64 - sh)) : f0a[k];
+            const unsigned long long far = sh ? (P.f0a[k] >> sh) | (P.f1a[k] << (64 - sh)) : P.f0a[k];
             const unsigned long long add = (mo | far) & (q + 64 <= hi ? ~0ull : ((1ull << (hi - q)) - 1ull));
             if (add) atomicOr(&L.lx[((q - lo) >> 6) % LX_WORDS], add);
         }
@@ -252,6 +261,12 @@ __device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) 
     return ((unsigned long long)b << 32) | a;
 }
 
+// THR_SW consecutive windows whose entries all fit are taken in one step.
+constexpr int THR_SW = 4;
+#ifndef SF_SOLVE_MIN_ROOM
+#define SF_SOLVE_MIN_ROOM 0
+#endif
+
 __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32_t q0, uint32_t lo, uint32_t hi,
                            double M, int64_t IM, int64_t& T, unsigned long long* pbits
 #ifdef SF_STREAM_PROF
@@ -283,87 +298,145 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
 #endif
     while (w < nwin) {
         const uint32_t q = q0 + 64 * w;
-        const uint32_t slot = (slot0 + w) % LX_WORDS;
-        const uint32_t xo = L.xo[buf][64 * w + lane];
-        const int32_t c = L.cn[buf][64 * w + lane];
-        const int eln = L.el[buf][64 * w + lane];
-        const unsigned long long me = rl64(r_ent, (int)w);
-        const uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)r_flags, (int)w);
         const int64_t room0 = IM - T;
         const bool tsmall = T >= (int64_t)INT32_MIN + 64 && T + (int64_t)THR_CBIG + 64 <= (int64_t)INT32_MAX;
+        {
+            // a run of windows without entries: their live exits only release threads
+            const unsigned long long noent = __ballot((uint32_t)lane < nwin && r_ent == 0ull) >> w;
+            if (noent & 1ull) {
+                const uint32_t e = min(w + (uint32_t)(__ffsll((long long)~noent) - 1), nwin);
+                const bool in = (uint32_t)lane >= w && (uint32_t)lane < e;
+                const int nl = wave_scan_add(in ? __popcll(r_lx) : 0);
+                T = uniform64(T - (int64_t)__builtin_amdgcn_readlane(nl, 63));
+                if (in) L.lx[(slot0 + (uint32_t)lane) % LX_WORDS] = 0ull;
+                w = e;
+#ifdef SF_STREAM_PROF
+                prof[9]++;
+#endif
+                continue;
+            }
+        }
         if (room0 <= 0 && tsmall) {
             // saturated: skip the windows with no live exit (all their entries block)
             const unsigned long long stop = (__ballot((uint32_t)lane < nwin && r_lx != 0ull) | bigm) >> w;
+#ifdef SF_STREAM_PROF
+            prof[9]++;
+#endif
             if (!stop) { w = nwin; break; }
             const uint32_t k = (uint32_t)(__ffsll((long long)stop) - 1);
             if (k > 0) { w += k; continue; }
+        }
+        const unsigned long long me = rl64(r_ent, (int)w);
+        const uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)r_flags, (int)w);
+        const uint32_t slot = (slot0 + w) % LX_WORDS;
+        if (w + THR_SW <= nwin && tsmall && room0 >= 64 && !((bigm >> w) & ((1ull << THR_SW) - 1ull))) {
+            // ---- THR_SW windows whose entries all fit even with every earlier entry
+            // of them holding a thread: all pass, every exit of them inside is live
+            const bool inr = (uint32_t)lane >= w && (uint32_t)lane < w + THR_SW;
+            const int ne_ = wave_scan_add(inr ? __popcll(r_ent) : 0);
+            const int sument = __builtin_amdgcn_readlane(ne_, 63);
+            const unsigned long long f1 = __ballot(inr && (r_flags & 1u)), f4 = __ballot(inr && (r_flags & 4u));
+            if (!f1 && room0 >= (int64_t)sument - 1 + (f4 ? THR_CSMALL : 1)) {
+                const uint32_t qe = q + 64u * THR_SW;
+                bool anyin = false;
+#pragma unroll
+                for (int k = 0; k < THR_SW; k++) {
+                    const int pos = 64 * k + lane;
+                    const uint32_t xo_k = L.xo[buf][64 * (w + k) + lane];
+                    const int d = L.dx[buf][64 * (w + k) + lane];
+                    const unsigned long long me_k = rl64(r_ent, (int)w + k);
+                    const unsigned long long ml_k = rl64(r_lx, (int)w + k) | __ballot(d >= 1 && d <= pos);
+                    T += (int64_t)__popcll(me_k) - (int64_t)__popcll(ml_k);
+                    // exits beyond the superwindow of its passed entries turn live
+                    const bool mk = ((me_k >> lane) & 1ull) && xo_k != XO_NONE && xo_k < hi && xo_k >= qe;
+                    bool fm2 = false;
+                    if (mk) fm2 = thr_mark_exit(L, lxfar, xo_k, q, lo);
+                    far_marked |= __ballot(fm2) != 0;
+                    anyin |= __ballot(mk && xo_k < qend) != 0ull;
+                    if ((uint32_t)lane == w + (uint32_t)k) pst = me_k;
+                }
+                T = uniform64(T);
+                if (anyin) r_lx |= ((uint32_t)lane >= w + THR_SW && (uint32_t)lane < nwin) ? L.lx[(slot0 + lane) % LX_WORDS] : 0ull;
+                if (inr) L.lx[(slot0 + (uint32_t)lane) % LX_WORDS] = 0ull;
+                w += THR_SW;
+#ifdef SF_STREAM_PROF
+                prof[4]++;
+#endif
+                continue;
+            }
         }
         unsigned long long ml = rl64(r_lx, (int)w);            // live exits of this window
         const int32_t maxrc = __builtin_amdgcn_readlane(r_maxrc, (int)w);
         unsigned long long pmask = 0;
         const bool nowrap = !(flags & 2u) && tsmall;
-        if (me == 0) {
-            T -= __popcll(ml);
-        } else if (nowrap && room0 + (int64_t)__popcll(ml) < 1) {
+        if (nowrap && room0 + (int64_t)__popcll(ml) < 1) {
             // even with every live exit first, no entry fits (acquireCount >= 1):
             // all entries block, so no exit of this window's entries turns live
             T -= __popcll(ml);
-        } else if (nowrap && room0 >= (int64_t)maxrc) {
-            // the thread count before an entry is <= T + (entries before it): all fit
-            pmask = me;
-            ml |= rl64(r_inw, (int)w);                     // exits of this window's entries, inside it
-            T += (int64_t)__popcll(me) - (int64_t)__popcll(ml);
-        } else if (nowrap && !(flags & 1u) && room0 >= 0) {
-            pmask = thr_window_solve((int)room0, me, ml, c, eln);
-            T += (int64_t)__popcll(pmask) - (int64_t)__popcll(ml);
         } else {
-            const bool small = nowrap && !(flags & 1u);
-            const bool ones = nowrap && !(flags & 4u);      // every acquireCount is 1: scalar candidates
-            // in-window exit of each entry lane: bit position, or 64
-            const uint32_t inpos = (xo != XO_NONE && xo - q < 64u && xo > q + (uint32_t)lane) ? xo - q : 64u;
-            const bool ent = (me >> lane) & 1ull;
-            int cursor = 0;
-            while (cursor < 64) {
-                unsigned long long fm = 0;
-                if (ones) {
-                    fm = IM - T > 0 ? me : 0ull;
-                } else if (small) {
-                    // without int wrap (int)(T + c) <= count  <=>  c <= floor(count) - T
-                    const int64_t room = IM - T;
-                    if (room >= THR_CSMALL) fm = me;
-                    else if (room > 0) fm = __ballot(ent && (int64_t)c <= room);
-                } else {
-                    fm = __ballot(ent && (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)c) <= M);
+            const uint32_t xo = L.xo[buf][64 * w + lane];
+            if (nowrap && room0 >= (int64_t)maxrc) {
+                // the thread count before an entry is <= T + (entries before it): all fit
+                pmask = me;
+                ml |= rl64(r_inw, (int)w);                 // exits of this window's entries, inside it
+                T += (int64_t)__popcll(me) - (int64_t)__popcll(ml);
+            } else if (nowrap && !(flags & 1u) && room0 >= SF_SOLVE_MIN_ROOM) {
+                const int32_t c = L.cn[buf][64 * w + lane];
+                const int dd = L.dx[buf][64 * w + lane];
+                const int eln = (dd >= 1 && dd <= lane) ? lane - dd : 255;   // in-window entry lane
+                pmask = thr_window_solve((int)room0, me, ml, c, eln);
+                T += (int64_t)__popcll(pmask) - (int64_t)__popcll(ml);
+            } else {
+                const int32_t c = L.cn[buf][64 * w + lane];
+                const bool small = nowrap && !(flags & 1u);
+                const bool ones = nowrap && !(flags & 4u);  // every acquireCount is 1: scalar candidates
+                // in-window exit of each entry lane: bit position, or 64
+                const uint32_t inpos = (xo != XO_NONE && xo - q < 64u && xo > q + (uint32_t)lane) ? xo - q : 64u;
+                const bool ent = (me >> lane) & 1ull;
+                int cursor = 0;
+                while (cursor < 64) {
+                    unsigned long long fm = 0;
+                    if (ones) {
+                        fm = IM - T > 0 ? me : 0ull;
+                    } else if (small) {
+                        // without int wrap (int)(T + c) <= count  <=>  c <= floor(count) - T
+                        const int64_t room = IM - T;
+                        if (room >= THR_CSMALL) fm = me;
+                        else if (room > 0) fm = __ballot(ent && (int64_t)c <= room);
+                    } else {
+                        fm = __ballot(ent && (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)c) <= M);
+                    }
+                    const unsigned long long cand = (fm | ml) & (~0ull << cursor);
+                    if (!cand) break;
+                    const int kk = __ffsll((long long)cand) - 1;
+                    const unsigned long long bit = 1ull << kk;
+                    if (me & bit) {
+                        T += 1; pmask |= bit;
+                        const uint32_t ip = (uint32_t)__builtin_amdgcn_readlane((int)inpos, kk);
+                        if (ip < 64u) ml |= 1ull << ip;
+                    } else {
+                        T -= 1;
+                    }
+                    cursor = kk + 1;
                 }
-                const unsigned long long cand = (fm | ml) & (~0ull << cursor);
-                if (!cand) break;
-                const int kk = __ffsll((long long)cand) - 1;
-                const unsigned long long bit = 1ull << kk;
-                if (me & bit) {
-                    T += 1; pmask |= bit;
-                    const uint32_t ip = (uint32_t)__builtin_amdgcn_readlane((int)inpos, kk);
-                    if (ip < 64u) ml |= 1ull << ip;
-                } else {
-                    T -= 1;
-                }
-                cursor = kk + 1;
+            }
+            T = uniform64(T);
+            if (pmask) {
+                // exits of the passed entries beyond this window turn live (one vector step)
+                const bool mk = ((pmask >> lane) & 1ull) && xo != XO_NONE && xo < hi && xo >= q + 64;
+                bool fm2 = false;
+                if (mk) fm2 = thr_mark_exit(L, lxfar, xo, q, lo);
+                far_marked |= __ballot(fm2) != 0;
+                if ((uint32_t)lane == w) pst = pmask;      // pass bits staged: lane w <-> window w
+                if (__ballot(mk && xo < qend))             // exits inside this chunk: refresh its words
+                    r_lx |= ((uint32_t)lane > w && (uint32_t)lane < nwin) ? L.lx[(slot0 + lane) % LX_WORDS] : 0ull;
             }
         }
         T = uniform64(T);
-        if (pmask) {
-            // exits of the passed entries beyond this window turn live (one vector step)
-            const bool mk = ((pmask >> lane) & 1ull) && xo != XO_NONE && xo < hi && xo >= q + 64;
-            bool fm2 = false;
-            if (mk) fm2 = thr_mark_exit(L, lxfar, xo, q, lo);
-            far_marked |= __ballot(fm2) != 0;
-            if ((uint32_t)lane == w) pst = pmask;          // pass bits staged: lane w <-> window w
-            if (__ballot(mk && xo < qend))                 // exits inside this chunk: refresh its words
-                r_lx |= ((uint32_t)lane > w && (uint32_t)lane < nwin) ? L.lx[(slot0 + lane) % LX_WORDS] : 0ull;
-        }
         if (lane == 0) L.lx[slot] = 0ull;                  // consumed: reused LX_WORDS windows later
         w++;
 #ifdef SF_STREAM_PROF
-        prof[3]++;
+        prof[7]++;
 #endif
     }
 #ifdef SF_STREAM_PROF
@@ -498,10 +571,15 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
         int64_t T = st.threads[res];
         const int h = (int)(threadIdx.x >> 6);
         const uint32_t ntc = (hi - lo + THR_CH - 1) / THR_CH;
-        if (h > 0) thr_prepare(L, 0, io, hc.exit_of, hc.lxfar, lo, lo, hi, h);
+        ThrPre P;
+        if (h > 0) {
+            thr_issue(P, io, hc.exit_of, hc.lxfar, lo, hi, h);
+            thr_finish(L, 0, P, lo, lo, hi, h);
+            if (ntc > 1) thr_issue(P, io, hc.exit_of, hc.lxfar, lo + THR_CH, hi, h);
+        }
         __syncthreads();
 #ifdef SF_STREAM_PROF
-        uint64_t t_work = 0, t_bar = 0, tprof[4] = {0, 0, 0, 0};
+        uint64_t t_work = 0, t_bar = 0, tprof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
         for (uint32_t k = 0; k < ntc; k++) {
             const uint32_t q0 = lo + k * THR_CH;
@@ -513,7 +591,10 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
 #else
             if (h == 0) thr_decide(L, k & 1, hc.lxfar, q0, lo, hi, M, IM, T, hc.passbits);
 #endif
-            else if (k + 1 < ntc) thr_prepare(L, (k + 1) & 1, io, hc.exit_of, hc.lxfar, q0 + THR_CH, lo, hi, h);
+            else if (k + 1 < ntc) {
+                thr_finish(L, (k + 1) & 1, P, q0 + THR_CH, lo, hi, h);
+                if (k + 2 < ntc) thr_issue(P, io, hc.exit_of, hc.lxfar, q0 + 2 * THR_CH, hi, h);
+            }
 #ifdef SF_STREAM_PROF
             const uint64_t c1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -527,6 +608,10 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
             printf("SF_STREAM_PROF seg %u wave %d events %u chunks %u: work %lu barrier %lu cycles; prologue %lu loop %lu epilogue %lu windows %lu\n",
                    s, h, hi - lo, ntc, (unsigned long)t_work, (unsigned long)t_bar, (unsigned long)tprof[0],
                    (unsigned long)tprof[1], (unsigned long)tprof[2], (unsigned long)tprof[3]);
+        if (h == 0 && (threadIdx.x & 63) == 0)
+            printf("SF_STREAM_PROF2 sw %lu solve %lu sw_total %lu single %lu single_cyc %lu skips %lu rounds %lu\n",
+                   (unsigned long)tprof[4], (unsigned long)tprof[5], (unsigned long)tprof[6], (unsigned long)tprof[7],
+                   (unsigned long)tprof[8], (unsigned long)tprof[9], (unsigned long)tprof[3]);
 #endif
     } else {                                                     // SM_RL
         int64_t* tsb = (int64_t*)smem;                           // [2][HS_CH]

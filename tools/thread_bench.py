@@ -9,6 +9,7 @@ import numpy as np  # noqa: E402
 from sentinel_amd import abi, engine, trace  # noqa: E402
 
 engine.lib()
+CHECK = os.environ.get("CHECK", "1") == "1"
 
 
 def one(n_entry, count, rt_mean=20.0, duration=4000, seed=1, exits=True):
@@ -38,7 +39,6 @@ def one(n_entry, count, rt_mean=20.0, duration=4000, seed=1, exits=True):
     e.load_flow_rules(rules)
     db = engine.DeviceBatch(e, b)
     out = engine.DeviceVerdicts(e, b.n)
-    e.submit_device(db, out)
     e.set_timing(True)
     e.submit_device(db, out)
     e.sync()
@@ -46,6 +46,13 @@ def one(n_entry, count, rt_mean=20.0, duration=4000, seed=1, exits=True):
     prof = e.heavy_profile()
     us = prof[0][3] if prof else -1
     npass = int((out.status.numpy() == abi.V_PASS).sum())
+    if CHECK and b.n <= 6_000_000:
+        from oracle import oracle as so
+        o = so.OracleEngine(cfg)
+        o.load_flow_rules(rules)
+        want = o.submit(b)
+        o.close()
+        assert (want.status == out.status.numpy()).all(), "verdicts differ from the oracle"
     print(f"entries {n_entry:9d} events {b.n:9d} count {count:5d} exits {exits}: stream {st.stream_ms:8.3f} ms "
           f"segment {us:9.0f} us  {us * 1e3 / b.n:7.2f} ns/event  passes {npass}", flush=True)
 
