@@ -530,8 +530,8 @@ SF_HD void emit_verdict(const SegIO& io, uint32_t j, uint8_t status, int32_t wai
     if (!io.perm) return;
     const uint32_t i = io.perm[j];
     io.o_status[i] = status;
-    if (io.o_wait) io.o_wait[i] = wait;
-    if (io.o_rule) io.o_rule[i] = rule;
+    if (io.o_wait && wait) io.o_wait[i] = wait;          // (cleared before the decide phase)
+    if (io.o_rule && rule) io.o_rule[i] = rule;
 }
 
 // ParamFlowChecker.passLocalCheck (:84-112): one value, or every element of a

@@ -71,6 +71,7 @@ struct HeavyCtx {
     unsigned long long* passbits;                       // [n/64+2] bit j: entry j passed (QPS/WarmUp/RL/THREAD)
     const uint32_t* exit_of;                            // [n] sorted index of an entry's exit (or ~0)
     unsigned long long* lxfar;                          // [n/64+2] live exits beyond the LDS ring (SM_THREAD)
+    const uint2* thr_rec;                               // [n] SM_THREAD event records (k_thr_prep)
 };
 
 SF_HD bool pass_bit(const unsigned long long* pb, uint32_t j) { return (pb[j >> 6] >> (j & 63)) & 1ull; }

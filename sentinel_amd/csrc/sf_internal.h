@@ -109,7 +109,11 @@ struct EntryAcc {
 };
 
 // 16-B radix-sort payload of one event (batch time span < 2^32 ms)
-struct alignas(16) PackedEv { uint32_t idx, dts; int32_t cnt; uint32_t flags; };
+// Sort payload, 8 B: submission index, and meta = time offset from the batch's
+// first event (16 bits, PV_DTS_FAR: read the batch's ts) | flags (8 bits) << 16
+// | acquireCount (8 bits, 1..255; 0: read the batch's count) << 24.
+struct alignas(8) PackedEv { uint32_t idx, meta; };
+constexpr uint32_t PV_DTS_FAR = 0xffffu;
 
 // light segments are listed by length class (len 1, 2, 3-4, 5-8, ...) so the
 // lanes of a wavefront interpret segments of similar length
@@ -159,6 +163,7 @@ struct Work {
     unsigned long long* passbits;                       // [n/64+2] pass bit per sorted entry (heavy segments)
     uint32_t* exit_of;                                  // [n] sorted index of each entry's exit, ~0 if none
     unsigned long long* lxfar;                          // [n/64+2] far live exits (SM_THREAD)
+    uint2* thr_rec;                                     // [n] THREAD-segment event records (k_thr_prep, sf_stream.h)
 };
 
 // Device view of a caller batch (pointers already on device).

@@ -39,14 +39,13 @@ __global__ void k_init_state(DevState st, size_t n_sec, size_t n_min) {
     for (size_t k = i; k < st.R; k += stride) st.threads[k] = 0;
 }
 
-// Sort payload: the radix sort carries each event's (index, time offset from
-// the batch's first event, acquireCount, flags) as a 16-B value, so the sorted
-// order is read back with coalesced loads instead of a random gather from the
-// submission-order arrays.  A batch whose times do not fit 32-bit offsets from
-// its first event (never for a time-ordered batch shorter than 49 days) sets
-// *wide and k_unpack reads those times from the batch instead.
+// Sort payload: the radix sort carries each event's index, time offset from
+// the batch's first event, flags and acquireCount packed into 8 bytes
+// (PackedEv), so the sorted order is read back with coalesced loads instead of
+// a random gather from the submission-order arrays; an offset or count that
+// does not fit is read from the batch by k_unpack for that event only.
 __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t shard_count, uint32_t shard_index,
-                              uint32_t R, int32_t* err, uint32_t* wide, const int64_t* last_ts) {
+                              uint32_t R, int32_t* err, const int64_t* last_ts) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;
     uint32_t r = b.res[i];
@@ -57,18 +56,21 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t
     if (b.ts[i] < (i ? b.ts[i - 1] : *last_ts)) *err = SF_ERR_INVALID;
     keys[i] = l;
     const int64_t d = b.ts[i] - b.ts[0];
-    if (d < 0 || d > (int64_t)0xffffffffLL) *wide = 1u;
-    PackedEv v;
+    const uint32_t dts = (d >= 0 && d < (int64_t)PV_DTS_FAR) ? (uint32_t)d : PV_DTS_FAR;
     const uint8_t f = b.flags[i];
-    v.idx = i; v.dts = (uint32_t)d; v.cnt = b.cnt[i]; v.flags = f & 0x0Fu;
+    uint32_t fl = f & 0x0Fu;
     if (b.sys && (f & SF_EV_IN) && !(f & SF_EV_EXIT)) {          // SystemBlockException forced by the planner
-        const uint8_t r = b.sys[i];
-        if (r != SYS_NONE) v.flags |= EVF_SYSBLK | ((uint32_t)r << EVF_SYSREASON_SHIFT);
+        const uint8_t sr = b.sys[i];
+        if (sr != SYS_NONE) fl |= EVF_SYSBLK | ((uint32_t)sr << EVF_SYSREASON_SHIFT);
     }
+    const int32_t c = b.cnt[i];
+    const uint32_t c8 = (c >= 1 && c <= 255) ? (uint32_t)c : 0u;
+    PackedEv v;
+    v.idx = i; v.meta = dts | (fl << 16) | (c8 << 24);
     pv[i] = v;
 }
 
-__global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* wide, uint32_t* perm, int64_t* s_ts,
+__global__ void k_unpack(DevBatch b, const PackedEv* pv, uint32_t* perm, int64_t* s_ts,
                          int32_t* s_cnt, uint8_t* s_flags, uint8_t* s_nargs, uint8_t* s_atag,
                          uint64_t* s_abits, const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag,
                          int64_t* last_ts, const int32_t* err) {
@@ -77,10 +79,11 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* wide, u
     if (j == 0 && *err == 0) *last_ts = b.ts[b.n - 1];   // k_keys_packed of this batch has read the old value
     const PackedEv v = pv[j];
     const uint32_t i = v.idx;
-    const int32_t c = v.cnt;
-    const uint8_t f = (uint8_t)v.flags;
+    const uint32_t dts = v.meta & 0xffffu, c8 = v.meta >> 24;
+    const int32_t c = c8 ? (int32_t)c8 : b.cnt[i];
+    const uint8_t f = (uint8_t)(v.meta >> 16);
     perm[j] = i;
-    s_ts[j] = *wide ? b.ts[i] : b.ts[0] + (int64_t)v.dts; s_cnt[j] = c; s_flags[j] = f;
+    s_ts[j] = dts != PV_DTS_FAR ? b.ts[0] + (int64_t)dts : b.ts[i]; s_cnt[j] = c; s_flags[j] = f;
     if (!(f & SF_EV_EXIT) && ((f & (SF_EV_PRIO | EVF_SYSBLK)) || c <= 0)) {
         uint32_t s = head_scan[j] + head[j] - 1;
         atomicOr(&segflag[s], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) |
@@ -263,6 +266,7 @@ static HeavyCtx heavy_ctx(const Work& w) {
     hc.passbits = w.passbits;
     hc.exit_of = w.exit_of;
     hc.lxfar = w.lxfar;
+    hc.thr_rec = w.thr_rec;
     return hc;
 }
 
@@ -422,6 +426,32 @@ __global__ void __launch_bounds__(1024) k_fill_tiles(HeavyCtx hc, StreamCtx sc, 
     if (threadIdx.x == 0) ntiles[c] = min(carry, cap);
 }
 
+// Event records of the THREAD-grade stream segments (state-independent, so in
+// the sort phase): the serial chain's loaders then move 8 B per event with one
+// load each and no decoding (sf_stream.h ThrRec).  Grid-stride over the
+// stream class's fill tiles.
+__global__ void __launch_bounds__(256) k_thr_prep(const uint8_t* flags, const int32_t* cnt, const int64_t* eref,
+                                                  HeavyCtx hc, const uint2* tiles, const uint32_t* ntiles) {
+    const uint32_t nt = ntiles[1];
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const uint2 tl = tiles[t];
+        const uint32_t s = tl.x;
+        if (hc.seg_mode[s] != SM_THREAD) continue;
+        const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1];
+        for (uint32_t j = max(tl.y * FILL_TILE, lo) + threadIdx.x; j < min(tl.y * FILL_TILE + FILL_TILE, hi); j += 256) {
+            const uint8_t f = flags[j];
+            uint2 r;
+            if (!(f & SF_EV_EXIT)) { r.x = hc.exit_of[j]; r.y = (uint32_t)cnt[j]; }
+            else {
+                const int64_t ref = eref ? eref[j] : -1;
+                r.x = ref >= 0 ? j - (uint32_t)ref : 0u;
+                r.y = THR_REC_EXIT | (ref == -1 ? THR_REC_LIVE : 0u);
+            }
+            ((uint2*)hc.thr_rec)[j] = r;
+        }
+    }
+}
+
 // Verdicts and per-window counter deltas of the heavy segments of one class.
 // A tile is one segment's part of an aligned FILL_TILE-event block of the
 // sorted batch; lane t owns the aligned group of 16 events at block + 16 t, so
@@ -563,8 +593,8 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
             const uint32_t j = base + (uint32_t)k;
             if (j < a || j >= b) continue;
             io.o_status[pm[k]] = vs[k];
-            if (io.o_wait) io.o_wait[pm[k]] = vw[k];
-            if (io.o_rule) io.o_rule[pm[k]] = vr[k];
+            if (io.o_wait && vw[k]) io.o_wait[pm[k]] = vw[k];       // (cleared before the decide phase)
+            if (io.o_rule && vr[k]) io.o_rule[pm[k]] = vr[k];
         }
         if (!gp.n_touch) continue;
         // window rows of the group's first and last event (time-sorted): usually one
@@ -688,9 +718,8 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     const unsigned T = 256;
     if (timing) hipEventRecord(ev[0], s);
     hipError_t e;
-    hipMemsetAsync(w.wide, 0, 4, s);
     hipLaunchKernelGGL(k_keys_packed, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.pv_in, shard_count,
-                       shard_index, st.R, st.err, w.wide, st.last_ts);
+                       shard_index, st.R, st.err, st.last_ts);
     e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.pv_in, w.pv_out, n, 0u,
                                   key_bits, s);
     if (e != hipSuccess) return e;
@@ -701,7 +730,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     hipLaunchKernelGGL(k_segments, dim3(blocks(n, T)), dim3(T), 0, s, w.keys_out, w.head, w.head_scan, n,
                        w.seg_start, w.seg_res, w.n_seg, w.segflag);
     if (timing) hipEventRecord(ev[1], s);
-    hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.wide, w.perm, w.s_ts, w.s_cnt,
+    hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.perm, w.s_ts, w.s_cnt,
                        w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag, st.last_ts, st.err);
     hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
     if (b.eref)
@@ -720,6 +749,8 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     HeavyCtx hc = heavy_ctx(w);
     StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, nullptr, w.counters + 7};
     hipLaunchKernelGGL(k_fill_tiles, dim3(2), dim3(1024), 0, s, hc, sc, w.fill_tiles, w.fill_tile_cap, w.fill_ntiles);
+    hipLaunchKernelGGL(k_thr_prep, dim3(1024), dim3(256), 0, s, w.s_flags, w.s_cnt, b.eref ? w.s_eref : nullptr, hc,
+                       w.fill_tiles + w.fill_tile_cap, w.fill_ntiles);
     if (timing) hipEventRecord(ev[2], s);
     return hipGetLastError();
 }
@@ -744,6 +775,10 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     const uint32_t max_seg = n < st.R ? n : st.R;
     const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
     StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, timing ? w.sticks : nullptr, w.counters + 7};
+    // waits and rule indices are zero for almost every event: clear them with
+    // coalesced stores, then the deciding kernels scatter only the nonzero ones
+    if (out.wait) hipMemsetAsync(out.wait, 0, (size_t)n * sizeof(int32_t), s);
+    if (out.rule) hipMemsetAsync(out.rule, 0, (size_t)n * sizeof(uint16_t), s);
     hipEventRecord(ev[5], s);                      // fork
     hipEventRecord(ev[11], s);
     hipLaunchKernelGGL(k_heavy_stream, dim3(std::min(max_heavy, w.stream_grid)), dim3(HS_T), 0, s, st, io, hc, sc);

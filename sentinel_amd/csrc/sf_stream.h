@@ -89,13 +89,23 @@ struct ThrWin {                                    // 24 B per window
     uint32_t flags;                                // bit 0: an acquireCount > 8, bit 1: > THR_CBIG, bit 2: > 1
 };
 
+// Event record (k_thr_prep, one per event of a THREAD segment, 8 B):
+//   entry: x = sorted position of its exit (or XO_NONE), y = acquireCount (>= 1)
+//   exit:  x = distance back to its entry in the segment (0: none), y = THR_REC_EXIT
+//          (| THR_REC_LIVE: the entry was decided earlier, the exit is live)
+constexpr uint32_t THR_REC_EXIT = 0x80000000u;
+constexpr uint32_t THR_REC_LIVE = 1u;
+
 struct ThrLds {
     unsigned long long lx[LX_WORDS];               // live exits of window (pos - lo) / 64 at word % LX_WORDS
     ThrWin win[2][THR_WPC];
-    uint32_t xo[2][THR_CH];                        // exit position (sorted index) of each entry, or XO_NONE
-    int32_t cn[2][THR_CH];                         // acquireCount (exact path)
-    uint16_t dx[2][THR_CH];                        // exit: distance back to its entry (1..65535), else 0
+    uint2 rec[2][THR_CH];                          // event records of the chunk
 };
+__device__ __forceinline__ uint32_t rec_xo(uint2 r) { return r.x; }                    // entries
+__device__ __forceinline__ int32_t rec_c(uint2 r) { return (int32_t)r.y; }              // entries
+__device__ __forceinline__ int rec_d(uint2 r) {                                         // exits: distance, or 0
+    return (r.y & THR_REC_EXIT) && r.x < 65536u ? (int)r.x : 0;
+}
 static_assert(sizeof(ThrLds) <= HS_LDS_WORDS * 8, "THREAD LDS layout exceeds the stream kernel's LDS");
 
 __device__ __forceinline__ int64_t uniform64(int64_t v) {
@@ -121,20 +131,16 @@ __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) 
 // entry that makes it, and the decider fences those before each barrier.
 constexpr int THR_WPW = THR_WPC / 3;              // windows per helper wave
 struct ThrPre {
-    uint8_t fa[THR_WPW]; int32_t ca[THR_WPW]; int64_t ra[THR_WPW]; uint32_t xa[THR_WPW];
+    uint2 rec[THR_WPW];
     unsigned long long f0a[THR_WPW], f1a[THR_WPW];
 };
-__device__ __forceinline__ void thr_issue(ThrPre& P, const SegIO& io, const uint32_t* exit_of,
-                                          const unsigned long long* lxfar, uint32_t q0, uint32_t hi, int h) {
+__device__ __forceinline__ void thr_issue(ThrPre& P, const uint2* rec, const unsigned long long* lxfar,
+                                          uint32_t q0, uint32_t hi, int h) {
     const int lane = (int)(threadIdx.x & 63);
 #pragma unroll
     for (int k = 0; k < THR_WPW; k++) {
-        const uint32_t q = q0 + 64u * (uint32_t)(h - 1 + 3 * k);
-        const uint32_t jc = min(q + (uint32_t)lane, hi - 1);
-        P.fa[k] = io.flags[jc];
-        P.ca[k] = io.cnt[jc];
-        P.ra[k] = io.eref ? io.eref[jc] : -1;
-        P.xa[k] = exit_of[jc];
+        const uint32_t q = min(q0, hi) + 64u * (uint32_t)(h - 1 + 3 * k);
+        P.rec[k] = rec[min(q + (uint32_t)lane, hi - 1)];
         const uint32_t g = min(q, hi - 1) >> 6;
         P.f0a[k] = __hip_atomic_load(lxfar + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         P.f1a[k] = __hip_atomic_load(lxfar + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -147,24 +153,20 @@ __device__ void thr_finish(ThrLds& L, int buf, const ThrPre& P, uint32_t q0, uin
         const int wl = h - 1 + 3 * k;
         const uint32_t q = q0 + 64u * (uint32_t)wl;
         if (q >= hi) break;
-        const uint32_t j = q + (uint32_t)lane;
-        const bool valid = j < hi;
-        const uint8_t f = P.fa[k];
-        const int32_t c = P.ca[k];
-        const int64_t ref = P.ra[k];
-        const bool ent = valid && !(f & SF_EV_EXIT);
-        const bool ex = valid && (f & SF_EV_EXIT);
+        const bool valid = q + (uint32_t)lane < hi;
+        const uint2 r = P.rec[k];
+        const bool ex = valid && (r.y & THR_REC_EXIT);
+        const bool ent = valid && !(r.y & THR_REC_EXIT);
+        const int32_t c = (int32_t)r.y;
         ThrWin wn;
         wn.ent = __ballot(ent);
-        wn.inw = __ballot(ex && ref >= (int64_t)q && ref < (int64_t)j);
+        wn.inw = __ballot(ex && r.x >= 1u && r.x <= (uint32_t)lane);
         const bool gt1 = __ballot(ent && c > 1) != 0ull, gt8 = __ballot(ent && c > THR_CSMALL) != 0ull;
         wn.flags = (gt8 ? 1u : 0u) | (__ballot(ent && c > THR_CBIG) ? 2u : 0u) | (gt1 ? 4u : 0u);
         // bound of max(rank + acquireCount): (entries - 1) + (1, or 8 when some count is 2..8)
         wn.maxrc = gt8 ? INT32_MAX : (int32_t)__popcll(wn.ent) - 1 + (gt1 ? THR_CSMALL : 1);
-        L.xo[buf][64 * wl + lane] = ent ? P.xa[k] : XO_NONE;
-        L.cn[buf][64 * wl + lane] = c;
-        L.dx[buf][64 * wl + lane] = (ex && ref >= 0 && (int64_t)j - ref <= 65535) ? (uint16_t)((int64_t)j - ref) : (uint16_t)0;
-        const unsigned long long mo = __ballot(ex && ref == -1);       // entry of an earlier batch: live
+        L.rec[buf][64 * wl + lane] = valid ? r : make_uint2(XO_NONE, THR_REC_EXIT);
+        const unsigned long long mo = __ballot(ex && (r.y & THR_REC_LIVE));   // entry of an earlier batch: live
         if (lane == 0) {
             L.win[buf][wl] = wn;
             // live exits of far-away entries (written into HBM when those entries passed)
@@ -342,8 +344,9 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
 #pragma unroll
                 for (int k = 0; k < THR_SW; k++) {
                     const int pos = 64 * k + lane;
-                    const uint32_t xo_k = L.xo[buf][64 * (w + k) + lane];
-                    const int d = L.dx[buf][64 * (w + k) + lane];
+                    const uint2 rk = L.rec[buf][64 * (w + k) + lane];
+                    const uint32_t xo_k = rec_xo(rk);
+                    const int d = rec_d(rk);
                     const unsigned long long me_k = rl64(r_ent, (int)w + k);
                     const unsigned long long ml_k = rl64(r_lx, (int)w + k) | __ballot(d >= 1 && d <= pos);
                     T += (int64_t)__popcll(me_k) - (int64_t)__popcll(ml_k);
@@ -374,20 +377,21 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
             // all entries block, so no exit of this window's entries turns live
             T -= __popcll(ml);
         } else {
-            const uint32_t xo = L.xo[buf][64 * w + lane];
+            const uint2 rw = L.rec[buf][64 * w + lane];
+            const uint32_t xo = rec_xo(rw);
             if (nowrap && room0 >= (int64_t)maxrc) {
                 // the thread count before an entry is <= T + (entries before it): all fit
                 pmask = me;
                 ml |= rl64(r_inw, (int)w);                 // exits of this window's entries, inside it
                 T += (int64_t)__popcll(me) - (int64_t)__popcll(ml);
             } else if (nowrap && !(flags & 1u) && room0 >= SF_SOLVE_MIN_ROOM) {
-                const int32_t c = L.cn[buf][64 * w + lane];
-                const int dd = L.dx[buf][64 * w + lane];
+                const int32_t c = rec_c(rw);
+                const int dd = rec_d(rw);
                 const int eln = (dd >= 1 && dd <= lane) ? lane - dd : 255;   // in-window entry lane
                 pmask = thr_window_solve((int)room0, me, ml, c, eln);
                 T += (int64_t)__popcll(pmask) - (int64_t)__popcll(ml);
             } else {
-                const int32_t c = L.cn[buf][64 * w + lane];
+                const int32_t c = rec_c(rw);
                 const bool small = nowrap && !(flags & 1u);
                 const bool ones = nowrap && !(flags & 4u);  // every acquireCount is 1: scalar candidates
                 // in-window exit of each entry lane: bit position, or 64
@@ -571,48 +575,49 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
         int64_t T = st.threads[res];
         const int h = (int)(threadIdx.x >> 6);
         const uint32_t ntc = (hi - lo + THR_CH - 1) / THR_CH;
-        ThrPre P;
-        if (h > 0) {
-            thr_issue(P, io, hc.exit_of, hc.lxfar, lo, hi, h);
-            thr_finish(L, 0, P, lo, lo, hi, h);
-            if (ntc > 1) thr_issue(P, io, hc.exit_of, hc.lxfar, lo + THR_CH, hi, h);
-        }
-        __syncthreads();
+        // The two roles run separate loops with one barrier per chunk each, so the
+        // helpers' code has straight-line load/consume order: their loads run two
+        // chunks ahead, chunk c's records in register set c & 1 (loop unrolled by 2).
+        if (h == 0) {
 #ifdef SF_STREAM_PROF
-        uint64_t t_work = 0, t_bar = 0, tprof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-        for (uint32_t k = 0; k < ntc; k++) {
-            const uint32_t q0 = lo + k * THR_CH;
-#ifdef SF_STREAM_PROF
-            const uint64_t c0 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef SF_STREAM_PROF
-            if (h == 0) thr_decide(L, k & 1, hc.lxfar, q0, lo, hi, M, IM, T, hc.passbits, tprof);
-#else
-            if (h == 0) thr_decide(L, k & 1, hc.lxfar, q0, lo, hi, M, IM, T, hc.passbits);
-#endif
-            else if (k + 1 < ntc) {
-                thr_finish(L, (k + 1) & 1, P, q0 + THR_CH, lo, hi, h);
-                if (k + 2 < ntc) thr_issue(P, io, hc.exit_of, hc.lxfar, q0 + 2 * THR_CH, hi, h);
-            }
-#ifdef SF_STREAM_PROF
-            const uint64_t c1 = __builtin_amdgcn_s_memtime();
+            uint64_t tprof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
             lds_barrier();
+            for (uint32_t k = 0; k < ntc; k++) {
 #ifdef SF_STREAM_PROF
-            t_work += c1 - c0; t_bar += __builtin_amdgcn_s_memtime() - c1;
+                thr_decide(L, k & 1, hc.lxfar, lo + k * THR_CH, lo, hi, M, IM, T, hc.passbits, tprof);
+#else
+                thr_decide(L, k & 1, hc.lxfar, lo + k * THR_CH, lo, hi, M, IM, T, hc.passbits);
 #endif
+                lds_barrier();
+            }
+#ifdef SF_STREAM_PROF
+            if ((threadIdx.x & 63) == 0)
+                printf("SF_STREAM_PROF seg %u events %u chunks %u: prologue %lu loop %lu epilogue %lu; allfit-runs %lu single %lu skips %lu\n",
+                       s, hi - lo, ntc, (unsigned long)tprof[0], (unsigned long)tprof[1], (unsigned long)tprof[2],
+                       (unsigned long)tprof[4], (unsigned long)tprof[7], (unsigned long)tprof[9]);
+#endif
+        } else {
+            // (loads past the segment are clamped into it, so every issue is
+            // unconditional and the compiler's wait counts stay exact)
+            ThrPre P0, P1;
+            thr_issue(P0, hc.thr_rec, hc.lxfar, lo, hi, h);
+            thr_issue(P1, hc.thr_rec, hc.lxfar, lo + THR_CH, hi, h);
+            thr_finish(L, 0, P0, lo, lo, hi, h);
+            thr_issue(P0, hc.thr_rec, hc.lxfar, lo + 2 * THR_CH, hi, h);
+            lds_barrier();                                           // (no fence: the loads stay in flight)
+            for (uint32_t k = 0; k < ntc; k += 2) {
+                const uint32_t q1 = lo + (k + 1) * THR_CH;            // chunk k + 1 (odd: set P1, buffer 1)
+                thr_finish(L, 1, P1, q1, lo, hi, h);
+                thr_issue(P1, hc.thr_rec, hc.lxfar, q1 + 2 * THR_CH, hi, h);
+                lds_barrier();
+                if (k + 1 >= ntc) break;
+                thr_finish(L, 0, P0, q1 + THR_CH, lo, hi, h);        // chunk k + 2 (even: set P0, buffer 0)
+                thr_issue(P0, hc.thr_rec, hc.lxfar, q1 + 3 * THR_CH, hi, h);
+                lds_barrier();
+            }
+            __builtin_amdgcn_s_waitcnt(0);                           // nothing in flight into the next segment
         }
-#ifdef SF_STREAM_PROF
-        if ((threadIdx.x & 63) == 0)
-            printf("SF_STREAM_PROF seg %u wave %d events %u chunks %u: work %lu barrier %lu cycles; prologue %lu loop %lu epilogue %lu windows %lu\n",
-                   s, h, hi - lo, ntc, (unsigned long)t_work, (unsigned long)t_bar, (unsigned long)tprof[0],
-                   (unsigned long)tprof[1], (unsigned long)tprof[2], (unsigned long)tprof[3]);
-        if (h == 0 && (threadIdx.x & 63) == 0)
-            printf("SF_STREAM_PROF2 sw %lu solve %lu sw_total %lu single %lu single_cyc %lu skips %lu rounds %lu\n",
-                   (unsigned long)tprof[4], (unsigned long)tprof[5], (unsigned long)tprof[6], (unsigned long)tprof[7],
-                   (unsigned long)tprof[8], (unsigned long)tprof[9], (unsigned long)tprof[3]);
-#endif
     } else {                                                     // SM_RL
         int64_t* tsb = (int64_t*)smem;                           // [2][HS_CH]
         int32_t* cb = (int32_t*)(smem + 2 * HS_CH);              // [2][HS_CH]

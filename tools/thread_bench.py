@@ -57,8 +57,8 @@ def one(n_entry, count, rt_mean=20.0, duration=4000, seed=1, exits=True):
           f"segment {us:9.0f} us  {us * 1e3 / b.n:7.2f} ns/event  passes {npass}", flush=True)
 
 
-if len(sys.argv) > 2:                      # one case: entries count
-    one(int(sys.argv[1]), int(sys.argv[2]))
+if len(sys.argv) > 2:                      # one case: entries count [noexit]
+    one(int(sys.argv[1]), int(sys.argv[2]), exits=len(sys.argv) < 4)
 else:
     for n, cnt in [(2_430_000, 242), (150_000, 525), (2_430_000, 100000), (150_000, 100000)]:
         one(n, cnt)
