@@ -1,0 +1,177 @@
+package com.alibaba.csp.sentinel.gpu;
+
+import java.lang.foreign.Arena;
+import java.lang.foreign.MemorySegment;
+import java.util.ArrayList;
+import java.util.List;
+import java.util.concurrent.ArrayBlockingQueue;
+import java.util.concurrent.BlockingQueue;
+import java.util.concurrent.TimeUnit;
+import java.util.concurrent.locks.LockSupport;
+
+import static com.alibaba.csp.sentinel.gpu.SentinelFlowNative.*;
+import static java.lang.foreign.ValueLayout.ADDRESS;
+import static java.lang.foreign.ValueLayout.JAVA_BYTE;
+import static java.lang.foreign.ValueLayout.JAVA_INT;
+import static java.lang.foreign.ValueLayout.JAVA_LONG;
+import static java.lang.foreign.ValueLayout.JAVA_SHORT;
+
+/**
+ * Callers enqueue one {@link Ticket} per entry / exit; a single flusher thread
+ * drains the queue into off-heap sf_event_batch SoA arrays, calls sf_submit
+ * once per batch (events in enqueue order = the mocked clock order), writes
+ * each verdict into its ticket and unparks the caller.  Timestamps are
+ * TimeUtil.currentTimeMillis() taken at enqueue and made non-decreasing in
+ * queue order, as the engine requires.
+ */
+final class EventBatcher implements Runnable {
+    static final class Ticket {
+        final Thread caller = Thread.currentThread();
+        int resource, count;
+        byte flags;
+        long ts, entryRef = -1, createTs;
+        Object[] args;
+        Ticket entry;                    // EXIT: the ENTRY's ticket (its batch index, if in the same batch)
+        long batchSeq = -1; int batchIndex = -1;
+        volatile int status = -1;
+        int waitMs, ruleIdx;
+    }
+
+    private final GpuEngine engine;
+    private final BlockingQueue<Ticket> queue;
+    private final int maxBatch;
+    private final Arena arena = Arena.ofShared();
+    private final MemorySegment res, ts, cnt, flags, eref, cts, nArgs, argTag, argBits, elemOff, elemTag, elemBits;
+    private final MemorySegment status, waitMs, ruleIdx, batch, verdicts;
+    private long seq, lastTs = Long.MIN_VALUE, loadedRuleVersion = -1;
+    static final int ARG_SLOTS = Integer.getInteger("sentinel.gpu.argSlots", 2);
+    static final int MAX_ELEMS = Integer.getInteger("sentinel.gpu.maxElems", 1 << 20);
+
+    EventBatcher(GpuEngine engine, int maxBatch) {
+        this.engine = engine;
+        this.maxBatch = maxBatch;
+        this.queue = new ArrayBlockingQueue<>(maxBatch * 4);
+        res = arena.allocate(4L * maxBatch); ts = arena.allocate(8L * maxBatch); cnt = arena.allocate(4L * maxBatch);
+        flags = arena.allocate(maxBatch); eref = arena.allocate(8L * maxBatch); cts = arena.allocate(8L * maxBatch);
+        nArgs = arena.allocate(maxBatch); argTag = arena.allocate((long) ARG_SLOTS * maxBatch);
+        argBits = arena.allocate(8L * ARG_SLOTS * maxBatch);
+        elemOff = arena.allocate(4L * ((long) ARG_SLOTS * maxBatch + 1));
+        elemTag = arena.allocate(MAX_ELEMS); elemBits = arena.allocate(8L * MAX_ELEMS);
+        status = arena.allocate(maxBatch); waitMs = arena.allocate(4L * maxBatch); ruleIdx = arena.allocate(2L * maxBatch);
+        batch = arena.allocate(EVENT_BATCH); verdicts = arena.allocate(VERDICTS);
+        Thread t = new Thread(this, "sentinel-gpu-flusher");
+        t.setDaemon(true);
+        t.start();
+    }
+
+    /** Enqueue and wait for the verdict (the caller parks; the flusher unparks it). */
+    Ticket submit(Ticket t) {
+        try {
+            queue.put(t);
+        } catch (InterruptedException ex) {
+            Thread.currentThread().interrupt();
+            throw new IllegalStateException(ex);
+        }
+        while (t.status < 0) LockSupport.park(this);
+        return t;
+    }
+
+    @Override
+    public void run() {
+        List<Ticket> drained = new ArrayList<>(maxBatch);
+        while (true) {
+            try {
+                Ticket first = queue.poll(1, TimeUnit.SECONDS);
+                if (first == null) continue;
+                drained.clear();
+                drained.add(first);
+                queue.drainTo(drained, maxBatch - 1);
+                flush(drained);
+            } catch (Throwable t) {
+                // an engine error fails the batch open (the reference never blocks on
+                // an internal error, CtSph.java:155-158): every caller passes
+                for (Ticket k : drained) { k.waitMs = 0; k.ruleIdx = 0; k.status = V_PASS; LockSupport.unpark(k.caller); }
+            }
+        }
+    }
+
+    private void flush(List<Ticket> b) throws Throwable {
+        if (engine.ruleVersion.get() != loadedRuleVersion) {
+            loadedRuleVersion = engine.ruleVersion.get();
+            engine.loadRulesNow();
+        }
+        engine.pushSystemStatus();
+        final long bs = ++seq;
+        int n = b.size(), ne = 0;
+        boolean anyExit = false;
+        elemOff.set(JAVA_INT, 0, 0);
+        for (int i = 0; i < n; i++) {
+            Ticket t = b.get(i);
+            t.batchSeq = bs; t.batchIndex = i;
+            lastTs = Math.max(lastTs, t.ts);               // non-decreasing clock in submission order
+            res.setAtIndex(JAVA_INT, i, t.resource);
+            ts.setAtIndex(JAVA_LONG, i, lastTs);
+            cnt.setAtIndex(JAVA_INT, i, t.count);
+            flags.setAtIndex(JAVA_BYTE, i, t.flags);
+            if ((t.flags & EV_EXIT) != 0) {
+                anyExit = true;
+                boolean same = t.entry != null && t.entry.batchSeq == bs;
+                eref.setAtIndex(JAVA_LONG, i, same ? t.entry.batchIndex : -1L);
+                cts.setAtIndex(JAVA_LONG, i, t.createTs);
+            } else {
+                eref.setAtIndex(JAVA_LONG, i, -1L);
+                cts.setAtIndex(JAVA_LONG, i, 0L);
+            }
+            int na = t.args == null ? 0 : Math.min(t.args.length, ARG_SLOTS);
+            nArgs.setAtIndex(JAVA_BYTE, i, (byte) na);
+            for (int s = 0; s < ARG_SLOTS; s++) {
+                long k = (long) s * n + i;
+                Object v = s < na ? t.args[s] : null;
+                byte tag = ParamPacker.tag(v);
+                argTag.setAtIndex(JAVA_BYTE, k, tag);
+                argBits.setAtIndex(JAVA_LONG, k, tag == TAG_COLLECTION ? 0L : ParamPacker.bits(v));
+            }
+        }
+        // collection / array arguments: element CSR over (slot, event), slot-major
+        for (int s = 0; s < ARG_SLOTS; s++) {
+            for (int i = 0; i < n; i++) {
+                long k = (long) s * n + i;
+                Ticket t = b.get(i);
+                Object v = t.args != null && s < t.args.length ? t.args[s] : null;
+                if (v != null && ParamPacker.tag(v) == TAG_COLLECTION) {
+                    for (Object el : ParamPacker.elements(v)) {
+                        elemTag.setAtIndex(JAVA_BYTE, ne, ParamPacker.tag(el));
+                        elemBits.setAtIndex(JAVA_LONG, ne, ParamPacker.bits(el));
+                        ne++;
+                    }
+                }
+                elemOff.setAtIndex(JAVA_INT, k + 1, ne);
+            }
+        }
+        batch.set(JAVA_INT, 0, n); batch.set(JAVA_INT, 4, SF_MEM_HOST_);
+        long o = 8;
+        for (MemorySegment p : new MemorySegment[]{res, ts, cnt, flags}) { batch.set(ADDRESS, o, p); o += 8; }
+        batch.set(ADDRESS, o, anyExit ? eref : MemorySegment.NULL); o += 8;
+        batch.set(ADDRESS, o, anyExit ? cts : MemorySegment.NULL); o += 8;
+        batch.set(JAVA_INT, o, ARG_SLOTS); o += 8;
+        batch.set(ADDRESS, o, nArgs); o += 8;
+        batch.set(ADDRESS, o, argTag); o += 8;
+        batch.set(ADDRESS, o, argBits); o += 8;
+        batch.set(ADDRESS, o, ne > 0 ? elemOff : MemorySegment.NULL); o += 8;
+        batch.set(ADDRESS, o, elemTag); o += 8;
+        batch.set(ADDRESS, o, elemBits); o += 8;
+        batch.set(JAVA_INT, o, ne);
+        verdicts.set(JAVA_INT, 0, SF_MEM_HOST_);
+        verdicts.set(ADDRESS, 8, status); verdicts.set(ADDRESS, 16, waitMs); verdicts.set(ADDRESS, 24, ruleIdx);
+        check((int) SUBMIT.invokeExact(engine.handle, batch, verdicts));
+        for (int i = 0; i < n; i++) {
+            Ticket t = b.get(i);
+            t.waitMs = waitMs.getAtIndex(JAVA_INT, i);
+            t.ruleIdx = Short.toUnsignedInt(ruleIdx.getAtIndex(JAVA_SHORT, i));
+            t.status = status.getAtIndex(JAVA_BYTE, i);
+            LockSupport.unpark(t.caller);
+        }
+    }
+
+    private static final int SF_MEM_HOST_ = 0;
+}

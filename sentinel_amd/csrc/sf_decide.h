@@ -529,7 +529,9 @@ struct SegIO {          // sorted-order batch arrays
 SF_HD void emit_verdict(const SegIO& io, uint32_t j, uint8_t status, int32_t wait, uint16_t rule) {
     if (!io.perm) return;
     const uint32_t i = io.perm[j];
+#ifndef SF_EXP_NOSCATTER
     io.o_status[i] = status;
+#endif
     if (io.o_wait && wait) io.o_wait[i] = wait;          // (cleared before the decide phase)
     if (io.o_rule && rule) io.o_rule[i] = rule;
 }

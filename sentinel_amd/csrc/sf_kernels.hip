@@ -592,7 +592,9 @@ __global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, Heavy
         for (int k = 0; k < FG; k++) {
             const uint32_t j = base + (uint32_t)k;
             if (j < a || j >= b) continue;
+#ifndef SF_EXP_NOSCATTER
             io.o_status[pm[k]] = vs[k];
+#endif
             if (io.o_wait && vw[k]) io.o_wait[pm[k]] = vw[k];       // (cleared before the decide phase)
             if (io.o_rule && vr[k]) io.o_rule[pm[k]] = vr[k];
         }
