@@ -601,10 +601,28 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
     bool pm_exists = pm_init != 0;
     ParamTable pt{st.ptab, st.pcap_mask, st.err};
 
+    // The lane's events are read EV_CH at a time with all loads in flight together
+    // (each cache line of the sorted arrays is then fetched once, not once per
+    // event after the lines of the other lanes' segments evicted it), and picked
+    // out of registers by unrolled selects (no dynamic register indexing).
+#ifndef SF_EV_CH
+#define SF_EV_CH 8
+#endif
+    constexpr uint32_t EV_CH = SF_EV_CH;
+    int64_t t_[EV_CH]; int32_t c_[EV_CH]; uint8_t f_[EV_CH];
     for (uint32_t j = lo; j < hi; j++) {
-        const int64_t now = io.ts[j];
-        const int32_t c = io.cnt[j];
-        const uint8_t fl = io.flags[j];
+        const uint32_t k_ = (j - lo) % EV_CH;
+        if (k_ == 0) {
+#pragma unroll
+            for (uint32_t q = 0; q < EV_CH; q++) {
+                const uint32_t jj = j + q < hi ? j + q : hi - 1;
+                t_[q] = io.ts[jj]; c_[q] = io.cnt[jj]; f_[q] = io.flags[jj];
+            }
+        }
+        int64_t now = t_[0]; int32_t c = c_[0]; uint8_t fl = f_[0];
+#pragma unroll
+        for (uint32_t q = 1; q < EV_CH; q++)
+            if (k_ == q) { now = t_[q]; c = c_[q]; fl = f_[q]; }
         const uint32_t na = io.arg_slots ? (io.nargs ? io.nargs[j] : io.arg_slots) : 0;
         uint8_t status; int64_t wait = 0; int rule_idx = 0;
 
@@ -634,8 +652,6 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
                 status = SF_V_EXIT_IGNORED;
             }
             io.v_status[j] = status;
-            if (io.v_wait) io.v_wait[j] = 0;
-            if (io.v_rule) io.v_rule[j] = 0;
             emit_verdict(io, j, status, 0, 0);
             continue;
         }
@@ -689,9 +705,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
             }
             if (pm_exists) pm_thread_event(pt, res, pm_init, io, j, na, +1);
         }
-        io.v_status[j] = status;
-        if (io.v_wait) io.v_wait[j] = (int32_t)wait;
-        if (io.v_rule) io.v_rule[j] = (uint16_t)rule_idx;
+        io.v_status[j] = status;                             // (exits of this segment read it back)
         emit_verdict(io, j, status, (int32_t)wait, (uint16_t)rule_idx);
     }
 

@@ -118,12 +118,23 @@ constexpr uint32_t PV_DTS_FAR = 0xffffu;
 // light segments are listed by length class (len 1, 2, 3-4, 5-8, ...) so the
 // lanes of a wavefront interpret segments of similar length
 constexpr int LCLS = 16;
+// Light segments of at most SHORT_MAX events are decided in sorted (resource
+// id) order by k_decide_short, so a wavefront's lanes touch neighbouring rows
+// of every state array and neighbouring events; longer light segments go to
+// the length-class lists of k_decide_light.
+#ifndef SF_SHORT_MAX
+#define SF_SHORT_MAX 8
+#endif
+constexpr uint32_t SHORT_MAX = SF_SHORT_MAX;
 __host__ __device__ inline int light_class(uint32_t len) {
     if (len <= 1) return 0;
     const int c = 32 - __builtin_clz(len - 1);
     return c < LCLS - 1 ? c : LCLS - 1;
 }
-constexpr uint32_t FILL_TILE = 2048;             // events per k_heavy_fill tile (256 threads x 8)
+#ifndef SF_FILL_TILE
+#define SF_FILL_TILE 2048
+#endif
+constexpr uint32_t FILL_TILE = SF_FILL_TILE;             // events per k_heavy_fill tile (256 threads x 8)
 
 // Sorted-order working buffers of one batch.
 struct Work {

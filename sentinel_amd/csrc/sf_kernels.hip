@@ -178,12 +178,12 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     __shared__ uint32_t hcnt[LCLS], hbase[LCLS];
     if (threadIdx.x < LCLS) hcnt[threadIdx.x] = 0;
     __syncthreads();
-    const int lc = light ? light_class(hi - lo) : -1;
+    const int lc = (light && hi - lo > SHORT_MAX) ? light_class(hi - lo) : -1;
     const uint32_t lrank = lc >= 0 ? atomicAdd(&hcnt[lc], 1u) : 0u;
     __syncthreads();
     if (threadIdx.x < LCLS) hbase[threadIdx.x] = hcnt[threadIdx.x] ? atomicAdd(&w.lcounts[threadIdx.x], hcnt[threadIdx.x]) : 0u;
     __syncthreads();
-    if (light) { w.seg_mode[s] = SM_LIGHT; w.light_list[w.loff[lc] + hbase[lc] + lrank] = s; }
+    if (light) { w.seg_mode[s] = SM_LIGHT; if (lc >= 0) w.light_list[w.loff[lc] + hbase[lc] + lrank] = s; }
     const bool heavy = valid && !light;
     if (!__ballot(heavy)) return;
     uint8_t mode = SM_GENERIC;
@@ -253,6 +253,18 @@ __global__ void __launch_bounds__(128) k_decide_light(DevState st, SegIO io, con
     if (c < 0) return;
     const uint32_t s = ll.list[ll.off[c] + t];
     decide_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
+}
+
+// One lane per short light segment, in sorted order (see SHORT_MAX).
+template <int MAXS>
+__global__ void __launch_bounds__(128) k_decide_short(DevState st, SegIO io, const uint32_t* seg_start,
+                                                      const uint32_t* seg_res, const uint8_t* seg_mode,
+                                                      const uint32_t* n_seg) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= *n_seg || seg_mode[s] != SM_LIGHT) return;
+    const uint32_t lo = seg_start[s], hi = seg_start[s + 1];
+    if (hi - lo > SHORT_MAX) return;
+    decide_segment<MAXS>(st, io, seg_res[s], lo, hi);
 }
 
 static HeavyCtx heavy_ctx(const Work& w) {
@@ -477,7 +489,10 @@ __device__ __forceinline__ void store16(void* dst, const void* src, int bytes) {
     for (int k = 0; k < bytes / 16; k++) d[k] = q[k];
 }
 
-__global__ void __launch_bounds__(256) k_heavy_fill(DevState st, SegIO io, HeavyCtx hc, const uint2* tiles,
+#ifndef SF_FILL_MINB
+#define SF_FILL_MINB 1
+#endif
+__global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, SegIO io, HeavyCtx hc, const uint2* tiles,
                                                     const uint32_t* ntiles, int cls) {
     __shared__ PAccSlot lds_h[4], lds_s[4];
     const uint32_t NONE = 0xffffffffu;
@@ -803,12 +818,17 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     const unsigned TD = 128;
     LightLists ll{w.light_list, w.lcounts, {}};
     for (int c = 0; c < LCLS; c++) ll.off[c] = w.loff[c];
-    if (st.S <= 2)
+    if (st.S <= 2) {
         hipLaunchKernelGGL(k_decide_light<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
                            w.seg_res, ll);
-    else
+        hipLaunchKernelGGL(k_decide_short<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+                           w.seg_res, w.seg_mode, w.n_seg);
+    } else {
         hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, ll);
+        hipLaunchKernelGGL(k_decide_short<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
+                           w.seg_start, w.seg_res, w.seg_mode, w.n_seg);
+    }
     hipEventRecord(ev[9], s3);                     // light done (also the join of C)
     hipEventRecord(ev[6], s2);                     // join B and C
     hipStreamWaitEvent(s, ev[6], 0);

@@ -142,6 +142,11 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
              in->entry_ref ? cts.data() : nullptr, in->arg_slots, in->n_args ? nargs.data() : nullptr,
              atag.data(), abits.data(), n, in->arg_elem_off, in->elem_tag, in->elem_bits,
              vs.data(), vw.data(), vr.data()};
+    // light / generic segments emit their verdicts through the identity permutation
+    // into the sorted-order arrays (the final loop below scatters them)
+    std::vector<uint32_t> ident(n);
+    std::iota(ident.begin(), ident.end(), 0u);
+    io.perm = ident.data(); io.o_status = vs.data(); io.o_wait = vw.data(); io.o_rule = vr.data();
     // segments + routing (k_segments / k_classify)
     std::vector<uint32_t> seg_start, seg_res, segflag;
     for (uint32_t j = 0; j < n; j++) {
