@@ -201,7 +201,7 @@ static int alloc_work(sf_engine* e, Work& w) {
     WALLOC(w.keys_in, N * 4); WALLOC(w.keys_out, N * 4); WALLOC(w.perm, N * 4);
     WALLOC(w.pv_in, N * sizeof(PackedEv)); WALLOC(w.pv_out, N * sizeof(PackedEv));
     WALLOC(w.wide, 4); WALLOC(w.err, 4);
-    WALLOC(w.head, N * 4); WALLOC(w.head_scan, N * 4);
+    WALLOC(w.head_scan, N * 4);
     WALLOC(w.seg_start, (N + 1) * 4); WALLOC(w.seg_res, N * 4); WALLOC(w.n_seg, 4);
     WALLOC(w.s_ts, N * 8); WALLOC(w.s_cnt, N * 4); WALLOC(w.s_flags, N);
     WALLOC(w.s_eref, N * 8); WALLOC(w.s_cts, N * 8);

@@ -70,12 +70,17 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t
     pv[i] = v;
 }
 
-__global__ void k_unpack(DevBatch b, const PackedEv* pv, uint32_t* perm, int64_t* s_ts,
+// Also the segment table (segment id of sorted event j = inclusive count of
+// segment heads up to j, minus one): start, resource and the segment count.
+__global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* keys, uint32_t* perm, int64_t* s_ts,
                          int32_t* s_cnt, uint8_t* s_flags, uint8_t* s_nargs, uint8_t* s_atag,
-                         uint64_t* s_abits, const uint32_t* head, const uint32_t* head_scan, uint32_t* segflag,
-                         int64_t* last_ts, const int32_t* err) {
+                         uint64_t* s_abits, const uint32_t* head_scan, uint32_t* seg_start, uint32_t* seg_res,
+                         uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts, const int32_t* err) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
+    const uint32_t sid = head_scan[j] - 1;
+    if (j == 0 || head_scan[j - 1] != head_scan[j]) { seg_start[sid] = j; seg_res[sid] = keys[j]; }
+    if (j == b.n - 1) { *n_seg = sid + 1; seg_start[sid + 1] = b.n; }
     if (j == 0 && *err == 0) *last_ts = b.ts[b.n - 1];   // k_keys_packed of this batch has read the old value
     const PackedEv v = pv[j];
     const uint32_t i = v.idx;
@@ -85,8 +90,7 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, uint32_t* perm, int64_t
     perm[j] = i;
     s_ts[j] = dts != PV_DTS_FAR ? b.ts[0] + (int64_t)dts : b.ts[i]; s_cnt[j] = c; s_flags[j] = f;
     if (!(f & SF_EV_EXIT) && ((f & (SF_EV_PRIO | EVF_SYSBLK)) || c <= 0)) {
-        uint32_t s = head_scan[j] + head[j] - 1;
-        atomicOr(&segflag[s], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) |
+        atomicOr(&segflag[sid], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) |
                               ((f & EVF_SYSBLK) ? SEGF_SYS : 0u));
     }
     if (b.arg_slots) {
@@ -101,26 +105,17 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, uint32_t* perm, int64_t
     }
 }
 
-__global__ void k_heads(const uint32_t* keys, uint32_t n, uint32_t* head) {
-    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    head[j] = (j == 0 || keys[j] != keys[j - 1]) ? 1u : 0u;
-}
-
-__global__ void k_segments(const uint32_t* keys, const uint32_t* head, const uint32_t* pos, uint32_t n,
-                           uint32_t* seg_start, uint32_t* seg_res, uint32_t* n_seg, uint32_t* segflag) {
-    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    if (head[j]) { seg_start[pos[j]] = j; seg_res[pos[j]] = keys[j]; segflag[pos[j]] = 0; }
-    if (j == n - 1) { uint32_t ns = pos[j] + head[j]; *n_seg = ns; seg_start[ns] = n; }
-}
+struct HeadFlag {       // 1 where a new resource segment starts in the sorted keys
+    const uint32_t* keys;
+    __device__ uint32_t operator()(uint32_t j) const { return (j == 0 || keys[j] != keys[j - 1]) ? 1u : 0u; }
+};
 
 // Exits only: the sorted position of each exit's entry.  The sort is stable
 // and the segment holds one resource's events in submission order, so the
 // entry is found by a binary search of the segment's submission indices (no
 // inverse permutation scattered over the whole batch).  Forward map exit_of
 // for THREAD-grade liveness; s_cts for entries of earlier batches.
-__global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint8_t* s_flags, const uint32_t* head,
+__global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint8_t* s_flags,
                               const uint32_t* head_scan, const uint32_t* seg_start, int64_t* s_eref,
                               int64_t* s_cts, uint32_t* exit_of, int32_t* err) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -139,7 +134,7 @@ __global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint8_t* s
         s_cts[j] = b.ts[r];
         return;
     }
-    uint32_t a = seg_start[head_scan[j] + head[j] - 1], e = j;          // entry in [segment start, j)
+    uint32_t a = seg_start[head_scan[j] - 1], e = j;          // entry in [segment start, j)
     if (r >= (int64_t)i) { *err = SF_ERR_INVALID; s_eref[j] = -1; s_cts[j] = 0; return; }
     while (a < e) { const uint32_t m = (a + e) >> 1; if ((int64_t)perm[m] < r) a = m + 1; else e = m; }
     if (a >= j || (int64_t)perm[a] != r) { *err = SF_ERR_INVALID; s_eref[j] = -1; s_cts[j] = 0; return; }
@@ -241,7 +236,10 @@ struct LightLists { const uint32_t* list; const uint32_t* counts; uint32_t off[L
 // longest down, so a wavefront holds segments of one class (similar length)
 // and the long ones are dispatched first.
 template <int MAXS>
-__global__ void __launch_bounds__(128) k_decide_light(DevState st, SegIO io, const uint32_t* seg_start,
+#ifndef SF_LIGHT_MINB
+#define SF_LIGHT_MINB 1
+#endif
+__global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_light(DevState st, SegIO io, const uint32_t* seg_start,
                                                       const uint32_t* seg_res, LightLists ll) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     int c = LCLS - 1;
@@ -257,7 +255,7 @@ __global__ void __launch_bounds__(128) k_decide_light(DevState st, SegIO io, con
 
 // One lane per short light segment, in sorted order (see SHORT_MAX).
 template <int MAXS>
-__global__ void __launch_bounds__(128) k_decide_short(DevState st, SegIO io, const uint32_t* seg_start,
+__global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_short(DevState st, SegIO io, const uint32_t* seg_start,
                                                       const uint32_t* seg_res, const uint8_t* seg_mode,
                                                       const uint32_t* n_seg) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -472,6 +470,43 @@ __global__ void __launch_bounds__(256) k_thr_prep(const uint8_t* flags, const in
 // are in flight together.  Each event is one pass-bit lookup (its entry's bit
 // for an exit).  Persistent grid, each workgroup a contiguous run of tiles; a
 // thread's partial sums carry across the run while the window row repeats.
+// Window rows of a run of tiles accumulated in LDS: ACC_K consecutive
+// accumulator slots from `base`, 64-bit LDS atomics; flushed to the global
+// rows (one set of atomics per touched slot) only when a tile's window range
+// leaves the table or the workgroup's run ends, so the rows of a hot
+// resource take one flush per window, not one per thread or tile.
+constexpr int ACC_K = 32;
+struct LdsAcc {
+    unsigned long long v[8][ACC_K];                 // pass, block, succ, rt, exc, n_pass, n_exit, n_touch
+    long long min_rt[ACC_K];
+};
+__device__ __forceinline__ void lds_acc_clear(LdsAcc& A) {
+    for (int i = threadIdx.x; i < 8 * ACC_K; i += blockDim.x) A.v[i / ACC_K][i % ACC_K] = 0ull;
+    for (int i = threadIdx.x; i < ACC_K; i += blockDim.x) A.min_rt[i] = INT64_MAX;
+}
+__device__ __forceinline__ void lds_acc_add(LdsAcc& A, uint32_t k, const PAcc& p) {
+    if (!p.n_touch) return;
+    if (p.pass) atomicAdd(&A.v[0][k], p.pass);
+    if (p.block) atomicAdd(&A.v[1][k], p.block);
+    if (p.succ) atomicAdd(&A.v[2][k], p.succ);
+    if (p.rt) atomicAdd(&A.v[3][k], p.rt);
+    if (p.exc) atomicAdd(&A.v[4][k], p.exc);
+    if (p.n_pass) atomicAdd(&A.v[5][k], p.n_pass);
+    if (p.n_exit) atomicAdd(&A.v[6][k], p.n_exit);
+    atomicAdd(&A.v[7][k], p.n_touch);
+    if (p.min_rt != INT64_MAX) atomicMin(&A.min_rt[k], p.min_rt);
+}
+// flush slots to table[base + k] (thread k), then clear; callers bracket with barriers
+__device__ __forceinline__ void lds_acc_flush(LdsAcc& A, Acc* table, uint32_t base) {
+    const int k = (int)threadIdx.x;
+    if (k < ACC_K && A.v[7][k]) {
+        PAcc p;
+        p.pass = A.v[0][k]; p.block = A.v[1][k]; p.succ = A.v[2][k]; p.rt = A.v[3][k]; p.exc = A.v[4][k];
+        p.n_pass = A.v[5][k]; p.n_exit = A.v[6][k]; p.n_touch = A.v[7][k]; p.min_rt = A.min_rt[k];
+        p.flush(table, base + (uint32_t)k);
+    }
+}
+
 constexpr int FG = (int)FILL_TILE / 256;         // events per lane
 struct FillGrp { uint8_t f[FG]; int32_t c[FG]; int64_t t[FG]; };
 
@@ -494,14 +529,15 @@ __device__ __forceinline__ void store16(void* dst, const void* src, int bytes) {
 #endif
 __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, SegIO io, HeavyCtx hc, const uint2* tiles,
                                                     const uint32_t* ntiles, int cls) {
-    __shared__ PAccSlot lds_h[4], lds_s[4];
+    __shared__ LdsAcc acc_h, acc_s;
     const uint32_t NONE = 0xffffffffu;
     const uint32_t nt = ntiles[cls];
     const uint32_t wl = (uint32_t)st.wl;
     const uint32_t tb = (uint32_t)((uint64_t)nt * blockIdx.x / gridDim.x);
     const uint32_t te = (uint32_t)((uint64_t)nt * (blockIdx.x + 1) / gridDim.x);
-    PAcc ph, ps; ph.clear(); ps.clear();
-    uint32_t kh = NONE, ks = NONE;
+    lds_acc_clear(acc_h); lds_acc_clear(acc_s);
+    uint32_t bh_k = NONE, bs_k = NONE;                // LDS table bases (workgroup-uniform)
+    __syncthreads();
     for (uint32_t t = tb; t < te; t++) {
         const uint2 tl = tiles[t];
         const uint32_t s = tl.x;
@@ -512,6 +548,23 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
         const int64_t hw0 = hc.seg_hw0[s], sec0 = hc.seg_sec0[s];
         const int64_t bh = hw0 * st.wl, bs = sec0 * 1000;
         const bool rel32 = io.ts[hi - 1] - bs < (int64_t)0xffffffffLL;   // window keys by 32-bit division
+        auto key_of = [&](int64_t tj, uint32_t& kh_, uint32_t& ks_) {
+            if (rel32) { kh_ = hwb + (uint32_t)(tj - bh) / wl; ks_ = secb + (uint32_t)(tj - bs) / 1000u; }
+            else { kh_ = hwb + (uint32_t)(tj / st.wl - hw0); ks_ = secb + (uint32_t)(tj / 1000 - sec0); }
+        };
+        // the tile's window rows; a range that leaves the LDS tables flushes them first
+        uint32_t th0, ts0, th1, ts1;
+        key_of(io.ts[max(tl.y * FILL_TILE, lo)], th0, ts0);
+        key_of(io.ts[min(tl.y * FILL_TILE + FILL_TILE, hi) - 1], th1, ts1);
+        const bool wide = th1 - th0 >= (uint32_t)ACC_K || ts1 - ts0 >= (uint32_t)ACC_K;
+        if (wide || bh_k == NONE || th0 < bh_k || th1 >= bh_k + ACC_K || ts0 < bs_k || ts1 >= bs_k + ACC_K) {
+            __syncthreads();
+            if (bh_k != NONE) { lds_acc_flush(acc_h, hc.acc_hw, bh_k); lds_acc_flush(acc_s, hc.acc_sec, bs_k); }
+            __syncthreads();
+            lds_acc_clear(acc_h); lds_acc_clear(acc_s);
+            bh_k = wide ? NONE : th0; bs_k = wide ? NONE : ts0;
+            __syncthreads();
+        }
         const uint32_t base = tl.y * FILL_TILE + (uint32_t)FG * threadIdx.x;
         const uint32_t a = max(base, lo), b = min(base + (uint32_t)FG, hi);
         if (a >= b) continue;
@@ -613,12 +666,11 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
             if (io.o_wait && vw[k]) io.o_wait[pm[k]] = vw[k];       // (cleared before the decide phase)
             if (io.o_rule && vr[k]) io.o_rule[pm[k]] = vr[k];
         }
+#ifdef SF_EXP_NOACC
+        continue;
+#endif
         if (!gp.n_touch) continue;
         // window rows of the group's first and last event (time-sorted): usually one
-        auto key_of = [&](int64_t tj, uint32_t& kh_, uint32_t& ks_) {
-            if (rel32) { kh_ = hwb + (uint32_t)(tj - bh) / wl; ks_ = secb + (uint32_t)(tj - bs) / 1000u; }
-            else { kh_ = hwb + (uint32_t)(tj / st.wl - hw0); ks_ = secb + (uint32_t)(tj / 1000 - sec0); }
-        };
         int64_t tfirst = 0, tlast = 0;                    // unrolled selects (no dynamic register indexing)
 #pragma unroll
         for (int k = 0; k < FG; k++) {
@@ -629,10 +681,16 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
         key_of(tfirst, h0, s0);
         key_of(tlast, h1, s1);
         if (h0 == h1 && s0 == s1) {
-            if (h0 != kh) { if (kh != NONE) ph.flush(hc.acc_hw, kh); ph.clear(); kh = h0; }
-            if (s0 != ks) { if (ks != NONE) ps.flush(hc.acc_sec, ks); ps.clear(); ks = s0; }
-            ph.merge(gp); ps.merge(gp);
+            if (bh_k != NONE) { lds_acc_add(acc_h, h0 - bh_k, gp); lds_acc_add(acc_s, s0 - bs_k, gp); }
+            else { gp.flush(hc.acc_hw, h0); gp.flush(hc.acc_sec, s0); }
         } else {
+            PAcc ph, ps; ph.clear(); ps.clear();
+            uint32_t kh = NONE, ks = NONE;
+            auto out = [&](PAcc& p, uint32_t key, bool sec) {
+                if (key == NONE) return;
+                if (bh_k != NONE) lds_acc_add(sec ? acc_s : acc_h, key - (sec ? bs_k : bh_k), p);
+                else p.flush(sec ? hc.acc_sec : hc.acc_hw, key);
+            };
 #pragma unroll
             for (int k = 0; k < FG; k++) {
                 const uint32_t j = base + (uint32_t)k;
@@ -647,14 +705,15 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
                 if (!e.touch) continue;
                 uint32_t kh_, ks_;
                 key_of(g.t[k], kh_, ks_);
-                if (kh_ != kh) { if (kh != NONE) ph.flush(hc.acc_hw, kh); ph.clear(); kh = kh_; }
-                if (ks_ != ks) { if (ks != NONE) ps.flush(hc.acc_sec, ks); ps.clear(); ks = ks_; }
+                if (kh_ != kh) { out(ph, kh, false); ph.clear(); kh = kh_; }
+                if (ks_ != ks) { out(ps, ks, true); ps.clear(); ks = ks_; }
                 ph.add(e); ps.add(e);
             }
+            out(ph, kh, false); out(ps, ks, true);
         }
     }
-    block_flush(ph, kh, hc.acc_hw, lds_h);
-    block_flush(ps, ks, hc.acc_sec, lds_s);
+    __syncthreads();
+    if (bh_k != NONE) { lds_acc_flush(acc_h, hc.acc_hw, bh_k); lds_acc_flush(acc_s, hc.acc_sec, bs_k); }
 }
 
 __global__ void k_heavy_apply(DevState st, HeavyCtx hc, StreamCtx sc, const uint32_t* seg_nhw,
@@ -694,6 +753,7 @@ hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipSt
 static inline unsigned blocks(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 using PcIter = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, EntryCount, int64_t>;
+using HeadIter = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, HeadFlag, uint32_t>;
 
 hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes,
                             size_t* pscan_bytes) {
@@ -705,8 +765,9 @@ hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_byte
                                   (PackedEv*)nullptr, (PackedEv*)nullptr, max_n, 0u, key_bits);
     if (e != hipSuccess) return e;
     if (packed_bytes > *sort_bytes) *sort_bytes = packed_bytes;
-    e = rocprim::exclusive_scan(nullptr, *scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
-                                (size_t)max_n, rocprim::plus<uint32_t>());
+    HeadIter hit(rocprim::counting_iterator<uint32_t>(0), HeadFlag{nullptr});
+    e = rocprim::inclusive_scan(nullptr, *scan_bytes, hit, (uint32_t*)nullptr, (size_t)max_n,
+                                rocprim::plus<uint32_t>());
     if (e != hipSuccess) return e;
     PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{nullptr, nullptr});
     return rocprim::inclusive_scan(nullptr, *pscan_bytes, it, (int64_t*)nullptr, (size_t)max_n,
@@ -740,18 +801,20 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.pv_in, w.pv_out, n, 0u,
                                   key_bits, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_heads, dim3(blocks(n, T)), dim3(T), 0, s, w.keys_out, n, w.head);
-    e = rocprim::exclusive_scan(w.scan_tmp, w.scan_tmp_bytes, w.head, w.head_scan, 0u, (size_t)n,
-                                rocprim::plus<uint32_t>(), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_segments, dim3(blocks(n, T)), dim3(T), 0, s, w.keys_out, w.head, w.head_scan, n,
-                       w.seg_start, w.seg_res, w.n_seg, w.segflag);
+    {
+        HeadIter hit(rocprim::counting_iterator<uint32_t>(0), HeadFlag{w.keys_out});
+        e = rocprim::inclusive_scan(w.scan_tmp, w.scan_tmp_bytes, hit, w.head_scan, (size_t)n,
+                                    rocprim::plus<uint32_t>(), s);
+        if (e != hipSuccess) return e;
+    }
+    hipMemsetAsync(w.segflag, 0, (size_t)(n < st.R ? n : st.R) * 4, s);
     if (timing) hipEventRecord(ev[1], s);
-    hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.perm, w.s_ts, w.s_cnt,
-                       w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head, w.head_scan, w.segflag, st.last_ts, st.err);
+    hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.keys_out, w.perm, w.s_ts, w.s_cnt,
+                       w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan, w.seg_start, w.seg_res, w.n_seg,
+                       w.segflag, st.last_ts, st.err);
     hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
     if (b.eref)
-        hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags, w.head,
+        hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags,
                            w.head_scan, w.seg_start, w.s_eref, w.s_cts, w.exit_of, st.err);
     PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
     e = rocprim::inclusive_scan(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n, rocprim::plus<int64_t>(), s);
