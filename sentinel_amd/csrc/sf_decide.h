@@ -109,6 +109,20 @@ struct NodeWin {
     int32_t S, wl, interval;
     int64_t max_rt;
     double interval_sec;
+    // last window looked up: events come in time order, so most lookups hit
+    // it and skip the 64-bit division by the runtime window length
+    int64_t c_ws = INT64_MIN; int32_t c_idx = 0;
+
+    // window start and slot of time t (t - t % wl, (t / wl) % S), cached
+    SF_HD int64_t win_of(int64_t t, int& idx) {
+        if (!(t >= c_ws && t < c_ws + (int64_t)wl)) {
+            const int64_t q = t / wl;
+            c_ws = t - (t - q * wl);
+            c_idx = (int)(q % S);
+        }
+        idx = c_idx;
+        return c_ws;
+    }
 
     template <class F> SF_HD void visit(int idx, F f) {
         if constexpr (MAXS == 1) { f(sec[0]); }
@@ -124,15 +138,16 @@ struct NodeWin {
     // ---- FutureBucketLeapArray (borrowArray) ----
     // getWindowValue(t) -> pass of the bucket containing t, or -1 when null (LeapArray.java:268-281)
     SF_HD int64_t borrow_value(int64_t t) {
-        int idx = (int)((t / wl) % S);
+        int idx;
+        win_of(t, idx);
         int64_t v = -1;
         visit_bor(idx, [&](Borrow& b) { if (b.ws <= t && t < b.ws + wl) v = b.pass; });
         return v;
     }
     // currentWindow(t): returns idx, or -1 for a throwaway window
     SF_HD int borrow_current(int64_t t) {
-        int idx = (int)((t / wl) % S);
-        int64_t ws = t - t % wl;
+        int idx;
+        const int64_t ws = win_of(t, idx);
         int r = idx;
         visit_bor(idx, [&](Borrow& b) {
             if (b.ws == ws) return;
@@ -158,8 +173,8 @@ struct NodeWin {
     // ---- OccupiableBucketLeapArray main window ----
     // currentWindow(t): returns idx or -1 (throwaway window, LeapArray.java:220-223)
     SF_HD int sec_current(int64_t t) {
-        int idx = (int)((t / wl) % S);
-        int64_t ws = t - t % wl;
+        int idx;
+        const int64_t ws = win_of(t, idx);
         int r = idx;
         bool reset = false;
         visit(idx, [&](Bucket& b) {
@@ -209,7 +224,8 @@ struct NodeWin {
         return m > 1 ? m : 1;
     }
     SF_HD int64_t sec_window_pass(int64_t t) {            // ArrayMetric.getWindowPass :324-330
-        int idx = (int)((t / wl) % S);
+        int idx;
+        win_of(t, idx);
         int64_t v = 0;
         visit(idx, [&](Bucket& b) { if (b.ws <= t && t < b.ws + wl) v = b.pass; });
         return v;
