@@ -112,6 +112,7 @@ struct NodeWin {
     // last window looked up: events come in time order, so most lookups hit
     // it and skip the 64-bit division by the runtime window length
     int64_t c_ws = INT64_MIN; int32_t c_idx = 0;
+    int32_t bdirty = 0;                        // a borrow bucket changed (written back only then)
 
     // window start and slot of time t (t - t % wl, (t / wl) % S), cached
     SF_HD int64_t win_of(int64_t t, int& idx) {
@@ -151,7 +152,7 @@ struct NodeWin {
         int r = idx;
         visit_bor(idx, [&](Borrow& b) {
             if (b.ws == ws) return;
-            if (ws > b.ws) { b.ws = ws; b.pass = 0; return; }          // FutureBucketLeapArray.resetWindowTo :41-46
+            if (ws > b.ws) { b.ws = ws; b.pass = 0; bdirty = 1; return; }   // FutureBucketLeapArray.resetWindowTo :41-46
             r = -1;
         });
         return r;
@@ -168,6 +169,7 @@ struct NodeWin {
         int i = borrow_current(t);
         if (i < 0) return;                                               // throwaway window
         visit_bor(i, [&](Borrow& b) { b.pass = wadd(b.pass, c); });
+        bdirty = 1;
     }
 
     // ---- OccupiableBucketLeapArray main window ----
@@ -725,12 +727,15 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
         emit_verdict(io, j, status, (int32_t)wait, (uint16_t)rule_idx);
     }
 
-    // write back
+    // write back (borrow and the first rule's controller state only when they can have changed)
     for (int i = 0; i < MAXS; i++)
-        if (i < st.S) { st.second[(size_t)res * st.S + i] = nd.sec[i]; st.borrow[(size_t)res * st.S + i] = nd.bor[i]; }
+        if (i < st.S) {
+            st.second[(size_t)res * st.S + i] = nd.sec[i];
+            if (nd.bdirty) st.borrow[(size_t)res * st.S + i] = nd.bor[i];
+        }
     nd.min_flush();
     st.threads[res] = nd.threads;
-    if (nrules) st.rstate[r0] = rs0;
+    if (nrules && st.rules[r0].kind != CT_DEFAULT) st.rstate[r0] = rs0;   // DefaultController keeps no state
     if (nprules) st.pm_init[res] = pm_init;
 }
 
