@@ -27,8 +27,9 @@
 namespace sf {
 
 // segment modes (seg_mode[s])
-enum : uint8_t { SM_LIGHT = 0, SM_GENERIC = 1, SM_QPS = 2, SM_WARM = 3, SM_RL = 4, SM_NORULE = 5, SM_THREAD = 6 };
-constexpr uint32_t SEGF_PRIO = 1u, SEGF_NONPOS = 2u, SEGF_SYS = 4u;
+enum : uint8_t { SM_LIGHT = 0, SM_GENERIC = 1, SM_QPS = 2, SM_WARM = 3, SM_RL = 4, SM_NORULE = 5, SM_THREAD = 6,
+                 SM_PARAM = 7 };
+constexpr uint32_t SEGF_PRIO = 1u, SEGF_NONPOS = 2u, SEGF_SYS = 4u, SEGF_EXIT = 8u, SEGF_COLL = 16u;
 
 struct Acc {            // per (segment, window) counter deltas
     unsigned long long pass, block, succ, rt, exc, n_pass, n_exit, n_touch;
@@ -49,7 +50,22 @@ SF_HD uint8_t heavy_mode(const DevState& st, uint32_t res, uint32_t segflags, in
         if (st.borrow[(size_t)res * st.S + i].ws >= ws_first) return SM_GENERIC;
     const uint32_t nr = st.rule_off[res + 1] - st.rule_off[res];
     const uint32_t np = st.prule_off[res + 1] - st.prule_off[res];
-    if (np != 0 || (segflags & (SEGF_NONPOS | SEGF_SYS)) || st.interval != 1000) return SM_GENERIC;
+    if ((segflags & (SEGF_NONPOS | SEGF_SYS)) || st.interval != 1000) return SM_GENERIC;
+    if (np != 0) {
+        // ParamFlow-only resources whose decisions are independent per parameter
+        // value (QPS-grade rules on one argument index, no exits, no collection
+        // arguments): k_heavy_decide's wavefront path by value (heavy_param)
+        if (st.rule_off[res + 1] != st.rule_off[res] || (segflags & (SEGF_EXIT | SEGF_COLL))) return SM_GENERIC;
+        const uint32_t p0 = st.prule_off[res];
+        const int32_t idx = st.prules[p0].param_idx;
+        if (idx < 0 || idx >= 8 || (st.pm_init[res] & ~(1u << idx))) return SM_GENERIC;
+        for (uint32_t k = p0; k < p0 + np; k++) {
+            const DevParamRule& pr = st.prules[k];
+            if (pr.param_idx != idx || pr.grade != SF_GRADE_QPS ||
+                (pr.behavior != SF_BEHAVIOR_DEFAULT && pr.behavior != SF_BEHAVIOR_RATE_LIMITER)) return SM_GENERIC;
+        }
+        return SM_PARAM;
+    }
     if (nr == 0) return SM_NORULE;
     if (nr != 1 || (segflags & SEGF_PRIO)) return SM_GENERIC;
     const DevRule& r = st.rules[st.rule_off[res]];

@@ -89,6 +89,12 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* keys, u
     const uint8_t f = (uint8_t)(v.meta >> 16);
     perm[j] = i;
     s_ts[j] = dts != PV_DTS_FAR ? b.ts[0] + (int64_t)dts : b.ts[i]; s_cnt[j] = c; s_flags[j] = f;
+    {   // the segment has exits: one atomic per run of exits within a wavefront
+        const bool ex = (f & SF_EV_EXIT) != 0;
+        const int lane = (int)(threadIdx.x & 63);
+        const int pex = __shfl_up((int)ex, 1), psid = __shfl_up((int)sid, 1);
+        if (ex && !(lane > 0 && pex && (uint32_t)psid == sid)) atomicOr(&segflag[sid], SEGF_EXIT);
+    }
     if (!(f & SF_EV_EXIT) && ((f & (SF_EV_PRIO | EVF_SYSBLK)) || c <= 0)) {
         atomicOr(&segflag[sid], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) |
                               ((f & EVF_SYSBLK) ? SEGF_SYS : 0u));
@@ -98,6 +104,7 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* keys, u
         for (uint32_t a = 0; a < b.arg_slots; a++) {
             const uint8_t tg = b.atag[(size_t)a * b.arg_stride + i];
             s_atag[(size_t)a * b.n + j] = tg;
+            if (tg == SF_TAG_COLLECTION) atomicOr(&segflag[sid], SEGF_COLL);
             // a collection argument carries its index into the batch's element CSR
             s_abits[(size_t)a * b.n + j] = tg == SF_TAG_COLLECTION ? (uint64_t)a * b.arg_stride + (uint64_t)b.base + i
                                                                   : b.abits[(size_t)a * b.arg_stride + i];
@@ -280,6 +287,75 @@ static HeavyCtx heavy_ctx(const Work& w) {
     return hc;
 }
 
+// SM_PARAM: a ParamFlow-only resource whose rules are QPS-grade on one
+// argument index (heavy_mode).  ParamFlowChecker's state is per (rule, value)
+// (ParameterMetric token / time maps) and the node counters are only summed,
+// so events of different values are independent: the wavefront takes 64
+// events at a time and runs them in rounds, round r holding every lane whose
+// value occurred r times before in the 64 (an event sees its value's state
+// after all earlier events of that value).  Lanes of one round only touch
+// different keys; the table's finds all complete before any insert of the
+// round (lock-step).  Verdict inputs go to the pass bits, v_wait (throttled
+// passes) and v_rule (the blocking rule); k_heavy_fill and k_heavy_apply
+// then do the StatisticSlot accounting as for the other window modes.
+__device__ void heavy_param(const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t res, uint32_t lo,
+                            uint32_t hi) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t p0 = st.prule_off[res], np = st.prule_off[res + 1] - p0;
+    const int32_t pidx = st.prules[p0].param_idx;
+    const uint8_t pm_init = (uint8_t)(st.pm_init[res] | (1u << pidx));   // initParamMetricsFor on the first entry
+    ParamTable pt{st.ptab, st.pcap_mask, st.err};
+    for (uint32_t q = lo; q < hi; q += 64) {
+        const uint32_t j = q + (uint32_t)lane;
+        const bool valid = j < hi;
+        const uint32_t jc = valid ? j : hi - 1;
+        const int64_t now = io.ts[jc];
+        const int32_t c = io.cnt[jc];
+        const uint32_t na = io.arg_slots ? (io.nargs ? io.nargs[jc] : io.arg_slots) : 0;
+        uint32_t tag = SF_TAG_NULL; uint64_t bits = 0;
+        if ((int32_t)na > pidx) { tag = io.atag[(size_t)pidx * io.n + jc]; bits = io.abits[(size_t)pidx * io.n + jc]; }
+        const bool key = valid && tag != SF_TAG_NULL;      // a null value skips every rule (passCheck :53-60)
+        // rank of this event among the earlier events of its value in the 64
+        unsigned long long pend = __ballot(key);
+        int rank = 0, maxr = 0;
+        while (pend) {
+            const int l = __ffsll((long long)pend) - 1;
+            const uint32_t kt = (uint32_t)__builtin_amdgcn_readlane((int)tag, l);
+            const uint64_t kb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits >> 32), l) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, l);
+            const unsigned long long same = __ballot(key && tag == kt && bits == kb);
+            if ((same >> lane) & 1ull) rank = __popcll(same & ((1ull << lane) - 1ull));
+            maxr = max(maxr, __popcll(same) - 1);
+            pend &= ~same;
+        }
+        bool blocked = false;
+        int64_t wait = 0;
+        int rule = 0;
+        for (int r = 0; r <= maxr; r++) {
+            if (valid && rank == r) {
+                if (key) {
+                    for (uint32_t k = 0; k < np; k++) {
+                        int64_t w = 0;
+                        if (!param_pass_value(pt, res, (int)k, st.prules[p0 + k], st.items, now, c, tag, bits, io, &w)) {
+                            blocked = true; rule = (int)k; break;
+                        }
+                        if (w > 0) wait += w;
+                    }
+                }
+                if (!blocked) pm_thread_event(pt, res, pm_init, io, j, na, +1);   // ParamFlowStatisticEntryCallback
+            }
+        }
+        const unsigned long long pm = __ballot(valid && !blocked);
+        if (lane == 0 && pm) {
+            const uint32_t sh = q & 63;
+            atomicOr(hc.passbits + (q >> 6), pm << sh);
+            if (sh) atomicOr(hc.passbits + (q >> 6) + 1, pm >> (64 - sh));
+        }
+        if (valid) { io.v_wait[j] = blocked ? 0 : (int32_t)wait; io.v_rule[j] = (uint16_t)rule; }
+    }
+    if (lane == 0) st.pm_init[res] = pm_init;
+}
+
 // One wavefront per heavy QPS / WarmUp / no-rule / generic segment (64-thread
 // workgroups: the team needs no barriers).  THREAD and RateLimiter segments
 // run in k_heavy_stream (sf_stream.h).
@@ -294,6 +370,7 @@ __global__ void __launch_bounds__(64) k_heavy_decide(DevState st, SegIO io, Heav
     case SM_QPS: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, false); break;
     case SM_WARM: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, true); break;
     case SM_NORULE: break;                          // every entry passes (k_heavy_fill)
+    case SM_PARAM: heavy_param(st, io, hc, res, lo, hi); break;
     default:
         if (tm.leader()) decide_segment<MAXS>(st, io, res, lo, hi);
         break;
@@ -543,7 +620,7 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
         const uint32_t s = tl.x;
         const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1];
         const uint8_t mode = hc.seg_mode[s];
-        const bool all = mode == SM_NORULE, rl = mode == SM_RL;
+        const bool all = mode == SM_NORULE, rl = mode == SM_RL, prm = mode == SM_PARAM;
         const uint32_t hwb = hc.acc_hw_base[s], secb = hc.acc_sec_base[s];
         const int64_t hw0 = hc.seg_hw0[s], sec0 = hc.seg_sec0[s];
         const int64_t bh = hw0 * st.wl, bs = sec0 * 1000;
@@ -573,7 +650,7 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
         int32_t wt[FG];
         if (full) {
             load16(g.f, io.flags + base, FG); load16(g.c, io.cnt + base, FG * 4); load16(g.t, io.ts + base, FG * 8);
-            if (rl) load16(wt, io.v_wait + base, FG * 4);
+            if (rl || prm) load16(wt, io.v_wait + base, FG * 4);
         } else {
 #pragma unroll
             for (int k = 0; k < FG; k++) {
@@ -582,7 +659,7 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
                 g.f[k] = in ? io.flags[j] : (uint8_t)0;
                 g.c[k] = in ? io.cnt[j] : 0;
                 g.t[k] = in ? io.ts[j] : 0;
-                wt[k] = (in && rl) ? io.v_wait[j] : 0;
+                wt[k] = (in && (rl || prm)) ? io.v_wait[j] : 0;
             }
         }
         const unsigned long long pw = hc.passbits[base >> 6];
@@ -636,8 +713,9 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
             e.c = g.c[k];
             if (!(g.f[k] & SF_EV_EXIT)) {
                 e.passed = (bits >> k) & 1u;
-                e.wait = (rl && e.passed) ? wt[k] : 0;
-                e.status = e.passed ? (e.wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : SF_V_BLOCK_FLOW;
+                e.wait = ((rl || prm) && e.passed) ? wt[k] : 0;
+                e.status = e.passed ? (e.wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : (prm ? SF_V_BLOCK_PARAM : SF_V_BLOCK_FLOW);
+                if (prm && !e.passed) vr[k] = io.v_rule[j];
                 e.touch = true;
             } else {
                 e.live_exit = (rlive >> k) & 1u;

@@ -165,6 +165,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         if (hi - lo <= e->heavy_min) { mode[s] = SM_LIGHT; continue; }
         e->n_heavy_segments++;
         mode[s] = heavy_mode(e->st, seg_res[s], segflag[s], ts[lo]);
+        if (mode[s] == SM_PARAM) mode[s] = SM_GENERIC;          // (the wavefront param path is GPU-only)
         e->mode_count[mode[s] & 7]++;
         if (mode[s] != SM_GENERIC) {
             e->n_heavy_item_segments++;
