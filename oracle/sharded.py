@@ -1,0 +1,83 @@
+"""TEST INFRASTRUCTURE / CPU BASELINE ONLY -- the C oracle replayed on several
+host cores: the batch is split by resource (res % T, local id res // T, the
+engine's own shard map), each shard replays on its own OracleEngine in its own
+thread (the ctypes call releases the GIL), and the verdicts are merged back
+into batch order.  Without SystemRules (node-wide ENTRY_NODE) the shards are
+independent, so the merged verdicts equal one replay of the whole batch
+(SURVEY.md §6 / BASELINE.md: the multi-core CPU baseline, resource-sharded).
+Used by bench.py's cpu_baseline leg and tests/test_oracle_sharded.py."""
+import threading
+
+import numpy as np
+
+from sentinel_amd import abi
+
+
+def split(hb: abi.HostBatch, T: int):
+    """Per-shard HostBatch (local resource ids, entry refs remapped) and the
+    batch positions of each shard's events."""
+    res = hb.res_id.astype(np.int64)
+    shard = (res % T).astype(np.uint8 if T <= 255 else np.int32)   # uint8: numpy sorts it by radix
+    order = np.argsort(shard, kind="stable")
+    counts = np.bincount(shard, minlength=T)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    pos = np.empty(hb.n, np.int64)                          # batch index -> index inside its shard
+    for k in range(T):
+        idx = order[starts[k]:starts[k + 1]]
+        pos[idx] = np.arange(idx.size)
+    out = []
+    for k in range(T):
+        idx = order[starts[k]:starts[k + 1]]
+        eref = None
+        if hb.entry_ref is not None:
+            r = hb.entry_ref[idx]
+            eref = np.where(r >= 0, pos[np.clip(r, 0, None)], r).astype(np.int64)
+        b = abi.HostBatch((res[idx] // T).astype(np.uint32), hb.ts_ms[idx], hb.count[idx], hb.flags[idx],
+                          entry_ref=eref, create_ts=None if hb.create_ts is None else hb.create_ts[idx])
+        out.append((idx, b))
+    return out
+
+
+def shard_rules(rules, T: int, k: int):
+    """Flow rules of shard k with local resource ids (list order kept)."""
+    out = []
+    for r in rules:
+        if r.resource % T == k:
+            c = abi.sf_flow_rule.from_buffer_copy(r)
+            c.resource = r.resource // T
+            out.append(c)
+    return out
+
+
+def replay(rules, hb: abi.HostBatch, R: int, T: int):
+    """Replays hb on T threads; returns (verdicts in batch order, seconds of
+    the parallel replay, excluding the split and the rule loads)."""
+    from oracle import oracle as so
+    parts = split(hb, T)
+    engines = []
+    for k in range(T):
+        e = so.OracleEngine(abi.default_config(max_resources=R // T + 1, max_batch=max(1, parts[k][1].n)))
+        e.load_flow_rules(shard_rules(rules, T, k))
+        engines.append(e)
+    outs = [None] * T
+
+    def run(k):
+        outs[k] = engines[k].submit(parts[k][1])
+
+    import time
+    ths = [threading.Thread(target=run, args=(k,)) for k in range(T)]
+    t = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t
+    for e in engines:
+        e.close()
+    v = abi.HostVerdicts(hb.n)
+    for k in range(T):
+        idx = parts[k][0]
+        v.status[idx] = outs[k].status
+        v.wait_ms[idx] = outs[k].wait_ms
+        v.rule_idx[idx] = outs[k].rule_idx
+    return v, dt

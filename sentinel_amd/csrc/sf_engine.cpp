@@ -1510,7 +1510,9 @@ int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uin
     if (nh) {
         HIP_TRY(hipMemcpy(full.data(), lw.heavy_list, (size_t)lw.seg_cap * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(full2.data(), lw.stream_list, (size_t)lw.seg_cap * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(ticks.data(), lw.hticks, n1 * 8, hipMemcpyDeviceToHost));
+        // per-block clocks exist for the first grid-size entries only (grid-stride beyond)
+        const size_t hcap = (size_t)e->cfg.max_batch / (lw.heavy_min + 1) + 2;
+        HIP_TRY(hipMemcpy(ticks.data(), lw.hticks, std::min<size_t>(n1, hcap) * 8, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(ticks2.data(), lw.sticks, n2 * 8, hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < nh; i++) {
             if (i < n1) {

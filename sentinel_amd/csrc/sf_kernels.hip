@@ -174,7 +174,12 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     const bool valid = s < *w.n_seg;
     uint32_t lo = 0, hi = 0, res = 0;
     if (valid) { lo = w.seg_start[s]; hi = w.seg_start[s + 1]; res = w.seg_res[s]; }
-    const bool light = valid && hi - lo <= w.heavy_min;
+    bool light = valid && hi - lo <= w.heavy_min;
+    // a ParamFlow-only segment of more than 32 events is faster on the
+    // wavefront-by-value path (SM_PARAM) than as one lane's serial table walk
+    if (light && hi - lo > 32 && st.prule_off[res + 1] != st.prule_off[res] &&
+        heavy_mode(st, res, w.segflag[s], s_ts[lo]) == SM_PARAM)
+        light = false;
     // light list slot: workgroup histogram of the length classes in LDS, one
     // global atomic per class and workgroup
     __shared__ uint32_t hcnt[LCLS], hbase[LCLS];
@@ -361,21 +366,24 @@ __device__ void heavy_param(const DevState& st, const SegIO& io, const HeavyCtx&
 // run in k_heavy_stream (sf_stream.h).
 template <int MAXS>
 __global__ void __launch_bounds__(64) k_heavy_decide(DevState st, SegIO io, HeavyCtx hc) {
+    // grid-stride over the list (medium ParamFlow segments can outnumber the
+    // grid sized for segments above heavy_min); long segments are listed first
     uint32_t s;
-    if (!heavy_at(hc, blockIdx.x, &s)) return;
-    const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1], res = hc.seg_res[s];
-    Team tm{(int)threadIdx.x};
-    const uint64_t t_start = hc.hticks ? wall_clock64() : 0;
-    switch (hc.seg_mode[s]) {
-    case SM_QPS: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, false); break;
-    case SM_WARM: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, true); break;
-    case SM_NORULE: break;                          // every entry passes (k_heavy_fill)
-    case SM_PARAM: heavy_param(st, io, hc, res, lo, hi); break;
-    default:
-        if (tm.leader()) decide_segment<MAXS>(st, io, res, lo, hi);
-        break;
+    for (uint32_t b = blockIdx.x; heavy_at(hc, b, &s); b += gridDim.x) {
+        const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1], res = hc.seg_res[s];
+        Team tm{(int)threadIdx.x};
+        const uint64_t t_start = hc.hticks ? wall_clock64() : 0;
+        switch (hc.seg_mode[s]) {
+        case SM_QPS: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, false); break;
+        case SM_WARM: heavy_qps<MAXS>(tm, st, io, hc, s, res, lo, hi, true); break;
+        case SM_NORULE: break;                      // every entry passes (k_heavy_fill)
+        case SM_PARAM: heavy_param(st, io, hc, res, lo, hi); break;
+        default:
+            if (tm.leader()) decide_segment<MAXS>(st, io, res, lo, hi);
+            break;
+        }
+        if (hc.hticks && tm.leader() && b < gridDim.x) hc.hticks[b] = wall_clock64() - t_start;
     }
-    if (hc.hticks && tm.leader()) hc.hticks[blockIdx.x] = wall_clock64() - t_start;
 }
 
 struct PAcc {            // per-thread partial of one accumulator slot
@@ -796,11 +804,12 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
 
 __global__ void k_heavy_apply(DevState st, HeavyCtx hc, StreamCtx sc, const uint32_t* seg_nhw,
                               const uint32_t* seg_nsec, int cls) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, s;
-    if (cls == 0) { if (!heavy_at(hc, t, &s)) return; }
-    else if (!stream_at(sc, t, &s)) return;
-    if (hc.seg_mode[s] < SM_QPS) return;
-    heavy_apply(st, hc, s, hc.seg_res[s], seg_nhw[s], seg_nsec[s]);
+    uint32_t s;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;; t += gridDim.x * blockDim.x) {
+        if (cls == 0) { if (!heavy_at(hc, t, &s)) return; }
+        else if (!stream_at(sc, t, &s)) return;
+        if (hc.seg_mode[s] >= SM_QPS) heavy_apply(st, hc, s, hc.seg_res[s], seg_nhw[s], seg_nsec[s]);
+    }
 }
 
 // occupancy and longest probe distance of the exact param table (diagnostics)
