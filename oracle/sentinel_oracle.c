@@ -30,7 +30,7 @@
 /* ======================================================================
  * Mocked clock — CORE/util/TimeUtil.java:222-224 (mockStatic in tests)
  * ==================================================================== */
-static int64_t g_now = 0;
+static _Thread_local int64_t g_now = 0;  /* per thread: oracle/sharded.py replays shards on threads */
 static int64_t g_stat_max_rt = 5000;   /* CORE/config/SentinelConfig.java:69,247 */
 
 void so_set_time(int64_t t) { g_now = t; }
