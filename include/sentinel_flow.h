@@ -363,6 +363,32 @@ int  sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
  * timing mode fall back to sf_submit. */
 int  sf_submit_async(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
 
+/* SystemRules on a resource-sharded node (shard_count > 1).
+ * SystemRuleManager.checkSystem (SystemRuleManager.java:291-348) reads the
+ * node-wide ENTRY_NODE, which every earlier IN event of every resource (every
+ * shard) updates, so a sharded engine with SystemRules refuses sf_submit and
+ * is driven by rounds instead (sentinel_amd/system_shard.py does it over
+ * torch.distributed):
+ *   1. the ranks all-gather the IN events of the batch (global submission
+ *      order; an exit's entry_ref indexes this merged stream, -1 for an entry
+ *      of an earlier batch) -- every rank holds the same merged stream;
+ *   2. sf_system_plan(merged, verdicts of merged[0, p), p) -> q and the forced
+ *      SystemBlockException of every IN entry of merged[p, q) (SYS_NONE = 0xFF
+ *      for none; else 0 qps, 1 thread, 2 rt, 3 load, 4 cpu), identical on every
+ *      rank (same inputs, same ENTRY_NODE);
+ *   3. each rank decides its own events before merged[q] in global order with
+ *      sf_submit_forced (sys_mask per event; an exit whose entry lay in an
+ *      earlier sub-batch carries entry_ref -1 and its create_ts when the entry
+ *      passed, -2 when it was blocked);
+ *   4. the ranks combine the verdicts of merged[p, q) (each event is decided by
+ *      exactly one rank) and every rank adds them to its ENTRY_NODE with
+ *      sf_entry_node_add; p = q.
+ * Host arrays; calls of one batch use increasing p. */
+int  sf_system_plan(sf_engine* e, const sf_event_batch* in_events, const uint8_t* status, uint32_t p,
+                    uint32_t* q, uint8_t* sys_mask);
+int  sf_submit_forced(sf_engine* e, const sf_event_batch* in, sf_verdicts* out, const uint8_t* sys_mask);
+int  sf_entry_node_add(sf_engine* e, const sf_event_batch* in_events, const uint8_t* status);
+
 /* Cluster token server (DefaultTokenService). */
 int  sf_load_namespaces(sf_engine* e, const sf_namespace* ns, uint32_t n);
 int  sf_load_cluster_rules(sf_engine* e, const sf_cluster_flow_rule* flow, uint32_t n_flow,

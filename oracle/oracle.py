@@ -143,6 +143,9 @@ def _declare(L):
     f("so_submit", C.c_int, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
     f("so_read_node", C.c_int, P, U32, C.POINTER(abi.sf_node_state))
     f("so_read_entry_node", C.c_int, P, C.POINTER(abi.sf_node_state))
+    f("so_system_plan", C.c_int, P, C.POINTER(abi.sf_event_batch), P, U32, C.POINTER(U32), P)
+    f("so_submit_forced", C.c_int, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts), P)
+    f("so_entry_node_add", C.c_int, P, C.POINTER(abi.sf_event_batch), P)
     f("so_read_rule_state", C.c_int, P, U32, C.POINTER(abi.sf_rule_state))
     f("so_read_param", C.c_int, P, U32, U8, U64, C.POINTER(I64), C.POINTER(I64), C.POINTER(C.c_int))
     f("so_param_thread", I64, P, U32, C.c_int, U8, U64)
@@ -486,6 +489,27 @@ class OracleEngine:
         rc = lib().so_submit(self.h, C.byref(b), C.byref(v))
         assert rc == 0, rc
         return out
+
+    # node-wide SystemRule rounds (sentinel_amd/system_shard.py), one IN event per round
+    def system_plan(self, merged: abi.HostBatch, status, p: int, sys_mask) -> int:
+        b = merged.c_struct()
+        q = U32(0)
+        rc = lib().so_system_plan(self.h, C.byref(b), None, p, C.byref(q), sys_mask.ctypes.data)
+        assert rc == 0, rc
+        return int(q.value)
+
+    def submit_forced(self, batch: abi.HostBatch, sys_mask) -> abi.HostVerdicts:
+        m = np.ascontiguousarray(sys_mask, np.uint8)
+        out = abi.HostVerdicts(batch.n)
+        b, v = batch.c_struct(), out.c_struct()
+        rc = lib().so_submit_forced(self.h, C.byref(b), C.byref(v), m.ctypes.data)
+        assert rc == 0, rc
+        return out
+
+    def entry_node_add(self, batch: abi.HostBatch, status):
+        st = np.ascontiguousarray(status, np.uint8)
+        b = batch.c_struct()
+        assert lib().so_entry_node_add(self.h, C.byref(b), st.ctypes.data) == 0
 
     def read_node(self, res):
         st = abi.sf_node_state()

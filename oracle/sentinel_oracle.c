@@ -1060,6 +1060,7 @@ struct so_engine {
     so_node* entry_node;              /* Constants.ENTRY_NODE (Constants.java:66) */
     /* entries of the batch being replayed */
     uint8_t* entry_blocked; uint32_t cap_entries;
+    const uint8_t* forced;            /* so_submit_forced: planned SystemRule verdicts, ENTRY_NODE untouched */
     /* cluster */
     cluster_rt* cl; uint32_t n_cl;
     sf_hot_item* cl_items; uint32_t n_cl_items;
@@ -1256,6 +1257,7 @@ static void pm_thread_event(so_param_metric* pm, const sf_event_batch* in, uint3
 }
 
 int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
+    so_node* const en = e->forced ? NULL : e->entry_node;      /* the node-wide rounds update it themselves */
     apply_statics(&e->cfg);
     if (in->mem != SF_MEM_HOST || out->mem != SF_MEM_HOST) return SF_ERR_INVALID;
     if (in->n > e->cap_entries) {
@@ -1283,7 +1285,7 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
                 blocked = e->entry_blocked[ref];
                 create_ts = in->ts_ms[ref];
             } else {
-                blocked = 0;
+                blocked = ref == -2;                            /* the entry was blocked in an earlier batch */
                 create_ts = in->create_ts ? in->create_ts[i] : g_now;
             }
             if (!blocked) {
@@ -1294,10 +1296,10 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
                 so_node_add_rt_and_success(rr->node, rt, count);
                 so_node_decrease_thread_num(rr->node);
                 if (err) so_node_increase_exception_qps(rr->node, count);
-                if (is_in) {
-                    so_node_add_rt_and_success(e->entry_node, rt, count);
-                    so_node_decrease_thread_num(e->entry_node);
-                    if (err) so_node_increase_exception_qps(e->entry_node, count);
+                if (is_in && en) {
+                    so_node_add_rt_and_success(en, rt, count);
+                    so_node_decrease_thread_num(en);
+                    if (err) so_node_increase_exception_qps(en, count);
                 }
                 /* ParamFlowStatisticExitCallback.onExit -> decreaseThreadCount(args) */
                 if (rr->pm) pm_thread_event(rr->pm, in, i, na, 0);
@@ -1318,7 +1320,7 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
 
         /* SystemSlot -> SystemRuleManager.checkSystem */
         if (is_in) {
-            int reason = check_system(e, count);
+            int reason = e->forced ? (e->forced[i] == 0xFF ? -1 : (int)e->forced[i]) : check_system(e, count);
             if (reason >= 0) { blocked = 1; status = SF_V_BLOCK_SYSTEM; rule_idx = reason; }
         }
         /* ParamFlowSlot.checkFlow :82-103 (args never null from SphU.entry) */
@@ -1359,16 +1361,16 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         /* StatisticSlot.entry accounting :64-123 */
         if (blocked) {
             so_node_increase_block_qps(rr->node, count);
-            if (is_in) so_node_increase_block_qps(e->entry_node, count);
+            if (is_in && en) so_node_increase_block_qps(en, count);
         } else if (prio_wait) {
             so_node_increase_thread_num(rr->node);
-            if (is_in) so_node_increase_thread_num(e->entry_node);
+            if (is_in && en) so_node_increase_thread_num(en);
             if (rr->pm) pm_thread_event(rr->pm, in, i, na, 1);
             status = SF_V_PRIORITY_WAIT;
         } else {
             so_node_increase_thread_num(rr->node);
             so_node_add_pass_request(rr->node, count);
-            if (is_in) { so_node_increase_thread_num(e->entry_node); so_node_add_pass_request(e->entry_node, count); }
+            if (is_in && en) { so_node_increase_thread_num(en); so_node_add_pass_request(en, count); }
             if (rr->pm) pm_thread_event(rr->pm, in, i, na, 1);
             status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS;
         }
@@ -1376,6 +1378,59 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         out->status[i] = status;
         if (out->wait_ms) out->wait_ms[i] = (int32_t)wait;
         if (out->rule_idx) out->rule_idx[i] = (uint16_t)rule_idx;
+    }
+    return SF_OK;
+}
+
+/* The node-wide SystemRule rounds of a sharded node (include/sentinel_flow.h:
+ * sf_system_plan / sf_submit_forced / sf_entry_node_add), restated one IN event
+ * per round: the plan of merged[p] is checkSystem on the ENTRY_NODE as every
+ * earlier IN event of the node left it (SystemRuleManager.checkSystem
+ * :291-348; StatisticSlot.java:64-165 the updates). */
+int so_system_plan(so_engine* e, const sf_event_batch* in, const uint8_t* status, uint32_t p, uint32_t* q,
+                   uint8_t* sys_mask) {
+    (void)status;
+    if (p >= in->n) return SF_ERR_INVALID;
+    apply_statics(&e->cfg);
+    g_now = in->ts_ms[p];
+    const uint8_t f = in->flags[p];
+    int reason = -1;
+    if ((f & SF_EV_IN) && !(f & SF_EV_EXIT)) reason = check_system(e, in->count[p]);
+    sys_mask[p] = reason < 0 ? 0xFF : (uint8_t)reason;
+    *q = p + 1;
+    return SF_OK;
+}
+
+int so_submit_forced(so_engine* e, const sf_event_batch* in, sf_verdicts* out, const uint8_t* sys_mask) {
+    e->forced = sys_mask;
+    const int rc = so_submit(e, in, out);
+    e->forced = NULL;
+    return rc;
+}
+
+int so_entry_node_add(so_engine* e, const sf_event_batch* in, const uint8_t* status) {
+    apply_statics(&e->cfg);
+    so_node* en = e->entry_node;
+    for (uint32_t i = 0; i < in->n; i++) {
+        const uint8_t f = in->flags[i], v = status[i];
+        if (!(f & SF_EV_IN)) continue;
+        g_now = in->ts_ms[i];
+        const int32_t c = in->count[i];
+        if (f & SF_EV_EXIT) {
+            if (v != SF_V_EXIT) continue;
+            const int64_t ref = in->entry_ref ? in->entry_ref[i] : -1;
+            const int64_t cts = ref >= 0 ? in->ts_ms[ref] : (in->create_ts ? in->create_ts[i] : g_now);
+            so_node_add_rt_and_success(en, g_now - cts, c);
+            so_node_decrease_thread_num(en);
+            if (f & SF_EV_ERROR) so_node_increase_exception_qps(en, c);
+        } else if (v == SF_V_PASS || v == SF_V_PASS_WAIT) {
+            so_node_increase_thread_num(en);
+            so_node_add_pass_request(en, c);
+        } else if (v == SF_V_PRIORITY_WAIT) {
+            so_node_increase_thread_num(en);
+        } else {
+            so_node_increase_block_qps(en, c);
+        }
     }
     return SF_OK;
 }

@@ -190,6 +190,10 @@ int  so_load_param_rules(so_engine* e, const sf_param_rule* rules, uint32_t n,
 int  so_load_system_rules(so_engine* e, const sf_system_rule* rules, uint32_t n);
 int  so_set_system_status(so_engine* e, double load, double cpu);
 int  so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out);
+int  so_system_plan(so_engine* e, const sf_event_batch* in, const uint8_t* status, uint32_t p, uint32_t* q,
+                    uint8_t* sys_mask);
+int  so_submit_forced(so_engine* e, const sf_event_batch* in, sf_verdicts* out, const uint8_t* sys_mask);
+int  so_entry_node_add(so_engine* e, const sf_event_batch* in, const uint8_t* status);
 int  so_read_node(so_engine* e, uint32_t res, sf_node_state* out);
 int  so_read_entry_node(so_engine* e, sf_node_state* out);
 int  so_read_rule_state(so_engine* e, uint32_t rule_index, sf_rule_state* out);

@@ -59,6 +59,7 @@ struct sf_engine {
     // staging for host-memory batches
     void* stage_in = nullptr; size_t stage_in_bytes = 0;
     void* stage_out = nullptr; size_t stage_out_bytes = 0;
+    void* plan_stage = nullptr; size_t plan_stage_bytes = 0;   // sf_system_plan / sf_entry_node_add inputs
     hipEvent_t evs[2][SF_NUM_EVENTS]{};   // per Work set: fork/join and timing events of its batch
     bool timed[2] = {false, false};       // that batch ran with timing on and is not yet in stats
     bool timing = false;
@@ -157,7 +158,7 @@ void sf_destroy(sf_engine* e) {
     for (Work& w : e->w) free_work(w);
     void* ptrs[] = {e->st.second, e->st.borrow, e->st.minute, e->st.threads, (void*)e->st.rule_off,
                     (void*)e->st.rules, e->st.rstate, (void*)e->st.prule_off, e->st.prules, (void*)e->st.items,
-                    e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out};
+                    e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out, e->plan_stage};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
@@ -493,8 +494,6 @@ int sf_load_system_rules(sf_engine* e, const sf_system_rule* rules, uint32_t n) 
     if (!e || (n && !rules)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     { const int rc = drain(e); if (rc) return rc; }
-    if (n && e->cfg.shard_count > 1)
-        return fail(SF_ERR_UNSUPPORTED, "SystemRule reads the node-wide ENTRY_NODE: not on a sharded engine");
     SysRule r{};
     r.qps = r.highest_load = r.highest_cpu = 1.7976931348623157e308;
     r.max_rt = r.max_thread = INT64_MAX;
@@ -524,7 +523,8 @@ int sf_set_system_status(sf_engine* e, double avg_load, double cpu_usage) {
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out, bool async) {
+static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out, bool async,
+                       const uint8_t* forced = nullptr) {
     if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
     if (in->n == 0) return SF_OK;
     if (!in->res_id || !in->ts_ms || !in->count || !in->flags) return fail(SF_ERR_INVALID, "missing event array");
@@ -533,12 +533,17 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         return fail(SF_ERR_INVALID, "bad arg arrays");
     if (in->arg_elem_off && in->n_elems && (!in->elem_tag || !in->elem_bits))
         return fail(SF_ERR_INVALID, "collection arguments without element arrays");
+    // SystemRules read the node-wide ENTRY_NODE: a sharded engine decides them
+    // only through the round protocol (sf_system_plan / sf_submit_forced)
+    if (e->sys.check && e->cfg.shard_count > 1 && !forced)
+        return fail(SF_ERR_UNSUPPORTED, "SystemRules on a sharded engine: use sf_system_plan + sf_submit_forced "
+                                        "+ sf_entry_node_add (the node-wide round protocol)");
     const uint32_t n = in->n;
     DevBatch b{};
     b.n = n; b.arg_slots = in->arg_slots;
     hipStream_t s = e->stream, ss = e->serial ? e->stream : e->sstream;
     // asynchronous only for HBM-resident batches and verdicts, without SystemRules
-    async = async && in->mem != SF_MEM_HOST && out->mem != SF_MEM_HOST && !e->sys.check;
+    async = async && in->mem != SF_MEM_HOST && out->mem != SF_MEM_HOST && !e->sys.check && !forced;
     if (!async) { const int rc = drain(e); if (rc) return rc; }
     if (async && !e->w_ready[1]) {                 // second Work set on first asynchronous use
         HIP_TRY(hipStreamSynchronize(s));
@@ -618,7 +623,13 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         dv.status = out->status; dv.wait = out->wait_ms; dv.rule = out->rule_idx;
     }
     b.arg_stride = n;
-    if (e->sys.check) {
+    if (forced) {
+        // the forced SystemRule verdicts of this (sub-)batch, planned node-wide
+        if (!e->sys_mask) HIP_TRY(hipMalloc((void**)&e->sys_mask, e->cfg.max_batch));
+        HIP_TRY(hipMemcpyAsync(e->sys_mask, forced, n, hipMemcpyHostToDevice, e->serial ? e->stream : e->sstream));
+        b.sys = e->sys_mask;
+    }
+    if (e->sys.check && !forced) {
         // SystemRules couple every IN entry to the global ENTRY_NODE: the batch
         // is decided as a sequence of safe sub-batches (sf_system.h), each
         // planned on the exact ENTRY_NODE, then sorted / decided / reduced by
@@ -691,9 +702,12 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
     le = launch_decide(stl, w, b, dv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3, e->evs[slot], e->timing);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
-    // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream order)
-    le = launch_entry_node(stl, b, dv.status, e->en, e->en_acc, s);
-    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
+    // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream
+    // order); under the round protocol the node-wide stream updates it (sf_entry_node_add)
+    if (!forced) {
+        le = launch_entry_node(stl, b, dv.status, e->en, e->en_acc, s);
+        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
+    }
     HIP_TRY(hipEventRecord(e->ev_done[slot], s));
     e->used[slot] = true;
     e->timed[slot] = e->timing;
@@ -732,6 +746,104 @@ int sf_submit_async(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     if (!e) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     return submit_core(e, in, out, true);
+}
+
+// ---------------------------------------------------------------- node-wide SystemRule rounds
+// (sentinel_flow.h: sf_system_plan / sf_submit_forced / sf_entry_node_add)
+int sf_submit_forced(sf_engine* e, const sf_event_batch* in, sf_verdicts* out, const uint8_t* sys_mask) {
+    if (!e || !in || !out || !sys_mask) return fail(SF_ERR_INVALID, "null argument");
+    if (in->mem != SF_MEM_HOST) return fail(SF_ERR_INVALID, "sf_submit_forced takes host arrays");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return submit_core(e, in, out, false, sys_mask);
+}
+
+// stage host IN-event arrays (ts, count, flags, entry_ref, create_ts) + optional
+// verdicts at a device scratch; DevBatch over them
+static int stage_in_events(sf_engine* e, const sf_event_batch* in, const uint8_t* status, uint32_t n_status,
+                           DevBatch& b, uint8_t** dstatus) {
+    const uint32_t n = in->n;
+    size_t need = 0;
+    const size_t o_ts = need; need += align_up((size_t)n * 8);
+    const size_t o_cnt = need; need += align_up((size_t)n * 4);
+    const size_t o_fl = need; need += align_up((size_t)n);
+    const size_t o_er = need; need += align_up((size_t)n * 8);
+    const size_t o_ct = need; need += align_up((size_t)n * 8);
+    const size_t o_st = need; need += align_up((size_t)n + 1);
+    if (need > e->plan_stage_bytes) {
+        if (e->plan_stage) hipFree(e->plan_stage);
+        e->plan_stage = nullptr; e->plan_stage_bytes = 0;
+        HIP_TRY(hipMalloc(&e->plan_stage, need));
+        e->plan_stage_bytes = need;
+    }
+    char* base = (char*)e->plan_stage;
+    hipStream_t s = e->stream;
+    HIP_TRY(hipMemcpyAsync(base + o_ts, in->ts_ms, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(base + o_cnt, in->count, (size_t)n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(base + o_fl, in->flags, n, hipMemcpyHostToDevice, s));
+    if (in->entry_ref) HIP_TRY(hipMemcpyAsync(base + o_er, in->entry_ref, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    if (in->create_ts) HIP_TRY(hipMemcpyAsync(base + o_ct, in->create_ts, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    if (status && n_status) HIP_TRY(hipMemcpyAsync(base + o_st, status, n_status, hipMemcpyHostToDevice, s));
+    b = DevBatch{};
+    b.n = n;
+    b.ts = (const int64_t*)(base + o_ts); b.cnt = (const int32_t*)(base + o_cnt); b.flags = (const uint8_t*)(base + o_fl);
+    b.eref = in->entry_ref ? (const int64_t*)(base + o_er) : nullptr;
+    b.cts = in->create_ts ? (const int64_t*)(base + o_ct) : nullptr;
+    *dstatus = (uint8_t*)(base + o_st);
+    return SF_OK;
+}
+
+int sf_system_plan(sf_engine* e, const sf_event_batch* in, const uint8_t* status, uint32_t p, uint32_t* q,
+                   uint8_t* sys_mask) {
+    if (!e || !in || !q || !sys_mask || (p && !status)) return fail(SF_ERR_INVALID, "null argument");
+    if (in->mem != SF_MEM_HOST || !in->ts_ms || !in->count || !in->flags)
+        return fail(SF_ERR_INVALID, "sf_system_plan takes the node's IN events in host arrays");
+    if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
+    if (p >= in->n) return fail(SF_ERR_INVALID, "plan position past the batch");
+    std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }
+    const uint32_t n = in->n;
+    if (!e->sys.check) {                                   // no SystemRule: nothing is forced
+        std::memset(sys_mask + p, SYS_NONE, n - p);
+        *q = n;
+        return SF_OK;
+    }
+    if (!e->sys_plan) {
+        HIP_TRY(hipMalloc((void**)&e->sys_plan, sizeof(SysPlanDev)));
+        HIP_TRY(hipMalloc((void**)&e->sys_pa, SYS_PLAN_BLOCKS * sizeof(SysExitQ)));
+        HIP_TRY(hipMalloc((void**)&e->sys_pb, SYS_PLAN_BLOCKS * sizeof(SysEntQ)));
+        HIP_TRY(hipMalloc((void**)&e->sys_mask, e->cfg.max_batch));
+    }
+    DevBatch b;
+    uint8_t* dstatus = nullptr;
+    { const int rc = stage_in_events(e, in, status, p, b, &dstatus); if (rc) return rc; }
+    hipStream_t s = e->stream;
+    DevState stl = e->st;
+    hipError_t le = sys_plan(stl, b, dstatus, e->sys_mask, e->sys, e->en, p, e->sys_plan, e->sys_pa, e->sys_pb, s);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("system plan: ") + hipGetErrorString(le));
+    uint32_t qq = 0;
+    HIP_TRY(hipMemcpyAsync(&qq, &e->sys_plan->q, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (qq <= p || qq > n) return fail(SF_ERR_DEVICE, "system planner made no progress");
+    HIP_TRY(hipMemcpy(sys_mask + p, e->sys_mask + p, qq - p, hipMemcpyDeviceToHost));
+    *q = qq;
+    return SF_OK;
+}
+
+int sf_entry_node_add(sf_engine* e, const sf_event_batch* in, const uint8_t* status) {
+    if (!e || !in || !status) return fail(SF_ERR_INVALID, "null argument");
+    if (in->mem != SF_MEM_HOST || !in->ts_ms || !in->count || !in->flags)
+        return fail(SF_ERR_INVALID, "sf_entry_node_add takes host arrays");
+    if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
+    std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }
+    if (!in->n) return SF_OK;
+    DevBatch b;
+    uint8_t* dstatus = nullptr;
+    { const int rc = stage_in_events(e, in, status, in->n, b, &dstatus); if (rc) return rc; }
+    hipError_t le = launch_entry_node(e->st, b, dstatus, e->en, e->en_acc, e->stream);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return SF_OK;
 }
 
 static void to_abi_bucket(const Bucket& d, sf_bucket* o) {

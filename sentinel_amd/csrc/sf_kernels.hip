@@ -129,7 +129,9 @@ __global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint8_t* s
     if (j >= b.n || !(s_flags[j] & SF_EV_EXIT)) return;
     const uint32_t i = perm[j];
     const int64_t raw = b.eref[i];
-    if (raw < 0) { s_eref[j] = -1; s_cts[j] = b.cts ? b.cts[i] : 0; return; }
+    // -1: the entry passed before this batch (live, create_ts gives its time);
+    // EREF_DEAD: it was blocked before this batch (the exit is ignored)
+    if (raw < 0) { s_eref[j] = raw == EREF_DEAD ? EREF_DEAD : -1; s_cts[j] = b.cts ? b.cts[i] : 0; return; }
     const int64_t r = raw - b.base;                                      // view-local index
     if (r < 0) {
         // the entry was decided in an earlier sub-batch of this batch: live
@@ -167,6 +169,9 @@ __device__ uint32_t wave_append(uint32_t* counter, bool take) {
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
+#ifndef SF_MED_MIN
+#define SF_MED_MIN 64
+#endif
 // Route each segment: light lane interpreter, heavy window algorithms, or the
 // heavy generic interpreter (one lane of a wavefront).
 __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
@@ -180,6 +185,12 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     if (light && hi - lo > 32 && st.prule_off[res + 1] != st.prule_off[res] &&
         heavy_mode(st, res, w.segflag[s], s_ts[lo]) == SM_PARAM)
         light = false;
+    // likewise a QPS / WarmUp / no-rule segment of more than SF_MED_MIN events:
+    // the window algorithms of k_heavy_decide + the tiled fill beat a lane's walk
+    if (light && hi - lo > SF_MED_MIN) {
+        const uint8_t m = heavy_mode(st, res, w.segflag[s], s_ts[lo]);
+        if (m == SM_QPS || m == SM_WARM || m == SM_NORULE) light = false;
+    }
     // light list slot: workgroup histogram of the length classes in LDS, one
     // global atomic per class and workgroup
     __shared__ uint32_t hcnt[LCLS], hbase[LCLS];

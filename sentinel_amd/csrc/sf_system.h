@@ -187,6 +187,7 @@ SF_HD SysExitQ sys_exit_q(const int64_t* ts, const int32_t* cnt, const uint8_t* 
     }
     const int64_t ref = eref ? eref[i] : -1;
     const int64_t t = ts[i];
+    if (ref == EREF_DEAD) return q;                      // the entry was blocked earlier: nothing recorded
     if (ref < 0) {                                       // entry passed in an earlier batch
         const int64_t rt = t - (cts ? cts[i] : t);
         q.xc = 1; q.xc_c = c; q.xc_rt = rt; q.xc_min = rt;

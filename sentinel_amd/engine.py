@@ -95,6 +95,9 @@ def _declare(L):
     f("sf_param_table_stats", I, P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(U32))
     f("sf_token_shard", I, C.POINTER(abi.sf_cluster_flow_rule), U32, C.POINTER(abi.sf_cluster_param_rule), U32,
       C.POINTER(abi.sf_namespace), U32, U32, P, P, U32, P)
+    f("sf_system_plan", I, P, C.POINTER(abi.sf_event_batch), P, U32, C.POINTER(U32), P)
+    f("sf_submit_forced", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts), P)
+    f("sf_entry_node_add", I, P, C.POINTER(abi.sf_event_batch), P)
     f("sf_flow_rule_order", I, C.POINTER(abi.sf_flow_rule), C.POINTER(abi.sf_rule_key), U32, P, C.POINTER(U32))
     f("sf_param_rule_order", I, C.POINTER(abi.sf_param_rule), C.POINTER(abi.sf_rule_key), U32,
       C.POINTER(abi.sf_hot_item), U32, P, C.POINTER(U32))
@@ -284,6 +287,35 @@ class FlowEngine:
         b = batch.c_struct()
         v = out.c_struct()
         _check(lib().sf_submit(self.h, C.byref(b), C.byref(v)))
+
+    # ---- node-wide SystemRule rounds of a sharded node (sentinel_flow.h; system_shard.py)
+    def system_plan(self, merged: abi.HostBatch, status: np.ndarray, p: int, sys_mask: np.ndarray) -> int:
+        """Plans merged[p, q) (the node's IN events; status = verdicts of
+        merged[0, p)); fills sys_mask[p:q], returns q."""
+        assert sys_mask.dtype == np.uint8 and sys_mask.shape == (merged.n,)
+        st = np.ascontiguousarray(status, np.uint8)
+        b = merged.c_struct()
+        q = C.c_uint32(0)
+        _check(lib().sf_system_plan(self.h, C.byref(b), st.ctypes.data if p else None, p, C.byref(q),
+                                    sys_mask.ctypes.data))
+        return int(q.value)
+
+    def submit_forced(self, batch: abi.HostBatch, sys_mask: np.ndarray) -> abi.HostVerdicts:
+        """A (sub-)batch whose SystemRule verdicts were planned node-wide."""
+        m = np.ascontiguousarray(sys_mask, np.uint8)
+        assert m.shape == (batch.n,)
+        out = abi.HostVerdicts(batch.n)
+        b = batch.c_struct()
+        v = out.c_struct()
+        _check(lib().sf_submit_forced(self.h, C.byref(b), C.byref(v), m.ctypes.data))
+        return out
+
+    def entry_node_add(self, batch: abi.HostBatch, status: np.ndarray):
+        """ENTRY_NODE update with decided IN events of the node."""
+        st = np.ascontiguousarray(status, np.uint8)
+        assert st.shape == (batch.n,)
+        b = batch.c_struct()
+        _check(lib().sf_entry_node_add(self.h, C.byref(b), st.ctypes.data))
 
     def submit_device_async(self, batch: DeviceBatch, out: DeviceVerdicts):
         """Enqueue a batch (HBM arrays; keep them alive until sync()): batch k+1 is

@@ -145,6 +145,31 @@ def test_system_rule_large(eng_mod, so, kind):
           f"{(st == abi.V_BLOCK_SYSTEM).sum()} system blocks, reasons {np.bincount(reasons)}")
 
 
+@pytest.mark.parametrize("kind", ["qps", "thread", "rt", "load", "cpu", "mixed"])
+def test_system_sharded_two_engines(eng_mod, so, kind):
+    """SystemRules on a resource-sharded node (two engines on cuda:0, one per
+    rank, in threads): the node-wide round protocol (system_shard.py:
+    sf_system_plan / sf_submit_forced / sf_entry_node_add) gives the verdicts
+    of one oracle replay of the whole node batch, and every rank's ENTRY_NODE
+    equals the oracle's."""
+    from tests import test_system_shard as ts
+    w = workloads.system_large("mixed") if kind == "mixed" else workloads.system(kind)
+    got, ens = ts.run_local_ranks(eng_mod.FlowEngine, w, w["batches"])
+    ts.check_against_reference(w, w["batches"], got, ens)
+
+
+def test_system_sharded_plain_submit_refused(eng_mod):
+    """A sharded engine with SystemRules refuses sf_submit (ENTRY_NODE is node-wide)."""
+    w = workloads.system("thread")
+    cfg = abi.default_config(max_resources=w["cfg"].max_resources, max_batch=w["cfg"].max_batch,
+                             shard_count=2, shard_index=0)
+    e = eng_mod.FlowEngine(cfg)
+    e.load_system_rules(list(w["system"]))
+    b = w["batches"][0].shard(2, 0)
+    with pytest.raises(RuntimeError, match="round protocol"):
+        e.submit(b)
+
+
 def test_config2_large_properties(eng_mod, so):
     """1M-event uniform batch: oracle parity plus the window invariant
     passes(hw) + passes(hw-1) <= count for every resource."""
