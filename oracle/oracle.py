@@ -146,6 +146,8 @@ def _declare(L):
     f("so_system_plan", C.c_int, P, C.POINTER(abi.sf_event_batch), P, U32, C.POINTER(U32), P)
     f("so_submit_forced", C.c_int, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts), P)
     f("so_entry_node_add", C.c_int, P, C.POINTER(abi.sf_event_batch), P)
+    f("so_load_degrade_rules", C.c_int, P, C.POINTER(abi.sf_degrade_rule), U32, C.POINTER(U32))
+    f("so_read_breaker", C.c_int, P, U32, C.POINTER(abi.sf_breaker_state))
     f("so_read_rule_state", C.c_int, P, U32, C.POINTER(abi.sf_rule_state))
     f("so_read_param", C.c_int, P, U32, U8, U64, C.POINTER(I64), C.POINTER(I64), C.POINTER(C.c_int))
     f("so_param_thread", I64, P, U32, C.c_int, U8, U64)
@@ -489,6 +491,24 @@ class OracleEngine:
         rc = lib().so_submit(self.h, C.byref(b), C.byref(v))
         assert rc == 0, rc
         return out
+
+    def load_degrade_rules(self, rules) -> int:
+        """DegradeSlot inside the chain (after FlowSlot); rules as for
+        FlowEngine.load_degrade_rules (dicts of sf_degrade_rule fields)."""
+        arr = (abi.sf_degrade_rule * max(1, len(rules)))()
+        for i, r in enumerate(rules):
+            for k, v in r.items():
+                setattr(arr[i], k, v)
+        n = U32(0)
+        rc = lib().so_load_degrade_rules(self.h, arr, len(rules), C.byref(n))
+        if rc:
+            raise ValueError(f"so_load_degrade_rules: {rc}")
+        return int(n.value)
+
+    def read_breaker(self, k) -> abi.sf_breaker_state:
+        st = abi.sf_breaker_state()
+        assert lib().so_read_breaker(self.h, k, C.byref(st)) == 0
+        return st
 
     # node-wide SystemRule rounds (sentinel_amd/system_shard.py), one IN event per round
     def system_plan(self, merged: abi.HostBatch, status, p: int, sys_mask) -> int:

@@ -1035,7 +1035,21 @@ typedef struct {
     int* flow_rules; int n_flow;      /* indices into e->flow (list order)    */
     int* param_rules; int n_param;
     so_param_metric* pm;              /* ParameterMetricStorage entry          */
+    int* cbs; int n_cb;               /* circuit breakers (indices into e->cb, rule list order) */
 } res_rt;
+
+/* One CircuitBreaker (DegradeRuleManager.newCircuitBreakerFrom, :206-219) with
+ * its LeapArray(1, statIntervalMs) counter (ResponseTimeCircuitBreaker.java:48-56,
+ * ExceptionCircuitBreaker.java:47-56, AbstractCircuitBreaker.java:47-55). */
+typedef struct {
+    sf_degrade_rule rule;
+    int64_t max_rt;                   /* Math.round(count) (ResponseTimeCircuitBreaker :52) */
+    double threshold;                 /* slowRatioThreshold (RT) / count */
+    int64_t recovery;                 /* timeWindow * 1000 */
+    int state;                        /* SF_CB_* */
+    int64_t next_retry;
+    int has_bucket; int64_t ws, hit, total;
+} so_breaker;
 
 typedef struct {                      /* cluster flow / param rule state */
     int64_t flow_id; int is_param; double count; int threshold_type; uint32_t ns;
@@ -1061,6 +1075,7 @@ struct so_engine {
     /* entries of the batch being replayed */
     uint8_t* entry_blocked; uint32_t cap_entries;
     const uint8_t* forced;            /* so_submit_forced: planned SystemRule verdicts, ENTRY_NODE untouched */
+    so_breaker* cb; uint32_t n_cb;    /* DegradeRuleManager's circuit breakers, load order of the valid rules */
     /* cluster */
     cluster_rt* cl; uint32_t n_cl;
     sf_hot_item* cl_items; uint32_t n_cl_items;
@@ -1098,6 +1113,8 @@ static void clear_param(so_engine* e) {
     }
 }
 void so_destroy(so_engine* e) {
+    free(e->cb);
+    for (uint32_t r = 0; e->res && r < e->n_res; r++) free(e->res[r].cbs);
     if (!e) return;
     clear_flow(e); clear_param(e);
     for (uint32_t r = 0; r < e->n_res; r++) so_node_free(e->res[r].node);
@@ -1190,6 +1207,133 @@ int so_load_system_rules(so_engine* e, const sf_system_rule* rules, uint32_t n) 
     }
     return SF_OK;
 }
+/* ---- DegradeSlot (DegradeSlot.java:42-94) ---------------------------------
+ * DegradeRuleManager.isValidRule :183-204 */
+static int cb_valid(const sf_degrade_rule* r) {
+    if (!(r->count >= 0) || r->time_window_s <= 0) return 0;
+    if (r->min_request_amount <= 0 || r->stat_interval_ms <= 0) return 0;
+    if (r->grade == SF_DEGRADE_GRADE_RT) return r->slow_ratio_threshold >= 0 && r->slow_ratio_threshold <= 1;
+    if (r->grade == SF_DEGRADE_GRADE_EXCEPTION_RATIO) return r->count <= 1;
+    return r->grade == SF_DEGRADE_GRADE_EXCEPTION_COUNT;
+}
+static int same_double(double a, double b) {   /* Double.compare(a, b) == 0 */
+    if (a != a || b != b) return a != a && b != b;
+    return memcmp(&a, &b, sizeof a) == 0;
+}
+/* DegradeRule.equals (DegradeRule.java:153-164) */
+static int cb_rule_equal(const sf_degrade_rule* a, const sf_degrade_rule* b) {
+    return a->resource == b->resource && a->grade == b->grade && same_double(a->count, b->count) &&
+           a->time_window_s == b->time_window_s && a->min_request_amount == b->min_request_amount &&
+           same_double(a->slow_ratio_threshold, b->slow_ratio_threshold) && a->stat_interval_ms == b->stat_interval_ms;
+}
+
+/* buildCircuitBreakers (:236-265) with getExistingSameCbOrNew (:151-163): an
+ * equal rule of the resource keeps its breaker and state (two equal new rules
+ * sharing one breaker are refused, like the engine). */
+int so_load_degrade_rules(so_engine* e, const sf_degrade_rule* rules, uint32_t n, uint32_t* n_loaded) {
+    so_breaker* nb = calloc(n ? n : 1, sizeof *nb);
+    uint8_t* taken = calloc(e->n_cb ? e->n_cb : 1, 1);
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const sf_degrade_rule* r = &rules[i];
+        uint32_t l;
+        if (!cb_valid(r)) continue;
+        if (!local_id(e, r->resource, &l)) { free(nb); free(taken); return SF_ERR_INVALID; }
+        int reuse = -1;
+        for (uint32_t o = 0; o < e->n_cb; o++)
+            if (cb_rule_equal(&e->cb[o].rule, r)) {
+                if (taken[o]) { free(nb); free(taken); return SF_ERR_UNSUPPORTED; }
+                reuse = (int)o; taken[o] = 1; break;
+            }
+        if (reuse >= 0) {
+            nb[k] = e->cb[reuse];
+        } else {
+            so_breaker* b = &nb[k];
+            b->rule = *r;
+            b->max_rt = so_java_round(r->count);
+            b->threshold = r->grade == SF_DEGRADE_GRADE_RT ? r->slow_ratio_threshold : r->count;
+            b->recovery = (int64_t)r->time_window_s * 1000;
+            b->state = SF_CB_CLOSED;
+        }
+        k++;
+    }
+    free(taken);
+    free(e->cb);
+    e->cb = nb; e->n_cb = k;
+    for (uint32_t r = 0; r < e->n_res; r++) { free(e->res[r].cbs); e->res[r].cbs = NULL; e->res[r].n_cb = 0; }
+    for (uint32_t c = 0; c < k; c++) {
+        uint32_t l = 0;
+        local_id(e, e->cb[c].rule.resource, &l);
+        res_rt* rr = &e->res[l];
+        rr->cbs = realloc(rr->cbs, (size_t)(rr->n_cb + 1) * sizeof(int));
+        rr->cbs[rr->n_cb++] = (int)c;
+    }
+    if (n_loaded) *n_loaded = k;
+    return SF_OK;
+}
+
+int so_read_breaker(so_engine* e, uint32_t k, sf_breaker_state* out) {
+    if (k >= e->n_cb) return SF_ERR_INVALID;
+    const so_breaker* b = &e->cb[k];
+    memset(out, 0, sizeof *out);
+    out->state = b->state; out->next_retry_ms = b->next_retry;
+    out->window_start = b->has_bucket ? b->ws : SF_WS_ABSENT;
+    out->hit_count = b->hit; out->total_count = b->total;
+    return SF_OK;
+}
+
+/* LeapArray(1, interval).currentWindow(now) of the breaker's counter */
+static void cb_current(so_breaker* b) {
+    const int64_t ws = g_now - g_now % b->rule.stat_interval_ms;
+    if (!b->has_bucket || ws > b->ws) { b->has_bucket = 1; b->ws = ws; b->hit = 0; b->total = 0; }
+}
+static void cb_to_open(so_breaker* b) {          /* transformToOpen + updateNextRetryTimestamp (:93-95) */
+    b->state = SF_CB_OPEN;
+    b->next_retry = g_now + b->recovery;
+}
+/* onRequestComplete + handleStateChangeWhenThresholdExceeded
+ * (ResponseTimeCircuitBreaker.java:64-130, ExceptionCircuitBreaker.java:64-119) */
+static void cb_on_complete(so_breaker* b, int64_t rt, int error) {
+    cb_current(b);
+    const int hit = b->rule.grade == SF_DEGRADE_GRADE_RT ? rt > b->max_rt : error != 0;
+    b->hit += hit;
+    b->total += 1;
+    if (b->state == SF_CB_OPEN) return;
+    if (b->state == SF_CB_HALF_OPEN) {
+        if (hit) cb_to_open(b);                                           /* fromHalfOpenToOpen */
+        else { b->state = SF_CB_CLOSED; cb_current(b); b->hit = b->total = 0; }   /* fromHalfOpenToClose + resetStat */
+        return;
+    }
+    if (b->total < b->rule.min_request_amount) return;
+    if (b->rule.grade == SF_DEGRADE_GRADE_RT) {
+        const double ratio = b->hit * 1.0 / b->total;
+        if (ratio > b->threshold || (ratio == b->threshold && b->threshold == 1.0)) cb_to_open(b);
+    } else {
+        const double cur = b->rule.grade == SF_DEGRADE_GRADE_EXCEPTION_RATIO ? b->hit * 1.0 / b->total : (double)b->hit;
+        if (cur > b->threshold) cb_to_open(b);
+    }
+}
+/* DegradeSlot.performChecking (:50-61): tryPass of each breaker
+ * (AbstractCircuitBreaker.tryPass :67-82); the breakers the entry moved to
+ * HALF_OPEN go back to OPEN when a later one refuses (whenTerminate :113-129).
+ * Returns the refusing breaker's position in the resource list or -1. */
+static int cb_check(so_engine* e, res_rt* rr) {
+    int moved[SF_MAX_BREAKERS_PER_RESOURCE], n_moved = 0;
+    for (int k = 0; k < rr->n_cb; k++) {
+        so_breaker* b = &e->cb[rr->cbs[k]];
+        if (b->state == SF_CB_CLOSED) continue;
+        if (b->state == SF_CB_OPEN && g_now >= b->next_retry) {
+            b->state = SF_CB_HALF_OPEN;
+            if (n_moved < SF_MAX_BREAKERS_PER_RESOURCE) moved[n_moved++] = rr->cbs[k];
+            continue;
+        }
+        for (int q = 0; q < n_moved; q++)
+            if (e->cb[moved[q]].state == SF_CB_HALF_OPEN) e->cb[moved[q]].state = SF_CB_OPEN;
+        return k;
+    }
+    return -1;
+}
+
 int so_set_system_status(so_engine* e, double load, double cpu) { e->cur_load = load; e->cur_cpu = cpu; return SF_OK; }
 
 /* SystemRuleManager.checkSystem :291-340 ; checkBbr :342-348.  Returns -1 pass or the reason. */
@@ -1303,6 +1447,8 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
                 }
                 /* ParamFlowStatisticExitCallback.onExit -> decreaseThreadCount(args) */
                 if (rr->pm) pm_thread_event(rr->pm, in, i, na, 0);
+                /* DegradeSlot.exit :72-91: onRequestComplete of every breaker */
+                for (int k = 0; k < rr->n_cb; k++) cb_on_complete(&e->cb[rr->cbs[k]], rt, err);
                 status = SF_V_EXIT;
             } else {
                 status = SF_V_EXIT_IGNORED;
@@ -1357,6 +1503,12 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
                 if (!ok) { blocked = 1; status = SF_V_BLOCK_FLOW; rule_idx = k; break; }
                 wait += w;
             }
+        }
+        /* DegradeSlot.entry (DegradeSlot.java:42-61), the last slot: not reached
+         * after a block or a PriorityWaitException from FlowSlot */
+        if (!blocked && !prio_wait && rr->n_cb) {
+            const int k = cb_check(e, rr);
+            if (k >= 0) { blocked = 1; status = SF_V_BLOCK_DEGRADE; rule_idx = k; }
         }
         /* StatisticSlot.entry accounting :64-123 */
         if (blocked) {

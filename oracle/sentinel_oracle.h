@@ -194,6 +194,8 @@ int  so_system_plan(so_engine* e, const sf_event_batch* in, const uint8_t* statu
                     uint8_t* sys_mask);
 int  so_submit_forced(so_engine* e, const sf_event_batch* in, sf_verdicts* out, const uint8_t* sys_mask);
 int  so_entry_node_add(so_engine* e, const sf_event_batch* in, const uint8_t* status);
+int  so_load_degrade_rules(so_engine* e, const sf_degrade_rule* rules, uint32_t n, uint32_t* n_loaded);
+int  so_read_breaker(so_engine* e, uint32_t k, sf_breaker_state* out);
 int  so_read_node(so_engine* e, uint32_t res, sf_node_state* out);
 int  so_read_entry_node(so_engine* e, sf_node_state* out);
 int  so_read_rule_state(so_engine* e, uint32_t rule_index, sf_rule_state* out);

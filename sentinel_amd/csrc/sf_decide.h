@@ -589,7 +589,17 @@ SF_HD void pm_thread_event(const ParamTable& pt, uint32_t res, uint8_t pm_init, 
     }
 }
 
-SF_HD bool v_blocked(uint8_t v) { return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM; }
+SF_HD bool v_blocked(uint8_t v) {
+    return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM || v == SF_V_BLOCK_DEGRADE;
+}
+
+// the resource's circuit breakers [*b0, *b1) (DegradeRuleManager's list order)
+SF_HD void breakers_of(const DevState& st, uint32_t res, uint32_t* b0, uint32_t* b1) {
+    *b0 = *b1 = 0;
+    if (!st.dg_rr_of) return;
+    const uint32_t k = st.dg_rr_of[res];
+    if (k < st.dg_n) { *b0 = st.dg_off[k]; *b1 = st.dg_off[k + 1]; }
+}
 
 // SystemRules: a SystemBlockException of an IN entry is decided by the
 // planner (sf_system.h) and arrives as EVF_SYSBLK on the event.
@@ -618,6 +628,8 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
     uint8_t pm_init = nprules ? st.pm_init[res] : 0;
     bool pm_exists = pm_init != 0;
     ParamTable pt{st.ptab, st.pcap_mask, st.err};
+    uint32_t cb0, cb1;                                         // DegradeSlot breakers (this lane owns them)
+    breakers_of(st, res, &cb0, &cb1);
 
     // The lane's events are read EV_CH at a time with all loads in flight together
     // (each cache line of the sorted arrays is then fetched once, not once per
@@ -665,6 +677,11 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
                 nd.threads--;
                 if (fl & SF_EV_ERROR) nd.add_exception(now, c);
                 if (pm_exists) pm_thread_event(pt, res, pm_init, io, j, na, -1);   // ParamFlowStatisticExitCallback
+                for (uint32_t cb = cb0; cb < cb1; cb++) {        // DegradeSlot.exit :72-91 (after StatisticSlot.exit)
+                    sf_breaker_state bs = st.dg_state[cb];
+                    dg_complete(bs, st.dg_rules[cb], now, rt, (fl & SF_EV_ERROR) != 0);
+                    st.dg_state[cb] = bs;
+                }
                 status = SF_V_EXIT;
             } else {
                 status = SF_V_EXIT_IGNORED;
@@ -711,6 +728,12 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
                 if (!ok) { blocked = true; status = SF_V_BLOCK_FLOW; rule_idx = k; break; }
                 wait += w;
             }
+        }
+        // DegradeSlot.entry (DegradeSlot.java:42-61), last in the chain; a
+        // PriorityWaitException from FlowSlot never reaches it
+        if (!blocked && !prio_wait && cb1 > cb0) {
+            const int k = dg_entry_check(st.dg_state, cb0, cb1, now);
+            if (k >= 0) { blocked = true; status = SF_V_BLOCK_DEGRADE; rule_idx = k; }
         }
         // StatisticSlot.entry accounting :64-123
         if (blocked) {
@@ -770,6 +793,29 @@ inline DevRule make_dev_rule(const sf_flow_rule& r, int cold_factor, int host_in
         d.max_token = d.warning_token + j_d2i(2 * period * r.count / (1.0 + cold_factor));
         d.slope = (cold_factor - 1.0) / r.count / (double)(d.max_token - d.warning_token);
     }
+    return d;
+}
+// DegradeRuleManager.isValidRule (DegradeRuleManager.java:183-204)
+inline bool dg_valid(const sf_degrade_rule& r) {
+    if (!(r.count >= 0) || r.time_window_s <= 0) return false;
+    if (r.min_request_amount <= 0 || r.stat_interval_ms <= 0) return false;
+    switch (r.grade) {
+        case SF_DEGRADE_GRADE_RT: return r.slow_ratio_threshold >= 0 && r.slow_ratio_threshold <= 1;
+        case SF_DEGRADE_GRADE_EXCEPTION_RATIO: return r.count <= 1;
+        case SF_DEGRADE_GRADE_EXCEPTION_COUNT: return true;
+        default: return false;
+    }
+}
+// a breaker's constants (ResponseTimeCircuitBreaker.java:48-56, ExceptionCircuitBreaker.java:47-56,
+// AbstractCircuitBreaker.java:47-55)
+inline DevBreakerRule make_dev_breaker_rule(const sf_degrade_rule& r) {
+    DevBreakerRule d{};
+    d.grade = r.grade;
+    d.min_req = r.min_request_amount;
+    d.max_rt = j_round(r.count);                             // Math.round (ResponseTimeCircuitBreaker.java:52)
+    d.thr = r.grade == SF_DEGRADE_GRADE_RT ? r.slow_ratio_threshold : r.count;
+    d.recovery = (int64_t)r.time_window_s * 1000;
+    d.interval = r.stat_interval_ms;
     return d;
 }
 inline DevParamRule make_dev_param_rule(const sf_param_rule& r, int host_index) {

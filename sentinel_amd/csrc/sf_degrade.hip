@@ -56,52 +56,6 @@ __global__ void __launch_bounds__(BLK) k_dg_bounds(const uint32_t* keys, uint32_
     if (j == n - 1 || keys[j + 1] != k) end[k] = j + 1;
 }
 
-__device__ __forceinline__ void dg_roll(sf_breaker_state& s, const DevBreakerRule& r, int64_t t) {
-    // LeapArray(1, interval).currentWindow(t): create, keep, or reset the single bucket (LeapArray.java:128-225)
-    if (t >= 0 && s.window_start != DG_WS_NONE && t >= s.window_start && t - s.window_start < r.interval)
-        return;                                // same window: no 64-bit modulo on the serial chain
-    const int64_t ws = t - t % r.interval;
-    if (s.window_start == DG_WS_NONE || ws > s.window_start) {
-        s.window_start = ws;
-        s.hit_count = 0;
-        s.total_count = 0;
-    }
-}
-
-__device__ __forceinline__ void dg_open(sf_breaker_state& s, const DevBreakerRule& r, int64_t t) {
-    s.state = SF_CB_OPEN;
-    s.next_retry_ms = t + r.recovery;          // updateNextRetryTimestamp (AbstractCircuitBreaker.java:93-95)
-}
-
-// onRequestComplete + handleStateChangeWhenThresholdExceeded of one breaker.
-__device__ __forceinline__ void dg_complete(sf_breaker_state& s, const DevBreakerRule& r, int64_t t, int64_t rt,
-                                            bool error) {
-    dg_roll(s, r, t);
-    const bool hit = r.grade == SF_DEGRADE_GRADE_RT ? rt > r.max_rt : error;
-    s.hit_count += hit;
-    s.total_count += 1;
-    if (s.state == SF_CB_OPEN) return;
-    if (s.state == SF_CB_HALF_OPEN) {
-        if (hit) {
-            dg_open(s, r, t);                  // fromHalfOpenToOpen
-        } else {
-            s.state = SF_CB_CLOSED;            // fromHalfOpenToClose -> resetStat (current bucket)
-            s.hit_count = 0;
-            s.total_count = 0;
-        }
-        return;
-    }
-    if (s.total_count < r.min_req) return;
-    const double cur = (r.grade == SF_DEGRADE_GRADE_EXCEPTION_COUNT) ? (double)s.hit_count
-                                                                      : (double)s.hit_count * 1.0 / (double)s.total_count;
-    if (cur > r.thr) {
-        dg_open(s, r, t);
-    } else if (r.grade == SF_DEGRADE_GRADE_RT && cur == r.thr && r.thr == 1.0) {
-        dg_open(s, r, t);                      // ResponseTimeCircuitBreaker.java:126-129
-    }
-}
-
-
 __device__ __forceinline__ int64_t rl64(int64_t v, int l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
@@ -396,27 +350,8 @@ __global__ void __launch_bounds__(BLK) k_dg_walk(DegradeDev d, DegradeBatch b, c
         const int64_t t = b.ts[i];
         const uint8_t f = b.flags[i];
         if (!(f & SF_EV_EXIT)) {
-            // DegradeSlot.performChecking: tryPass of each breaker, first refusal blocks
-            uint64_t moved = 0;
-            int blocked = -1;
-            for (uint32_t c = c0; c < c1; c++) {
-                const int st = S[c].state;
-                if (st == SF_CB_CLOSED) continue;
-                if (st == SF_CB_OPEN && t >= S[c].next_retry_ms) {   // retryTimeoutArrived && fromOpenToHalfOpen
-                    S[c].state = SF_CB_HALF_OPEN;
-                    moved |= 1ull << (c - c0);
-                    continue;
-                }
-                blocked = (int)(c - c0);
-                break;
-            }
+            const int blocked = dg_entry_check(S, c0, c1, t);   // DegradeSlot.performChecking
             if (blocked >= 0) {
-                // whenTerminate hook of the probes this entry opened: HALF_OPEN -> OPEN, retry time kept
-                while (moved) {
-                    const int q = __builtin_ctzll(moved);
-                    moved &= moved - 1;
-                    if (S[c0 + q].state == SF_CB_HALF_OPEN) S[c0 + q].state = SF_CB_OPEN;
-                }
                 status[i] = SF_V_BLOCK_DEGRADE;
                 if (rule) rule[i] = (uint16_t)blocked;
             }

@@ -1657,18 +1657,6 @@ int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uin
 
 
 // ---------------------------------------------------------------- DegradeSlot circuit breakers
-// DegradeRuleManager.isValidRule (DegradeRuleManager.java:183-204)
-static bool dg_valid(const sf_degrade_rule& r) {
-    if (!(r.count >= 0) || r.time_window_s <= 0) return false;
-    if (r.min_request_amount <= 0 || r.stat_interval_ms <= 0) return false;
-    switch (r.grade) {
-        case SF_DEGRADE_GRADE_RT: return r.slow_ratio_threshold >= 0 && r.slow_ratio_threshold <= 1;
-        case SF_DEGRADE_GRADE_EXCEPTION_RATIO: return r.count <= 1;
-        case SF_DEGRADE_GRADE_EXCEPTION_COUNT: return true;
-        default: return false;
-    }
-}
-
 // DegradeRule.equals (DegradeRule.java:153-164, AbstractRule.equals :76-93):
 // resource, limitApp (always "default" here) and the six fields, doubles by
 // Double.compare (bit pattern; every NaN equal).
@@ -1718,13 +1706,7 @@ int sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t n
         if (p - off.back() >= SF_MAX_BREAKERS_PER_RESOURCE)
             return fail(SF_ERR_UNSUPPORTED, "more than SF_MAX_BREAKERS_PER_RESOURCE degrade rules on one resource");
         const sf_degrade_rule& r = rules[valid[v]];
-        DevBreakerRule& d = dr[p];
-        d.grade = r.grade;
-        d.min_req = r.min_request_amount;
-        d.max_rt = j_round(r.count);                             // Math.round (ResponseTimeCircuitBreaker.java:52)
-        d.thr = r.grade == SF_DEGRADE_GRADE_RT ? r.slow_ratio_threshold : r.count;
-        d.recovery = (int64_t)r.time_window_s * 1000;
-        d.interval = r.stat_interval_ms;
+        dr[p] = make_dev_breaker_rule(r);
         st[p] = sf_breaker_state{SF_CB_CLOSED, 0, 0, DG_WS_NONE, 0, 0};
         pos[v] = p;
     }
@@ -1775,6 +1757,9 @@ int sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t n
     e->dg = DegradeDev{};
     e->dg.rr_of = d_rr; e->dg.off = d_off; e->dg.rules = d_rules; e->dg.state = d_st;
     e->dg.n_rres = n_rres;
+    // DegradeSlot inside sf_submit's chain (sf_decide.h decide_segment)
+    e->st.dg_rr_of = n_rres ? d_rr : nullptr;
+    e->st.dg_off = d_off; e->st.dg_rules = d_rules; e->st.dg_state = d_st; e->st.dg_n = n_rres;
     e->dg_pos = pos;
     e->dg_rules.clear();
     for (uint32_t v = 0; v < nv; v++) e->dg_rules.push_back(rules[valid[v]]);

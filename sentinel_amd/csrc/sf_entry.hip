@@ -37,7 +37,7 @@ __device__ __forceinline__ EnEvent en_event(const DevBatch& b, const uint8_t* vs
     e.t = b.ts[i];
     if (!(f & SF_EV_EXIT)) {
         e.pass = v == SF_V_PASS || v == SF_V_PASS_WAIT;
-        e.block = v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM;
+        e.block = v_blocked(v);
         e.touch = e.pass || e.block;                                 // PriorityWait: thread only
         e.thr = (e.pass || v == SF_V_PRIORITY_WAIT) ? 1 : 0;
     } else if (v == SF_V_EXIT) {

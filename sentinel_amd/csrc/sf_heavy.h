@@ -42,6 +42,9 @@ static_assert(sizeof(Acc) == ACC_BYTES, "Acc layout must match the engine alloca
 // QPS / WarmUp / RateLimiter resources (and resources without rules) when no
 // entry is prioritized or has acquireCount <= 0 and IntervalProperty is 1 s.
 SF_HD uint8_t heavy_mode(const DevState& st, uint32_t res, uint32_t segflags, int64_t first_ts) {
+    // circuit breakers (DegradeSlot) feed back into the node's pass / block
+    // counts event by event: the generic lane walk (decide_segment) only
+    if (st.dg_rr_of && st.dg_rr_of[res] < st.dg_n) return SM_GENERIC;
     // a borrowed (prioritized) pass waiting for a window of this batch would be
     // copied into that window when it is created: keep such resources exact
     // on the generic path (OccupiableBucketLeapArray.java:40-64)

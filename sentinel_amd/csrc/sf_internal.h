@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include "../../include/sentinel_flow.h"
+#include "sf_degrade.h"
 
 namespace sf {
 
@@ -78,6 +79,13 @@ struct DevState {
     int32_t* err;                  // device error word (capacity, invalid input)
     int64_t* last_fetch;           // [R] StatisticNode.lastFetchTime (metric snapshot)
     int64_t* last_ts;              // engine clock: last event time of the previous batch (time never goes back)
+    // DegradeSlot (after FlowSlot): breakers of local resource l are
+    // [dg_off[k], dg_off[k+1]) with k = dg_rr_of[l] < dg_n; dg_rr_of null = none
+    const uint32_t* dg_rr_of;
+    const uint32_t* dg_off;
+    const DevBreakerRule* dg_rules;
+    sf_breaker_state* dg_state;
+    uint32_t dg_n;
 };
 
 // Constants.ENTRY_NODE (Constants.java:66): the ClusterNode of all inbound

@@ -28,6 +28,10 @@ struct hs_engine {
     std::vector<DevHotItem> items;
     std::vector<uint8_t> pm_init;
     std::vector<ParamSlot> ptab;
+    std::vector<uint32_t> dg_rr, dg_off;
+    std::vector<DevBreakerRule> dg_rules;
+    std::vector<sf_breaker_state> dg_state;
+    std::vector<uint32_t> dg_pos;                  // load order -> position
     int32_t err = 0;
     uint32_t R;
     uint32_t heavy_min;
@@ -38,6 +42,9 @@ struct hs_engine {
         st.rstate = rstate.data(); st.prule_off = prule_off.data(); st.prules = prules.data();
         st.items = items.data(); st.pm_init = pm_init.data(); st.ptab = ptab.data();
         st.pcap_mask = ptab.size() - 1; st.err = &err;
+        st.dg_n = dg_off.empty() ? 0 : (uint32_t)dg_off.size() - 1;
+        st.dg_rr_of = st.dg_n ? dg_rr.data() : nullptr;
+        st.dg_off = dg_off.data(); st.dg_rules = dg_rules.data(); st.dg_state = dg_state.data();
     }
 };
 
@@ -106,6 +113,42 @@ int hs_load_param_rules(hs_engine* e, const sf_param_rule* rules, uint32_t n, co
     std::fill(e->pm_init.begin(), e->pm_init.end(), 0);
     std::fill(e->ptab.begin(), e->ptab.end(), ParamSlot{0, 0, 0, 0});
     e->refresh();
+    return SF_OK;
+}
+
+// DegradeSlot rules (fresh breakers; list order per resource)
+int hs_load_degrade_rules(hs_engine* e, const sf_degrade_rule* rules, uint32_t n, uint32_t* n_loaded) {
+    std::vector<uint32_t> loc, valid;
+    for (uint32_t i = 0; i < n; i++) {
+        if (!dg_valid(rules[i])) continue;
+        uint32_t l; if (!local_of(e, rules[i].resource, &l)) return SF_ERR_INVALID;
+        valid.push_back(i); loc.push_back(l);
+    }
+    const uint32_t nv = (uint32_t)valid.size();
+    std::vector<uint32_t> order(nv);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return loc[a] < loc[b]; });
+    e->dg_rr.assign(e->R, 0); e->dg_off.clear(); e->dg_rules.assign(std::max<uint32_t>(1, nv), DevBreakerRule{});
+    e->dg_state.assign(std::max<uint32_t>(1, nv), sf_breaker_state{SF_CB_CLOSED, 0, 0, DG_WS_NONE, 0, 0});
+    e->dg_pos.assign(nv, 0);
+    for (uint32_t p = 0; p < nv; p++) {
+        const uint32_t v = order[p];
+        if (p == 0 || loc[order[p - 1]] != loc[v]) e->dg_off.push_back(p);
+        e->dg_rules[p] = make_dev_breaker_rule(rules[valid[v]]);
+        e->dg_pos[v] = p;
+    }
+    const uint32_t nr = (uint32_t)e->dg_off.size();
+    if (nv) e->dg_off.push_back(nv);
+    for (auto& x : e->dg_rr) x = nr;
+    for (uint32_t k = 0; k < nr; k++) e->dg_rr[loc[order[e->dg_off[k]]]] = k;
+    e->refresh();
+    if (n_loaded) *n_loaded = nv;
+    return SF_OK;
+}
+int hs_read_breaker(hs_engine* e, uint32_t k, sf_breaker_state* out) {
+    if (k >= e->dg_pos.size()) return SF_ERR_INVALID;
+    *out = e->dg_state[e->dg_pos[k]];
+    if (out->window_start == DG_WS_NONE) out->window_start = SF_WS_ABSENT;
     return SF_OK;
 }
 

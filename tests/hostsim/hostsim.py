@@ -27,6 +27,8 @@ def lib():
         L.hs_submit.argtypes = [P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts)]
         L.hs_read_node.argtypes = [P, C.c_uint32, C.POINTER(abi.sf_node_state)]
         L.hs_read_rule_state.argtypes = [P, C.c_uint32, C.POINTER(abi.sf_rule_state)]
+        L.hs_load_degrade_rules.argtypes = [P, C.POINTER(abi.sf_degrade_rule), C.c_uint32, C.POINTER(C.c_uint32)]
+        L.hs_read_breaker.argtypes = [P, C.c_uint32, C.POINTER(abi.sf_breaker_state)]
         _lib = L
     return _lib
 
@@ -49,6 +51,20 @@ class HostSimEngine:
     def load_param_rules(self, rules, items=()):
         assert lib().hs_load_param_rules(self.h, abi.rules_array(abi.sf_param_rule, rules), len(rules),
                                          abi.rules_array(abi.sf_hot_item, list(items)), len(items)) == 0
+
+    def load_degrade_rules(self, rules) -> int:
+        arr = (abi.sf_degrade_rule * max(1, len(rules)))()
+        for i, r in enumerate(rules):
+            for k, v in r.items():
+                setattr(arr[i], k, v)
+        n = C.c_uint32(0)
+        assert lib().hs_load_degrade_rules(self.h, arr, len(rules), C.byref(n)) == 0
+        return int(n.value)
+
+    def read_breaker(self, k):
+        st = abi.sf_breaker_state()
+        assert lib().hs_read_breaker(self.h, k, C.byref(st)) == 0
+        return st
 
     def submit(self, batch):
         out = abi.HostVerdicts(batch.n)

@@ -170,6 +170,33 @@ def test_system_sharded_plain_submit_refused(eng_mod):
         e.submit(b)
 
 
+@pytest.mark.parametrize("seed,prio,heavy_min,system", [(11, 0.0, 512, False), (12, 0.2, 8, False),
+                                                        (13, 0.0, 64, True), (14, 0.1, 512, True)])
+def test_degrade_in_submit_chain(eng_mod, so, seed, prio, heavy_min, system):
+    """DegradeSlot after FlowSlot inside sf_submit (DegradeSlot.java:42-94):
+    verdicts, breaker states, nodes and ENTRY_NODE equal to the oracle's chain;
+    with a SystemRule the planner's forced verdicts precede the breakers."""
+    from tests import test_degrade_chain as tc
+    cfg, flow, rules, b = tc.chain_workload(seed, prio=prio, n=60_000)
+    cfg.heavy_min_events = heavy_min
+    sysr = [abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=-1, avg_rt=-1,
+                               max_thread=60)] if system else None
+    cut = b.n // 3
+    batches = [b.subset(0, cut), b.subset(cut, b.n)]
+    e, got, n = tc.run_chain(eng_mod.FlowEngine, cfg, flow, rules, batches, sysr)
+    o, want, n2 = tc.run_chain(so.OracleEngine, cfg, flow, rules, batches, sysr)
+    assert n == n2
+    for k, (g, w) in enumerate(zip(got, want)):
+        parity.compare_verdicts(g, w, f"batch{k}")
+    st = np.concatenate([w.status for w in want])
+    assert (st == abi.V_BLOCK_DEGRADE).sum() > 0 and (st == abi.V_BLOCK_FLOW).sum() > 0
+    if system:
+        assert (st == abi.V_BLOCK_SYSTEM).sum() > 0
+    assert np.array_equal(tc._breaker_rows(e, n), tc._breaker_rows(o, n))
+    parity.compare_nodes(e, o, range(0, cfg.max_resources, 3), sample_count=cfg.sample_count)
+    parity.compare_entry_node(e, o, sample_count=cfg.sample_count)
+
+
 def test_config2_large_properties(eng_mod, so):
     """1M-event uniform batch: oracle parity plus the window invariant
     passes(hw) + passes(hw-1) <= count for every resource."""
