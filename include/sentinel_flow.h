@@ -529,7 +529,13 @@ int  sf_entry_node_allreduce(sf_engine* e, sf_node_state* out);
  * (DegradeRuleManager.getExistingSameCbOrNew :151-163; two equal new rules
  * that would share one breaker are refused with SF_ERR_UNSUPPORTED); a
  * failed load leaves the loaded rules in place.  Event times must be
- * non-decreasing within a batch and across batches (SF_ERR_INVALID).      */
+ * non-decreasing within a batch and across batches (SF_ERR_INVALID).
+ * With degrade rules loaded, sf_submit runs DegradeSlot last in its chain
+ * (after SystemSlot, ParamFlowSlot, FlowSlot): the same breakers, a
+ * DegradeException counted as a block by StatisticSlot, entries blocked
+ * earlier (or PriorityWaitException) never checked, and only exits of
+ * entries that passed the chain completing requests.  Both calls share the
+ * breaker state.                                                          */
 #define SF_DEGRADE_GRADE_RT              0   /* RuleConstant.DEGRADE_GRADE_RT */
 #define SF_DEGRADE_GRADE_EXCEPTION_RATIO 1
 #define SF_DEGRADE_GRADE_EXCEPTION_COUNT 2
