@@ -169,9 +169,6 @@ __device__ uint32_t wave_append(uint32_t* counter, bool take) {
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-#ifndef SF_MED_MIN
-#define SF_MED_MIN 64
-#endif
 // Route each segment: light lane interpreter, heavy window algorithms, or the
 // heavy generic interpreter (one lane of a wavefront).
 __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
@@ -185,12 +182,6 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     if (light && hi - lo > 32 && st.prule_off[res + 1] != st.prule_off[res] &&
         heavy_mode(st, res, w.segflag[s], s_ts[lo]) == SM_PARAM)
         light = false;
-    // likewise a QPS / WarmUp / no-rule segment of more than SF_MED_MIN events:
-    // the window algorithms of k_heavy_decide + the tiled fill beat a lane's walk
-    if (light && hi - lo > SF_MED_MIN) {
-        const uint8_t m = heavy_mode(st, res, w.segflag[s], s_ts[lo]);
-        if (m == SM_QPS || m == SM_WARM || m == SM_NORULE) light = false;
-    }
     // light list slot: workgroup histogram of the length classes in LDS, one
     // global atomic per class and workgroup
     __shared__ uint32_t hcnt[LCLS], hbase[LCLS];

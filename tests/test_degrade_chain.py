@@ -24,7 +24,11 @@ def _breaker_rows(e, n):
     out = []
     for k in range(n):
         s = e.read_breaker(k)
-        out.append([s.state, s.next_retry_ms, s.window_start, s.hit_count, s.total_count])
+        if isinstance(s, dict):                              # FlowEngine.read_breaker
+            ws = abi.SF_WS_ABSENT if s["window_start"] is None else s["window_start"]
+            out.append([s["state"], s["next_retry_ms"], ws, s["hit_count"], s["total_count"]])
+        else:
+            out.append([s.state, s.next_retry_ms, s.window_start, s.hit_count, s.total_count])
     return np.array(out, np.int64).reshape(n, 5)
 
 
