@@ -90,26 +90,59 @@ typedef struct sf_config {
     uint32_t max_flow_ids;        /* capacity of the flowId table              */
     uint32_t heavy_min_events;    /* resource segments longer than this use the
                                      window/skip algorithms (0 = engine default) */
+    uint32_t aux_capacity;        /* origin / context statistic nodes kept for
+                                     the rules that read them (0 = 4096)       */
+    uint32_t pad;
 } sf_config;
 
 /* Fill *cfg with the reference defaults listed above. */
 void sf_config_default(sf_config* cfg);
 
 /* ---- rules ------------------------------------------------------------- */
-/* One FlowRule (FlowRule.java:36-241).  limitApp is "default", no origin;
- * the caller passes rules already in the order Java iterates them
- * (FlowRuleUtil.buildFlowRuleMap: HashSet order + stable FlowRuleComparator
- * sort, FlowRuleUtil.java:83-130).  Rules of one resource keep array order. */
+/* Origins and context names are interned by the caller into one id space:
+ * 0 is the string "default", 1 is "other" (RuleConstant.LIMIT_APP_DEFAULT /
+ * LIMIT_APP_OTHER), any other origin name is an id >= 2, and the empty origin
+ * "" (no ContextUtil.enter origin) is SF_ORIGIN_NONE.  Context names are a
+ * separate id space (0 is whatever name the host interns first, normally
+ * "sentinel_default_context").                                              */
+#define SF_APP_DEFAULT 0u
+#define SF_APP_OTHER   1u
+#define SF_ORIGIN_NONE 0xFFFFFFFFu
+#define SF_REF_NONE    0xFFFFFFFFu   /* blank refResource                       */
+
+/* One FlowRule (FlowRule.java:36-241); the caller passes rules already in the
+ * order Java iterates them (FlowRuleUtil.buildFlowRuleMap: HashSet order +
+ * stable FlowRuleComparator sort, FlowRuleUtil.java:83-130; sf_flow_rule_order).
+ * Rules of one resource keep array order.  FlowRuleChecker.
+ * selectNodeByRequesterAndStrategy (FlowRuleChecker.java:129-161) picks the
+ * node a rule checks:
+ *   limit_app == the event's origin (not "default"/"other") or limit_app
+ *   "other" with an origin no rule of the resource names
+ *       DIRECT -> the origin node of (resource, origin)
+ *   limit_app "default"  DIRECT -> the resource's ClusterNode
+ *   RELATE (any matching limit_app) -> the ClusterNode of ref_resource (a
+ *       resource id; none until that resource's first entry -> pass);
+ *       ref_resource must live on the same shard (res % shard_count)
+ *   CHAIN -> the resource's DefaultNode of context ref_resource (a context id)
+ *       when the event's context is that one, else pass
+ *   anything else -> no node -> pass.
+ * cluster_mode: ClusterStateManager is not started in the engine's process
+ * (pickClusterService() == null, FlowRuleChecker.java:163-203), so a cluster
+ * rule is checked locally when cluster_fallback (fallbackToLocalWhenFail,
+ * ClusterFlowConfig default true) is set and passes otherwise.  Cluster
+ * token rules themselves go to sf_load_cluster_rules (the token server).   */
 typedef struct sf_flow_rule {
     uint32_t resource;            /* resource id (interned name)               */
     int32_t  grade;               /* SF_GRADE_*                                */
     double   count;
-    int32_t  strategy;            /* SF_STRATEGY_DIRECT (RELATE/CHAIN: UNSUPPORTED) */
+    int32_t  strategy;            /* SF_STRATEGY_*                             */
     int32_t  control_behavior;    /* SF_BEHAVIOR_*                             */
     int32_t  warm_up_period_sec;  /* default 10                                */
     int32_t  max_queueing_time_ms;/* default 500                               */
-    int32_t  cluster_mode;        /* 0 only (cluster: see sf_cluster_flow_rule) */
-    uint32_t ref_resource;
+    int32_t  cluster_mode;        /* FlowRule.clusterMode                      */
+    uint32_t ref_resource;        /* RELATE: resource id; CHAIN: context id    */
+    uint32_t limit_app;           /* SF_APP_DEFAULT (also a blank limitApp), SF_APP_OTHER, or an origin id */
+    int32_t  cluster_fallback;    /* ClusterFlowConfig.fallbackToLocalWhenFail */
 } sf_flow_rule;
 
 /* Param value identity = Java equals(): (type tag, 64-bit payload); strings
@@ -197,6 +230,12 @@ typedef struct sf_event_batch {
     const uint8_t*  elem_tag;     /* [n_elems]                                 */
     const uint64_t* elem_bits;    /* [n_elems]                                 */
     uint32_t        n_elems;
+    /* Context of each event (ContextUtil.enter(name, origin)): origin id
+     * (SF_ORIGIN_NONE = "") and context-name id; an EXIT carries its entry's.
+     * NULL: no origin / context 0 for every event.  Read only for resources
+     * whose flow rules select an origin or context node (sf_flow_rule).     */
+    const uint32_t* origin;       /* [n] or NULL                               */
+    const uint32_t* context;      /* [n] or NULL                               */
 } sf_event_batch;
 
 /* ---- verdicts ---------------------------------------------------------- */
@@ -479,6 +518,15 @@ int  sf_cluster_sum(sf_engine* e, int64_t flow_id, int event, int64_t now_ms, in
 int  sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out);
 int  sf_read_entry_node(sf_engine* e, sf_node_state* out);
 int  sf_read_rule_state(sf_engine* e, uint32_t rule_index, sf_rule_state* out);
+/* The origin node of (resource, origin) (ClusterNode.getOrCreateOriginNode,
+ * ClusterNode.java:101-120) and the DefaultNode of (context, resource)
+ * (NodeSelectorSlot), for the resources whose rules read them.  The engine
+ * keeps an origin node while the resource has a DIRECT rule with a limit_app
+ * other than "default", a context node while it has a CHAIN rule naming that
+ * context (statistics start when such a rule is loaded: DESIGN.md §2
+ * divergences); SF_ERR_INVALID for a node it does not keep. */
+int  sf_read_origin_node(sf_engine* e, uint32_t resource, uint32_t origin, sf_node_state* out);
+int  sf_read_context_node(sf_engine* e, uint32_t context, uint32_t resource, sf_node_state* out);
 int  sf_snapshot(sf_engine* e, int64_t now_ms, sf_metric_row* out, uint32_t cap, uint32_t* n_out);
 
 /* metrics.log (MetricTimerListener -> MetricWriter) ------------------------

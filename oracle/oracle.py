@@ -142,6 +142,9 @@ def _declare(L):
     f("so_set_system_status", C.c_int, P, D, D)
     f("so_submit", C.c_int, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
     f("so_read_node", C.c_int, P, U32, C.POINTER(abi.sf_node_state))
+    f("so_read_origin_node", C.c_int, P, U32, U32, C.POINTER(abi.sf_node_state))
+    f("so_read_context_node", C.c_int, P, U32, U32, C.POINTER(abi.sf_node_state))
+    f("so_select_node", C.c_int, P, U32, U32, U32)
     f("so_read_entry_node", C.c_int, P, C.POINTER(abi.sf_node_state))
     f("so_system_plan", C.c_int, P, C.POINTER(abi.sf_event_batch), P, U32, C.POINTER(U32), P)
     f("so_submit_forced", C.c_int, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts), P)
@@ -535,6 +538,26 @@ class OracleEngine:
         st = abi.sf_node_state()
         assert lib().so_read_node(self.h, res, C.byref(st)) == 0
         return st
+
+    def read_origin_node(self, res, origin):
+        st = abi.sf_node_state()
+        rc = lib().so_read_origin_node(self.h, res, origin, C.byref(st))
+        if rc:
+            raise KeyError((res, origin))
+        return st
+
+    def read_context_node(self, context, res):
+        st = abi.sf_node_state()
+        rc = lib().so_read_context_node(self.h, context, res, C.byref(st))
+        if rc:
+            raise KeyError((context, res))
+        return st
+
+    # FlowRuleChecker.selectNodeByRequesterAndStrategy of a loaded rule (SEL_*)
+    SEL_NONE, SEL_CLUSTER, SEL_ORIGIN, SEL_CONTEXT, SEL_REF = range(5)
+
+    def select_node(self, rule_index, origin=abi.ORIGIN_NONE, context=0):
+        return lib().so_select_node(self.h, rule_index, origin, context)
 
     def read_entry_node(self):
         st = abi.sf_node_state()

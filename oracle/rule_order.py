@@ -152,6 +152,8 @@ def valid_flow_rule(r) -> bool:
     if not (r.count >= 0) or r.grade < 0 or r.strategy < 0 or r.control_behavior < 0:
         return False
     if r.grade == 1:                               # FLOW_GRADE_QPS
+        if r.strategy in (1, 2) and r.ref_resource == 0xFFFFFFFF:   # checkStrategyField: blank refResource
+            return False
         cb = r.control_behavior
         if cb == 1:
             return r.warm_up_period_sec > 0

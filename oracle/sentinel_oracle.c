@@ -1024,7 +1024,11 @@ int so_rl_try_pass(so_request_limiter* l) {                                   /*
 typedef struct {
     sf_flow_rule rule;
     so_controller* ctrl;              /* FlowRuleUtil.generateRater :132-152 */
+    int64_t ref_local;                /* RELATE: refResource's local id (-1: never a ClusterNode) */
 } flow_rule_rt;
+
+/* a StatisticNode keyed by an origin or a context name id */
+typedef struct { uint32_t id; so_node* node; } keyed_node;
 
 typedef struct {
     sf_param_rule rule;               /* param_idx mutated by applyRealParamIdx */
@@ -1036,6 +1040,11 @@ typedef struct {
     int* param_rules; int n_param;
     so_param_metric* pm;              /* ParameterMetricStorage entry          */
     int* cbs; int n_cb;               /* circuit breakers (indices into e->cb, rule list order) */
+    /* ClusterNode.originCountMap (ClusterNode.java:101-120) and the resource's
+     * DefaultNodes by context name (NodeSelectorSlot), kept for the resources
+     * whose rules read them (the engine's set, sentinel_flow.h) */
+    keyed_node* onodes; int n_on;
+    keyed_node* dnodes; int n_dn;
 } res_rt;
 
 /* One CircuitBreaker (DegradeRuleManager.newCircuitBreakerFrom, :206-219) with
@@ -1099,6 +1108,13 @@ so_engine* so_create(const sf_config* cfg) {
     e->max_rt = e->max_thread = INT64_MAX;
     return e;
 }
+static so_node* keyed_get(keyed_node** arr, int* n, uint32_t id, int create) {
+    for (int k = 0; k < *n; k++) if ((*arr)[k].id == id) return (*arr)[k].node;
+    if (!create) return NULL;
+    *arr = realloc(*arr, sizeof(keyed_node) * (size_t)(*n + 1));
+    (*arr)[*n].id = id; (*arr)[*n].node = so_node_new();
+    return (*arr)[(*n)++].node;
+}
 static void clear_flow(so_engine* e) {
     for (uint32_t i = 0; i < e->n_flow; i++) so_ctrl_free(e->flow[i].ctrl);
     free(e->flow); e->flow = NULL; e->n_flow = 0;
@@ -1117,7 +1133,12 @@ void so_destroy(so_engine* e) {
     for (uint32_t r = 0; e->res && r < e->n_res; r++) free(e->res[r].cbs);
     if (!e) return;
     clear_flow(e); clear_param(e);
-    for (uint32_t r = 0; r < e->n_res; r++) so_node_free(e->res[r].node);
+    for (uint32_t r = 0; r < e->n_res; r++) {
+        so_node_free(e->res[r].node);
+        for (int k = 0; k < e->res[r].n_on; k++) so_node_free(e->res[r].onodes[k].node);
+        for (int k = 0; k < e->res[r].n_dn; k++) so_node_free(e->res[r].dnodes[k].node);
+        free(e->res[r].onodes); free(e->res[r].dnodes);
+    }
     free(e->res);
     so_node_free(e->entry_node);
     free(e->entry_blocked);
@@ -1145,6 +1166,10 @@ int so_load_flow_rules(so_engine* e, const sf_flow_rule* rules, uint32_t n) {
         if (!local_id(e, r->resource, &l)) return SF_ERR_INVALID;
         /* FlowRuleUtil.isValidRule :170-185 + checkControlBehaviorField :233-246 */
         int valid = r->count >= 0 && r->grade >= 0 && r->strategy >= 0 && r->control_behavior >= 0;
+        /* checkStrategyField :236-241 (QPS grade only) */
+        if (valid && r->grade == SF_GRADE_QPS && (r->strategy == SF_STRATEGY_RELATE || r->strategy == SF_STRATEGY_CHAIN) &&
+            r->ref_resource == SF_REF_NONE)
+            valid = 0;
         if (valid && r->grade == SF_GRADE_QPS) {
             if (r->control_behavior == SF_BEHAVIOR_WARM_UP) valid = r->warm_up_period_sec > 0;
             else if (r->control_behavior == SF_BEHAVIOR_RATE_LIMITER) valid = r->max_queueing_time_ms > 0;
@@ -1152,9 +1177,13 @@ int so_load_flow_rules(so_engine* e, const sf_flow_rule* rules, uint32_t n) {
                 valid = r->warm_up_period_sec > 0 && r->max_queueing_time_ms > 0;
         } else if (valid && r->grade != SF_GRADE_THREAD) valid = 0;
         if (!valid) continue;
-        if (r->strategy != SF_STRATEGY_DIRECT || r->cluster_mode) return SF_ERR_UNSUPPORTED;
         flow_rule_rt* f = &e->flow[e->n_flow];
         f->rule = *r;
+        f->ref_local = -1;
+        if (r->strategy == SF_STRATEGY_RELATE && r->ref_resource != SF_REF_NONE) {
+            if (r->ref_resource % e->cfg.shard_count != e->cfg.shard_index) return SF_ERR_UNSUPPORTED;
+            if (r->ref_resource / e->cfg.shard_count < e->n_res) f->ref_local = r->ref_resource / e->cfg.shard_count;
+        }
         /* generateRater :132-152 */
         if (r->grade == SF_GRADE_QPS && r->control_behavior == SF_BEHAVIOR_WARM_UP)
             f->ctrl = so_ctrl_warm_up(r->count, r->warm_up_period_sec, e->cfg.cold_factor);
@@ -1400,6 +1429,37 @@ static void pm_thread_event(so_param_metric* pm, const sf_event_batch* in, uint3
     }
 }
 
+/* FlowRuleManager.isOtherOrigin (FlowRuleManager.java:132-148): "" is never other */
+static int is_other_origin(so_engine* e, const res_rt* rr, uint32_t origin) {
+    if (origin == SF_ORIGIN_NONE) return 0;
+    for (int k = 0; k < rr->n_flow; k++)
+        if (e->flow[rr->flow_rules[k]].rule.limit_app == origin) return 0;
+    return 1;
+}
+/* FlowRuleChecker.selectReferenceNode (:93-115) */
+static int select_reference(const flow_rule_rt* f, uint32_t ctx) {
+    if (f->rule.ref_resource == SF_REF_NONE) return SO_SEL_NONE;           /* StringUtil.isEmpty */
+    if (f->rule.strategy == SF_STRATEGY_RELATE) return SO_SEL_REF;
+    if (f->rule.strategy == SF_STRATEGY_CHAIN) return f->rule.ref_resource == ctx ? SO_SEL_CONTEXT : SO_SEL_NONE;
+    return SO_SEL_NONE;
+}
+/* FlowRuleChecker.selectNodeByRequesterAndStrategy (:129-161); filterOrigin :117-120 */
+static int select_node(so_engine* e, const res_rt* rr, const flow_rule_rt* f, uint32_t origin, uint32_t ctx) {
+    const uint32_t app = f->rule.limit_app;
+    const int direct = f->rule.strategy == SF_STRATEGY_DIRECT;
+    if (origin != SF_ORIGIN_NONE && app == origin && origin != SF_APP_DEFAULT && origin != SF_APP_OTHER)
+        return direct ? SO_SEL_ORIGIN : select_reference(f, ctx);
+    if (app == SF_APP_DEFAULT) return direct ? SO_SEL_CLUSTER : select_reference(f, ctx);
+    if (app == SF_APP_OTHER && is_other_origin(e, rr, origin)) return direct ? SO_SEL_ORIGIN : select_reference(f, ctx);
+    return SO_SEL_NONE;
+}
+int so_select_node(so_engine* e, uint32_t rule_index, uint32_t origin, uint32_t context) {
+    if (rule_index >= e->n_flow) return -1;
+    uint32_t l = 0;
+    if (!local_id(e, e->flow[rule_index].rule.resource, &l)) return -1;
+    return select_node(e, &e->res[l], &e->flow[rule_index], origin, context);
+}
+
 int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     so_node* const en = e->forced ? NULL : e->entry_node;      /* the node-wide rounds update it themselves */
     apply_statics(&e->cfg);
@@ -1418,6 +1478,18 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         int is_in = (fl & SF_EV_IN) != 0;
         uint32_t na = nargs_of(in, i);
         uint8_t status = SF_V_PASS; int64_t wait = 0; int rule_idx = 0;
+        /* Context: origin and name (ContextUtil.enter); the origin node and the
+         * DefaultNode of (context, resource) are kept when a rule can read them */
+        const uint32_t origin = in->origin ? in->origin[i] : SF_ORIGIN_NONE;
+        const uint32_t ctx = in->context ? in->context[i] : 0u;
+        int want_on = 0, want_dn = 0;
+        for (int k = 0; k < rr->n_flow; k++) {
+            const sf_flow_rule* fr = &e->flow[rr->flow_rules[k]].rule;
+            if (fr->strategy == SF_STRATEGY_DIRECT && fr->limit_app != SF_APP_DEFAULT) want_on = 1;
+            if (fr->strategy == SF_STRATEGY_CHAIN && fr->ref_resource == ctx) want_dn = 1;
+        }
+        so_node* on = (want_on && origin != SF_ORIGIN_NONE) ? keyed_get(&rr->onodes, &rr->n_on, origin, 1) : NULL;
+        so_node* dn = want_dn ? keyed_get(&rr->dnodes, &rr->n_dn, ctx, 1) : NULL;
 
         if (fl & SF_EV_EXIT) {
             /* StatisticSlot.exit :134-165 */
@@ -1436,10 +1508,12 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
                 if (!rr->node) rr->node = so_node_new();
                 int64_t rt = g_now - create_ts;
                 int err = (fl & SF_EV_ERROR) != 0;
-                /* recordCompleteFor(node) :167-178 */
+                /* recordCompleteFor(DefaultNode -> ClusterNode), recordCompleteFor(originNode) :150-151, :167-178 */
+                if (dn) { so_node_add_rt_and_success(dn, rt, count); so_node_decrease_thread_num(dn); if (err) so_node_increase_exception_qps(dn, count); }
                 so_node_add_rt_and_success(rr->node, rt, count);
                 so_node_decrease_thread_num(rr->node);
                 if (err) so_node_increase_exception_qps(rr->node, count);
+                if (on) { so_node_add_rt_and_success(on, rt, count); so_node_decrease_thread_num(on); if (err) so_node_increase_exception_qps(on, count); }
                 if (is_in && en) {
                     so_node_add_rt_and_success(en, rt, count);
                     so_node_decrease_thread_num(en);
@@ -1497,8 +1571,20 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
             for (int k = 0; k < rr->n_flow; k++) {
                 flow_rule_rt* f = &e->flow[rr->flow_rules[k]];
                 int64_t w = 0; int pw = 0;
-                /* canPassCheck -> passLocalCheck -> selectNodeByRequesterAndStrategy (default, DIRECT) */
-                int ok = so_ctrl_can_pass(f->ctrl, rr->node, NULL, count, (fl & SF_EV_PRIO) != 0, &w, &pw);
+                /* canPassCheck :66-80: a cluster rule finds no TokenService (ClusterStateManager not
+                 * started, pickClusterService :195-203) -> fallbackToLocalOrPass :184-193 */
+                if (f->rule.cluster_mode && !f->rule.cluster_fallback) continue;
+                /* passLocalCheck :82-91 -> selectNodeByRequesterAndStrategy; no node -> pass */
+                so_node* sel = NULL;
+                switch (select_node(e, rr, f, origin, ctx)) {
+                case SO_SEL_CLUSTER: sel = rr->node; break;
+                case SO_SEL_ORIGIN: sel = on; break;
+                case SO_SEL_CONTEXT: sel = dn; break;
+                case SO_SEL_REF: sel = f->ref_local >= 0 ? e->res[f->ref_local].node : NULL; break;  /* getClusterNode */
+                default: break;
+                }
+                if (!sel) continue;
+                int ok = so_ctrl_can_pass(f->ctrl, sel, NULL, count, (fl & SF_EV_PRIO) != 0, &w, &pw);
                 if (pw) { prio_wait = 1; wait += w; rule_idx = k; break; }  /* PriorityWaitException */
                 if (!ok) { blocked = 1; status = SF_V_BLOCK_FLOW; rule_idx = k; break; }
                 wait += w;
@@ -1510,18 +1596,24 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
             const int k = cb_check(e, rr);
             if (k >= 0) { blocked = 1; status = SF_V_BLOCK_DEGRADE; rule_idx = k; }
         }
-        /* StatisticSlot.entry accounting :64-123 */
+        /* StatisticSlot.entry accounting :64-123 (DefaultNode -> ClusterNode, origin node) */
         if (blocked) {
+            if (dn) so_node_increase_block_qps(dn, count);
             so_node_increase_block_qps(rr->node, count);
+            if (on) so_node_increase_block_qps(on, count);
             if (is_in && en) so_node_increase_block_qps(en, count);
         } else if (prio_wait) {
+            if (dn) so_node_increase_thread_num(dn);
             so_node_increase_thread_num(rr->node);
+            if (on) so_node_increase_thread_num(on);
             if (is_in && en) so_node_increase_thread_num(en);
             if (rr->pm) pm_thread_event(rr->pm, in, i, na, 1);
             status = SF_V_PRIORITY_WAIT;
         } else {
+            if (dn) { so_node_increase_thread_num(dn); so_node_add_pass_request(dn, count); }
             so_node_increase_thread_num(rr->node);
             so_node_add_pass_request(rr->node, count);
+            if (on) { so_node_increase_thread_num(on); so_node_add_pass_request(on, count); }
             if (is_in && en) { so_node_increase_thread_num(en); so_node_add_pass_request(en, count); }
             if (rr->pm) pm_thread_event(rr->pm, in, i, na, 1);
             status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS;
@@ -1594,6 +1686,22 @@ int so_read_node(so_engine* e, uint32_t res, sf_node_state* out) {
     return SF_OK;
 }
 int so_read_entry_node(so_engine* e, sf_node_state* out) { so_node_read(e->entry_node, out); return SF_OK; }
+int so_read_origin_node(so_engine* e, uint32_t res, uint32_t origin, sf_node_state* out) {
+    uint32_t l;
+    if (!local_id(e, res, &l)) return SF_ERR_INVALID;
+    so_node* n = keyed_get(&e->res[l].onodes, &e->res[l].n_on, origin, 0);
+    if (!n) return SF_ERR_INVALID;
+    so_node_read(n, out);
+    return SF_OK;
+}
+int so_read_context_node(so_engine* e, uint32_t context, uint32_t res, sf_node_state* out) {
+    uint32_t l;
+    if (!local_id(e, res, &l)) return SF_ERR_INVALID;
+    so_node* n = keyed_get(&e->res[l].dnodes, &e->res[l].n_dn, context, 0);
+    if (!n) return SF_ERR_INVALID;
+    so_node_read(n, out);
+    return SF_OK;
+}
 int so_read_rule_state(so_engine* e, uint32_t idx, sf_rule_state* out) {
     if (idx >= e->n_flow) return SF_ERR_INVALID;
     so_ctrl_state(e->flow[idx].ctrl, out);

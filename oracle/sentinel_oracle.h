@@ -197,6 +197,12 @@ int  so_entry_node_add(so_engine* e, const sf_event_batch* in, const uint8_t* st
 int  so_load_degrade_rules(so_engine* e, const sf_degrade_rule* rules, uint32_t n, uint32_t* n_loaded);
 int  so_read_breaker(so_engine* e, uint32_t k, sf_breaker_state* out);
 int  so_read_node(so_engine* e, uint32_t res, sf_node_state* out);
+int  so_read_origin_node(so_engine* e, uint32_t res, uint32_t origin, sf_node_state* out);
+int  so_read_context_node(so_engine* e, uint32_t context, uint32_t res, sf_node_state* out);
+/* FlowRuleChecker.selectNodeByRequesterAndStrategy of loaded rule rule_index
+ * for a Context (origin, name): SO_SEL_* (-1: bad index). */
+enum { SO_SEL_NONE = 0, SO_SEL_CLUSTER = 1, SO_SEL_ORIGIN = 2, SO_SEL_CONTEXT = 3, SO_SEL_REF = 4 };
+int  so_select_node(so_engine* e, uint32_t rule_index, uint32_t origin, uint32_t context);
 int  so_read_entry_node(so_engine* e, sf_node_state* out);
 int  so_read_rule_state(so_engine* e, uint32_t rule_index, sf_rule_state* out);
 int  so_read_param(so_engine* e, uint32_t param_rule_index, uint8_t tag, uint64_t bits,

@@ -59,6 +59,7 @@ class sf_config(C.Structure):
         ("cluster_sample_count", C.c_int32), ("cluster_interval_ms", C.c_int32),
         ("exceed_count", C.c_double), ("max_occupy_ratio", C.c_double),
         ("max_flow_ids", C.c_uint32), ("heavy_min_events", C.c_uint32),
+        ("aux_capacity", C.c_uint32), ("pad", C.c_uint32),
     ]
 
 
@@ -68,10 +69,16 @@ def default_config(**kw) -> sf_config:
                     statistic_max_rt=5000, max_resources=1024, max_batch=1 << 20,
                     param_capacity=1 << 16, shard_count=1, shard_index=0, device=0,
                     cluster_sample_count=10, cluster_interval_ms=1000, exceed_count=1.0,
-                    max_occupy_ratio=1.0, max_flow_ids=1024, heavy_min_events=0)
+                    max_occupy_ratio=1.0, max_flow_ids=1024, heavy_min_events=0, aux_capacity=4096)
     for k, v in kw.items():
         setattr(cfg, k, v)
     return cfg
+
+
+# origin / limitApp ids (sentinel_flow.h): 0 "default", 1 "other", >= 2 an origin name, NONE = ""
+APP_DEFAULT, APP_OTHER = 0, 1
+ORIGIN_NONE = 0xFFFFFFFF
+REF_NONE = 0xFFFFFFFF
 
 
 class sf_flow_rule(C.Structure):
@@ -80,6 +87,7 @@ class sf_flow_rule(C.Structure):
         ("strategy", C.c_int32), ("control_behavior", C.c_int32),
         ("warm_up_period_sec", C.c_int32), ("max_queueing_time_ms", C.c_int32),
         ("cluster_mode", C.c_int32), ("ref_resource", C.c_uint32),
+        ("limit_app", C.c_uint32), ("cluster_fallback", C.c_int32),
     ]
 
 
@@ -118,7 +126,7 @@ class sf_event_batch(C.Structure):
         ("arg_slots", C.c_uint32), ("n_args", C.c_void_p),
         ("arg_tag", C.c_void_p), ("arg_bits", C.c_void_p),
         ("arg_elem_off", C.c_void_p), ("elem_tag", C.c_void_p), ("elem_bits", C.c_void_p),
-        ("n_elems", C.c_uint32),
+        ("n_elems", C.c_uint32), ("origin", C.c_void_p), ("context", C.c_void_p),
     ]
 
 
@@ -230,7 +238,8 @@ class HostBatch:
     """
 
     def __init__(self, res_id, ts_ms, count, flags, entry_ref=None, create_ts=None,
-                 arg_tag=None, arg_bits=None, n_args=None, elem_off=None, elem_tag=None, elem_bits=None):
+                 arg_tag=None, arg_bits=None, n_args=None, elem_off=None, elem_tag=None, elem_bits=None,
+                 origin=None, context=None):
         self.res_id = np.ascontiguousarray(res_id, dtype=np.uint32)
         self.ts_ms = np.ascontiguousarray(ts_ms, dtype=np.int64)
         self.count = np.ascontiguousarray(count, dtype=np.int32)
@@ -257,6 +266,15 @@ class HostBatch:
         if self.elem_off is not None:
             assert arg_tag is not None and self.elem_off.shape == (arg_tag.shape[0] * n + 1,)
             assert self.elem_tag.shape == self.elem_bits.shape == (int(self.elem_off[-1]),)
+        # Context origin / name ids per event (ORIGIN_NONE = ""); None: no origin, context 0
+        self.origin = None if origin is None else np.ascontiguousarray(origin, dtype=np.uint32)
+        self.context = None if context is None else np.ascontiguousarray(context, dtype=np.uint32)
+        assert self.origin is None or self.origin.shape == (n,)
+        assert self.context is None or self.context.shape == (n,)
+
+    def _take_ctx(self, sel):
+        return (None if self.origin is None else self.origin[sel].copy(),
+                None if self.context is None else self.context[sel].copy())
 
     @staticmethod
     def collections(slots, n, values):
@@ -310,8 +328,9 @@ class HostBatch:
             er[er >= 0] = pos[er[er >= 0]]
             ct = None if self.create_ts is None else self.create_ts[sel].copy()
         at, ab, na, eo, et, eb = self._take_args(sel)
+        og, cx = self._take_ctx(sel)
         return HostBatch(self.res_id[sel], self.ts_ms[sel], self.count[sel], self.flags[sel], er, ct, at, ab, na,
-                         eo, et, eb)
+                         eo, et, eb, og, cx)
 
     def subset(self, lo: int, hi: int) -> "HostBatch":
         """Contiguous slice [lo, hi); entry_ref indices are rebased (refs before lo become -1)."""
@@ -325,8 +344,9 @@ class HostBatch:
             er[prior] = -1
             er[er >= lo] -= lo
         at, ab, na, eo, et, eb = self._take_args(np.arange(lo, hi))
+        og, cx = self._take_ctx(np.arange(lo, hi))
         return HostBatch(self.res_id[lo:hi], self.ts_ms[lo:hi], self.count[lo:hi], self.flags[lo:hi],
-                         er, ct, at, ab, na, eo, et, eb)
+                         er, ct, at, ab, na, eo, et, eb, og, cx)
 
     def c_struct(self) -> sf_event_batch:
         b = sf_event_batch()
@@ -345,6 +365,7 @@ class HostBatch:
         if self.elem_off is not None:
             b.arg_elem_off, b.elem_tag, b.elem_bits = _ptr(self.elem_off), _ptr(self.elem_tag), _ptr(self.elem_bits)
             b.n_elems = int(self.elem_off[-1])
+        b.origin, b.context = _ptr(self.origin), _ptr(self.context)
         return b
 
 

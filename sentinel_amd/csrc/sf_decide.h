@@ -541,6 +541,10 @@ struct SegIO {          // sorted-order batch arrays
     uint8_t* v_status; int32_t* v_wait; uint16_t* v_rule;     // sorted order (read back by exits)
     const uint32_t* perm;                                       // sorted -> submission index, or null
     uint8_t* o_status; int32_t* o_wait; uint16_t* o_rule;       // the caller's verdicts (submission order)
+    // xflow walk (sf_xflow.h): resource id, origin and context of each event in
+    // submission order (read through perm; origin / context may be null)
+    const uint32_t* ev_res; const uint32_t* ev_origin; const uint32_t* ev_ctx;
+    uint32_t shard_count;
 };
 
 // final verdict of sorted event j, straight into the caller's arrays
@@ -763,10 +767,14 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
 }
 
 // ============================================================ rule tables (host side)
-// FlowRuleUtil.isValidRule (FlowRuleUtil.java:170-185) + checkControlBehaviorField (:233-246)
+// FlowRuleUtil.isValidRule (FlowRuleUtil.java:170-185) + checkStrategyField (:236-241)
+// + checkControlBehaviorField (:243-254); a cluster rule's ClusterFlowConfig is
+// taken to be valid (checkClusterField :210-230: the ABI does not carry it)
 inline bool valid_flow_rule(const sf_flow_rule& r) {
     if (!(r.count >= 0) || r.grade < 0 || r.strategy < 0 || r.control_behavior < 0) return false;
     if (r.grade == SF_GRADE_QPS) {
+        if ((r.strategy == SF_STRATEGY_RELATE || r.strategy == SF_STRATEGY_CHAIN) && r.ref_resource == SF_REF_NONE)
+            return false;
         switch (r.control_behavior) {
         case SF_BEHAVIOR_WARM_UP: return r.warm_up_period_sec > 0;
         case SF_BEHAVIOR_RATE_LIMITER: return r.max_queueing_time_ms > 0;
@@ -777,10 +785,14 @@ inline bool valid_flow_rule(const sf_flow_rule& r) {
     return r.grade == SF_GRADE_THREAD;
 }
 // FlowRuleUtil.generateRater (:132-152) + WarmUpController.construct (WarmUpController.java:113-139)
-inline DevRule make_dev_rule(const sf_flow_rule& r, int cold_factor, int host_index) {
+// ref_local: RELATE's referenced resource as a local id (XNONE: none); CHAIN keeps the context id
+inline DevRule make_dev_rule(const sf_flow_rule& r, int cold_factor, int host_index, uint32_t ref_local = XNONE) {
     DevRule d{};
     d.grade = r.grade; d.count = r.count; d.max_queue_ms = r.max_queueing_time_ms;
     d.cold_factor = cold_factor; d.host_index = host_index;
+    d.strategy = r.strategy; d.limit_app = r.limit_app;
+    d.ref = r.strategy == SF_STRATEGY_RELATE ? ref_local : r.ref_resource;
+    d.always_pass = (r.cluster_mode && !r.cluster_fallback) ? 1 : 0;
     d.kind = CT_DEFAULT;
     if (r.grade == SF_GRADE_QPS) {
         if (r.control_behavior == SF_BEHAVIOR_WARM_UP) d.kind = CT_WARM_UP;

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "sf_decide.h"
+#include "sf_xflow.h"
 #include "sf_system.h"
 #include "sf_token.h"
 #include "sf_wire.h"
@@ -102,6 +103,8 @@ struct sf_engine {
     std::vector<uint32_t> dg_pos;         // breaker index (load order) -> CSR position
     std::vector<sf_degrade_rule> dg_rules;   // the valid rules of the loaded breakers (load order)
     void* dg_stage = nullptr; size_t dg_stage_bytes = 0;
+    // xflow walk (sf_xflow.h): group keys and the origin / context node pool
+    uint32_t* xmap_buf = nullptr;
 };
 
 static void free_tok_work(TokWork& w) {
@@ -122,7 +125,7 @@ void sf_config_default(sf_config* c) {
     c->statistic_max_rt = 5000; c->max_resources = 1024; c->max_batch = 1u << 20;
     c->param_capacity = 1u << 16; c->shard_count = 1; c->shard_index = 0; c->device = 0;
     c->cluster_sample_count = 10; c->cluster_interval_ms = 1000; c->exceed_count = 1.0;
-    c->max_occupy_ratio = 1.0; c->max_flow_ids = 1024;
+    c->max_occupy_ratio = 1.0; c->max_flow_ids = 1024; c->aux_capacity = 4096;
 }
 
 static int dalloc(void** p, size_t bytes) {
@@ -174,6 +177,9 @@ void sf_destroy(sf_engine* e) {
                      e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
                      e->dgw.err, e->dg_stage, e->dgw.heavy, e->dgw.n_heavy, e->dgw.sev, e->dgw.inv};
     for (void* p : dptrs) if (p) hipFree(p);
+    void* xptrs[] = {e->xmap_buf, e->st.xtab, e->st.ax_second, e->st.ax_borrow, e->st.ax_minute, e->st.ax_threads,
+                     e->st.ax_count};
+    for (void* p : xptrs) if (p) hipFree(p);
     if (e->comm) ncclCommDestroy(e->comm);
     free_tok_work(e->tw);
     for (auto& a : e->evs) for (auto& x : a) if (x) hipEventDestroy(x);
@@ -298,6 +304,7 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     DevState& st = e->st;
     st.S = c.sample_count; st.wl = c.interval_ms / c.sample_count; st.interval = c.interval_ms;
     st.occupy_timeout = c.occupy_timeout_ms; st.max_rt = c.statistic_max_rt; st.R = e->R;
+    st.shard_count = c.shard_count;
     const size_t R = e->R, S = c.sample_count;
     DALLOC(st.second, R * S * sizeof(Bucket));
     DALLOC(st.borrow, R * S * sizeof(Borrow));
@@ -399,19 +406,55 @@ static int drain(sf_engine* e) {
     return SF_OK;
 }
 
+// The origin / context node pool and its index table (sf_xflow.h), allocated
+// with the first rule that reads such nodes; the nodes live as long as the
+// engine (ClusterNode.originCountMap / NodeSelectorSlot maps are never pruned).
+static int ensure_aux(sf_engine* e) {
+    DevState& st = e->st;
+    if (st.ax_second) return SF_OK;
+    const uint32_t cap = e->cfg.aux_capacity ? e->cfg.aux_capacity : 4096;
+    const size_t S = st.S;
+    uint64_t tcap = 16;
+    while (tcap < 2ull * cap) tcap <<= 1;
+    HIP_TRY(hipMalloc((void**)&st.ax_second, (size_t)cap * S * sizeof(Bucket)));
+    HIP_TRY(hipMalloc((void**)&st.ax_borrow, (size_t)cap * S * sizeof(Borrow)));
+    HIP_TRY(hipMalloc((void**)&st.ax_minute, (size_t)cap * MINUTE * sizeof(Bucket)));
+    HIP_TRY(hipMalloc((void**)&st.ax_threads, (size_t)cap * sizeof(int64_t)));
+    HIP_TRY(hipMalloc((void**)&st.ax_count, sizeof(uint32_t)));
+    HIP_TRY(hipMalloc((void**)&st.xtab, tcap * sizeof(ParamSlot)));
+    HIP_TRY(hipMemsetAsync(st.ax_count, 0, sizeof(uint32_t), e->stream));
+    HIP_TRY(hipMemsetAsync(st.xtab, 0, tcap * sizeof(ParamSlot), e->stream));
+    st.xcap_mask = tcap - 1;
+    st.ax_cap = cap;
+    DevState pool = st;                    // fresh nodes: the resource-row initialiser on the pool
+    pool.second = st.ax_second; pool.borrow = st.ax_borrow; pool.minute = st.ax_minute;
+    pool.threads = st.ax_threads; pool.R = cap;
+    const hipError_t le = launch_init_state(pool, e->stream);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("aux init: ") + hipGetErrorString(le));
+    return SF_OK;
+}
+
 int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
     if (!e || (n && !rules)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     { const int rc = drain(e); if (rc) return rc; }   // pending batches were sorted under the old rules
     std::vector<uint32_t> counts(e->R + 1, 0);
     std::vector<const sf_flow_rule*> valid;
-    std::vector<uint32_t> valid_local;
+    std::vector<uint32_t> valid_local, valid_ref;
     for (uint32_t i = 0; i < n; i++) {
         uint32_t l;
         if (!local_of(e, rules[i].resource, &l)) return fail(SF_ERR_INVALID, "rule resource outside this shard");
         if (!valid_flow_rule(rules[i])) continue;
-        if (rules[i].strategy != SF_STRATEGY_DIRECT || rules[i].cluster_mode)
-            return fail(SF_ERR_UNSUPPORTED, "only DIRECT, non-cluster flow rules run in the engine");
+        uint32_t ref = XNONE;
+        if (rules[i].strategy == SF_STRATEGY_RELATE && rules[i].ref_resource != SF_REF_NONE) {
+            // RELATE reads refResource's ClusterNode: it must be decided by the same
+            // engine (co-locate the pair); an id beyond this shard's
+            // resources never gets a node (the rule passes)
+            if (rules[i].ref_resource % e->cfg.shard_count != e->cfg.shard_index)
+                return fail(SF_ERR_UNSUPPORTED, "RELATE refResource on another shard: co-locate it with the resource");
+            const uint32_t rl = rules[i].ref_resource / e->cfg.shard_count;
+            if (rl < e->R) ref = rl;
+        }
         if (rules[i].control_behavior != SF_BEHAVIOR_DEFAULT && rules[i].grade == SF_GRADE_QPS &&
             e->cfg.cold_factor <= 1 &&
             (rules[i].control_behavior == SF_BEHAVIOR_WARM_UP || rules[i].control_behavior == SF_BEHAVIOR_WARM_UP_RATE_LIMITER))
@@ -420,6 +463,7 @@ int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
             return fail(SF_ERR_UNSUPPORTED, "more than SF_MAX_RULES_PER_RESOURCE rules on one resource");
         valid.push_back(&rules[i]);
         valid_local.push_back(l);
+        valid_ref.push_back(ref);
     }
     std::vector<uint32_t> off(e->R + 1, 0);
     for (uint32_t r = 0; r < e->R; r++) off[r + 1] = off[r] + counts[r];
@@ -431,9 +475,18 @@ int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
         const sf_flow_rule& r = *valid[k];
         uint32_t pos = fill[valid_local[k]]++;
         e->flow_pos[k] = pos;
-        DevRule d = make_dev_rule(r, e->cfg.cold_factor, (int32_t)k);
+        DevRule d = make_dev_rule(r, e->cfg.cold_factor, (int32_t)k, valid_ref[k]);
         dr[pos] = d;
         ds[pos] = fresh_rule_state();
+    }
+    std::vector<uint32_t> xmap;
+    const bool xflow = build_xmap(dr.data(), off.data(), e->R, xmap);
+    if (xflow) {
+        const int rc = ensure_aux(e);
+        if (rc) return rc;
+        if (!e->xmap_buf) HIP_TRY(hipMalloc((void**)&e->xmap_buf, (size_t)e->R * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpyAsync(e->xmap_buf, xmap.data(), (size_t)e->R * sizeof(uint32_t), hipMemcpyHostToDevice,
+                               e->stream));
     }
     e->n_flow = (uint32_t)valid.size();
     if (e->st.rules) { hipFree((void*)e->st.rules); e->st.rules = nullptr; }
@@ -446,6 +499,7 @@ int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
     }
     HIP_TRY(hipMemcpyAsync((void*)e->st.rule_off, off.data(), off.size() * 4, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    e->st.xmap = xflow ? e->xmap_buf : nullptr;
     return SF_OK;
 }
 
@@ -574,6 +628,8 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         size_t o_eo = need; need += coll ? align_up(((size_t)n * in->arg_slots + 1) * 4) : 0;
         size_t o_et = need; need += coll ? align_up((size_t)in->n_elems) : 0;
         size_t o_eb = need; need += coll ? align_up((size_t)in->n_elems * 8) : 0;
+        size_t o_og = need; need += in->origin ? align_up((size_t)n * 4) : 0;
+        size_t o_cx = need; need += in->context ? align_up((size_t)n * 4) : 0;
         if (need > e->stage_in_bytes) {
             if (e->stage_in) hipFree(e->stage_in);
             e->stage_in = nullptr;
@@ -600,11 +656,14 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
             b.etag = (const uint8_t*)up(o_et, in->elem_tag, in->n_elems);
             b.ebits = (const uint64_t*)up(o_eb, in->elem_bits, (size_t)in->n_elems * 8);
         }
+        b.origin = (const uint32_t*)up(o_og, in->origin, (size_t)n * 4);
+        b.ctx = (const uint32_t*)up(o_cx, in->context, (size_t)n * 4);
     } else {
         b.res = in->res_id; b.ts = in->ts_ms; b.cnt = in->count; b.flags = in->flags;
         b.eref = in->entry_ref; b.cts = in->entry_ref ? in->create_ts : nullptr;
         b.nargs = in->n_args; b.atag = in->arg_tag; b.abits = in->arg_bits;
         b.aoff = in->arg_elem_off; b.etag = in->elem_tag; b.ebits = in->elem_bits;
+        b.origin = in->origin; b.ctx = in->context;
     }
     DevVerdicts dv{};
     if (out->mem == SF_MEM_HOST) {
@@ -660,6 +719,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
             v.eref = b.eref ? b.eref + p : nullptr; v.cts = b.cts ? b.cts + p : nullptr;
             v.nargs = b.nargs ? b.nargs + p : nullptr;
             v.atag = b.atag ? b.atag + p : nullptr; v.abits = b.abits ? b.abits + p : nullptr;
+            v.origin = b.origin ? b.origin + p : nullptr; v.ctx = b.ctx ? b.ctx + p : nullptr;
             v.sys = e->sys_mask + p; v.vprev = dv.status + p;
             DevVerdicts dvv{dv.status + p, dv.wait ? dv.wait + p : nullptr, dv.rule ? dv.rule + p : nullptr};
             le = launch_sort(stl, w, v, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s, e->evs[slot], false);
@@ -853,19 +913,17 @@ static void to_abi_bucket(const Bucket& d, sf_bucket* o) {
     if (d.ws == WS_NONE) { o->pass = o->block = o->exception = o->success = o->rt = o->occupied_pass = o->min_rt = 0; }
 }
 
-int sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out) {
-    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
-    uint32_t l;
-    if (!local_of(e, resource, &l)) return fail(SF_ERR_INVALID, "resource outside this shard");
-    std::lock_guard<std::mutex> lk(e->mu);
+// one node's rows (a resource row or an origin / context pool slot) -> sf_node_state
+static int read_rows(sf_engine* e, const Bucket* gsec, const Borrow* gbor, const Bucket* gmin, const int64_t* gthr,
+                     sf_node_state* out) {
     const int S = e->cfg.sample_count;
     std::vector<Bucket> sec(S), mins(MINUTE);
     std::vector<Borrow> bor(S);
     int64_t th = 0;
-    HIP_TRY(hipMemcpyAsync(sec.data(), e->st.second + (size_t)l * S, S * sizeof(Bucket), hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipMemcpyAsync(bor.data(), e->st.borrow + (size_t)l * S, S * sizeof(Borrow), hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipMemcpyAsync(mins.data(), e->st.minute + (size_t)l * MINUTE, MINUTE * sizeof(Bucket), hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipMemcpyAsync(&th, e->st.threads + l, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(sec.data(), gsec, S * sizeof(Bucket), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(bor.data(), gbor, S * sizeof(Borrow), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(mins.data(), gmin, MINUTE * sizeof(Bucket), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(&th, gthr, 8, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     std::memset(out, 0, sizeof *out);
     for (int i = 0; i < SF_MAX_SAMPLE_COUNT; i++) { out->second[i].window_start = SF_WS_ABSENT; out->borrow_ws[i] = SF_WS_ABSENT; }
@@ -877,6 +935,40 @@ int sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out) {
     for (int i = 0; i < MINUTE; i++) to_abi_bucket(mins[i], &out->minute[i]);
     out->cur_thread_num = th;
     return SF_OK;
+}
+
+int sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    uint32_t l;
+    if (!local_of(e, resource, &l)) return fail(SF_ERR_INVALID, "resource outside this shard");
+    std::lock_guard<std::mutex> lk(e->mu);
+    const NodeRows r = cluster_rows(e->st, l);
+    return read_rows(e, r.sec, r.bor, r.min, r.thr, out);
+}
+
+// origin / context node of local resource l (sf_xflow.h aux_get), looked up
+// in a host copy of the index table
+static int read_aux(sf_engine* e, uint32_t resource, uint32_t kind, uint32_t id, sf_node_state* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    uint32_t l;
+    if (!local_of(e, resource, &l)) return fail(SF_ERR_INVALID, "resource outside this shard");
+    std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }
+    if (!e->st.xtab) return fail(SF_ERR_INVALID, "no origin / context node is kept");
+    std::vector<ParamSlot> tab(e->st.xcap_mask + 1);
+    HIP_TRY(hipMemcpy(tab.data(), e->st.xtab, tab.size() * sizeof(ParamSlot), hipMemcpyDeviceToHost));
+    int32_t err = 0;
+    const ParamTable t{tab.data(), e->st.xcap_mask, &err};
+    const ParamSlot* s = t.find(pkey_hi(l, PK_AUX, kind, 0), id);
+    if (!s) return fail(SF_ERR_INVALID, "that origin / context node is not kept");
+    const NodeRows r = aux_rows(e->st, (uint32_t)s->a);
+    return read_rows(e, r.sec, r.bor, r.min, r.thr, out);
+}
+int sf_read_origin_node(sf_engine* e, uint32_t resource, uint32_t origin, sf_node_state* out) {
+    return read_aux(e, resource, AX_ORIGIN, origin, out);
+}
+int sf_read_context_node(sf_engine* e, uint32_t context, uint32_t resource, sf_node_state* out) {
+    return read_aux(e, resource, AX_CTX, context, out);
 }
 
 int sf_read_entry_node(sf_engine* e, sf_node_state* out) {

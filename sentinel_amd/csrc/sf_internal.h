@@ -32,14 +32,21 @@ struct Borrow {          // WindowWrap<MetricBucket> of FutureBucketLeapArray: o
 // Controller kinds (FlowRuleUtil.generateRater, FlowRuleUtil.java:132-152)
 enum : int32_t { CT_DEFAULT = 0, CT_WARM_UP = 1, CT_RATE_LIMITER = 2, CT_WARM_UP_RATE_LIMITER = 3 };
 
-struct DevRule {         // 48 B, constants precomputed at load (WarmUpController.construct :113-139)
+struct DevRule {         // 64 B, constants precomputed at load (WarmUpController.construct :113-139)
     int32_t kind, grade;
     double count;
     int32_t warning_token, max_token;
     double slope;
     int32_t cold_factor, max_queue_ms;
-    int32_t host_index, pad;
+    int32_t host_index, strategy;
+    // node selection (FlowRuleChecker.selectNodeByRequesterAndStrategy :129-161);
+    // rules other than limitApp "default" + DIRECT run on the xflow walk (sf_xflow.h)
+    uint32_t limit_app;            // SF_APP_DEFAULT / SF_APP_OTHER / origin id
+    uint32_t ref;                  // RELATE: local resource id (XNONE: never a node); CHAIN: context id
+    int32_t always_pass;           // cluster rule without fallback (no token service in the process)
+    int32_t pad;
 };
+constexpr uint32_t XNONE = 0xFFFFFFFFu;
 struct DevRuleState {    // AtomicLong fields of the controllers
     int64_t stored_tokens, last_filled, latest_passed, pad;
 };
@@ -63,6 +70,7 @@ struct DevState {
     int32_t S, wl, interval, occupy_timeout;
     int64_t max_rt;
     uint32_t R;
+    uint32_t shard_count;          // resource sharding (local id = res / shard_count)
     Bucket* second;
     Borrow* borrow;
     Bucket* minute;
@@ -86,6 +94,16 @@ struct DevState {
     const DevBreakerRule* dg_rules;
     sf_breaker_state* dg_state;
     uint32_t dg_n;
+    // xflow walk (sf_xflow.h): resources whose rules read an origin node, a
+    // context (DefaultNode) node or another resource's ClusterNode (RELATE),
+    // grouped by RELATE references.  xmap[l] = the group's key (its smallest
+    // member), XNONE for every other resource; null: no such rule loaded.
+    const uint32_t* xmap;
+    // origin / context nodes: index table (key (kind, resource, id) -> pool
+    // slot) and the node pool in the layout of the resource rows
+    ParamSlot* xtab; uint64_t xcap_mask;
+    Bucket* ax_second; Borrow* ax_borrow; Bucket* ax_minute; int64_t* ax_threads;
+    uint32_t* ax_count; uint32_t ax_cap;
 };
 
 // Constants.ENTRY_NODE (Constants.java:66): the ClusterNode of all inbound
@@ -197,6 +215,7 @@ struct DevBatch {
     uint32_t arg_slots; const uint8_t* nargs; const uint8_t* atag; const uint64_t* abits;
     uint32_t arg_stride;           // slot stride of atag / abits (the whole batch's n)
     const uint32_t* aoff; const uint8_t* etag; const uint64_t* ebits;   // collection elements (batch-wide CSR)
+    const uint32_t* origin; const uint32_t* ctx;   // context of each event (or null)
     int64_t base;                  // index of the view's first event in the batch (0: whole batch)
     const uint8_t* sys;            // planner verdicts of IN entries (SYS_NONE: none), or null
     const uint8_t* vprev;          // verdicts of the batch (decided before the view), or null

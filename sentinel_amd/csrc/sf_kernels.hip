@@ -25,6 +25,7 @@
 
 #include "sf_stream.h"
 #include "sf_system.h"
+#include "sf_xflow.h"
 
 namespace sf {
 
@@ -45,12 +46,16 @@ __global__ void k_init_state(DevState st, size_t n_sec, size_t n_min) {
 // a random gather from the submission-order arrays; an offset or count that
 // does not fit is read from the batch by k_unpack for that event only.
 __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t shard_count, uint32_t shard_index,
-                              uint32_t R, int32_t* err, const int64_t* last_ts) {
+                              uint32_t R, int32_t* err, const int64_t* last_ts, const uint32_t* xmap) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;
     uint32_t r = b.res[i];
     uint32_t l = r / shard_count;
     if (r % shard_count != shard_index || l >= R) { *err = SF_ERR_INVALID; l = 0; }
+    if (xmap) {                                                  // an xflow group is one segment (sf_xflow.h)
+        const uint32_t g = xmap[l];
+        if (g != XNONE) l = g;
+    }
     // the mocked clock never goes back: within the batch and across batches
     // (LeapArray would hand such an event a throwaway window)
     if (b.ts[i] < (i ? b.ts[i - 1] : *last_ts)) *err = SF_ERR_INVALID;
@@ -176,7 +181,10 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     const bool valid = s < *w.n_seg;
     uint32_t lo = 0, hi = 0, res = 0;
     if (valid) { lo = w.seg_start[s]; hi = w.seg_start[s + 1]; res = w.seg_res[s]; }
-    bool light = valid && hi - lo <= w.heavy_min;
+    // an xflow group (sf_xflow.h) is decided by k_decide_x only
+    const bool xs = valid && st.xmap && st.xmap[res] != XNONE;
+    if (xs) w.seg_mode[s] = SM_XFLOW;
+    bool light = valid && !xs && hi - lo <= w.heavy_min;
     // a ParamFlow-only segment of more than 32 events is faster on the
     // wavefront-by-value path (SM_PARAM) than as one lane's serial table walk
     if (light && hi - lo > 32 && st.prule_off[res + 1] != st.prule_off[res] &&
@@ -193,7 +201,7 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     if (threadIdx.x < LCLS) hbase[threadIdx.x] = hcnt[threadIdx.x] ? atomicAdd(&w.lcounts[threadIdx.x], hcnt[threadIdx.x]) : 0u;
     __syncthreads();
     if (light) { w.seg_mode[s] = SM_LIGHT; if (lc >= 0) w.light_list[w.loff[lc] + hbase[lc] + lrank] = s; }
-    const bool heavy = valid && !light;
+    const bool heavy = valid && !light && !xs;
     if (!__ballot(heavy)) return;
     uint8_t mode = SM_GENERIC;
     if (heavy) {
@@ -277,6 +285,15 @@ __global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_short(DevState st
     const uint32_t lo = seg_start[s], hi = seg_start[s + 1];
     if (hi - lo > SHORT_MAX) return;
     decide_segment<MAXS>(st, io, seg_res[s], lo, hi);
+}
+
+// One lane per xflow group segment (sf_xflow.h): origin / context / RELATE rules.
+template <int MAXS>
+__global__ void __launch_bounds__(64) k_decide_x(DevState st, SegIO io, const uint32_t* seg_start,
+                                                 const uint8_t* seg_mode, const uint32_t* n_seg) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= *n_seg || seg_mode[s] != SM_XFLOW) return;
+    decide_xgroup<MAXS>(st, io, seg_start[s], seg_start[s + 1]);
 }
 
 static HeavyCtx heavy_ctx(const Work& w) {
@@ -886,7 +903,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     if (timing) hipEventRecord(ev[0], s);
     hipError_t e;
     hipLaunchKernelGGL(k_keys_packed, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.pv_in, shard_count,
-                       shard_index, st.R, st.err, st.last_ts);
+                       shard_index, st.R, st.err, st.last_ts, st.xmap);
     e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.pv_in, w.pv_out, n, 0u,
                                   key_bits, s);
     if (e != hipSuccess) return e;
@@ -939,6 +956,7 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     io.aoff = b.aoff; io.etag = b.etag; io.ebits = b.ebits;
     io.v_status = w.v_status; io.v_wait = w.v_wait; io.v_rule = w.v_rule;
     io.perm = w.perm; io.o_status = out.status; io.o_wait = out.wait; io.o_rule = out.rule;
+    io.ev_res = b.res; io.ev_origin = b.origin; io.ev_ctx = b.ctx; io.shard_count = st.shard_count;
     HeavyCtx hc = heavy_ctx(w);
     if (timing) hc.hticks = w.hticks;
     const uint32_t max_seg = n < st.R ? n : st.R;
@@ -980,6 +998,14 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
                            w.seg_start, w.seg_res, ll);
         hipLaunchKernelGGL(k_decide_short<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, w.seg_mode, w.n_seg);
+    }
+    if (st.xmap) {
+        if (st.S <= 2)
+            hipLaunchKernelGGL(k_decide_x<2>, dim3(blocks(max_seg, 64)), dim3(64), 0, s3, st, io, w.seg_start,
+                               w.seg_mode, w.n_seg);
+        else
+            hipLaunchKernelGGL(k_decide_x<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, 64)), dim3(64), 0, s3, st, io,
+                               w.seg_start, w.seg_mode, w.n_seg);
     }
     hipEventRecord(ev[9], s3);                     // light done (also the join of C)
     hipEventRecord(ev[6], s2);                     // join B and C

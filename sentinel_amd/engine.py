@@ -76,6 +76,8 @@ def _declare(L):
     f("sf_read_node", I, P, U32, C.POINTER(abi.sf_node_state))
     f("sf_read_entry_node", I, P, C.POINTER(abi.sf_node_state))
     f("sf_read_rule_state", I, P, U32, C.POINTER(abi.sf_rule_state))
+    f("sf_read_origin_node", I, P, U32, U32, C.POINTER(abi.sf_node_state))
+    f("sf_read_context_node", I, P, U32, U32, C.POINTER(abi.sf_node_state))
     f("sf_load_degrade_rules", I, P, C.POINTER(abi.sf_degrade_rule), U32, C.POINTER(U32))
     f("sf_degrade_submit", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
     f("sf_read_breaker", I, P, U32, C.POINTER(abi.sf_breaker_state))
@@ -184,7 +186,8 @@ class DeviceBatch:
     def __init__(self, eng: "FlowEngine", hb: abi.HostBatch):
         self.n = hb.n
         self.arrays = {k: DeviceArray(eng, getattr(hb, k)) for k in ("res_id", "ts_ms", "count", "flags")}
-        for k in ("entry_ref", "create_ts", "arg_tag", "arg_bits", "n_args", "elem_off", "elem_tag", "elem_bits"):
+        for k in ("entry_ref", "create_ts", "arg_tag", "arg_bits", "n_args", "elem_off", "elem_tag", "elem_bits",
+                  "origin", "context"):
             a = getattr(hb, k)
             self.arrays[k] = DeviceArray(eng, a) if a is not None else None
         self.arg_slots = 0 if hb.arg_tag is None else hb.arg_tag.shape[0]
@@ -213,6 +216,7 @@ class DeviceBatch:
         if self.arrays.get("elem_off") is not None:
             b.arg_elem_off, b.elem_tag, b.elem_bits = g("elem_off"), g("elem_tag"), g("elem_bits")
             b.n_elems = self.arrays["elem_tag"].shape[0]
+        b.origin, b.context = g("origin"), g("context")
         return b
 
     def free(self):
@@ -327,6 +331,18 @@ class FlowEngine:
     def read_node(self, res) -> abi.sf_node_state:
         st = abi.sf_node_state()
         _check(lib().sf_read_node(self.h, res, C.byref(st)))
+        return st
+
+    def read_origin_node(self, res, origin) -> abi.sf_node_state:
+        """Origin node of (res, origin) (ClusterNode.getOrCreateOriginNode), if the engine keeps it."""
+        st = abi.sf_node_state()
+        _check(lib().sf_read_origin_node(self.h, res, origin, C.byref(st)))
+        return st
+
+    def read_context_node(self, context, res) -> abi.sf_node_state:
+        """DefaultNode of (context, res) (NodeSelectorSlot), if the engine keeps it."""
+        st = abi.sf_node_state()
+        _check(lib().sf_read_context_node(self.h, context, res, C.byref(st)))
         return st
 
     has_entry_node = True

@@ -21,6 +21,8 @@ Seeds are fixed; inputs are the shapes of BASELINE.json's configs at test size:
 import os
 import sys
 
+import ctypes as C
+
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -57,7 +59,8 @@ def flow_case(name, w):
         o.load_param_rules(w["param"], w.get("items", ()))
     out = {"cfg": np.frombuffer(bytes(cfg), np.uint8), "flow": rules_array(w.get("flow", ())),
            "param": rules_array(w.get("param", ())), "items": rules_array(list(w.get("items", ()))),
-           "n_batches": np.array(len(w["batches"]))}
+           "n_batches": np.array(len(w["batches"])),
+           "flow_rec": np.array(C.sizeof(abi.sf_flow_rule))}
     for k, b in enumerate(w["batches"]):
         v = o.submit(b)
         out.update(batch_arrays(f"b{k}_", b))

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../sentinel_amd/csrc/sf_heavy.h"
+#include "../../sentinel_amd/csrc/sf_xflow.h"
 
 using namespace sf;
 
@@ -32,6 +33,13 @@ struct hs_engine {
     std::vector<DevBreakerRule> dg_rules;
     std::vector<sf_breaker_state> dg_state;
     std::vector<uint32_t> dg_pos;                  // load order -> position
+    // xflow walk: group keys, origin / context node pool and its index table
+    std::vector<uint32_t> xmap;
+    std::vector<ParamSlot> xtab;
+    std::vector<Bucket> ax_second, ax_minute;
+    std::vector<Borrow> ax_borrow;
+    std::vector<int64_t> ax_threads;
+    uint32_t ax_count = 0;
     int32_t err = 0;
     uint32_t R;
     uint32_t heavy_min;
@@ -45,6 +53,10 @@ struct hs_engine {
         st.dg_n = dg_off.empty() ? 0 : (uint32_t)dg_off.size() - 1;
         st.dg_rr_of = st.dg_n ? dg_rr.data() : nullptr;
         st.dg_off = dg_off.data(); st.dg_rules = dg_rules.data(); st.dg_state = dg_state.data();
+        st.xmap = xmap.empty() ? nullptr : xmap.data();
+        st.xtab = xtab.data(); st.xcap_mask = xtab.empty() ? 0 : xtab.size() - 1;
+        st.ax_second = ax_second.data(); st.ax_borrow = ax_borrow.data(); st.ax_minute = ax_minute.data();
+        st.ax_threads = ax_threads.data(); st.ax_count = &ax_count; st.ax_cap = (uint32_t)ax_threads.size();
     }
 };
 
@@ -68,6 +80,7 @@ hs_engine* hs_create(const sf_config* c) {
     DevState& st = e->st;
     st.S = c->sample_count; st.wl = c->interval_ms / c->sample_count; st.interval = c->interval_ms;
     st.occupy_timeout = c->occupy_timeout_ms; st.max_rt = c->statistic_max_rt; st.R = e->R;
+    st.shard_count = c->shard_count;
     e->refresh();
     return e;
 }
@@ -79,13 +92,18 @@ static bool local_of(hs_engine* e, uint32_t res, uint32_t* l) {
 }
 
 int hs_load_flow_rules(hs_engine* e, const sf_flow_rule* rules, uint32_t n) {
-    std::vector<uint32_t> counts(e->R + 1, 0), loc;
+    std::vector<uint32_t> counts(e->R + 1, 0), loc, refl;
     std::vector<const sf_flow_rule*> valid;
     for (uint32_t i = 0; i < n; i++) {
         uint32_t l; if (!local_of(e, rules[i].resource, &l)) return SF_ERR_INVALID;
         if (!valid_flow_rule(rules[i])) continue;
+        uint32_t ref = XNONE;
+        if (rules[i].strategy == SF_STRATEGY_RELATE && rules[i].ref_resource != SF_REF_NONE) {
+            if (rules[i].ref_resource % e->cfg.shard_count != e->cfg.shard_index) return SF_ERR_UNSUPPORTED;
+            if (rules[i].ref_resource / e->cfg.shard_count < e->R) ref = rules[i].ref_resource / e->cfg.shard_count;
+        }
         if (++counts[l] > SF_MAX_RULES_PER_RESOURCE) return SF_ERR_UNSUPPORTED;
-        valid.push_back(&rules[i]); loc.push_back(l);
+        valid.push_back(&rules[i]); loc.push_back(l); refl.push_back(ref);
     }
     for (uint32_t r = 0; r < e->R; r++) e->rule_off[r + 1] = e->rule_off[r] + counts[r];
     std::vector<uint32_t> fill(e->rule_off.begin(), e->rule_off.end() - 1);
@@ -95,7 +113,22 @@ int hs_load_flow_rules(hs_engine* e, const sf_flow_rule* rules, uint32_t n) {
     for (size_t k = 0; k < valid.size(); k++) {
         uint32_t pos = fill[loc[k]]++;
         e->flow_pos[k] = pos;
-        e->rules[pos] = make_dev_rule(*valid[k], e->cfg.cold_factor, (int)k);
+        e->rules[pos] = make_dev_rule(*valid[k], e->cfg.cold_factor, (int)k, refl[k]);
+    }
+    std::vector<uint32_t> xm;
+    if (build_xmap(e->rules.data(), e->rule_off.data(), e->R, xm)) {
+        e->xmap = xm;
+        if (e->ax_threads.empty()) {                 // the pool lives as long as the engine
+            const size_t cap = e->cfg.aux_capacity ? e->cfg.aux_capacity : 4096, S = e->cfg.sample_count;
+            size_t tcap = 16; while (tcap < 2 * cap) tcap <<= 1;
+            e->xtab.assign(tcap, ParamSlot{0, 0, 0, 0});
+            e->ax_second.assign(cap * S, fresh_bucket(WS_NONE, e->cfg.statistic_max_rt));
+            e->ax_borrow.assign(cap * S, Borrow{WS_NONE, 0});
+            e->ax_minute.assign(cap * MINUTE, fresh_bucket(WS_NONE, e->cfg.statistic_max_rt));
+            e->ax_threads.assign(cap, 0);
+        }
+    } else {
+        e->xmap.clear();
     }
     e->refresh();
     return SF_OK;
@@ -156,7 +189,10 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     const uint32_t n = in->n;
     e->err = 0;
     std::vector<uint32_t> key(n), perm(n), inv(n);
-    for (uint32_t i = 0; i < n; i++) if (!local_of(e, in->res_id[i], &key[i])) return SF_ERR_INVALID;
+    for (uint32_t i = 0; i < n; i++) {
+        if (!local_of(e, in->res_id[i], &key[i])) return SF_ERR_INVALID;
+        if (!e->xmap.empty() && e->xmap[key[i]] != XNONE) key[i] = e->xmap[key[i]];   // xflow group segment
+    }
     std::iota(perm.begin(), perm.end(), 0u);
     std::stable_sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
     std::vector<int64_t> ts(n), eref(n, -1), cts(n, 0), pcg(n);
@@ -190,6 +226,13 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     std::vector<uint32_t> ident(n);
     std::iota(ident.begin(), ident.end(), 0u);
     io.perm = ident.data(); io.o_status = vs.data(); io.o_wait = vw.data(); io.o_rule = vr.data();
+    std::vector<uint32_t> sres(n), sorigin(n), sctx(n);          // xflow walk: sorted order (perm is the identity)
+    for (uint32_t j = 0; j < n; j++) {
+        sres[j] = in->res_id[perm[j]];
+        sorigin[j] = in->origin ? in->origin[perm[j]] : SF_ORIGIN_NONE;
+        sctx[j] = in->context ? in->context[perm[j]] : 0u;
+    }
+    io.ev_res = sres.data(); io.ev_origin = sorigin.data(); io.ev_ctx = sctx.data(); io.shard_count = e->cfg.shard_count;
     // segments + routing (k_segments / k_classify)
     std::vector<uint32_t> seg_start, seg_res, segflag;
     for (uint32_t j = 0; j < n; j++) {
@@ -205,6 +248,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     std::vector<Acc> acc_hw, acc_sec;
     for (uint32_t s = 0; s < ns; s++) {
         uint32_t lo = seg_start[s], hi = seg_start[s + 1];
+        if (!e->xmap.empty() && e->xmap[seg_res[s]] != XNONE) { mode[s] = SM_XFLOW; continue; }
         if (hi - lo <= e->heavy_min) { mode[s] = SM_LIGHT; continue; }
         e->n_heavy_segments++;
         mode[s] = heavy_mode(e->st, seg_res[s], segflag[s], ts[lo]);
@@ -235,6 +279,10 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         case SM_RL: heavy_rl(tm, e->st, io, hc, s, res, lo, hi); break;
         case SM_THREAD: heavy_thread(tm, e->st, io, hc, s, res, lo, hi, nullptr, nullptr); break;
         case SM_NORULE: break;                    // every entry passes (fill)
+        case SM_XFLOW:
+            if (e->st.S <= 2) decide_xgroup<2>(e->st, io, lo, hi);
+            else decide_xgroup<SF_MAX_SAMPLE_COUNT>(e->st, io, lo, hi);
+            break;
         default:
             if (e->st.S <= 2) decide_segment<2>(e->st, io, res, lo, hi);
             else decide_segment<SF_MAX_SAMPLE_COUNT>(e->st, io, res, lo, hi);
@@ -242,7 +290,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     }
     // k_heavy_fill
     for (uint32_t s = 0; s < ns; s++) {
-        if (mode[s] < SM_QPS) continue;
+        if (mode[s] < SM_QPS || mode[s] == SM_XFLOW) continue;
         for (uint32_t j = seg_start[s]; j < seg_start[s + 1]; j++) {
             EvContrib c = heavy_event(hc, io, seg_start[s], mode[s], j);
             vs[j] = c.status; vw[j] = c.wait; vr[j] = 0;
@@ -260,7 +308,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     }
     // k_heavy_apply
     for (uint32_t s = 0; s < ns; s++)
-        if (mode[s] >= SM_QPS) heavy_apply(e->st, hc, s, seg_res[s], nhw[s], nsec[s]);
+        if (mode[s] >= SM_QPS && mode[s] != SM_XFLOW) heavy_apply(e->st, hc, s, seg_res[s], nhw[s], nsec[s]);
     for (uint32_t j = 0; j < n; j++) {
         uint32_t i = perm[j];
         ((uint8_t*)out->status)[i] = vs[j];
@@ -292,6 +340,37 @@ int hs_read_node(hs_engine* e, uint32_t res, sf_node_state* out) {
     for (int i = 0; i < MINUTE; i++) conv(e->minute[(size_t)l * MINUTE + i], &out->minute[i]);
     out->cur_thread_num = e->threads[l];
     return SF_OK;
+}
+
+static void read_rows(hs_engine* e, const NodeRows& r, sf_node_state* out) {
+    std::memset(out, 0, sizeof *out);
+    for (int i = 0; i < SF_MAX_SAMPLE_COUNT; i++) { out->second[i].window_start = SF_WS_ABSENT; out->borrow_ws[i] = SF_WS_ABSENT; }
+    auto conv = [](const Bucket& d, sf_bucket* o) {
+        if (d.ws == WS_NONE) { std::memset(o, 0, sizeof *o); o->window_start = SF_WS_ABSENT; return; }
+        o->window_start = d.ws; o->pass = d.pass; o->block = d.block; o->exception = d.exc; o->success = d.succ;
+        o->rt = d.rt; o->occupied_pass = d.occ; o->min_rt = d.min_rt;
+    };
+    for (int i = 0; i < e->cfg.sample_count; i++) {
+        conv(r.sec[i], &out->second[i]);
+        out->borrow_ws[i] = r.bor[i].ws == WS_NONE ? SF_WS_ABSENT : r.bor[i].ws;
+        out->borrow_pass[i] = r.bor[i].ws == WS_NONE ? 0 : r.bor[i].pass;
+    }
+    for (int i = 0; i < MINUTE; i++) conv(r.min[i], &out->minute[i]);
+    out->cur_thread_num = *r.thr;
+}
+static int read_aux(hs_engine* e, uint32_t res, uint32_t kind, uint32_t id, sf_node_state* out) {
+    uint32_t l; if (!local_of(e, res, &l) || e->xtab.empty()) return SF_ERR_INVALID;
+    const ParamTable t{e->xtab.data(), e->xtab.size() - 1, &e->err};
+    const ParamSlot* s = t.find(pkey_hi(l, PK_AUX, kind, 0), id);
+    if (!s) return SF_ERR_INVALID;
+    read_rows(e, aux_rows(e->st, (uint32_t)s->a), out);
+    return SF_OK;
+}
+int hs_read_origin_node(hs_engine* e, uint32_t res, uint32_t origin, sf_node_state* out) {
+    return read_aux(e, res, AX_ORIGIN, origin, out);
+}
+int hs_read_context_node(hs_engine* e, uint32_t context, uint32_t res, sf_node_state* out) {
+    return read_aux(e, res, AX_CTX, context, out);
 }
 
 int hs_read_rule_state(hs_engine* e, uint32_t idx, sf_rule_state* out) {

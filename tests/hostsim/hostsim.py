@@ -27,6 +27,8 @@ def lib():
         L.hs_submit.argtypes = [P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts)]
         L.hs_read_node.argtypes = [P, C.c_uint32, C.POINTER(abi.sf_node_state)]
         L.hs_read_rule_state.argtypes = [P, C.c_uint32, C.POINTER(abi.sf_rule_state)]
+        L.hs_read_origin_node.argtypes = [P, C.c_uint32, C.c_uint32, C.POINTER(abi.sf_node_state)]
+        L.hs_read_context_node.argtypes = [P, C.c_uint32, C.c_uint32, C.POINTER(abi.sf_node_state)]
         L.hs_load_degrade_rules.argtypes = [P, C.POINTER(abi.sf_degrade_rule), C.c_uint32, C.POINTER(C.c_uint32)]
         L.hs_read_breaker.argtypes = [P, C.c_uint32, C.POINTER(abi.sf_breaker_state)]
         _lib = L
@@ -46,7 +48,8 @@ class HostSimEngine:
     __del__ = close
 
     def load_flow_rules(self, rules):
-        assert lib().hs_load_flow_rules(self.h, abi.rules_array(abi.sf_flow_rule, rules), len(rules)) == 0
+        ptr, n = abi.flow_rules_ptr(rules)
+        assert lib().hs_load_flow_rules(self.h, ptr, n) == 0
 
     def load_param_rules(self, rules, items=()):
         assert lib().hs_load_param_rules(self.h, abi.rules_array(abi.sf_param_rule, rules), len(rules),
@@ -82,3 +85,15 @@ class HostSimEngine:
         s = abi.sf_rule_state()
         assert lib().hs_read_rule_state(self.h, idx, C.byref(s)) == 0
         return s
+
+    def read_origin_node(self, res, origin):
+        st = abi.sf_node_state()
+        if lib().hs_read_origin_node(self.h, res, origin, C.byref(st)):
+            raise KeyError((res, origin))
+        return st
+
+    def read_context_node(self, context, res):
+        st = abi.sf_node_state()
+        if lib().hs_read_context_node(self.h, context, res, C.byref(st)):
+            raise KeyError((context, res))
+        return st

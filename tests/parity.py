@@ -65,3 +65,15 @@ def compare_entry_node(eng, ora, sample_count=2, what=""):
 def metric_rows(rows):
     return sorted((r.resource, r.timestamp, r.pass_qps, r.block_qps, r.success_qps, r.exception_qps, r.rt,
                    r.occupied_pass_qps) for r in rows)
+
+
+def compare_aux_nodes(eng, ora, origin_nodes=(), context_nodes=(), sample_count=2, what=""):
+    """Origin nodes (res, origin) and context DefaultNodes (context, res) kept for the rules."""
+    for r, o in origin_nodes:
+        x = abi.node_state_to_dict(eng.read_origin_node(r, o), sample_count)
+        y = abi.node_state_to_dict(ora.read_origin_node(r, o), sample_count)
+        assert x == y, f"{what}: origin node ({r}, {o}) differs:\n engine={x}\n oracle={y}"
+    for c, r in context_nodes:
+        x = abi.node_state_to_dict(eng.read_context_node(c, r), sample_count)
+        y = abi.node_state_to_dict(ora.read_context_node(c, r), sample_count)
+        assert x == y, f"{what}: context node ({c}, {r}) differs:\n engine={x}\n oracle={y}"

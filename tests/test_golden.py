@@ -13,13 +13,21 @@ HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 FLOW_CASES = ["flowqps_demo", "mixed_1k", "param_40", "param_mixed"]
 
 
+# Record sizes of the structs as the committed vectors were written (ABI fields
+# appended since then are zero: limitApp "default", no aux_capacity override).
+_LEGACY = {"sf_flow_rule": 40, "sf_config": 80}
+
+
 def _struct(cls, arr):
-    return cls.from_buffer_copy(arr.tobytes())
+    raw = arr.tobytes()
+    return cls.from_buffer_copy(raw + b"\0" * (C_sizeof(cls) - len(raw)))
 
 
-def _rules(cls, arr):
-    n = arr.size // C_sizeof(cls)
-    return [cls.from_buffer_copy(arr[i * C_sizeof(cls):(i + 1) * C_sizeof(cls)].tobytes()) for i in range(n)]
+def _rules(cls, arr, rec=None):
+    rec = rec or _LEGACY.get(cls.__name__, C_sizeof(cls))
+    n = arr.size // rec
+    pad = b"\0" * (C_sizeof(cls) - rec)
+    return [cls.from_buffer_copy(arr[i * rec:(i + 1) * rec].tobytes() + pad) for i in range(n)]
 
 
 def C_sizeof(cls):
@@ -29,7 +37,7 @@ def C_sizeof(cls):
 
 def load_flow_case(name):
     z = np.load(os.path.join(HERE, f"{name}.npz"))
-    case = {"cfg": _struct(abi.sf_config, z["cfg"]), "flow": _rules(abi.sf_flow_rule, z["flow"]),
+    case = {"cfg": _struct(abi.sf_config, z["cfg"]), "flow": _rules(abi.sf_flow_rule, z["flow"], int(z["flow_rec"]) if "flow_rec" in z else None),
             "param": _rules(abi.sf_param_rule, z["param"]), "items": _rules(abi.sf_hot_item, z["items"]),
             "batches": [], "want": [], "nodes": z["nodes"], "node_states": z["node_states"],
             "entry_node": z["entry_node"]}

@@ -247,6 +247,88 @@ def system_large(kind, seed=43):
                 status=(0.0, 0.0))
 
 
+def xflow(seed=51, R=400, n=60_000, origins=6, contexts=4, duration_ms=6000, zipf=1.1, split=2):
+    """Flow rules that read other nodes (FlowRuleChecker.selectNodeByRequesterAndStrategy):
+    origin-specific and "other" limitApps (origin nodes), RELATE (another
+    resource's ClusterNode, chains and self references included), CHAIN
+    (the DefaultNode of a context), cluster rules with / without fallback,
+    beside plain rules.  Events carry origins (some "", some the strings
+    "default" / "other") and context names; prioritized entries; THREAD exits
+    carry their entry's context."""
+    rng = np.random.default_rng(seed)
+    O0 = 2                                                   # origin ids >= 2 are names
+    rules = []
+
+    def rule(r, **kw):
+        beh = int(kw.pop("beh", rng.choice([0, 0, 1, 2, 3])))
+        grade = kw.pop("grade", abi.GRADE_THREAD if (beh == 0 and rng.random() < 0.25) else abi.GRADE_QPS)
+        rules.append(abi.sf_flow_rule(resource=r, grade=grade, count=float(kw.pop("count", rng.integers(1, 30))),
+                                      strategy=kw.pop("strategy", 0),
+                                      control_behavior=beh if grade == abi.GRADE_QPS else 0,
+                                      warm_up_period_sec=int(rng.integers(1, 5)),
+                                      max_queueing_time_ms=int(rng.integers(1, 600)), **kw))
+    for r in range(R):
+        u = rng.random()
+        if u < 0.4:
+            rule(r)
+        elif u < 0.55:                                       # origin-specific (+ a default rule)
+            for _ in range(int(rng.integers(1, 3))):
+                rule(r, limit_app=int(rng.integers(O0, O0 + origins)))
+            if rng.random() < 0.5:
+                rule(r)
+        elif u < 0.65:                                       # "other" beside a specific origin
+            rule(r, limit_app=int(rng.integers(O0, O0 + origins)))
+            rule(r, limit_app=abi.APP_OTHER)
+        elif u < 0.78:                                       # RELATE
+            refs = [r, int(rng.integers(0, R)), int(rng.integers(0, R)), R + 5, abi.REF_NONE]
+            rule(r, strategy=abi.STRATEGY_RELATE, ref_resource=refs[int(rng.integers(0, len(refs)))],
+                 limit_app=int(rng.choice([abi.APP_DEFAULT, abi.APP_DEFAULT, O0])))
+        elif u < 0.88:                                       # CHAIN on a context
+            rule(r, strategy=abi.STRATEGY_CHAIN, ref_resource=int(rng.integers(0, contexts)))
+            if rng.random() < 0.4:
+                rule(r)
+        elif u < 0.94:                                       # cluster rule, ClusterStateManager not started
+            rule(r, cluster_mode=1, cluster_fallback=int(rng.random() < 0.5))
+        # else: no rule (may still be a RELATE target)
+    # events: Zipf resources, contexts, origins; THREAD exits
+    w = 1.0 / np.arange(1, R + 1) ** zipf
+    perm_r = rng.permutation(R)
+    res = perm_r[rng.choice(R, size=n, p=w / w.sum())].astype(np.uint32)
+    ts = np.sort(rng.integers(0, duration_ms, n)) + trace.T0
+    og = rng.integers(0, O0 + origins + 1, n).astype(np.uint32)
+    og[rng.random(n) < 0.3] = abi.ORIGIN_NONE
+    cx = rng.integers(0, contexts, n).astype(np.uint32)
+    cnt = np.where(rng.random(n) < 0.85, 1, rng.integers(2, 4, n)).astype(np.int32)
+    flags = (np.where(rng.random(n) < 0.1, abi.EV_PRIO, 0) | abi.EV_IN).astype(np.uint8)
+    ent = np.nonzero(rng.random(n) < 0.4)[0]
+    ex_ts = ts[ent] + rng.integers(0, 60, ent.size)
+    all_ts = np.concatenate([ts, ex_ts])
+    key = np.lexsort((np.concatenate([np.zeros(n), np.ones(ent.size)]), all_ts))
+    pos = np.empty(key.size, np.int64)
+    pos[key] = np.arange(key.size)
+    src = np.concatenate([np.arange(n), ent])
+    err = np.where(rng.random(ent.size) < 0.2, abi.EV_ERROR, 0)
+    fl = np.concatenate([flags, (abi.EV_EXIT | abi.EV_IN | err).astype(np.uint8)])
+    eref = np.full(key.size, -1, np.int64)
+    eref[pos[n:]] = pos[ent]
+    full = abi.HostBatch(res[src][key], all_ts[key], cnt[src][key], fl[key], entry_ref=eref,
+                         origin=og[src][key], context=cx[src][key])
+    cuts = np.linspace(0, full.n, split + 1).astype(int)
+    batches = [full.subset(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
+    # the origin / context nodes a rule can read (the set both sides keep)
+    on, dn = set(), set()
+    for r in rules:
+        sel = full.res_id == r.resource
+        if r.strategy == abi.STRATEGY_DIRECT and r.limit_app != abi.APP_DEFAULT:
+            on |= {(int(r.resource), int(o)) for o in np.unique(full.origin[sel]) if o != abi.ORIGIN_NONE}
+        if r.strategy == abi.STRATEGY_CHAIN and np.any(full.context[sel] == r.ref_resource):
+            dn.add((int(r.ref_resource), int(r.resource)))
+    n_valid = sum(1 for r in rules if not (r.grade == abi.GRADE_QPS and r.strategy in (1, 2) and
+                                            r.ref_resource == abi.REF_NONE))   # checkStrategyField
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=full.n), flow=rules, batches=batches,
+                nodes=list(range(R)), n_flow=n_valid, origin_nodes=sorted(on), context_nodes=sorted(dn))
+
+
 ALL = {
     "config1": config1, "config2": config2, "config3": config3, "config4": config4,
     "prioritized": prioritized, "multi_rule": multi_rule, "param_mixed": param_mixed,
@@ -268,4 +350,6 @@ def run(make_engine, make_oracle, w):
         parity.compare_entry_node(eng, ora, sample_count=w["cfg"].sample_count)
     if w.get("n_flow"):
         parity.compare_rule_states(eng, ora, w["n_flow"])
+    parity.compare_aux_nodes(eng, ora, w.get("origin_nodes", ()), w.get("context_nodes", ()),
+                             sample_count=w["cfg"].sample_count)
     return eng, ora, outs
