@@ -28,6 +28,7 @@ final class EventBatcher implements Runnable {
     static final class Ticket {
         final Thread caller = Thread.currentThread();
         int resource, count;
+        int origin = -1, context;        // interned Context origin (-1: "") and context name
         byte flags;
         long ts, entryRef = -1, createTs;
         Object[] args;
@@ -42,6 +43,7 @@ final class EventBatcher implements Runnable {
     private final int maxBatch;
     private final Arena arena = Arena.ofShared();
     private final MemorySegment res, ts, cnt, flags, eref, cts, nArgs, argTag, argBits, elemOff, elemTag, elemBits;
+    private final MemorySegment origin, context;
     private final MemorySegment status, waitMs, ruleIdx, batch, verdicts;
     private long seq, lastTs = Long.MIN_VALUE, loadedRuleVersion = -1;
     static final int ARG_SLOTS = Integer.getInteger("sentinel.gpu.argSlots", 2);
@@ -57,6 +59,7 @@ final class EventBatcher implements Runnable {
         argBits = arena.allocate(8L * ARG_SLOTS * maxBatch);
         elemOff = arena.allocate(4L * ((long) ARG_SLOTS * maxBatch + 1));
         elemTag = arena.allocate(MAX_ELEMS); elemBits = arena.allocate(8L * MAX_ELEMS);
+        origin = arena.allocate(4L * maxBatch); context = arena.allocate(4L * maxBatch);
         status = arena.allocate(maxBatch); waitMs = arena.allocate(4L * maxBatch); ruleIdx = arena.allocate(2L * maxBatch);
         batch = arena.allocate(EVENT_BATCH); verdicts = arena.allocate(VERDICTS);
         Thread t = new Thread(this, "sentinel-gpu-flusher");
@@ -113,6 +116,8 @@ final class EventBatcher implements Runnable {
             ts.setAtIndex(JAVA_LONG, i, lastTs);
             cnt.setAtIndex(JAVA_INT, i, t.count);
             flags.setAtIndex(JAVA_BYTE, i, t.flags);
+            origin.setAtIndex(JAVA_INT, i, t.origin);
+            context.setAtIndex(JAVA_INT, i, t.context);
             if ((t.flags & EV_EXIT) != 0) {
                 anyExit = true;
                 boolean same = t.entry != null && t.entry.batchSeq == bs;
@@ -160,7 +165,9 @@ final class EventBatcher implements Runnable {
         batch.set(ADDRESS, o, ne > 0 ? elemOff : MemorySegment.NULL); o += 8;
         batch.set(ADDRESS, o, elemTag); o += 8;
         batch.set(ADDRESS, o, elemBits); o += 8;
-        batch.set(JAVA_INT, o, ne);
+        batch.set(JAVA_INT, o, ne); o += 8;
+        batch.set(ADDRESS, o, origin); o += 8;
+        batch.set(ADDRESS, o, context);
         verdicts.set(JAVA_INT, 0, SF_MEM_HOST_);
         verdicts.set(ADDRESS, 8, status); verdicts.set(ADDRESS, 16, waitMs); verdicts.set(ADDRESS, 24, ruleIdx);
         check((int) SUBMIT.invokeExact(engine.handle, batch, verdicts));

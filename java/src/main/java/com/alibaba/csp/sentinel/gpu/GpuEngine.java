@@ -1,5 +1,6 @@
 package com.alibaba.csp.sentinel.gpu;
 
+import com.alibaba.csp.sentinel.slots.block.RuleConstant;
 import com.alibaba.csp.sentinel.slots.block.flow.FlowRule;
 import com.alibaba.csp.sentinel.slots.block.flow.FlowRuleManager;
 import com.alibaba.csp.sentinel.slots.block.flow.param.ParamFlowItem;
@@ -94,6 +95,30 @@ public final class GpuEngine {
         }
     }
 
+    private final ConcurrentHashMap<String, Integer> originIds = new ConcurrentHashMap<>();
+    private final ConcurrentHashMap<String, Integer> contextIds = new ConcurrentHashMap<>();
+
+    /** Origin / limitApp id: "default" 0, "other" 1, names from 2; "" (no origin) -1 (SF_ORIGIN_NONE). */
+    int originId(String origin) {
+        if (origin == null || origin.isEmpty()) return -1;
+        if (RuleConstant.LIMIT_APP_DEFAULT.equals(origin)) return 0;
+        if (RuleConstant.LIMIT_APP_OTHER.equals(origin)) return 1;
+        Integer id = originIds.get(origin);
+        if (id != null) return id;
+        synchronized (originIds) {
+            return originIds.computeIfAbsent(origin, k -> originIds.size() + 2);
+        }
+    }
+
+    /** Context-name id (CHAIN refResource / Context.getName()). */
+    int contextId(String name) {
+        Integer id = contextIds.get(name);
+        if (id != null) return id;
+        synchronized (contextIds) {
+            return contextIds.computeIfAbsent(name, k -> contextIds.size());
+        }
+    }
+
     /** Called after FlowRuleManager / ParamFlowRuleManager / SystemRuleManager.loadRules. */
     public void reloadRules() {
         ruleVersion.incrementAndGet();
@@ -119,7 +144,13 @@ public final class GpuEngine {
                 s.set(JAVA_INT, 24, r.getWarmUpPeriodSec());
                 s.set(JAVA_INT, 28, r.getMaxQueueingTimeMs());
                 s.set(JAVA_INT, 32, r.isClusterMode() ? 1 : 0);
-                s.set(JAVA_INT, 36, r.getRefResource() == null ? 0 : resourceId(r.getRefResource()));
+                String ref = r.getRefResource();
+                int refId = ref == null || ref.isEmpty() ? -1            // SF_REF_NONE
+                        : r.getStrategy() == RuleConstant.STRATEGY_CHAIN ? contextId(ref) : resourceId(ref);
+                s.set(JAVA_INT, 36, refId);
+                String app = r.getLimitApp();                            // blank -> "default" (FlowRuleUtil.java:99-101)
+                s.set(JAVA_INT, 40, app == null || app.trim().isEmpty() ? 0 : originId(app));
+                s.set(JAVA_INT, 44, r.getClusterConfig() == null || r.getClusterConfig().isFallbackToLocalWhenFail() ? 1 : 0);
             }
             check((int) LOAD_FLOW.invokeExact(handle, fr, flow.size()));
             flowRulesByResource = byRes;

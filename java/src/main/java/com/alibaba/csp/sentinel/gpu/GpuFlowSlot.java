@@ -41,6 +41,8 @@ public class GpuFlowSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
                       boolean prioritized, Object... args) throws Throwable {
         EventBatcher.Ticket t = new EventBatcher.Ticket();
         t.resource = engine.resourceId(resourceWrapper.getName());
+        t.origin = engine.originId(context.getOrigin());    // limitApp / origin node (FlowRuleChecker.java:129-161)
+        t.context = engine.contextId(context.getName());    // CHAIN rules' DefaultNode
         t.count = count;
         t.flags = (byte) ((resourceWrapper.getEntryType() == EntryType.IN ? EV_IN : 0) | (prioritized ? EV_PRIO : 0));
         t.ts = TimeUtil.currentTimeMillis();
@@ -96,6 +98,7 @@ public class GpuFlowSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
         if (context.getCurEntry().getBlockError() == null && entry != null) {
             EventBatcher.Ticket t = new EventBatcher.Ticket();
             t.resource = entry.resource;
+            t.origin = entry.origin; t.context = entry.context;
             t.count = count;
             t.flags = (byte) (EV_EXIT | (entry.flags & EV_IN)
                     | (context.getCurEntry().getError() != null ? EV_ERROR : 0));

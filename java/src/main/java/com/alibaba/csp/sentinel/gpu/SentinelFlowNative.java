@@ -57,7 +57,7 @@ final class SentinelFlowNative {
     static final MethodHandle REQUEST_TOKENS = fn("sf_request_tokens",
             FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
 
-    /** sf_config (sentinel_flow.h): 17 fields, natural alignment. */
+    /** sf_config (sentinel_flow.h): 19 fields, natural alignment. */
     static final StructLayout CONFIG = MemoryLayout.structLayout(
             JAVA_INT.withName("sample_count"), JAVA_INT.withName("interval_ms"),
             JAVA_INT.withName("occupy_timeout_ms"), JAVA_INT.withName("cold_factor"),
@@ -67,14 +67,17 @@ final class SentinelFlowNative {
             JAVA_INT.withName("shard_index"), JAVA_INT.withName("device"),
             JAVA_INT.withName("cluster_sample_count"), JAVA_INT.withName("cluster_interval_ms"),
             JAVA_DOUBLE.withName("exceed_count"), JAVA_DOUBLE.withName("max_occupy_ratio"),
-            JAVA_INT.withName("max_flow_ids"), JAVA_INT.withName("heavy_min_events"));
+            JAVA_INT.withName("max_flow_ids"), JAVA_INT.withName("heavy_min_events"),
+            JAVA_INT.withName("aux_capacity"), JAVA_INT.withName("pad"));
 
-    /** sf_flow_rule: 48 bytes. */
+    /** sf_flow_rule: 48 bytes.  limit_app: 0 "default", 1 "other", else an interned origin id;
+     *  ref_resource: RELATE a resource id, CHAIN a context-name id (0xFFFFFFFF blank). */
     static final StructLayout FLOW_RULE = MemoryLayout.structLayout(
             JAVA_INT.withName("resource"), JAVA_INT.withName("grade"), JAVA_DOUBLE.withName("count"),
             JAVA_INT.withName("strategy"), JAVA_INT.withName("control_behavior"),
             JAVA_INT.withName("warm_up_period_sec"), JAVA_INT.withName("max_queueing_time_ms"),
-            JAVA_INT.withName("cluster_mode"), JAVA_INT.withName("ref_resource"));
+            JAVA_INT.withName("cluster_mode"), JAVA_INT.withName("ref_resource"),
+            JAVA_INT.withName("limit_app"), JAVA_INT.withName("cluster_fallback"));
 
     /** sf_hot_item: {u8 tag, pad[3], i32 count, u64 bits}: 16 bytes. */
     static final StructLayout HOT_ITEM = MemoryLayout.structLayout(
@@ -102,7 +105,8 @@ final class SentinelFlowNative {
             JAVA_INT.withName("arg_slots"), MemoryLayout.paddingLayout(4),
             ADDRESS.withName("n_args"), ADDRESS.withName("arg_tag"), ADDRESS.withName("arg_bits"),
             ADDRESS.withName("arg_elem_off"), ADDRESS.withName("elem_tag"), ADDRESS.withName("elem_bits"),
-            JAVA_INT.withName("n_elems"), MemoryLayout.paddingLayout(4));
+            JAVA_INT.withName("n_elems"), MemoryLayout.paddingLayout(4),
+            ADDRESS.withName("origin"), ADDRESS.withName("context"));
 
     /** sf_verdicts. */
     static final StructLayout VERDICTS = MemoryLayout.structLayout(

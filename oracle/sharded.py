@@ -39,12 +39,22 @@ def split(hb: abi.HostBatch, T: int):
 
 
 def shard_rules(rules, T: int, k: int):
-    """Flow rules of shard k with local resource ids (list order kept)."""
+    """Flow rules of shard k with local resource ids (list order kept); rules is
+    a list of abi.sf_flow_rule or an abi.FLOW_RULE_DTYPE array.  A RELATE
+    reference (same shard by construction) gets its local id too."""
+    if isinstance(rules, np.ndarray):
+        out = rules[rules["resource"] % T == k].copy()
+        out["resource"] //= T
+        rel = (out["strategy"] == abi.STRATEGY_RELATE) & (out["ref_resource"] != abi.REF_NONE)
+        out["ref_resource"][rel] //= T
+        return out
     out = []
     for r in rules:
         if r.resource % T == k:
             c = abi.sf_flow_rule.from_buffer_copy(r)
             c.resource = r.resource // T
+            if c.strategy == abi.STRATEGY_RELATE and c.ref_resource != abi.REF_NONE:
+                c.ref_resource //= T
             out.append(c)
     return out
 

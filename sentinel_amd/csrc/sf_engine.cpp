@@ -401,7 +401,7 @@ static int drain(sf_engine* e) {
         HIP_TRY(hipMemcpy(&nseg, e->w[e->last].n_seg, 4, hipMemcpyDeviceToHost));
         e->stats.n_segments = nseg;
     }
-    if (first) return fail(first, first == SF_ERR_CAPACITY ? "param table capacity exceeded"
+    if (first) return fail(first, first == SF_ERR_CAPACITY ? "capacity exceeded (param table, or the origin / context node pool: aux_capacity)"
                                                            : "invalid batch (resource outside shard or bad entry_ref)");
     return SF_OK;
 }
@@ -745,7 +745,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         int32_t err = 0;
         HIP_TRY(hipMemcpyAsync(&err, w.err, 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (err) return fail(err, err == SF_ERR_CAPACITY ? "param table capacity exceeded"
+        if (err) return fail(err, err == SF_ERR_CAPACITY ? "capacity exceeded (param table, or the origin / context node pool: aux_capacity)"
                                                          : "invalid batch (resource outside shard or bad entry_ref)");
         return SF_OK;
     }
@@ -791,7 +791,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     HIP_TRY(hipStreamSynchronize(s));
     e->stats.n_segments = nseg;
     acc_timing(e, slot);
-    if (err) return fail(err, err == SF_ERR_CAPACITY ? "param table capacity exceeded"
+    if (err) return fail(err, err == SF_ERR_CAPACITY ? "capacity exceeded (param table, or the origin / context node pool: aux_capacity)"
                                                      : "invalid batch (resource outside shard or bad entry_ref)");
     return SF_OK;
 }

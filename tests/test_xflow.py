@@ -149,8 +149,9 @@ def test_gpu_xflow_sharded_colocated():
     from tests import parity
     w = workloads.xflow(seed=57, R=400, n=60_000)
     for r in w["flow"]:                      # co-locate: refResource on the resource's shard
-        if r.strategy == abi.STRATEGY_RELATE and r.ref_resource < 400 and r.ref_resource % 2 != r.resource % 2:
-            r.ref_resource = (r.ref_resource + 1) % 400
+        ref = r.ref_resource
+        if r.strategy == abi.STRATEGY_RELATE and ref != abi.REF_NONE and ref % 2 != r.resource % 2:
+            r.ref_resource = ref + 1 if ref >= 400 else (ref + 1) % 400   # (beyond 400: never a node)
     cfg1 = w["cfg"]
     ora = OracleEngine(cfg1)
     ora.load_flow_rules(w["flow"])
@@ -167,3 +168,17 @@ def test_gpu_xflow_sharded_colocated():
         parity.compare_aux_nodes(eng, ora, [x for x in w["origin_nodes"] if x[0] % 2 == k],
                                  [x for x in w["context_nodes"] if x[1] % 2 == k])
         eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_xflow_pool_capacity():
+    """More origin / context nodes than aux_capacity: SF_ERR_CAPACITY, not a silent drop."""
+    from sentinel_amd.engine import EngineError, FlowEngine
+    w = workloads.xflow(seed=58, R=300, n=30_000)
+    w["cfg"].aux_capacity = 8
+    eng = FlowEngine(w["cfg"])
+    eng.load_flow_rules(w["flow"])
+    with pytest.raises(EngineError) as ex:
+        for b in w["batches"]:
+            eng.submit(b)
+    assert ex.value.code == abi.SF_ERR_CAPACITY

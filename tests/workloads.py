@@ -325,8 +325,9 @@ def xflow(seed=51, R=400, n=60_000, origins=6, contexts=4, duration_ms=6000, zip
             dn.add((int(r.ref_resource), int(r.resource)))
     n_valid = sum(1 for r in rules if not (r.grade == abi.GRADE_QPS and r.strategy in (1, 2) and
                                             r.ref_resource == abi.REF_NONE))   # checkStrategyField
-    return dict(cfg=abi.default_config(max_resources=R, max_batch=full.n), flow=rules, batches=batches,
-                nodes=list(range(R)), n_flow=n_valid, origin_nodes=sorted(on), context_nodes=sorted(dn))
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=full.n, aux_capacity=max(4096, 2 * (len(on) + len(dn)))),
+                flow=rules, batches=batches, nodes=list(range(R)), n_flow=n_valid, origin_nodes=sorted(on),
+                context_nodes=sorted(dn))
 
 
 ALL = {
