@@ -441,10 +441,9 @@ def rules_array(cls, rules):
 # numpy views of the rule structs, for loading millions of rules without
 # building Python objects (layouts pinned by tests/test_abi.py).
 FLOW_RULE_DTYPE = np.dtype({
-    "names": ["resource", "grade", "count", "strategy", "control_behavior", "warm_up_period_sec",
-              "max_queueing_time_ms", "cluster_mode", "ref_resource"],
-    "formats": [np.uint32, np.int32, np.float64, np.int32, np.int32, np.int32, np.int32, np.int32, np.uint32],
-    "offsets": [f[1].offset for f in [(n, getattr(sf_flow_rule, n)) for n, _ in sf_flow_rule._fields_]],
+    "names": [n for n, _ in sf_flow_rule._fields_],
+    "formats": [{C.c_uint32: np.uint32, C.c_int32: np.int32, C.c_double: np.float64}[t] for _, t in sf_flow_rule._fields_],
+    "offsets": [getattr(sf_flow_rule, n).offset for n, _ in sf_flow_rule._fields_],
     "itemsize": C.sizeof(sf_flow_rule)})
 
 
