@@ -18,8 +18,9 @@
 // into ONE segment (k_keys_packed maps every member to the group key), so one
 // lane replays the group in submission order — a RELATE check reads the other
 // resource's ClusterNode exactly as the events before it left it.  All node
-// state of the walk lives in HBM (loaded into a NodeWin per event and stored
-// back); origin and context nodes sit in a pool indexed by an exact hash table.
+// state of the walk lives in HBM (held in NodeWins while consecutive events
+// use the same node, stored back on a switch); origin and context nodes sit in
+// a pool indexed by an exact hash table.
 // This is the rare path: the common DIRECT/"default" rules never come here.
 #pragma once
 #include <vector>
@@ -115,9 +116,15 @@ SF_HD int xflow_select(const DevState& st, const DevRule& r, uint32_t r0, uint32
 }
 
 // One group segment [lo, hi) (events of several resources, submission order).
+// The current resource's ClusterNode and the last origin / context node stay
+// in registers while consecutive events use them (a group of one resource
+// keeps its node for the whole segment); a switch stores the old node back
+// first, so a RELATE read of another member always sees HBM up to date.
 template <int MAXS>
 SF_HD void decide_xgroup(const DevState& st, const SegIO& io, uint32_t lo, uint32_t hi) {
     const ParamTable pt{st.ptab, st.pcap_mask, st.err};
+    NodeWin<MAXS> cn, on, dn;
+    uint32_t cl = XNONE, oi = XNONE, di = XNONE;          // nodes held in cn / on / dn
     for (uint32_t j = lo; j < hi; j++) {
         const uint32_t i = io.perm[j];
         const uint32_t gres = io.ev_res[i];
@@ -136,13 +143,25 @@ SF_HD void decide_xgroup(const DevState& st, const SegIO& io, uint32_t lo, uint3
             if (r.strategy == SF_STRATEGY_DIRECT && r.limit_app != SF_APP_DEFAULT) want_on = true;
             if (r.strategy == SF_STRATEGY_CHAIN && r.ref == ctx) want_dn = true;
         }
-        const NodeRows cr = cluster_rows(st, l);
-        NodeWin<MAXS> cn, on, dn;
-        nw_load(cn, st, cr);
-        const uint32_t oi = (want_on && origin != SF_ORIGIN_NONE) ? aux_get(st, l, AX_ORIGIN, origin) : XNONE;
-        const uint32_t di = want_dn ? aux_get(st, l, AX_CTX, ctx) : XNONE;
-        if (oi != XNONE) nw_load(on, st, aux_rows(st, oi));
-        if (di != XNONE) nw_load(dn, st, aux_rows(st, di));
+        if (l != cl) {
+            if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl));
+            nw_load(cn, st, cluster_rows(st, l));
+            cl = l;
+        }
+        {
+            const uint32_t k = (want_on && origin != SF_ORIGIN_NONE) ? aux_get(st, l, AX_ORIGIN, origin) : XNONE;
+            if (k != oi) {
+                if (oi != XNONE) nw_store(on, st, aux_rows(st, oi));
+                if (k != XNONE) nw_load(on, st, aux_rows(st, k));
+                oi = k;
+            }
+            const uint32_t m = want_dn ? aux_get(st, l, AX_CTX, ctx) : XNONE;
+            if (m != di) {
+                if (di != XNONE) nw_store(dn, st, aux_rows(st, di));
+                if (m != XNONE) nw_load(dn, st, aux_rows(st, m));
+                di = m;
+            }
+        }
         const uint32_t p0 = st.prule_off[l], p1 = st.prule_off[l + 1];
         const int nprules = (int)(p1 - p0);
         uint8_t pm_init = nprules ? st.pm_init[l] : 0;
@@ -263,13 +282,13 @@ SF_HD void decide_xgroup(const DevState& st, const SegIO& io, uint32_t lo, uint3
                 if (pm_exists) pm_thread_event(pt, l, pm_init, io, j, na, +1);
             }
         }
-        nw_store(cn, st, cr);
-        if (oi != XNONE) nw_store(on, st, aux_rows(st, oi));
-        if (di != XNONE) nw_store(dn, st, aux_rows(st, di));
         if (nprules) st.pm_init[l] = pm_init;
         io.v_status[j] = status;
         emit_verdict(io, j, status, (int32_t)wait, (uint16_t)rule_idx);
     }
+    if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl));
+    if (oi != XNONE) nw_store(on, st, aux_rows(st, oi));
+    if (di != XNONE) nw_store(dn, st, aux_rows(st, di));
 }
 
 // ============================================================ groups (host side)
