@@ -788,9 +788,10 @@ inline bool valid_flow_rule(const sf_flow_rule& r) {
 // ref_local: RELATE's referenced resource as a local id (XNONE: none); CHAIN keeps the context id
 inline DevRule make_dev_rule(const sf_flow_rule& r, int cold_factor, int host_index, uint32_t ref_local = XNONE) {
     DevRule d{};
-    d.grade = r.grade; d.count = r.count; d.max_queue_ms = r.max_queueing_time_ms;
+    d.grade = (uint8_t)r.grade; d.count = r.count; d.max_queue_ms = r.max_queueing_time_ms;
     d.cold_factor = cold_factor; d.host_index = host_index;
-    d.strategy = r.strategy; d.limit_app = r.limit_app;
+    d.strategy = (uint8_t)(r.strategy <= SF_STRATEGY_CHAIN ? r.strategy : 3);   // 3+: no reference node
+    d.limit_app = r.limit_app;
     d.ref = r.strategy == SF_STRATEGY_RELATE ? ref_local : r.ref_resource;
     d.always_pass = (r.cluster_mode && !r.cluster_fallback) ? 1 : 0;
     d.kind = CT_DEFAULT;

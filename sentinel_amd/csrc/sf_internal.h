@@ -32,20 +32,21 @@ struct Borrow {          // WindowWrap<MetricBucket> of FutureBucketLeapArray: o
 // Controller kinds (FlowRuleUtil.generateRater, FlowRuleUtil.java:132-152)
 enum : int32_t { CT_DEFAULT = 0, CT_WARM_UP = 1, CT_RATE_LIMITER = 2, CT_WARM_UP_RATE_LIMITER = 3 };
 
-struct DevRule {         // 64 B, constants precomputed at load (WarmUpController.construct :113-139)
-    int32_t kind, grade;
+struct DevRule {         // 48 B, constants precomputed at load (WarmUpController.construct :113-139)
+    uint8_t kind, grade;
+    uint8_t strategy;              // SF_STRATEGY_* (>= 3: another value, selects no node)
+    uint8_t always_pass;           // cluster rule without fallback (no token service in the process)
+    int32_t max_queue_ms;
     double count;
-    int32_t warning_token, max_token;
     double slope;
-    int32_t cold_factor, max_queue_ms;
-    int32_t host_index, strategy;
+    int32_t warning_token, max_token;
+    int32_t cold_factor, host_index;
     // node selection (FlowRuleChecker.selectNodeByRequesterAndStrategy :129-161);
     // rules other than limitApp "default" + DIRECT run on the xflow walk (sf_xflow.h)
     uint32_t limit_app;            // SF_APP_DEFAULT / SF_APP_OTHER / origin id
     uint32_t ref;                  // RELATE: local resource id (XNONE: never a node); CHAIN: context id
-    int32_t always_pass;           // cluster rule without fallback (no token service in the process)
-    int32_t pad;
 };
+static_assert(sizeof(DevRule) == 48, "DevRule layout");
 constexpr uint32_t XNONE = 0xFFFFFFFFu;
 struct DevRuleState {    // AtomicLong fields of the controllers
     int64_t stored_tokens, last_filled, latest_passed, pad;
