@@ -527,6 +527,7 @@ int sf_load_param_rules(sf_engine* e, const sf_param_rule* rules, uint32_t n, co
     std::vector<DevHotItem> di(n_items);
     for (uint32_t i = 0; i < n_items; i++) { di[i].bits = items[i].bits; di[i].count = items[i].count; di[i].tag = items[i].tag; }
     e->n_prule = n;
+    e->st.n_prule = n;
     if (e->st.prules) { hipFree(e->st.prules); e->st.prules = nullptr; }
     if (e->st.items) { hipFree((void*)e->st.items); e->st.items = nullptr; }
     HIP_TRY(hipMalloc((void**)&e->st.prules, std::max<size_t>(1, dp.size()) * sizeof(DevParamRule)));

@@ -80,6 +80,7 @@ struct DevState {
     const DevRule* rules;
     DevRuleState* rstate;
     const uint32_t* prule_off;     // [R+1]
+    uint32_t n_prule;              // ParamFlow rules loaded (0: no segment needs the ParamFlow routing flags)
     DevParamRule* prules;          // param_idx is mutated (ParamFlowSlot.applyRealParamIdx)
     const DevHotItem* items;
     uint8_t* pm_init;              // [R] bitmask: thread maps created per paramIdx (<8)

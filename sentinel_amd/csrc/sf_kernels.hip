@@ -80,7 +80,7 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t
 __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* keys, uint32_t* perm, int64_t* s_ts,
                          int32_t* s_cnt, uint8_t* s_flags, uint8_t* s_nargs, uint8_t* s_atag,
                          uint64_t* s_abits, const uint32_t* head_scan, uint32_t* seg_start, uint32_t* seg_res,
-                         uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts, const int32_t* err) {
+                         uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts, const int32_t* err, bool exit_marks) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
     const uint32_t sid = head_scan[j] - 1;
@@ -94,11 +94,17 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* keys, u
     const uint8_t f = (uint8_t)(v.meta >> 16);
     perm[j] = i;
     s_ts[j] = dts != PV_DTS_FAR ? b.ts[0] + (int64_t)dts : b.ts[i]; s_cnt[j] = c; s_flags[j] = f;
-    {   // the segment has exits: one atomic per run of exits within a wavefront
+    if (exit_marks) {
+        // the segment has exits (read only by the ParamFlow routing, heavy_mode):
+        // one atomic per segment and wavefront, by the segment's first exit lane
         const bool ex = (f & SF_EV_EXIT) != 0;
         const int lane = (int)(threadIdx.x & 63);
-        const int pex = __shfl_up((int)ex, 1), psid = __shfl_up((int)sid, 1);
-        if (ex && !(lane > 0 && pex && (uint32_t)psid == sid)) atomicOr(&segflag[sid], SEGF_EXIT);
+        const int psid = __shfl_up((int)sid, 1);
+        const unsigned long long heads = __ballot(lane == 0 || (uint32_t)psid != sid);
+        const unsigned long long em = __ballot(ex);
+        const unsigned long long below = (1ull << lane) - 1ull;
+        const int sl = 63 - __builtin_clzll(heads & (below | (1ull << lane)));   // this segment's first lane
+        if (ex && !(em & below & ~((1ull << sl) - 1ull))) atomicOr(&segflag[sid], SEGF_EXIT);
     }
     if (!(f & SF_EV_EXIT) && ((f & (SF_EV_PRIO | EVF_SYSBLK)) || c <= 0)) {
         atomicOr(&segflag[sid], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) |
@@ -917,7 +923,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     if (timing) hipEventRecord(ev[1], s);
     hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.keys_out, w.perm, w.s_ts, w.s_cnt,
                        w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan, w.seg_start, w.seg_res, w.n_seg,
-                       w.segflag, st.last_ts, st.err);
+                       w.segflag, st.last_ts, st.err, st.n_prule != 0);
     hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags,
