@@ -766,6 +766,82 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
     if (nprules) st.pm_init[res] = pm_init;
 }
 
+// The lean lane walk of a segment whose resource has exactly one rule, a
+// QPS-grade DefaultController, and nothing else in the chain (no ParamFlow
+// rules, no breakers) and whose entries are neither prioritized nor blocked by
+// a planned SystemBlockException (k_classify routes on the segment flags).
+// This is exactly decide_segment's path for such a segment
+// (DefaultController.canPass :50-72, StatisticSlot entry / exit accounting
+// :55-178) with a fraction of its live registers (no controller state, params,
+// breakers, occupy path), so more wavefronts fit per SIMD.
+template <int MAXS>
+SF_HD void decide_qps_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi) {
+    NodeWin<MAXS> nd;
+    nd.S = st.S; nd.wl = st.wl; nd.interval = st.interval; nd.max_rt = st.max_rt;
+    nd.interval_sec = st.interval / 1000.0;
+    for (int i = 0; i < MAXS; i++) {
+        if (i < st.S) { nd.sec[i] = st.second[(size_t)res * st.S + i]; nd.bor[i] = st.borrow[(size_t)res * st.S + i]; }
+        else { nd.sec[i] = fresh_bucket(WS_NONE, st.max_rt); nd.bor[i].ws = WS_NONE; nd.bor[i].pass = 0; }
+    }
+    nd.threads = st.threads[res];
+    nd.gmin = st.minute + (size_t)res * MINUTE;
+    nd.mi = -1; nd.mdirty = 0;
+    nd.mb = fresh_bucket(WS_NONE, st.max_rt);
+    const double count = st.rules[st.rule_off[res]].count;
+    for (uint32_t j = lo; j < hi; j++) {
+        const int64_t now = io.ts[j];
+        const int32_t c = io.cnt[j];
+        const uint8_t fl = io.flags[j];
+        uint8_t status;
+        if (fl & SF_EV_EXIT) {                                  // StatisticSlot.exit :134-165
+            int64_t ref = io.eref ? io.eref[j] : -1;
+            bool blocked; int64_t create_ts;
+            if (ref >= 0) {
+                if (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT)) { *st.err = SF_ERR_INVALID; ref = j; }
+                blocked = ref == (int64_t)j ? true : v_blocked(io.v_status[ref]);
+                create_ts = io.ts[ref];
+            } else {
+                blocked = ref == EREF_DEAD; create_ts = io.cts ? io.cts[j] : now;
+            }
+            if (!blocked) {
+                nd.add_rt_success(now, now - create_ts, c);
+                nd.threads--;
+                if (fl & SF_EV_ERROR) nd.add_exception(now, c);
+                status = SF_V_EXIT;
+            } else {
+                status = SF_V_EXIT_IGNORED;
+            }
+        } else {
+            const int32_t cur = j_d2i(nd.pass_qps(now));
+            if ((double)(int32_t)((uint32_t)cur + (uint32_t)c) > count) {
+                nd.add_block(now, c); status = SF_V_BLOCK_FLOW;
+            } else {
+                nd.threads++; nd.add_pass(now, c); status = SF_V_PASS;
+            }
+        }
+        io.v_status[j] = status;
+        emit_verdict(io, j, status, 0, 0);
+    }
+    for (int i = 0; i < MAXS; i++)
+        if (i < st.S) {
+            st.second[(size_t)res * st.S + i] = nd.sec[i];
+            if (nd.bdirty) st.borrow[(size_t)res * st.S + i] = nd.bor[i];
+        }
+    nd.min_flush();
+    st.threads[res] = nd.threads;
+}
+
+// k_classify: the lean walk applies to this segment (SM_LIGHTQ)
+constexpr uint32_t SEGF_PRIO_ = 1u, SEGF_SYS_ = 4u;   // = SEGF_PRIO / SEGF_SYS (sf_heavy.h)
+SF_HD bool qps_lean(const DevState& st, uint32_t res, uint32_t segflags) {
+    if (segflags & (SEGF_PRIO_ | SEGF_SYS_)) return false;
+    const uint32_t r0 = st.rule_off[res];
+    if (st.rule_off[res + 1] != r0 + 1 || st.prule_off[res + 1] != st.prule_off[res]) return false;
+    if (st.dg_rr_of && st.dg_rr_of[res] < st.dg_n) return false;
+    const DevRule& r = st.rules[r0];
+    return r.kind == CT_DEFAULT && r.grade == SF_GRADE_QPS;
+}
+
 // ============================================================ rule tables (host side)
 // FlowRuleUtil.isValidRule (FlowRuleUtil.java:170-185) + checkStrategyField (:236-241)
 // + checkControlBehaviorField (:243-254); a cluster rule's ClusterFlowConfig is

@@ -233,13 +233,14 @@ static int alloc_work(sf_engine* e, Work& w) {
     }
     const size_t SC = std::min<size_t>(N, R) + 1;
     w.seg_cap = (uint32_t)SC;
-    WALLOC(w.segflag, SC * 4); WALLOC(w.seg_mode, SC); WALLOC(w.lcounts, LCLS * 4);
+    WALLOC(w.segflag, SC * 4); WALLOC(w.seg_mode, SC); WALLOC(w.lcounts, 2 * LCLS * 4);
     {   // light_list regions per length class: class c holds segments of >= lo_len(c) events
         size_t off = 0;
         for (int k = 0; k < LCLS; k++) {
             const size_t lo_len = k == 0 ? 1 : (k == 1 ? 2 : ((size_t)1 << (k - 1)) + 1);
             const size_t cap = lo_len > w.heavy_min ? 0 : std::min<size_t>(SC, N / lo_len + 1);
             w.loff[k] = (uint32_t)off;
+            w.lcap[k] = (uint32_t)cap;
             off += cap;
         }
         WALLOC(w.light_list, off * 4);

@@ -28,8 +28,9 @@ namespace sf {
 
 // segment modes (seg_mode[s])
 enum : uint8_t { SM_LIGHT = 0, SM_GENERIC = 1, SM_QPS = 2, SM_WARM = 3, SM_RL = 4, SM_NORULE = 5, SM_THREAD = 6,
-                 SM_PARAM = 7, SM_XFLOW = 8 };
-constexpr uint32_t SEGF_PRIO = 1u, SEGF_NONPOS = 2u, SEGF_SYS = 4u, SEGF_EXIT = 8u, SEGF_COLL = 16u;
+                 SM_PARAM = 7, SM_XFLOW = 8,
+                 SM_LIGHTQ = 9 };   // short light segment of a lone QPS DefaultController rule (decide_qps_segment)
+constexpr uint32_t SEGF_PRIO = SEGF_PRIO_, SEGF_NONPOS = 2u, SEGF_SYS = SEGF_SYS_, SEGF_EXIT = 8u, SEGF_COLL = 16u;
 
 struct Acc {            // per (segment, window) counter deltas
     unsigned long long pass, block, succ, rt, exc, n_pass, n_exit, n_touch;

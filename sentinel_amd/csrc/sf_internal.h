@@ -184,8 +184,9 @@ struct Work {
     uint32_t seg_cap;                                   // min(max_batch, R)
     uint32_t* segflag; uint8_t* seg_mode;
     uint32_t* light_list; uint32_t* heavy_list; uint32_t* counters;
-    uint32_t* lcounts;                                  // [LCLS] light segments per length class
-    uint32_t loff[LCLS];                                // light_list region of each length class   // [0] n_light [1] n_heavy front [2] hw slots [3] sec slots [4] n_heavy back
+    uint32_t* lcounts;                                  // [2][LCLS] light segments per length class: generic, lean QPS
+    uint32_t loff[LCLS];                                // light_list region of each class: generic from the
+    uint32_t lcap[LCLS];                                //   front, lean QPS (SM_LIGHTQ) from the back                                // light_list region of each length class   // [0] n_light [1] n_heavy front [2] hw slots [3] sec slots [4] n_heavy back
                                                                       // [5] n_stream front [6] n_stream back
     int64_t* pcg; void* pscan_tmp; size_t pscan_tmp_bytes;
     uint2* fill_tiles; uint32_t fill_tile_cap;         // [2][cap] (segment, tile) of each class for k_heavy_fill

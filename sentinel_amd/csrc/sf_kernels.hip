@@ -198,15 +198,27 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
         light = false;
     // light list slot: workgroup histogram of the length classes in LDS, one
     // global atomic per class and workgroup
-    __shared__ uint32_t hcnt[LCLS], hbase[LCLS];
-    if (threadIdx.x < LCLS) hcnt[threadIdx.x] = 0;
+    // (hcnt / hbase [0, LCLS): generic lane walk, [LCLS, 2 LCLS): lean QPS walk)
+    __shared__ uint32_t hcnt[2 * LCLS], hbase[2 * LCLS];
+    if (threadIdx.x < 2 * LCLS) hcnt[threadIdx.x] = 0;
     __syncthreads();
+    // a segment of a resource whose only check is one QPS DefaultController rule
+    // runs the lean lane walk (decide_qps_segment: k_decide_short_qps / k_decide_light_qps)
+    const bool lean = light && qps_lean(st, res, w.segflag[s]);
     const int lc = (light && hi - lo > SHORT_MAX) ? light_class(hi - lo) : -1;
-    const uint32_t lrank = lc >= 0 ? atomicAdd(&hcnt[lc], 1u) : 0u;
+    const int hk = lc + (lean ? LCLS : 0);
+    const uint32_t lrank = lc >= 0 ? atomicAdd(&hcnt[hk], 1u) : 0u;
     __syncthreads();
-    if (threadIdx.x < LCLS) hbase[threadIdx.x] = hcnt[threadIdx.x] ? atomicAdd(&w.lcounts[threadIdx.x], hcnt[threadIdx.x]) : 0u;
+    if (threadIdx.x < 2 * LCLS)
+        hbase[threadIdx.x] = hcnt[threadIdx.x] ? atomicAdd(&w.lcounts[threadIdx.x], hcnt[threadIdx.x]) : 0u;
     __syncthreads();
-    if (light) { w.seg_mode[s] = SM_LIGHT; if (lc >= 0) w.light_list[w.loff[lc] + hbase[lc] + lrank] = s; }
+    if (light) {
+        w.seg_mode[s] = lean ? SM_LIGHTQ : SM_LIGHT;
+        if (lc >= 0) {
+            if (lean) w.light_list[w.loff[lc] + w.lcap[lc] - 1 - (hbase[hk] + lrank)] = s;
+            else w.light_list[w.loff[lc] + hbase[hk] + lrank] = s;
+        }
+    }
     const bool heavy = valid && !light && !xs;
     if (!__ballot(heavy)) return;
     uint8_t mode = SM_GENERIC;
@@ -258,7 +270,7 @@ __device__ __forceinline__ bool heavy_at(const HeavyCtx& hc, uint32_t b, uint32_
     return false;
 }
 
-struct LightLists { const uint32_t* list; const uint32_t* counts; uint32_t off[LCLS]; };
+struct LightLists { const uint32_t* list; const uint32_t* counts; uint32_t off[LCLS]; uint32_t cap[LCLS]; };
 
 // One lane per light segment; thread t walks the length classes from the
 // longest down, so a wavefront holds segments of one class (similar length)
@@ -281,6 +293,23 @@ __global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_light(DevState st
     decide_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
 }
 
+// The lean QPS light segments (SM_LIGHTQ, > SHORT_MAX events) from the back
+// of each class region, longest class first (decide_qps_segment).
+template <int MAXS>
+__global__ void __launch_bounds__(128) k_decide_light_qps(DevState st, SegIO io, const uint32_t* seg_start,
+                                                          const uint32_t* seg_res, LightLists ll) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    int c = LCLS - 1;
+    for (; c >= 0; c--) {
+        const uint32_t n = ll.counts[LCLS + c];
+        if (t < n) break;
+        t -= n;
+    }
+    if (c < 0) return;
+    const uint32_t s = ll.list[ll.off[c] + ll.cap[c] - 1 - t];
+    decide_qps_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
+}
+
 // One lane per short light segment, in sorted order (see SHORT_MAX).
 template <int MAXS>
 __global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_short(DevState st, SegIO io, const uint32_t* seg_start,
@@ -300,6 +329,19 @@ __global__ void __launch_bounds__(64) k_decide_x(DevState st, SegIO io, const ui
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= *n_seg || seg_mode[s] != SM_XFLOW) return;
     decide_xgroup<MAXS>(st, io, seg_start[s], seg_start[s + 1]);
+}
+
+// One lane per short segment routed to the lean QPS walk (SM_LIGHTQ), in
+// sorted order like k_decide_short.
+template <int MAXS>
+__global__ void __launch_bounds__(128) k_decide_short_qps(DevState st, SegIO io, const uint32_t* seg_start,
+                                                          const uint32_t* seg_res, const uint8_t* seg_mode,
+                                                          const uint32_t* n_seg) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= *n_seg || seg_mode[s] != SM_LIGHTQ) return;
+    const uint32_t lo = seg_start[s], hi = seg_start[s + 1];
+    if (hi - lo > SHORT_MAX) return;                        // (k_decide_light_qps)
+    decide_qps_segment<MAXS>(st, io, seg_res[s], lo, hi);
 }
 
 static HeavyCtx heavy_ctx(const Work& w) {
@@ -866,6 +908,20 @@ static inline unsigned blocks(size_t n, unsigned t) { return (unsigned)((n + t -
 
 using PcIter = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, EntryCount, int64_t>;
 using HeadIter = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, HeadFlag, uint32_t>;
+// rocprim has no tuned scan configs for gfx950 (its default is 256 threads x
+// 16 / 8 items); tools/micro/scanbench.hip at 2^27 elements: u32 heads 0.516
+// (default) -> 0.480 ms (256 x 21, warp scan), int64 counts 0.922 -> 0.822 ms
+// (256 x 12, warp scan)
+#ifndef SF_HEAD_SCAN_CFG
+#define SF_HEAD_SCAN_CFG rocprim::scan_config<256, 21, rocprim::block_load_method::block_load_transpose, \
+    rocprim::block_store_method::block_store_transpose, rocprim::block_scan_algorithm::using_warp_scan>
+#endif
+#ifndef SF_PC_SCAN_CFG
+#define SF_PC_SCAN_CFG rocprim::scan_config<256, 12, rocprim::block_load_method::block_load_transpose, \
+    rocprim::block_store_method::block_store_transpose, rocprim::block_scan_algorithm::using_warp_scan>
+#endif
+using HeadScanCfg = SF_HEAD_SCAN_CFG;
+using PcScanCfg = SF_PC_SCAN_CFG;
 
 hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes,
                             size_t* pscan_bytes) {
@@ -878,11 +934,11 @@ hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_byte
     if (e != hipSuccess) return e;
     if (packed_bytes > *sort_bytes) *sort_bytes = packed_bytes;
     HeadIter hit(rocprim::counting_iterator<uint32_t>(0), HeadFlag{nullptr});
-    e = rocprim::inclusive_scan(nullptr, *scan_bytes, hit, (uint32_t*)nullptr, (size_t)max_n,
+    e = rocprim::inclusive_scan<HeadScanCfg>(nullptr, *scan_bytes, hit, (uint32_t*)nullptr, (size_t)max_n,
                                 rocprim::plus<uint32_t>());
     if (e != hipSuccess) return e;
     PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{nullptr, nullptr});
-    return rocprim::inclusive_scan(nullptr, *pscan_bytes, it, (int64_t*)nullptr, (size_t)max_n,
+    return rocprim::inclusive_scan<PcScanCfg>(nullptr, *pscan_bytes, it, (int64_t*)nullptr, (size_t)max_n,
                                    rocprim::plus<int64_t>());
 }
 
@@ -915,7 +971,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     if (e != hipSuccess) return e;
     {
         HeadIter hit(rocprim::counting_iterator<uint32_t>(0), HeadFlag{w.keys_out});
-        e = rocprim::inclusive_scan(w.scan_tmp, w.scan_tmp_bytes, hit, w.head_scan, (size_t)n,
+        e = rocprim::inclusive_scan<HeadScanCfg>(w.scan_tmp, w.scan_tmp_bytes, hit, w.head_scan, (size_t)n,
                                     rocprim::plus<uint32_t>(), s);
         if (e != hipSuccess) return e;
     }
@@ -929,10 +985,11 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags,
                            w.head_scan, w.seg_start, w.s_eref, w.s_cts, w.exit_of, st.err);
     PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
-    e = rocprim::inclusive_scan(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n, rocprim::plus<int64_t>(), s);
+    e = rocprim::inclusive_scan<PcScanCfg>(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n,
+                                           rocprim::plus<int64_t>(), s);
     if (e != hipSuccess) return e;
     hipMemsetAsync(w.counters, 0, 8 * sizeof(uint32_t), s);
-    hipMemsetAsync(w.lcounts, 0, LCLS * sizeof(uint32_t), s);
+    hipMemsetAsync(w.lcounts, 0, 2 * LCLS * sizeof(uint32_t), s);
     hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
     hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
     const uint32_t max_seg = n < st.R ? n : st.R;
@@ -992,16 +1049,24 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s, st, hc, sc, w.seg_nhw, w.seg_nsec, 1);
 
     const unsigned TD = 128;
-    LightLists ll{w.light_list, w.lcounts, {}};
-    for (int c = 0; c < LCLS; c++) ll.off[c] = w.loff[c];
+    LightLists ll{w.light_list, w.lcounts, {}, {}};
+    for (int c = 0; c < LCLS; c++) { ll.off[c] = w.loff[c]; ll.cap[c] = w.lcap[c]; }
     if (st.S <= 2) {
         hipLaunchKernelGGL(k_decide_light<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
                            w.seg_res, ll);
+        hipLaunchKernelGGL(k_decide_light_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+                           w.seg_res, ll);
+        hipLaunchKernelGGL(k_decide_short_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+                           w.seg_res, w.seg_mode, w.n_seg);
         hipLaunchKernelGGL(k_decide_short<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
                            w.seg_res, w.seg_mode, w.n_seg);
     } else {
         hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, ll);
+        hipLaunchKernelGGL(k_decide_light_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st,
+                           io, w.seg_start, w.seg_res, ll);
+        hipLaunchKernelGGL(k_decide_short_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st,
+                           io, w.seg_start, w.seg_res, w.seg_mode, w.n_seg);
         hipLaunchKernelGGL(k_decide_short<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, w.seg_mode, w.n_seg);
     }

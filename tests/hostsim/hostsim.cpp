@@ -283,9 +283,16 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
             if (e->st.S <= 2) decide_xgroup<2>(e->st, io, lo, hi);
             else decide_xgroup<SF_MAX_SAMPLE_COUNT>(e->st, io, lo, hi);
             break;
-        default:
+        default: {
+            // the lean QPS walk of short segments (k_classify's SM_LIGHTQ routing)
+            if (mode[s] == SM_LIGHT && qps_lean(e->st, res, segflag[s])) {
+                if (e->st.S <= 2) decide_qps_segment<2>(e->st, io, res, lo, hi);
+                else decide_qps_segment<SF_MAX_SAMPLE_COUNT>(e->st, io, res, lo, hi);
+                break;
+            }
             if (e->st.S <= 2) decide_segment<2>(e->st, io, res, lo, hi);
             else decide_segment<SF_MAX_SAMPLE_COUNT>(e->st, io, res, lo, hi);
+        }
         }
     }
     // k_heavy_fill
