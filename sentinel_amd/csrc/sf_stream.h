@@ -28,8 +28,8 @@ namespace sf {
 constexpr int HS_T = 256;                 // threads per workgroup
 constexpr int HS_PL = 8;                  // events per lane per chunk
 constexpr int HS_CH = HS_T * HS_PL;       // events per chunk (2048)
-// LDS: THREAD codes 2 x 8 KiB + pass ring 16 KiB; RL timestamps 2 x 16 KiB + counts 2 x 8 KiB
-constexpr int HS_LDS_WORDS = (2 * HS_CH * 8 + 2 * HS_CH * 4) / 8;   // 48 KiB as u64 words
+// LDS: THREAD records 2 x 24 KiB + live-exit ring 16 KiB; RL timestamps 2 x 16 KiB + counts 2 x 8 KiB
+constexpr int HS_LDS_WORDS = (2 * HS_CH * 8 + 2 * HS_CH * 4) / 8;   // RL: 48 KiB as u64 words
 constexpr uint32_t CODE_EXIT = 0x80000000u;
 constexpr uint32_t CODE_DEAD = 0x7fffffffu;   // exit distance field: entry not in this segment (never live)
 
@@ -76,7 +76,10 @@ __device__ __forceinline__ void lds_barrier() {
 //     next live exit, or the next entry that fits at the current room).
 // Work is proportional to windows plus passes, not to events.
 constexpr uint32_t LX_WORDS = 2048;               // live-exit ring: 128 Ki events ahead (16 KiB)
-constexpr int THR_WPC = 24;                       // windows per chunk (8 per helper wave)
+#ifndef SF_THR_WPC
+#define SF_THR_WPC 48
+#endif
+constexpr int THR_WPC = SF_THR_WPC;               // windows per chunk (16 per helper wave, <= 64 lanes)
 constexpr uint32_t THR_CH = THR_WPC * 64;          // events per chunk
 constexpr uint32_t XO_NONE = 0xffffffffu;
 constexpr int32_t THR_CSMALL = 8;                  // scalar walk for acquireCount <= 8
@@ -106,7 +109,9 @@ __device__ __forceinline__ int32_t rec_c(uint2 r) { return (int32_t)r.y; }      
 __device__ __forceinline__ int rec_d(uint2 r) {                                         // exits: distance, or 0
     return (r.y & THR_REC_EXIT) && r.x < 65536u ? (int)r.x : 0;
 }
-static_assert(sizeof(ThrLds) <= HS_LDS_WORDS * 8, "THREAD LDS layout exceeds the stream kernel's LDS");
+static_assert(THR_WPC % 3 == 0 && THR_WPC <= 64, "one decider lane per window, windows split over 3 helpers");
+// the kernel's LDS: the larger of the THREAD and RateLimiter layouts
+constexpr int HS_SMEM_WORDS = (int)(sizeof(ThrLds) + 7) / 8 > HS_LDS_WORDS ? (int)(sizeof(ThrLds) + 7) / 8 : HS_LDS_WORDS;
 
 __device__ __forceinline__ int64_t uniform64(int64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
@@ -118,6 +123,12 @@ __device__ __forceinline__ int64_t uniform64_at(int64_t v, int l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
+__device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) {
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((unsigned long long)b << 32) | a;
+}
+
 __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) {
     return (unsigned long long)uniform64((int64_t)v);
 }
@@ -132,7 +143,7 @@ __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long v) 
 constexpr int THR_WPW = THR_WPC / 3;              // windows per helper wave
 struct ThrPre {
     uint2 rec[THR_WPW];
-    unsigned long long f0a[THR_WPW], f1a[THR_WPW];
+    unsigned long long f0, f1;                     // far live-exit words of window k in lane k
 };
 __device__ __forceinline__ void thr_issue(ThrPre& P, const uint2* rec, const unsigned long long* lxfar,
                                           uint32_t q0, uint32_t hi, int h) {
@@ -141,10 +152,12 @@ __device__ __forceinline__ void thr_issue(ThrPre& P, const uint2* rec, const uns
     for (int k = 0; k < THR_WPW; k++) {
         const uint32_t q = min(q0, hi) + 64u * (uint32_t)(h - 1 + 3 * k);
         P.rec[k] = rec[min(q + (uint32_t)lane, hi - 1)];
-        const uint32_t g = min(q, hi - 1) >> 6;
-        P.f0a[k] = __hip_atomic_load(lxfar + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        P.f1a[k] = __hip_atomic_load(lxfar + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // the two far-bitmap words under window k, loaded by lane k (two loads per chunk)
+    const uint32_t qk = min(q0, hi) + 64u * (uint32_t)(h - 1 + 3 * min(lane, THR_WPW - 1));
+    const uint32_t g = min(qk, hi - 1) >> 6;
+    P.f0 = __hip_atomic_load(lxfar + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    P.f1 = __hip_atomic_load(lxfar + g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ void thr_finish(ThrLds& L, int buf, const ThrPre& P, uint32_t q0, uint32_t lo, uint32_t hi, int h) {
     const int lane = (int)(threadIdx.x & 63);
@@ -167,11 +180,12 @@ __device__ void thr_finish(ThrLds& L, int buf, const ThrPre& P, uint32_t q0, uin
         wn.maxrc = gt8 ? INT32_MAX : (int32_t)__popcll(wn.ent) - 1 + (gt1 ? THR_CSMALL : 1);
         L.rec[buf][64 * wl + lane] = valid ? r : make_uint2(XO_NONE, THR_REC_EXIT);
         const unsigned long long mo = __ballot(ex && (r.y & THR_REC_LIVE));   // entry of an earlier batch: live
+        const unsigned long long f0 = rl64(P.f0, k), f1 = rl64(P.f1, k);
         if (lane == 0) {
             L.win[buf][wl] = wn;
             // live exits of far-away entries (written into HBM when those entries passed)
             const uint32_t sh = q & 63;
-            const unsigned long long far = sh ? (P.f0a[k] >> sh) | (P.f1a[k] << (64 - sh)) : P.f0a[k];
+            const unsigned long long far = sh ? (f0 >> sh) | (f1 << (64 - sh)) : f0;
             const unsigned long long add = (mo | far) & (q + 64 <= hi ? ~0ull : ((1ull << (hi - q)) - 1ull));
             if (add) atomicOr(&L.lx[((q - lo) >> 6) % LX_WORDS], add);
         }
@@ -255,12 +269,6 @@ __device__ __forceinline__ unsigned long long thr_window_solve(int room0, unsign
         if (j1 < ne) forced |= 1ull << j1;
     }
     return pm;
-}
-
-__device__ __forceinline__ unsigned long long rl64(unsigned long long v, int l) {
-    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-    return ((unsigned long long)b << 32) | a;
 }
 
 // THR_SW consecutive windows whose entries all fit are taken in one step.
@@ -656,7 +664,7 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
 // them one segment at a time.  Every workgroup leaves when the queue is
 // exhausted.
 __global__ void __launch_bounds__(HS_T) k_heavy_stream(DevState st, SegIO io, HeavyCtx hc, StreamCtx sc) {
-    __shared__ unsigned long long smem[HS_LDS_WORDS];
+    __shared__ unsigned long long smem[HS_SMEM_WORDS];
     __shared__ uint32_t slot;
     while (true) {
         if (threadIdx.x == 0) slot = atomicAdd(sc.next, 1u);
