@@ -2,10 +2,10 @@
 //
 // Sort phase (sort stream, one of two Work sets; overlaps the previous
 // batch's decide phase):
-//   k_keys_packed  validate + map resource ids to shard-local keys, 16-B payload
+//   k_keys_packed  validate + map resource ids to shard-local keys, 8-B payload
 //   radix sort     stable (key, payload) sort by resource: per-resource time order
 //                  is the input order (LeapArray semantics need it)
-//   k_heads + exclusive scan + k_segments   segment table of touched resources
+//   head scan      inclusive scan of segment-head flags (segment table written by k_unpack)
 //   k_unpack       events into sorted order (SoA), per-segment flags
 //   k_gather_exit  exits: sorted position of the entry (binary search in its segment), exit_of map
 //   pc scan        inclusive prefix of entry acquireCount (heavy window budgets)
