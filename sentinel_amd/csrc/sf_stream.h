@@ -334,6 +334,24 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
 #endif
             if (!stop) { w = nwin; break; }
             const uint32_t k = (uint32_t)(__ffsll((long long)stop) - 1);
+            // The first window with live exits, x: when all of them follow its last
+            // entry, its entries block too and the exits only release threads, as
+            // do the live exits of the entry-free windows after it.  The skipped
+            // run, x and that entry-free run are taken in this one step.
+            const uint32_t x = w + k;
+            const bool tail = r_lx != 0ull &&
+                              (r_ent == 0ull || 63 - (int)__builtin_clzll(r_ent) < (int)__builtin_ctzll(r_lx));
+            const unsigned long long tailm = __ballot((uint32_t)lane < nwin && tail) & ~bigm;
+            if ((tailm >> x) & 1ull) {
+                const unsigned long long ne = __ballot((uint32_t)lane < nwin && r_ent == 0ull) >> (x + 1);
+                const uint32_t e = min(x + 1 + (uint32_t)(__ffsll((long long)~ne) - 1), nwin);
+                const bool in = (uint32_t)lane >= x && (uint32_t)lane < e;
+                const int nl = wave_scan_add(in ? __popcll(r_lx) : 0);
+                T = uniform64(T - (int64_t)__builtin_amdgcn_readlane(nl, 63));
+                if (in) L.lx[(slot0 + (uint32_t)lane) % LX_WORDS] = 0ull;
+                w = e;
+                continue;
+            }
             if (k > 0) { w += k; continue; }
         }
         const unsigned long long me = rl64(r_ent, (int)w);
