@@ -58,6 +58,44 @@ def test_heavy_thread_long_range(eng_mod, so):
     workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
 
 
+def ms_block_thread_workload(seed, n_entry=200_000, duration=300, count=50.0, rt_mean=5.0):
+    """One saturated THREAD-grade resource with the config-3 head's layout:
+    every millisecond holds its entries, then the exits that fall due in it
+    (so runs of entry-only windows end in a window whose live exits all follow
+    its entries, then exit-only windows); acquireCount 1 (90 %), 2-5, and a
+    few above 2^20 (the exact walk's int-wrap guard), two batches."""
+    rng = np.random.default_rng(900 + seed)
+    ts = np.sort(rng.integers(0, duration, n_entry)).astype(np.int64) + trace.T0
+    acq = np.ones(n_entry, np.int32)
+    multi = rng.random(n_entry) < 0.1
+    acq[multi] = rng.integers(2, 6, int(multi.sum()))
+    acq[rng.choice(n_entry, 8, replace=False)] = 1 << 21
+    rt = np.floor(rng.exponential(rt_mean, n_entry)).astype(np.int64)
+    ets = np.minimum(ts + rt, trace.T0 + duration - 1)
+    all_ts = np.concatenate([ts, ets])
+    isx = np.concatenate([np.zeros(n_entry, bool), np.ones(n_entry, bool)])
+    order = np.lexsort((isx, all_ts))
+    pos = np.empty(order.size, np.int64)
+    pos[order] = np.arange(order.size)
+    src = np.concatenate([np.arange(n_entry), np.arange(n_entry)])
+    fl = np.where(isx[order], abi.EV_EXIT | abi.EV_IN, abi.EV_IN).astype(np.uint8)
+    eref = np.full(order.size, -1, np.int64)
+    eref[pos[n_entry:]] = pos[:n_entry]
+    b = abi.HostBatch(np.zeros(order.size, np.uint32), all_ts[order], acq[src][order], fl, entry_ref=eref)
+    rules = [abi.sf_flow_rule(resource=0, grade=abi.GRADE_THREAD, count=count, control_behavior=0)]
+    k = b.n // 2
+    return dict(cfg=abi.default_config(max_resources=1, max_batch=b.n), flow=rules,
+                batches=[b.subset(0, k), b.subset(k, b.n)], nodes=[0], n_flow=1)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_heavy_thread_ms_blocks(eng_mod, so, seed):
+    """The saturated THREAD walk's merged step (skipped windows + a window
+    whose live exits follow its entries + the exit-only run) against the
+    oracle, on per-millisecond entry / exit blocks."""
+    workloads.run(eng_mod.FlowEngine, so.OracleEngine, ms_block_thread_workload(seed))
+
+
 def test_device_resident_batch(eng_mod, so):
     """Inputs already in HBM (the bench path): same verdicts as the host path."""
     w = workloads.config3(R=5000, n=200_000, seed=5, split=1)
