@@ -219,6 +219,30 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
             else w.light_list[w.loff[lc] + hbase[hk] + lrank] = s;
         }
     }
+    // short segments (<= SHORT_MAX events) listed densely for k_decide_short /
+    // k_decide_short_qps, in segment (resource) order within each workgroup,
+    // one global atomic per workgroup and list: a deciding wavefront's lanes
+    // hold neighbouring resource rows and no idle lanes for the segments of
+    // the other kernel.  Class 0's light_list region (every segment fits)
+    // holds both lists: generic from the front, lean QPS from the back.
+    static_assert(SHORT_MAX >= 1, "class 0 (one-event segments) must be a short class");
+    __shared__ uint32_t wsh[2][32], bsh[2];
+    const bool shrt = light && hi - lo <= SHORT_MAX;
+    const unsigned long long mg = __ballot(shrt && !lean), mq = __ballot(shrt && lean);
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6), nwv = (int)(blockDim.x >> 6);
+    if (lane == 0) { wsh[0][wv] = (uint32_t)__popcll(mg); wsh[1][wv] = (uint32_t)__popcll(mq); }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        uint32_t acc = 0;
+        for (int k = 0; k < nwv; k++) { const uint32_t c = wsh[threadIdx.x][k]; wsh[threadIdx.x][k] = acc; acc += c; }
+        bsh[threadIdx.x] = acc ? atomicAdd(&w.counters[8 + threadIdx.x], acc) : 0u;
+    }
+    __syncthreads();
+    if (shrt) {
+        const unsigned long long below = (1ull << lane) - 1ull;
+        if (lean) w.light_list[w.loff[0] + w.lcap[0] - 1 - (bsh[1] + wsh[1][wv] + (uint32_t)__popcll(mq & below))] = s;
+        else w.light_list[w.loff[0] + bsh[0] + wsh[0][wv] + (uint32_t)__popcll(mg & below)] = s;
+    }
     const bool heavy = valid && !light && !xs;
     if (!__ballot(heavy)) return;
     uint8_t mode = SM_GENERIC;
@@ -310,16 +334,16 @@ __global__ void __launch_bounds__(128) k_decide_light_qps(DevState st, SegIO io,
     decide_qps_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
 }
 
-// One lane per short light segment, in sorted order (see SHORT_MAX).
+// One lane per short light segment, from the dense short list (k_classify;
+// see SHORT_MAX).
 template <int MAXS>
 __global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_short(DevState st, SegIO io, const uint32_t* seg_start,
-                                                      const uint32_t* seg_res, const uint8_t* seg_mode,
-                                                      const uint32_t* n_seg) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= *n_seg || seg_mode[s] != SM_LIGHT) return;
-    const uint32_t lo = seg_start[s], hi = seg_start[s + 1];
-    if (hi - lo > SHORT_MAX) return;
-    decide_segment<MAXS>(st, io, seg_res[s], lo, hi);
+                                                      const uint32_t* seg_res, LightLists ll,
+                                                      const uint32_t* n_short) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_short[0]) return;
+    const uint32_t s = ll.list[ll.off[0] + t];
+    decide_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
 }
 
 // One lane per xflow group segment (sf_xflow.h): origin / context / RELATE rules.
@@ -331,17 +355,16 @@ __global__ void __launch_bounds__(64) k_decide_x(DevState st, SegIO io, const ui
     decide_xgroup<MAXS>(st, io, seg_start[s], seg_start[s + 1]);
 }
 
-// One lane per short segment routed to the lean QPS walk (SM_LIGHTQ), in
-// sorted order like k_decide_short.
+// One lane per short segment routed to the lean QPS walk (SM_LIGHTQ), from
+// the back of the dense short list like k_decide_short.
 template <int MAXS>
 __global__ void __launch_bounds__(128) k_decide_short_qps(DevState st, SegIO io, const uint32_t* seg_start,
-                                                          const uint32_t* seg_res, const uint8_t* seg_mode,
-                                                          const uint32_t* n_seg) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= *n_seg || seg_mode[s] != SM_LIGHTQ) return;
-    const uint32_t lo = seg_start[s], hi = seg_start[s + 1];
-    if (hi - lo > SHORT_MAX) return;                        // (k_decide_light_qps)
-    decide_qps_segment<MAXS>(st, io, seg_res[s], lo, hi);
+                                                          const uint32_t* seg_res, LightLists ll,
+                                                          const uint32_t* n_short) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_short[1]) return;
+    const uint32_t s = ll.list[ll.off[0] + ll.cap[0] - 1 - t];
+    decide_qps_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
 }
 
 static HeavyCtx heavy_ctx(const Work& w) {
@@ -988,7 +1011,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     e = rocprim::inclusive_scan<PcScanCfg>(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n,
                                            rocprim::plus<int64_t>(), s);
     if (e != hipSuccess) return e;
-    hipMemsetAsync(w.counters, 0, 8 * sizeof(uint32_t), s);
+    hipMemsetAsync(w.counters, 0, 10 * sizeof(uint32_t), s);
     hipMemsetAsync(w.lcounts, 0, 2 * LCLS * sizeof(uint32_t), s);
     hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
     hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
@@ -1057,18 +1080,18 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
         hipLaunchKernelGGL(k_decide_light_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
                            w.seg_res, ll);
         hipLaunchKernelGGL(k_decide_short_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
-                           w.seg_res, w.seg_mode, w.n_seg);
+                           w.seg_res, ll, w.counters + 8);
         hipLaunchKernelGGL(k_decide_short<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
-                           w.seg_res, w.seg_mode, w.n_seg);
+                           w.seg_res, ll, w.counters + 8);
     } else {
         hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, ll);
         hipLaunchKernelGGL(k_decide_light_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st,
                            io, w.seg_start, w.seg_res, ll);
         hipLaunchKernelGGL(k_decide_short_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st,
-                           io, w.seg_start, w.seg_res, w.seg_mode, w.n_seg);
+                           io, w.seg_start, w.seg_res, ll, w.counters + 8);
         hipLaunchKernelGGL(k_decide_short<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
-                           w.seg_start, w.seg_res, w.seg_mode, w.n_seg);
+                           w.seg_start, w.seg_res, ll, w.counters + 8);
     }
     if (st.xmap) {
         if (st.S <= 2)
