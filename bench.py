@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the whole-batch oracle replay (parity + cpu_baseline)")
     ap.add_argument("--no-metric-log", action="store_true")
     ap.add_argument("--no-degrade", action="store_true")
+    ap.add_argument("--heavy-min", type=int, default=0,
+                    help="segments of more events than this go to the heavy kernels (0: the engine default, 512)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -67,7 +69,7 @@ def main():
     log(f"[rank {rank}] trace {hb.n} events ({n_entry} entries) over {R_local} resources in {time.time()-t0:.1f}s")
 
     cfg = abi.default_config(max_resources=R_local, max_batch=hb.n, shard_count=world, shard_index=rank,
-                             device=local)
+                             device=local, heavy_min_events=args.heavy_min)
     eng = engine.FlowEngine(cfg)
     eng.load_flow_rules(rules)
     steps = args.warmup + args.steps
@@ -125,7 +127,7 @@ def main():
     # k_classify routes segments of more than heavy_min events to the heavy
     # kernels: THREAD-grade and RateLimiter ones to k_heavy_stream, the rest
     # to k_heavy_decide.
-    heavy_min = 512
+    heavy_min = args.heavy_min or 512
     local = hb.res_id // world if world > 1 else hb.res_id
     per_res = np.bincount(local, minlength=R_local)
     is_heavy_res = per_res > heavy_min
