@@ -196,6 +196,15 @@ typedef struct sf_system_rule {
 #define SF_EV_IN     0x02u   /* EntryType.IN (feeds ENTRY_NODE / SystemRule)   */
 #define SF_EV_PRIO   0x04u   /* prioritized entry                              */
 #define SF_EV_ERROR  0x08u   /* EXIT: business exception recorded (Tracer)     */
+/* ENTRY blocked by a slot that StatisticSlot wraps but the engine does not run
+ * (AuthoritySlot, order -6000, between StatisticSlot -7000 and SystemSlot
+ * -5000: Constants.java:80-84).  StatisticSlot.entry catches its
+ * BlockException (AuthorityException) like any other (StatisticSlot.java:102-124):
+ * block += count on the resource's ClusterNode and, for EntryType.IN, on
+ * ENTRY_NODE; no SystemRule / ParamFlowRule / FlowRule / breaker sees the
+ * entry; its EXIT records nothing (blockError set, :139).  Verdict
+ * SF_V_BLOCK_OTHER.                                                         */
+#define SF_EV_BLOCKED 0x10u
 
 #define SF_MEM_HOST   0
 #define SF_MEM_DEVICE 1
@@ -588,6 +597,7 @@ int  sf_entry_node_allreduce(sf_engine* e, sf_node_state* out);
 #define SF_DEGRADE_GRADE_EXCEPTION_RATIO 1
 #define SF_DEGRADE_GRADE_EXCEPTION_COUNT 2
 #define SF_V_BLOCK_DEGRADE 8   /* DegradeException (rule_idx = breaker index in the resource's list) */
+#define SF_V_BLOCK_OTHER   9   /* SF_EV_BLOCKED entry (AuthorityException): counted as a block, no check ran */
 #define SF_CB_CLOSED    0
 #define SF_CB_OPEN      1
 #define SF_CB_HALF_OPEN 2

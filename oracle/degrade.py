@@ -24,8 +24,8 @@ import numpy as np
 GRADE_RT, GRADE_EXC_RATIO, GRADE_EXC_COUNT = 0, 1, 2
 CLOSED, OPEN, HALF_OPEN = 0, 1, 2
 
-EV_EXIT, EV_ERROR = 0x01, 0x08
-V_PASS, V_EXIT, V_EXIT_IGNORED, V_BLOCK_DEGRADE = 0, 6, 7, 8
+EV_EXIT, EV_ERROR, EV_BLOCKED = 0x01, 0x08, 0x10
+V_PASS, V_EXIT, V_EXIT_IGNORED, V_BLOCK_DEGRADE, V_BLOCK_OTHER = 0, 6, 7, 8, 9
 
 
 def java_round(x: float) -> int:
@@ -171,6 +171,9 @@ class DegradeOracle:
             r, t, f = int(res[i]), int(ts[i]), int(flags[i])
             cbs = self.by_res.get(r, ())
             if not f & EV_EXIT:
+                if f & EV_BLOCKED:                          # blocked by an earlier slot: DegradeSlot never runs
+                    status[i] = V_BLOCK_OTHER
+                    continue
                 moved = []
                 blocked = -1
                 for k, b in enumerate(cbs):                 # DegradeSlot.performChecking (:50-61)
@@ -189,8 +192,11 @@ class DegradeOracle:
                     status[i] = V_PASS
                 continue
             ref = -1 if entry_ref is None else int(entry_ref[i])
+            if ref == -2:                                   # entry blocked in an earlier batch
+                status[i] = V_EXIT_IGNORED
+                continue
             if ref >= 0:
-                if status[ref] == V_BLOCK_DEGRADE:          # DegradeSlot.exit (:72-77)
+                if status[ref] in (V_BLOCK_DEGRADE, V_BLOCK_OTHER):   # DegradeSlot.exit (:72-77): blockError set
                     status[i] = V_EXIT_IGNORED
                     continue
                 created = int(ts[ref])

@@ -1538,8 +1538,13 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         if (!rr->node) rr->node = so_node_new();
         int blocked = 0, prio_wait = 0;
 
+        /* A slot StatisticSlot wraps but the engine does not run (AuthoritySlot,
+         * order -6000 < SystemSlot -5000, Constants.java:80-84) threw a
+         * BlockException: StatisticSlot counts it (StatisticSlot.java:102-124),
+         * no later slot runs */
+        if (fl & SF_EV_BLOCKED) { blocked = 1; status = SF_V_BLOCK_OTHER; }
         /* SystemSlot -> SystemRuleManager.checkSystem */
-        if (is_in) {
+        if (is_in && !blocked) {
             int reason = e->forced ? (e->forced[i] == 0xFF ? -1 : (int)e->forced[i]) : check_system(e, count);
             if (reason >= 0) { blocked = 1; status = SF_V_BLOCK_SYSTEM; rule_idx = reason; }
         }
@@ -1639,7 +1644,7 @@ int so_system_plan(so_engine* e, const sf_event_batch* in, const uint8_t* status
     g_now = in->ts_ms[p];
     const uint8_t f = in->flags[p];
     int reason = -1;
-    if ((f & SF_EV_IN) && !(f & SF_EV_EXIT)) reason = check_system(e, in->count[p]);
+    if ((f & SF_EV_IN) && !(f & (SF_EV_EXIT | SF_EV_BLOCKED))) reason = check_system(e, in->count[p]);
     sys_mask[p] = reason < 0 ? 0xFF : (uint8_t)reason;
     *q = p + 1;
     return SF_OK;

@@ -36,6 +36,7 @@ TAG_NULL, TAG_INT, TAG_LONG, TAG_STRING, TAG_DOUBLE, TAG_BOOL, TAG_OTHER, TAG_BY
 TAG_COLLECTION = 0x40        # a Collection / array argument: elements listed in the CSR
 
 EV_EXIT, EV_IN, EV_PRIO, EV_ERROR = 0x01, 0x02, 0x04, 0x08
+EV_BLOCKED = 0x10            # entry blocked by a slot the engine wraps but does not run (AuthoritySlot)
 MEM_HOST, MEM_DEVICE = 0, 1
 
 V_PASS, V_PASS_WAIT, V_PRIORITY_WAIT, V_BLOCK_FLOW, V_BLOCK_PARAM, V_BLOCK_SYSTEM, V_EXIT, V_EXIT_IGNORED = range(8)
@@ -518,6 +519,7 @@ class WireResult:
 
 # ---- DegradeSlot circuit breakers (include/sentinel_flow.h, sf_degrade_*) ----
 V_BLOCK_DEGRADE = 8
+V_BLOCK_OTHER = 9            # SF_EV_BLOCKED entry: counted as a block by StatisticSlot, no check ran
 DEGRADE_GRADE_RT, DEGRADE_GRADE_EXCEPTION_RATIO, DEGRADE_GRADE_EXCEPTION_COUNT = 0, 1, 2
 CB_CLOSED, CB_OPEN, CB_HALF_OPEN = 0, 1, 2
 

@@ -594,7 +594,17 @@ SF_HD void pm_thread_event(const ParamTable& pt, uint32_t res, uint8_t pm_init, 
 }
 
 SF_HD bool v_blocked(uint8_t v) {
-    return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM || v == SF_V_BLOCK_DEGRADE;
+    return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM || v == SF_V_BLOCK_DEGRADE ||
+           v == SF_V_BLOCK_OTHER;
+}
+// verdict of an entry carrying EVF_SYSBLK: a planned SystemBlockException
+// (reason 0..4 in rule_idx) or an SF_EV_BLOCKED entry (SYSR_OTHER)
+SF_HD uint8_t sysblk_status(uint8_t fl) {
+    return ((fl >> EVF_SYSREASON_SHIFT) & 7) == SYSR_OTHER ? (uint8_t)SF_V_BLOCK_OTHER : (uint8_t)SF_V_BLOCK_SYSTEM;
+}
+SF_HD int sysblk_rule(uint8_t fl) {
+    const int r = (fl >> EVF_SYSREASON_SHIFT) & 7;
+    return r == SYSR_OTHER ? 0 : r;
 }
 
 // the resource's circuit breakers [*b0, *b1) (DegradeRuleManager's list order)
@@ -697,8 +707,8 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
 
         bool blocked = false, prio_wait = false;
         status = SF_V_PASS;
-        if (fl & EVF_SYSBLK) {                                  // SystemBlockException (planned, sf_system.h)
-            blocked = true; status = SF_V_BLOCK_SYSTEM; rule_idx = (fl >> EVF_SYSREASON_SHIFT) & 7;
+        if (fl & EVF_SYSBLK) {        // SF_EV_BLOCKED (AuthoritySlot) or a planned SystemBlockException (sf_system.h)
+            blocked = true; status = sysblk_status(fl); rule_idx = sysblk_rule(fl);
         }
         // ParamFlowSlot.checkFlow :82-103
         if (!blocked && nprules) {

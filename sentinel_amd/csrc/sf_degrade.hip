@@ -35,10 +35,24 @@ __global__ void __launch_bounds__(BLK) k_dg_keys(DegradeDev d, DegradeBatch b, u
     } else if (d.n_rres) {               // rr_of exists once degrade rules were loaded
         key = d.rr_of[r / b.shard_count];
     }
-    keys[i] = key;
+    // an entry blocked by an earlier slot (SF_EV_BLOCKED) never reaches
+    // DegradeSlot, and its exit returns early there (blockError set,
+    // DegradeSlot.java:72-77); so does the exit of an entry blocked in an
+    // earlier batch (entry_ref -2): none of them is walked
+    bool skip = false;
+    uint8_t st = (f & SF_EV_EXIT) ? SF_V_EXIT : SF_V_PASS;
+    if (!(f & SF_EV_EXIT)) {
+        if (f & SF_EV_BLOCKED) { skip = true; st = SF_V_BLOCK_OTHER; }
+    } else if (b.eref) {
+        const int64_t ref = b.eref[i];
+        if (ref == -2 || (ref >= 0 && ref < (int64_t)i && (b.flags[ref] & (SF_EV_BLOCKED | SF_EV_EXIT)) == SF_EV_BLOCKED)) {
+            skip = true; st = SF_V_EXIT_IGNORED;
+        }
+    }
+    keys[i] = skip ? d.n_rres : key;
     idx[i] = i;
     // no breaker (or not yet decided): entries pass the degrade check, exits record
-    status[i] = (f & SF_EV_EXIT) ? SF_V_EXIT : SF_V_PASS;
+    status[i] = st;
     if (rule) rule[i] = 0;
     if (wait) wait[i] = 0;
 }

@@ -54,7 +54,9 @@ SF_HD uint8_t heavy_mode(const DevState& st, uint32_t res, uint32_t segflags, in
         if (st.borrow[(size_t)res * st.S + i].ws >= ws_first) return SM_GENERIC;
     const uint32_t nr = st.rule_off[res + 1] - st.rule_off[res];
     const uint32_t np = st.prule_off[res + 1] - st.prule_off[res];
-    if ((segflags & (SEGF_NONPOS | SEGF_SYS)) || st.interval != 1000) return SM_GENERIC;
+    // (EVF_SYSBLK entries, SEGF_SYS, are blocks no controller sees: the window
+    // paths skip them as candidates and k_heavy_fill counts them as blocks)
+    if ((segflags & SEGF_NONPOS) || st.interval != 1000) return SM_GENERIC;
     if (np != 0) {
         // ParamFlow-only resources whose decisions are independent per parameter
         // value (QPS-grade rules on one argument index, no exits, no collection
@@ -159,6 +161,8 @@ SF_HD uint32_t team_next(Team& tm, uint32_t lo, uint32_t hi, P pred) {
 }
 
 SF_HD bool is_entry(uint8_t f) { return (f & SF_EV_EXIT) == 0; }
+// an entry the controllers decide (not blocked before them: EVF_SYSBLK)
+SF_HD bool is_checked_entry(uint8_t f) { return (f & (SF_EV_EXIT | EVF_SYSBLK)) == 0; }
 
 // Σ acquireCount of entries in [a, b] inclusive (a <= b), from the global prefix
 SF_HD int64_t csum(const int64_t* pcg, uint32_t a, uint32_t b) { return pcg[b] - (a ? pcg[a - 1] : 0); }
@@ -274,7 +278,7 @@ SF_HD void heavy_qps(Team& tm, const DevState& st, const SegIO& io, const HeavyC
             uint32_t j = f + 1;
             while (j < b && (double)(base + passed + 1) <= thr) {      // else no c >= 1 can pass any more
                 j = team_next(tm, j, b, [&](uint32_t k) {
-                    return is_entry(io.flags[k]) && (double)(base + passed + io.cnt[k]) <= thr;
+                    return is_checked_entry(io.flags[k]) && (double)(base + passed + io.cnt[k]) <= thr;
                 });
                 if (j >= b) break;
                 passed += io.cnt[j];
@@ -308,7 +312,7 @@ SF_HD void heavy_rl(Team& tm, const DevState& st, const SegIO& io, const HeavyCt
             uint32_t j = (p < hi && io.ts[p] >= thr) ? p
                          : team_first_true(tm, p, hi, [&](uint32_t k) { return io.ts[k] >= thr; });
             j = team_next(tm, j, hi, [&](uint32_t k) {
-                if (!is_entry(io.flags[k])) return false;
+                if (!is_checked_entry(io.flags[k])) return false;
                 const int32_t c = io.cnt[k];
                 const int64_t ck = c == 1 ? cost1 : j_round(1.0 * c / rule.count * 1000);
                 return io.ts[k] >= L + ck - rule.max_queue_ms;
@@ -348,7 +352,7 @@ inline void heavy_thread(Team&, const DevState& st, const SegIO& io, const Heavy
     int64_t T = st.threads[res];
     for (uint32_t j = lo; j < hi; j++) {
         if (is_entry(io.flags[j])) {
-            if ((double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)io.cnt[j]) <= M) {
+            if (!(io.flags[j] & EVF_SYSBLK) && (double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)io.cnt[j]) <= M) {
                 T++;
                 hc.passbits[j >> 6] |= 1ull << (j & 63);
             }
@@ -406,13 +410,15 @@ SF_HD EvContrib heavy_event(const HeavyCtx& hc, const SegIO& io, uint32_t lo, ui
     r.c = io.cnt[j];
     const bool all = mode == SM_NORULE;
     if (is_entry(f)) {
-        r.passed = all || pass_bit(hc.passbits, j);
+        const bool sysb = (f & EVF_SYSBLK) != 0;
+        r.passed = !sysb && (all || pass_bit(hc.passbits, j));
         r.wait = (mode == SM_RL && r.passed && io.v_wait) ? io.v_wait[j] : 0;
-        r.status = r.passed ? (r.wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : SF_V_BLOCK_FLOW;
+        r.status = r.passed ? (r.wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : (sysb ? sysblk_status(f) : SF_V_BLOCK_FLOW);
         r.touch = true;
     } else {
         const int64_t ref = io.eref ? io.eref[j] : -1;
-        r.live_exit = ref == -1 || (ref >= (int64_t)lo && ref < (int64_t)j && (all || pass_bit(hc.passbits, (uint32_t)ref)));
+        r.live_exit = ref == -1 || (ref >= (int64_t)lo && ref < (int64_t)j && !(io.flags[ref] & EVF_SYSBLK) &&
+                                    (all || pass_bit(hc.passbits, (uint32_t)ref)));
         r.status = r.live_exit ? SF_V_EXIT : SF_V_EXIT_IGNORED;
         r.touch = r.live_exit;
         r.rt = io.ts[j] - (ref >= 0 ? io.ts[ref] : (io.cts ? io.cts[j] : io.ts[j]));

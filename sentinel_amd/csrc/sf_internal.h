@@ -230,6 +230,10 @@ struct DevVerdicts { uint8_t* status; int32_t* wait; uint16_t* rule; };
 constexpr uint8_t EVF_SYSBLK = 0x80u;
 constexpr uint8_t EVF_SYSREASON_SHIFT = 4;
 constexpr uint8_t SYS_NONE = 0xFFu;      // planner mask: no forced block
+// EVF_SYSBLK reason of an SF_EV_BLOCKED entry: blocked by a slot StatisticSlot
+// wraps but the engine does not run (AuthoritySlot), verdict SF_V_BLOCK_OTHER.
+// Like a SystemBlockException it is only a block count to every other slot.
+constexpr uint8_t SYSR_OTHER = 7;
 // sorted entry_ref of an exit whose entry was decided in an earlier sub-batch:
 // -1 it passed (the exit is live, like an entry of an earlier batch), -2 blocked
 constexpr int64_t EREF_DEAD = -2;

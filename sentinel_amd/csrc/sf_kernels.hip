@@ -64,7 +64,9 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t
     const uint32_t dts = (d >= 0 && d < (int64_t)PV_DTS_FAR) ? (uint32_t)d : PV_DTS_FAR;
     const uint8_t f = b.flags[i];
     uint32_t fl = f & 0x0Fu;
-    if (b.sys && (f & SF_EV_IN) && !(f & SF_EV_EXIT)) {          // SystemBlockException forced by the planner
+    if ((f & (SF_EV_BLOCKED | SF_EV_EXIT)) == SF_EV_BLOCKED)     // blocked by AuthoritySlot (before SystemSlot)
+        fl |= EVF_SYSBLK | ((uint32_t)SYSR_OTHER << EVF_SYSREASON_SHIFT);
+    else if (b.sys && (f & SF_EV_IN) && !(f & SF_EV_EXIT)) {     // SystemBlockException forced by the planner
         const uint8_t sr = b.sys[i];
         if (sr != SYS_NONE) fl |= EVF_SYSBLK | ((uint32_t)sr << EVF_SYSREASON_SHIFT);
     }
@@ -162,9 +164,11 @@ __global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint8_t* s
     exit_of[a] = j;
 }
 
-struct EntryCount {     // acquireCount of entries, 0 for exits (input of the pc scan)
-    const int32_t* cnt; const uint8_t* flags;
-    __device__ int64_t operator()(uint32_t j) const { return (flags[j] & SF_EV_EXIT) ? 0 : (int64_t)cnt[j]; }
+struct EntryCount {     // acquireCount of the entries the controllers see (input of the pc scan):
+    const int32_t* cnt; const uint8_t* flags;    // 0 for exits and EVF_SYSBLK entries
+    __device__ int64_t operator()(uint32_t j) const {
+        return (flags[j] & (SF_EV_EXIT | EVF_SYSBLK)) ? 0 : (int64_t)cnt[j];
+    }
 };
 
 // Append to a list with one atomic per wavefront (a single hot counter would
@@ -409,7 +413,8 @@ __device__ void heavy_param(const DevState& st, const SegIO& io, const HeavyCtx&
         const uint32_t na = io.arg_slots ? (io.nargs ? io.nargs[jc] : io.arg_slots) : 0;
         uint32_t tag = SF_TAG_NULL; uint64_t bits = 0;
         if ((int32_t)na > pidx) { tag = io.atag[(size_t)pidx * io.n + jc]; bits = io.abits[(size_t)pidx * io.n + jc]; }
-        const bool key = valid && tag != SF_TAG_NULL;      // a null value skips every rule (passCheck :53-60)
+        const bool sysb = valid && (io.flags[jc] & EVF_SYSBLK);   // blocked before ParamFlowSlot
+        const bool key = valid && !sysb && tag != SF_TAG_NULL;  // a null value skips every rule (passCheck :53-60)
         // rank of this event among the earlier events of its value in the 64
         unsigned long long pend = __ballot(key);
         int rank = 0, maxr = 0;
@@ -423,11 +428,11 @@ __device__ void heavy_param(const DevState& st, const SegIO& io, const HeavyCtx&
             maxr = max(maxr, __popcll(same) - 1);
             pend &= ~same;
         }
-        bool blocked = false;
+        bool blocked = sysb;
         int64_t wait = 0;
         int rule = 0;
         for (int r = 0; r <= maxr; r++) {
-            if (valid && rank == r) {
+            if (valid && !sysb && rank == r) {
                 if (key) {
                     for (uint32_t k = 0; k < np; k++) {
                         int64_t w = 0;
@@ -626,7 +631,8 @@ __global__ void __launch_bounds__(256) k_thr_prep(const uint8_t* flags, const in
         for (uint32_t j = max(tl.y * FILL_TILE, lo) + threadIdx.x; j < min(tl.y * FILL_TILE + FILL_TILE, hi); j += 256) {
             const uint8_t f = flags[j];
             uint2 r;
-            if (!(f & SF_EV_EXIT)) { r.x = hc.exit_of[j]; r.y = (uint32_t)cnt[j]; }
+            if (!(f & SF_EV_EXIT) && !(f & EVF_SYSBLK)) { r.x = hc.exit_of[j]; r.y = (uint32_t)cnt[j]; }
+            else if (!(f & SF_EV_EXIT)) { r.x = 0u; r.y = THR_REC_EXIT; }   // blocked before: a no-op (dead exit)
             else {
                 const int64_t ref = eref ? eref[j] : -1;
                 r.x = ref >= 0 ? j - (uint32_t)ref : 0u;
@@ -761,7 +767,11 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
             }
         }
         const unsigned long long pw = hc.passbits[base >> 6];
-        const uint32_t bits = all ? 0xffffu : (uint32_t)(pw >> (base & 63)) & ((1u << FG) - 1u);
+        uint32_t sysm = 0;                                 // entries blocked before the controllers (EVF_SYSBLK)
+#pragma unroll
+        for (int k = 0; k < FG; k++)
+            if ((g.f[k] & (SF_EV_EXIT | EVF_SYSBLK)) == EVF_SYSBLK) sysm |= 1u << k;
+        const uint32_t bits = (all ? 0xffffu : (uint32_t)(pw >> (base & 63)) & ((1u << FG) - 1u)) & ~sysm;
         // exits: their entries' bits and times (gathers, all issued together)
         uint32_t exm = 0;
 #pragma unroll
@@ -794,7 +804,7 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
                 const int64_t r = rf[k];
                 const uint32_t j = base + (uint32_t)k;
                 if (r >= 0 && (r < (int64_t)lo || r >= (int64_t)j || !is_entry(rfl[k]))) *st.err = SF_ERR_INVALID;
-                const bool live = r == -1 || (r >= (int64_t)lo && r < (int64_t)j &&
+                const bool live = r == -1 || (r >= (int64_t)lo && r < (int64_t)j && !(rfl[k] & EVF_SYSBLK) &&
                                             (all || ((rw[k] >> ((uint32_t)r & 63)) & 1ull)));
                 if (live) rlive |= 1u << k;
             }
@@ -812,8 +822,11 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
             if (!(g.f[k] & SF_EV_EXIT)) {
                 e.passed = (bits >> k) & 1u;
                 e.wait = ((rl || prm) && e.passed) ? wt[k] : 0;
-                e.status = e.passed ? (e.wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : (prm ? SF_V_BLOCK_PARAM : SF_V_BLOCK_FLOW);
-                if (prm && !e.passed) vr[k] = io.v_rule[j];
+                if ((sysm >> k) & 1u) { e.status = sysblk_status(g.f[k]); vr[k] = (uint16_t)sysblk_rule(g.f[k]); }
+                else {
+                    e.status = e.passed ? (e.wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : (prm ? SF_V_BLOCK_PARAM : SF_V_BLOCK_FLOW);
+                    if (prm && !e.passed) vr[k] = io.v_rule[j];
+                }
                 e.touch = true;
             } else {
                 e.live_exit = (rlive >> k) & 1u;

@@ -503,7 +503,7 @@ __device__ __forceinline__ void rl_load(RlRegs& r, const SegIO& io, uint32_t q0,
     for (int i = 0; i < HS_PL; i++) {
         const bool v = q0 + (uint32_t)(i * HS_T) + threadIdx.x < hi;
         r.ts[i] = v ? r.ts[i] : INT64_MAX;
-        r.c[i] = (v && !(f[i] & SF_EV_EXIT)) ? r.c[i] : 0;        // 0: exit / padding (never a candidate)
+        r.c[i] = (v && !(f[i] & (SF_EV_EXIT | EVF_SYSBLK))) ? r.c[i] : 0;   // 0: exit / blocked before / padding
     }
 }
 __device__ __forceinline__ void rl_store(const RlRegs& r, int64_t* tsb, int32_t* cb) {

@@ -166,9 +166,7 @@ SF_HD int sys_classify(const SysRule& r, const SysBase& b, int S, double interva
     return -2;
 }
 
-SF_HD bool v_blocked_any(uint8_t v) {
-    return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM || v == SF_V_BLOCK_DEGRADE;
-}
+SF_HD bool v_blocked_any(uint8_t v) { return v_blocked(v); }
 
 // Exit-side contribution of event i (submission index) when planning from p:
 // ts / cnt / flags / eref / cts are the whole batch's arrays, vstatus its
@@ -196,6 +194,8 @@ SF_HD SysExitQ sys_exit_q(const int64_t* ts, const int32_t* cnt, const uint8_t* 
             const int64_t rt = t - ts[ref];
             q.xc = 1; q.xc_c = c; q.xc_rt = rt; q.xc_min = rt;
         }
+    } else if (flags[ref] & SF_EV_BLOCKED) {             // entry blocked before SystemSlot: nothing recorded
+        return q;
     } else {                                             // entry inside the plan: live iff it passes
         const int64_t rt = t - ts[ref];
         q.xu = 1; q.xu_c = c; q.xu_min = rt;

@@ -83,9 +83,11 @@ __device__ Q block_prefix(const Q* tot, uint32_t k, Q* lds) {
 __device__ __forceinline__ SysExitQ exit_q(const SysPlanArgs& a, uint32_t i) {
     return sys_exit_q(a.ts, a.cnt, a.flags, a.eref, a.cts, a.vstatus, a.p, i, a.r.max_rt);
 }
+// IN entries that reach SystemSlot (an SF_EV_BLOCKED entry was blocked by
+// AuthoritySlot before it: certainly blocked, no system verdict)
 __device__ __forceinline__ bool in_entry(const SysPlanArgs& a, uint32_t i) {
     const uint8_t f = a.flags[i];
-    return (f & SF_EV_IN) && !(f & SF_EV_EXIT);
+    return (f & SF_EV_IN) && !(f & (SF_EV_EXIT | SF_EV_BLOCKED));
 }
 
 __global__ void __launch_bounds__(SP_T) k_sp_a(SysPlanArgs a) {
@@ -186,6 +188,8 @@ __global__ void __launch_bounds__(SP_T) k_sp_c(SysPlanArgs a) {
             if (res == -1) { atomicMin(&pl.first_unc, i); break; }
             a.mask[i] = res >= 0 ? (uint8_t)res : SYS_NONE;
             if (!fire) { en.nb++; en.nb_c = wadd(en.nb_c, c > 0 ? c : 0); en.nb_neg += c < 0 ? 1 : 0; }
+        } else if ((a.flags[i] & (SF_EV_IN | SF_EV_EXIT | SF_EV_BLOCKED)) == (SF_EV_IN | SF_EV_BLOCKED)) {
+            a.mask[i] = SYS_NONE;                          // blocked before SystemSlot: no system verdict
         }
         x.add(exit_q(a, i));
     }

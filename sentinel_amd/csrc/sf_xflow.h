@@ -204,8 +204,8 @@ SF_HD void decide_xgroup(const DevState& st, const SegIO& io, uint32_t lo, uint3
         } else {
             bool blocked = false, prio_wait = false;
             status = SF_V_PASS;
-            if (fl & EVF_SYSBLK) {                              // SystemBlockException (planned, sf_system.h)
-                blocked = true; status = SF_V_BLOCK_SYSTEM; rule_idx = (fl >> EVF_SYSREASON_SHIFT) & 7;
+            if (fl & EVF_SYSBLK) {    // SF_EV_BLOCKED (AuthoritySlot) or a planned SystemBlockException
+                blocked = true; status = sysblk_status(fl); rule_idx = sysblk_rule(fl);
             }
             if (!blocked && nprules) {                          // ParamFlowSlot.checkFlow :82-103
                 pm_exists = true;

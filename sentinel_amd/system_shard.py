@@ -29,7 +29,7 @@ import numpy as np
 from . import abi
 
 SYS_NONE = 0xFF
-_BLOCKED = (abi.V_BLOCK_FLOW, abi.V_BLOCK_PARAM, abi.V_BLOCK_SYSTEM, abi.V_BLOCK_DEGRADE)
+_BLOCKED = (abi.V_BLOCK_FLOW, abi.V_BLOCK_PARAM, abi.V_BLOCK_SYSTEM, abi.V_BLOCK_DEGRADE, abi.V_BLOCK_OTHER)
 
 
 def _blocked(v: np.ndarray) -> np.ndarray:

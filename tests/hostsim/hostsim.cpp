@@ -202,19 +202,22 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     std::vector<int32_t> vw(n); std::vector<uint16_t> vr(n);
     for (uint32_t j = 0; j < n; j++) {
         uint32_t i = perm[j]; inv[i] = j;
-        ts[j] = in->ts_ms[i]; cnt[j] = in->count[i]; fl[j] = in->flags[i];
+        ts[j] = in->ts_ms[i]; cnt[j] = in->count[i];
+        fl[j] = in->flags[i] & 0x0Fu;                            // k_keys_packed's internal flags
+        if ((in->flags[i] & (SF_EV_BLOCKED | SF_EV_EXIT)) == SF_EV_BLOCKED)
+            fl[j] |= EVF_SYSBLK | (uint8_t)(SYSR_OTHER << EVF_SYSREASON_SHIFT);
         if (in->n_args) nargs[j] = in->n_args[i];
         for (uint32_t a = 0; a < in->arg_slots; a++) {
             atag[(size_t)a * n + j] = in->arg_tag[(size_t)a * n + i];
             abits[(size_t)a * n + j] = atag[(size_t)a * n + j] == SF_TAG_COLLECTION ? (uint64_t)a * n + i
                                                                                   : in->arg_bits[(size_t)a * n + i];
         }
-        pcg[j] = (j ? pcg[j - 1] : 0) + ((fl[j] & SF_EV_EXIT) ? 0 : (int64_t)cnt[j]);
+        pcg[j] = (j ? pcg[j - 1] : 0) + ((fl[j] & (SF_EV_EXIT | EVF_SYSBLK)) ? 0 : (int64_t)cnt[j]);
     }
     if (in->entry_ref)
         for (uint32_t j = 0; j < n; j++) {
             int64_t r = in->entry_ref[perm[j]];
-            eref[j] = r >= 0 ? (int64_t)inv[r] : (int64_t)-1;
+            eref[j] = r >= 0 ? (int64_t)inv[r] : (r == EREF_DEAD ? EREF_DEAD : (int64_t)-1);
             cts[j] = in->create_ts ? in->create_ts[perm[j]] : 0;
         }
     SegIO io{ts.data(), cnt.data(), fl.data(), in->entry_ref ? eref.data() : nullptr,
@@ -237,8 +240,9 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     std::vector<uint32_t> seg_start, seg_res, segflag;
     for (uint32_t j = 0; j < n; j++) {
         if (j == 0 || key[perm[j]] != key[perm[j - 1]]) { seg_start.push_back(j); seg_res.push_back(key[perm[j]]); segflag.push_back(0); }
-        if (!(fl[j] & SF_EV_EXIT) && ((fl[j] & SF_EV_PRIO) || cnt[j] <= 0))
-            segflag.back() |= ((fl[j] & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (cnt[j] <= 0 ? SEGF_NONPOS : 0u);
+        if (!(fl[j] & SF_EV_EXIT) && ((fl[j] & (SF_EV_PRIO | EVF_SYSBLK)) || cnt[j] <= 0))
+            segflag.back() |= ((fl[j] & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (cnt[j] <= 0 ? SEGF_NONPOS : 0u) |
+                              ((fl[j] & EVF_SYSBLK) ? SEGF_SYS : 0u);
     }
     const uint32_t ns = (uint32_t)seg_start.size();
     seg_start.push_back(n);

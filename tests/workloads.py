@@ -330,6 +330,37 @@ def xflow(seed=51, R=400, n=60_000, origins=6, contexts=4, duration_ms=6000, zip
                 context_nodes=sorted(dn))
 
 
+def preblocked(w, frac=0.05, seed=0):
+    """The workload with a fraction of its entries flagged SF_EV_BLOCKED: blocked
+    by AuthoritySlot, which StatisticSlot wraps (StatisticSlot.java:102-124)
+    but the engine does not run.  Each such entry is a block on its resource's
+    ClusterNode and ENTRY_NODE that no rule sees; its exit records nothing.
+    Entries are picked by a hash of (resource, time), so an exit in a later
+    batch (entry_ref -1, create_ts) knows its entry was blocked and carries
+    entry_ref -2 as a caller would."""
+    thr = np.uint64(int(frac * (1 << 20)))
+
+    def pick(res, ts):
+        h = (res.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15) ^ ts.astype(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F)
+             ^ np.uint64((seed * 0x165667B19E3779F9 + 1) % (1 << 64)))
+        h ^= h >> np.uint64(29)
+        h *= np.uint64(0xBF58476D1CE4E5B9)
+        h ^= h >> np.uint64(32)
+        return (h & np.uint64((1 << 20) - 1)) < thr
+
+    for b in w["batches"]:
+        b.flags = b.flags.copy()
+        ent = (b.flags & abi.EV_EXIT) == 0
+        b.flags[ent & pick(b.res_id, b.ts_ms)] |= abi.EV_BLOCKED
+        if b.entry_ref is not None and b.create_ts is not None:
+            early = ~ent & (b.entry_ref == -1)
+            dead = early & pick(b.res_id, b.create_ts)
+            if dead.any():
+                b.entry_ref = b.entry_ref.copy()
+                b.entry_ref[dead] = -2
+    return w
+
+
 ALL = {
     "config1": config1, "config2": config2, "config3": config3, "config4": config4,
     "prioritized": prioritized, "multi_rule": multi_rule, "param_mixed": param_mixed,
