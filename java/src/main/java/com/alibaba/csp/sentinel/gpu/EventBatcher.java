@@ -131,7 +131,7 @@ final class EventBatcher implements Runnable {
             nArgs.setAtIndex(JAVA_BYTE, i, (byte) na);
             for (int s = 0; s < ARG_SLOTS; s++) {
                 long k = (long) s * n + i;
-                Object v = s < na ? t.args[s] : null;
+                Object v = s < na ? ParamPacker.key(t.args[s]) : null;
                 byte tag = ParamPacker.tag(v);
                 argTag.setAtIndex(JAVA_BYTE, k, tag);
                 argBits.setAtIndex(JAVA_LONG, k, tag == TAG_COLLECTION ? 0L : ParamPacker.bits(v));
@@ -142,7 +142,7 @@ final class EventBatcher implements Runnable {
             for (int i = 0; i < n; i++) {
                 long k = (long) s * n + i;
                 Ticket t = b.get(i);
-                Object v = t.args != null && s < t.args.length ? t.args[s] : null;
+                Object v = t.args != null && s < t.args.length ? ParamPacker.key(t.args[s]) : null;
                 if (v != null && ParamPacker.tag(v) == TAG_COLLECTION) {
                     for (Object el : ParamPacker.elements(v)) {
                         elemTag.setAtIndex(JAVA_BYTE, ne, ParamPacker.tag(el));
@@ -153,23 +153,28 @@ final class EventBatcher implements Runnable {
                 elemOff.setAtIndex(JAVA_INT, k + 1, ne);
             }
         }
-        batch.set(JAVA_INT, 0, n); batch.set(JAVA_INT, 4, SF_MEM_HOST_);
-        long o = 8;
-        for (MemorySegment p : new MemorySegment[]{res, ts, cnt, flags}) { batch.set(ADDRESS, o, p); o += 8; }
-        batch.set(ADDRESS, o, anyExit ? eref : MemorySegment.NULL); o += 8;
-        batch.set(ADDRESS, o, anyExit ? cts : MemorySegment.NULL); o += 8;
-        batch.set(JAVA_INT, o, ARG_SLOTS); o += 8;
-        batch.set(ADDRESS, o, nArgs); o += 8;
-        batch.set(ADDRESS, o, argTag); o += 8;
-        batch.set(ADDRESS, o, argBits); o += 8;
-        batch.set(ADDRESS, o, ne > 0 ? elemOff : MemorySegment.NULL); o += 8;
-        batch.set(ADDRESS, o, elemTag); o += 8;
-        batch.set(ADDRESS, o, elemBits); o += 8;
-        batch.set(JAVA_INT, o, ne); o += 8;
-        batch.set(ADDRESS, o, origin); o += 8;
-        batch.set(ADDRESS, o, context);
-        verdicts.set(JAVA_INT, 0, SF_MEM_HOST_);
-        verdicts.set(ADDRESS, 8, status); verdicts.set(ADDRESS, 16, waitMs); verdicts.set(ADDRESS, 24, ruleIdx);
+        batch.set(JAVA_INT, off(EVENT_BATCH, "n"), n);
+        batch.set(JAVA_INT, off(EVENT_BATCH, "mem"), SF_MEM_HOST_);
+        batch.set(ADDRESS, off(EVENT_BATCH, "res_id"), res);
+        batch.set(ADDRESS, off(EVENT_BATCH, "ts_ms"), ts);
+        batch.set(ADDRESS, off(EVENT_BATCH, "count"), cnt);
+        batch.set(ADDRESS, off(EVENT_BATCH, "flags"), flags);
+        batch.set(ADDRESS, off(EVENT_BATCH, "entry_ref"), anyExit ? eref : MemorySegment.NULL);
+        batch.set(ADDRESS, off(EVENT_BATCH, "create_ts"), anyExit ? cts : MemorySegment.NULL);
+        batch.set(JAVA_INT, off(EVENT_BATCH, "arg_slots"), ARG_SLOTS);
+        batch.set(ADDRESS, off(EVENT_BATCH, "n_args"), nArgs);
+        batch.set(ADDRESS, off(EVENT_BATCH, "arg_tag"), argTag);
+        batch.set(ADDRESS, off(EVENT_BATCH, "arg_bits"), argBits);
+        batch.set(ADDRESS, off(EVENT_BATCH, "arg_elem_off"), ne > 0 ? elemOff : MemorySegment.NULL);
+        batch.set(ADDRESS, off(EVENT_BATCH, "elem_tag"), elemTag);
+        batch.set(ADDRESS, off(EVENT_BATCH, "elem_bits"), elemBits);
+        batch.set(JAVA_INT, off(EVENT_BATCH, "n_elems"), ne);
+        batch.set(ADDRESS, off(EVENT_BATCH, "origin"), origin);
+        batch.set(ADDRESS, off(EVENT_BATCH, "context"), context);
+        verdicts.set(JAVA_INT, off(VERDICTS, "mem"), SF_MEM_HOST_);
+        verdicts.set(ADDRESS, off(VERDICTS, "status"), status);
+        verdicts.set(ADDRESS, off(VERDICTS, "wait_ms"), waitMs);
+        verdicts.set(ADDRESS, off(VERDICTS, "rule_idx"), ruleIdx);
         check((int) SUBMIT.invokeExact(engine.handle, batch, verdicts));
         for (int i = 0; i < n; i++) {
             Ticket t = b.get(i);

@@ -1,6 +1,8 @@
 package com.alibaba.csp.sentinel.gpu;
 
 import com.alibaba.csp.sentinel.slots.block.RuleConstant;
+import com.alibaba.csp.sentinel.slots.block.degrade.DegradeRule;
+import com.alibaba.csp.sentinel.slots.block.degrade.DegradeRuleManager;
 import com.alibaba.csp.sentinel.slots.block.flow.FlowRule;
 import com.alibaba.csp.sentinel.slots.block.flow.FlowRuleManager;
 import com.alibaba.csp.sentinel.slots.block.flow.param.ParamFlowItem;
@@ -57,6 +59,8 @@ public final class GpuEngine {
     /** Per resource: the rule lists the engine's rule indices refer to (exception payloads). */
     volatile Map<Integer, List<FlowRule>> flowRulesByResource = new HashMap<>();
     volatile Map<Integer, List<ParamFlowRule>> paramRulesByResource = new HashMap<>();
+    /** Per resource: its circuit breakers' rules in the engine's breaker order (DegradeException payload). */
+    volatile Map<Integer, List<DegradeRule>> degradeRulesByResource = new HashMap<>();
     final EventBatcher batcher;
 
     private GpuEngine(int maxResources, int maxBatch) {
@@ -64,8 +68,8 @@ public final class GpuEngine {
         MemorySegment cfg = arena.allocate(CONFIG);
         try {
             CONFIG_DEFAULT.invokeExact(cfg);
-            cfg.set(JAVA_INT, CONFIG.byteOffset(MemoryLayout_path("max_resources")), maxResources);
-            cfg.set(JAVA_INT, CONFIG.byteOffset(MemoryLayout_path("max_batch")), maxBatch);
+            cfg.set(JAVA_INT, off(CONFIG, "max_resources"), maxResources);
+            cfg.set(JAVA_INT, off(CONFIG, "max_batch"), maxBatch);
             MemorySegment out = arena.allocate(ADDRESS);
             check((int) CREATE.invokeExact(cfg, out));
             handle = out.get(ADDRESS, 0);
@@ -76,10 +80,6 @@ public final class GpuEngine {
         }
         batcher = new EventBatcher(this, maxBatch);
         reloadRules();
-    }
-
-    private static java.lang.foreign.MemoryLayout.PathElement MemoryLayout_path(String name) {
-        return java.lang.foreign.MemoryLayout.PathElement.groupElement(name);
     }
 
     /** Dense id of a resource name (ResourceWrapper identity is the name, ResourceWrapper.java:81-95). */
@@ -119,7 +119,7 @@ public final class GpuEngine {
         }
     }
 
-    /** Called after FlowRuleManager / ParamFlowRuleManager / SystemRuleManager.loadRules. */
+    /** Called after FlowRuleManager / ParamFlowRuleManager / SystemRuleManager / DegradeRuleManager.loadRules. */
     public void reloadRules() {
         ruleVersion.incrementAndGet();
     }
@@ -136,21 +136,21 @@ public final class GpuEngine {
                 int res = resourceId(r.getResource());
                 byRes.computeIfAbsent(res, k -> new ArrayList<>()).add(r);
                 MemorySegment s = fr.asSlice((long) i++ * FLOW_RULE.byteSize(), FLOW_RULE.byteSize());
-                s.set(JAVA_INT, 0, res);
-                s.set(JAVA_INT, 4, r.getGrade());
-                s.set(JAVA_DOUBLE, 8, r.getCount());
-                s.set(JAVA_INT, 16, r.getStrategy());
-                s.set(JAVA_INT, 20, r.getControlBehavior());
-                s.set(JAVA_INT, 24, r.getWarmUpPeriodSec());
-                s.set(JAVA_INT, 28, r.getMaxQueueingTimeMs());
-                s.set(JAVA_INT, 32, r.isClusterMode() ? 1 : 0);
+                s.set(JAVA_INT, off(FLOW_RULE, "resource"), res);
+                s.set(JAVA_INT, off(FLOW_RULE, "grade"), r.getGrade());
+                s.set(JAVA_DOUBLE, off(FLOW_RULE, "count"), r.getCount());
+                s.set(JAVA_INT, off(FLOW_RULE, "strategy"), r.getStrategy());
+                s.set(JAVA_INT, off(FLOW_RULE, "control_behavior"), r.getControlBehavior());
+                s.set(JAVA_INT, off(FLOW_RULE, "warm_up_period_sec"), r.getWarmUpPeriodSec());
+                s.set(JAVA_INT, off(FLOW_RULE, "max_queueing_time_ms"), r.getMaxQueueingTimeMs());
+                s.set(JAVA_INT, off(FLOW_RULE, "cluster_mode"), r.isClusterMode() ? 1 : 0);
                 String ref = r.getRefResource();
                 int refId = ref == null || ref.isEmpty() ? -1            // SF_REF_NONE
                         : r.getStrategy() == RuleConstant.STRATEGY_CHAIN ? contextId(ref) : resourceId(ref);
-                s.set(JAVA_INT, 36, refId);
+                s.set(JAVA_INT, off(FLOW_RULE, "ref_resource"), refId);
                 String app = r.getLimitApp();                            // blank -> "default" (FlowRuleUtil.java:99-101)
-                s.set(JAVA_INT, 40, app == null || app.trim().isEmpty() ? 0 : originId(app));
-                s.set(JAVA_INT, 44, r.getClusterConfig() == null || r.getClusterConfig().isFallbackToLocalWhenFail() ? 1 : 0);
+                s.set(JAVA_INT, off(FLOW_RULE, "limit_app"), app == null || app.trim().isEmpty() ? 0 : originId(app));
+                s.set(JAVA_INT, off(FLOW_RULE, "cluster_fallback"), r.getClusterConfig() == null || r.getClusterConfig().isFallbackToLocalWhenFail() ? 1 : 0);
             }
             check((int) LOAD_FLOW.invokeExact(handle, fr, flow.size()));
             flowRulesByResource = byRes;
@@ -167,28 +167,28 @@ public final class GpuEngine {
                 int res = resourceId(r.getResource());
                 pByRes.computeIfAbsent(res, x -> new ArrayList<>()).add(r);
                 MemorySegment s = pr.asSlice((long) k++ * PARAM_RULE.byteSize(), PARAM_RULE.byteSize());
-                s.set(JAVA_INT, 0, res);
-                s.set(JAVA_INT, 4, r.getGrade());
-                s.set(JAVA_INT, 8, r.getParamIdx() == null ? 0 : r.getParamIdx());
-                s.set(JAVA_INT, 12, r.getControlBehavior());
-                s.set(JAVA_DOUBLE, 16, r.getCount());
-                s.set(JAVA_INT, 24, r.getMaxQueueingTimeMs());
-                s.set(JAVA_INT, 28, r.getBurstCount());
-                s.set(JAVA_LONG, 32, r.getDurationInSec());
-                s.set(JAVA_INT, 40, it);
+                s.set(JAVA_INT, off(PARAM_RULE, "resource"), res);
+                s.set(JAVA_INT, off(PARAM_RULE, "grade"), r.getGrade());
+                s.set(JAVA_INT, off(PARAM_RULE, "param_idx"), r.getParamIdx() == null ? 0 : r.getParamIdx());
+                s.set(JAVA_INT, off(PARAM_RULE, "control_behavior"), r.getControlBehavior());
+                s.set(JAVA_DOUBLE, off(PARAM_RULE, "count"), r.getCount());
+                s.set(JAVA_INT, off(PARAM_RULE, "max_queueing_time_ms"), r.getMaxQueueingTimeMs());
+                s.set(JAVA_INT, off(PARAM_RULE, "burst_count"), r.getBurstCount());
+                s.set(JAVA_LONG, off(PARAM_RULE, "duration_in_sec"), r.getDurationInSec());
+                s.set(JAVA_INT, off(PARAM_RULE, "item_offset"), it);
                 int cnt = 0;
                 if (r.getParamFlowItemList() != null) {
                     for (ParamFlowItem item : r.getParamFlowItemList()) {
                         Object v = HotItems.parse(item);          // ParamFlowRuleUtil.parseValue (:188-240)
                         if (v == null) continue;
                         MemorySegment h = items.asSlice((long) it++ * HOT_ITEM.byteSize(), HOT_ITEM.byteSize());
-                        h.set(JAVA_BYTE, 0, ParamPacker.tag(v));
-                        h.set(JAVA_INT, 4, item.getCount());
-                        h.set(JAVA_LONG, 8, ParamPacker.bits(v));
+                        h.set(JAVA_BYTE, off(HOT_ITEM, "tag"), ParamPacker.tag(v));
+                        h.set(JAVA_INT, off(HOT_ITEM, "count"), item.getCount());
+                        h.set(JAVA_LONG, off(HOT_ITEM, "bits"), ParamPacker.bits(v));
                         cnt++;
                     }
                 }
-                s.set(JAVA_INT, 44, cnt);
+                s.set(JAVA_INT, off(PARAM_RULE, "item_count"), cnt);
             }
             check((int) LOAD_PARAM.invokeExact(handle, pr, param.size(), items, it));
             paramRulesByResource = pByRes;
@@ -199,13 +199,38 @@ public final class GpuEngine {
             int j = 0;
             for (SystemRule r : sys) {
                 MemorySegment s = sr.asSlice((long) j++ * SYSTEM_RULE.byteSize(), SYSTEM_RULE.byteSize());
-                s.set(JAVA_DOUBLE, 0, r.getHighestSystemLoad());
-                s.set(JAVA_DOUBLE, 8, r.getHighestCpuUsage());
-                s.set(JAVA_DOUBLE, 16, r.getQps());
-                s.set(JAVA_LONG, 24, r.getAvgRt());
-                s.set(JAVA_LONG, 32, r.getMaxThread());
+                s.set(JAVA_DOUBLE, off(SYSTEM_RULE, "highest_system_load"), r.getHighestSystemLoad());
+                s.set(JAVA_DOUBLE, off(SYSTEM_RULE, "highest_cpu_usage"), r.getHighestCpuUsage());
+                s.set(JAVA_DOUBLE, off(SYSTEM_RULE, "qps"), r.getQps());
+                s.set(JAVA_LONG, off(SYSTEM_RULE, "avg_rt"), r.getAvgRt());
+                s.set(JAVA_LONG, off(SYSTEM_RULE, "max_thread"), r.getMaxThread());
             }
             check((int) LOAD_SYSTEM.invokeExact(handle, sr, sys.size()));
+
+            // circuit breakers: DegradeSlot is the last slot of the engine's chain.  The valid
+            // rules (DegradeRuleManager.isValidRule :183-204) in list order; sf_load_degrade_rules
+            // keeps the breaker of every unchanged rule (getExistingSameCbOrNew :151-163) and
+            // rule_idx of a DegradeException is the position in the resource's list
+            List<DegradeRule> dg = new ArrayList<>();
+            for (DegradeRule r : DegradeRuleManager.getRules()) if (DegradeRuleManager.isValidRule(r)) dg.add(r);
+            Map<Integer, List<DegradeRule>> dByRes = new HashMap<>();
+            MemorySegment dr = a.allocate(DEGRADE_RULE, Math.max(1, dg.size()));
+            int d = 0;
+            for (DegradeRule r : dg) {
+                int res = resourceId(r.getResource());
+                dByRes.computeIfAbsent(res, x -> new ArrayList<>()).add(r);
+                MemorySegment s = dr.asSlice((long) d++ * DEGRADE_RULE.byteSize(), DEGRADE_RULE.byteSize());
+                s.set(JAVA_INT, off(DEGRADE_RULE, "resource"), res);
+                s.set(JAVA_INT, off(DEGRADE_RULE, "grade"), r.getGrade());
+                s.set(JAVA_DOUBLE, off(DEGRADE_RULE, "count"), r.getCount());
+                s.set(JAVA_INT, off(DEGRADE_RULE, "time_window_s"), r.getTimeWindow());
+                s.set(JAVA_INT, off(DEGRADE_RULE, "min_request_amount"), r.getMinRequestAmount());
+                s.set(JAVA_DOUBLE, off(DEGRADE_RULE, "slow_ratio_threshold"), r.getSlowRatioThreshold());
+                s.set(JAVA_INT, off(DEGRADE_RULE, "stat_interval_ms"), r.getStatIntervalMs());
+                s.set(JAVA_INT, off(DEGRADE_RULE, "pad"), 0);
+            }
+            check((int) LOAD_DEGRADE.invokeExact(handle, dr, dg.size(), MemorySegment.NULL));
+            degradeRulesByResource = dByRes;
         }
     }
 

@@ -6,6 +6,10 @@ import com.alibaba.csp.sentinel.node.DefaultNode;
 import com.alibaba.csp.sentinel.slotchain.AbstractLinkedProcessorSlot;
 import com.alibaba.csp.sentinel.slotchain.ResourceWrapper;
 import com.alibaba.csp.sentinel.slots.block.BlockException;
+import com.alibaba.csp.sentinel.slots.block.authority.AuthorityException;
+import com.alibaba.csp.sentinel.slots.block.authority.AuthoritySlot;
+import com.alibaba.csp.sentinel.slots.block.degrade.DegradeException;
+import com.alibaba.csp.sentinel.slots.block.degrade.DegradeRule;
 import com.alibaba.csp.sentinel.slots.block.flow.FlowException;
 import com.alibaba.csp.sentinel.slots.block.flow.FlowRule;
 import com.alibaba.csp.sentinel.slots.block.flow.param.ParamFlowException;
@@ -18,27 +22,51 @@ import java.util.List;
 import static com.alibaba.csp.sentinel.gpu.SentinelFlowNative.*;
 
 /**
- * StatisticSlot + SystemSlot + ParamFlowSlot + FlowSlot in one slot, decided
- * on the GPU: each entry and exit becomes one event of the engine's next
- * batch (EventBatcher), and the verdict is turned back into the reference's
- * behaviour (StatisticSlot.java:64-130, DefaultController.java:60-72,
- * RateLimiterController.java:80-95, SystemRuleManager.java:291-348,
- * ParamFlowSlot.java:58-88).  The statistics the reference keeps in
- * StatisticNode live in the engine (sf_read_node / sf_snapshot serve the
+ * The default chain's StatisticSlot (-7000) and every slot it wraps --
+ * AuthoritySlot (-6000), SystemSlot (-5000), ParamFlowSlot (-3000), FlowSlot
+ * (-2000), DegradeSlot (-1000) (Constants.java:77-84) -- in one slot whose
+ * checks and statistics run on the GPU.  Each entry and exit is one event of
+ * the engine's next batch (EventBatcher); the engine does StatisticSlot's
+ * accounting of every outcome (StatisticSlot.java:55-131), so this slot only
+ * turns the verdict back into the reference's behaviour:
+ * <ul>
+ * <li>AuthoritySlot reads no statistics and runs here, on the caller's thread,
+ * before the event is submitted: an AuthorityException is submitted as an
+ * SF_EV_BLOCKED entry (the engine counts block += count on the node and, for
+ * an IN entry, on ENTRY_NODE, and runs no other check), then thrown;</li>
+ * <li>SystemBlockException, ParamFlowException, FlowException and
+ * DegradeException (the engine's circuit breakers, loaded from
+ * DegradeRuleManager) are thrown with the blocking rule, after setting the
+ * entry's blockError as StatisticSlot does (:102-105);</li>
+ * <li>PASS_WAIT: RateLimiterController slept, then passed (:80-95);
+ * PRIORITY_WAIT: DefaultController slept and threw PriorityWaitException,
+ * which StatisticSlot catches (:86-101) -- the entry returns normally and the
+ * slots after FlowSlot (DegradeSlot, any later slot) do not run.</li>
+ * </ul>
+ * The exit of a passed entry is one EXIT event (RT, success, thread count,
+ * breaker completion); a blocked entry's exit submits nothing (:139).
+ * The statistics live in the engine (sf_read_node / sf_snapshot serve the
  * dashboard and MetricWriter); the DefaultNode passed along is untouched.
  */
 public class GpuFlowSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
     private static final String[] SYSTEM_LIMIT = {"qps", "thread", "rt", "load", "cpu"};
-    private static final String TICKET_KEY = "sentinel.gpu.ticket";
     private final GpuEngine engine;
+    /** The reference AuthoritySlot, ending the chain it is called through (no next slot). */
+    private final AuthoritySlot authority = new AuthoritySlot();
 
     public GpuFlowSlot(GpuEngine engine) {
         this.engine = engine;
+        authority.setNext(new AbstractLinkedProcessorSlot<DefaultNode>() {
+            @Override
+            public void entry(Context c, ResourceWrapper r, DefaultNode n, int k, boolean p, Object... a) {}
+
+            @Override
+            public void exit(Context c, ResourceWrapper r, int k, Object... a) {}
+        });
     }
 
-    @Override
-    public void entry(Context context, ResourceWrapper resourceWrapper, DefaultNode node, int count,
-                      boolean prioritized, Object... args) throws Throwable {
+    private EventBatcher.Ticket ticket(Context context, ResourceWrapper resourceWrapper, int count, boolean prioritized,
+                                       Object[] args) {
         EventBatcher.Ticket t = new EventBatcher.Ticket();
         t.resource = engine.resourceId(resourceWrapper.getName());
         t.origin = engine.originId(context.getOrigin());    // limitApp / origin node (FlowRuleChecker.java:129-161)
@@ -47,6 +75,20 @@ public class GpuFlowSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
         t.flags = (byte) ((resourceWrapper.getEntryType() == EntryType.IN ? EV_IN : 0) | (prioritized ? EV_PRIO : 0));
         t.ts = TimeUtil.currentTimeMillis();
         t.args = args;
+        return t;
+    }
+
+    @Override
+    public void entry(Context context, ResourceWrapper resourceWrapper, DefaultNode node, int count,
+                      boolean prioritized, Object... args) throws Throwable {
+        EventBatcher.Ticket t = ticket(context, resourceWrapper, count, prioritized, args);
+        try {
+            authority.entry(context, resourceWrapper, node, count, prioritized, args);   // AuthoritySlot.java:38-44
+        } catch (AuthorityException ex) {
+            t.flags |= EV_BLOCKED;                           // counted as a block by the engine's StatisticSlot
+            engine.batcher.submit(t);
+            throw block(context, ex);
+        }
         engine.batcher.submit(t);
         switch (t.status) {
             case V_PASS:
@@ -54,9 +96,10 @@ public class GpuFlowSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
             case V_PASS_WAIT:                                  // RateLimiterController: sleep, then pass
                 if (t.waitMs > 0) Thread.sleep(t.waitMs);
                 break;
-            case V_PRIORITY_WAIT:                              // DefaultController occupy: sleep, pass borrowed
-                Thread.sleep(t.waitMs);                        // (the engine counted it as PriorityWaitException)
-                break;
+            case V_PRIORITY_WAIT:                              // DefaultController occupy: sleep, then
+                Thread.sleep(t.waitMs);                        // PriorityWaitException, caught by StatisticSlot
+                remember(context, t);
+                return;                                        // (no later slot runs)
             case V_BLOCK_FLOW: {
                 List<FlowRule> rules = engine.flowRulesByResource.get(t.resource);
                 FlowRule rule = rules != null && t.ruleIdx < rules.size() ? rules.get(t.ruleIdx) : null;
@@ -67,20 +110,25 @@ public class GpuFlowSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
                 ParamFlowRule rule = rules != null && t.ruleIdx < rules.size() ? rules.get(t.ruleIdx) : null;
                 Object value = rule != null && args != null && rule.getParamIdx() != null ?
                         args[rule.getParamIdx() < 0 ? args.length + rule.getParamIdx() : rule.getParamIdx()] : null;
-                throw block(context, new ParamFlowException(resourceWrapper.getName(), String.valueOf(value), rule));
+                throw block(context, new ParamFlowException(resourceWrapper.getName(),
+                        String.valueOf(ParamPacker.key(value)), rule));
             }
             case V_BLOCK_SYSTEM:
                 throw block(context, new SystemBlockException(resourceWrapper.getName(), SYSTEM_LIMIT[t.ruleIdx]));
+            case V_BLOCK_DEGRADE: {                            // DegradeSlot.performChecking (DegradeSlot.java:50-61)
+                List<DegradeRule> rules = engine.degradeRulesByResource.get(t.resource);
+                DegradeRule rule = rules != null && t.ruleIdx < rules.size() ? rules.get(t.ruleIdx) : null;
+                throw block(context, new DegradeException(rule == null ? "default" : rule.getLimitApp(), rule));
+            }
             default:
                 throw new IllegalStateException("unexpected verdict " + t.status);
         }
         remember(context, t);
-        // the slots after FlowSlot (AuthoritySlot has run before, DegradeSlot after)
         fireEntry(context, resourceWrapper, node, count, prioritized, args);
     }
 
     private static BlockException block(Context context, BlockException e) {
-        context.getCurEntry().setBlockError(e);               // StatisticSlot.java:99-101
+        context.getCurEntry().setBlockError(e);               // StatisticSlot.java:102-105
         return e;
     }
 
@@ -106,7 +154,7 @@ public class GpuFlowSlot extends AbstractLinkedProcessorSlot<DefaultNode> {
             t.entry = entry;
             t.createTs = context.getCurEntry().getCreateTimestamp();
             t.args = args;
-            engine.batcher.submit(t);                         // SF_V_EXIT: recorded (RT, success, thread count)
+            engine.batcher.submit(t);                         // SF_V_EXIT: StatisticSlot.exit + DegradeSlot.exit
         }
         fireExit(context, resourceWrapper, count, args);
     }

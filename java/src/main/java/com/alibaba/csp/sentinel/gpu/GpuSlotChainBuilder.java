@@ -3,8 +3,6 @@ package com.alibaba.csp.sentinel.gpu;
 import com.alibaba.csp.sentinel.slotchain.DefaultProcessorSlotChain;
 import com.alibaba.csp.sentinel.slotchain.ProcessorSlotChain;
 import com.alibaba.csp.sentinel.slotchain.SlotChainBuilder;
-import com.alibaba.csp.sentinel.slots.block.authority.AuthoritySlot;
-import com.alibaba.csp.sentinel.slots.block.degrade.DegradeSlot;
 import com.alibaba.csp.sentinel.slots.clusterbuilder.ClusterBuilderSlot;
 import com.alibaba.csp.sentinel.slots.logger.LogSlot;
 import com.alibaba.csp.sentinel.slots.nodeselector.NodeSelectorSlot;
@@ -13,11 +11,13 @@ import com.alibaba.csp.sentinel.spi.Spi;
 /**
  * SlotChainProvider.newSlotChain() takes the first SlotChainBuilder that is
  * not the default (SlotChainProvider.java:39-56, SpiLoader.java:228-238).
- * This one keeps the reference's slots around the GPU slot; the statistic,
- * system, param-flow and flow checks are one GpuFlowSlot.  AuthoritySlot runs
- * before it (its origin check reads no statistics); DegradeSlot after it, as
- * in the reference order (Constants.ORDER_*).  For the GPU circuit breakers
- * replace DegradeSlot with a slot over sf_degrade_submit (INTEGRATION.md §2).
+ * The reference's slots before StatisticSlot stay (NodeSelectorSlot -10000,
+ * ClusterBuilderSlot -9000, LogSlot -8000); StatisticSlot and everything it
+ * wraps -- AuthoritySlot, SystemSlot, ParamFlowSlot, FlowSlot, DegradeSlot
+ * (Constants.java:77-84) -- is one GpuFlowSlot: the engine accounts for every
+ * outcome of those slots as StatisticSlot does (StatisticSlot.java:55-131),
+ * including the circuit breakers (DegradeRuleManager's rules, loaded into the
+ * engine) and AuthorityExceptions (AuthoritySlot runs inside GpuFlowSlot).
  */
 @Spi(order = -100)
 public final class GpuSlotChainBuilder implements SlotChainBuilder {
@@ -27,9 +27,7 @@ public final class GpuSlotChainBuilder implements SlotChainBuilder {
         chain.addLast(new NodeSelectorSlot());
         chain.addLast(new ClusterBuilderSlot());
         chain.addLast(new LogSlot());
-        chain.addLast(new AuthoritySlot());
         chain.addLast(new GpuFlowSlot(GpuEngine.get()));
-        chain.addLast(new DegradeSlot());
         return chain;
     }
 }

@@ -57,7 +57,7 @@ final class SentinelFlowNative {
     static final MethodHandle REQUEST_TOKENS = fn("sf_request_tokens",
             FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
 
-    /** sf_config (sentinel_flow.h): 19 fields, natural alignment. */
+    /** sf_config (sentinel_flow.h): 19 fields, natural alignment: 88 bytes. */
     static final StructLayout CONFIG = MemoryLayout.structLayout(
             JAVA_INT.withName("sample_count"), JAVA_INT.withName("interval_ms"),
             JAVA_INT.withName("occupy_timeout_ms"), JAVA_INT.withName("cold_factor"),
@@ -91,6 +91,13 @@ final class SentinelFlowNative {
             JAVA_INT.withName("max_queueing_time_ms"), JAVA_INT.withName("burst_count"),
             JAVA_LONG.withName("duration_in_sec"), JAVA_INT.withName("item_offset"),
             JAVA_INT.withName("item_count"));
+
+    /** sf_degrade_rule: 40 bytes. */
+    static final StructLayout DEGRADE_RULE = MemoryLayout.structLayout(
+            JAVA_INT.withName("resource"), JAVA_INT.withName("grade"), JAVA_DOUBLE.withName("count"),
+            JAVA_INT.withName("time_window_s"), JAVA_INT.withName("min_request_amount"),
+            JAVA_DOUBLE.withName("slow_ratio_threshold"), JAVA_INT.withName("stat_interval_ms"),
+            JAVA_INT.withName("pad"));
 
     /** sf_system_rule: 40 bytes (negative = unset). */
     static final StructLayout SYSTEM_RULE = MemoryLayout.structLayout(
@@ -126,12 +133,17 @@ final class SentinelFlowNative {
             ADDRESS.withName("status"), ADDRESS.withName("remaining"), ADDRESS.withName("wait_ms"));
 
     // SF_EV_* / SF_V_* / SF_TOK_* / SF_TAG_* (sentinel_flow.h)
-    static final byte EV_EXIT = 0x01, EV_IN = 0x02, EV_PRIO = 0x04, EV_ERROR = 0x08;
+    static final byte EV_EXIT = 0x01, EV_IN = 0x02, EV_PRIO = 0x04, EV_ERROR = 0x08, EV_BLOCKED = 0x10;
     static final int V_PASS = 0, V_PASS_WAIT = 1, V_PRIORITY_WAIT = 2, V_BLOCK_FLOW = 3, V_BLOCK_PARAM = 4,
-            V_BLOCK_SYSTEM = 5, V_EXIT = 6, V_EXIT_IGNORED = 7, V_BLOCK_DEGRADE = 8;
+            V_BLOCK_SYSTEM = 5, V_EXIT = 6, V_EXIT_IGNORED = 7, V_BLOCK_DEGRADE = 8, V_BLOCK_OTHER = 9;
     static final byte TOK_PRIORITIZED = 0x01, TOK_PARAM = 0x02;
     static final byte TAG_NULL = 0, TAG_INT = 1, TAG_LONG = 2, TAG_STRING = 3, TAG_DOUBLE = 4, TAG_BOOL = 5,
             TAG_OTHER = 6, TAG_BYTE = 7, TAG_SHORT = 8, TAG_FLOAT = 9, TAG_COLLECTION = 0x40;
+
+    /** Byte offset of a named field (the C struct's offsetof; tests/test_java_shim.py). */
+    static long off(StructLayout layout, String field) {
+        return layout.byteOffset(MemoryLayout.PathElement.groupElement(field));
+    }
 
     static void check(int rc) {
         if (rc != 0) {

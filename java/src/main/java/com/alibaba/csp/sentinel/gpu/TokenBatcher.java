@@ -110,19 +110,25 @@ final class TokenBatcher implements Runnable {
                 for (Object v : r.params) {
                     if (nv == maxValues) throw new IllegalStateException("too many parameter values in one batch");
                     ptag.setAtIndex(JAVA_BYTE, nv, ParamPacker.tag(v));
-                    pbits.setAtIndex(JAVA_LONG, nv, v instanceof String ? ParamPacker.stringKey((String) v) : ParamPacker.bits(v));
+                    pbits.setAtIndex(JAVA_LONG, nv, ParamPacker.bits(v));      // a String: sf_string_key
                     nv++;
                 }
             }
             poff.setAtIndex(JAVA_INT, i + 1, nv);
         }
-        batch.set(JAVA_INT, 0, n); batch.set(JAVA_INT, 4, 0);
-        batch.set(ADDRESS, 8, flow); batch.set(ADDRESS, 16, cnt); batch.set(ADDRESS, 24, flags); batch.set(ADDRESS, 32, ts);
-        batch.set(ADDRESS, 40, anyParam ? ptag : MemorySegment.NULL);
-        batch.set(ADDRESS, 48, anyParam ? pbits : MemorySegment.NULL);
-        batch.set(ADDRESS, 56, anyParam ? poff : MemorySegment.NULL);
-        results.set(JAVA_INT, 0, 0);
-        results.set(ADDRESS, 8, status); results.set(ADDRESS, 16, remaining); results.set(ADDRESS, 24, waitMs);
+        batch.set(JAVA_INT, off(TOKEN_BATCH, "n"), n);
+        batch.set(JAVA_INT, off(TOKEN_BATCH, "mem"), 0);
+        batch.set(ADDRESS, off(TOKEN_BATCH, "flow_id"), flow);
+        batch.set(ADDRESS, off(TOKEN_BATCH, "count"), cnt);
+        batch.set(ADDRESS, off(TOKEN_BATCH, "flags"), flags);
+        batch.set(ADDRESS, off(TOKEN_BATCH, "ts_ms"), ts);
+        batch.set(ADDRESS, off(TOKEN_BATCH, "param_tag"), anyParam ? ptag : MemorySegment.NULL);
+        batch.set(ADDRESS, off(TOKEN_BATCH, "param_bits"), anyParam ? pbits : MemorySegment.NULL);
+        batch.set(ADDRESS, off(TOKEN_BATCH, "param_off"), anyParam ? poff : MemorySegment.NULL);
+        results.set(JAVA_INT, off(TOKEN_RESULTS, "mem"), 0);
+        results.set(ADDRESS, off(TOKEN_RESULTS, "status"), status);
+        results.set(ADDRESS, off(TOKEN_RESULTS, "remaining"), remaining);
+        results.set(ADDRESS, off(TOKEN_RESULTS, "wait_ms"), waitMs);
         check((int) REQUEST_TOKENS.invokeExact(engine.handle, batch, results));
         for (int i = 0; i < n; i++) {
             Req r = b.get(i);

@@ -1,0 +1,127 @@
+"""The Java SPI shim (java/) against the C ABI, statically: there is no JDK in
+this image, so the sources are read, not compiled.  Every Panama FFM struct
+layout equals the C struct (field offsets by gcc's offsetof, total size by
+sizeof: arrays of structs are strided by the layout size), every write goes
+through a named field of the right width, every flag / verdict / tag constant
+equals the header's, every downcall names an exported function, the chain
+matches the reference's StatisticSlot accounting (StatisticSlot.java:55-131:
+no reference DegradeSlot after the GPU slot, AuthoritySlot run inside it,
+PriorityWait without fireEntry), and INTEGRATION.md quotes the sources
+verbatim."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from tests import javashim as j
+from tests.test_abi import HEADER, declared_functions
+
+ROOT = j.ROOT
+
+
+@pytest.fixture(scope="module")
+def c_layout(tmp_path_factory):
+    """{struct: (sizeof, {field: (offsetof, sizeof)})} for the structs the shim mirrors."""
+    lay = j.layouts()
+    lines = []
+    for jl, cs in j.C_STRUCT.items():
+        lines.append('printf("%s - %%zu 0\\n", sizeof(%s));' % (cs, cs))
+        for f, _, _ in lay[jl][1]:
+            lines.append('printf("%s %s %%zu %%zu\\n", offsetof(%s, %s), sizeof(((%s*)0)->%s));'
+                         % (cs, f, cs, f, cs, f))
+    d = tmp_path_factory.mktemp("jshim")
+    prog = d / "off.c"
+    prog.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s"\nint main(void){\n%s\nreturn 0;}\n'
+                    % (HEADER, "\n".join(lines)))
+    exe = d / "off"
+    subprocess.check_call(["gcc", "-o", str(exe), str(prog)])
+    out = {}
+    for l in subprocess.check_output([str(exe)]).decode().split("\n"):
+        if not l.strip():
+            continue
+        s, f, a, b = l.split()
+        ent = out.setdefault(s, [0, {}])
+        if f == "-":
+            ent[0] = int(a)
+        else:
+            ent[1][f] = (int(a), int(b))
+    return out
+
+
+def test_every_layout_matches_the_c_struct(c_layout):
+    for jl, (size, fields) in j.layouts().items():
+        cs = j.C_STRUCT[jl]
+        csize, cf = c_layout[cs]
+        assert size == csize, f"{jl}: FFM layout {size} B, sizeof({cs}) {csize} B"
+        for f, off, sz in fields:
+            assert cf[f] == (off, sz), f"{jl}.{f}: Java ({off}, {sz}) vs C {cf[f]}"
+
+
+def test_layouts_cover_the_whole_struct(c_layout):
+    """No C field is missing from a layout (its bytes would be left as padding)."""
+    src = open(HEADER).read()
+    for jl, cs in j.C_STRUCT.items():
+        body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cs, cs), src, re.S).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        names = re.findall(r"(\w+)(?:\[\w+\])?\s*;", body)
+        have = {f for f, _, _ in j.layouts()[jl][1]}
+        missing = [n for n in names if n not in have and not n.startswith("pad")]
+        assert not missing, f"{jl}: {missing}"
+
+
+def test_writes_use_named_fields_of_the_right_width(c_layout):
+    lay = j.layouts()
+    refs = j.field_refs()
+    assert len(refs) > 60
+    for fn, l, f, t in refs:
+        fields = {a: c for a, b, c in lay[l][1]}
+        assert f in fields, f"{fn}: {l} has no field {f}"
+        assert j.SIZES[t] == fields[f], f"{fn}: {l}.{f} written as {t}"
+    assert j.numeric_struct_writes() == []
+
+
+def test_constants_equal_the_header():
+    src = open(HEADER).read()
+    hdr = {k: int(v.rstrip("u"), 0) for k, v in re.findall(r"#define (SF_\w+)\s+(-?0x[0-9a-fA-F]+u?|-?\d+)", src)}
+    for k, v in j.constants().items():
+        assert hdr["SF_" + k] == v, f"{k}: Java {v} vs header {hdr['SF_' + k]}"
+    assert {"EV_BLOCKED", "V_BLOCK_DEGRADE", "V_BLOCK_OTHER"} <= set(j.constants())
+
+
+def test_downcalls_name_declared_functions():
+    fns = set(declared_functions())
+    for f in j.downcalls():
+        assert f in fns, f
+
+
+def test_chain_is_statistic_slot_accounting():
+    """StatisticSlot wraps AuthoritySlot .. DegradeSlot (Constants.java:77-84):
+    all of them are inside GpuFlowSlot / the engine."""
+    builder = j.source("GpuSlotChainBuilder.java")
+    chain = re.findall(r"chain\.addLast\(new (\w+)\(", builder)
+    assert chain == ["NodeSelectorSlot", "ClusterBuilderSlot", "LogSlot", "GpuFlowSlot"]
+    for fn in os.listdir(j.JDIR):
+        assert "new DegradeSlot(" not in j.source(fn), fn
+    slot = j.source("GpuFlowSlot.java")
+    assert "authority.entry(" in slot and "EV_BLOCKED" in slot and "catch (AuthorityException" in slot
+    assert "case V_BLOCK_DEGRADE" in slot and "new DegradeException(" in slot
+    pw = slot[slot.index("case V_PRIORITY_WAIT"):]
+    pw = pw[:pw.index("case V_BLOCK_FLOW")]
+    assert "return;" in pw and "fireEntry" not in pw
+    eng = j.source("GpuEngine.java")
+    assert "DegradeRuleManager.getRules()" in eng and "LOAD_DEGRADE.invokeExact" in eng
+    pk = j.source("ParamPacker.java")
+    assert "paramFlowKey()" in pk and "STRINGS" not in pk
+    assert "ParamPacker.key(" in j.source("EventBatcher.java")
+
+
+def test_integration_md_quotes_the_sources():
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```java\n// java/\.\.\./(\w+\.java)\n(.*?)```", doc, re.S)
+    assert len(blocks) >= 2
+    for fn, body in blocks:
+        src = j.source(fn)
+        for line in body.split("\n"):
+            if line.strip():
+                assert line.strip() in src, f"INTEGRATION.md line not in {fn}: {line.strip()}"
