@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the whole-batch oracle replay (parity + cpu_baseline)")
     ap.add_argument("--no-metric-log", action="store_true")
     ap.add_argument("--no-degrade", action="store_true")
+    ap.add_argument("--no-legs", action="store_true", help="skip the config2 / config4 / config5 / end-to-end legs")
     ap.add_argument("--heavy-min", type=int, default=0,
                     help="segments of more events than this go to the heavy kernels (0: the engine default, 512)")
     args = ap.parse_args()
@@ -237,11 +238,31 @@ def main():
         except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
             degrade = {"error": str(ex)[:200]}
 
-    # whole-batch parity (batch 0 from a fresh engine vs the oracle replaying
-    # the same batch) -- the same replay, timed, is the CPU baseline
+    # the other BASELINE configs and the end-to-end form (rank 0, N=1 only;
+    # after the timed region, each on its own engine except e2e)
+    legs = {}
+    if rank == 0 and world == 1 and not args.no_legs:
+        for b in batches[1:]:
+            b.free()
+        batches = batches[:1]
+        for nm, fn in (("e2e_pinned", lambda: e2e_leg(eng, hb, steps * DURATION_MS)),
+                       ("config2", config2_leg), ("config4", config4_leg), ("config5", config5_leg)):
+            try:
+                t_leg = time.perf_counter()
+                legs[nm] = fn()
+                log(f"[leg {nm}] {time.perf_counter() - t_leg:.1f}s")
+            except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
+                legs[nm] = {"error": str(ex)[:300]}
+
+    # whole-batch parity: batch 0 from a fresh engine vs the one-core oracle
+    # replay of the same batch (that replay, timed, is the one-core CPU
+    # baseline), then the steady state: the resource-sharded oracle replays
+    # every batch of the run (warmup + timed, the first one timed as the
+    # multi-core CPU baseline) and the last timed batch's verdicts, a sample of
+    # nodes, their controller state and ENTRY_NODE are compared with the GPU's
     cpu, parity = None, None
     if rank == 0 and world == 1 and not args.no_cpu and args.warmup > 0:
-        cpu, parity = oracle_leg(rules, hb, R_local, out0)
+        cpu, parity = oracle_leg(rules, hb, R_local, out0, out, eng, steps, per_res)
 
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
@@ -254,13 +275,235 @@ def main():
                            "resources_touched": n_seg, "pass_fraction": round(n_pass / max(1, n_entry), 4),
                            "parallelism": f"resource-sharded x{world}"},
                 "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "aggregate": aggregate,
-                "metric_log": metric_log, "degrade": degrade}
+                "metric_log": metric_log, "degrade": degrade, **legs}
         print(json.dumps(line), flush=True)
     for b in batches[1:]:
         b.free()
     base.free()
     if dist:
         dist.destroy_process_group()
+
+
+def config2_leg(R=1_000_000, n=1 << 27, steps=3):
+    """BASELINE config 2 (its own engine): 1M resources, one QPS
+    DefaultController rule each (count U{5..50}), a uniform trace of 2^27
+    events per 4 s, HBM-resident batches decided back to back (async), and the
+    roofline of the whole pipeline with SURVEY.md §8(d)'s byte model
+    (25 B per event + 528 B per touched resource: 28.9 B per decision).
+    Parity: batch 0 against the resource-sharded oracle."""
+    counts = trace.uniform_rules(R)
+    rules = abi.flow_rules_np(np.arange(R, dtype=np.uint32), np.full(R, abi.GRADE_QPS, np.int32), counts,
+                              np.zeros(R, np.int32))
+    hb = trace.uniform_qps(R, n)
+    e = engine.FlowEngine(abi.default_config(max_resources=R, max_batch=hb.n))
+    try:
+        e.load_flow_rules(rules)
+        base = engine.DeviceBatch(e, hb)
+        bl = [base] + [engine.DeviceBatch.with_ts(e, base, hb.ts_ms + k * DURATION_MS) for k in range(1, steps + 1)]
+        out0 = engine.DeviceVerdicts(e, hb.n, with_wait=True, with_rule=True)
+        out = engine.DeviceVerdicts(e, hb.n, with_wait=True, with_rule=False)
+        e.submit_device_async(bl[0], out0)
+        e.sync()
+        t = time.perf_counter()
+        for k in range(1, steps + 1):
+            e.submit_device_async(bl[k], out)
+        e.sync()
+        wall = (time.perf_counter() - t) / steps
+        touched = int(np.count_nonzero(np.bincount(hb.res_id, minlength=R)))
+        b_alg = 25 * hb.n + 528 * touched
+        res = {"what": "config2: 1M resources uniform, QPS DefaultController (count U{5..50}), 2^27 events / 4 s, "
+                       "HBM-resident, batches pipelined", "events_per_batch": int(hb.n), "resources_touched": touched,
+               "ms_per_step": round(wall * 1e3, 3), "decisions_per_s": round(hb.n / wall, 1),
+               "roofline": {"bound": "hbm", "what": "whole pipeline, SURVEY §8(d) byte model",
+                            "alg_bytes_per_step": b_alg, "bytes_per_decision": round(b_alg / hb.n, 2),
+                            "achieved": round(b_alg / wall / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(b_alg / wall / 1e9 / HBM_PEAK_GBS, 5)},
+               "pass_fraction": round(float(np.isin(out.status.numpy(), abi.PASSED).mean()), 4)}
+        try:
+            from oracle import sharded
+            g = out0.status.numpy()
+            v, dt = sharded.replay(rules, hb, R, 16)
+            res["parity"] = {"what": "batch 0 vs the resource-sharded oracle (16 threads)",
+                             "mismatches": int((g != v.status).sum()), "exact": bool((g == v.status).all())}
+            res["cpu_baseline"] = {"value": round(hb.n / dt, 1), "unit": "decisions/s", "cores": 16, "kind": "port",
+                                   "sample": "batch 0, resource-sharded C oracle"}
+        except Exception as ex:  # pragma: no cover
+            res["parity"] = {"error": str(ex)[:200]}
+        for b in bl:
+            b.free()
+        return res
+    finally:
+        e.close()
+
+
+def config4_leg(R=1000, n=1 << 24, keys=100_000_000, qps_frac=0.6, reps=3):
+    """BASELINE config 4 (its own engine): 1k resources with one QPS
+    ParamFlowRule each (+10 % with a throttle rule), keys Zipf(1.1) over 100M
+    distinct values, every event EntryType.IN, and the inbound-QPS SystemRule
+    at qps_frac x the offered rate so that it blocks (the ParamFlow rules block
+    ~21 %, so at 0.8x the SystemRule never fires).  One sf_submit of an
+    HBM-resident batch from a fresh engine per rep; the planner cuts it into
+    safe sub-batches (sf_system.h).  Parity: every verdict against the
+    one-core oracle."""
+    rules, b = trace.param_zipf(R, n, keys, duration_ms=DURATION_MS, seed=4)
+    offered = b.n / (DURATION_MS / 1000.0)
+    sysr = [abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=qps_frac * offered,
+                               avg_rt=-1, max_thread=-1)]
+    pairs = np.unique(b.res_id.astype(np.uint64) << np.uint64(40) ^ (b.arg_bits[0] & np.uint64((1 << 40) - 1))).size
+    cap = 1 << int(np.ceil(np.log2(max(2.5 * pairs * 1.1, 1 << 16))))
+    cfg = abi.default_config(max_resources=R, max_batch=b.n, param_capacity=cap)
+    walls, st, tab, rounds = [], None, None, 0
+    for rep in range(reps):
+        e = engine.FlowEngine(cfg)
+        try:
+            e.load_system_rules(sysr)
+            e.load_param_rules(rules)
+            db = engine.DeviceBatch(e, b)
+            dv = engine.DeviceVerdicts(e, b.n, with_wait=True, with_rule=True)
+            e.set_timing(True)
+            e.sync()
+            t = time.perf_counter()
+            e.submit_device(db, dv)
+            walls.append(time.perf_counter() - t)
+            if rep == reps - 1:
+                st = (dv.status.numpy(), dv.wait_ms.numpy(), dv.rule_idx.numpy())
+                tab = e.param_table_stats()
+                rounds = int(e.stats().sys_rounds)
+            db.free()
+            dv.free()
+        finally:
+            e.close()
+    ms = 1e3 * float(np.median(walls))
+    ent = int(((b.flags & abi.EV_EXIT) == 0).sum())
+    res = {"what": f"config4: ParamFlow 100M-key Zipf(1.1) on {R} resources + SystemRule qps {qps_frac}x offered, "
+                   f"one HBM-resident batch from a fresh engine", "events": int(b.n),
+           "ms_per_batch": round(ms, 3), "decisions_per_s": round(ent / (ms / 1e3), 1),
+           "planner_rounds": rounds, "distinct_pairs": int(pairs), "param_table": tab,
+           "load_factor": round(tab["used"] / tab["capacity"], 4) if tab else None,
+           "system_blocks": int((st[0] == abi.V_BLOCK_SYSTEM).sum()),
+           "param_blocks": int((st[0] == abi.V_BLOCK_PARAM).sum()),
+           "passed": int(np.isin(st[0], abi.PASSED).sum()), "reps_ms": [round(1e3 * w, 3) for w in walls]}
+    try:
+        from oracle import oracle as so
+        o = so.OracleEngine(cfg)
+        o.load_system_rules(sysr)
+        o.load_param_rules(rules)
+        t = time.perf_counter()
+        want = o.submit(b)
+        dt = time.perf_counter() - t
+        o.close()
+        bad = {"status": int((st[0] != want.status).sum()), "wait_ms": int((st[1] != want.wait_ms).sum()),
+               "rule_idx": int((st[2] != want.rule_idx).sum())}
+        res["parity"] = {"what": "every verdict vs the one-core oracle replay", "mismatches": bad,
+                         "exact": all(v == 0 for v in bad.values())}
+        res["cpu_baseline"] = {"value": round(ent / dt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+                               "sample": "the whole batch, one-core C oracle"}
+    except Exception as ex:  # pragma: no cover
+        res["parity"] = {"error": str(ex)[:200]}
+    return res
+
+
+def config5_leg(n_req=1 << 22, n_streams=500, steps=3):
+    """BASELINE config 5 (its own engine): the cluster token server for 500
+    client connections -- 10k flow rules + 1k param rules (Zipf(1.1) values
+    over 1M), 10 % prioritized, namespace limiter open.  sf_serve_frames: the
+    raw C1 request frames of all connections in, response frames out (device
+    clock, framing to encoded responses); sf_request_tokens: the same requests
+    as a token batch (wall clock incl. PCIe).  Parity: a 64k-request instance
+    replayed through the oracle's wire path, every response byte compared."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import wire_bench
+    ns, flow, param, streams = wire_bench.frames(n_req, n_streams, 7)
+    cfg = abi.default_config(max_resources=4, max_batch=n_req, param_capacity=1 << 22)
+    cfg.max_flow_ids = 1 << 15
+    e = engine.FlowEngine(cfg)
+    try:
+        e.load_namespaces(ns)
+        e.load_cluster_rules(flow, param, [])
+        e.serve_frames(streams, trace.T0)
+        e.set_timing(True)
+        dev, wall = [], []
+        for k in range(steps):
+            t = time.perf_counter()
+            r = e.serve_frames(streams, trace.T0 + 1000 * (k + 1))
+            wall.append(time.perf_counter() - t)
+            dev.append(e.stats().wire_ms)
+        n_bytes = sum(len(x) for x in streams)
+        ms = float(np.median(dev))
+        res = {"what": "config5: cluster token server, 500 connections, C1 frames -> DefaultTokenService -> frames",
+               "requests": int(r.n_requests), "in_bytes": int(n_bytes), "out_bytes": int(r.n_responses) * 16,
+               "serve_frames": {"device_ms": round(ms, 3), "requests_per_s": round(r.n_requests / (ms / 1e3), 1),
+                                "wall_ms_incl_pcie": round(float(np.median(wall)) * 1e3, 2)}}
+    finally:
+        e.close()
+    # sf_request_tokens on a decoded batch of the same shape
+    tns, tflow, tparam, titems, tbatch = trace.token_workload(n_req, n_flow=10_000, n_param=1000, n_values=1 << 20,
+                                                              connected=n_streams, max_qps=1e12)
+    cfg3 = abi.default_config(max_resources=4, max_batch=n_req, param_capacity=1 << 22)
+    cfg3.max_flow_ids = 1 << 15
+    e = engine.FlowEngine(cfg3)
+    try:
+        e.load_namespaces(tns)
+        e.load_cluster_rules(tflow, tparam, titems)
+        w = []
+        for k in range(steps):
+            tb = abi.HostTokenBatch(tbatch.flow_id, tbatch.count, tbatch.flags, tbatch.ts_ms + k * DURATION_MS,
+                                    param_tag=tbatch.param_tag, param_bits=tbatch.param_bits)
+            t = time.perf_counter()
+            e.request_tokens(tb)
+            w.append(time.perf_counter() - t)
+        ms = float(np.median(w)) * 1e3
+        res["request_tokens"] = {"requests": int(tbatch.n), "wall_ms_incl_pcie": round(ms, 3),
+                                 "requests_per_s": round(tbatch.n / (ms / 1e3), 1)}
+    except Exception as ex:  # pragma: no cover
+        res["request_tokens"] = {"error": str(ex)[:200]}
+    finally:
+        e.close()
+    try:
+        from oracle import oracle as so
+        ns2, flow2, param2, st2 = wire_bench.frames(1 << 16, n_streams, 8)
+        cfg2 = abi.default_config(max_resources=4, max_batch=1 << 16, param_capacity=1 << 18)
+        cfg2.max_flow_ids = 1 << 15
+        g = engine.FlowEngine(cfg2)
+        o = so.OracleEngine(cfg2)
+        for x in (g, o):
+            x.load_namespaces(ns2)
+            x.load_cluster_rules(flow2, param2, [])
+        rg, ro = g.serve_frames(st2, trace.T0), o.serve_frames(st2, trace.T0)
+        same = all(rg.responses(s) == ro.responses(s) for s in range(n_streams))
+        g.close()
+        o.close()
+        res["parity"] = {"what": "64k requests over 500 connections: every response frame vs the oracle's wire path",
+                         "requests": int(ro.n_requests), "exact": bool(same)}
+    except Exception as ex:  # pragma: no cover
+        res["parity"] = {"error": str(ex)[:200]}
+    return res
+
+
+def e2e_leg(eng, hb, t_shift, reps=3):
+    """Config 3 end to end from page-locked host memory (sf_host_alloc): each
+    sf_submit copies the batch H2D, decides it and copies the verdicts back
+    (status, wait, rule index), timed on the wall clock -- the PCIe-inclusive
+    rate a host that submits from its own buffers sees (never the headline)."""
+    pin = engine.PinnedArrays(eng)
+    try:
+        hp = pin.batch(hb)
+        vp = pin.verdicts(hb.n)
+        w = []
+        for k in range(reps):
+            hp.ts_ms[...] = hb.ts_ms + t_shift + k * DURATION_MS
+            t = time.perf_counter()
+            eng.submit(hp, vp)
+            w.append(time.perf_counter() - t)
+        ms = float(np.median(w)) * 1e3
+        in_b = hb.n * (4 + 8 + 4 + 1) + int(((hb.flags & abi.EV_EXIT) != 0).sum()) * 8
+        out_b = hb.n * (1 + 4 + 2)
+        ent = int(((hb.flags & abi.EV_EXIT) == 0).sum())
+        return {"what": "config3 batch from pinned host buffers: H2D + decide + D2H per sf_submit (not pipelined)",
+                "events": int(hb.n), "ms_per_batch": round(ms, 3), "decisions_per_s": round(ent / (ms / 1e3), 1),
+                "h2d_bytes": in_b, "d2h_bytes": out_b, "reps_ms": [round(x * 1e3, 2) for x in w]}
+    finally:
+        pin.free()
 
 
 def degrade_leg(R=1_000_000, entries=1 << 22, steps=3):
@@ -334,13 +577,24 @@ def metric_log_leg(eng, hb, R_total, R_local, world, rank, steps):
             "sample_line": data[:data.find(b"\n")].decode(errors="replace") if data else ""}
 
 
-def oracle_leg(rules, hb, R, out0):
-    """The C restatement (oracle/, test infrastructure) replays the whole
-    batch 0 on one host core from fresh state: its verdicts are compared with
-    the GPU's verdicts of that batch (status, wait, rule index: parity), and
-    its time is the CPU baseline."""
+def oracle_leg(rules, hb, R, out0, out_last, eng, steps, per_res):
+    """The C restatement (oracle/, test infrastructure only).
+
+    1. One core replays batch 0 from fresh state: verdicts compared with the
+       GPU's batch 0 (status, wait, rule index of blocks); its time is the
+       one-core CPU baseline.
+    2. The resource-sharded oracle (one OracleEngine per res % T shard on T
+       host threads, oracle/sharded.py) replays every batch of the run in
+       order -- the same trace shifted by DURATION_MS per step, state carried
+       across batches (minute buckets reused after the 60 s wrap, RateLimiter
+       latestPassedTime, WarmUp tokens).  Batch 0's replay time is the
+       multi-core CPU baseline (its verdicts must equal the one-core replay);
+       the last batch's verdicts (status, wait) are compared with the GPU's
+       last timed batch, and so are the node state and controller state of a
+       sample of resources (the 64 busiest and 1024 others) and ENTRY_NODE."""
     try:
         from oracle import oracle as so
+        from oracle import sharded
     except Exception as ex:  # pragma: no cover
         return {"error": str(ex)}, {"error": str(ex)}
     ora = so.OracleEngine(abi.default_config(max_resources=R, max_batch=hb.n))
@@ -359,27 +613,56 @@ def oracle_leg(rules, hb, R, out0):
     single = {"value": round(ent / dt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
               "sample": f"the whole batch 0 ({hb.n} events, {ent} entries) of the timed workload from fresh state, "
                         f"single-threaded C oracle (rule load {t_load:.1f}s excluded)", "seconds": round(dt, 2)}
-    # the multi-core CPU baseline: the same batch split by resource
-    # over the box's cores, one oracle per shard (oracle/sharded.py)
     cpu = single
+    steady = None
     try:
-        from oracle import sharded
         try:
             ncore = len(os.sched_getaffinity(0))
         except AttributeError:  # pragma: no cover
             ncore = os.cpu_count() or 1
         T = max(1, min(16, ncore))                       # the box's CPU share is 16
-        got, dtm = sharded.replay(rules, hb, R, T)
-        same = bool((got.status == want.status).all() and (got.wait_ms == want.wait_ms).all())
-        cpu = {"value": round(ent / dtm, 1), "unit": "decisions/s", "cores": T, "kind": "port",
-               "sample": f"the whole batch 0 ({hb.n} events, {ent} entries) split by resource (res % {T}) over {T} "
-                         f"threads, one C oracle per shard, verdicts merged (equal to the one-core replay: {same})",
-               "seconds": round(dtm, 2), "single_core": single}
+        sh = sharded.ShardedOracle(rules, R, T, hb.n)
+        sh.split_like(hb)
+        t_all = time.perf_counter()
+        for k in range(steps):
+            v, dtk = sh.submit(hb, k * DURATION_MS)
+            if k == 0:
+                same = bool((v.status == want.status).all() and (v.wait_ms == want.wait_ms).all())
+                cpu = {"value": round(ent / dtk, 1), "unit": "decisions/s", "cores": T, "kind": "port",
+                       "sample": f"the whole batch 0 ({hb.n} events, {ent} entries) split by resource (res % {T}) "
+                                 f"over {T} threads, one C oracle per shard, verdicts merged (equal to the one-core "
+                                 f"replay: {same})", "seconds": round(dtk, 2), "single_core": single}
+        t_all = time.perf_counter() - t_all
+        gs, gw = out_last.status.numpy(), out_last.wait_ms.numpy()
+        busiest = np.argsort(-per_res)[:64]
+        rng = np.random.default_rng(99)
+        touched = np.nonzero(per_res)[0]
+        sample = np.unique(np.concatenate([busiest, rng.choice(touched, size=min(1024, touched.size), replace=False)]))
+        node_bad = rule_bad = 0
+        for r in sample:
+            if abi.node_state_to_dict(eng.read_node(int(r))) != abi.node_state_to_dict(sh.read_node(int(r))):
+                node_bad += 1
+            a, b = eng.read_rule_state(int(r)), sh.read_rule_state(int(r))
+            if (a.stored_tokens, a.last_filled_time, a.latest_passed_time) != \
+                    (b.stored_tokens, b.last_filled_time, b.latest_passed_time):
+                rule_bad += 1
+        from sentinel_amd import dist as sdist
+        en_same = abi.node_state_to_dict(eng.read_entry_node()) == \
+            abi.node_state_to_dict(sdist.merge_entry_nodes(sh.entry_nodes()))
+        sh.close()
+        lm = {"status": int((gs != v.status).sum()), "wait_ms": int((gw != v.wait_ms).sum()),
+              "nodes": node_bad, "rule_states": rule_bad, "entry_node": 0 if en_same else 1}
+        steady = {"what": f"every batch of the run ({steps}: warmup + timed, state carried across batches, "
+                          f"{steps * DURATION_MS // 1000} s of trace time) replayed by the resource-sharded oracle; "
+                          f"batch {steps - 1} (the last timed one) compared",
+                  "batch": steps - 1, "events": int(hb.n), "nodes_compared": int(sample.size),
+                  "mismatches": lm, "exact": all(x == 0 for x in lm.values()), "replay_s": round(t_all, 1)}
     except Exception as ex:  # pragma: no cover - the one-core figure stays
         cpu = dict(single, multicore_error=str(ex)[:200])
+        steady = {"error": str(ex)[:200]}
     parity = {"what": "batch 0 of the timed run (fresh engine) vs the oracle replay of the same batch",
               "events": int(hb.n), "mismatches": mism,
-              "exact": all(v == 0 for v in mism.values())}
+              "exact": all(v == 0 for v in mism.values()), "steady_state": steady}
     return cpu, parity
 
 

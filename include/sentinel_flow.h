@@ -666,6 +666,11 @@ int  sf_param_rule_order(const sf_param_rule* rules, const sf_rule_key* keys, ui
 int  sf_device_alloc(sf_engine* e, size_t bytes, void** ptr);
 int  sf_device_free(sf_engine* e, void* ptr);
 int  sf_memcpy(sf_engine* e, void* dst, const void* src, size_t bytes, int kind /*0 H2D 1 D2H 2 D2D*/);
+/* Page-locked host memory (hipHostMalloc): batch and verdict arrays of an
+ * SF_MEM_HOST sf_submit placed here move over PCIe by DMA at full rate
+ * instead of through pageable staging (the Java flusher's off-heap buffers). */
+int  sf_host_alloc(sf_engine* e, size_t bytes, void** ptr);
+int  sf_host_free(sf_engine* e, void* ptr);
 int  sf_sync(sf_engine* e);      /* waits for sf_submit_async batches; their first error */
 int  sf_get_stats(sf_engine* e, sf_stats* out);
 int  sf_set_timing(sf_engine* e, int enabled);

@@ -91,3 +91,68 @@ def replay(rules, hb: abi.HostBatch, R: int, T: int):
         v.wait_ms[idx] = outs[k].wait_ms
         v.rule_idx[idx] = outs[k].rule_idx
     return v, dt
+
+
+class ShardedOracle:
+    """The C oracle over T host threads for a sequence of batches of the same
+    resource set: one OracleEngine per resource shard (res % T) keeps its
+    state across batches.  ``split_like`` reuses one batch's partition for
+    batches that differ only in their timestamps (bench.py's time-shifted
+    steps)."""
+
+    def __init__(self, rules, R: int, T: int, max_batch: int):
+        from oracle import oracle as so
+        self.T = T
+        self.engines = []
+        for k in range(T):
+            e = so.OracleEngine(abi.default_config(max_resources=R // T + 1, max_batch=max(1, max_batch // T * 2 + 64)))
+            e.load_flow_rules(shard_rules(rules, T, k))
+            self.engines.append(e)
+        self.parts = None
+
+    def split_like(self, hb: abi.HostBatch):
+        self.parts = split(hb, self.T)
+
+    def submit(self, hb: abi.HostBatch, ts_shift: int = 0):
+        """Replays hb (partitioned like the split_like batch, timestamps +
+        ts_shift); returns (verdicts in batch order, seconds)."""
+        import time
+        if self.parts is None:
+            self.split_like(hb)
+        outs = [None] * self.T
+
+        def run(k):
+            idx, b = self.parts[k]
+            if ts_shift:
+                b = abi.HostBatch(b.res_id, b.ts_ms + ts_shift, b.count, b.flags, entry_ref=b.entry_ref,
+                                  create_ts=None if b.create_ts is None else b.create_ts + ts_shift)
+            outs[k] = self.engines[k].submit(b)
+
+        ths = [threading.Thread(target=run, args=(k,)) for k in range(self.T)]
+        t = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t
+        v = abi.HostVerdicts(hb.n)
+        for k in range(self.T):
+            idx = self.parts[k][0]
+            v.status[idx] = outs[k].status
+            v.wait_ms[idx] = outs[k].wait_ms
+            v.rule_idx[idx] = outs[k].rule_idx
+        return v, dt
+
+    def read_node(self, res: int):
+        return self.engines[res % self.T].read_node(res // self.T)
+
+    def read_rule_state(self, res_rule: int):
+        """Rule state of the resource's single rule (one rule per resource)."""
+        return self.engines[res_rule % self.T].read_rule_state(res_rule // self.T)
+
+    def entry_nodes(self):
+        return [e.read_entry_node() for e in self.engines]
+
+    def close(self):
+        for e in self.engines:
+            e.close()

@@ -66,6 +66,7 @@ struct sf_engine {
     bool timing = false;
     sf_stats stats{};
     std::vector<void*> user_allocs;
+    std::vector<void*> host_allocs;      // sf_host_alloc (pinned host memory)
     std::mutex mu;
     // cluster token server (sf_token.hip)
     TokState ts{};
@@ -164,6 +165,7 @@ void sf_destroy(sf_engine* e) {
                     e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out, e->plan_stage};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
+    for (void* p : e->host_allocs) hipHostFree(p);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
                      (void*)e->ts.items, e->ts.rmulti, e->tok_stage, e->wire_arena, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
                      e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch, e->st.last_ts, e->nm_bytes, e->nm_off,
@@ -1653,6 +1655,22 @@ int sf_device_free(sf_engine* e, void* ptr) {
     if (it == e->user_allocs.end()) return fail(SF_ERR_INVALID, "pointer not from sf_device_alloc");
     e->user_allocs.erase(it);
     HIP_TRY(hipFree(ptr));
+    return SF_OK;
+}
+int sf_host_alloc(sf_engine* e, size_t bytes, void** ptr) {
+    if (!e || !ptr) return fail(SF_ERR_INVALID, "null argument");
+    HIP_TRY(hipHostMalloc(ptr, bytes ? bytes : 16, hipHostMallocDefault));
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->host_allocs.push_back(*ptr);
+    return SF_OK;
+}
+int sf_host_free(sf_engine* e, void* ptr) {
+    if (!e) return fail(SF_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto it = std::find(e->host_allocs.begin(), e->host_allocs.end(), ptr);
+    if (it == e->host_allocs.end()) return fail(SF_ERR_INVALID, "pointer not from sf_host_alloc");
+    e->host_allocs.erase(it);
+    HIP_TRY(hipHostFree(ptr));
     return SF_OK;
 }
 int sf_memcpy(sf_engine* e, void* dst, const void* src, size_t bytes, int kind) {

@@ -72,6 +72,33 @@ def entry_node_allreduce(state: abi.sf_node_state, sample_count: int = 2, device
     return out
 
 
+def merge_entry_nodes(states, sample_count: int = 2, statistic_max_rt: int = 5000) -> abi.sf_node_state:
+    """The same merge over host copies of every shard's ENTRY_NODE (no
+    process group): per slot the latest window, SUM of its counters, MIN of
+    minRt, SUM of curThreadNum."""
+    arrs = [_state_arrays(st, sample_count) for st in states]
+    ws = np.stack([np.where(a[0] == abi.SF_WS_ABSENT, I64_MIN, a[0]) for a in arrs])
+    gws = ws.max(axis=0)
+    keep = (ws == gws[None, :]) & (ws != I64_MIN)
+    gcnt = sum(np.where(keep[k][:, None], arrs[k][1], 0) for k in range(len(arrs)))
+    gmin = np.min(np.stack([np.where(keep[k], arrs[k][2], np.iinfo(np.int64).max) for k in range(len(arrs))]), axis=0)
+    out = abi.sf_node_state()
+    for i in range(abi.SF_MAX_SAMPLE_COUNT):
+        out.second[i].window_start = abi.SF_WS_ABSENT
+        out.borrow_ws[i] = abi.SF_WS_ABSENT
+    buckets = [out.second[i] for i in range(sample_count)] + [out.minute[i] for i in range(abi.SF_MINUTE_BUCKETS)]
+    for k, b in enumerate(buckets):
+        if gws[k] == I64_MIN:
+            b.window_start = abi.SF_WS_ABSENT
+            continue
+        b.window_start = int(gws[k])
+        for j, f in enumerate(FIELDS):
+            setattr(b, f, int(gcnt[k, j]))
+        b.min_rt = int(gmin[k]) if gmin[k] != np.iinfo(np.int64).max else statistic_max_rt
+    out.cur_thread_num = int(sum(st.cur_thread_num for st in states))
+    return out
+
+
 def gather_snapshot(rows, group=None):
     """Gather every rank's MetricNode rows to rank 0 (object gather, off the decision path)."""
     import torch.distributed as dist

@@ -89,6 +89,8 @@ def _declare(L):
       C.POINTER(C.c_uint64))
     f("sf_device_alloc", I, P, C.c_size_t, C.POINTER(P))
     f("sf_device_free", I, P, P)
+    f("sf_host_alloc", I, P, C.c_size_t, C.POINTER(P))
+    f("sf_host_free", I, P, P)
     f("sf_memcpy", I, P, P, P, C.c_size_t, I)
     f("sf_sync", I, P)
     f("sf_get_stats", I, P, C.POINTER(abi.sf_stats))
@@ -178,6 +180,43 @@ class DeviceArray:
         if self.ptr:
             lib().sf_device_free(self.eng.h, self.ptr)
             self.ptr = None
+
+
+class PinnedArrays:
+    """numpy arrays in page-locked host memory (sf_host_alloc), freed together."""
+
+    def __init__(self, eng: "FlowEngine"):
+        self.eng, self.ptrs = eng, []
+
+    def array(self, shape, dtype, fill=None) -> np.ndarray:
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape)) * dtype.itemsize
+        p = P()
+        _check(lib().sf_host_alloc(self.eng.h, max(16, n), C.byref(p)))
+        self.ptrs.append(p.value)
+        a = np.ctypeslib.as_array((C.c_uint8 * max(16, n)).from_address(p.value))[:n].view(dtype).reshape(shape)
+        if fill is not None:
+            a[...] = fill
+        return a
+
+    def batch(self, hb: abi.HostBatch) -> abi.HostBatch:
+        """A copy of hb (res, ts, count, flags, entry_ref, create_ts) in pinned memory."""
+        def cp(x):
+            return None if x is None else self.array(x.shape, x.dtype, x)
+        return abi.HostBatch(cp(hb.res_id), cp(hb.ts_ms), cp(hb.count), cp(hb.flags), entry_ref=cp(hb.entry_ref),
+                             create_ts=cp(hb.create_ts))
+
+    def verdicts(self, n: int, with_wait=True, with_rule=True) -> abi.HostVerdicts:
+        v = abi.HostVerdicts(n)
+        v.status = self.array((n,), np.uint8)
+        v.wait_ms = self.array((n,), np.int32) if with_wait else None
+        v.rule_idx = self.array((n,), np.uint16) if with_rule else None
+        return v
+
+    def free(self):
+        for p in self.ptrs:
+            lib().sf_host_free(self.eng.h, p)
+        self.ptrs = []
 
 
 class DeviceBatch:
@@ -280,8 +319,8 @@ class FlowEngine:
     def set_system_status(self, load, cpu):
         _check(lib().sf_set_system_status(self.h, load, cpu))
 
-    def submit(self, batch: abi.HostBatch) -> abi.HostVerdicts:
-        out = abi.HostVerdicts(batch.n)
+    def submit(self, batch: abi.HostBatch, out: abi.HostVerdicts = None) -> abi.HostVerdicts:
+        out = abi.HostVerdicts(batch.n) if out is None else out
         b = batch.c_struct()
         v = out.c_struct()
         _check(lib().sf_submit(self.h, C.byref(b), C.byref(v)))

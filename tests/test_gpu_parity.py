@@ -32,6 +32,17 @@ def test_config3_many_batches(eng_mod, so, heavy_min):
     workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
 
 
+def test_long_run_minute_wrap(eng_mod, so):
+    """70 s of config-3 traffic in 7 batches with the default split (light
+    segments up to 512 events on the lane walks): nodes (minute buckets
+    reused after the 60 s wrap), every rule's controller state (WarmUp tokens,
+    RateLimiter latestPassedTime) and ENTRY_NODE equal the oracle's."""
+    w = workloads.long_run()
+    eng, ora, outs = workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
+    span = int(w["batches"][-1].ts_ms[-1] - w["batches"][0].ts_ms[0])
+    assert span > 60_000, span
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_heavy_edge_traces(eng_mod, so, seed):
     from tests.test_hostsim_parity import test_heavy_edge_traces as body

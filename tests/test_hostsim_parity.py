@@ -129,3 +129,11 @@ def test_heavy_thread_traces(hs, so, seed):
     mc = (C.c_uint64 * 8)()
     hs.lib().hs_mode_counts(eng.h, mc)
     assert mc[6] >= 8     # SM_THREAD segments
+
+
+def test_long_run_minute_wrap(hs, so):
+    """70 s of config-3 traffic in 7 batches on the host build of the lane
+    walk and the window paths: minute-bucket reuse after the 60 s wrap,
+    controller state carried across batches."""
+    w = workloads.long_run(R=4000, n=300_000)
+    workloads.run(hs.HostSimEngine, so.OracleEngine, w)

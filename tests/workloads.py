@@ -330,6 +330,20 @@ def xflow(seed=51, R=400, n=60_000, origins=6, contexts=4, duration_ms=6000, zip
                 context_nodes=sorted(dn))
 
 
+def long_run(R=20_000, n=1_400_000, duration_ms=70_000, batches=7, seed=61):
+    """Config 3's traffic over 70 s of trace time in 7 batches: light lane
+    walks (most resources see tens of events) across the minute-window wrap
+    (buckets reused after 60 s), WarmUp token state, RateLimiter
+    latestPassedTime and THREAD exits carried across batches."""
+    rules = trace.mixed_rules(R, seed=seed)
+    full = trace.mixed_zipf(R, n, duration_ms=duration_ms, seed=seed)
+    cuts = np.linspace(0, full.n, batches + 1).astype(int)
+    bl = [full.subset(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
+    hot = np.argsort(-np.bincount(full.res_id, minlength=R))[:40]
+    return dict(cfg=abi.default_config(max_resources=R, max_batch=max(b.n for b in bl)), flow=rules, batches=bl,
+                nodes=sorted(set(int(x) for x in hot) | set(range(0, R, 53))), n_flow=len(rules))
+
+
 def preblocked(w, frac=0.05, seed=0):
     """The workload with a fraction of its entries flagged SF_EV_BLOCKED: blocked
     by AuthoritySlot, which StatisticSlot wraps (StatisticSlot.java:102-124)
