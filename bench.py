@@ -249,6 +249,7 @@ def main():
                        ("config2", config2_leg), ("config4", config4_leg), ("config5", config5_leg)):
             try:
                 t_leg = time.perf_counter()
+                log(f"[leg {nm}] ...")
                 legs[nm] = fn()
                 log(f"[leg {nm}] {time.perf_counter() - t_leg:.1f}s")
             except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
@@ -353,6 +354,7 @@ def config4_leg(R=1000, n=1 << 24, keys=100_000_000, qps_frac=0.6, reps=3):
     cap = 1 << int(np.ceil(np.log2(max(2.5 * pairs * 1.1, 1 << 16))))
     cfg = abi.default_config(max_resources=R, max_batch=b.n, param_capacity=cap)
     walls, st, tab, rounds = [], None, None, 0
+    log(f"[leg config4] trace {b.n} events, ~{pairs} (resource, key) pairs")
     for rep in range(reps):
         e = engine.FlowEngine(cfg)
         try:
@@ -383,6 +385,7 @@ def config4_leg(R=1000, n=1 << 24, keys=100_000_000, qps_frac=0.6, reps=3):
            "system_blocks": int((st[0] == abi.V_BLOCK_SYSTEM).sum()),
            "param_blocks": int((st[0] == abi.V_BLOCK_PARAM).sum()),
            "passed": int(np.isin(st[0], abi.PASSED).sum()), "reps_ms": [round(1e3 * w, 3) for w in walls]}
+    log(f"[leg config4] GPU {ms:.1f} ms per batch; oracle replay ...")
     try:
         from oracle import oracle as so
         o = so.OracleEngine(cfg)
@@ -601,9 +604,11 @@ def oracle_leg(rules, hb, R, out0, out_last, eng, steps, per_res):
     t = time.perf_counter()
     ora.load_flow_rules(rules)
     t_load = time.perf_counter() - t
+    log("[oracle] one-core replay of batch 0 ...")
     t = time.perf_counter()
     want = ora.submit(hb)
     dt = time.perf_counter() - t
+    log(f"[oracle] one-core replay of batch 0: {dt:.1f}s")
     ent = int(((hb.flags & abi.EV_EXIT) == 0).sum())
     ora.close()
     st, wt, ru = out0.status.numpy(), out0.wait_ms.numpy(), out0.rule_idx.numpy()
@@ -626,6 +631,7 @@ def oracle_leg(rules, hb, R, out0, out_last, eng, steps, per_res):
         t_all = time.perf_counter()
         for k in range(steps):
             v, dtk = sh.submit(hb, k * DURATION_MS)
+            log(f"[oracle] sharded replay of batch {k}: {dtk:.1f}s")
             if k == 0:
                 same = bool((v.status == want.status).all() and (v.wait_ms == want.wait_ms).all())
                 cpu = {"value": round(ent / dtk, 1), "unit": "decisions/s", "cores": T, "kind": "port",

@@ -568,6 +568,14 @@ int  sf_format_metric_rows(sf_engine* e, const sf_metric_row* rows, uint32_t n, 
 int  sf_comm_unique_id(uint8_t* out, size_t len /* >= 128 */);
 int  sf_comm_init(sf_engine* e, int nranks, int rank, const uint8_t* id, size_t len);
 int  sf_entry_node_allreduce(sf_engine* e, sf_node_state* out);
+/* The ENTRY_NODE whose "__total_inbound_traffic__" line sf_metric_log writes
+ * (MetricTimerListener.java:40-69 reads Constants.ENTRY_NODE, the node-wide
+ * node): NULL = this engine's own (its shard's inbound traffic, the default);
+ * else a copy of *node -- on the rank that writes the node's metrics.log, the
+ * node-wide merge sf_entry_node_allreduce returned, set before each fetch.
+ * Its windows are reported; lastFetchTime stays this engine's.  Decisions
+ * (SystemRule) never read it. */
+int  sf_set_report_entry_node(sf_engine* e, const sf_node_state* node);
 
 /* ---- DegradeSlot circuit breakers -----------------
  * Replaces DegradeSlot.performChecking / exit (DegradeSlot.java:50-94) and

@@ -159,6 +159,7 @@ def _declare(L):
       C.POINTER(U64))
     f("so_metric_log", C.c_int, P, C.POINTER(SoNames), I64, I64, C.c_int, C.c_char_p, U64, C.POINTER(U64),
       C.POINTER(U32))
+    f("so_set_report_entry_node", C.c_int, P, C.POINTER(abi.sf_node_state))
     f("so_load_namespaces", C.c_int, P, C.POINTER(abi.sf_namespace), U32)
     f("so_load_cluster_rules", C.c_int, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
@@ -595,6 +596,9 @@ class OracleEngine:
                                  C.byref(n), C.byref(k))
         assert rc == 0, rc
         return buf.raw[:n.value]
+
+    def set_report_entry_node(self, node=None):
+        lib().so_set_report_entry_node(self.h, None if node is None else C.byref(node))
 
     def load_namespaces(self, ns):
         lib().so_load_namespaces(self.h, abi.rules_array(abi.sf_namespace, ns), len(ns))

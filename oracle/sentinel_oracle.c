@@ -1081,6 +1081,8 @@ struct so_engine {
     int load_set, cpu_set;
     double cur_load, cur_cpu;
     so_node* entry_node;              /* Constants.ENTRY_NODE (Constants.java:66) */
+    int report_set;                   /* so_set_report_entry_node: the ENTRY_NODE the metric log reports */
+    sf_node_state report;
     /* entries of the batch being replayed */
     uint8_t* entry_blocked; uint32_t cap_entries;
     const uint8_t* forced;            /* so_submit_forced: planned SystemRule verdicts, ENTRY_NODE untouched */
@@ -1825,13 +1827,43 @@ static int cmp_ts(const void* a, const void* b) {
     if (x->ts != y->ts) return x->ts < y->ts ? -1 : 1;
     return x->pos < y->pos ? -1 : x->pos > y->pos;    /* list position: stable */
 }
+/* A node holding the given windows (restated state: each stored WindowWrap
+ * with its counters), for the reported ENTRY_NODE. */
+static so_node* node_from_state(const sf_node_state* st) {
+    so_node* n = so_node_new();
+    so_leap_array* m = n->minute->data;
+    for (int i = 0; i < SF_MINUTE_BUCKETS; i++) {
+        const sf_bucket* b = &st->minute[i];
+        if (b->window_start == SF_WS_ABSENT) continue;
+        so_wrap* w = new_wrap(m, b->window_start, b->window_start);
+        mbucket* v = w->value;
+        v->c[EV_PASS] = b->pass; v->c[EV_BLOCK] = b->block; v->c[EV_EXCEPTION] = b->exception;
+        v->c[EV_SUCCESS] = b->success; v->c[EV_RT] = b->rt; v->c[EV_OCCUPIED_PASS] = b->occupied_pass;
+        v->min_rt = b->min_rt;
+        m->array[i] = w;
+    }
+    n->cur_thread_num = st->cur_thread_num;
+    return n;
+}
+int so_set_report_entry_node(so_engine* e, const sf_node_state* node) {
+    e->report_set = node != NULL;
+    if (node) e->report = *node;
+    return SF_OK;
+}
 int so_metric_log(so_engine* e, const so_names* nt, int64_t now, int64_t tz_offset_ms, int include_entry_node,
                   char* out, uint64_t cap, uint64_t* len_out, uint32_t* n_lines) {
     uint32_t k = 0, cap_rows = 1024;
     sf_metric_row* rows = malloc(cap_rows * sizeof *rows);
     g_now = now;
+    /* MetricTimerListener reads Constants.ENTRY_NODE: on a sharded node the
+     * node-wide merge, when set (lastFetchTime stays this engine's) */
+    so_node* rep = NULL;
+    if (include_entry_node && e->report_set) {
+        rep = node_from_state(&e->report);
+        rep->last_fetch_time = e->entry_node->last_fetch_time;
+    }
     for (uint32_t l = 0; l <= e->n_res; l++) {
-        so_node* n = l < e->n_res ? e->res[l].node : (include_entry_node ? e->entry_node : NULL);
+        so_node* n = l < e->n_res ? e->res[l].node : (include_entry_node ? (rep ? rep : e->entry_node) : NULL);
         if (!n) continue;
         if (k + 64 > cap_rows) { cap_rows = 2 * (k + 64); rows = realloc(rows, cap_rows * sizeof *rows); }
         node_metrics(n, now, l < e->n_res ? l * e->cfg.shard_count + e->cfg.shard_index : SF_RES_ENTRY_NODE,
@@ -1842,6 +1874,7 @@ int so_metric_log(so_engine* e, const so_names* nt, int64_t now, int64_t tz_offs
     for (uint32_t i = 0; i < k; i++) { order[i].ts = rows[i].timestamp; order[i].pos = i; }
     qsort(order, k, sizeof *order, cmp_ts);
     for (uint32_t i = 0; i < k; i++) sorted[i] = rows[order[i].pos];
+    if (rep) { e->entry_node->last_fetch_time = rep->last_fetch_time; so_node_free(rep); }
     int rc = so_format_fat(nt, sorted, k, tz_offset_ms, out, cap, len_out);
     free(rows); free(order); free(sorted);
     *n_lines = k;

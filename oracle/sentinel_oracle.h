@@ -214,6 +214,7 @@ int  so_snapshot(so_engine* e, int64_t now, sf_metric_row* out, uint32_t cap, ui
 typedef struct so_names { const char* bytes; const uint64_t* offsets; const int32_t* types; uint32_t n; } so_names;
 int  so_format_fat(const so_names* nt, const sf_metric_row* rows, uint32_t n, int64_t tz_offset_ms, char* out,
                    uint64_t cap, uint64_t* len_out);
+int  so_set_report_entry_node(so_engine* e, const sf_node_state* node);
 int  so_metric_log(so_engine* e, const so_names* nt, int64_t now, int64_t tz_offset_ms, int include_entry_node,
                    char* out, uint64_t cap, uint64_t* len_out, uint32_t* n_lines);
 int  so_load_namespaces(so_engine* e, const sf_namespace* ns, uint32_t n);

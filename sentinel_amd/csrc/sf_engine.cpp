@@ -83,6 +83,10 @@ struct sf_engine {
     // ENTRY_NODE and the metric snapshot (sf_entry.hip)
     EntryNode* en = nullptr;
     EntryAcc* en_acc = nullptr;
+    // sf_set_report_entry_node: the ENTRY_NODE sf_metric_log writes (node-wide merge), host copy
+    bool report_set = false;
+    EntryNode report{};
+    EntryNode* en_report = nullptr;    // device staging of `report` for the metric kernels
     uint32_t* snap_counts = nullptr; uint32_t* snap_offsets = nullptr; uint32_t* snap_total = nullptr;
     sf_metric_row* snap_rows = nullptr; uint32_t snap_cap = 0;
     void* snap_scan = nullptr; size_t snap_scan_bytes = 0;
@@ -166,6 +170,7 @@ void sf_destroy(sf_engine* e) {
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     for (void* p : e->host_allocs) hipHostFree(p);
+    if (e->en_report) hipFree(e->en_report);
     void* tptrs[] = {(void*)e->ts.rules, e->ts.fstate, (void*)e->ts.idtab, (void*)e->ts.ns, e->ts.lim, e->ts.cptab,
                      (void*)e->ts.items, e->ts.rmulti, e->tok_stage, e->wire_arena, e->d_sum, e->en, e->en_acc, e->snap_counts, e->snap_offsets,
                      e->snap_total, e->snap_rows, e->snap_scan, e->st.last_fetch, e->st.last_ts, e->nm_bytes, e->nm_off,
@@ -910,6 +915,13 @@ int sf_entry_node_add(sf_engine* e, const sf_event_batch* in, const uint8_t* sta
     return SF_OK;
 }
 
+static Bucket from_abi_bucket(const sf_bucket& o, int64_t max_rt) {
+    Bucket d{};
+    if (o.window_start == SF_WS_ABSENT) { d = Bucket{WS_NONE, 0, 0, 0, 0, 0, 0, max_rt}; return d; }
+    d.ws = o.window_start; d.pass = o.pass; d.block = o.block; d.exc = o.exception; d.succ = o.success; d.rt = o.rt;
+    d.occ = o.occupied_pass; d.min_rt = o.min_rt;
+    return d;
+}
 static void to_abi_bucket(const Bucket& d, sf_bucket* o) {
     o->window_start = d.ws == WS_NONE ? SF_WS_ABSENT : d.ws;
     o->pass = d.pass; o->block = d.block; o->exception = d.exc; o->success = d.succ; o->rt = d.rt;
@@ -1123,11 +1135,20 @@ int sf_metric_log(sf_engine* e, int64_t now_ms, int64_t tz_offset_ms, int includ
     hipStream_t s = e->stream;
     const bool with_en = include_entry_node != 0;
     const uint32_t nodes = e->R + (with_en ? 1u : 0u);
+    // the ENTRY_NODE line: this engine's node, or the one set by sf_set_report_entry_node
+    // (its windows; lastFetchTime stays this engine's, MetricTimerListener.java:40-69)
+    EntryNode* en = e->en;
+    if (with_en && e->report_set) {
+        if (!e->en_report) HIP_TRY(hipMalloc((void**)&e->en_report, sizeof(EntryNode)));
+        HIP_TRY(hipMemcpyAsync(e->en_report, &e->report, sizeof(EntryNode), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(&e->en_report->last_fetch, &e->en->last_fetch, 8, hipMemcpyDeviceToDevice, s));
+        en = e->en_report;
+    }
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const unsigned grid = (unsigned)std::min<uint64_t>(((uint64_t)nodes + 3) / 4, (uint64_t)cus * 16);
     HIP_TRY(hipEventRecord(e->ml_ev[0], s));
-    HIP_TRY(launch_mlog_count(e->st, e->en, with_en, e->cfg.shard_count, e->cfg.shard_index, now_ms, e->ml_mask,
+    HIP_TRY(launch_mlog_count(e->st, en, with_en, e->cfg.shard_count, e->cfg.shard_index, now_ms, e->ml_mask,
                               e->ml_counts, e->ml_offsets, e->ml_total, e->ml_tmp, e->ml_tmp_bytes, grid, e->ml_ev[1], s));
     uint32_t rows = 0;
     HIP_TRY(hipMemcpyAsync(&rows, e->ml_total, 4, hipMemcpyDeviceToHost, s));
@@ -1135,10 +1156,11 @@ int sf_metric_log(sf_engine* e, int64_t now_ms, int64_t tz_offset_ms, int includ
     rc = ml_reserve(e, rows);
     if (rc) return rc;
     uint32_t* ord = e->ml_order;
-    HIP_TRY(launch_mlog_rows(e->st, e->en, with_en, e->cfg.shard_count, e->cfg.shard_index, now_ms, e->ml_mask,
+    HIP_TRY(launch_mlog_rows(e->st, en, with_en, e->cfg.shard_count, e->cfg.shard_index, now_ms, e->ml_mask,
                              e->ml_offsets, rows, e->ml_rows, e->ml_keys, e->ml_keys + e->ml_row_cap, ord,
                              ord + e->ml_row_cap, e->ml_tmp, e->ml_tmp_bytes, grid, s));
     if (n_lines) *n_lines = rows;
+    if (en != e->en) HIP_TRY(hipMemcpyAsync(&e->en->last_fetch, &en->last_fetch, 8, hipMemcpyDeviceToDevice, s));
     rc = ml_format(e, ord + e->ml_row_cap, rows, tz_offset_ms, out, cap, len_out);
     if (rc) return rc;
     float ms = 0.f;
@@ -1602,6 +1624,21 @@ int sf_comm_init(sf_engine* e, int nranks, int rank, const uint8_t* id, size_t l
     ncclResult_t r = ncclCommInitRank(&e->comm, nranks, uid, rank);
     if (r != ncclSuccess) { e->comm = nullptr; return fail(SF_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)); }
     if (!e->agg) HIP_TRY(hipMalloc((void**)&e->agg, 4096 * sizeof(int64_t)));
+    return SF_OK;
+}
+
+int sf_set_report_entry_node(sf_engine* e, const sf_node_state* node) {
+    if (!e) return fail(SF_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!node) { e->report_set = false; return SF_OK; }
+    EntryNode& r = e->report;
+    r = EntryNode{};
+    const int64_t mrt = e->cfg.statistic_max_rt;
+    for (int i = 0; i < SF_MAX_SAMPLE_COUNT; i++)
+        r.second[i] = i < e->cfg.sample_count ? from_abi_bucket(node->second[i], mrt) : Bucket{WS_NONE, 0, 0, 0, 0, 0, 0, mrt};
+    for (int i = 0; i < MINUTE; i++) r.minute[i] = from_abi_bucket(node->minute[i], mrt);
+    r.threads = node->cur_thread_num;
+    e->report_set = true;
     return SF_OK;
 }
 

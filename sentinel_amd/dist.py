@@ -121,3 +121,28 @@ def rccl_join(eng, group=None):
     box = [_engine.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(box, src=0, group=group)
     eng.comm_init(world, rank, box[0])
+
+
+ENTRY_NODE_NAME = b"__total_inbound_traffic__"
+
+
+def merge_metric_logs(parts):
+    """metrics.log of a resource-sharded node from every rank's sf_metric_log
+    bytes (rank 0's carries the node-wide ENTRY_NODE line, set with
+    sf_set_report_entry_node): lines grouped by second ascending as
+    MetricTimerListener's TreeMap does (MetricTimerListener.java:40-69), each
+    second's resource lines in rank order and the ENTRY_NODE line last."""
+    by_sec = {}
+    for part in parts:
+        for line in part.split(b"\n"):
+            if not line:
+                continue
+            f = line.split(b"|")
+            sec = int(f[0])
+            ent = by_sec.setdefault(sec, ([], []))
+            (ent[1] if f[2] == ENTRY_NODE_NAME else ent[0]).append(line)
+    out = []
+    for sec in sorted(by_sec):
+        res, en = by_sec[sec]
+        out += res + en
+    return b"".join(x + b"\n" for x in out)

@@ -73,6 +73,7 @@ def _declare(L):
     f("sf_comm_unique_id", I, C.c_char_p, C.c_size_t)
     f("sf_comm_init", I, P, I, I, C.c_char_p, C.c_size_t)
     f("sf_entry_node_allreduce", I, P, C.POINTER(abi.sf_node_state))
+    f("sf_set_report_entry_node", I, P, C.POINTER(abi.sf_node_state))
     f("sf_read_node", I, P, U32, C.POINTER(abi.sf_node_state))
     f("sf_read_entry_node", I, P, C.POINTER(abi.sf_node_state))
     f("sf_read_rule_state", I, P, U32, C.POINTER(abi.sf_rule_state))
@@ -400,6 +401,10 @@ class FlowEngine:
         st = abi.sf_node_state()
         _check(lib().sf_entry_node_allreduce(self.h, C.byref(st)))
         return st
+
+    def set_report_entry_node(self, node: abi.sf_node_state = None):
+        """The ENTRY_NODE metric_log reports (None: this engine's own)."""
+        _check(lib().sf_set_report_entry_node(self.h, None if node is None else C.byref(node)))
 
     def snapshot(self, now, cap=1 << 20):
         """StatisticNode.metrics() of every node (MetricTimerListener): MetricNode rows."""

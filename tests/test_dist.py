@@ -66,6 +66,74 @@ def test_entry_node_allreduce_two_ranks():
     assert rows == want_rows
 
 
+def _metric_worker(rank, world, port, q):
+    """Node-wide metrics.log: every rank's engine holds its shard; the
+    all-reduced ENTRY_NODE is set as the reported one on rank 0
+    (sf_set_report_entry_node), every rank writes its shard's lines, and the
+    merged log (lines per second, ENTRY_NODE last) equals one engine's log over
+    the whole batch."""
+    import torch.distributed as dist
+    from oracle import oracle as so
+    from sentinel_amd import dist as sd
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    R = 1200
+    rules = trace.mixed_rules(R, seed=37)
+    full = trace.mixed_zipf(R, 50_000, duration_ms=5000, seed=37)
+    sub = full.shard(world, rank)
+    cfg = abi.default_config(max_resources=(R + world - 1) // world, max_batch=max(sub.n, 1), shard_count=world,
+                             shard_index=rank)
+    o = so.OracleEngine(cfg)
+    o.load_flow_rules([r for r in rules if r.resource % world == rank])
+    o.submit(sub)
+    logs = []
+    t_end = int(full.ts_ms[-1])
+    for now in (t_end - 2500, t_end + 1500):           # two MetricTimerListener runs (lastFetchTime advances)
+        merged = sd.entry_node_allreduce(o.read_entry_node())
+        if rank == 0:
+            o.set_report_entry_node(merged)
+        part = o.metric_log(now, entry_node=(rank == 0))
+        parts = [None] * world
+        dist.all_gather_object(parts, part)
+        logs.append(sd.merge_metric_logs(parts))
+    if rank == 0:
+        ref = so.OracleEngine(abi.default_config(max_resources=R, max_batch=full.n))
+        ref.load_flow_rules(rules)
+        ref.submit(full)
+        want = [ref.metric_log(now, entry_node=True) for now in (t_end - 2500, t_end + 1500)]
+        q.put((logs, want))
+    dist.destroy_process_group()
+
+
+def _sec_groups(log):
+    g = {}
+    for line in log.split(b"\n"):
+        if line:
+            g.setdefault(int(line.split(b"|")[0]), []).append(line)
+    return g
+
+
+def test_node_wide_metric_log_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_metric_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    logs, want = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for got, ref in zip(logs, want):
+        assert got.count(b"\n") == ref.count(b"\n") > 0
+        gg, rr = _sec_groups(got), _sec_groups(ref)
+        assert sorted(gg) == sorted(rr)
+        for sec in rr:
+            # the ENTRY_NODE line (last in its second) is the node-wide one
+            assert gg[sec][-1] == rr[sec][-1] and b"__total_inbound_traffic__" in rr[sec][-1]
+            assert sorted(gg[sec]) == sorted(rr[sec])
+
+
 def _degrade_worker(rank, world, port, q):
     """DegradeSlot over resource shards: each rank replays its shard with the
     degrade oracle; rank 0 gathers the verdicts (gloo all_gather of the

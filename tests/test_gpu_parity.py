@@ -336,6 +336,46 @@ def test_metric_log_matches_oracle(eng_mod, so):
     parity.compare_nodes(e, o, w["nodes"])
 
 
+def test_node_wide_metric_log_two_shards(eng_mod, so):
+    """Two resource shards (two engines on cuda:0): every shard's ENTRY_NODE
+    merged on the host (sentinel_amd.dist.merge_entry_nodes, the merge the
+    RCCL all-reduce does), set as the reported ENTRY_NODE of shard 0
+    (sf_set_report_entry_node); the merged metrics.log of the two shards
+    (lines per second, ENTRY_NODE last, MetricTimerListener.java:40-69) equals
+    one oracle engine's over the whole batch."""
+    from sentinel_amd import dist as sd
+    R = 3000
+    rules = trace.mixed_rules(R, seed=33)
+    full = trace.mixed_zipf(R, 120_000, duration_ms=6000, seed=33)
+    engs = []
+    for k in range(2):
+        sub = full.shard(2, k)
+        e = eng_mod.FlowEngine(abi.default_config(max_resources=R // 2, max_batch=sub.n, shard_count=2, shard_index=k))
+        e.load_flow_rules([r for r in rules if r.resource % 2 == k])
+        e.submit(sub)
+        engs.append(e)
+    ref = so.OracleEngine(abi.default_config(max_resources=R, max_batch=full.n))
+    ref.load_flow_rules(rules)
+    ref.submit(full)
+    t_end = int(full.ts_ms[-1])
+    for now in (t_end - 2500, t_end + 1500):
+        merged = sd.merge_entry_nodes([e.read_entry_node() for e in engs])
+        engs[0].set_report_entry_node(merged)
+        parts = [engs[0].metric_log(now, entry_node=True), engs[1].metric_log(now, entry_node=False)]
+        got = sd.merge_metric_logs(parts)
+        want = ref.metric_log(now, entry_node=True)
+        g, w = {}, {}
+        for log, d in ((got, g), (want, w)):
+            for line in log.split(b"\n"):
+                if line:
+                    d.setdefault(int(line.split(b"|")[0]), []).append(line)
+        assert sorted(g) == sorted(w) and len(w) > 0
+        for sec in w:
+            assert g[sec][-1] == w[sec][-1] and b"__total_inbound_traffic__" in w[sec][-1]
+            assert sorted(g[sec]) == sorted(w[sec])
+        engs[0].set_report_entry_node(None)
+
+
 def test_format_metric_rows_kat(eng_mod, so):
     """MetricNodeTest.java:29-36 fat line, formatted by the GPU kernel, and
     the formatter on edge values against the oracle's."""
