@@ -61,10 +61,17 @@ def main():
     R_total = args.resources
     R_local = (R_total - rank + world - 1) // world
     t0 = time.time()
-    grade, beh, count = trace.mixed_rule_table(R_local, seed=3 + rank)
-    rules = abi.flow_rules_np(np.arange(R_local, dtype=np.uint32) * world + rank, grade, count, beh)
-    hb = trace.mixed_zipf(R_local, args.events, duration_ms=DURATION_MS, seed=3 + rank)
-    hb.res_id = (hb.res_id.astype(np.uint64) * world + rank).astype(np.uint32)
+    # rules of the whole node (config 3's table over the 10M resources), this
+    # rank's shard res % N == rank
+    grade_all, beh_all, count_all = trace.mixed_rule_table(R_total, seed=3)
+    mine = np.arange(rank, R_total, world, dtype=np.uint32)
+    grade, beh, count = grade_all[mine], beh_all[mine], count_all[mine]
+    rules = abi.flow_rules_np(mine, grade, count, beh)
+    del grade_all, beh_all, count_all
+    # the node-wide trace: N = 1 is config 3's batch; N > 1 superposes N
+    # config-3 traces over all 10M resources (component c = seed 3 + c, built
+    # by rank c) and hash-shards the result, rank r keeping res % N == r
+    hb = node_trace(R_total, args.events, world, rank, dist)
     n_entry = int(((hb.flags & abi.EV_EXIT) == 0).sum())
     n_exit = hb.n - n_entry
     log(f"[rank {rank}] trace {hb.n} events ({n_entry} entries) over {R_local} resources in {time.time()-t0:.1f}s")
@@ -119,6 +126,14 @@ def main():
         total_decisions = n_entry * args.steps
     wall = times[0]
     value = total_decisions / wall
+    per_rank = None
+    if dist:
+        box = [None] * world
+        dist.all_gather_object(box, (int(hb.n), n_entry, round(elapsed / args.steps * 1e3, 3)))
+        per_rank = {"events": [b[0] for b in box], "entries": [b[1] for b in box],
+                    "ms_per_step": [b[2] for b in box],
+                    "max_over_min_ms": round(max(b[2] for b in box) / max(1e-9, min(b[2] for b in box)), 3),
+                    "max_over_mean_events": round(max(b[0] for b in box) / (sum(b[0] for b in box) / world), 3)}
 
     # roofline of the dominant decision kernel: SURVEY.md §8(d) byte model,
     # B = 25 E + 4 E_wait + 12 E_exit + 528 R_touched, restricted to the
@@ -238,23 +253,6 @@ def main():
         except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
             degrade = {"error": str(ex)[:200]}
 
-    # the other BASELINE configs and the end-to-end form (rank 0, N=1 only;
-    # after the timed region, each on its own engine except e2e)
-    legs = {}
-    if rank == 0 and world == 1 and not args.no_legs:
-        for b in batches[1:]:
-            b.free()
-        batches = batches[:1]
-        for nm, fn in (("e2e_pinned", lambda: e2e_leg(eng, hb, steps * DURATION_MS)),
-                       ("config2", config2_leg), ("config4", config4_leg), ("config5", config5_leg)):
-            try:
-                t_leg = time.perf_counter()
-                log(f"[leg {nm}] ...")
-                legs[nm] = fn()
-                log(f"[leg {nm}] {time.perf_counter() - t_leg:.1f}s")
-            except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
-                legs[nm] = {"error": str(ex)[:300]}
-
     # whole-batch parity: batch 0 from a fresh engine vs the one-core oracle
     # replay of the same batch (that replay, timed, is the one-core CPU
     # baseline), then the steady state: the resource-sharded oracle replays
@@ -265,6 +263,24 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu and args.warmup > 0:
         cpu, parity = oracle_leg(rules, hb, R_local, out0, out, eng, steps, per_res)
 
+    # the other BASELINE configs and the end-to-end form (rank 0, N=1 only;
+    # after the timed region, each on its own engine except e2e)
+    legs = {}
+    if rank == 0 and world == 1 and not args.no_legs:
+        for b in batches[1:]:
+            b.free()
+        batches = batches[:1]
+        # (after the oracle leg: e2e advances this engine's state)
+        for nm, fn in (("e2e_pinned", lambda: e2e_leg(eng, hb, steps * DURATION_MS)),
+                       ("config2", config2_leg), ("config4", config4_leg), ("config5", config5_leg)):
+            try:
+                t_leg = time.perf_counter()
+                log(f"[leg {nm}] ...")
+                legs[nm] = fn()
+                log(f"[leg {nm}] {time.perf_counter() - t_leg:.1f}s")
+            except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
+                legs[nm] = {"error": str(ex)[:300]}
+
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 3),
@@ -274,7 +290,10 @@ def main():
                                        "15% RateLimiter, acquireCount 1 (90%) or 2-5, RT~Exp(20ms) exits",
                            "resources": R_total, "events_per_batch_per_gpu": hb.n, "entries_per_batch_per_gpu": n_entry,
                            "resources_touched": n_seg, "pass_fraction": round(n_pass / max(1, n_entry), 4),
-                           "parallelism": f"resource-sharded x{world}"},
+                           "parallelism": f"resource-sharded x{world}",
+                           "trace": "one node-wide trace: N config-3 batches of 2^27 events over all 10M resources "
+                                    "(seeds 3..3+N-1, the same 4 s) superposed, rank r deciding res % N == r"
+                                    if world > 1 else "config-3 batch, seed 3", "per_rank": per_rank},
                 "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "aggregate": aggregate,
                 "metric_log": metric_log, "degrade": degrade, **legs}
         print(json.dumps(line), flush=True)
@@ -283,6 +302,58 @@ def main():
     base.free()
     if dist:
         dist.destroy_process_group()
+
+
+def node_trace(R_total, n, world, rank, dist):
+    """This rank's shard of one node-wide trace.  Component c (built by rank
+    c) is a config-3 batch of n events over all R_total resources (seed 3 + c,
+    the same 4 s of trace time); the node's trace is the superposition of the
+    N components (N times the traffic of one), merged in time order (events of
+    one millisecond in component order), and hash-sharded: rank r keeps the
+    events of res % N == r, so the rank holding the Zipf head gets more events
+    than the others.  Exits stay with their entries (same resource).  The
+    components' parts travel between ranks by all_to_all over the host
+    process group."""
+    comp = trace.mixed_zipf(R_total, n, duration_ms=DURATION_MS, seed=3 + rank)
+    if world == 1:
+        return comp
+    import torch
+    dest = (comp.res_id % world).astype(np.uint8)
+    order = np.argsort(dest, kind="stable")
+    send = np.bincount(dest, minlength=world).astype(np.int64)
+    pos = np.empty(comp.n, np.int64)                       # index of each event inside its destination part
+    starts = np.concatenate([[0], np.cumsum(send)])
+    for d in range(world):
+        idx = order[starts[d]:starts[d + 1]]
+        pos[idx] = np.arange(idx.size)
+    eref = np.where(comp.entry_ref >= 0, pos[np.clip(comp.entry_ref, 0, None)], -1)
+    recv = torch.empty(world, dtype=torch.int64)
+    dist.all_to_all_single(recv, torch.from_numpy(send))
+    recv = recv.numpy()
+    ss, rs = [int(x) for x in send], [int(x) for x in recv]
+
+    def a2a(arr, dtype):
+        x = torch.from_numpy(np.ascontiguousarray(arr[order]).astype(dtype, copy=False))
+        y = torch.empty(sum(rs), dtype=x.dtype)
+        dist.all_to_all_single(y, x, output_split_sizes=rs, input_split_sizes=ss)
+        return y.numpy()
+
+    res = a2a(comp.res_id.astype(np.int32), np.int32).astype(np.uint32)
+    ts = a2a(comp.ts_ms, np.int64)
+    cnt = a2a(comp.count, np.int32)
+    fl = a2a(comp.flags.astype(np.int32), np.int32).astype(np.uint8)
+    er = a2a(eref, np.int64)
+    del comp, order, pos, eref
+    part0 = np.concatenate([[0], np.cumsum(recv)])[:-1]
+    part = np.repeat(np.arange(world), recv)
+    er = np.where(er >= 0, er + part0[part], -1)             # index into the concatenation
+    key = (ts - trace.T0).astype(np.uint16 if DURATION_MS < 65536 else np.uint32)
+    mo = np.argsort(key, kind="stable")                      # time order; a millisecond keeps component order
+    newpos = np.empty(mo.size, np.int64)
+    newpos[mo] = np.arange(mo.size)
+    er = er[mo]
+    er = np.where(er >= 0, newpos[np.clip(er, 0, None)], -1)
+    return abi.HostBatch(res[mo], ts[mo], cnt[mo], fl[mo], entry_ref=er)
 
 
 def config2_leg(R=1_000_000, n=1 << 27, steps=3):

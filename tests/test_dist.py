@@ -324,3 +324,49 @@ def test_flow_engine_hostsim_sharded_two_ranks():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert np.array_equal(got, want)
+
+
+def _node_trace_worker(rank, world, port, q):
+    import torch.distributed as dist
+    import bench
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    hb = bench.node_trace(5000, 200_000, world, rank, dist)
+    q.put((rank, hb.res_id, hb.ts_ms, hb.count, hb.flags, hb.entry_ref))
+    dist.destroy_process_group()
+
+
+def test_node_trace_two_ranks():
+    """bench.py's node-wide trace for N > 1: rank r holds exactly the events of
+    res % N == r of the superposed components (mixed_zipf seeds 3, 4), in
+    time order (a millisecond in component order), exits pointing at their
+    entries -- the same as building the node's trace on one host."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_node_trace_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((x[0], x[1:]) for x in (q.get(timeout=240), q.get(timeout=240)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    comps = [trace.mixed_zipf(5000, 200_000, duration_ms=4000, seed=3 + c) for c in range(2)]
+    for r in range(2):
+        res, ts, cnt, fl, er = got[r]
+        parts = []
+        for c, b in enumerate(comps):
+            sel = np.nonzero(b.res_id % 2 == r)[0]
+            parts.append((b.ts_ms[sel], np.full(sel.size, c), b.res_id[sel], b.count[sel], b.flags[sel]))
+        wts = np.concatenate([p[0] for p in parts])
+        wc = np.concatenate([p[1] for p in parts])
+        o = np.lexsort((wc, wts))
+        assert np.array_equal(ts, wts[o])
+        assert np.array_equal(res, np.concatenate([p[2] for p in parts])[o])
+        assert np.array_equal(cnt, np.concatenate([p[3] for p in parts])[o])
+        assert np.array_equal(fl, np.concatenate([p[4] for p in parts])[o])
+        assert np.all(res % 2 == r)
+        ex = np.nonzero(fl & abi.EV_EXIT)[0]
+        assert ex.size > 0 and np.all(er[ex] >= 0) and np.all(er[ex] < ex)
+        assert np.all(res[er[ex]] == res[ex]) and np.all((fl[er[ex]] & abi.EV_EXIT) == 0)
+    assert got[0][0].size + got[1][0].size == 400_000
