@@ -90,8 +90,9 @@ typedef struct sf_config {
     uint32_t max_flow_ids;        /* capacity of the flowId table              */
     uint32_t heavy_min_events;    /* resource segments longer than this use the
                                      window/skip algorithms (0 = engine default) */
-    uint32_t aux_capacity;        /* origin / context statistic nodes kept for
-                                     the rules that read them (0 = 4096)       */
+    uint32_t aux_capacity;        /* origin nodes (one per (resource, origin) of
+                                     the traffic) + context nodes of CHAIN rules
+                                     (0 = 65536)                               */
     uint32_t pad;
 } sf_config;
 

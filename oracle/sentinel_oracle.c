@@ -1480,17 +1480,19 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         int is_in = (fl & SF_EV_IN) != 0;
         uint32_t na = nargs_of(in, i);
         uint8_t status = SF_V_PASS; int64_t wait = 0; int rule_idx = 0;
-        /* Context: origin and name (ContextUtil.enter); the origin node and the
-         * DefaultNode of (context, resource) are kept when a rule can read them */
+        /* Context: origin and name (ContextUtil.enter).  ClusterBuilderSlot
+         * creates the origin node of every entry with an origin
+         * (ClusterBuilderSlot.java:107-110: clusterNode.getOrCreateOriginNode);
+         * the DefaultNode of (context, resource) is kept while a CHAIN rule of the
+         * resource names the context (DESIGN.md §2 divergences) */
         const uint32_t origin = in->origin ? in->origin[i] : SF_ORIGIN_NONE;
         const uint32_t ctx = in->context ? in->context[i] : 0u;
-        int want_on = 0, want_dn = 0;
+        int want_dn = 0;
         for (int k = 0; k < rr->n_flow; k++) {
             const sf_flow_rule* fr = &e->flow[rr->flow_rules[k]].rule;
-            if (fr->strategy == SF_STRATEGY_DIRECT && fr->limit_app != SF_APP_DEFAULT) want_on = 1;
             if (fr->strategy == SF_STRATEGY_CHAIN && fr->ref_resource == ctx) want_dn = 1;
         }
-        so_node* on = (want_on && origin != SF_ORIGIN_NONE) ? keyed_get(&rr->onodes, &rr->n_on, origin, 1) : NULL;
+        so_node* on = origin != SF_ORIGIN_NONE ? keyed_get(&rr->onodes, &rr->n_on, origin, 1) : NULL;
         so_node* dn = want_dn ? keyed_get(&rr->dnodes, &rr->n_dn, ctx, 1) : NULL;
 
         if (fl & SF_EV_EXIT) {

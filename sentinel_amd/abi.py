@@ -70,7 +70,7 @@ def default_config(**kw) -> sf_config:
                     statistic_max_rt=5000, max_resources=1024, max_batch=1 << 20,
                     param_capacity=1 << 16, shard_count=1, shard_index=0, device=0,
                     cluster_sample_count=10, cluster_interval_ms=1000, exceed_count=1.0,
-                    max_occupy_ratio=1.0, max_flow_ids=1024, heavy_min_events=0, aux_capacity=4096)
+                    max_occupy_ratio=1.0, max_flow_ids=1024, heavy_min_events=0, aux_capacity=65536)
     for k, v in kw.items():
         setattr(cfg, k, v)
     return cfg

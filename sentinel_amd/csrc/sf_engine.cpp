@@ -130,7 +130,7 @@ void sf_config_default(sf_config* c) {
     c->statistic_max_rt = 5000; c->max_resources = 1024; c->max_batch = 1u << 20;
     c->param_capacity = 1u << 16; c->shard_count = 1; c->shard_index = 0; c->device = 0;
     c->cluster_sample_count = 10; c->cluster_interval_ms = 1000; c->exceed_count = 1.0;
-    c->max_occupy_ratio = 1.0; c->max_flow_ids = 1024; c->aux_capacity = 4096;
+    c->max_occupy_ratio = 1.0; c->max_flow_ids = 1024; c->aux_capacity = 65536;
 }
 
 static int dalloc(void** p, size_t bytes) {
@@ -420,7 +420,7 @@ static int drain(sf_engine* e) {
 static int ensure_aux(sf_engine* e) {
     DevState& st = e->st;
     if (st.ax_second) return SF_OK;
-    const uint32_t cap = e->cfg.aux_capacity ? e->cfg.aux_capacity : 4096;
+    const uint32_t cap = e->cfg.aux_capacity ? e->cfg.aux_capacity : 65536;
     const size_t S = st.S;
     uint64_t tcap = 16;
     while (tcap < 2ull * cap) tcap <<= 1;
@@ -605,6 +605,14 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     DevBatch b{};
     b.n = n; b.arg_slots = in->arg_slots;
     hipStream_t s = e->stream, ss = e->serial ? e->stream : e->sstream;
+    if (in->origin && !e->st.ax_second) {
+        // the first batch with origins: the origin-node pool (every entry with an
+        // origin has one, ClusterBuilderSlot.java:107-110)
+        { const int rc = drain(e); if (rc) return rc; }
+        const int rc = ensure_aux(e);
+        if (rc) return rc;
+        HIP_TRY(hipStreamSynchronize(e->stream));
+    }
     // asynchronous only for HBM-resident batches and verdicts, without SystemRules
     async = async && in->mem != SF_MEM_HOST && out->mem != SF_MEM_HOST && !e->sys.check && !forced;
     if (!async) { const int rc = drain(e); if (rc) return rc; }

@@ -108,6 +108,18 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* keys, u
         const int sl = 63 - __builtin_clzll(heads & (below | (1ull << lane)));   // this segment's first lane
         if (ex && !(em & below & ~((1ull << sl) - 1ull))) atomicOr(&segflag[sid], SEGF_EXIT);
     }
+    if (b.origin) {
+        // an event with an origin updates its origin node (ClusterBuilderSlot.java:107-110):
+        // the segment goes to the xflow walk; one atomic per segment and wavefront
+        const bool og = b.origin[i] != SF_ORIGIN_NONE;
+        const int lane = (int)(threadIdx.x & 63);
+        const int psid = __shfl_up((int)sid, 1);
+        const unsigned long long heads = __ballot(lane == 0 || (uint32_t)psid != sid);
+        const unsigned long long om = __ballot(og);
+        const unsigned long long below = (1ull << lane) - 1ull;
+        const int sl = 63 - __builtin_clzll(heads & (below | (1ull << lane)));
+        if (og && !(om & below & ~((1ull << sl) - 1ull))) atomicOr(&segflag[sid], SEGF_ORIGIN);
+    }
     if (!(f & SF_EV_EXIT) && ((f & (SF_EV_PRIO | EVF_SYSBLK)) || c <= 0)) {
         atomicOr(&segflag[sid], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) |
                               ((f & EVF_SYSBLK) ? SEGF_SYS : 0u));
@@ -192,7 +204,7 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     uint32_t lo = 0, hi = 0, res = 0;
     if (valid) { lo = w.seg_start[s]; hi = w.seg_start[s + 1]; res = w.seg_res[s]; }
     // an xflow group (sf_xflow.h) is decided by k_decide_x only
-    const bool xs = valid && st.xmap && st.xmap[res] != XNONE;
+    const bool xs = valid && ((st.xmap && st.xmap[res] != XNONE) || (w.segflag[s] & SEGF_ORIGIN));
     if (xs) w.seg_mode[s] = SM_XFLOW;
     bool light = valid && !xs && hi - lo <= w.heavy_min;
     // a ParamFlow-only segment of more than 32 events is faster on the
@@ -1106,7 +1118,7 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
         hipLaunchKernelGGL(k_decide_short<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, ll, w.counters + 8);
     }
-    if (st.xmap) {
+    if (st.xmap || b.origin) {
         if (st.S <= 2)
             hipLaunchKernelGGL(k_decide_x<2>, dim3(blocks(max_seg, 64)), dim3(64), 0, s3, st, io, w.seg_start,
                                w.seg_mode, w.n_seg);

@@ -136,11 +136,13 @@ SF_HD void decide_xgroup(const DevState& st, const SegIO& io, uint32_t lo, uint3
         const uint8_t fl = io.flags[j];
         const uint32_t na = io.arg_slots ? (io.nargs ? io.nargs[j] : io.arg_slots) : 0;
         const uint32_t r0 = st.rule_off[l], r1 = st.rule_off[l + 1];
-        // the nodes StatisticSlot updates that a rule of this resource can read
-        bool want_on = false, want_dn = false;
+        // the origin node of every entry with an origin (ClusterBuilderSlot.java:107-110:
+        // getOrCreateOriginNode whatever the rules); a context DefaultNode while a CHAIN
+        // rule of the resource names the context (DESIGN.md §2 divergences)
+        const bool want_on = origin != SF_ORIGIN_NONE;
+        bool want_dn = false;
         for (uint32_t k = r0; k < r1; k++) {
             const DevRule& r = st.rules[k];
-            if (r.strategy == SF_STRATEGY_DIRECT && r.limit_app != SF_APP_DEFAULT) want_on = true;
             if (r.strategy == SF_STRATEGY_CHAIN && r.ref == ctx) want_dn = true;
         }
         if (l != cl) {
@@ -149,7 +151,7 @@ SF_HD void decide_xgroup(const DevState& st, const SegIO& io, uint32_t lo, uint3
             cl = l;
         }
         {
-            const uint32_t k = (want_on && origin != SF_ORIGIN_NONE) ? aux_get(st, l, AX_ORIGIN, origin) : XNONE;
+            const uint32_t k = want_on ? aux_get(st, l, AX_ORIGIN, origin) : XNONE;
             if (k != oi) {
                 if (oi != XNONE) nw_store(on, st, aux_rows(st, oi));
                 if (k != XNONE) nw_load(on, st, aux_rows(st, k));

@@ -91,6 +91,18 @@ static bool local_of(hs_engine* e, uint32_t res, uint32_t* l) {
     *l = res / e->cfg.shard_count; return *l < e->R;
 }
 
+// the origin / context node pool (lives as long as the engine)
+static void ensure_pool(hs_engine* e) {
+    if (!e->ax_threads.empty()) return;
+    const size_t cap = e->cfg.aux_capacity ? e->cfg.aux_capacity : 65536, S = e->cfg.sample_count;
+    size_t tcap = 16; while (tcap < 2 * cap) tcap <<= 1;
+    e->xtab.assign(tcap, ParamSlot{0, 0, 0, 0});
+    e->ax_second.assign(cap * S, fresh_bucket(WS_NONE, e->cfg.statistic_max_rt));
+    e->ax_borrow.assign(cap * S, Borrow{WS_NONE, 0});
+    e->ax_minute.assign(cap * MINUTE, fresh_bucket(WS_NONE, e->cfg.statistic_max_rt));
+    e->ax_threads.assign(cap, 0);
+}
+
 int hs_load_flow_rules(hs_engine* e, const sf_flow_rule* rules, uint32_t n) {
     std::vector<uint32_t> counts(e->R + 1, 0), loc, refl;
     std::vector<const sf_flow_rule*> valid;
@@ -118,15 +130,7 @@ int hs_load_flow_rules(hs_engine* e, const sf_flow_rule* rules, uint32_t n) {
     std::vector<uint32_t> xm;
     if (build_xmap(e->rules.data(), e->rule_off.data(), e->R, xm)) {
         e->xmap = xm;
-        if (e->ax_threads.empty()) {                 // the pool lives as long as the engine
-            const size_t cap = e->cfg.aux_capacity ? e->cfg.aux_capacity : 4096, S = e->cfg.sample_count;
-            size_t tcap = 16; while (tcap < 2 * cap) tcap <<= 1;
-            e->xtab.assign(tcap, ParamSlot{0, 0, 0, 0});
-            e->ax_second.assign(cap * S, fresh_bucket(WS_NONE, e->cfg.statistic_max_rt));
-            e->ax_borrow.assign(cap * S, Borrow{WS_NONE, 0});
-            e->ax_minute.assign(cap * MINUTE, fresh_bucket(WS_NONE, e->cfg.statistic_max_rt));
-            e->ax_threads.assign(cap, 0);
-        }
+        ensure_pool(e);
     } else {
         e->xmap.clear();
     }
@@ -186,6 +190,7 @@ int hs_read_breaker(hs_engine* e, uint32_t k, sf_breaker_state* out) {
 }
 
 int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
+    if (in->origin) { ensure_pool(e); e->refresh(); }        // origin nodes of every entry with an origin
     const uint32_t n = in->n;
     e->err = 0;
     std::vector<uint32_t> key(n), perm(n), inv(n);
@@ -240,6 +245,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     std::vector<uint32_t> seg_start, seg_res, segflag;
     for (uint32_t j = 0; j < n; j++) {
         if (j == 0 || key[perm[j]] != key[perm[j - 1]]) { seg_start.push_back(j); seg_res.push_back(key[perm[j]]); segflag.push_back(0); }
+        if (in->origin && in->origin[perm[j]] != SF_ORIGIN_NONE) segflag.back() |= SEGF_ORIGIN;
         if (!(fl[j] & SF_EV_EXIT) && ((fl[j] & (SF_EV_PRIO | EVF_SYSBLK)) || cnt[j] <= 0))
             segflag.back() |= ((fl[j] & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (cnt[j] <= 0 ? SEGF_NONPOS : 0u) |
                               ((fl[j] & EVF_SYSBLK) ? SEGF_SYS : 0u);
@@ -252,7 +258,7 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     std::vector<Acc> acc_hw, acc_sec;
     for (uint32_t s = 0; s < ns; s++) {
         uint32_t lo = seg_start[s], hi = seg_start[s + 1];
-        if (!e->xmap.empty() && e->xmap[seg_res[s]] != XNONE) { mode[s] = SM_XFLOW; continue; }
+        if ((!e->xmap.empty() && e->xmap[seg_res[s]] != XNONE) || (segflag[s] & SEGF_ORIGIN)) { mode[s] = SM_XFLOW; continue; }
         if (hi - lo <= e->heavy_min) { mode[s] = SM_LIGHT; continue; }
         e->n_heavy_segments++;
         mode[s] = heavy_mode(e->st, seg_res[s], segflag[s], ts[lo]);

@@ -87,6 +87,70 @@ def test_origin_rule_counts_per_origin():
         o.read_origin_node(0, abi.ORIGIN_NONE)
 
 
+def test_origin_node_exists_without_rules():
+    """ClusterBuilderSlot creates the origin node of every entry with an origin
+    (ClusterBuilderSlot.java:107-110), whatever the rules: an origin rule loaded
+    mid-stream sees the traffic before it (QPS), and the exits of entries made
+    before it keep the origin node's thread count exact (THREAD grade)."""
+    o = _oracle([])
+    o.submit(_entries([0] * 4, origin=[APP_A] * 4))                   # no rules: 4 passes on A's node
+    st = abi.node_state_to_dict(o.read_origin_node(0, APP_A))
+    assert sum(b[1] for b in st["second"]) == 4
+    o.load_flow_rules([_rule(count=5, limit_app=APP_A)])
+    v = o.submit(_entries([0] * 3, origin=[APP_A] * 3, ts=[trace.T0 + 1] * 3))
+    assert list(v.status) == [0, abi.V_BLOCK_FLOW, abi.V_BLOCK_FLOW]   # (int)passQps 4 + 1 <= 5, then 5 + 1 > 5
+
+
+def _threads_trace(seed, n=4000, R=3):
+    """Entries with origins and their exits; a THREAD-grade origin rule is
+    loaded after the first batch (mid-stream)."""
+    rng = np.random.default_rng(seed)
+    ts = trace.T0 + np.cumsum(rng.integers(0, 3, n))
+    res = rng.integers(0, R, n).astype(np.uint32)
+    org = rng.choice([APP_A, APP_B, abi.ORIGIN_NONE], n).astype(np.uint32)
+    ent = np.nonzero(rng.random(n) < 0.8)[0]
+    ex_ts = ts[ent] + rng.integers(0, 40, ent.size)
+    all_ts = np.concatenate([ts, ex_ts])
+    key = np.lexsort((np.concatenate([np.zeros(n), np.ones(ent.size)]), all_ts))
+    pos = np.empty(key.size, np.int64)
+    pos[key] = np.arange(key.size)
+    src = np.concatenate([np.arange(n), ent])
+    fl = np.concatenate([np.full(n, abi.EV_IN, np.uint8), np.full(ent.size, abi.EV_IN | abi.EV_EXIT, np.uint8)])
+    eref = np.full(key.size, -1, np.int64)
+    eref[pos[n:]] = pos[ent]
+    return abi.HostBatch(res[src][key], all_ts[key], np.ones(key.size, np.int32), fl[key], entry_ref=eref,
+                         origin=org[src][key])
+
+
+@pytest.mark.parametrize("seed", [61, 62])
+def test_hostsim_origin_rules_loaded_mid_stream(seed):
+    """The engine's xflow walk (host build) against the oracle when THREAD /
+    QPS origin rules are loaded after traffic with origins has flowed: every
+    verdict, every ClusterNode and origin node equal, no origin node with a
+    negative thread count."""
+    from tests.hostsim.hostsim import HostSimEngine
+    b = _threads_trace(seed)
+    cut = b.n // 2
+    batches = [b.subset(0, cut), b.subset(cut, b.n)]
+    cfg = abi.default_config(max_resources=3, max_batch=b.n)
+    rules = [_rule(0, count=3, grade=abi.GRADE_THREAD, limit_app=APP_A),
+             _rule(1, count=2, grade=abi.GRADE_THREAD, limit_app=abi.APP_OTHER),
+             _rule(2, count=4, limit_app=APP_B)]
+    h, o = HostSimEngine(cfg), OracleEngine(cfg)
+    from tests import parity
+    parity.compare_verdicts(h.submit(batches[0]), o.submit(batches[0]), "before the rules")
+    for x in (h, o):
+        x.load_flow_rules(rules)
+    v = o.submit(batches[1])
+    parity.compare_verdicts(h.submit(batches[1]), v, "after the rules")
+    assert (v.status == abi.V_BLOCK_FLOW).sum() > 0
+    parity.compare_nodes(h, o, range(3))
+    pairs = [(r, g) for r in range(3) for g in (APP_A, APP_B)]
+    parity.compare_aux_nodes(h, o, origin_nodes=pairs)
+    for r, g in pairs:
+        assert abi.node_state_to_dict(o.read_origin_node(r, g))["threads"] >= 0
+
+
 def test_relate_reads_the_referenced_cluster_node():
     o = _oracle([_rule(0, count=1, strategy=abi.STRATEGY_RELATE, ref_resource=1)])
     # resource 1 has no node yet -> pass; after two passes of 1, (int)passQps = 2 > 1 - 1 -> block
@@ -182,3 +246,30 @@ def test_gpu_xflow_pool_capacity():
         for b in w["batches"]:
             eng.submit(b)
     assert ex.value.code == abi.SF_ERR_CAPACITY
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [61, 62])
+def test_gpu_origin_rules_loaded_mid_stream(seed):
+    """The HIP xflow walk with origin nodes for every entry with an origin
+    (segments routed by the SEGF_ORIGIN flag) and origin rules loaded
+    mid-stream: verdicts, ClusterNodes and origin nodes equal the oracle's."""
+    from sentinel_amd.engine import FlowEngine
+    from tests import parity
+    b = _threads_trace(seed)
+    cut = b.n // 2
+    batches = [b.subset(0, cut), b.subset(cut, b.n)]
+    cfg = abi.default_config(max_resources=3, max_batch=b.n)
+    rules = [_rule(0, count=3, grade=abi.GRADE_THREAD, limit_app=APP_A),
+             _rule(1, count=2, grade=abi.GRADE_THREAD, limit_app=abi.APP_OTHER),
+             _rule(2, count=4, limit_app=APP_B)]
+    e, o = FlowEngine(cfg), OracleEngine(cfg)
+    try:
+        parity.compare_verdicts(e.submit(batches[0]), o.submit(batches[0]), "before the rules")
+        for x in (e, o):
+            x.load_flow_rules(rules)
+        parity.compare_verdicts(e.submit(batches[1]), o.submit(batches[1]), "after the rules")
+        parity.compare_nodes(e, o, range(3))
+        parity.compare_aux_nodes(e, o, origin_nodes=[(r, g) for r in range(3) for g in (APP_A, APP_B)])
+    finally:
+        e.close()

@@ -4,7 +4,7 @@ out=$1; shift
 for i in 1 2 3 4 5 6 7 8 9 10; do
   timeout 1500 /usr/local/graft/bin/gpurun "$@" > $out 2>&1
   rc=$?
-  if grep -q "status=transient\|GPU slot(s) on this pod are busy\|backing off" $out && ! grep -q "status=ok\|status=fail" $out; then
+  if grep -q "status=transient\|GPU slot(s) on this pod are busy\|backing off\|taken away" $out && ! grep -q "status=ok\|status=fail" $out; then
     sleep 120; continue
   fi
   exit $rc
