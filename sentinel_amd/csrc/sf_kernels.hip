@@ -1046,8 +1046,11 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     HeavyCtx hc = heavy_ctx(w);
     StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, nullptr, w.counters + 7};
     hipLaunchKernelGGL(k_fill_tiles, dim3(2), dim3(1024), 0, s, hc, sc, w.fill_tiles, w.fill_tile_cap, w.fill_ntiles);
-    hipLaunchKernelGGL(k_thr_prep, dim3(1024), dim3(256), 0, s, w.s_flags, w.s_cnt, b.eref ? w.s_eref : nullptr, hc,
-                       w.fill_tiles + w.fill_tile_cap, w.fill_ntiles);
+    // (grids sized to the most tiles a batch of n events can have: small
+    // SystemRule sub-batches do not pay for full-chip launches)
+    const uint32_t tile_ub = n / FILL_TILE + n / (w.heavy_min + 1) + 2;
+    hipLaunchKernelGGL(k_thr_prep, dim3(std::min<uint32_t>(1024u, tile_ub)), dim3(256), 0, s, w.s_flags, w.s_cnt,
+                       b.eref ? w.s_eref : nullptr, hc, w.fill_tiles + w.fill_tile_cap, w.fill_ntiles);
     if (timing) hipEventRecord(ev[2], s);
     return hipGetLastError();
 }
@@ -1089,10 +1092,11 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
         hipLaunchKernelGGL(k_heavy_decide<SF_MAX_SAMPLE_COUNT>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     if (timing) hipEventRecord(ev[7], s2);
     // verdicts + window deltas of each heavy class as soon as its decisions are done
-    hipLaunchKernelGGL(k_heavy_fill, dim3(w.fill_grid), dim3(256), 0, s2, st, io, hc, w.fill_tiles, w.fill_ntiles, 0);
+    const uint32_t fgrid = std::min<uint32_t>(w.fill_grid, n / FILL_TILE + max_heavy + 1);   // tiles of this batch at most
+    hipLaunchKernelGGL(k_heavy_fill, dim3(fgrid), dim3(256), 0, s2, st, io, hc, w.fill_tiles, w.fill_ntiles, 0);
     if (timing) hipEventRecord(ev[8], s2);
     hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, sc, w.seg_nhw, w.seg_nsec, 0);
-    hipLaunchKernelGGL(k_heavy_fill, dim3(w.fill_grid), dim3(256), 0, s, st, io, hc,
+    hipLaunchKernelGGL(k_heavy_fill, dim3(fgrid), dim3(256), 0, s, st, io, hc,
                        w.fill_tiles + w.fill_tile_cap, w.fill_ntiles, 1);
     hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s, st, hc, sc, w.seg_nhw, w.seg_nsec, 1);
 
