@@ -55,7 +55,14 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)              # gloo prints its connection banner on stdout: keep stdout to the one JSON line
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     assert world == args.gpus or world == 1, "launch N>1 with torch.distributed.run"
 
     R_total = args.resources
@@ -209,6 +216,18 @@ def main():
                                "k_heavy_fill": round(st.heavy_fill_ms / k, 3),
                                "scatter": round(st.scatter_ms / k, 3)}}
 
+    # (first after the timed region: the metrics.log leg below rolls every
+    # node's current minute bucket, as StatisticNode.metrics() does)
+    # whole-batch parity: batch 0 from a fresh engine vs the one-core oracle
+    # replay of the same batch (that replay, timed, is the one-core CPU
+    # baseline), then the steady state: the resource-sharded oracle replays
+    # every batch of the run (warmup + timed, the first one timed as the
+    # multi-core CPU baseline) and the last timed batch's verdicts, a sample of
+    # nodes, their controller state and ENTRY_NODE are compared with the GPU's
+    cpu, parity = None, None
+    if rank == 0 and world == 1 and not args.no_cpu and args.warmup > 0:
+        cpu, parity = oracle_leg(rules, hb, R_local, out0, out, eng, steps, per_res)
+
     # node-wide ENTRY_NODE over the shards: RCCL all-reduce (off the decision
     # path, after the timed region)
     aggregate = None
@@ -252,16 +271,6 @@ def main():
             degrade = degrade_leg()
         except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
             degrade = {"error": str(ex)[:200]}
-
-    # whole-batch parity: batch 0 from a fresh engine vs the one-core oracle
-    # replay of the same batch (that replay, timed, is the one-core CPU
-    # baseline), then the steady state: the resource-sharded oracle replays
-    # every batch of the run (warmup + timed, the first one timed as the
-    # multi-core CPU baseline) and the last timed batch's verdicts, a sample of
-    # nodes, their controller state and ENTRY_NODE are compared with the GPU's
-    cpu, parity = None, None
-    if rank == 0 and world == 1 and not args.no_cpu and args.warmup > 0:
-        cpu, parity = oracle_leg(rules, hb, R_local, out0, out, eng, steps, per_res)
 
     # the other BASELINE configs and the end-to-end form (rank 0, N=1 only;
     # after the timed region, each on its own engine except e2e)
