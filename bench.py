@@ -365,7 +365,7 @@ def node_trace(R_total, n, world, rank, dist):
     return abi.HostBatch(res[mo], ts[mo], cnt[mo], fl[mo], entry_ref=er)
 
 
-def config2_leg(R=1_000_000, n=1 << 27, steps=3):
+def config2_leg(R=1_000_000, n=1 << 27, steps=3, parity=1):
     """BASELINE config 2 (its own engine): 1M resources, one QPS
     DefaultController rule each (count U{5..50}), a uniform trace of 2^27
     events per 4 s, HBM-resident batches decided back to back (async), and the
@@ -401,6 +401,8 @@ def config2_leg(R=1_000_000, n=1 << 27, steps=3):
                             "frac": round(b_alg / wall / 1e9 / HBM_PEAK_GBS, 5)},
                "pass_fraction": round(float(np.isin(out.status.numpy(), abi.PASSED).mean()), 4)}
         try:
+            if not parity:
+                raise RuntimeError("parity leg skipped (parity=0)")
             from oracle import sharded
             g = out0.status.numpy()
             v, dt = sharded.replay(rules, hb, R, 16)

@@ -106,6 +106,7 @@ struct NodeWin {
     // minute window: row in HBM + one cached bucket
     Bucket* gmin;
     Bucket mb; int32_t mi; int32_t mdirty;
+    int64_t m_ws = INT64_MIN;                  // window start of mb's slot for the last time looked up
     int32_t S, wl, interval;
     int64_t max_rt;
     double interval_sec;
@@ -239,10 +240,15 @@ struct NodeWin {
     }
     // currentWindow(t): true when the cached bucket is the live one, false
     // for a throwaway window (older than the slot's bucket)
+    // (the slot and window start of the last second looked up are cached:
+    // events come in time order, so most lookups skip the 64-bit division)
     SF_HD bool min_current(int64_t t) {
-        int idx = (int)((t / 1000) % MINUTE);
-        int64_t ws = t - t % 1000;
-        if (idx != mi) { min_flush(); mb = gmin[idx]; mi = idx; }
+        if (!(t >= m_ws && t < m_ws + 1000)) {
+            const int idx = (int)((t / 1000) % MINUTE);
+            m_ws = t - t % 1000;
+            if (idx != mi) { min_flush(); mb = gmin[idx]; mi = idx; }
+        }
+        const int64_t ws = m_ws;
         if (mb.ws == ws) return true;
         if (ws > mb.ws) { mb = fresh_bucket(ws, max_rt); mdirty = 1; return true; }
         return false;
@@ -548,14 +554,15 @@ struct SegIO {          // sorted-order batch arrays
 };
 
 // final verdict of sorted event j, straight into the caller's arrays
+// (the status itself stays in sorted order, v_status: launch_scatter moves all
+// of them to submission order in bucketed passes after the decide phase)
 SF_HD void emit_verdict(const SegIO& io, uint32_t j, uint8_t status, int32_t wait, uint16_t rule) {
-    if (!io.perm) return;
+    (void)status;
+    const bool w = io.o_wait && wait, r = io.o_rule && rule;
+    if (!io.perm || !(w || r)) return;
     const uint32_t i = io.perm[j];
-#ifndef SF_EXP_NOSCATTER
-    io.o_status[i] = status;
-#endif
-    if (io.o_wait && wait) io.o_wait[i] = wait;          // (cleared before the decide phase)
-    if (io.o_rule && rule) io.o_rule[i] = rule;
+    if (w) io.o_wait[i] = wait;                          // (cleared before the decide phase)
+    if (r) io.o_rule[i] = rule;
 }
 
 // ParamFlowChecker.passLocalCheck (:84-112): one value, or every element of a
@@ -798,10 +805,46 @@ SF_HD void decide_qps_segment(const DevState& st, const SegIO& io, uint32_t res,
     nd.mi = -1; nd.mdirty = 0;
     nd.mb = fresh_bucket(WS_NONE, st.max_rt);
     const double count = st.rules[st.rule_off[res]].count;
+    // events read QC at a time with every load in flight together (time,
+    // acquireCount and flags), picked out of registers by
+    // unrolled selects: a lane walking a long segment then waits for memory
+    // once per chunk instead of once per event
+#ifndef SF_QPS_CH
+#define SF_QPS_CH 8
+#endif
+    constexpr uint32_t QC = SF_QPS_CH;
+    static_assert(QC % 4 == 0, "flags are packed four to a register");
+    // times as 32-bit offsets from the chunk's first (a chunk spanning 2^31 ms
+    // or more falls back to per-event loads), flags four to a register
+    int64_t t0_ = 0; uint32_t td_[QC]; int32_t c_[QC]; uint32_t f4_[QC / 4];
+    bool wide_ = false;
     for (uint32_t j = lo; j < hi; j++) {
-        const int64_t now = io.ts[j];
-        const int32_t c = io.cnt[j];
-        const uint8_t fl = io.flags[j];
+        const uint32_t k_ = (j - lo) % QC;
+        if (k_ == 0) {
+            int64_t tt[QC]; uint8_t ff[QC];
+#pragma unroll
+            for (uint32_t q = 0; q < QC; q++) {
+                const uint32_t jj = j + q < hi ? j + q : hi - 1;
+                tt[q] = io.ts[jj]; c_[q] = io.cnt[jj]; ff[q] = io.flags[jj];
+            }
+            t0_ = tt[0];
+            wide_ = tt[QC - 1] - t0_ >= (int64_t)0x7fffffff;
+#pragma unroll
+            for (uint32_t q = 0; q < QC; q++) td_[q] = (uint32_t)(tt[q] - t0_);
+#pragma unroll
+            for (uint32_t q = 0; q < QC / 4; q++)
+                f4_[q] = (uint32_t)ff[4 * q] | ((uint32_t)ff[4 * q + 1] << 8) | ((uint32_t)ff[4 * q + 2] << 16) |
+                         ((uint32_t)ff[4 * q + 3] << 24);
+        }
+        uint32_t td = td_[0]; int32_t c = c_[0]; uint32_t fw = f4_[0];
+#pragma unroll
+        for (uint32_t q = 1; q < QC; q++)
+            if (k_ == q) { td = td_[q]; c = c_[q]; }
+#pragma unroll
+        for (uint32_t q = 1; q < QC / 4; q++)
+            if (k_ / 4 == q) fw = f4_[q];
+        const uint8_t fl = (uint8_t)(fw >> (8 * (k_ % 4)));
+        const int64_t now = wide_ ? io.ts[j] : t0_ + (int64_t)td;
         uint8_t status;
         if (fl & SF_EV_EXIT) {                                  // StatisticSlot.exit :134-165
             int64_t ref = io.eref ? io.eref[j] : -1;
@@ -829,8 +872,7 @@ SF_HD void decide_qps_segment(const DevState& st, const SegIO& io, uint32_t res,
                 nd.threads++; nd.add_pass(now, c); status = SF_V_PASS;
             }
         }
-        io.v_status[j] = status;
-        emit_verdict(io, j, status, 0, 0);
+        io.v_status[j] = status;                            // (waits and rule indices are 0 here)
     }
     for (int i = 0; i < MAXS; i++)
         if (i < st.S) {

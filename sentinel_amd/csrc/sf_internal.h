@@ -204,7 +204,12 @@ struct Work {
     uint32_t* exit_of;                                  // [n] sorted index of each entry's exit, ~0 if none
     unsigned long long* lxfar;                          // [n/64+2] far live exits (SM_THREAD)
     uint2* thr_rec;                                     // [n] THREAD-segment event records (k_thr_prep, sf_stream.h)
+    uint32_t* vs_cursor;                                // [VS_CURSORS(N)] fill counts of the verdict scatter's buckets
 };
+// verdict scatter (sorted order -> submission order, launch_scatter): regions of
+// 2^VS_REG verdicts are assembled in LDS; its first pass has at most 256 buckets
+constexpr uint32_t VS_REG = 14;
+inline size_t VS_CURSORS(size_t N) { return 256 + (N >> VS_REG) + 1024 + 16; }
 
 // Device view of a caller batch (pointers already on device).
 // A sub-batch (SystemRule planner, sf_system.h) is a view of events

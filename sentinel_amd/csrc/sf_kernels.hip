@@ -850,22 +850,26 @@ __global__ void __launch_bounds__(256, SF_FILL_MINB) k_heavy_fill(DevState st, S
             vs[k] = e.status; vw[k] = e.wait;
             if (e.touch) gp.add(e);
         }
-        // verdicts straight to the caller's arrays (submission order)
-        uint32_t pm[FG];
-        if (full) load16(pm, io.perm + base, FG * 4);
+        // statuses in sorted order (launch_scatter moves them); the few nonzero
+        // waits and rule indices straight to the caller's arrays
+        if (full) store16(io.v_status + base, vs, FG);     // (aligned like the flags loaded above)
         else {
 #pragma unroll
-            for (int k = 0; k < FG; k++) pm[k] = (base + (uint32_t)k >= a && base + (uint32_t)k < b) ? io.perm[base + k] : 0u;
+            for (int k = 0; k < FG; k++)
+                if (base + (uint32_t)k >= a && base + (uint32_t)k < b) io.v_status[base + k] = vs[k];
         }
+        bool sparse = false;
 #pragma unroll
-        for (int k = 0; k < FG; k++) {
-            const uint32_t j = base + (uint32_t)k;
-            if (j < a || j >= b) continue;
-#ifndef SF_EXP_NOSCATTER
-            io.o_status[pm[k]] = vs[k];
-#endif
-            if (io.o_wait && vw[k]) io.o_wait[pm[k]] = vw[k];       // (cleared before the decide phase)
-            if (io.o_rule && vr[k]) io.o_rule[pm[k]] = vr[k];
+        for (int k = 0; k < FG; k++) sparse |= (io.o_wait && vw[k]) || (io.o_rule && vr[k]);
+        if (sparse) {
+#pragma unroll
+            for (int k = 0; k < FG; k++) {
+                const uint32_t j = base + (uint32_t)k;
+                if (j < a || j >= b || !((io.o_wait && vw[k]) || (io.o_rule && vr[k]))) continue;
+                const uint32_t pi = io.perm[j];
+                if (io.o_wait && vw[k]) io.o_wait[pi] = vw[k];       // (cleared before the decide phase)
+                if (io.o_rule && vr[k]) io.o_rule[pi] = vr[k];
+            }
         }
 #ifdef SF_EXP_NOACC
         continue;
@@ -1055,6 +1059,159 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     return hipGetLastError();
 }
 
+// ============================================================ verdict scatter
+// Every deciding kernel leaves its statuses in sorted order (v_status); the
+// caller's array is in submission order, a permutation away (perm).  One byte
+// stored per event at a random address costs a partial-line write each (the
+// lean QPS walk of config 2 spent half its time on them), so the statuses
+// travel instead in bucketed passes whose every global store is part of a
+// run: A buckets by submission index >> s1 (<= 256 buckets of 2^s1), B by
+// index >> VS_REG inside an A bucket, C assembles each 2^VS_REG region in LDS
+// and stores it with coalesced writes.  A record is (status << 24) | (the
+// index bits below its bucket).  A permutation fills every bucket exactly, so
+// bucket sizes are known and no histogram pass is needed: each workgroup
+// counting-sorts its tile in LDS, claims a run per bucket with one global
+// atomic, and writes the run.
+constexpr uint32_t VS_T = 256, VS_PER = 32, VS_TILE = VS_T * VS_PER;
+constexpr uint32_t VS_DIRECT_MAX = 1u << 20;        // smaller batches: one direct scatter
+
+// A (FIRST: sorted positions [blockIdx * VS_TILE, +VS_TILE) -> bucket idx >> s1)
+// or B (records of A bucket blockIdx / tpb, tile blockIdx % tpb -> region idx >> VS_REG)
+template <bool FIRST>
+__global__ void __launch_bounds__(VS_T) k_vs_bucket(const uint32_t* perm, const uint8_t* v_status, const uint32_t* in,
+                                                     uint32_t* out, uint32_t* cursor, uint32_t n, uint32_t s1,
+                                                     uint32_t tpb, int32_t* err) {
+    __shared__ uint32_t hist[1024], lbase[1024], gbase[1024], part[VS_T];
+    __shared__ uint32_t buf[VS_TILE];
+    __shared__ uint16_t kb[VS_TILE];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t m1 = s1 >= 32 ? 0xffffffffu : (1u << s1) - 1u;
+    uint32_t lo, hi, nk, bb = 0;
+    if (FIRST) {
+        lo = blockIdx.x * VS_TILE;
+        hi = min(n, lo + VS_TILE);
+        nk = (uint32_t)(((uint64_t)n + m1) >> s1);
+    } else {
+        bb = blockIdx.x / tpb;
+        const uint64_t b0 = (uint64_t)bb << s1;
+        const uint64_t bend = min((uint64_t)n, b0 + (1ull << s1));
+        const uint64_t l = b0 + (uint64_t)(blockIdx.x % tpb) * VS_TILE;
+        if (l >= bend) return;                           // (whole workgroup)
+        lo = (uint32_t)l; hi = (uint32_t)min(bend, l + VS_TILE);
+        nk = 1u << (s1 - VS_REG);
+    }
+    for (uint32_t k = tid; k < nk; k += VS_T) hist[k] = 0;
+    __syncthreads();
+    uint32_t rec[VS_PER], kr[VS_PER];                    // record, key << 16 | rank in the tile's bucket
+#pragma unroll
+    for (uint32_t r = 0; r < VS_PER; r++) {
+        const uint32_t e = lo + r * VS_T + tid;
+        kr[r] = 0xffffffffu;
+        if (e < hi) {
+            uint32_t key;
+            if (FIRST) {
+                const uint32_t i = perm[e];
+                key = i >> s1; rec[r] = ((uint32_t)v_status[e] << 24) | (i & m1);
+            } else {
+                const uint32_t v = in[e];
+                key = (v & m1) >> VS_REG; rec[r] = (v & 0xff000000u) | (v & ((1u << VS_REG) - 1u));
+            }
+            kr[r] = (key << 16) | atomicAdd(&hist[key], 1u);
+        }
+    }
+    __syncthreads();
+    // exclusive scan of the bucket counts (<= 4 per thread), then one claim per bucket
+    const uint32_t per = (nk + VS_T - 1) / VS_T;
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < per; q++) { const uint32_t k = tid * per + q; if (k < nk) sum += hist[k]; }
+    part[tid] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < VS_T; d <<= 1) {
+        const uint32_t v = tid >= d ? part[tid - d] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[tid] - sum;
+    for (uint32_t q = 0; q < per; q++) {
+        const uint32_t k = tid * per + q;
+        if (k >= nk) break;
+        const uint32_t h = hist[k];
+        lbase[k] = run; run += h;
+        if (h) {
+            const uint32_t c = FIRST ? k : 256u + bb * nk + k;
+            const uint32_t g = atomicAdd(&cursor[c], h);
+            // bucket capacity: what the permutation puts there (anything more is a broken permutation)
+            const uint64_t first = FIRST ? ((uint64_t)k << s1) : (((uint64_t)bb * nk + k) << VS_REG);
+            const uint64_t cap = min((uint64_t)(FIRST ? (1ull << s1) : (1ull << VS_REG)), (uint64_t)n - min((uint64_t)n, first));
+            if ((uint64_t)g + h > cap) *err = SF_ERR_INVALID;
+            gbase[k] = g;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < VS_PER; r++)
+        if (kr[r] != 0xffffffffu) {
+            const uint32_t key = kr[r] >> 16, p = lbase[key] + (kr[r] & 0xffffu);
+            buf[p] = rec[r]; kb[p] = (uint16_t)key;
+        }
+    __syncthreads();
+    for (uint32_t k = tid; k < hi - lo; k += VS_T) {
+        const uint32_t key = kb[k];
+        const uint64_t first = FIRST ? ((uint64_t)key << s1) : (((uint64_t)bb * nk + key) << VS_REG);
+        const uint64_t dst = first + gbase[key] + (k - lbase[key]);
+        if (dst < n) out[dst] = buf[k];
+    }
+}
+
+// C: region blockIdx (2^VS_REG submission indices) assembled in LDS, stored coalesced
+__global__ void __launch_bounds__(VS_T) k_vs_region(const uint32_t* in, uint8_t* o_status, uint32_t n) {
+    __shared__ __align__(16) uint8_t reg[1u << VS_REG];
+    const uint32_t base = blockIdx.x << VS_REG;
+    const uint32_t cnt = min(1u << VS_REG, n - base);
+    for (uint32_t k = threadIdx.x; k < cnt; k += VS_T) {
+        const uint32_t v = in[base + k];
+        reg[v & ((1u << VS_REG) - 1u)] = (uint8_t)(v >> 24);
+    }
+    __syncthreads();
+    uint8_t* o = o_status + base;
+    if (((uintptr_t)o & 15) == 0) {
+        for (uint32_t k = threadIdx.x; k < cnt / 16; k += VS_T) ((uint4*)o)[k] = ((const uint4*)reg)[k];
+        for (uint32_t k = (cnt & ~15u) + threadIdx.x; k < cnt; k += VS_T) o[k] = reg[k];
+    } else {
+        for (uint32_t k = threadIdx.x; k < cnt; k += VS_T) o[k] = reg[k];
+    }
+}
+
+__global__ void k_vs_direct(const uint32_t* perm, const uint8_t* v_status, uint8_t* o_status, uint32_t n) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) o_status[perm[j]] = v_status[j];
+}
+
+// statuses of a decided batch: sorted order -> the caller's array (submission order)
+static void launch_scatter(Work& w, uint32_t n, uint8_t* o_status, hipStream_t s) {
+    if (n <= VS_DIRECT_MAX) {
+        hipLaunchKernelGGL(k_vs_direct, dim3(blocks(n, 256)), dim3(256), 0, s, w.perm, w.v_status, o_status, n);
+        return;
+    }
+    const uint32_t lg = 32u - (uint32_t)__builtin_clz(n - 1u);          // ceil(log2 n)
+    const uint32_t s1 = std::max(VS_REG, lg - 8u);                      // <= 256 A buckets
+    const uint32_t nb1 = (uint32_t)(((uint64_t)n + (1ull << s1) - 1) >> s1);
+    const uint32_t nk = 1u << (s1 - VS_REG);
+    hipMemsetAsync(w.vs_cursor, 0, (256 + (size_t)nb1 * nk) * 4, s);
+    // staging: the sort's key buffers (dead once the batch is unpacked)
+    hipLaunchKernelGGL(k_vs_bucket<true>, dim3((n + VS_TILE - 1) / VS_TILE), dim3(VS_T), 0, s, w.perm, w.v_status,
+                       nullptr, w.keys_in, w.vs_cursor, n, s1, 0u, w.err);
+    const uint32_t* regions = w.keys_in;
+    if (s1 > VS_REG) {
+        const uint32_t tpb = (1u << s1) / VS_TILE;
+        hipLaunchKernelGGL(k_vs_bucket<false>, dim3(nb1 * tpb), dim3(VS_T), 0, s, nullptr, nullptr, w.keys_in,
+                           w.keys_out, w.vs_cursor, n, s1, tpb, w.err);
+        regions = w.keys_out;
+    }
+    hipLaunchKernelGGL(k_vs_region, dim3((n + (1u << VS_REG) - 1) >> VS_REG), dim3(VS_T), 0, s, regions, o_status, n);
+}
+
 // Decide phase (stateful, batch order): the serial chains (k_heavy_stream)
 // start first, on A; QPS/WarmUp heavy segments on B, the light lanes on C;
 // then the verdicts are scattered back to submission order.
@@ -1135,8 +1292,9 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     hipStreamWaitEvent(s, ev[6], 0);
     hipStreamWaitEvent(s, ev[9], 0);
     hipEventRecord(ev[13], s);
-    // every kernel wrote its verdicts straight into submission order (no scatter pass)
-    if (timing) { hipEventRecord(ev[3], s); hipEventRecord(ev[4], s); }
+    if (timing) hipEventRecord(ev[3], s);
+    launch_scatter(w, n, out.status, s);
+    if (timing) hipEventRecord(ev[4], s);
     return hipGetLastError();
 }
 

@@ -391,3 +391,13 @@ def test_format_metric_rows_kat(eng_mod, so):
     got = e.format_metric_rows(rows, tz_offset_ms=-5 * 3600 * 1000)
     want = so.format_fat(rows, names=["/foo/*", "a|b"], types=[1, 2], tz_offset_ms=-5 * 3600 * 1000)
     assert got == want
+
+
+@pytest.mark.parametrize("n", [1_500_007, 5_000_011])
+def test_bucketed_verdict_scatter(eng_mod, so, n):
+    """Batches above the direct-scatter size (2^20): the statuses go from
+    sorted order to submission order in bucketed passes (A + C at 1.5M
+    events, A + B + C above 2^22); every verdict, wait and rule index equals
+    the oracle's, and so do the nodes."""
+    w = workloads.config3(R=100_000, n=n, seed=41, split=1)
+    workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)

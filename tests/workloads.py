@@ -315,12 +315,14 @@ def xflow(seed=51, R=400, n=60_000, origins=6, contexts=4, duration_ms=6000, zip
                          origin=og[src][key], context=cx[src][key])
     cuts = np.linspace(0, full.n, split + 1).astype(int)
     batches = [full.subset(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
-    # the origin / context nodes a rule can read (the set both sides keep)
-    on, dn = set(), set()
+    # every entry with an origin has its origin node (ClusterBuilderSlot.java:107-110);
+    # context nodes are kept for the CHAIN rules that read them
+    has_o = full.origin != abi.ORIGIN_NONE
+    pairs = np.unique(full.res_id[has_o].astype(np.uint64) << np.uint64(32) | full.origin[has_o].astype(np.uint64))
+    on = {(int(p >> np.uint64(32)), int(p & np.uint64(0xffffffff))) for p in pairs}
+    dn = set()
     for r in rules:
         sel = full.res_id == r.resource
-        if r.strategy == abi.STRATEGY_DIRECT and r.limit_app != abi.APP_DEFAULT:
-            on |= {(int(r.resource), int(o)) for o in np.unique(full.origin[sel]) if o != abi.ORIGIN_NONE}
         if r.strategy == abi.STRATEGY_CHAIN and np.any(full.context[sel] == r.ref_resource):
             dn.add((int(r.ref_resource), int(r.resource)))
     n_valid = sum(1 for r in rules if not (r.grade == abi.GRADE_QPS and r.strategy in (1, 2) and
