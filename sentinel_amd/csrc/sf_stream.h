@@ -271,6 +271,115 @@ __device__ __forceinline__ unsigned long long thr_window_solve(int room0, unsign
     return pm;
 }
 
+// Run mode: a chunk made of few long runs of entries and of exits (a
+// saturated head resource whose events of each millisecond are its entries,
+// then its exits) is decided run by run instead of window by window.
+//   - a run of entries only adds threads: with room R = floor(count) - T, the
+//     passes are the greedy left-to-right choice of entries with
+//     acquireCount <= R, R falling by one per pass -- every entry of
+//     acquireCount 1 up to the R-th one, plus the few larger counts that still
+//     fit, found 64 entries at a time with ballots (no scan);
+//   - a run of exits only releases threads: T falls by the number of live
+//     exits in it, one vector read of its live-exit words and a wave sum.
+// The exits of a run's passed entries are marked live before the next run is
+// read (same wave, LDS order), so a run of exits always sees every entry
+// before it.  Applies to chunks of at most THR_RUNS runs, without an
+// acquireCount > THR_CBIG and with T far from int wrap; other chunks use the
+// window walk below, which keeps the same state (T, the live-exit ring).
+#ifndef SF_THR_RUNS
+#define SF_THR_RUNS 40
+#endif
+constexpr int THR_RUNS = SF_THR_RUNS;
+
+// Decide chunk [q0, q0 + 64 nwin) in run mode (thr_decide checked that it applies).
+__device__ __forceinline__ void thr_decide_runs(ThrLds& L, int buf, unsigned long long* lxfar, uint32_t q0,
+                                                uint32_t lo, uint32_t hi, int64_t IM, int64_t& T,
+                                                unsigned long long r_ent, uint32_t nwin, uint32_t slot0,
+                                                unsigned long long& pst, bool& far_marked) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t nev = min(hi - q0, 64u * nwin);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    uint32_t p = 0;
+    while (p < nev) {
+        const uint32_t w = p >> 6, b = p & 63;
+        const bool is_ent = (rl64(r_ent, (int)w) >> b) & 1ull;
+        // the run's end: the first later event of the other kind (or the chunk's end)
+        unsigned long long x = (uint32_t)lane < nwin ? (is_ent ? ~r_ent : r_ent) : ~0ull;
+        if ((uint32_t)lane < w) x = 0ull;
+        else if ((uint32_t)lane == w) x &= ~0ull << b;
+        const unsigned long long mw = __ballot(x != 0ull);
+        const int l = __ffsll((long long)mw) - 1;
+        const uint32_t e = min(64u * (uint32_t)l + (uint32_t)__builtin_ctzll(rl64(x, l)), nev);
+        if (is_ent) {
+            int64_t R = IM - T;
+            for (uint32_t g = p; g < e && R > 0; g += 64) {
+                const uint32_t k = g + (uint32_t)lane;
+                const bool valid = k < e;
+                const uint2 rc = valid ? L.rec[buf][k] : make_uint2(XO_NONE, 1u);
+                const int32_t c = (int32_t)rc.y;
+                const unsigned long long vm = __ballot(valid);
+                const unsigned long long big = __ballot(valid && c > 1);
+                const unsigned long long ones = vm & ~big;
+                unsigned long long pm = 0;
+                int from = 0;
+                // every entry fits even after all earlier ones of the group passed
+                const bool allfit = !__ballot(valid && c > THR_CSMALL) &&
+                                    R >= (int64_t)__popcll(vm) - 1 + (big ? THR_CSMALL : 1);
+                if (allfit) { pm = vm; R -= __popcll(vm); }
+                else while (true) {
+                    const unsigned long long bz = big & (from < 64 ? ~0ull << from : 0ull);
+                    const int z = bz ? __ffsll((long long)bz) - 1 : 64;
+                    const unsigned long long m1 = ones & (from < 64 ? ~0ull << from : 0ull) &
+                                                  (z < 64 ? (1ull << z) - 1ull : ~0ull);
+                    const int n1 = __popcll(m1);
+                    if ((int64_t)n1 >= R) {                    // the first R of them pass, then R = 0
+                        const int rank = __popcll(m1 & below);
+                        pm |= __ballot(((m1 >> lane) & 1ull) && (int64_t)rank < R);
+                        R = 0;
+                        break;
+                    }
+                    pm |= m1; R -= n1;
+                    if (z == 64) break;
+                    if ((int64_t)__builtin_amdgcn_readlane(c, z) <= R) { pm |= 1ull << z; R -= 1; }
+                    from = z + 1;
+                    if (R == 0) break;
+                }
+                R = uniform64(R);
+                if (pm) {
+                    T += __popcll(pm);
+                    const bool mk = ((pm >> lane) & 1ull) && rc.x != XO_NONE && rc.x < hi;
+                    bool fm2 = false;
+                    if (mk) fm2 = thr_mark_exit(L, lxfar, rc.x, q0, lo);
+                    far_marked |= __ballot(fm2) != 0ull;
+                    // pass bits staged per window (lane w <-> window w)
+                    const uint32_t gw = g >> 6, sh = g & 63;
+                    if ((uint32_t)lane == gw) pst |= pm << sh;
+                    if (sh && (uint32_t)lane == gw + 1) pst |= pm >> (64 - sh);
+                }
+            }
+            T = uniform64(T);
+        } else {
+            // live exits of [p, e): their ring words, edges masked
+            int64_t nl = 0;
+            for (uint32_t w0 = w; 64u * w0 < e; w0 += 64) {
+                const uint32_t ww = w0 + (uint32_t)lane;
+                unsigned long long v = 0;
+                if (64u * ww < e) {
+                    v = L.lx[(slot0 + ww) % LX_WORDS];
+                    if (ww == w) v &= ~0ull << b;
+                    const uint32_t lim = e - 64u * ww;             // events of this word inside the run
+                    if (lim < 64u) v &= (1ull << lim) - 1ull;
+                }
+                const int s = wave_scan_add(__popcll(v));
+                nl += __builtin_amdgcn_readlane(s, 63);
+            }
+            T = uniform64(T - nl);
+        }
+        p = e;
+    }
+    if ((uint32_t)lane < nwin) L.lx[(slot0 + (uint32_t)lane) % LX_WORDS] = 0ull;   // the chunk's words consumed
+}
+
 // THR_SW consecutive windows whose entries all fit are taken in one step.
 constexpr int THR_SW = 4;
 #ifndef SF_SOLVE_MIN_ROOM
@@ -306,6 +415,24 @@ __device__ void thr_decide(ThrLds& L, int buf, unsigned long long* lxfar, uint32
 #ifdef SF_STREAM_PROF
     const uint64_t tb = __builtin_amdgcn_s_memtime();
 #endif
+    {
+        // run mode (thr_decide_runs) for a chunk of few runs: count the runs
+        // (kind changes between neighbouring events, inside and across words)
+        const bool act = (uint32_t)lane < nwin;
+        const unsigned long long b0 = __ballot(act && (r_ent & 1ull)), bt = __ballot(act && (r_ent >> 63));
+        const int inner = wave_scan_add(act ? __popcll((r_ent ^ (r_ent << 1)) & ~1ull) : 0);
+        const unsigned long long edge = nwin > 1 ? ((b0 >> 1) ^ bt) & ((1ull << (nwin - 1)) - 1ull) : 0ull;
+        const int runs = 1 + __builtin_amdgcn_readlane(inner, 63) + __popcll(edge);
+        const int64_t span = 64 * THR_WPC;
+        if (!bigm && runs <= THR_RUNS && T >= (int64_t)INT32_MIN + span &&
+            T + (int64_t)THR_CBIG + span <= (int64_t)INT32_MAX) {
+            thr_decide_runs(L, buf, lxfar, q0, lo, hi, IM, T, r_ent, nwin, slot0, pst, far_marked);
+            w = nwin;
+#ifdef SF_STREAM_PROF
+            prof[5]++;
+#endif
+        }
+    }
     while (w < nwin) {
         const uint32_t q = q0 + 64 * w;
         const int64_t room0 = IM - T;

@@ -107,6 +107,17 @@ def test_heavy_thread_ms_blocks(eng_mod, so, seed):
     workloads.run(eng_mod.FlowEngine, so.OracleEngine, ms_block_thread_workload(seed))
 
 
+@pytest.mark.parametrize("count,rt_mean,duration", [(50.0, 5.0, 300), (3.0, 2.0, 300), (5000.0, 20.0, 300),
+                                                   (400.0, 0.3, 150), (80.0, 200.0, 400)])
+def test_heavy_thread_runs(eng_mod, so, count, rt_mean, duration):
+    """The THREAD walk's run mode (chunks of a few long runs of entries and of
+    exits): saturated with a small and a tiny room, never saturated, exits in
+    their entry's millisecond, and exits far beyond the LDS ring (the HBM
+    live-exit bitmap) -- against the oracle, two batches."""
+    workloads.run(eng_mod.FlowEngine, so.OracleEngine,
+                  ms_block_thread_workload(7, n_entry=150_000, duration=duration, count=count, rt_mean=rt_mean))
+
+
 def test_device_resident_batch(eng_mod, so):
     """Inputs already in HBM (the bench path): same verdicts as the host path."""
     w = workloads.config3(R=5000, n=200_000, seed=5, split=1)
