@@ -154,7 +154,7 @@ static void free_work(Work& w) {
                     w.pscan_tmp, w.fill_tiles, w.fill_ntiles, w.acc_hw,
                     w.acc_sec, w.acc_hw_base, w.acc_sec_base, w.seg_hw0, w.seg_sec0,
                     w.seg_nhw, w.seg_nsec, w.hticks, w.passbits, w.stream_list, w.sticks,
-                    w.exit_of, w.lxfar, w.thr_rec, w.vs_cursor};
+                    w.exit_of, w.lxfar, w.thr_rec, w.vs_cursor, w.tile_rc, w.seg_rb, w.seg_re};
     for (void* p : ptrs) if (p) hipFree(p);
     w = Work{};
 }
@@ -267,6 +267,7 @@ static int alloc_work(sf_engine* e, Work& w) {
     WALLOC(w.exit_of, N * 4);
     WALLOC(w.lxfar, (N / 64 + 2) * 8);
     WALLOC(w.thr_rec, N * 8);
+    WALLOC(w.tile_rc, (size_t)w.fill_tile_cap * 4); WALLOC(w.seg_rb, SC * 4); WALLOC(w.seg_re, SC * 4);
     WALLOC(w.vs_cursor, VS_CURSORS(N) * 4);
     return SF_OK;
 }

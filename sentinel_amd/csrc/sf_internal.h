@@ -204,6 +204,10 @@ struct Work {
     uint32_t* exit_of;                                  // [n] sorted index of each entry's exit, ~0 if none
     unsigned long long* lxfar;                          // [n/64+2] far live exits (SM_THREAD)
     uint2* thr_rec;                                     // [n] THREAD-segment event records (k_thr_prep, sf_stream.h)
+    uint32_t* tile_rc;                                  // [fill_tile_cap] runs starting in each stream tile -> run id base
+    uint32_t* seg_rb; uint32_t* seg_re;                 // [seg_cap] run id range of each SM_THREAD segment
+    // (THREAD run mode also borrows buffers dead after the sort: rid = keys_in,
+    //  run_start = head_scan, run_pre = keys_out, entry records = pv_in; sf_kernels.hip heavy_ctx)
     uint32_t* vs_cursor;                                // [VS_CURSORS(N)] fill counts of the verdict scatter's buckets
 };
 // verdict scatter (sorted order -> submission order, launch_scatter): regions of

@@ -395,6 +395,8 @@ static HeavyCtx heavy_ctx(const Work& w) {
     hc.exit_of = w.exit_of;
     hc.lxfar = w.lxfar;
     hc.thr_rec = w.thr_rec;
+    hc.rid = w.keys_in; hc.run_start = w.head_scan; hc.run_pre = w.keys_out; hc.rrec = (uint2*)w.pv_in;
+    hc.seg_rb = w.seg_rb; hc.seg_re = w.seg_re; hc.segflag = w.segflag;
     return hc;
 }
 
@@ -632,18 +634,30 @@ __global__ void __launch_bounds__(1024) k_fill_tiles(HeavyCtx hc, StreamCtx sc, 
 // the sort phase): the serial chain's loaders then move 8 B per event with one
 // load each and no decoding (sf_stream.h ThrRec).  Grid-stride over the
 // stream class's fill tiles.
+// Also the run heads of each tile (run mode, sf_stream.h: a run is a maximal
+// stretch of the segment's checked entries, or of its other events) and the
+// segment flag of an acquireCount beyond THR_CBIG.
 __global__ void __launch_bounds__(256) k_thr_prep(const uint8_t* flags, const int32_t* cnt, const int64_t* eref,
-                                                  HeavyCtx hc, const uint2* tiles, const uint32_t* ntiles) {
+                                                  HeavyCtx hc, const uint2* tiles, const uint32_t* ntiles,
+                                                  uint32_t* tile_rc, uint32_t* segflag) {
+    __shared__ uint32_t heads;
     const uint32_t nt = ntiles[1];
     for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
         const uint2 tl = tiles[t];
         const uint32_t s = tl.x;
-        if (hc.seg_mode[s] != SM_THREAD) continue;
+        if (hc.seg_mode[s] != SM_THREAD) { if (threadIdx.x == 0) tile_rc[t] = 0; continue; }
+        if (threadIdx.x == 0) heads = 0;
+        __syncthreads();
         const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1];
+        uint32_t nh = 0;
+        bool big = false;
         for (uint32_t j = max(tl.y * FILL_TILE, lo) + threadIdx.x; j < min(tl.y * FILL_TILE + FILL_TILE, hi); j += 256) {
             const uint8_t f = flags[j];
             uint2 r;
-            if (!(f & SF_EV_EXIT) && !(f & EVF_SYSBLK)) { r.x = hc.exit_of[j]; r.y = (uint32_t)cnt[j]; }
+            if (!(f & SF_EV_EXIT) && !(f & EVF_SYSBLK)) {
+                r.x = hc.exit_of[j]; r.y = (uint32_t)cnt[j];
+                big |= cnt[j] > THR_CBIG;
+            }
             else if (!(f & SF_EV_EXIT)) { r.x = 0u; r.y = THR_REC_EXIT; }   // blocked before: a no-op (dead exit)
             else {
                 const int64_t ref = eref ? eref[j] : -1;
@@ -651,6 +665,101 @@ __global__ void __launch_bounds__(256) k_thr_prep(const uint8_t* flags, const in
                 r.y = THR_REC_EXIT | (ref == -1 ? THR_REC_LIVE : 0u);
             }
             ((uint2*)hc.thr_rec)[j] = r;
+            nh += (j == lo || is_checked_entry(f) != is_checked_entry(flags[j - 1])) ? 1u : 0u;
+        }
+        if (__ballot(big) && (threadIdx.x & 63) == 0) atomicOr(&segflag[s], SEGF_BIGC);
+        nh = (uint32_t)wave_sum(nh);
+        if ((threadIdx.x & 63) == 0 && nh) atomicAdd(&heads, nh);
+        __syncthreads();
+        if (threadIdx.x == 0) tile_rc[t] = heads;
+        __syncthreads();
+    }
+}
+
+// Run mode tables (sf_stream.h thr_runs_segment), after k_thr_prep:
+//   k_thr_rscan  exclusive scan of the tiles' run counts (global run ids:
+//                the runs of a segment are a contiguous range, in order)
+//   k_thr_rid    run id of every event, run starts, the segment's run range
+//   k_thr_rrec   run-mode segments: entry records (run id of the exit,
+//                acquireCount); exits live from before the batch counted per run
+__global__ void __launch_bounds__(1024) k_thr_rscan(uint32_t* tile_rc, const uint32_t* ntiles) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
+    const uint32_t nt = ntiles[1];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < nt; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < nt ? tile_rc[i] : 0u;
+        const uint32_t incl = (uint32_t)wave_scan_add((int)v);
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t before = carry;
+        for (int k = 0; k < wv; k++) before += wsum[k];
+        if (i < nt) tile_rc[i] = before + incl - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = before + incl;
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_thr_rid(const uint8_t* flags, HeavyCtx hc, const uint2* tiles,
+                                                 const uint32_t* ntiles, const uint32_t* tile_rb) {
+    __shared__ uint32_t wsum[4];
+    constexpr uint32_t PER = FILL_TILE / 256;
+    const uint32_t nt = ntiles[1];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const uint2 tl = tiles[t];
+        const uint32_t s = tl.x;
+        if (hc.seg_mode[s] != SM_THREAD) continue;
+        const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1];
+        const uint32_t base = tl.y * FILL_TILE + PER * threadIdx.x;
+        uint32_t hm = 0;                                   // heads among this thread's PER events
+#pragma unroll
+        for (uint32_t k = 0; k < PER; k++) {
+            const uint32_t j = base + k;
+            if (j >= lo && j < hi && (j == lo || is_checked_entry(flags[j]) != is_checked_entry(flags[j - 1])))
+                hm |= 1u << k;
+        }
+        const uint32_t c = (uint32_t)__popc(hm);
+        const uint32_t incl = (uint32_t)wave_scan_add((int)c);
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        uint32_t run = tile_rb[t] + incl - c;              // heads before this thread's events in the tile
+        for (int k = 0; k < wv; k++) run += wsum[k];
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < PER; k++) {
+            const uint32_t j = base + k;
+            if (j < lo || j >= hi) continue;
+            if ((hm >> k) & 1u) { run++; hc.run_start[run - 1] = j; hc.run_pre[run - 1] = 0u; }
+            hc.rid[j] = run - 1;                           // (a tile's events before its first head: the last run before it)
+            if (j == lo) hc.seg_rb[s] = run - 1;
+            if (j == hi - 1) hc.seg_re[s] = run;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_thr_rrec(const uint8_t* flags, const int32_t* cnt, const int64_t* eref,
+                                                  HeavyCtx hc, const uint2* tiles, const uint32_t* ntiles,
+                                                  const uint32_t* segflag) {
+    const uint32_t nt = ntiles[1];
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        const uint2 tl = tiles[t];
+        const uint32_t s = tl.x;
+        if (hc.seg_mode[s] != SM_THREAD) continue;
+        const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1];
+        if (!thr_run_mode(hc, s, lo, hi, segflag[s])) continue;
+        for (uint32_t j = max(tl.y * FILL_TILE, lo) + threadIdx.x; j < min(tl.y * FILL_TILE + FILL_TILE, hi); j += 256) {
+            const uint8_t f = flags[j];
+            if (is_checked_entry(f)) {
+                const uint32_t x = hc.exit_of[j];
+                hc.rrec[j] = make_uint2(x < hi ? hc.rid[x] : XO_NONE, (uint32_t)cnt[j]);
+            } else if ((f & SF_EV_EXIT) && (eref ? eref[j] : -1) == -1) {
+                atomicAdd(&hc.run_pre[hc.rid[j]], 1u);      // its entry passed before this batch: live
+            }
         }
     }
 }
@@ -1053,8 +1162,16 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     // (grids sized to the most tiles a batch of n events can have: small
     // SystemRule sub-batches do not pay for full-chip launches)
     const uint32_t tile_ub = n / FILL_TILE + n / (w.heavy_min + 1) + 2;
-    hipLaunchKernelGGL(k_thr_prep, dim3(std::min<uint32_t>(1024u, tile_ub)), dim3(256), 0, s, w.s_flags, w.s_cnt,
-                       b.eref ? w.s_eref : nullptr, hc, w.fill_tiles + w.fill_tile_cap, w.fill_ntiles);
+    const uint2* tiles1 = w.fill_tiles + w.fill_tile_cap;
+    const int64_t* seref = b.eref ? w.s_eref : nullptr;
+    const dim3 tgrid(std::min<uint32_t>(1024u, tile_ub));
+    hipLaunchKernelGGL(k_thr_prep, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, seref, hc, tiles1, w.fill_ntiles,
+                       w.tile_rc, w.segflag);
+    // THREAD run mode tables (sf_stream.h thr_runs_segment)
+    hipLaunchKernelGGL(k_thr_rscan, dim3(1), dim3(1024), 0, s, w.tile_rc, w.fill_ntiles);
+    hipLaunchKernelGGL(k_thr_rid, tgrid, dim3(256), 0, s, w.s_flags, hc, tiles1, w.fill_ntiles, w.tile_rc);
+    hipLaunchKernelGGL(k_thr_rrec, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, seref, hc, tiles1, w.fill_ntiles,
+                       w.segflag);
     if (timing) hipEventRecord(ev[2], s);
     return hipGetLastError();
 }

@@ -708,6 +708,202 @@ __device__ __forceinline__ void rl_decide_chunk(const int64_t* tsb, const int32_
     }
 }
 
+// ------------------------------------------------------------ THREAD run mode
+// A THREAD segment whose runs are long on average (thr_run_mode; the config-3
+// head resource: every millisecond its entries, then its exits) is decided
+// run by run from tables the sort phase prepared (k_thr_rid, k_thr_rrec), by
+// wave 0 alone:
+//   - a run of exits releases the live exits in it: a counter per run (an LDS
+//     ring of RUN_RC runs; farther ones in run_pre, with the exits whose entry
+//     passed before this batch), so the run costs one LDS read whatever its length;
+//   - a run of entries with room R = floor(count) - T > 0 passes entries
+//     greedily (thr_group_passes), 64 at a time, until R is 0; each pass adds
+//     one to the counter of its exit's run.  With no room the run is skipped.
+// The run table (start, run_pre) is read 64 runs per load, two loads ahead;
+// the first 64 entry records of each entry run of the next 64 runs are loaded
+// into registers one table step ahead and parked in LDS, so the chain waits on
+// global memory only when one run passes more than 64 entries.
+constexpr uint32_t RUN_RC = 8192;                  // live-exit counters: runs ahead of the walk (32 KiB)
+constexpr int THR_RG = 8;                          // groups of an entry run loaded together past the staged one
+struct RunLds {
+    uint32_t cnt[RUN_RC];
+    uint2 stage[2][32][64];                        // first 64 records of each entry run of a table step
+};
+static_assert(sizeof(RunLds) <= sizeof(unsigned long long) * (size_t)HS_SMEM_WORDS, "run mode LDS");
+
+// passes of one group of 64 entries (valid lanes) with room R > 0; R is lowered
+__device__ __forceinline__ unsigned long long thr_group_passes(bool valid, int32_t c, int64_t& R) {
+    const int lane = (int)(threadIdx.x & 63);
+#ifdef SF_EXP_SIMPLE
+    { const unsigned long long vm0 = __ballot(valid && lane < R); R = 0; return vm0; }
+#endif
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const unsigned long long vm = __ballot(valid);
+    const unsigned long long big = __ballot(valid && c > 1);
+    const unsigned long long ones = vm & ~big;
+    // every entry fits even after all earlier ones of the group passed
+    if (!__ballot(valid && c > THR_CSMALL) && R >= (int64_t)__popcll(vm) - 1 + (big ? THR_CSMALL : 1)) {
+        R -= __popcll(vm);
+        return vm;
+    }
+    unsigned long long pm = 0;
+    int from = 0;
+    while (true) {
+        const unsigned long long fr = from < 64 ? ~0ull << from : 0ull;
+        const unsigned long long bz = big & fr;
+        const int z = bz ? __ffsll((long long)bz) - 1 : 64;
+        const unsigned long long m1 = ones & fr & (z < 64 ? (1ull << z) - 1ull : ~0ull);
+        const int n1 = __popcll(m1);
+        if ((int64_t)n1 >= R) {                    // the first R of them pass, then no room
+            const int rank = __popcll(m1 & below);
+            pm |= __ballot(((m1 >> lane) & 1ull) && (int64_t)rank < R);
+            R = 0;
+            break;
+        }
+        pm |= m1; R -= n1;
+        if (z == 64) break;
+        if ((int64_t)__builtin_amdgcn_readlane(c, z) <= R) { pm |= 1ull << z; R -= 1; }
+        from = z + 1;
+        if (R == 0) break;
+    }
+    R = uniform64(R);
+    return pm;
+}
+
+__device__ void thr_runs_segment(const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t s, uint32_t lo,
+                                 uint32_t hi, uint32_t res, int64_t IM, RunLds& L) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t rb = hc.seg_rb[s], nr = hc.seg_re[s] - rb;
+    // runs alternate kinds: run k holds entries iff (k & 1) == e0
+    const uint32_t e0 = is_checked_entry(io.flags[lo]) ? 0u : 1u;
+    int64_t T = uniform64(st.threads[res]);
+    unsigned long long* pbits = hc.passbits;
+    const uint2* rrec = hc.rrec;
+    auto tbl = [&](uint32_t c, uint32_t& ts, uint32_t& tp) {
+        const uint32_t k = 64u * c + (uint32_t)lane;
+        ts = k < nr ? hc.run_start[rb + k] : hi;
+        tp = k < nr ? __hip_atomic_load(hc.run_pre + rb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    };
+    uint2 sr[32];                                  // staged first records of the entry runs of a table step
+    auto stage_issue = [&](uint32_t ts) {
+#pragma unroll
+        for (int i = 0; i < 32; i++) {
+            const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)ts, 2 * i + (int)e0);
+            sr[i] = rrec[min(a + (uint32_t)lane, hi - 1)];
+        }
+    };
+    auto stage_park = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 32; i++) L.stage[buf][i][lane] = sr[i];
+    };
+    const uint32_t nchunk = (nr + 63) / 64;
+    uint32_t s0, p0, s1, p1, s2, p2;
+    tbl(0, s0, p0);
+    tbl(1, s1, p1);
+    stage_issue(s0);
+    stage_park(0);
+    bool far = false;
+#ifdef SF_STREAM_PROF
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};     // cycles: table steps, exit runs, entry runs; counts: exit runs, entry runs with room, groups
+    const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#endif
+    for (uint32_t c = 0; c < nchunk; c++) {
+#ifdef SF_STREAM_PROF
+        const uint64_t pa = __builtin_amdgcn_s_memtime();
+#endif
+        if (far) {                                 // counters of far runs must be in HBM before their table loads
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+            __builtin_amdgcn_s_waitcnt(0);
+            far = false;
+        }
+        tbl(c + 2, s2, p2);
+        stage_issue(s1);
+        const int buf = (int)(c & 1);
+        const uint32_t kn = min(64u, nr - 64u * c);
+        const uint32_t next0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s1);
+#ifdef SF_STREAM_PROF
+        uint64_t pb = __builtin_amdgcn_s_memtime();
+        pf[0] += pb - pa;
+#endif
+        for (uint32_t k = 0; k < kn; k++) {
+            const uint32_t r = rb + 64u * c + k;                     // global run id
+            const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)s0, (int)k);
+            const uint32_t e = k + 1 < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)s0, (int)k + 1) : next0;
+            if ((k & 1u) != e0) {
+                // exits: release the live ones (marked by earlier passes, or from before the batch)
+                const uint32_t slot = r % RUN_RC;
+                const uint32_t nl = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.cnt[slot]) +
+                                    (uint32_t)__builtin_amdgcn_readlane((int)p0, (int)k);
+                if (lane == 0) L.cnt[slot] = 0u;
+                T -= (int64_t)nl;
+#ifdef SF_STREAM_PROF
+                { const uint64_t pc = __builtin_amdgcn_s_memtime(); pf[1] += pc - pb; pb = pc; pf[3]++; }
+#endif
+                continue;
+            }
+            int64_t R = IM - T;
+#ifdef SF_STREAM_PROF
+            if (R > 0) pf[4]++;
+#endif
+            // one group of 64 entries from g: passes, their exits' run counters, pass bits
+            auto group = [&](uint2 rc, uint32_t g) {
+                const bool valid = g + (uint32_t)lane < e;
+                const unsigned long long pm = thr_group_passes(valid, (int32_t)rc.y, R);
+#ifdef SF_STREAM_PROF
+                pf[5]++;
+#endif
+                if (!pm) return;
+                T += __popcll(pm);
+                const bool mk = ((pm >> lane) & 1ull) && rc.x != XO_NONE;
+                bool fm = false;
+#ifndef SF_EXP_NOMARK
+                if (mk) {
+                    if (rc.x - r < RUN_RC - 1) atomicAdd(&L.cnt[rc.x % RUN_RC], 1u);
+                    else { atomicAdd(hc.run_pre + rc.x, 1u); fm = true; }
+                }
+#endif
+                far |= __ballot(fm) != 0ull;
+                const uint32_t sh = g & 63;
+#ifndef SF_EXP_NOPB
+                if (lane == 0) atomicOr(pbits + (g >> 6), pm << sh);
+                if (lane == 1 && sh) atomicOr(pbits + (g >> 6) + 1, pm >> (64 - sh));
+#endif
+            };
+            if (R > 0) group(L.stage[buf][k >> 1][lane], a);           // the staged first group
+            // more room than the first group used: the rest of the run from HBM,
+            // THR_RG groups per round with all their loads in flight
+            for (uint32_t g = a + 64; g < e && R > 0; g += 64 * THR_RG) {
+                uint2 nx[THR_RG];
+#pragma unroll
+                for (int i = 0; i < THR_RG; i++) nx[i] = rrec[min(g + 64u * (uint32_t)i + (uint32_t)lane, hi - 1)];
+#pragma unroll
+                for (int i = 0; i < THR_RG; i++) {
+                    if (g + 64u * (uint32_t)i >= e || R <= 0) break;
+                    group(nx[i], g + 64u * (uint32_t)i);
+                }
+            }
+            T = uniform64(T);
+#ifdef SF_STREAM_PROF
+            { const uint64_t pc = __builtin_amdgcn_s_memtime(); pf[2] += pc - pb; pb = pc; }
+#endif
+        }
+#ifdef SF_STREAM_PROF
+        const uint64_t pd = __builtin_amdgcn_s_memtime();
+#endif
+        stage_park(buf ^ 1);
+#ifdef SF_STREAM_PROF
+        pf[0] += __builtin_amdgcn_s_memtime() - pd;
+#endif
+        s0 = s1; p0 = p1; s1 = s2; p1 = p2;
+    }
+#ifdef SF_STREAM_PROF
+    if (lane == 0)
+        printf("SF_RUN_PROF seg %u events %u runs %u: total %lu table %lu exit-runs %lu (%lu) entry-runs %lu (%lu with room, %lu groups)\n",
+               s, hi - lo, nr, (unsigned long)(__builtin_amdgcn_s_memtime() - pt0), (unsigned long)pf[0],
+               (unsigned long)pf[1], (unsigned long)pf[3], (unsigned long)pf[2], (unsigned long)pf[4], (unsigned long)pf[5]);
+#endif
+}
+
 __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyCtx& hc, const StreamCtx& sc,
                                uint32_t s, uint32_t b, unsigned long long* smem) {
     const uint64_t t_start = sc.sticks ? wall_clock64() : 0;
@@ -719,7 +915,19 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
     // the deciding wave is the serial chain: it wins issue arbitration on its
     // SIMD against the memory-bound waves of the concurrent kernels
     if (wave0) __builtin_amdgcn_s_setprio(3);
-    if (hc.seg_mode[s] == SM_THREAD) {
+    bool runs = false;
+    if (hc.seg_mode[s] == SM_THREAD && thr_run_mode(hc, s, lo, hi, hc.segflag[s])) {
+        // (the run walk compares T + acquireCount with floor(count) in 64 bits:
+        // exact while no int wrap can occur, i.e. T stays far from the int range)
+        const int64_t T0 = st.threads[res], span = (int64_t)(hi - lo);
+        runs = T0 >= (int64_t)INT32_MIN + span && T0 + (int64_t)THR_CBIG + span <= (int64_t)INT32_MAX;
+    }
+    if (runs) {
+        RunLds& RL = *reinterpret_cast<RunLds*>(smem);
+        for (uint32_t i = threadIdx.x; i < RUN_RC; i += HS_T) RL.cnt[i] = 0u;
+        __syncthreads();
+        if (wave0) thr_runs_segment(st, io, hc, s, lo, hi, res, (int64_t)floor(rule.count), RL);
+    } else if (hc.seg_mode[s] == SM_THREAD) {
         ThrLds& L = *reinterpret_cast<ThrLds*>(smem);
         for (uint32_t i = threadIdx.x; i < LX_WORDS; i += HS_T) L.lx[i] = 0ull;
         __syncthreads();
