@@ -1145,10 +1145,6 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags,
                            w.head_scan, w.seg_start, w.s_eref, w.s_cts, w.exit_of, st.err);
-    PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
-    e = rocprim::inclusive_scan<PcScanCfg>(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg, (size_t)n,
-                                           rocprim::plus<int64_t>(), s);
-    if (e != hipSuccess) return e;
     hipMemsetAsync(w.counters, 0, 10 * sizeof(uint32_t), s);
     hipMemsetAsync(w.lcounts, 0, 2 * LCLS * sizeof(uint32_t), s);
     hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
@@ -1159,19 +1155,6 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     HeavyCtx hc = heavy_ctx(w);
     StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, nullptr, w.counters + 7};
     hipLaunchKernelGGL(k_fill_tiles, dim3(2), dim3(1024), 0, s, hc, sc, w.fill_tiles, w.fill_tile_cap, w.fill_ntiles);
-    // (grids sized to the most tiles a batch of n events can have: small
-    // SystemRule sub-batches do not pay for full-chip launches)
-    const uint32_t tile_ub = n / FILL_TILE + n / (w.heavy_min + 1) + 2;
-    const uint2* tiles1 = w.fill_tiles + w.fill_tile_cap;
-    const int64_t* seref = b.eref ? w.s_eref : nullptr;
-    const dim3 tgrid(std::min<uint32_t>(1024u, tile_ub));
-    hipLaunchKernelGGL(k_thr_prep, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, seref, hc, tiles1, w.fill_ntiles,
-                       w.tile_rc, w.segflag);
-    // THREAD run mode tables (sf_stream.h thr_runs_segment)
-    hipLaunchKernelGGL(k_thr_rscan, dim3(1), dim3(1024), 0, s, w.tile_rc, w.fill_ntiles);
-    hipLaunchKernelGGL(k_thr_rid, tgrid, dim3(256), 0, s, w.s_flags, hc, tiles1, w.fill_ntiles, w.tile_rc);
-    hipLaunchKernelGGL(k_thr_rrec, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, seref, hc, tiles1, w.fill_ntiles,
-                       w.segflag);
     if (timing) hipEventRecord(ev[2], s);
     return hipGetLastError();
 }
@@ -1329,6 +1312,27 @@ static void launch_scatter(Work& w, uint32_t n, uint8_t* o_status, hipStream_t s
     hipLaunchKernelGGL(k_vs_region, dim3((n + (1u << VS_REG) - 1) >> VS_REG), dim3(VS_T), 0, s, regions, o_status, n);
 }
 
+// THREAD stream records and run tables (state-independent; at the head of the
+// decide phase on stream A, before k_heavy_stream reads them: the sort phase of
+// the next batch is the longer of the two pipelined phases)
+static void launch_thr_prep(Work& w, const DevBatch& b, hipStream_t s) {
+    const uint32_t n = b.n;
+    HeavyCtx hc = heavy_ctx(w);
+    // (grids sized to the most tiles a batch of n events can have: small
+    // SystemRule sub-batches do not pay for full-chip launches)
+    const uint32_t tile_ub = n / FILL_TILE + n / (w.heavy_min + 1) + 2;
+    const uint2* tiles1 = w.fill_tiles + w.fill_tile_cap;
+    const int64_t* seref = b.eref ? w.s_eref : nullptr;
+    const dim3 tgrid(std::min<uint32_t>(1024u, tile_ub));
+    hipLaunchKernelGGL(k_thr_prep, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, seref, hc, tiles1, w.fill_ntiles,
+                       w.tile_rc, w.segflag);
+    // THREAD run mode tables (sf_stream.h thr_runs_segment)
+    hipLaunchKernelGGL(k_thr_rscan, dim3(1), dim3(1024), 0, s, w.tile_rc, w.fill_ntiles);
+    hipLaunchKernelGGL(k_thr_rid, tgrid, dim3(256), 0, s, w.s_flags, hc, tiles1, w.fill_ntiles, w.tile_rc);
+    hipLaunchKernelGGL(k_thr_rrec, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, seref, hc, tiles1, w.fill_ntiles,
+                       w.segflag);
+}
+
 // Decide phase (stateful, batch order): the serial chains (k_heavy_stream)
 // start first, on A; QPS/WarmUp heavy segments on B, the light lanes on C;
 // then the verdicts are scattered back to submission order.
@@ -1355,11 +1359,21 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     if (out.wait) hipMemsetAsync(out.wait, 0, (size_t)n * sizeof(int32_t), s);
     if (out.rule) hipMemsetAsync(out.rule, 0, (size_t)n * sizeof(uint16_t), s);
     hipEventRecord(ev[5], s);                      // fork
+    launch_thr_prep(w, b, s);
     hipEventRecord(ev[11], s);
     hipLaunchKernelGGL(k_heavy_stream, dim3(std::min(max_heavy, w.stream_grid)), dim3(HS_T), 0, s, st, io, hc, sc);
     hipEventRecord(ev[12], s);
     hipStreamWaitEvent(s2, ev[5], 0);
     hipStreamWaitEvent(s3, ev[5], 0);
+    {
+        // acquireCount prefix of the entries (QPS / WarmUp window budgets, k_heavy_decide
+        // only): state-independent, but here on stream B rather than in the sort phase,
+        // the longer of the two pipelined phases
+        PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
+        const hipError_t e = rocprim::inclusive_scan<PcScanCfg>(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg,
+                                                                (size_t)n, rocprim::plus<int64_t>(), s2);
+        if (e != hipSuccess) return e;
+    }
     if (st.S <= 2)
         hipLaunchKernelGGL(k_heavy_decide<2>, dim3(max_heavy), dim3(64), 0, s2, st, io, hc);
     else

@@ -1,6 +1,6 @@
 # GPU box: kernel timeline (per-kernel totals) of one config-4 batch with its SystemRule
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && OUT=gpurun_out/c4tl; rm -rf $OUT; mkdir -p $OUT
-timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d $OUT/kt -o kt -- python3 tools/system_bench.py --reps 1 --no-check > $OUT/c4.json 2> $OUT/c4.err || { echo FAILED; tail $OUT/c4.err; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --output-format rocpd -d $OUT/kt -o kt -- python3 tools/system_bench.py --reps 1 --no-check --qps-frac ${QF:-0.6} > $OUT/c4.json 2> $OUT/c4.err || { echo FAILED; tail $OUT/c4.err; exit 1; }
 python3 - $(find $OUT/kt -name '*.db' | head -1) <<'PY'
 import re, sqlite3, sys
 from collections import defaultdict
