@@ -32,7 +32,7 @@ enum : uint8_t { SM_LIGHT = 0, SM_GENERIC = 1, SM_QPS = 2, SM_WARM = 3, SM_RL = 
                  SM_LIGHTQ = 9 };   // short light segment of a lone QPS DefaultController rule (decide_qps_segment)
 constexpr uint32_t SEGF_PRIO = SEGF_PRIO_, SEGF_NONPOS = 2u, SEGF_SYS = SEGF_SYS_, SEGF_EXIT = 8u, SEGF_COLL = 16u;
 constexpr uint32_t SEGF_ORIGIN = 32u;   // an event carries an origin: its origin node is updated (xflow walk)
-constexpr uint32_t SEGF_BIGC = 64u;     // a checked entry with acquireCount > THR_CBIG (k_thr_prep; THREAD run mode off)
+constexpr uint32_t SEGF_BIGC = 64u;     // a checked entry with acquireCount > THR_CBIG (k_thr_heads; THREAD run mode off)
 
 struct Acc {            // per (segment, window) counter deltas
     unsigned long long pass, block, succ, rt, exc, n_pass, n_exit, n_touch;
@@ -95,8 +95,8 @@ struct HeavyCtx {
     unsigned long long* passbits;                       // [n/64+2] bit j: entry j passed (QPS/WarmUp/RL/THREAD)
     const uint32_t* exit_of;                            // [n] sorted index of an entry's exit (or ~0)
     unsigned long long* lxfar;                          // [n/64+2] live exits beyond the LDS ring (SM_THREAD)
-    const uint2* thr_rec;                               // [n] SM_THREAD event records (k_thr_prep)
-    // THREAD run mode (sf_stream.h thr_runs_segment; k_thr_rid / k_thr_rrec)
+    const uint2* thr_rec;                               // [n] SM_THREAD window-walk event records (k_thr_rec)
+    // THREAD run mode (sf_stream.h thr_runs_segment; k_thr_rid / k_thr_rec)
     uint32_t* rid;                                      // [n] global run id of each SM_THREAD event
     uint32_t* run_start;                                // [runs] first sorted position of each run
     uint32_t* run_pre;                                  // [runs] live exits of a run not marked by the walk
@@ -107,7 +107,7 @@ struct HeavyCtx {
 
 // A THREAD segment is decided run by run when its runs are long on average
 // (few kind changes); the decision needs only the prepared tables, so both the
-// sort phase (k_thr_rrec) and the stream kernel take it the same way.
+// record preparation (k_thr_rec) and the stream kernel take it the same way.
 #ifndef SF_THR_RUN_AVG
 #define SF_THR_RUN_AVG 16
 #endif

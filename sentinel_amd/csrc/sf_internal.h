@@ -203,7 +203,7 @@ struct Work {
     unsigned long long* passbits;                       // [n/64+2] pass bit per sorted entry (heavy segments)
     uint32_t* exit_of;                                  // [n] sorted index of each entry's exit, ~0 if none
     unsigned long long* lxfar;                          // [n/64+2] far live exits (SM_THREAD)
-    uint2* thr_rec;                                     // [n] THREAD-segment event records (k_thr_prep, sf_stream.h)
+    uint2* thr_rec;                                     // [n] THREAD-segment window-walk records (k_thr_rec, sf_stream.h)
     uint32_t* tile_rc;                                  // [fill_tile_cap] runs starting in each stream tile -> run id base
     uint32_t* seg_rb; uint32_t* seg_re;                 // [seg_cap] run id range of each SM_THREAD segment
     // (THREAD run mode also borrows buffers dead after the sort: rid = keys_in,

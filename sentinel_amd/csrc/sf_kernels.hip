@@ -630,16 +630,15 @@ __global__ void __launch_bounds__(1024) k_fill_tiles(HeavyCtx hc, StreamCtx sc, 
     if (threadIdx.x == 0) ntiles[c] = min(carry, cap);
 }
 
-// Event records of the THREAD-grade stream segments (state-independent, so in
-// the sort phase): the serial chain's loaders then move 8 B per event with one
-// load each and no decoding (sf_stream.h ThrRec).  Grid-stride over the
-// stream class's fill tiles.
-// Also the run heads of each tile (run mode, sf_stream.h: a run is a maximal
-// stretch of the segment's checked entries, or of its other events) and the
-// segment flag of an acquireCount beyond THR_CBIG.
-__global__ void __launch_bounds__(256) k_thr_prep(const uint8_t* flags, const int32_t* cnt, const int64_t* eref,
-                                                  HeavyCtx hc, const uint2* tiles, const uint32_t* ntiles,
-                                                  uint32_t* tile_rc, uint32_t* segflag) {
+// THREAD-grade stream segments, state-independent preparation (at the head of
+// the decide phase, launch_thr_prep), grid-stride over the stream class's fill
+// tiles.  A run is a maximal stretch of a segment's checked entries, or of its
+// other events (sf_stream.h run mode).
+//   k_thr_heads  run heads of each tile; the segment flag of an acquireCount
+//                beyond THR_CBIG
+__global__ void __launch_bounds__(256) k_thr_heads(const uint8_t* flags, const int32_t* cnt, HeavyCtx hc,
+                                                   const uint2* tiles, const uint32_t* ntiles, uint32_t* tile_rc,
+                                                   uint32_t* segflag) {
     __shared__ uint32_t heads;
     const uint32_t nt = ntiles[1];
     for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
@@ -653,19 +652,9 @@ __global__ void __launch_bounds__(256) k_thr_prep(const uint8_t* flags, const in
         bool big = false;
         for (uint32_t j = max(tl.y * FILL_TILE, lo) + threadIdx.x; j < min(tl.y * FILL_TILE + FILL_TILE, hi); j += 256) {
             const uint8_t f = flags[j];
-            uint2 r;
-            if (!(f & SF_EV_EXIT) && !(f & EVF_SYSBLK)) {
-                r.x = hc.exit_of[j]; r.y = (uint32_t)cnt[j];
-                big |= cnt[j] > THR_CBIG;
-            }
-            else if (!(f & SF_EV_EXIT)) { r.x = 0u; r.y = THR_REC_EXIT; }   // blocked before: a no-op (dead exit)
-            else {
-                const int64_t ref = eref ? eref[j] : -1;
-                r.x = ref >= 0 ? j - (uint32_t)ref : 0u;
-                r.y = THR_REC_EXIT | (ref == -1 ? THR_REC_LIVE : 0u);
-            }
-            ((uint2*)hc.thr_rec)[j] = r;
-            nh += (j == lo || is_checked_entry(f) != is_checked_entry(flags[j - 1])) ? 1u : 0u;
+            const bool ent = is_checked_entry(f);
+            if (ent) big |= cnt[j] > THR_CBIG;
+            nh += (j == lo || ent != is_checked_entry(flags[j - 1])) ? 1u : 0u;
         }
         if (__ballot(big) && (threadIdx.x & 63) == 0) atomicOr(&segflag[s], SEGF_BIGC);
         nh = (uint32_t)wave_sum(nh);
@@ -676,12 +665,13 @@ __global__ void __launch_bounds__(256) k_thr_prep(const uint8_t* flags, const in
     }
 }
 
-// Run mode tables (sf_stream.h thr_runs_segment), after k_thr_prep:
 //   k_thr_rscan  exclusive scan of the tiles' run counts (global run ids:
 //                the runs of a segment are a contiguous range, in order)
 //   k_thr_rid    run id of every event, run starts, the segment's run range
-//   k_thr_rrec   run-mode segments: entry records (run id of the exit,
-//                acquireCount); exits live from before the batch counted per run
+//   k_thr_rec    the event records the stream kernel reads: run-mode segments
+//                (thr_run_mode) entry records (run id of the exit,
+//                acquireCount), exits live from before the batch counted per
+//                run; the others one 8-B window-walk record per event
 __global__ void __launch_bounds__(1024) k_thr_rscan(uint32_t* tile_rc, const uint32_t* ntiles) {
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t carry;
@@ -742,24 +732,36 @@ __global__ void __launch_bounds__(256) k_thr_rid(const uint8_t* flags, HeavyCtx 
     }
 }
 
-__global__ void __launch_bounds__(256) k_thr_rrec(const uint8_t* flags, const int32_t* cnt, const int64_t* eref,
-                                                  HeavyCtx hc, const uint2* tiles, const uint32_t* ntiles,
-                                                  const uint32_t* segflag) {
+__global__ void __launch_bounds__(256) k_thr_rec(const uint8_t* flags, const int32_t* cnt, const int64_t* eref,
+                                                 HeavyCtx hc, const uint2* tiles, const uint32_t* ntiles,
+                                                 const uint32_t* segflag) {
     const uint32_t nt = ntiles[1];
     for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
         const uint2 tl = tiles[t];
         const uint32_t s = tl.x;
         if (hc.seg_mode[s] != SM_THREAD) continue;
         const uint32_t lo = hc.seg_start[s], hi = hc.seg_start[s + 1];
-        if (!thr_run_mode(hc, s, lo, hi, segflag[s])) continue;
+        const bool runs = thr_run_mode(hc, s, lo, hi, segflag[s]);
         for (uint32_t j = max(tl.y * FILL_TILE, lo) + threadIdx.x; j < min(tl.y * FILL_TILE + FILL_TILE, hi); j += 256) {
             const uint8_t f = flags[j];
-            if (is_checked_entry(f)) {
-                const uint32_t x = hc.exit_of[j];
-                hc.rrec[j] = make_uint2(x < hi ? hc.rid[x] : XO_NONE, (uint32_t)cnt[j]);
-            } else if ((f & SF_EV_EXIT) && (eref ? eref[j] : -1) == -1) {
-                atomicAdd(&hc.run_pre[hc.rid[j]], 1u);      // its entry passed before this batch: live
+            if (runs) {
+                if (is_checked_entry(f)) {
+                    const uint32_t x = hc.exit_of[j];
+                    hc.rrec[j] = make_uint2(x < hi ? hc.rid[x] : XO_NONE, (uint32_t)cnt[j]);
+                } else if ((f & SF_EV_EXIT) && (eref ? eref[j] : -1) == -1) {
+                    atomicAdd(&hc.run_pre[hc.rid[j]], 1u);      // its entry passed before this batch: live
+                }
+                continue;
             }
+            uint2 r;
+            if (is_checked_entry(f)) { r.x = hc.exit_of[j]; r.y = (uint32_t)cnt[j]; }
+            else if (!(f & SF_EV_EXIT)) { r.x = 0u; r.y = THR_REC_EXIT; }   // blocked before: a no-op (dead exit)
+            else {
+                const int64_t ref = eref ? eref[j] : -1;
+                r.x = ref >= 0 ? j - (uint32_t)ref : 0u;
+                r.y = THR_REC_EXIT | (ref == -1 ? THR_REC_LIVE : 0u);
+            }
+            ((uint2*)hc.thr_rec)[j] = r;
         }
     }
 }
@@ -1324,12 +1326,12 @@ static void launch_thr_prep(Work& w, const DevBatch& b, hipStream_t s) {
     const uint2* tiles1 = w.fill_tiles + w.fill_tile_cap;
     const int64_t* seref = b.eref ? w.s_eref : nullptr;
     const dim3 tgrid(std::min<uint32_t>(1024u, tile_ub));
-    hipLaunchKernelGGL(k_thr_prep, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, seref, hc, tiles1, w.fill_ntiles,
+    hipLaunchKernelGGL(k_thr_heads, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, hc, tiles1, w.fill_ntiles,
                        w.tile_rc, w.segflag);
     // THREAD run mode tables (sf_stream.h thr_runs_segment)
     hipLaunchKernelGGL(k_thr_rscan, dim3(1), dim3(1024), 0, s, w.tile_rc, w.fill_ntiles);
     hipLaunchKernelGGL(k_thr_rid, tgrid, dim3(256), 0, s, w.s_flags, hc, tiles1, w.fill_ntiles, w.tile_rc);
-    hipLaunchKernelGGL(k_thr_rrec, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, seref, hc, tiles1, w.fill_ntiles,
+    hipLaunchKernelGGL(k_thr_rec, tgrid, dim3(256), 0, s, w.s_flags, w.s_cnt, seref, hc, tiles1, w.fill_ntiles,
                        w.segflag);
 }
 

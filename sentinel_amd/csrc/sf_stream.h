@@ -92,7 +92,7 @@ struct ThrWin {                                    // 24 B per window
     uint32_t flags;                                // bit 0: an acquireCount > 8, bit 1: > THR_CBIG, bit 2: > 1
 };
 
-// Event record (k_thr_prep, one per event of a THREAD segment, 8 B):
+// Event record (k_thr_rec, one per event of a window-walk THREAD segment, 8 B):
 //   entry: x = sorted position of its exit (or XO_NONE), y = acquireCount (>= 1)
 //   exit:  x = distance back to its entry in the segment (0: none), y = THR_REC_EXIT
 //          (| THR_REC_LIVE: the entry was decided earlier, the exit is live)
@@ -711,7 +711,7 @@ __device__ __forceinline__ void rl_decide_chunk(const int64_t* tsb, const int32_
 // ------------------------------------------------------------ THREAD run mode
 // A THREAD segment whose runs are long on average (thr_run_mode; the config-3
 // head resource: every millisecond its entries, then its exits) is decided
-// run by run from tables the sort phase prepared (k_thr_rid, k_thr_rrec), by
+// run by run from tables prepared ahead of it (k_thr_rid, k_thr_rec), by
 // wave 0 alone:
 //   - a run of exits releases the live exits in it: a counter per run (an LDS
 //     ring of RUN_RC runs; farther ones in run_pre, with the exits whose entry
@@ -770,8 +770,22 @@ __device__ __forceinline__ unsigned long long thr_group_passes(bool valid, int32
     return pm;
 }
 
+// the same with Java's int arithmetic, entry by entry: (int)(T + c) <= count
+// (DefaultController.canPass); only when T may leave the int range
+__device__ __noinline__ unsigned long long thr_group_passes_exact(bool valid, int32_t c, int64_t T, double M) {
+    unsigned long long vm = __ballot(valid), pm = 0;
+    while (vm) {
+        const int z = __ffsll((long long)vm) - 1;
+        vm &= vm - 1;
+        const int32_t cz = __builtin_amdgcn_readlane(c, z);
+        if ((double)(int32_t)((uint32_t)(int32_t)T + (uint32_t)cz) <= M) { pm |= 1ull << z; T += 1; }
+    }
+    return pm;
+}
+
 __device__ void thr_runs_segment(const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t s, uint32_t lo,
-                                 uint32_t hi, uint32_t res, int64_t IM, RunLds& L) {
+                                 uint32_t hi, uint32_t res, double M, bool wrapsafe, RunLds& L) {
+    const int64_t IM = (int64_t)floor(M);
     const int lane = (int)(threadIdx.x & 63);
     const uint32_t rb = hc.seg_rb[s], nr = hc.seg_re[s] - rb;
     // runs alternate kinds: run k holds entries iff (k & 1) == e0
@@ -841,14 +855,16 @@ __device__ void thr_runs_segment(const DevState& st, const SegIO& io, const Heav
 #endif
                 continue;
             }
-            int64_t R = IM - T;
+            int64_t R = wrapsafe ? IM - T : 1;           // (exact path: every entry is tried)
 #ifdef SF_STREAM_PROF
             if (R > 0) pf[4]++;
 #endif
             // one group of 64 entries from g: passes, their exits' run counters, pass bits
             auto group = [&](uint2 rc, uint32_t g) {
                 const bool valid = g + (uint32_t)lane < e;
-                const unsigned long long pm = thr_group_passes(valid, (int32_t)rc.y, R);
+                unsigned long long pm;
+                if (wrapsafe) pm = thr_group_passes(valid, (int32_t)rc.y, R);
+                else pm = thr_group_passes_exact(valid, (int32_t)rc.y, T, M);   // (T + acquireCount may wrap)
 #ifdef SF_STREAM_PROF
                 pf[5]++;
 #endif
@@ -915,18 +931,16 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
     // the deciding wave is the serial chain: it wins issue arbitration on its
     // SIMD against the memory-bound waves of the concurrent kernels
     if (wave0) __builtin_amdgcn_s_setprio(3);
-    bool runs = false;
     if (hc.seg_mode[s] == SM_THREAD && thr_run_mode(hc, s, lo, hi, hc.segflag[s])) {
-        // (the run walk compares T + acquireCount with floor(count) in 64 bits:
-        // exact while no int wrap can occur, i.e. T stays far from the int range)
+        // (the run walk compares T + acquireCount with floor(count) in 64 bits,
+        // exact while no int wrap can occur: T far from the int range; else
+        // entry by entry in Java's int arithmetic)
         const int64_t T0 = st.threads[res], span = (int64_t)(hi - lo);
-        runs = T0 >= (int64_t)INT32_MIN + span && T0 + (int64_t)THR_CBIG + span <= (int64_t)INT32_MAX;
-    }
-    if (runs) {
+        const bool wrapsafe = T0 >= (int64_t)INT32_MIN + span && T0 + (int64_t)THR_CBIG + span <= (int64_t)INT32_MAX;
         RunLds& RL = *reinterpret_cast<RunLds*>(smem);
         for (uint32_t i = threadIdx.x; i < RUN_RC; i += HS_T) RL.cnt[i] = 0u;
         __syncthreads();
-        if (wave0) thr_runs_segment(st, io, hc, s, lo, hi, res, (int64_t)floor(rule.count), RL);
+        if (wave0) thr_runs_segment(st, io, hc, s, lo, hi, res, rule.count, wrapsafe, RL);
     } else if (hc.seg_mode[s] == SM_THREAD) {
         ThrLds& L = *reinterpret_cast<ThrLds*>(smem);
         for (uint32_t i = threadIdx.x; i < LX_WORDS; i += HS_T) L.lx[i] = 0ull;
