@@ -734,9 +734,6 @@ static_assert(sizeof(RunLds) <= sizeof(unsigned long long) * (size_t)HS_SMEM_WOR
 // passes of one group of 64 entries (valid lanes) with room R > 0; R is lowered
 __device__ __forceinline__ unsigned long long thr_group_passes(bool valid, int32_t c, int64_t& R) {
     const int lane = (int)(threadIdx.x & 63);
-#ifdef SF_EXP_SIMPLE
-    { const unsigned long long vm0 = __ballot(valid && lane < R); R = 0; return vm0; }
-#endif
     const unsigned long long below = (1ull << lane) - 1ull;
     const unsigned long long vm = __ballot(valid);
     const unsigned long long big = __ballot(valid && c > 1);
@@ -772,7 +769,7 @@ __device__ __forceinline__ unsigned long long thr_group_passes(bool valid, int32
 
 // the same with Java's int arithmetic, entry by entry: (int)(T + c) <= count
 // (DefaultController.canPass); only when T may leave the int range
-__device__ __noinline__ unsigned long long thr_group_passes_exact(bool valid, int32_t c, int64_t T, double M) {
+__device__ __forceinline__ unsigned long long thr_group_passes_exact(bool valid, int32_t c, int64_t T, double M) {
     unsigned long long vm = __ballot(valid), pm = 0;
     while (vm) {
         const int z = __ffsll((long long)vm) - 1;
@@ -783,8 +780,10 @@ __device__ __noinline__ unsigned long long thr_group_passes_exact(bool valid, in
     return pm;
 }
 
+template <bool EXACT>
 __device__ void thr_runs_segment(const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t s, uint32_t lo,
-                                 uint32_t hi, uint32_t res, double M, bool wrapsafe, RunLds& L) {
+                                 uint32_t hi, uint32_t res, double M, RunLds& L) {
+    constexpr bool wrapsafe = !EXACT;
     const int64_t IM = (int64_t)floor(M);
     const int lane = (int)(threadIdx.x & 63);
     const uint32_t rb = hc.seg_rb[s], nr = hc.seg_re[s] - rb;
@@ -846,8 +845,8 @@ __device__ void thr_runs_segment(const DevState& st, const SegIO& io, const Heav
             if ((k & 1u) != e0) {
                 // exits: release the live ones (marked by earlier passes, or from before the batch)
                 const uint32_t slot = r % RUN_RC;
-                const uint32_t nl = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.cnt[slot]) +
-                                    (uint32_t)__builtin_amdgcn_readlane((int)p0, (int)k);
+                const uint32_t cl = (uint32_t)__builtin_amdgcn_readfirstlane((int)L.cnt[slot]);
+                const uint32_t nl = cl + (uint32_t)__builtin_amdgcn_readlane((int)p0, (int)k);
                 if (lane == 0) L.cnt[slot] = 0u;
                 T -= (int64_t)nl;
 #ifdef SF_STREAM_PROF
@@ -863,7 +862,7 @@ __device__ void thr_runs_segment(const DevState& st, const SegIO& io, const Heav
             auto group = [&](uint2 rc, uint32_t g) {
                 const bool valid = g + (uint32_t)lane < e;
                 unsigned long long pm;
-                if (wrapsafe) pm = thr_group_passes(valid, (int32_t)rc.y, R);
+                if constexpr (!EXACT) pm = thr_group_passes(valid, (int32_t)rc.y, R);
                 else pm = thr_group_passes_exact(valid, (int32_t)rc.y, T, M);   // (T + acquireCount may wrap)
 #ifdef SF_STREAM_PROF
                 pf[5]++;
@@ -872,20 +871,16 @@ __device__ void thr_runs_segment(const DevState& st, const SegIO& io, const Heav
                 T += __popcll(pm);
                 const bool mk = ((pm >> lane) & 1ull) && rc.x != XO_NONE;
                 bool fm = false;
-#ifndef SF_EXP_NOMARK
                 if (mk) {
                     if (rc.x - r < RUN_RC - 1) atomicAdd(&L.cnt[rc.x % RUN_RC], 1u);
                     else { atomicAdd(hc.run_pre + rc.x, 1u); fm = true; }
                 }
-#endif
                 far |= __ballot(fm) != 0ull;
                 const uint32_t sh = g & 63;
-#ifndef SF_EXP_NOPB
                 if (lane == 0) atomicOr(pbits + (g >> 6), pm << sh);
                 if (lane == 1 && sh) atomicOr(pbits + (g >> 6) + 1, pm >> (64 - sh));
-#endif
             };
-            if (R > 0) group(L.stage[buf][k >> 1][lane], a);           // the staged first group
+            if (R > 0) group(L.stage[buf][k >> 1][lane], a);            // the staged first group
             // more room than the first group used: the rest of the run from HBM,
             // THR_RG groups per round with all their loads in flight
             for (uint32_t g = a + 64; g < e && R > 0; g += 64 * THR_RG) {
@@ -940,7 +935,10 @@ __device__ void stream_segment(const DevState& st, const SegIO& io, const HeavyC
         RunLds& RL = *reinterpret_cast<RunLds*>(smem);
         for (uint32_t i = threadIdx.x; i < RUN_RC; i += HS_T) RL.cnt[i] = 0u;
         __syncthreads();
-        if (wave0) thr_runs_segment(st, io, hc, s, lo, hi, res, rule.count, wrapsafe, RL);
+        if (wave0) {
+            if (wrapsafe) thr_runs_segment<false>(st, io, hc, s, lo, hi, res, rule.count, RL);
+            else thr_runs_segment<true>(st, io, hc, s, lo, hi, res, rule.count, RL);
+        }
     } else if (hc.seg_mode[s] == SM_THREAD) {
         ThrLds& L = *reinterpret_cast<ThrLds*>(smem);
         for (uint32_t i = threadIdx.x; i < LX_WORDS; i += HS_T) L.lx[i] = 0ull;
