@@ -295,13 +295,15 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     e->cfg = c;
     e->R = c.max_resources;
     while ((1ull << e->key_bits) < e->R) e->key_bits++;
-    HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
-    {   // stream C carries k_heavy_stream (the serial chains): its workgroups are
-        // dispatched ahead of the light lanes' when CU slots free up
+    {   // stream priorities of the decide phase (SF_STREAM_PRIO, diagnostics):
+        // 0 = the light lanes' stream C first, 1 = stream A (THREAD / RL chains) first
         int least = 0, greatest = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(&e->stream3, hipStreamNonBlocking, greatest));
+        const char* pv = getenv("SF_STREAM_PRIO");
+        const bool a_first = pv && pv[0] == '1';
+        HIP_TRY(hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, a_first ? greatest : least));
+        HIP_TRY(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithPriority(&e->stream3, hipStreamNonBlocking, a_first ? least : greatest));
     }
     HIP_TRY(hipStreamCreateWithFlags(&e->sstream, hipStreamNonBlocking));
     if (const char* v = getenv("SF_SERIAL_STREAMS")) e->serial = v[0] == '1';

@@ -731,39 +731,42 @@ struct RunLds {
 };
 static_assert(sizeof(RunLds) <= sizeof(unsigned long long) * (size_t)HS_SMEM_WORDS, "run mode LDS");
 
-// passes of one group of 64 entries (valid lanes) with room R > 0; R is lowered
+// passes of one group of 64 entries (valid lanes) with room R > 0; R is lowered.
+// The greedy walk runs on wave-uniform masks (scalar unit): every entry of
+// acquireCount 1 before the next larger count passes while room is left; a
+// larger count passes iff it fits.
 __device__ __forceinline__ unsigned long long thr_group_passes(bool valid, int32_t c, int64_t& R) {
     const int lane = (int)(threadIdx.x & 63);
-    const unsigned long long below = (1ull << lane) - 1ull;
     const unsigned long long vm = __ballot(valid);
     const unsigned long long big = __ballot(valid && c > 1);
-    const unsigned long long ones = vm & ~big;
+    const int nv = __popcll(vm);
     // every entry fits even after all earlier ones of the group passed
-    if (!__ballot(valid && c > THR_CSMALL) && R >= (int64_t)__popcll(vm) - 1 + (big ? THR_CSMALL : 1)) {
-        R -= __popcll(vm);
+    if (!__ballot(valid && c > THR_CSMALL) && R >= (int64_t)nv - 1 + (big ? THR_CSMALL : 1)) {
+        R -= nv;
         return vm;
     }
-    unsigned long long pm = 0;
-    int from = 0;
-    while (true) {
-        const unsigned long long fr = from < 64 ? ~0ull << from : 0ull;
-        const unsigned long long bz = big & fr;
+    const int r0 = __builtin_amdgcn_readfirstlane((int)(R < (1 << 30) ? R : (1 << 30)));
+    int r = r0;
+    const unsigned long long ones = vm & ~big;
+    unsigned long long pm = 0, rest = vm;                  // entries not yet visited
+    while (r > 0 && rest) {
+        const unsigned long long bz = big & rest;
         const int z = bz ? __ffsll((long long)bz) - 1 : 64;
-        const unsigned long long m1 = ones & fr & (z < 64 ? (1ull << z) - 1ull : ~0ull);
+        const unsigned long long m1 = ones & rest & (z < 64 ? (1ull << z) - 1ull : ~0ull);
         const int n1 = __popcll(m1);
-        if ((int64_t)n1 >= R) {                    // the first R of them pass, then no room
-            const int rank = __popcll(m1 & below);
-            pm |= __ballot(((m1 >> lane) & 1ull) && (int64_t)rank < R);
-            R = 0;
+        if (n1 >= r) {                                     // the first r of them pass, then no room
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+            pm |= __ballot(((m1 >> lane) & 1ull) && (int)below < r);
+            r = 0;
             break;
         }
-        pm |= m1; R -= n1;
+        pm |= m1; r -= n1;
         if (z == 64) break;
-        if ((int64_t)__builtin_amdgcn_readlane(c, z) <= R) { pm |= 1ull << z; R -= 1; }
-        from = z + 1;
-        if (R == 0) break;
+        if (__builtin_amdgcn_readlane(c, z) <= r) { pm |= 1ull << z; r -= 1; }
+        rest = z < 63 ? rest & (~0ull << (z + 1)) : 0ull;
     }
-    R = uniform64(R);
+    R -= (int64_t)(r0 - r);
     return pm;
 }
 
