@@ -501,6 +501,14 @@ int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
                                e->stream));
     }
     e->n_flow = (uint32_t)valid.size();
+    {   // which segment classes the rules allow (launches of absent classes are skipped)
+        uint32_t ns = 0, nw = 0;
+        for (const DevRule& r : dr) {
+            if (r.kind == CT_RATE_LIMITER || (r.kind == CT_DEFAULT && r.grade == SF_GRADE_THREAD)) ns++;
+            if ((r.kind == CT_DEFAULT && r.grade == SF_GRADE_QPS) || r.kind == CT_WARM_UP) nw++;
+        }
+        e->st.n_stream_rules = ns; e->st.n_window_rules = nw;
+    }
     if (e->st.rules) { hipFree((void*)e->st.rules); e->st.rules = nullptr; }
     if (e->st.rstate) { hipFree(e->st.rstate); e->st.rstate = nullptr; }
     HIP_TRY(hipMalloc((void**)&e->st.rules, std::max<size_t>(1, dr.size()) * sizeof(DevRule)));

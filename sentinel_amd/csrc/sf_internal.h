@@ -78,6 +78,8 @@ struct DevState {
     int64_t* threads;
     const uint32_t* rule_off;      // [R+1]
     const DevRule* rules;
+    uint32_t n_stream_rules;       // THREAD-grade / RateLimiter rules (0: no k_heavy_stream segment can exist)
+    uint32_t n_window_rules;       // QPS / WarmUp rules (0: no k_heavy_decide window segment, no acquireCount scan)
     DevRuleState* rstate;
     const uint32_t* prule_off;     // [R+1]
     uint32_t n_prule;              // ParamFlow rules loaded (0: no segment needs the ParamFlow routing flags)

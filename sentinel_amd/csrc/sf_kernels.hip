@@ -1143,14 +1143,14 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.keys_out, w.perm, w.s_ts, w.s_cnt,
                        w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan, w.seg_start, w.seg_res, w.n_seg,
                        w.segflag, st.last_ts, st.err, st.n_prule != 0);
-    hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);
+    if (b.eref || st.n_stream_rules) hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);   // (read by k_gather_exit, k_thr_rec)
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags,
                            w.head_scan, w.seg_start, w.s_eref, w.s_cts, w.exit_of, st.err);
     hipMemsetAsync(w.counters, 0, 10 * sizeof(uint32_t), s);
     hipMemsetAsync(w.lcounts, 0, 2 * LCLS * sizeof(uint32_t), s);
     hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
-    hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
+    if (st.n_stream_rules) hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
     const uint32_t max_seg = n < st.R ? n : st.R;
     if (timing) hipEventRecord(ev[10], s);
     hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, 1024)), dim3(1024), 0, s, st, w, w.s_ts);
@@ -1361,13 +1361,15 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     if (out.wait) hipMemsetAsync(out.wait, 0, (size_t)n * sizeof(int32_t), s);
     if (out.rule) hipMemsetAsync(out.rule, 0, (size_t)n * sizeof(uint16_t), s);
     hipEventRecord(ev[5], s);                      // fork
-    launch_thr_prep(w, b, s);
+    // (the THREAD / RateLimiter class exists only with such rules loaded)
+    if (st.n_stream_rules) launch_thr_prep(w, b, s);
     hipEventRecord(ev[11], s);
-    hipLaunchKernelGGL(k_heavy_stream, dim3(std::min(max_heavy, w.stream_grid)), dim3(HS_T), 0, s, st, io, hc, sc);
+    if (st.n_stream_rules)
+        hipLaunchKernelGGL(k_heavy_stream, dim3(std::min(max_heavy, w.stream_grid)), dim3(HS_T), 0, s, st, io, hc, sc);
     hipEventRecord(ev[12], s);
     hipStreamWaitEvent(s2, ev[5], 0);
     hipStreamWaitEvent(s3, ev[5], 0);
-    {
+    if (st.n_window_rules) {
         // acquireCount prefix of the entries (QPS / WarmUp window budgets, k_heavy_decide
         // only): state-independent, but here on stream B rather than in the sort phase,
         // the longer of the two pipelined phases
@@ -1386,9 +1388,12 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     hipLaunchKernelGGL(k_heavy_fill, dim3(fgrid), dim3(256), 0, s2, st, io, hc, w.fill_tiles, w.fill_ntiles, 0);
     if (timing) hipEventRecord(ev[8], s2);
     hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s2, st, hc, sc, w.seg_nhw, w.seg_nsec, 0);
-    hipLaunchKernelGGL(k_heavy_fill, dim3(fgrid), dim3(256), 0, s, st, io, hc,
-                       w.fill_tiles + w.fill_tile_cap, w.fill_ntiles, 1);
-    hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s, st, hc, sc, w.seg_nhw, w.seg_nsec, 1);
+    if (st.n_stream_rules) {
+        hipLaunchKernelGGL(k_heavy_fill, dim3(fgrid), dim3(256), 0, s, st, io, hc,
+                           w.fill_tiles + w.fill_tile_cap, w.fill_ntiles, 1);
+        hipLaunchKernelGGL(k_heavy_apply, dim3(blocks(max_heavy, 64)), dim3(64), 0, s, st, hc, sc, w.seg_nhw,
+                           w.seg_nsec, 1);
+    }
 
     const unsigned TD = 128;
     LightLists ll{w.light_list, w.lcounts, {}, {}};
@@ -1396,19 +1401,23 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     if (st.S <= 2) {
         hipLaunchKernelGGL(k_decide_light<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
                            w.seg_res, ll);
-        hipLaunchKernelGGL(k_decide_light_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
-                           w.seg_res, ll);
-        hipLaunchKernelGGL(k_decide_short_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
-                           w.seg_res, ll, w.counters + 8);
+        if (st.n_window_rules) {   // (the lean QPS walk needs a QPS DefaultController rule)
+            hipLaunchKernelGGL(k_decide_light_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+                               w.seg_res, ll);
+            hipLaunchKernelGGL(k_decide_short_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+                               w.seg_res, ll, w.counters + 8);
+        }
         hipLaunchKernelGGL(k_decide_short<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
                            w.seg_res, ll, w.counters + 8);
     } else {
         hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, ll);
-        hipLaunchKernelGGL(k_decide_light_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st,
-                           io, w.seg_start, w.seg_res, ll);
-        hipLaunchKernelGGL(k_decide_short_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st,
-                           io, w.seg_start, w.seg_res, ll, w.counters + 8);
+        if (st.n_window_rules) {
+            hipLaunchKernelGGL(k_decide_light_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3,
+                               st, io, w.seg_start, w.seg_res, ll);
+            hipLaunchKernelGGL(k_decide_short_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3,
+                               st, io, w.seg_start, w.seg_res, ll, w.counters + 8);
+        }
         hipLaunchKernelGGL(k_decide_short<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, ll, w.counters + 8);
     }
