@@ -96,33 +96,32 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* keys, u
     const uint8_t f = (uint8_t)(v.meta >> 16);
     perm[j] = i;
     s_ts[j] = dts != PV_DTS_FAR ? b.ts[0] + (int64_t)dts : b.ts[i]; s_cnt[j] = c; s_flags[j] = f;
-    if (exit_marks) {
-        // the segment has exits (read only by the ParamFlow routing, heavy_mode):
-        // one atomic per segment and wavefront, by the segment's first exit lane
-        const bool ex = (f & SF_EV_EXIT) != 0;
-        const int lane = (int)(threadIdx.x & 63);
-        const int psid = __shfl_up((int)sid, 1);
-        const unsigned long long heads = __ballot(lane == 0 || (uint32_t)psid != sid);
-        const unsigned long long em = __ballot(ex);
-        const unsigned long long below = (1ull << lane) - 1ull;
-        const int sl = 63 - __builtin_clzll(heads & (below | (1ull << lane)));   // this segment's first lane
-        if (ex && !(em & below & ~((1ull << sl) - 1ull))) atomicOr(&segflag[sid], SEGF_EXIT);
-    }
-    if (b.origin) {
-        // an event with an origin updates its origin node (ClusterBuilderSlot.java:107-110):
-        // the segment goes to the xflow walk; one atomic per segment and wavefront
-        const bool og = b.origin[i] != SF_ORIGIN_NONE;
-        const int lane = (int)(threadIdx.x & 63);
-        const int psid = __shfl_up((int)sid, 1);
-        const unsigned long long heads = __ballot(lane == 0 || (uint32_t)psid != sid);
-        const unsigned long long om = __ballot(og);
-        const unsigned long long below = (1ull << lane) - 1ull;
-        const int sl = 63 - __builtin_clzll(heads & (below | (1ull << lane)));
-        if (og && !(om & below & ~((1ull << sl) - 1ull))) atomicOr(&segflag[sid], SEGF_ORIGIN);
-    }
-    if (!(f & SF_EV_EXIT) && ((f & (SF_EV_PRIO | EVF_SYSBLK)) || c <= 0)) {
-        atomicOr(&segflag[sid], ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) |
-                              ((f & EVF_SYSBLK) ? SEGF_SYS : 0u));
+    // segment flags (k_classify's routing): the exits (read only by the ParamFlow
+    // routing, heavy_mode), origins (ClusterBuilderSlot.java:107-110: the xflow
+    // walk), prioritized / non-positive / blocked-before entries; OR-ed per
+    // segment within the wavefront, one atomic per segment and wavefront
+    {
+        uint32_t mine = 0;
+        if (exit_marks && (f & SF_EV_EXIT)) mine |= SEGF_EXIT;
+        if (b.origin && b.origin[i] != SF_ORIGIN_NONE) mine |= SEGF_ORIGIN;
+        if (!(f & SF_EV_EXIT))
+            mine |= ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) | ((f & EVF_SYSBLK) ? SEGF_SYS : 0u);
+        const unsigned long long any = __ballot(mine != 0);
+        if (any) {
+            const int lane = (int)(threadIdx.x & 63);
+            const int psid = __shfl_up((int)sid, 1);
+            const unsigned long long heads = __ballot(lane == 0 || (uint32_t)psid != sid);
+            const unsigned long long below = (1ull << lane) - 1ull;
+            const unsigned long long after = heads & ~(below | (1ull << lane));
+            const int nxt = after ? __ffsll((long long)after) - 1 : 64;
+            const unsigned long long range = (nxt == 64 ? ~0ull : (1ull << nxt) - 1ull) & ~below;
+            uint32_t acc = 0;
+            const uint32_t kinds[5] = {SEGF_EXIT, SEGF_ORIGIN, SEGF_PRIO, SEGF_NONPOS, SEGF_SYS};
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                if (__ballot(mine & kinds[k]) & range) acc |= kinds[k];
+            if (((heads >> lane) & 1ull) && acc) atomicOr(&segflag[sid], acc);
+        }
     }
     if (b.arg_slots) {
         if (b.nargs) s_nargs[j] = b.nargs[i];
