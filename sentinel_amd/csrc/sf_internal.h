@@ -214,7 +214,10 @@ struct Work {
 };
 // verdict scatter (sorted order -> submission order, launch_scatter): regions of
 // 2^VS_REG verdicts are assembled in LDS; its first pass has at most 256 buckets
-constexpr uint32_t VS_REG = 14;
+#ifndef SF_VS_REG
+#define SF_VS_REG 14
+#endif
+constexpr uint32_t VS_REG = SF_VS_REG;
 inline size_t VS_CURSORS(size_t N) { return 256 + (N >> VS_REG) + 1024 + 16; }
 
 // Device view of a caller batch (pointers already on device).
