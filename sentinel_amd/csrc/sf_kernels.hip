@@ -1229,15 +1229,18 @@ __global__ void __launch_bounds__(VS_T) k_vs_bucket(const uint32_t* perm, const 
     const uint32_t per = (nk + VS_T - 1) / VS_T;
     uint32_t sum = 0;
     for (uint32_t q = 0; q < per; q++) { const uint32_t k = tid * per + q; if (k < nk) sum += hist[k]; }
-    part[tid] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < VS_T; d <<= 1) {
-        const uint32_t v = tid >= d ? part[tid - d] : 0u;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
+    // (wavefront scans, then the wavefronts' totals: one barrier)
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    uint32_t incl = sum;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
     }
-    uint32_t run = part[tid] - sum;
+    if (lane == 63u) part[wv] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (uint32_t q = 0; q < wv; q++) run += part[q];
     for (uint32_t q = 0; q < per; q++) {
         const uint32_t k = tid * per + q;
         if (k >= nk) break;
