@@ -1253,7 +1253,7 @@ __global__ void __launch_bounds__(VS_T) k_vs_bucket(const uint32_t* perm, const 
             const uint64_t first = FIRST ? ((uint64_t)k << s1) : (((uint64_t)bb * nk + k) << VS_REG);
             const uint64_t cap = min((uint64_t)(FIRST ? (1ull << s1) : (1ull << VS_REG)), (uint64_t)n - min((uint64_t)n, first));
             if ((uint64_t)g + h > cap) *err = SF_ERR_INVALID;
-            gbase[k] = g;
+            gbase[k] = (uint32_t)first + g - lbase[k];       // destination of the tile's k-th record, minus k
         }
     }
     __syncthreads();
@@ -1265,9 +1265,7 @@ __global__ void __launch_bounds__(VS_T) k_vs_bucket(const uint32_t* perm, const 
         }
     __syncthreads();
     for (uint32_t k = tid; k < hi - lo; k += VS_T) {
-        const uint32_t key = kb[k];
-        const uint64_t first = FIRST ? ((uint64_t)key << s1) : (((uint64_t)bb * nk + key) << VS_REG);
-        const uint64_t dst = first + gbase[key] + (k - lbase[key]);
+        const uint32_t dst = gbase[kb[k]] + k;              // (a broken permutation: flagged above, kept in bounds)
         if (dst < n) out[dst] = buf[k];
     }
 }
