@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--no-metric-log", action="store_true")
     ap.add_argument("--no-degrade", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the config2 / config4 / config5 / end-to-end legs")
+    ap.add_argument("--legs", default="", help="comma-separated subset of the legs to run (default: all)")
     ap.add_argument("--heavy-min", type=int, default=0,
                     help="segments of more events than this go to the heavy kernels (0: the engine default, 512)")
     args = ap.parse_args()
@@ -280,8 +281,13 @@ def main():
             b.free()
         batches = batches[:1]
         # (after the oracle leg: e2e advances this engine's state)
+        c3_ms = wall / args.steps * 1e3
         for nm, fn in (("e2e_pinned", lambda: e2e_leg(eng, hb, steps * DURATION_MS)),
+                       ("config3_origin", lambda: config3_origin_leg(hb, rules, R_local, c3_ms, eng,
+                                                                       parity=not args.no_cpu)),
                        ("config2", config2_leg), ("config4", config4_leg), ("config5", config5_leg)):
+            if args.legs and nm not in args.legs.split(","):
+                continue
             try:
                 t_leg = time.perf_counter()
                 log(f"[leg {nm}] ...")
@@ -363,6 +369,135 @@ def node_trace(R_total, n, world, rank, dist):
     er = er[mo]
     er = np.where(er >= 0, newpos[np.clip(er, 0, None)], -1)
     return abi.HostBatch(res[mo], ts[mo], cnt[mo], fl[mo], entry_ref=er)
+
+
+def config3_origin_leg(hb, rules, R, c3_ms, main_eng, steps=5, warmup=2, parity=True, n_origins=64):
+    """Config 3 with a caller origin on every entry (ContextUtil.enter(name,
+    origin)): one of 64 names drawn Zipf(1.1), exits carrying their entry's
+    (trace.with_origins).  ClusterBuilderSlot creates the origin node of every
+    entry with an origin (ClusterBuilderSlot.java:107-110), so every event also
+    updates its (resource, origin) node.  Two variants, each on a fresh engine
+    with HBM-resident batches pipelined like the headline run:
+    ``no_origin_rules`` (the config-3 rules: the origin-node pass after the
+    verdicts, sf_origin.hip) and ``other_rules_1pct`` (a limitApp "other" QPS
+    rule added on 1 % of the resources, chosen by hash: those resources read
+    origin nodes and run on the xflow walk).  ms/step is compared with the
+    headline config-3 step of the same run.  Parity: every verdict of batch 0
+    and of the last timed batch, and a sample of origin nodes (every origin of
+    the 16 busiest resources, 512 random pairs), ClusterNodes and ENTRY_NODE
+    after batch 0 and after the last batch, against the resource-sharded
+    oracle replaying the same batches."""
+    t0 = time.time()
+    ho = trace.with_origins(hb, n_origins=n_origins, seed=13)
+    log(f"[leg config3_origin] origins drawn in {time.time() - t0:.1f}s")
+    res_local = ho.res_id
+    per_res = np.bincount(res_local, minlength=R)
+    key = res_local.astype(np.uint64) << np.uint64(32) | ho.origin.astype(np.uint64)
+    busiest = np.argsort(-per_res)[:16]
+    rng = np.random.default_rng(17)
+    pick = rng.choice(ho.n, size=512, replace=False)
+    bsel = np.isin(res_local, busiest)
+    pairs = np.unique(np.concatenate([np.unique(key[bsel]), key[pick]]))
+    pairs = [(int(k >> np.uint64(32)), int(k & np.uint64(0xffffffff))) for k in pairs]
+    n_pairs = int(np.unique(key).size)
+    del key
+    node_sample = np.unique(np.concatenate([busiest, rng.choice(np.nonzero(per_res)[0], 256, replace=False)]))
+    out = {"what": "config3 + a Zipf(1.1) origin out of 64 on every entry (origin nodes, ClusterBuilderSlot.java:107-110)",
+           "events": int(ho.n), "distinct_pairs": n_pairs, "config3_ms_per_step": round(c3_ms, 3)}
+    h = ((np.arange(R, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(40)) % np.uint64(100)
+    xres = np.nonzero(h == 7)[0].astype(np.uint32)
+    other = np.zeros(xres.size, abi.FLOW_RULE_DTYPE)
+    other["resource"] = xres
+    other["grade"] = abi.GRADE_QPS
+    other["count"] = (20 + (xres % 200)).astype(np.float64)
+    other["limit_app"] = abi.APP_OTHER
+    other["warm_up_period_sec"] = 10
+    other["max_queueing_time_ms"] = 500
+    both = np.concatenate([rules, other])
+    both = both[np.argsort(both["resource"], kind="stable")]    # per resource: the config-3 rule, then "other"
+    variants = (("no_origin_rules", rules), ("other_rules_1pct", both))
+    main_eng.sync()
+    for name, rl in variants:
+        e = engine.FlowEngine(abi.default_config(max_resources=R, max_batch=ho.n))
+        res = {"rules": int(len(rl))}
+        try:
+            e.load_flow_rules(rl)
+            base = engine.DeviceBatch(e, ho)
+            n_b = warmup + steps
+            bl = [base] + [engine.DeviceBatch.with_ts(e, base, ho.ts_ms + k * DURATION_MS) for k in range(1, n_b)]
+            out0 = engine.DeviceVerdicts(e, ho.n, with_wait=True, with_rule=True)
+            outv = engine.DeviceVerdicts(e, ho.n, with_wait=True, with_rule=True)
+            t = time.perf_counter()
+            e.submit_device_async(bl[0], out0)
+            e.sync()
+            res["batch0_ms"] = round((time.perf_counter() - t) * 1e3, 2)
+            gpu0 = {"origin": [abi.node_state_to_dict(e.read_origin_node(r, o)) for r, o in pairs],
+                    "nodes": [abi.node_state_to_dict(e.read_node(int(r))) for r in node_sample],
+                    "entry": abi.node_state_to_dict(e.read_entry_node())}
+            for k in range(1, warmup):
+                e.submit_device_async(bl[k], outv)
+            e.sync()
+            e.set_timing(True)
+            t = time.perf_counter()
+            for k in range(warmup, n_b):
+                e.submit_device_async(bl[k], outv)
+            e.sync()
+            ms = (time.perf_counter() - t) / steps * 1e3
+            st = e.stats()
+            res.update({"ms_per_step": round(ms, 3), "vs_config3": round(ms / c3_ms, 3),
+                        "decisions_per_s": round(int(((ho.flags & abi.EV_EXIT) == 0).sum()) / (ms / 1e3), 1),
+                        "origin_nodes": int(st.aux_nodes), "pool_capacity": int(st.aux_capacity),
+                        "index_grows": int(st.aux_index_grows)})
+            log(f"[leg config3_origin] {name}: {ms:.2f} ms/step ({ms / c3_ms:.2f}x config 3), "
+                f"{st.aux_nodes} origin nodes")
+            g0 = (out0.status.numpy(), out0.wait_ms.numpy(), out0.rule_idx.numpy())
+            gl = (outv.status.numpy(), outv.wait_ms.numpy())
+            gpu1 = {"origin": [abi.node_state_to_dict(e.read_origin_node(r, o)) for r, o in pairs],
+                    "nodes": [abi.node_state_to_dict(e.read_node(int(r))) for r in node_sample],
+                    "entry": abi.node_state_to_dict(e.read_entry_node())}
+            for b in bl:
+                b.free()
+            out0.free(); outv.free()
+        finally:
+            e.close()
+        if parity:
+            try:
+                from oracle import sharded
+                from sentinel_amd import dist as sdist
+                T = max(1, min(16, len(os.sched_getaffinity(0))))
+                sh = sharded.ShardedOracle(rl, R, T, ho.n)
+                sh.split_like(ho)
+                v, dt = sh.submit(ho)
+                blk = np.isin(v.status, [abi.V_BLOCK_FLOW, abi.V_BLOCK_PARAM, abi.V_BLOCK_SYSTEM])
+                mm = {"status": int((g0[0] != v.status).sum()), "wait_ms": int((g0[1] != v.wait_ms).sum()),
+                      "rule_idx_of_blocks": int((g0[2][blk] != v.rule_idx[blk]).sum()),
+                      "origin_nodes": sum(a != abi.node_state_to_dict(sh.read_origin_node(r, o))
+                                          for a, (r, o) in zip(gpu0["origin"], pairs)),
+                      "nodes": sum(a != abi.node_state_to_dict(sh.read_node(int(r)))
+                                   for a, r in zip(gpu0["nodes"], node_sample)),
+                      "entry_node": int(gpu0["entry"] != abi.node_state_to_dict(
+                          sdist.merge_entry_nodes(sh.entry_nodes())))}
+                res["cpu_baseline"] = {"value": round(int(((ho.flags & abi.EV_EXIT) == 0).sum()) / dt, 1),
+                                       "unit": "decisions/s", "cores": T, "kind": "port",
+                                       "sample": "batch 0, resource-sharded C oracle with origin nodes"}
+                for k in range(1, warmup + steps):
+                    v, _ = sh.submit(ho, k * DURATION_MS)
+                mm_last = {"status": int((gl[0] != v.status).sum()), "wait_ms": int((gl[1] != v.wait_ms).sum()),
+                           "origin_nodes": sum(a != abi.node_state_to_dict(sh.read_origin_node(r, o))
+                                               for a, (r, o) in zip(gpu1["origin"], pairs)),
+                           "nodes": sum(a != abi.node_state_to_dict(sh.read_node(int(r)))
+                                        for a, r in zip(gpu1["nodes"], node_sample)),
+                           "entry_node": int(gpu1["entry"] != abi.node_state_to_dict(
+                               sdist.merge_entry_nodes(sh.entry_nodes())))}
+                sh.close()
+                res["parity"] = {"what": f"batch 0 and batch {warmup + steps - 1} (every verdict; {len(pairs)} origin "
+                                         f"nodes, {node_sample.size} ClusterNodes, ENTRY_NODE) vs the "
+                                         f"resource-sharded oracle", "batch0": mm, "last": mm_last,
+                                 "exact": all(x == 0 for x in mm.values()) and all(x == 0 for x in mm_last.values())}
+            except Exception as ex:  # pragma: no cover
+                res["parity"] = {"error": str(ex)[:200]}
+        out[name] = res
+    return out
 
 
 def config2_leg(R=1_000_000, n=1 << 27, steps=3, parity=1):

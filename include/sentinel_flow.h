@@ -376,6 +376,9 @@ typedef struct sf_stats {         /* device-clock timings, summed over sf_submit
     double   metric_log_ms;       /* last sf_metric_log: all its kernels, before the copy to the host */
     double   wire_ms;             /* last sf_serve_frames: device time from framing to encoded responses (host syncs included) */
     uint64_t sys_rounds;          /* SystemRule sub-batches (planner rounds) over the sf_submit calls */
+    uint64_t aux_nodes;           /* origin / context nodes kept (pool slots in use) */
+    uint64_t aux_capacity;        /* pool slots backed by device memory (grows by chunks between batches) */
+    uint64_t aux_index_grows;     /* times the pool's index table was rebuilt larger */
 } sf_stats;
 
 typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last sf_submit */

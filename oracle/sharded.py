@@ -33,7 +33,9 @@ def split(hb: abi.HostBatch, T: int):
             r = hb.entry_ref[idx]
             eref = np.where(r >= 0, pos[np.clip(r, 0, None)], r).astype(np.int64)
         b = abi.HostBatch((res[idx] // T).astype(np.uint32), hb.ts_ms[idx], hb.count[idx], hb.flags[idx],
-                          entry_ref=eref, create_ts=None if hb.create_ts is None else hb.create_ts[idx])
+                          entry_ref=eref, create_ts=None if hb.create_ts is None else hb.create_ts[idx],
+                          origin=None if hb.origin is None else hb.origin[idx],
+                          context=None if hb.context is None else hb.context[idx])
         out.append((idx, b))
     return out
 
@@ -125,7 +127,8 @@ class ShardedOracle:
             idx, b = self.parts[k]
             if ts_shift:
                 b = abi.HostBatch(b.res_id, b.ts_ms + ts_shift, b.count, b.flags, entry_ref=b.entry_ref,
-                                  create_ts=None if b.create_ts is None else b.create_ts + ts_shift)
+                                  create_ts=None if b.create_ts is None else b.create_ts + ts_shift,
+                                  origin=b.origin, context=b.context)
             outs[k] = self.engines[k].submit(b)
 
         ths = [threading.Thread(target=run, args=(k,)) for k in range(self.T)]
@@ -145,6 +148,9 @@ class ShardedOracle:
 
     def read_node(self, res: int):
         return self.engines[res % self.T].read_node(res // self.T)
+
+    def read_origin_node(self, res: int, origin: int):
+        return self.engines[res % self.T].read_origin_node(res // self.T, origin)
 
     def read_rule_state(self, res_rule: int):
         """Rule state of the resource's single rule (one rule per resource)."""

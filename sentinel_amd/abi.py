@@ -197,7 +197,8 @@ class sf_stats(C.Structure):
                 ("n_launches", C.c_uint64), ("light_ms", C.c_double), ("heavy_decide_ms", C.c_double),
                 ("heavy_fill_ms", C.c_double), ("classify_ms", C.c_double),
                 ("stream_ms", C.c_double), ("metric_scan_ms", C.c_double), ("metric_log_ms", C.c_double),
-                ("wire_ms", C.c_double), ("sys_rounds", C.c_uint64)]
+                ("wire_ms", C.c_double), ("sys_rounds", C.c_uint64), ("aux_nodes", C.c_uint64),
+                ("aux_capacity", C.c_uint64), ("aux_index_grows", C.c_uint64)]
 
 
 class sf_heavy_profile(C.Structure):

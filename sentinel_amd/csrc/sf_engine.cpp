@@ -110,6 +110,11 @@ struct sf_engine {
     void* dg_stage = nullptr; size_t dg_stage_bytes = 0;
     // xflow walk (sf_xflow.h): group keys and the origin / context node pool
     uint32_t* xmap_buf = nullptr;
+    // the pool's chunks (host mirror of the device directory st.ax_chunks) and
+    // the index table's growth (sf_origin.hip); counts for sf_stats
+    std::vector<AuxChunk> ax_host;
+    AuxChunk* ax_dir = nullptr;
+    uint64_t aux_grows = 0;
 };
 
 static void free_tok_work(TokWork& w) {
@@ -154,7 +159,8 @@ static void free_work(Work& w) {
                     w.pscan_tmp, w.fill_tiles, w.fill_ntiles, w.acc_hw,
                     w.acc_sec, w.acc_hw_base, w.acc_sec_base, w.seg_hw0, w.seg_sec0,
                     w.seg_nhw, w.seg_nsec, w.hticks, w.passbits, w.stream_list, w.sticks,
-                    w.exit_of, w.lxfar, w.thr_rec, w.vs_cursor, w.tile_rc, w.seg_rb, w.seg_re};
+                    w.exit_of, w.lxfar, w.thr_rec, w.vs_cursor, w.tile_rc, w.seg_rb, w.seg_re,
+                    w.s_origin, w.s_oslot, w.ox_cnt, w.ox_bflags, w.ox_hmap, w.ox_hslot, w.ox_thr, w.ox_acc};
     for (void* p : ptrs) if (p) hipFree(p);
     w = Work{};
 }
@@ -184,9 +190,9 @@ void sf_destroy(sf_engine* e) {
                      e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
                      e->dgw.err, e->dg_stage, e->dgw.heavy, e->dgw.n_heavy, e->dgw.sev, e->dgw.inv};
     for (void* p : dptrs) if (p) hipFree(p);
-    void* xptrs[] = {e->xmap_buf, e->st.xtab, e->st.ax_second, e->st.ax_borrow, e->st.ax_minute, e->st.ax_threads,
-                     e->st.ax_count};
+    void* xptrs[] = {e->xmap_buf, e->st.xtab, e->ax_dir, e->st.ax_count};
     for (void* p : xptrs) if (p) hipFree(p);
+    for (const AuxChunk& c : e->ax_host) hipFree(c.sec);          // (one allocation per chunk)
     if (e->comm) ncclCommDestroy(e->comm);
     free_tok_work(e->tw);
     for (auto& a : e->evs) for (auto& x : a) if (x) hipEventDestroy(x);
@@ -213,7 +219,8 @@ static int alloc_work(sf_engine* e, Work& w) {
     const sf_config& c = e->cfg;
     const size_t N = c.max_batch, R = e->R;
     WALLOC(w.keys_in, N * 4); WALLOC(w.keys_out, N * 4); WALLOC(w.perm, N * 4);
-    WALLOC(w.pv_in, N * sizeof(PackedEv)); WALLOC(w.pv_out, N * sizeof(PackedEv));
+    // (12-B payloads when the batch has origins)
+    WALLOC(w.pv_in, N * sizeof(PackedEvO)); WALLOC(w.pv_out, N * sizeof(PackedEvO));
     WALLOC(w.wide, 4); WALLOC(w.err, 4);
     WALLOC(w.head_scan, N * 4);
     WALLOC(w.seg_start, (N + 1) * 4); WALLOC(w.seg_res, N * 4); WALLOC(w.n_seg, 4);
@@ -269,6 +276,8 @@ static int alloc_work(sf_engine* e, Work& w) {
     WALLOC(w.thr_rec, N * 8);
     WALLOC(w.tile_rc, (size_t)w.fill_tile_cap * 4); WALLOC(w.seg_rb, SC * 4); WALLOC(w.seg_re, SC * 4);
     WALLOC(w.vs_cursor, VS_CURSORS(N) * 4);
+    WALLOC(w.s_origin, N * 4); WALLOC(w.s_oslot, N * 4); WALLOC(w.ox_cnt, 8 * 4);
+    WALLOC(w.ox_bflags, (N / OX_TILE + 1) * 4);
     return SF_OK;
 }
 
@@ -418,31 +427,161 @@ static int drain(sf_engine* e) {
     return SF_OK;
 }
 
-// The origin / context node pool and its index table (sf_xflow.h), allocated
-// with the first rule that reads such nodes; the nodes live as long as the
-// engine (ClusterNode.originCountMap / NodeSelectorSlot maps are never pruned).
+// The origin / context node pool and its index table (sf_xflow.h,
+// sf_origin.hip), allocated with the first batch with origins or the first
+// rule that reads such nodes; the nodes live as long as the engine
+// (ClusterNode.originCountMap / NodeSelectorSlot maps are never pruned).  The
+// pool grows by chunks of AX_CHUNK nodes (no node moves) and the index table
+// by rehashing into a larger one, both between batches, so that a batch never
+// fails on their capacity.
+static int pool_grow(sf_engine* e, uint64_t need) {
+    DevState& st = e->st;
+    const size_t S = st.S;
+    if ((uint64_t)st.ax_cap >= need) return SF_OK;
+    while ((uint64_t)st.ax_cap < need) {
+        if (e->ax_host.size() >= AX_MAX_CHUNKS) return fail(SF_ERR_CAPACITY, "origin / context node pool at its limit");
+        const size_t sec_b = (size_t)AX_CHUNK * S * sizeof(Bucket), bor_b = (size_t)AX_CHUNK * S * sizeof(Borrow);
+        const size_t min_b = (size_t)AX_CHUNK * MINUTE * sizeof(Bucket), thr_b = (size_t)AX_CHUNK * sizeof(int64_t);
+        char* m = nullptr;
+        HIP_TRY(hipMalloc((void**)&m, sec_b + bor_b + min_b + thr_b));
+        AuxChunk c{(Bucket*)m, (Borrow*)(m + sec_b), (Bucket*)(m + sec_b + bor_b), (int64_t*)(m + sec_b + bor_b + min_b)};
+        DevState pool = st;                    // fresh nodes: the resource-row initialiser on the chunk
+        pool.second = c.sec; pool.borrow = c.bor; pool.minute = c.min; pool.threads = c.thr; pool.R = AX_CHUNK;
+        const hipError_t le = launch_init_state(pool, e->stream);
+        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("aux init: ") + hipGetErrorString(le));
+        HIP_TRY(hipMemcpyAsync(e->ax_dir + e->ax_host.size(), &c, sizeof c, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        e->ax_host.push_back(c);
+        st.ax_cap += AX_CHUNK;
+    }
+    return SF_OK;
+}
+
 static int ensure_aux(sf_engine* e) {
     DevState& st = e->st;
-    if (st.ax_second) return SF_OK;
+    if (st.xtab) return SF_OK;
     const uint32_t cap = e->cfg.aux_capacity ? e->cfg.aux_capacity : 65536;
-    const size_t S = st.S;
     uint64_t tcap = 16;
     while (tcap < 2ull * cap) tcap <<= 1;
-    HIP_TRY(hipMalloc((void**)&st.ax_second, (size_t)cap * S * sizeof(Bucket)));
-    HIP_TRY(hipMalloc((void**)&st.ax_borrow, (size_t)cap * S * sizeof(Borrow)));
-    HIP_TRY(hipMalloc((void**)&st.ax_minute, (size_t)cap * MINUTE * sizeof(Bucket)));
-    HIP_TRY(hipMalloc((void**)&st.ax_threads, (size_t)cap * sizeof(int64_t)));
+    HIP_TRY(hipMalloc((void**)&e->ax_dir, AX_MAX_CHUNKS * sizeof(AuxChunk)));
     HIP_TRY(hipMalloc((void**)&st.ax_count, sizeof(uint32_t)));
     HIP_TRY(hipMalloc((void**)&st.xtab, tcap * sizeof(ParamSlot)));
     HIP_TRY(hipMemsetAsync(st.ax_count, 0, sizeof(uint32_t), e->stream));
     HIP_TRY(hipMemsetAsync(st.xtab, 0, tcap * sizeof(ParamSlot), e->stream));
     st.xcap_mask = tcap - 1;
-    st.ax_cap = cap;
-    DevState pool = st;                    // fresh nodes: the resource-row initialiser on the pool
-    pool.second = st.ax_second; pool.borrow = st.ax_borrow; pool.minute = st.ax_minute;
-    pool.threads = st.ax_threads; pool.R = cap;
-    const hipError_t le = launch_init_state(pool, e->stream);
-    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("aux init: ") + hipGetErrorString(le));
+    st.ax_chunks = e->ax_dir;
+    st.ax_cap = 0;
+    return pool_grow(e, cap);
+}
+
+// the index table rebuilt with room for `need` keys at half load (nothing in flight)
+static int index_grow(sf_engine* e, uint64_t need) {
+    DevState& st = e->st;
+    uint64_t tcap = (st.xcap_mask + 1) * 4;
+    while (tcap < 2 * need) tcap <<= 1;
+    ParamSlot* nt = nullptr;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMalloc((void**)&nt, tcap * sizeof(ParamSlot)));
+    HIP_TRY(hipMemsetAsync(nt, 0, tcap * sizeof(ParamSlot), e->stream));
+    const hipError_t le = launch_ox_rehash(st.xtab, st.xcap_mask + 1, nt, tcap - 1, st.err, e->stream);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("index rehash: ") + hipGetErrorString(le));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipFree(st.xtab));
+    st.xtab = nt;
+    st.xcap_mask = tcap - 1;
+    e->aux_grows++;
+    return SF_OK;
+}
+
+// per-Work-set maps of the origin pass sized for the index table (every pool
+// slot is below its capacity), the slot -> heavy id map reset to XNONE
+static int ox_maps(sf_engine* e, Work& w, bool reset, hipStream_t ss) {
+    const size_t need = (size_t)e->st.xcap_mask + 1;
+    if (w.ox_hmap_n < need) {
+        if (w.ox_hmap) hipFree(w.ox_hmap);
+        if (w.ox_hslot) hipFree(w.ox_hslot);
+        if (w.ox_thr) hipFree(w.ox_thr);
+        w.ox_hmap = nullptr; w.ox_hslot = nullptr; w.ox_thr = nullptr; w.ox_hmap_n = w.ox_hslot_n = 0;
+        HIP_TRY(hipMalloc((void**)&w.ox_hmap, need * 4));
+        HIP_TRY(hipMalloc((void**)&w.ox_hslot, need * 4));
+        HIP_TRY(hipMalloc((void**)&w.ox_thr, need * 8));
+        w.ox_hmap_n = w.ox_hslot_n = need;
+        reset = true;
+    }
+    if (reset) HIP_TRY(hipMemsetAsync(w.ox_hmap, 0xff, w.ox_hmap_n * 4, ss));
+    return SF_OK;
+}
+
+// After the sort phase of a batch with origins (or with rules that read origin
+// / context nodes): the index pass inserts every key the batch needs (growing
+// the table and running again when it fills), then the pool grows to cover
+// the new slots -- all before the decide phase, so nothing is ever dropped.
+// The host waits for the sort stream here (the previous batch's decide phase
+// keeps running).  Fills `plan` for the origin-node pass of the decide phase.
+static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t ss, OxPlan* plan) {
+    { const int rc = ensure_aux(e); if (rc) return rc; }
+    { const int rc = ox_maps(e, w, false, ss); if (rc) return rc; }
+    DevState stl = e->st;
+    stl.err = w.err;
+    uint32_t cnt[8] = {0};
+    uint32_t ax = 0;
+    for (int round = 0;; round++) {
+        const uint64_t xcap = e->st.xcap_mask + 1;
+        stl.xtab = e->st.xtab; stl.xcap_mask = e->st.xcap_mask;
+        const uint32_t lim = (uint32_t)std::min<uint64_t>(xcap * 7 / 10, 0xffffff00u);
+        DevBatch bi = b;
+        if (!w.s_origin || !b.origin) bi.origin = nullptr;
+        hipError_t le = launch_ox_index(stl, w, bi, lim, ss);
+        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("origin index: ") + hipGetErrorString(le));
+        HIP_TRY(hipMemcpyAsync(cnt, w.ox_cnt, sizeof cnt, hipMemcpyDeviceToHost, ss));
+        HIP_TRY(hipMemcpyAsync(&ax, e->st.ax_count, 4, hipMemcpyDeviceToHost, ss));
+        HIP_TRY(hipStreamSynchronize(ss));
+        if (!cnt[OXC_OVERFLOW]) break;
+        if (round > 12) return fail(SF_ERR_CAPACITY, "origin / context node index cannot grow");
+        // the table filled: everything drains, the table grows, the pass runs again
+        HIP_TRY(hipDeviceSynchronize());
+        { const int rc = index_grow(e, (uint64_t)ax + b.n); if (rc) return rc; }
+        { const int rc = ox_maps(e, w, true, ss); if (rc) return rc; }
+    }
+    { const int rc = pool_grow(e, ax); if (rc) return rc; }
+    // keep the index at most half full for the next batches
+    if ((uint64_t)ax * 2 > e->st.xcap_mask + 1) {
+        HIP_TRY(hipDeviceSynchronize());
+        // (the Work set's hmap entries of this batch are slot-indexed: still valid after a rehash)
+        const size_t old_n = w.ox_hmap_n;
+        { const int rc = index_grow(e, (uint64_t)ax * 2); if (rc) return rc; }
+        if (w.ox_hmap_n < (size_t)e->st.xcap_mask + 1) {
+            // regrow the maps keeping this batch's heavy ids
+            uint32_t* nh = nullptr; uint32_t* ns = nullptr; int64_t* nt = nullptr;
+            const size_t need = (size_t)e->st.xcap_mask + 1;
+            HIP_TRY(hipMalloc((void**)&nh, need * 4));
+            HIP_TRY(hipMalloc((void**)&ns, need * 4));
+            HIP_TRY(hipMalloc((void**)&nt, need * 8));
+            HIP_TRY(hipMemsetAsync(nh, 0xff, need * 4, e->stream));
+            HIP_TRY(hipMemcpyAsync(nh, w.ox_hmap, old_n * 4, hipMemcpyDeviceToDevice, e->stream));
+            HIP_TRY(hipMemcpyAsync(ns, w.ox_hslot, old_n * 4, hipMemcpyDeviceToDevice, e->stream));
+            HIP_TRY(hipStreamSynchronize(e->stream));
+            hipFree(w.ox_hmap); hipFree(w.ox_hslot); hipFree(w.ox_thr);
+            w.ox_hmap = nh; w.ox_hslot = ns; w.ox_thr = nt; w.ox_hmap_n = w.ox_hslot_n = need;
+        }
+    }
+    plan->n_heavy = cnt[OXC_HEAVY];
+    int64_t t01[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&t01[0], b.ts, 8, hipMemcpyDeviceToHost, ss));
+    HIP_TRY(hipMemcpyAsync(&t01[1], b.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, ss));
+    HIP_TRY(hipStreamSynchronize(ss));
+    const int64_t wl = e->st.wl;
+    plan->win.w0s = t01[0] / wl; plan->win.w0m = t01[0] / 1000;
+    plan->win.ws = (uint32_t)(t01[1] / wl - plan->win.w0s + 1);
+    plan->win.wm = (uint32_t)(t01[1] / 1000 - plan->win.w0m + 1);
+    const size_t acc_n = (size_t)plan->n_heavy * ((size_t)plan->win.ws + plan->win.wm);
+    if (w.ox_acc_n < acc_n) {
+        if (w.ox_acc) hipFree(w.ox_acc);
+        w.ox_acc = nullptr; w.ox_acc_n = 0;
+        const size_t n2 = acc_n + acc_n / 4;
+        HIP_TRY(hipMalloc(&w.ox_acc, n2 * sizeof(OxAcc)));
+        w.ox_acc_n = n2;
+    }
     return SF_OK;
 }
 
@@ -617,7 +756,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     DevBatch b{};
     b.n = n; b.arg_slots = in->arg_slots;
     hipStream_t s = e->stream, ss = e->serial ? e->stream : e->sstream;
-    if (in->origin && !e->st.ax_second) {
+    if ((in->origin || e->st.xmap) && !e->st.xtab) {
         // the first batch with origins: the origin-node pool (every entry with an
         // origin has one, ClusterBuilderSlot.java:107-110)
         { const int rc = drain(e); if (rc) return rc; }
@@ -625,6 +764,9 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         if (rc) return rc;
         HIP_TRY(hipStreamSynchronize(e->stream));
     }
+    // the origin-node pass (sf_origin.hip) runs for batches with origins and
+    // whenever rules read origin / context nodes (the xflow walk's node keys)
+    const bool with_ox = in->origin || e->st.xmap;
     // asynchronous only for HBM-resident batches and verdicts, without SystemRules
     async = async && in->mem != SF_MEM_HOST && out->mem != SF_MEM_HOST && !e->sys.check && !forced;
     if (!async) { const int rc = drain(e); if (rc) return rc; }
@@ -752,9 +894,15 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
             v.sys = e->sys_mask + p; v.vprev = dv.status + p;
             DevVerdicts dvv{dv.status + p, dv.wait ? dv.wait + p : nullptr, dv.rule ? dv.rule + p : nullptr};
             le = launch_sort(stl, w, v, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s, e->evs[slot], false);
+            OxPlan plan{};
+            if (le == hipSuccess && with_ox) {
+                const int rc = prepare_origins(e, w, v, s, &plan);
+                if (rc) return rc;
+                stl.xtab = e->st.xtab; stl.xcap_mask = e->st.xcap_mask; stl.ax_cap = e->st.ax_cap;
+            }
             if (le == hipSuccess)
                 le = launch_decide(stl, w, v, dvv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3,
-                                   e->evs[slot], false);
+                                   e->evs[slot], false, with_ox ? &plan : nullptr);
             if (le == hipSuccess) le = launch_entry_node(stl, v, dvv.status, e->en, e->en_acc, s);
             if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
             p = q;
@@ -786,10 +934,17 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     stl.err = w.err;
     hipError_t le = launch_sort(stl, w, b, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, ss, e->evs[slot], e->timing);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
+    OxPlan plan{};
+    if (with_ox) {
+        const int rc = prepare_origins(e, w, b, ss, &plan);
+        if (rc) return rc;
+        stl.xtab = e->st.xtab; stl.xcap_mask = e->st.xcap_mask; stl.ax_cap = e->st.ax_cap;
+    }
     HIP_TRY(hipEventRecord(e->ev_sorted[slot], ss));
     // decide phase in batch order on the main streams
     HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
-    le = launch_decide(stl, w, b, dv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3, e->evs[slot], e->timing);
+    le = launch_decide(stl, w, b, dv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3, e->evs[slot], e->timing,
+                       with_ox ? &plan : nullptr);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
     // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream
     // order); under the round protocol the node-wide stream updates it (sf_entry_node_add)
@@ -982,8 +1137,8 @@ int sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out) {
     return read_rows(e, r.sec, r.bor, r.min, r.thr, out);
 }
 
-// origin / context node of local resource l (sf_xflow.h aux_get), looked up
-// in a host copy of the index table
+// origin / context node of local resource l (sf_xflow.h aux_get): its pool
+// slot found on the device, its rows read through the host's chunk directory
 static int read_aux(sf_engine* e, uint32_t resource, uint32_t kind, uint32_t id, sf_node_state* out) {
     if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
     uint32_t l;
@@ -991,13 +1146,18 @@ static int read_aux(sf_engine* e, uint32_t resource, uint32_t kind, uint32_t id,
     std::lock_guard<std::mutex> lk(e->mu);
     { const int rc = drain(e); if (rc) return rc; }
     if (!e->st.xtab) return fail(SF_ERR_INVALID, "no origin / context node is kept");
-    std::vector<ParamSlot> tab(e->st.xcap_mask + 1);
-    HIP_TRY(hipMemcpy(tab.data(), e->st.xtab, tab.size() * sizeof(ParamSlot), hipMemcpyDeviceToHost));
-    int32_t err = 0;
-    const ParamTable t{tab.data(), e->st.xcap_mask, &err};
-    const ParamSlot* s = t.find(pkey_hi(l, PK_AUX, kind, 0), id);
-    if (!s) return fail(SF_ERR_INVALID, "that origin / context node is not kept");
-    const NodeRows r = aux_rows(e->st, (uint32_t)s->a);
+    uint32_t* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, 4));
+    uint32_t k = XNONE;
+    hipError_t le = launch_aux_find(e->st, pkey_hi(l, PK_AUX, kind, 0), id, d, e->stream);
+    if (le == hipSuccess) le = hipMemcpyAsync(&k, d, 4, hipMemcpyDeviceToHost, e->stream);
+    if (le == hipSuccess) le = hipStreamSynchronize(e->stream);
+    hipFree(d);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("aux find: ") + hipGetErrorString(le));
+    if (k == XNONE || k >= e->st.ax_cap) return fail(SF_ERR_INVALID, "that origin / context node is not kept");
+    DevState hs = e->st;
+    hs.ax_chunks = e->ax_host.data();            // host mirror of the chunk directory
+    const NodeRows r = aux_rows(hs, k);
     return read_rows(e, r.sec, r.bor, r.min, r.thr, out);
 }
 int sf_read_origin_node(sf_engine* e, uint32_t resource, uint32_t origin, sf_node_state* out) {
@@ -1746,7 +1906,15 @@ int sf_sync(sf_engine* e) {
 }
 int sf_get_stats(sf_engine* e, sf_stats* out) {
     if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
     *out = e->stats;
+    if (e->st.ax_count) {
+        uint32_t ax = 0;
+        HIP_TRY(hipMemcpy(&ax, e->st.ax_count, 4, hipMemcpyDeviceToHost));
+        out->aux_nodes = ax;
+    }
+    out->aux_capacity = e->st.ax_cap;
+    out->aux_index_grows = e->aux_grows;
     return SF_OK;
 }
 int sf_set_timing(sf_engine* e, int enabled) {

@@ -104,11 +104,16 @@ struct DevState {
     // member), XNONE for every other resource; null: no such rule loaded.
     const uint32_t* xmap;
     // origin / context nodes: index table (key (kind, resource, id) -> pool
-    // slot) and the node pool in the layout of the resource rows
+    // slot) and the node pool in the layout of the resource rows, in chunks of
+    // AX_CHUNK nodes (node k: chunk k >> AX_SHIFT), so the pool grows between
+    // batches without moving a node
     ParamSlot* xtab; uint64_t xcap_mask;
-    Bucket* ax_second; Borrow* ax_borrow; Bucket* ax_minute; int64_t* ax_threads;
+    const struct AuxChunk* ax_chunks;
     uint32_t* ax_count; uint32_t ax_cap;
 };
+// one chunk of the origin / context node pool
+struct AuxChunk { Bucket* sec; Borrow* bor; Bucket* min; int64_t* thr; };
+constexpr uint32_t AX_SHIFT = 16, AX_CHUNK = 1u << AX_SHIFT, AX_MAX_CHUNKS = 8192;
 
 // Constants.ENTRY_NODE (Constants.java:66): the ClusterNode of all inbound
 // traffic, updated by StatisticSlot for EntryType.IN (StatisticSlot.java:64-178)
@@ -143,6 +148,9 @@ struct EntryAcc {
 // first event (16 bits, PV_DTS_FAR: read the batch's ts) | flags (8 bits) << 16
 // | acquireCount (8 bits, 1..255; 0: read the batch's count) << 24.
 struct alignas(8) PackedEv { uint32_t idx, meta; };
+// the payload of a batch with origins: the origin id rides along (k_unpack
+// writes it in sorted order for the origin-node pass, sf_origin.hip)
+struct PackedEvO { uint32_t idx, meta, origin; };
 constexpr uint32_t PV_DTS_FAR = 0xffffu;
 
 // light segments are listed by length class (len 1, 2, 3-4, 5-8, ...) so the
@@ -211,6 +219,22 @@ struct Work {
     // (THREAD run mode also borrows buffers dead after the sort: rid = keys_in,
     //  run_start = head_scan, run_pre = keys_out, entry records = pv_in; sf_kernels.hip heavy_ctx)
     uint32_t* vs_cursor;                                // [VS_CURSORS(N)] fill counts of the verdict scatter's buckets
+    // origin nodes (sf_origin.hip), batches with origins only
+    uint32_t* s_origin;                                 // [N] origin id in sorted order
+    uint32_t* s_oslot;                                  // [N] pool slot of the event's origin node (XNONE: none)
+    uint32_t* ox_cnt;                                   // [8] OXC_* counters of the index pass
+    uint32_t* ox_bflags;                                // [N / OX_TILE + 1] origin work of each OX_TILE block
+    uint32_t* ox_hmap; size_t ox_hmap_n;                // [ox_hmap_n] pool slot -> heavy pair id (XNONE between batches)
+    uint32_t* ox_hslot; size_t ox_hslot_n;              // [ox_hslot_n] heavy pair id -> pool slot
+    int64_t* ox_thr;                                    // [ox_hslot_n] thread delta per heavy pair
+    void* ox_acc; size_t ox_acc_n;                      // [H][Ws + Wm] OxAcc window sums of the heavy pairs
+};
+// origin-node pass (sf_origin.hip): a block is OX_TILE sorted positions; a
+// segment of at most OX_LIGHT events is walked whole by the block it starts in
+constexpr uint32_t OX_TILE = 2048, OX_LIGHT = 512;
+enum : int { OXC_HEAVY = 0, OXC_LIGHT_BLOCKS = 1, OXC_HEAVY_BLOCKS = 2, OXC_OVERFLOW = 3 };
+struct OxAcc {             // one heavy pair's sums in one window; min_rt encoded for a max (0: none)
+    unsigned long long pass, block, succ, rt, exc, n_touch, min_rt_key;
 };
 // verdict scatter (sorted order -> submission order, launch_scatter): regions of
 // 2^VS_REG verdicts are assembled in LDS; its first pass has at most 256 buckets
@@ -286,12 +310,23 @@ hipError_t launch_fmt_write(const sf_metric_row* rows, const uint32_t* order, ui
 hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipStream_t s);   // out[0] used, out[1] max probe
 hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,
                        uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing);
+struct OxWin { int64_t w0s, w0m; uint32_t ws, wm; };    // the batch's first second / minute window and counts
+struct OxPlan { uint32_t n_heavy; OxWin win; };         // the batch's origin-node pass (sf_origin.hip)
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
-                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing);
+                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing,
+                         const OxPlan* ox = nullptr);
+// origin nodes (sf_origin.hip)
+hipError_t launch_ox_index(const DevState& st, Work& w, const DevBatch& b, uint32_t lim, hipStream_t s);
+hipError_t launch_ox_apply(const DevState& st, Work& w, const DevBatch& b, uint32_t n_heavy, const OxWin& win,
+                           hipStream_t s);
+hipError_t launch_ox_rehash(const ParamSlot* old_tab, uint64_t old_n, ParamSlot* new_tab, uint64_t new_mask,
+                            int32_t* err, hipStream_t s);
+hipError_t launch_aux_find(const DevState& st, uint64_t hi, uint64_t lo, uint32_t* out, hipStream_t s);
 constexpr size_t ACC_BYTES = 72;                         // sizeof(Acc)
 // pipeline events: 0 start, 1 segments, 2 classified, 3 joined, 4 scattered,
 // 5 fork, 6 join (stream B), 7 heavy decided, 8 heavy filled, 9 light decided, 10 before classify,
-// 11 stream start (stream C), 12 stream done (stream C), 13 stream fill + apply done (stream C)
-constexpr int SF_NUM_EVENTS = 14;
+// 11 stream start (stream C), 12 stream done (stream C), 13 stream fill + apply done (stream C),
+// 14 origin-node pass done (stream B)
+constexpr int SF_NUM_EVENTS = 15;
 
 }  // namespace sf

@@ -45,7 +45,8 @@ __global__ void k_init_state(DevState st, size_t n_sec, size_t n_min) {
 // (PackedEv), so the sorted order is read back with coalesced loads instead of
 // a random gather from the submission-order arrays; an offset or count that
 // does not fit is read from the batch by k_unpack for that event only.
-__global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t shard_count, uint32_t shard_index,
+template <bool ORG>
+__global__ void k_keys_packed(DevBatch b, uint32_t* keys, void* pvv, uint32_t shard_count, uint32_t shard_index,
                               uint32_t R, int32_t* err, const int64_t* last_ts, const uint32_t* xmap) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= b.n) return;
@@ -72,24 +73,39 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, PackedEv* pv, uint32_t
     }
     const int32_t c = b.cnt[i];
     const uint32_t c8 = (c >= 1 && c <= 255) ? (uint32_t)c : 0u;
-    PackedEv v;
-    v.idx = i; v.meta = dts | (fl << 16) | (c8 << 24);
-    pv[i] = v;
+    const uint32_t meta = dts | (fl << 16) | (c8 << 24);
+    if constexpr (ORG) {
+        PackedEvO v; v.idx = i; v.meta = meta; v.origin = b.origin[i];
+        ((PackedEvO*)pvv)[i] = v;
+    } else {
+        PackedEv v; v.idx = i; v.meta = meta;
+        ((PackedEv*)pvv)[i] = v;
+    }
 }
 
 // Also the segment table (segment id of sorted event j = inclusive count of
 // segment heads up to j, minus one): start, resource and the segment count.
-__global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* keys, uint32_t* perm, int64_t* s_ts,
+template <bool ORG>
+__global__ void k_unpack(DevBatch b, const void* pvv, const uint32_t* keys, uint32_t* perm, int64_t* s_ts,
                          int32_t* s_cnt, uint8_t* s_flags, uint8_t* s_nargs, uint8_t* s_atag,
                          uint64_t* s_abits, const uint32_t* head_scan, uint32_t* seg_start, uint32_t* seg_res,
-                         uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts, const int32_t* err, bool exit_marks) {
+                         uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts, const int32_t* err, bool exit_marks,
+                         uint32_t* s_origin) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
     const uint32_t sid = head_scan[j] - 1;
     if (j == 0 || head_scan[j - 1] != head_scan[j]) { seg_start[sid] = j; seg_res[sid] = keys[j]; }
     if (j == b.n - 1) { *n_seg = sid + 1; seg_start[sid + 1] = b.n; }
     if (j == 0 && *err == 0) *last_ts = b.ts[b.n - 1];   // k_keys_packed of this batch has read the old value
-    const PackedEv v = pv[j];
+    PackedEv v;
+    uint32_t org = SF_ORIGIN_NONE;
+    if constexpr (ORG) {
+        const PackedEvO vo = ((const PackedEvO*)pvv)[j];
+        v.idx = vo.idx; v.meta = vo.meta; org = vo.origin;
+        s_origin[j] = org;
+    } else {
+        v = ((const PackedEv*)pvv)[j];
+    }
     const uint32_t i = v.idx;
     const uint32_t dts = v.meta & 0xffffu, c8 = v.meta >> 24;
     const int32_t c = c8 ? (int32_t)c8 : b.cnt[i];
@@ -97,13 +113,14 @@ __global__ void k_unpack(DevBatch b, const PackedEv* pv, const uint32_t* keys, u
     perm[j] = i;
     s_ts[j] = dts != PV_DTS_FAR ? b.ts[0] + (int64_t)dts : b.ts[i]; s_cnt[j] = c; s_flags[j] = f;
     // segment flags (k_classify's routing): the exits (read only by the ParamFlow
-    // routing, heavy_mode), origins (ClusterBuilderSlot.java:107-110: the xflow
-    // walk), prioritized / non-positive / blocked-before entries; OR-ed per
-    // segment within the wavefront, one atomic per segment and wavefront
+    // routing, heavy_mode), origins (ClusterBuilderSlot.java:107-110: the
+    // origin-node pass, sf_origin.hip), prioritized / non-positive /
+    // blocked-before entries; OR-ed per segment within the wavefront, one
+    // atomic per segment and wavefront
     {
         uint32_t mine = 0;
         if (exit_marks && (f & SF_EV_EXIT)) mine |= SEGF_EXIT;
-        if (b.origin && b.origin[i] != SF_ORIGIN_NONE) mine |= SEGF_ORIGIN;
+        if (org != SF_ORIGIN_NONE) mine |= SEGF_ORIGIN;
         if (!(f & SF_EV_EXIT))
             mine |= ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) | ((f & EVF_SYSBLK) ? SEGF_SYS : 0u);
         const unsigned long long any = __ballot(mine != 0);
@@ -202,8 +219,9 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     const bool valid = s < *w.n_seg;
     uint32_t lo = 0, hi = 0, res = 0;
     if (valid) { lo = w.seg_start[s]; hi = w.seg_start[s + 1]; res = w.seg_res[s]; }
-    // an xflow group (sf_xflow.h) is decided by k_decide_x only
-    const bool xs = valid && ((st.xmap && st.xmap[res] != XNONE) || (w.segflag[s] & SEGF_ORIGIN));
+    // an xflow group (sf_xflow.h) is decided by k_decide_x only; origins alone
+    // do not route a segment there (their nodes: sf_origin.hip)
+    const bool xs = valid && st.xmap && st.xmap[res] != XNONE;
     if (xs) w.seg_mode[s] = SM_XFLOW;
     bool light = valid && !xs && hi - lo <= w.heavy_min;
     // a ParamFlow-only segment of more than 32 events is faster on the
@@ -1095,6 +1113,10 @@ hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_byte
                                   (PackedEv*)nullptr, (PackedEv*)nullptr, max_n, 0u, key_bits);
     if (e != hipSuccess) return e;
     if (packed_bytes > *sort_bytes) *sort_bytes = packed_bytes;
+    e = rocprim::radix_sort_pairs(nullptr, packed_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (PackedEvO*)nullptr, (PackedEvO*)nullptr, max_n, 0u, key_bits);
+    if (e != hipSuccess) return e;
+    if (packed_bytes > *sort_bytes) *sort_bytes = packed_bytes;
     HeadIter hit(rocprim::counting_iterator<uint32_t>(0), HeadFlag{nullptr});
     e = rocprim::inclusive_scan<HeadScanCfg>(nullptr, *scan_bytes, hit, (uint32_t*)nullptr, (size_t)max_n,
                                 rocprim::plus<uint32_t>());
@@ -1126,10 +1148,18 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     const unsigned T = 256;
     if (timing) hipEventRecord(ev[0], s);
     hipError_t e;
-    hipLaunchKernelGGL(k_keys_packed, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, w.pv_in, shard_count,
-                       shard_index, st.R, st.err, st.last_ts, st.xmap);
-    e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.pv_in, w.pv_out, n, 0u,
-                                  key_bits, s);
+    const bool org = b.origin != nullptr;                       // the origin rides in a 12-B payload
+    if (org) {
+        hipLaunchKernelGGL(k_keys_packed<true>, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, (void*)w.pv_in,
+                           shard_count, shard_index, st.R, st.err, st.last_ts, st.xmap);
+        e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, (PackedEvO*)w.pv_in,
+                                      (PackedEvO*)w.pv_out, n, 0u, key_bits, s);
+    } else {
+        hipLaunchKernelGGL(k_keys_packed<false>, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, (void*)w.pv_in,
+                           shard_count, shard_index, st.R, st.err, st.last_ts, st.xmap);
+        e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, w.pv_in, w.pv_out, n, 0u,
+                                      key_bits, s);
+    }
     if (e != hipSuccess) return e;
     {
         HeadIter hit(rocprim::counting_iterator<uint32_t>(0), HeadFlag{w.keys_out});
@@ -1139,9 +1169,15 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     }
     hipMemsetAsync(w.segflag, 0, (size_t)(n < st.R ? n : st.R) * 4, s);
     if (timing) hipEventRecord(ev[1], s);
-    hipLaunchKernelGGL(k_unpack, dim3(blocks(n, T)), dim3(T), 0, s, b, w.pv_out, w.keys_out, w.perm, w.s_ts, w.s_cnt,
-                       w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan, w.seg_start, w.seg_res, w.n_seg,
-                       w.segflag, st.last_ts, st.err, st.n_prule != 0);
+    if (org)
+        hipLaunchKernelGGL(k_unpack<true>, dim3(blocks(n, T)), dim3(T), 0, s, b, (const void*)w.pv_out, w.keys_out,
+                           w.perm, w.s_ts, w.s_cnt, w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan,
+                           w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err, st.n_prule != 0, w.s_origin);
+    else
+        hipLaunchKernelGGL(k_unpack<false>, dim3(blocks(n, T)), dim3(T), 0, s, b, (const void*)w.pv_out, w.keys_out,
+                           w.perm, w.s_ts, w.s_cnt, w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan,
+                           w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err, st.n_prule != 0,
+                           (uint32_t*)nullptr);
     if (b.eref || st.n_stream_rules) hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);   // (read by k_gather_exit, k_thr_rec)
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags,
@@ -1343,7 +1379,7 @@ static void launch_thr_prep(Work& w, const DevBatch& b, hipStream_t s) {
 // start first, on A; QPS/WarmUp heavy segments on B, the light lanes on C;
 // then the verdicts are scattered back to submission order.
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
-                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing) {
+                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing, const OxPlan* ox) {
     const uint32_t n = b.n;
     if (n == 0) return hipSuccess;
     SegIO io;
@@ -1425,7 +1461,7 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
         hipLaunchKernelGGL(k_decide_short<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
                            w.seg_start, w.seg_res, ll, w.counters + 8);
     }
-    if (st.xmap || b.origin) {
+    if (st.xmap) {
         if (st.S <= 2)
             hipLaunchKernelGGL(k_decide_x<2>, dim3(blocks(max_seg, 64)), dim3(64), 0, s3, st, io, w.seg_start,
                                w.seg_mode, w.n_seg);
@@ -1439,7 +1475,16 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     hipStreamWaitEvent(s, ev[9], 0);
     hipEventRecord(ev[13], s);
     if (timing) hipEventRecord(ev[3], s);
+    // origin nodes no rule reads (sf_origin.hip): from the sorted verdicts,
+    // beside the verdict scatter
+    if (ox) {
+        hipStreamWaitEvent(s2, ev[13], 0);
+        const hipError_t e = launch_ox_apply(st, w, b, ox->n_heavy, ox->win, s2);
+        if (e != hipSuccess) return e;
+        hipEventRecord(ev[14], s2);
+    }
     launch_scatter(w, n, out.status, s);
+    if (ox) hipStreamWaitEvent(s, ev[14], 0);
     if (timing) hipEventRecord(ev[4], s);
     return hipGetLastError();
 }

@@ -21,7 +21,10 @@
 // state of the walk lives in HBM (held in NodeWins while consecutive events
 // use the same node, stored back on a switch); origin and context nodes sit in
 // a pool indexed by an exact hash table.
-// This is the rare path: the common DIRECT/"default" rules never come here.
+// This is the rare path: the common DIRECT/"default" rules never come here,
+// and neither do origin nodes no rule reads (ClusterBuilderSlot creates one
+// for every entry with an origin): those are written after the verdicts by
+// the origin-node pass (sf_origin.hip).
 #pragma once
 #include <vector>
 
@@ -41,8 +44,9 @@ SF_HD NodeRows cluster_rows(const DevState& st, uint32_t l) {
                     st.threads + l};
 }
 SF_HD NodeRows aux_rows(const DevState& st, uint32_t k) {
-    return NodeRows{st.ax_second + (size_t)k * st.S, st.ax_borrow + (size_t)k * st.S,
-                    st.ax_minute + (size_t)k * MINUTE, st.ax_threads + k};
+    const AuxChunk& c = st.ax_chunks[k >> AX_SHIFT];
+    const size_t i = k & (AX_CHUNK - 1);
+    return NodeRows{c.sec + i * st.S, c.bor + i * st.S, c.min + i * MINUTE, c.thr + i};
 }
 template <int MAXS>
 SF_HD void nw_load(NodeWin<MAXS>& nd, const DevState& st, const NodeRows& r) {
@@ -71,8 +75,10 @@ SF_HD bool node_created(const DevState& st, const NodeRows& r) {
     return false;
 }
 
-// the pool slot of origin / context node (kind, id) of local resource l,
-// created (fresh) on first use; only the lane that owns l's group calls this
+// the pool slot of origin / context node (kind, id) of local resource l.  The
+// sort phase's index pass (sf_origin.hip k_ox_index) has inserted every key a
+// batch can ask for and the host has grown the pool to cover them, so on the
+// device this is a find; the insert below serves the host build (tests/hostsim)
 SF_HD uint32_t aux_get(const DevState& st, uint32_t l, uint32_t kind, uint32_t id) {
     ParamTable t{st.xtab, st.xcap_mask, st.err};
     const uint64_t hi = pkey_hi(l, PK_AUX, kind, 0);

@@ -190,6 +190,25 @@ def mixed_zipf(n_res: int, n_events: int, duration_ms: int = 4000, seed: int = 3
     return abi.HostBatch(res_all, all_ts[order], cnt_all, flags, entry_ref=eref)
 
 
+def with_origins(hb: abi.HostBatch, n_origins: int = 64, s: float = 1.1, seed: int = 13, none_frac: float = 0.0):
+    """The batch with a caller origin on every entry (ContextUtil.enter(name,
+    origin)): one of ``n_origins`` interned names (ids 2..n_origins+1) drawn
+    Zipf(s), or "" (ORIGIN_NONE) with probability ``none_frac``; an EXIT
+    carries its entry's origin (Entry.exit runs in the entry's context)."""
+    rng = np.random.default_rng(seed)
+    ent = (hb.flags & abi.EV_EXIT) == 0
+    org = np.empty(hb.n, np.uint32)
+    org[ent] = (zipf_bounded(rng, s, n_origins, int(ent.sum())) + 1).astype(np.uint32)
+    if none_frac > 0:
+        org[ent & (rng.random(hb.n) < none_frac)] = abi.ORIGIN_NONE
+    ex = np.nonzero(~ent)[0]
+    if ex.size:
+        ref = hb.entry_ref[ex]
+        org[ex] = np.where(ref >= 0, org[np.clip(ref, 0, None)], np.uint32(2) + (ex % n_origins).astype(np.uint32))
+    return abi.HostBatch(hb.res_id, hb.ts_ms, hb.count, hb.flags, entry_ref=hb.entry_ref, create_ts=hb.create_ts,
+                         arg_tag=hb.arg_tag, arg_bits=hb.arg_bits, n_args=hb.n_args, origin=org, context=hb.context)
+
+
 def mixed_rules(n_res: int, seed: int = 3):
     grade, beh, count = mixed_rule_table(n_res, seed)
     return flow_rules_from_counts(count, behaviors=beh, grades=grade)

@@ -39,6 +39,7 @@ struct hs_engine {
     std::vector<Bucket> ax_second, ax_minute;
     std::vector<Borrow> ax_borrow;
     std::vector<int64_t> ax_threads;
+    std::vector<AuxChunk> ax_chunks;          // the device's chunk directory over the contiguous host pool
     uint32_t ax_count = 0;
     int32_t err = 0;
     uint32_t R;
@@ -55,8 +56,12 @@ struct hs_engine {
         st.dg_off = dg_off.data(); st.dg_rules = dg_rules.data(); st.dg_state = dg_state.data();
         st.xmap = xmap.empty() ? nullptr : xmap.data();
         st.xtab = xtab.data(); st.xcap_mask = xtab.empty() ? 0 : xtab.size() - 1;
-        st.ax_second = ax_second.data(); st.ax_borrow = ax_borrow.data(); st.ax_minute = ax_minute.data();
-        st.ax_threads = ax_threads.data(); st.ax_count = &ax_count; st.ax_cap = (uint32_t)ax_threads.size();
+        ax_chunks.clear();
+        const size_t S_ = st.S;
+        for (size_t c = 0; c * AX_CHUNK < ax_threads.size(); c++)
+            ax_chunks.push_back(AuxChunk{ax_second.data() + c * AX_CHUNK * S_, ax_borrow.data() + c * AX_CHUNK * S_,
+                                         ax_minute.data() + c * AX_CHUNK * MINUTE, ax_threads.data() + c * AX_CHUNK});
+        st.ax_chunks = ax_chunks.data(); st.ax_count = &ax_count; st.ax_cap = (uint32_t)ax_threads.size();
     }
 };
 
@@ -94,7 +99,9 @@ static bool local_of(hs_engine* e, uint32_t res, uint32_t* l) {
 // the origin / context node pool (lives as long as the engine)
 static void ensure_pool(hs_engine* e) {
     if (!e->ax_threads.empty()) return;
-    const size_t cap = e->cfg.aux_capacity ? e->cfg.aux_capacity : 65536, S = e->cfg.sample_count;
+    size_t cap = e->cfg.aux_capacity ? e->cfg.aux_capacity : 65536;
+    const size_t S = e->cfg.sample_count;
+    cap = (cap + AX_CHUNK - 1) / AX_CHUNK * AX_CHUNK;          // whole chunks (sf_internal.h AuxChunk)
     size_t tcap = 16; while (tcap < 2 * cap) tcap <<= 1;
     e->xtab.assign(tcap, ParamSlot{0, 0, 0, 0});
     e->ax_second.assign(cap * S, fresh_bucket(WS_NONE, e->cfg.statistic_max_rt));
