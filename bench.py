@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--no-degrade", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the config2 / config4 / config5 / end-to-end legs")
     ap.add_argument("--legs", default="", help="comma-separated subset of the legs to run (default: all)")
+    ap.add_argument("--origin-variants", default="no_origin_rules,other_rules_1pct",
+                    help="config3_origin leg: the variants to run")
     ap.add_argument("--heavy-min", type=int, default=0,
                     help="segments of more events than this go to the heavy kernels (0: the engine default, 512)")
     args = ap.parse_args()
@@ -183,7 +185,10 @@ def main():
     light_names = ("k_decide_light", "k_decide_light_qps", "k_decide_short_qps", "k_decide_short")
     light_traffic = {}
     import glob
-    profs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_config3_summary.json")))
+    # the latest round's profile of the final tree (r??_config3_summary_final.json),
+    # else that round's plain summary
+    profs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_config3_summary*.json")),
+                   key=lambda p: (os.path.basename(p)[:3], p.endswith("_final.json")))
     prof = profs[-1] if profs else ""
     if prof:
         with open(prof) as fh:
@@ -200,13 +205,18 @@ def main():
                    "achieved": round(light_bytes / (light_ms / 1e3) / 1e9, 2),
                    "frac": round(light_bytes / (light_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
                    "traffic": sum(light_traffic.values()) if len(light_traffic) == len(light_names) else None}
-    roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+    roofline = {"bound": "hbm", "kernel": name,
+                "note": "achieved/frac: the dominant kernel's share of the byte model over its HIP-event time -- a "
+                        "latency figure for a serial-chain kernel (k_heavy_stream reads pre-digested records); "
+                        "pipeline.frac is the whole step's bytes over its wall time",
+                "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "traffic_source": traffic_src,
                 "alg_bytes_per_launch": bytes_k, "avg_launch_ms": round(ms, 4),
                 "light_phase": light_phase,
                 "pipeline": {"alg_bytes_per_step": b_alg,
                              "achieved_GBs": round(b_alg / (wall / k) / 1e9, 2),
+                             "frac": round(b_alg / (wall / k) / 1e9 / HBM_PEAK_GBS, 5),
                              "heavy_segments": n_heavy_res},
                 "kernels_ms": {"sort+segments+classify": round(st.sort_ms / k, 3),
                                "classify": round(st.classify_ms / k, 3),
@@ -277,14 +287,21 @@ def main():
     # after the timed region, each on its own engine except e2e)
     legs = {}
     if rank == 0 and world == 1 and not args.no_legs:
-        for b in batches[1:]:
+        # the headline engine's verdicts of batch 0 and of the last batch (the
+        # e2e leg repeats the run from host memory and must equal them); then
+        # the engine is released so that each leg has the device to itself
+        g0 = (out0.status.numpy(), out0.wait_ms.numpy(), out0.rule_idx.numpy())
+        glast = (out.status.numpy(), out.wait_ms.numpy())
+        for b in batches:
             b.free()
-        batches = batches[:1]
-        # (after the oracle leg: e2e advances this engine's state)
+        batches = []
+        base = None
+        out0.free(); out.free()
+        eng.close()
         c3_ms = wall / args.steps * 1e3
-        for nm, fn in (("e2e_pinned", lambda: e2e_leg(eng, hb, steps * DURATION_MS)),
-                       ("config3_origin", lambda: config3_origin_leg(hb, rules, R_local, c3_ms, eng,
-                                                                       parity=not args.no_cpu)),
+        for nm, fn in (("e2e_pinned", lambda: e2e_leg(hb, rules, R_local, steps, g0, glast)),
+                       ("config3_origin", lambda: config3_origin_leg(hb, rules, R_local, c3_ms, parity=not args.no_cpu,
+                                                                       variants=args.origin_variants.split(","))),
                        ("config2", config2_leg), ("config4", config4_leg), ("config5", config5_leg)):
             if args.legs and nm not in args.legs.split(","):
                 continue
@@ -314,7 +331,8 @@ def main():
         print(json.dumps(line), flush=True)
     for b in batches[1:]:
         b.free()
-    base.free()
+    if base is not None:
+        base.free()
     if dist:
         dist.destroy_process_group()
 
@@ -371,7 +389,8 @@ def node_trace(R_total, n, world, rank, dist):
     return abi.HostBatch(res[mo], ts[mo], cnt[mo], fl[mo], entry_ref=er)
 
 
-def config3_origin_leg(hb, rules, R, c3_ms, main_eng, steps=5, warmup=2, parity=True, n_origins=64):
+def config3_origin_leg(hb, rules, R, c3_ms, steps=5, warmup=2, parity=True, n_origins=64,
+                       variants=("no_origin_rules", "other_rules_1pct")):
     """Config 3 with a caller origin on every entry (ContextUtil.enter(name,
     origin)): one of 64 names drawn Zipf(1.1), exits carrying their entry's
     (trace.with_origins).  ClusterBuilderSlot creates the origin node of every
@@ -415,9 +434,9 @@ def config3_origin_leg(hb, rules, R, c3_ms, main_eng, steps=5, warmup=2, parity=
     other["max_queueing_time_ms"] = 500
     both = np.concatenate([rules, other])
     both = both[np.argsort(both["resource"], kind="stable")]    # per resource: the config-3 rule, then "other"
-    variants = (("no_origin_rules", rules), ("other_rules_1pct", both))
-    main_eng.sync()
-    for name, rl in variants:
+    for name, rl in (("no_origin_rules", rules), ("other_rules_1pct", both)):
+        if name not in variants:
+            continue
         e = engine.FlowEngine(abi.default_config(max_resources=R, max_batch=ho.n))
         res = {"rules": int(len(rl))}
         try:
@@ -467,7 +486,9 @@ def config3_origin_leg(hb, rules, R, c3_ms, main_eng, steps=5, warmup=2, parity=
                 T = max(1, min(16, len(os.sched_getaffinity(0))))
                 sh = sharded.ShardedOracle(rl, R, T, ho.n)
                 sh.split_like(ho)
+                log(f"[leg config3_origin] {name}: oracle replay of batch 0 ...")
                 v, dt = sh.submit(ho)
+                log(f"[leg config3_origin] {name}: oracle batch 0 in {dt:.1f}s")
                 blk = np.isin(v.status, [abi.V_BLOCK_FLOW, abi.V_BLOCK_PARAM, abi.V_BLOCK_SYSTEM])
                 mm = {"status": int((g0[0] != v.status).sum()), "wait_ms": int((g0[1] != v.wait_ms).sum()),
                       "rule_idx_of_blocks": int((g0[2][blk] != v.rule_idx[blk]).sum()),
@@ -481,7 +502,8 @@ def config3_origin_leg(hb, rules, R, c3_ms, main_eng, steps=5, warmup=2, parity=
                                        "unit": "decisions/s", "cores": T, "kind": "port",
                                        "sample": "batch 0, resource-sharded C oracle with origin nodes"}
                 for k in range(1, warmup + steps):
-                    v, _ = sh.submit(ho, k * DURATION_MS)
+                    v, dtk = sh.submit(ho, k * DURATION_MS)
+                    log(f"[leg config3_origin] {name}: oracle batch {k} in {dtk:.1f}s")
                 mm_last = {"status": int((gl[0] != v.status).sum()), "wait_ms": int((gl[1] != v.wait_ms).sum()),
                            "origin_nodes": sum(a != abi.node_state_to_dict(sh.read_origin_node(r, o))
                                                for a, (r, o) in zip(gpu1["origin"], pairs)),
@@ -568,7 +590,10 @@ def config4_leg(R=1000, n=1 << 24, keys=100_000_000, qps_frac=0.6, reps=3):
     sysr = [abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=qps_frac * offered,
                                avg_rt=-1, max_thread=-1)]
     pairs = np.unique(b.res_id.astype(np.uint64) << np.uint64(40) ^ (b.arg_bits[0] & np.uint64((1 << 40) - 1))).size
-    cap = 1 << int(np.ceil(np.log2(max(2.5 * pairs * 1.1, 1 << 16))))
+    # the engine keeps room for every key a batch can insert (events x 2 x the
+    # most rules on a resource, at half load: sf_engine.cpp param_reserve); a
+    # table that large from the start keeps the rebuild out of the timed submit
+    cap = 1 << int(np.ceil(np.log2(max(2 * b.n * 4, 2.5 * pairs * 1.1, 1 << 16))))
     cfg = abi.default_config(max_resources=R, max_batch=b.n, param_capacity=cap)
     walls, st, tab, rounds = [], None, None, 0
     log(f"[leg config4] trace {b.n} events, ~{pairs} (resource, key) pairs")
@@ -680,50 +705,79 @@ def config5_leg(n_req=1 << 22, n_streams=500, steps=3):
     finally:
         e.close()
     try:
+        # parity on the benchmarked frames themselves: all requests, a fresh
+        # engine and a fresh oracle wire path, every response frame compared
         from oracle import oracle as so
-        ns2, flow2, param2, st2 = wire_bench.frames(1 << 16, n_streams, 8)
-        cfg2 = abi.default_config(max_resources=4, max_batch=1 << 16, param_capacity=1 << 18)
+        cfg2 = abi.default_config(max_resources=4, max_batch=n_req, param_capacity=1 << 22)
         cfg2.max_flow_ids = 1 << 15
         g = engine.FlowEngine(cfg2)
         o = so.OracleEngine(cfg2)
         for x in (g, o):
-            x.load_namespaces(ns2)
-            x.load_cluster_rules(flow2, param2, [])
-        rg, ro = g.serve_frames(st2, trace.T0), o.serve_frames(st2, trace.T0)
-        same = all(rg.responses(s) == ro.responses(s) for s in range(n_streams))
+            x.load_namespaces(ns)
+            x.load_cluster_rules(flow, param, [])
+        t = time.perf_counter()
+        rg = g.serve_frames(streams, trace.T0)
+        ro = o.serve_frames(streams, trace.T0)
+        t_or = time.perf_counter() - t
+        bad = sum(rg.responses(s) != ro.responses(s) for s in range(n_streams))
         g.close()
         o.close()
-        res["parity"] = {"what": "64k requests over 500 connections: every response frame vs the oracle's wire path",
-                         "requests": int(ro.n_requests), "exact": bool(same)}
+        res["parity"] = {"what": f"all {int(ro.n_requests)} requests of the benchmarked frames over {n_streams} "
+                                 f"connections, fresh engine and fresh oracle wire path: every response frame",
+                         "requests": int(ro.n_requests), "connections_differing": int(bad), "exact": bad == 0,
+                         "seconds": round(t_or, 1)}
     except Exception as ex:  # pragma: no cover
         res["parity"] = {"error": str(ex)[:200]}
     return res
 
 
-def e2e_leg(eng, hb, t_shift, reps=3):
-    """Config 3 end to end from page-locked host memory (sf_host_alloc): each
-    sf_submit copies the batch H2D, decides it and copies the verdicts back
-    (status, wait, rule index), timed on the wall clock -- the PCIe-inclusive
-    rate a host that submits from its own buffers sees (never the headline)."""
-    pin = engine.PinnedArrays(eng)
+def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
+    """Config 3 end to end from page-locked host memory: the headline run's
+    batches (the same trace, shifted by DURATION_MS per step) submitted from
+    host buffers in the compact form (sf_submit_packed_async: 8 bytes per event
+    plus the exits' entry refs), so that the H2D copy of batch k+1, the
+    decision of batch k and the D2H copy of the verdicts (status, wait, rule
+    index) of batch k-1 overlap.  A fresh engine; the time shift is only the
+    batch's ts_base, so every step reuses the same pinned words.  Parity: the
+    verdicts of batch 0 and of the last batch equal the headline run's (itself
+    compared with the oracle).  PCIe-inclusive: never the headline."""
+    e = engine.FlowEngine(abi.default_config(max_resources=R, max_batch=hb.n))
+    pin = engine.PinnedArrays(e)
     try:
-        hp = pin.batch(hb)
-        vp = pin.verdicts(hb.n)
-        w = []
-        for k in range(reps):
-            hp.ts_ms[...] = hb.ts_ms + t_shift + k * DURATION_MS
-            t = time.perf_counter()
-            eng.submit(hp, vp)
-            w.append(time.perf_counter() - t)
-        ms = float(np.median(w)) * 1e3
-        in_b = hb.n * (4 + 8 + 4 + 1) + int(((hb.flags & abi.EV_EXIT) != 0).sum()) * 8
-        out_b = hb.n * (1 + 4 + 2)
+        e.load_flow_rules(rules)
+        t0 = time.perf_counter()
+        pb = abi.PackedBatch(hb, alloc=pin.array)
+        log(f"[leg e2e_pinned] packed {hb.n} events into {pb.nbytes() / 1e9:.2f} GB in {time.perf_counter() - t0:.1f}s")
+        outs = [pin.verdicts(hb.n) for _ in range(3)]
+        base_ts = pb.ts_base
+        timed = timed or max(3, steps - 2)
+        walls = []
+        t = None
+        for k in range(steps):
+            if k == steps - timed:
+                e.sync()
+                t = time.perf_counter()
+            pb.ts_base = base_ts + k * DURATION_MS
+            o = outs[0] if k == 0 else (outs[1] if k == steps - 1 else outs[2])
+            e.submit_packed_async(pb, o)
+            if k == 0:
+                e.sync()                                   # batch 0 kept for parity
+        e.sync()
+        ms = (time.perf_counter() - t) / timed * 1e3
         ent = int(((hb.flags & abi.EV_EXIT) == 0).sum())
-        return {"what": "config3 batch from pinned host buffers: H2D + decide + D2H per sf_submit (not pipelined)",
+        bad0 = {"status": int((outs[0].status != g0[0]).sum()), "wait_ms": int((outs[0].wait_ms != g0[1]).sum()),
+                "rule_idx": int((outs[0].rule_idx != g0[2]).sum())}
+        badl = {"status": int((outs[1].status != glast[0]).sum()), "wait_ms": int((outs[1].wait_ms != glast[1]).sum())}
+        return {"what": "config3 batches from pinned host buffers in the compact form (sf_submit_packed_async: "
+                        "H2D of batch k+1, decide of k and D2H of k-1 overlapped)",
                 "events": int(hb.n), "ms_per_batch": round(ms, 3), "decisions_per_s": round(ent / (ms / 1e3), 1),
-                "h2d_bytes": in_b, "d2h_bytes": out_b, "reps_ms": [round(x * 1e3, 2) for x in w]}
+                "timed_batches": timed, "h2d_bytes": int(pb.nbytes()), "d2h_bytes": int(hb.n * (1 + 4 + 2)),
+                "parity": {"what": "batch 0 and the last batch vs the headline run's verdicts", "batch0": bad0,
+                           "last": badl, "exact": all(v == 0 for v in bad0.values()) and
+                           all(v == 0 for v in badl.values())}}
     finally:
         pin.free()
+        e.close()
 
 
 def degrade_leg(R=1_000_000, entries=1 << 22, steps=3):

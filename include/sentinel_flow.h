@@ -379,6 +379,7 @@ typedef struct sf_stats {         /* device-clock timings, summed over sf_submit
     uint64_t aux_nodes;           /* origin / context nodes kept (pool slots in use) */
     uint64_t aux_capacity;        /* pool slots backed by device memory (grows by chunks between batches) */
     uint64_t aux_index_grows;     /* times the pool's index table was rebuilt larger */
+    uint64_t param_table_grows;   /* times the exact ParamFlow table was rebuilt larger (before a batch) */
 } sf_stats;
 
 typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last sf_submit */
@@ -414,6 +415,40 @@ int  sf_submit(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
  * and reports the first error any of them raised.  Host-memory batches and
  * timing mode fall back to sf_submit. */
 int  sf_submit_async(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
+
+/* ---- compact batches (the PCIe form: 8 bytes per event) -----------------
+ * For a host that submits from its own memory (the Java shim's EventBatcher):
+ * one uint64 per event instead of 17-25 bytes of SoA, so the batch crosses
+ * PCIe 2-3x faster, and with sf_submit_packed_async the copy of batch k+1,
+ * the decision of batch k and the copy back of the verdicts of batch k-1
+ * overlap (host arrays in page-locked memory from sf_host_alloc; pageable
+ * memory works, without the overlap).
+ *   bits  0..31  resource id
+ *   bits 32..51  ts_ms - ts_base (0 .. 2^20-1 ms; time-ordered as in sf_event_batch)
+ *   bits 52..58  acquireCount 1..127; 0: the next value of count_ext
+ *   bits 59..63  flags (SF_EV_EXIT | SF_EV_IN | SF_EV_PRIO | SF_EV_ERROR | SF_EV_BLOCKED)
+ * exit_ref / exit_cts hold, for the EXIT events in batch order, what
+ * entry_ref / create_ts hold for them in sf_event_batch (create_ts read where
+ * exit_ref < 0; NULL: 0).  origin (per event) as in sf_event_batch.
+ * The verdicts are sf_verdicts in the same memory kind as the batch.        */
+#define SF_PK_COUNT_SHIFT 52
+#define SF_PK_FLAGS_SHIFT 59
+typedef struct sf_packed_batch {
+    uint32_t        n;
+    int32_t         mem;          /* SF_MEM_HOST or SF_MEM_DEVICE (all arrays)  */
+    int64_t         ts_base;
+    const uint64_t* ev;           /* [n]                                        */
+    const int64_t*  exit_ref;     /* [n_exit] or NULL when the batch has no EXIT */
+    const int64_t*  exit_cts;     /* [n_exit] or NULL                           */
+    const int32_t*  count_ext;    /* [n_count_ext] or NULL                      */
+    const uint32_t* origin;       /* [n] or NULL                                */
+    uint32_t        n_exit;
+    uint32_t        n_count_ext;
+} sf_packed_batch;
+int  sf_submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out);
+/* Enqueued only; sf_sync waits and reports the first error.  Host arrays
+ * (batch and verdicts) must stay untouched until sf_sync.                   */
+int  sf_submit_packed_async(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out);
 
 /* SystemRules on a resource-sharded node (shard_count > 1).
  * SystemRuleManager.checkSystem (SystemRuleManager.java:291-348) reads the

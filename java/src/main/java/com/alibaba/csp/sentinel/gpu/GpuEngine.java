@@ -1,5 +1,8 @@
 package com.alibaba.csp.sentinel.gpu;
 
+import com.alibaba.csp.sentinel.property.DynamicSentinelProperty;
+import com.alibaba.csp.sentinel.property.PropertyListener;
+import com.alibaba.csp.sentinel.property.SentinelProperty;
 import com.alibaba.csp.sentinel.slots.block.RuleConstant;
 import com.alibaba.csp.sentinel.slots.block.degrade.DegradeRule;
 import com.alibaba.csp.sentinel.slots.block.degrade.DegradeRuleManager;
@@ -79,7 +82,41 @@ public final class GpuEngine {
             throw new IllegalStateException(t);
         }
         batcher = new EventBatcher(this, maxBatch);
+        installRuleListeners();
         reloadRules();
+    }
+
+    /**
+     * Every FlowRuleManager / ParamFlowRuleManager / SystemRuleManager /
+     * DegradeRuleManager.loadRules reaches the engine without a manual
+     * {@link #reloadRules()}: each manager gets a fresh property through its
+     * register2Property (FlowRuleManager.java:92-100, DegradeRuleManager.java:62-70;
+     * loadRules is currentProperty.updateValue, FlowRuleManager.java:120-122), the
+     * manager's own listener first, then ours, so the rule maps are up to date
+     * when the batcher sees the new version.  An application that registers its
+     * own data-source property afterwards adds {@link #ruleListener()} to it too.
+     */
+    private void installRuleListeners() {
+        DynamicSentinelProperty<List<FlowRule>> f = new DynamicSentinelProperty<>();
+        FlowRuleManager.register2Property(f);
+        f.addListener(ruleListener());
+        DynamicSentinelProperty<List<ParamFlowRule>> p = new DynamicSentinelProperty<>();
+        ParamFlowRuleManager.register2Property(p);
+        p.addListener(ruleListener());
+        DynamicSentinelProperty<List<SystemRule>> s = new DynamicSentinelProperty<>();
+        SystemRuleManager.register2Property(s);
+        s.addListener(ruleListener());
+        DynamicSentinelProperty<List<DegradeRule>> d = new DynamicSentinelProperty<>();
+        DegradeRuleManager.register2Property(d);
+        d.addListener(ruleListener());
+    }
+
+    /** A property listener that bumps the rule version (add it to a data-source property). */
+    public <T> PropertyListener<T> ruleListener() {
+        return new PropertyListener<T>() {
+            @Override public void configUpdate(T value) { reloadRules(); }
+            @Override public void configLoad(T value) { reloadRules(); }
+        };
     }
 
     /** Dense id of a resource name (ResourceWrapper identity is the name, ResourceWrapper.java:81-95). */
@@ -119,7 +156,7 @@ public final class GpuEngine {
         }
     }
 
-    /** Called after FlowRuleManager / ParamFlowRuleManager / SystemRuleManager / DegradeRuleManager.loadRules. */
+    /** Bumps the rule version; called by the managers' property listeners (installRuleListeners). */
     public void reloadRules() {
         ruleVersion.incrementAndGet();
     }

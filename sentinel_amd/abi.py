@@ -198,7 +198,7 @@ class sf_stats(C.Structure):
                 ("heavy_fill_ms", C.c_double), ("classify_ms", C.c_double),
                 ("stream_ms", C.c_double), ("metric_scan_ms", C.c_double), ("metric_log_ms", C.c_double),
                 ("wire_ms", C.c_double), ("sys_rounds", C.c_uint64), ("aux_nodes", C.c_uint64),
-                ("aux_capacity", C.c_uint64), ("aux_index_grows", C.c_uint64)]
+                ("aux_capacity", C.c_uint64), ("aux_index_grows", C.c_uint64), ("param_table_grows", C.c_uint64)]
 
 
 class sf_heavy_profile(C.Structure):
@@ -230,6 +230,72 @@ def node_state_to_dict(st: sf_node_state, sample_count: int = 2) -> dict:
 
 def _ptr(a):
     return None if a is None else a.ctypes.data
+
+
+PK_COUNT_SHIFT, PK_FLAGS_SHIFT = 52, 59
+
+
+class sf_packed_batch(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("mem", C.c_int32), ("ts_base", C.c_int64), ("ev", C.c_void_p),
+                ("exit_ref", C.c_void_p), ("exit_cts", C.c_void_p), ("count_ext", C.c_void_p),
+                ("origin", C.c_void_p), ("n_exit", C.c_uint32), ("n_count_ext", C.c_uint32)]
+
+
+STRUCT_SIZES["sf_packed_batch"] = C.sizeof(sf_packed_batch)
+
+
+class PackedBatch:
+    """A batch in the compact form of sf_submit_packed (8 bytes per event:
+    resource | ts - ts_base << 32 | acquireCount << 52 | flags << 59, plus the
+    EXIT events' entry_ref / create_ts and the acquireCounts outside 1..127 as
+    sparse arrays).  ``alloc`` places the arrays (np.empty by default; a
+    PinnedArrays.array for page-locked memory)."""
+
+    def __init__(self, hb: "HostBatch", alloc=None):
+        alloc = alloc or (lambda shape, dtype: np.empty(shape, dtype))
+        n = hb.n
+        self.n = n
+        self.ts_base = int(hb.ts_ms[0]) if n else 0
+        d = (hb.ts_ms - self.ts_base).astype(np.int64)
+        assert n == 0 or (d.min() >= 0 and d.max() < (1 << 20)), "batch spans more than 2^20 ms"
+        c = hb.count.astype(np.int64)
+        small = (c >= 1) & (c <= 127)
+        w = hb.res_id.astype(np.uint64) | (d.astype(np.uint64) << np.uint64(32)) | \
+            (np.where(small, c, 0).astype(np.uint64) << np.uint64(PK_COUNT_SHIFT)) | \
+            ((hb.flags.astype(np.uint64) & np.uint64(0x1f)) << np.uint64(PK_FLAGS_SHIFT))
+        self.ev = alloc((n,), np.uint64)
+        self.ev[...] = w
+        ex = np.nonzero(hb.flags & EV_EXIT)[0]
+        self.n_exit = int(ex.size)
+        self.exit_ref = self.exit_cts = None
+        if ex.size:
+            self.exit_ref = alloc((ex.size,), np.int64)
+            self.exit_ref[...] = hb.entry_ref[ex] if hb.entry_ref is not None else -1
+            if hb.create_ts is not None:
+                self.exit_cts = alloc((ex.size,), np.int64)
+                self.exit_cts[...] = hb.create_ts[ex]
+        big = np.nonzero(~small)[0]
+        self.n_count_ext = int(big.size)
+        self.count_ext = None
+        if big.size:
+            self.count_ext = alloc((big.size,), np.int32)
+            self.count_ext[...] = hb.count[big]
+        self.origin = None
+        if hb.origin is not None:
+            self.origin = alloc((n,), np.uint32)
+            self.origin[...] = hb.origin
+
+    def nbytes(self) -> int:
+        return sum(a.nbytes for a in (self.ev, self.exit_ref, self.exit_cts, self.count_ext, self.origin)
+                   if a is not None)
+
+    def c_struct(self) -> sf_packed_batch:
+        b = sf_packed_batch()
+        b.n, b.mem, b.ts_base = self.n, MEM_HOST, self.ts_base
+        b.ev, b.exit_ref, b.exit_cts = _ptr(self.ev), _ptr(self.exit_ref), _ptr(self.exit_cts)
+        b.count_ext, b.origin = _ptr(self.count_ext), _ptr(self.origin)
+        b.n_exit, b.n_count_ext = self.n_exit, self.n_count_ext
+        return b
 
 
 class HostBatch:

@@ -411,6 +411,9 @@ SF_HD int can_pass(const DevRule& r, DevRuleState& s, NodeWin<MAXS>& nd, int64_t
 constexpr uint64_t PT_MAX_PROBE = 4096;
 struct ParamTable {
     ParamSlot* slots; uint64_t mask; int32_t* err;
+    // inserts counted (the host grows the table between batches, sf_engine.cpp
+    // param_reserve): 256 counters 64 B apart, one per workgroup residue
+    unsigned int* ins = nullptr;
     SF_HD static uint64_t hash(uint64_t hi, uint64_t lo) { return mix64(hi ^ mix64(lo + 0x9e3779b97f4a7c15ULL)); }
     // find slot of key; returns nullptr if absent
     SF_HD ParamSlot* find(uint64_t hi, uint64_t lo) const {
@@ -438,6 +441,7 @@ struct ParamTable {
             if (__hip_atomic_compare_exchange_strong((unsigned long long*)&slots[i].hi, &expected,
                     (unsigned long long)hi, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 slots[i].lo = lo; slots[i].a = 0; slots[i].b = 0;
+                if (ins) atomicAdd(&ins[(blockIdx.x & 255u) * 16u], 1u);
                 return &slots[i];
             }
 #else
@@ -648,7 +652,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
     const int nprules = (int)(p1 - p0);
     uint8_t pm_init = nprules ? st.pm_init[res] : 0;
     bool pm_exists = pm_init != 0;
-    ParamTable pt{st.ptab, st.pcap_mask, st.err};
+    ParamTable pt{st.ptab, st.pcap_mask, st.err, st.pins};
     uint32_t cb0, cb1;                                         // DegradeSlot breakers (this lane owns them)
     breakers_of(st, res, &cb0, &cb1);
 

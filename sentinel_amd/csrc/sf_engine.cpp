@@ -20,6 +20,7 @@
 #include "sf_wire.h"
 #include "sf_degrade.h"
 #include <rccl/rccl.h>
+#include <functional>
 #include <unordered_map>
 
 using namespace sf;
@@ -57,6 +58,10 @@ struct sf_engine {
     // rules
     std::vector<uint32_t> flow_pos;        // loaded valid rule index -> CSR position
     uint32_t n_flow = 0, n_prule = 0;
+    // the exact ParamFlow table's fill (param_reserve): inserts counted on the
+    // device (st.pins), as of the last drain; upper bound of the inserts of
+    // batches enqueued since; the most keys one event can insert
+    uint64_t p_used = 0, p_pending = 0, p_kmax = 0, p_grows = 0;
     // staging for host-memory batches
     void* stage_in = nullptr; size_t stage_in_bytes = 0;
     void* stage_out = nullptr; size_t stage_out_bytes = 0;
@@ -115,6 +120,15 @@ struct sf_engine {
     std::vector<AuxChunk> ax_host;
     AuxChunk* ax_dir = nullptr;
     uint64_t aux_grows = 0;
+    // compact batches (sf_submit_packed): per Work set, the device copy of the
+    // packed input, its SoA expansion and the verdicts copied back; copy
+    // streams so that H2D(k+1), decide(k) and D2H(k-1) overlap
+    struct PkStage {
+        char* buf = nullptr; size_t bytes = 0;
+        hipEvent_t h2d = nullptr, d2h = nullptr;
+        bool d2h_pending = false;
+    } pk[2];
+    hipStream_t h2d = nullptr, d2h = nullptr;
 };
 
 static void free_tok_work(TokWork& w) {
@@ -160,7 +174,8 @@ static void free_work(Work& w) {
                     w.acc_sec, w.acc_hw_base, w.acc_sec_base, w.seg_hw0, w.seg_sec0,
                     w.seg_nhw, w.seg_nsec, w.hticks, w.passbits, w.stream_list, w.sticks,
                     w.exit_of, w.lxfar, w.thr_rec, w.vs_cursor, w.tile_rc, w.seg_rb, w.seg_re,
-                    w.s_origin, w.s_oslot, w.ox_cnt, w.ox_bflags, w.ox_hmap, w.ox_hslot, w.ox_thr, w.ox_acc};
+                    w.s_origin, w.s_oslot, w.ox_cnt, w.ox_bflags, w.ox_hmap, w.ox_hslot, w.ox_thr, w.ox_acc,
+                    w.ox_bseg, w.ox_pairs};
     for (void* p : ptrs) if (p) hipFree(p);
     w = Work{};
 }
@@ -172,7 +187,7 @@ void sf_destroy(sf_engine* e) {
     for (Work& w : e->w) free_work(w);
     void* ptrs[] = {e->st.second, e->st.borrow, e->st.minute, e->st.threads, (void*)e->st.rule_off,
                     (void*)e->st.rules, e->st.rstate, (void*)e->st.prule_off, e->st.prules, (void*)e->st.items,
-                    e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out, e->plan_stage};
+                    e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out, e->plan_stage, e->st.pins};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     for (void* p : e->host_allocs) hipHostFree(p);
@@ -193,6 +208,13 @@ void sf_destroy(sf_engine* e) {
     void* xptrs[] = {e->xmap_buf, e->st.xtab, e->ax_dir, e->st.ax_count};
     for (void* p : xptrs) if (p) hipFree(p);
     for (const AuxChunk& c : e->ax_host) hipFree(c.sec);          // (one allocation per chunk)
+    for (auto& p : e->pk) {
+        if (p.buf) hipFree(p.buf);
+        if (p.h2d) hipEventDestroy(p.h2d);
+        if (p.d2h) hipEventDestroy(p.d2h);
+    }
+    if (e->h2d) { hipStreamSynchronize(e->h2d); hipStreamDestroy(e->h2d); }
+    if (e->d2h) { hipStreamSynchronize(e->d2h); hipStreamDestroy(e->d2h); }
     if (e->comm) ncclCommDestroy(e->comm);
     free_tok_work(e->tw);
     for (auto& a : e->evs) for (auto& x : a) if (x) hipEventDestroy(x);
@@ -261,7 +283,9 @@ static int alloc_work(sf_engine* e, Work& w) {
     }
     WALLOC(w.heavy_list, SC * 4);
     WALLOC(w.counters, 16 * 4); WALLOC(w.pcg, N * 8);
-    w.fill_tile_cap = (uint32_t)(N / FILL_TILE + 2 * (N / (w.heavy_min + 1)) + 2);   // <= len/TILE + 2 per segment
+    // <= len/TILE + 2 tiles per heavy segment; a ParamFlow-only segment of more
+    // than 32 events is heavy too (SM_PARAM, k_classify), whatever heavy_min
+    w.fill_tile_cap = (uint32_t)(N / FILL_TILE + 2 * (N / (std::min<uint32_t>(w.heavy_min, 32u) + 1)) + 2);
     WALLOC(w.fill_tiles, (size_t)2 * w.fill_tile_cap * sizeof(uint2)); WALLOC(w.fill_ntiles, 2 * 4);
     w.acc_cap = (uint32_t)std::min<size_t>(std::max<size_t>(N / w.heavy_min * 64, 1 << 16), 1u << 24);
     WALLOC(w.acc_hw, (size_t)w.acc_cap * ACC_BYTES); WALLOC(w.acc_sec, (size_t)w.acc_cap * ACC_BYTES);
@@ -277,7 +301,7 @@ static int alloc_work(sf_engine* e, Work& w) {
     WALLOC(w.tile_rc, (size_t)w.fill_tile_cap * 4); WALLOC(w.seg_rb, SC * 4); WALLOC(w.seg_re, SC * 4);
     WALLOC(w.vs_cursor, VS_CURSORS(N) * 4);
     WALLOC(w.s_origin, N * 4); WALLOC(w.s_oslot, N * 4); WALLOC(w.ox_cnt, 8 * 4);
-    WALLOC(w.ox_bflags, (N / OX_TILE + 1) * 4);
+    WALLOC(w.ox_bflags, (N / OX_TILE + 1) * 4); WALLOC(w.ox_bseg, (N / OX_TILE + 1) * 8);
     return SF_OK;
 }
 
@@ -343,6 +367,8 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     HIP_TRY(hipMemsetAsync((void*)st.prule_off, 0, (R + 1) * sizeof(uint32_t), e->stream));
     HIP_TRY(hipMemsetAsync(st.pm_init, 0, R, e->stream));
     HIP_TRY(hipMemsetAsync(st.ptab, 0, pcap * sizeof(ParamSlot), e->stream));
+    DALLOC(st.pins, 256 * 16 * sizeof(unsigned int));
+    HIP_TRY(hipMemsetAsync(st.pins, 0, 256 * 16 * sizeof(unsigned int), e->stream));
     HIP_TRY(hipMemsetAsync(st.err, 0, sizeof(int32_t), e->stream));
     HIP_TRY(launch_init_state(st, e->stream));
     e->ts.err = st.err;
@@ -408,6 +434,8 @@ static int drain(sf_engine* e) {
     if (!e->pending) return SF_OK;
     HIP_TRY(hipStreamSynchronize(e->sstream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->d2h) HIP_TRY(hipStreamSynchronize(e->d2h));
+    for (auto& p : e->pk) p.d2h_pending = false;
     int first = 0;
     for (int k = 0; k < 2; k++) {
         if (!(e->pending & (1u << k))) continue;
@@ -521,6 +549,10 @@ static int ox_maps(sf_engine* e, Work& w, bool reset, hipStream_t ss) {
 static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t ss, OxPlan* plan) {
     { const int rc = ensure_aux(e); if (rc) return rc; }
     { const int rc = ox_maps(e, w, false, ss); if (rc) return rc; }
+    if (b.origin && !w.ox_pairs) {                 // (at most one pair per event)
+        HIP_TRY(hipMalloc((void**)&w.ox_pairs, (size_t)e->cfg.max_batch * sizeof(uint4)));
+        w.ox_pairs_cap = e->cfg.max_batch;
+    }
     DevState stl = e->st;
     stl.err = w.err;
     uint32_t cnt[8] = {0};
@@ -566,6 +598,7 @@ static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t
         }
     }
     plan->n_heavy = cnt[OXC_HEAVY];
+    plan->n_pairs = cnt[OXC_PAIRS];
     int64_t t01[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(&t01[0], b.ts, 8, hipMemcpyDeviceToHost, ss));
     HIP_TRY(hipMemcpyAsync(&t01[1], b.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, ss));
@@ -697,6 +730,13 @@ int sf_load_param_rules(sf_engine* e, const sf_param_rule* rules, uint32_t n, co
     // a rule reload drops all ParameterMetric state (new ParameterMetric per resource)
     HIP_TRY(hipMemsetAsync(e->st.pm_init, 0, e->R, e->stream));
     HIP_TRY(hipMemsetAsync(e->st.ptab, 0, (e->st.pcap_mask + 1) * sizeof(ParamSlot), e->stream));
+    HIP_TRY(hipMemsetAsync(e->st.pins, 0, 256 * 16 * sizeof(unsigned int), e->stream));
+    e->p_used = e->p_pending = 0;
+    // keys one event (or one collection element) can insert: a rule key per rule
+    // (ParameterMetric token / time maps) and a thread-count key per rule's index
+    uint32_t kmax = 0;
+    for (uint32_t r = 0; r < e->R; r++) kmax = std::max(kmax, counts[r]);
+    e->p_kmax = 2ull * kmax;
     HIP_TRY(hipStreamSynchronize(e->stream));
     return SF_OK;
 }
@@ -737,8 +777,50 @@ int sf_set_system_status(sf_engine* e, double avg_load, double cpu_usage) {
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// The exact ParamFlow table never fills during a batch: before a batch with
+// ParamFlow rules, the keys it can insert at most ((events + collection
+// elements) x the most keys per event) must fit in the table's free half,
+// counting the inserts of the batches still in flight the same way.  When
+// they may not, everything drains, the device's insert counters give the
+// exact fill, and the table is rebuilt larger if it is still too small
+// (ParameterMetric's maps have no capacity in the reference apart from the
+// LRU, ParameterMetric.java:99-118, whose eviction the exact table replaces).
+static int param_reserve(sf_engine* e, uint64_t bound) {
+    if (!e->n_prule || !bound) return SF_OK;
+    const uint64_t cap = e->st.pcap_mask + 1;
+    if ((e->p_used + e->p_pending + bound) * 2 <= cap) { e->p_pending += bound; return SF_OK; }
+    { const int rc = drain(e); if (rc) return rc; }
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    std::vector<unsigned int> c(256 * 16);
+    HIP_TRY(hipMemcpy(c.data(), e->st.pins, c.size() * sizeof(unsigned int), hipMemcpyDeviceToHost));
+    uint64_t used = 0;
+    for (int k = 0; k < 256; k++) used += c[k * 16];
+    e->p_used = used;
+    e->p_pending = 0;
+    if ((used + bound) * 2 > cap) {
+        uint64_t ncap = cap * 2;
+        while ((used + bound) * 2 > ncap) ncap <<= 1;
+        ParamSlot* nt = nullptr;
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMalloc((void**)&nt, ncap * sizeof(ParamSlot)));
+        HIP_TRY(hipMemsetAsync(nt, 0, ncap * sizeof(ParamSlot), e->stream));
+        const hipError_t le = launch_ox_rehash(e->st.ptab, cap, nt, ncap - 1, e->st.err, e->stream);
+        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("param rehash: ") + hipGetErrorString(le));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        HIP_TRY(hipFree(e->st.ptab));
+        e->st.ptab = nt;
+        e->st.pcap_mask = ncap - 1;
+        e->p_grows++;
+    }
+    e->p_pending = bound;
+    return SF_OK;
+}
+
+// pre: launched on the sort stream after the batch's error flag is cleared and
+// before its sort (sf_submit_packed's expansion of the packed words)
+using PreSort = std::function<hipError_t(hipStream_t, int32_t*)>;
 static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out, bool async,
-                       const uint8_t* forced = nullptr) {
+                       const uint8_t* forced = nullptr, const PreSort* pre = nullptr) {
     if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
     if (in->n == 0) return SF_OK;
     if (!in->res_id || !in->ts_ms || !in->count || !in->flags) return fail(SF_ERR_INVALID, "missing event array");
@@ -770,6 +852,11 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     // asynchronous only for HBM-resident batches and verdicts, without SystemRules
     async = async && in->mem != SF_MEM_HOST && out->mem != SF_MEM_HOST && !e->sys.check && !forced;
     if (!async) { const int rc = drain(e); if (rc) return rc; }
+    {   // room in the ParamFlow table for every key this batch can insert
+        const uint64_t elems = in->arg_elem_off ? in->n_elems : 0;
+        const int rc = param_reserve(e, ((uint64_t)n + elems) * e->p_kmax);
+        if (rc) return rc;
+    }
     if (async && !e->w_ready[1]) {                 // second Work set on first asynchronous use
         HIP_TRY(hipStreamSynchronize(s));
         const int rc = alloc_work(e, e->w[1]);
@@ -871,6 +958,10 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
             HIP_TRY(hipMalloc((void**)&e->sys_mask, e->cfg.max_batch));
         }
         HIP_TRY(hipMemsetAsync(w.err, 0, sizeof(int32_t), ss));
+        if (pre) {
+            const hipError_t pe = (*pre)(ss, w.err);
+            if (pe != hipSuccess) return fail(SF_ERR_DEVICE, std::string("pre-sort: ") + hipGetErrorString(pe));
+        }
         HIP_TRY(hipEventRecord(e->ev_sorted[slot], ss));
         HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
         DevState stl = e->st;
@@ -930,6 +1021,10 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     // decide phase of the batch that used it last)
     if (e->used[slot]) HIP_TRY(hipStreamWaitEvent(ss, e->ev_done[slot], 0));
     HIP_TRY(hipMemsetAsync(w.err, 0, sizeof(int32_t), ss));
+    if (pre) {
+        const hipError_t pe = (*pre)(ss, w.err);
+        if (pe != hipSuccess) return fail(SF_ERR_DEVICE, std::string("pre-sort: ") + hipGetErrorString(pe));
+    }
     DevState stl = e->st;
     stl.err = w.err;
     hipError_t le = launch_sort(stl, w, b, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, ss, e->evs[slot], e->timing);
@@ -990,6 +1085,117 @@ int sf_submit_async(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     if (!e) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     return submit_core(e, in, out, true);
+}
+
+// ---------------------------------------------------------------- compact batches
+// sf_packed_batch: the packed words (and the sparse exit / count arrays) go to
+// the Work set's device stage on the H2D stream, are expanded to the SoA batch
+// on the sort stream, decided by submit_core (asynchronously when asked), and
+// the verdicts come back on the D2H stream once the batch is decided.
+static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out, bool async) {
+    if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
+    if (in->n == 0) return SF_OK;
+    if (!in->ev || (in->n_exit && !in->exit_ref) || (in->n_count_ext && !in->count_ext))
+        return fail(SF_ERR_INVALID, "missing packed arrays");
+    if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
+    std::lock_guard<std::mutex> lk(e->mu);
+    const uint32_t n = in->n;
+    const bool host_in = in->mem == SF_MEM_HOST, host_out = out->mem == SF_MEM_HOST;
+    if (!e->h2d) {
+        HIP_TRY(hipStreamCreateWithFlags(&e->h2d, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&e->d2h, hipStreamNonBlocking));
+        for (auto& p : e->pk) {
+            HIP_TRY(hipEventCreateWithFlags(&p.h2d, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&p.d2h, hipEventDisableTiming));
+        }
+    }
+    // (submit_core decides asynchronously only without SystemRules; the slot it takes is e->cur)
+    const bool core_async = async && !e->sys.check;
+    if (!core_async) { const int rc = drain(e); if (rc) return rc; }
+    const int slot = e->cur;
+    auto& pk = e->pk[slot];
+    if (e->used[slot]) HIP_TRY(hipEventSynchronize(e->ev_done[slot]));   // its batch arrays are read until then
+    if (pk.d2h_pending) { HIP_TRY(hipEventSynchronize(pk.d2h)); pk.d2h_pending = false; }
+    const size_t N = e->cfg.max_batch;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += align_up(bytes); return o; };
+    const size_t o_ev = take(N * 8), o_xr = take(N * 8), o_xc = take(N * 8), o_ce = take(N * 4), o_og = take(N * 4);
+    const size_t o_res = take(N * 4), o_ts = take(N * 8), o_cnt = take(N * 4), o_fl = take(N), o_er = take(N * 8);
+    const size_t o_ct = take(N * 8), o_tc = take((N / 4096 + 2) * 8);
+    const size_t o_st = take(N), o_wt = take(N * 4), o_ru = take(N * 2);
+    if (pk.bytes < off) {
+        if (pk.buf) hipFree(pk.buf);
+        pk.buf = nullptr; pk.bytes = 0;
+        HIP_TRY(hipMalloc((void**)&pk.buf, off));
+        pk.bytes = off;
+    }
+    char* B = pk.buf;
+    hipStream_t ss = e->serial ? e->stream : e->sstream;
+    const uint64_t* ev = in->ev; const int64_t* xr = in->exit_ref; const int64_t* xc = in->exit_cts;
+    const int32_t* ce = in->count_ext; const uint32_t* og = in->origin;
+    if (host_in) {
+        hipStream_t h = e->serial ? e->stream : e->h2d;
+        HIP_TRY(hipMemcpyAsync(B + o_ev, in->ev, (size_t)n * 8, hipMemcpyHostToDevice, h));
+        ev = (const uint64_t*)(B + o_ev);
+        if (in->n_exit) {
+            HIP_TRY(hipMemcpyAsync(B + o_xr, in->exit_ref, (size_t)in->n_exit * 8, hipMemcpyHostToDevice, h));
+            xr = (const int64_t*)(B + o_xr);
+            if (in->exit_cts) {
+                HIP_TRY(hipMemcpyAsync(B + o_xc, in->exit_cts, (size_t)in->n_exit * 8, hipMemcpyHostToDevice, h));
+                xc = (const int64_t*)(B + o_xc);
+            }
+        }
+        if (in->n_count_ext) {
+            HIP_TRY(hipMemcpyAsync(B + o_ce, in->count_ext, (size_t)in->n_count_ext * 4, hipMemcpyHostToDevice, h));
+            ce = (const int32_t*)(B + o_ce);
+        }
+        if (in->origin) {
+            HIP_TRY(hipMemcpyAsync(B + o_og, in->origin, (size_t)n * 4, hipMemcpyHostToDevice, h));
+            og = (const uint32_t*)(B + o_og);
+        }
+        HIP_TRY(hipEventRecord(pk.h2d, h));
+        HIP_TRY(hipStreamWaitEvent(ss, pk.h2d, 0));
+    }
+    const bool exits = in->n_exit != 0;
+    const int64_t base = in->ts_base;
+    const uint32_t n_exit = in->n_exit, n_cext = in->n_count_ext;
+    const PreSort expand = [=](hipStream_t st_, int32_t* err) {
+        return launch_pk_expand(ev, xr, xc, ce, base, n, n_exit, n_cext, (uint2*)(B + o_tc), (uint32_t*)(B + o_res),
+                                (int64_t*)(B + o_ts), (int32_t*)(B + o_cnt), (uint8_t*)(B + o_fl),
+                                (int64_t*)(B + o_er), exits ? (int64_t*)(B + o_ct) : nullptr, err, st_);
+    };
+    sf_event_batch eb{};
+    eb.n = n; eb.mem = SF_MEM_DEVICE;
+    eb.res_id = (const uint32_t*)(B + o_res); eb.ts_ms = (const int64_t*)(B + o_ts);
+    eb.count = (const int32_t*)(B + o_cnt); eb.flags = (const uint8_t*)(B + o_fl);
+    eb.entry_ref = exits ? (const int64_t*)(B + o_er) : nullptr;
+    eb.create_ts = exits ? (const int64_t*)(B + o_ct) : nullptr;
+    eb.origin = og;
+    sf_verdicts dv{};
+    dv.mem = SF_MEM_DEVICE;
+    dv.status = host_out ? (uint8_t*)(B + o_st) : out->status;
+    dv.wait_ms = out->wait_ms ? (host_out ? (int32_t*)(B + o_wt) : out->wait_ms) : nullptr;
+    dv.rule_idx = out->rule_idx ? (host_out ? (uint16_t*)(B + o_ru) : out->rule_idx) : nullptr;
+    const int rc = submit_core(e, &eb, &dv, core_async, nullptr, &expand);
+    if (rc) return rc;
+    if (host_out) {
+        hipStream_t d = e->serial ? e->stream : e->d2h;
+        HIP_TRY(hipStreamWaitEvent(d, e->ev_done[slot], 0));
+        HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, d));
+        if (out->wait_ms) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait_ms, (size_t)n * 4, hipMemcpyDeviceToHost, d));
+        if (out->rule_idx) HIP_TRY(hipMemcpyAsync(out->rule_idx, dv.rule_idx, (size_t)n * 2, hipMemcpyDeviceToHost, d));
+        HIP_TRY(hipEventRecord(pk.d2h, d));
+        pk.d2h_pending = true;
+        if (!core_async) { HIP_TRY(hipEventSynchronize(pk.d2h)); pk.d2h_pending = false; }
+    }
+    return SF_OK;
+}
+
+int sf_submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out) {
+    return submit_packed(e, in, out, false);
+}
+int sf_submit_packed_async(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out) {
+    return submit_packed(e, in, out, true);
 }
 
 // ---------------------------------------------------------------- node-wide SystemRule rounds
@@ -1915,6 +2121,7 @@ int sf_get_stats(sf_engine* e, sf_stats* out) {
     }
     out->aux_capacity = e->st.ax_cap;
     out->aux_index_grows = e->aux_grows;
+    out->param_table_grows = e->p_grows;
     return SF_OK;
 }
 int sf_set_timing(sf_engine* e, int enabled) {

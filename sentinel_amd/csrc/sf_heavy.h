@@ -31,7 +31,7 @@ enum : uint8_t { SM_LIGHT = 0, SM_GENERIC = 1, SM_QPS = 2, SM_WARM = 3, SM_RL = 
                  SM_PARAM = 7, SM_XFLOW = 8,
                  SM_LIGHTQ = 9 };   // short light segment of a lone QPS DefaultController rule (decide_qps_segment)
 constexpr uint32_t SEGF_PRIO = SEGF_PRIO_, SEGF_NONPOS = 2u, SEGF_SYS = SEGF_SYS_, SEGF_EXIT = 8u, SEGF_COLL = 16u;
-constexpr uint32_t SEGF_ORIGIN = 32u;   // an event carries an origin: its origin node is updated (xflow walk)
+constexpr uint32_t SEGF_ORIGIN = 32u;   // (tests/hostsim's routing model only: an event carries an origin)
 constexpr uint32_t SEGF_BIGC = 64u;     // a checked entry with acquireCount > THR_CBIG (k_thr_heads; THREAD run mode off)
 
 struct Acc {            // per (segment, window) counter deltas

@@ -88,6 +88,7 @@ struct DevState {
     uint8_t* pm_init;              // [R] bitmask: thread maps created per paramIdx (<8)
     ParamSlot* ptab;
     uint64_t pcap_mask;
+    unsigned int* pins;            // [256 * 16] inserts into ptab (ParamTable::ins), null: not counted
     int32_t* err;                  // device error word (capacity, invalid input)
     int64_t* last_fetch;           // [R] StatisticNode.lastFetchTime (metric snapshot)
     int64_t* last_ts;              // engine clock: last event time of the previous batch (time never goes back)
@@ -219,11 +220,18 @@ struct Work {
     // (THREAD run mode also borrows buffers dead after the sort: rid = keys_in,
     //  run_start = head_scan, run_pre = keys_out, entry records = pv_in; sf_kernels.hip heavy_ctx)
     uint32_t* vs_cursor;                                // [VS_CURSORS(N)] fill counts of the verdict scatter's buckets
-    // origin nodes (sf_origin.hip), batches with origins only
+    // sf_packed_batch -> SoA (sf_kernels.hip); tile_cnt: [n / 4096 + 1] uint2
+hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64_t* xcts, const int32_t* cext,
+                            int64_t base, uint32_t n, uint32_t n_exit, uint32_t n_cext, uint2* tile_cnt,
+                            uint32_t* res, int64_t* ts, int32_t* cnt, uint8_t* flags, int64_t* eref, int64_t* cts,
+                            int32_t* err, hipStream_t s);
+// origin nodes (sf_origin.hip), batches with origins only
     uint32_t* s_origin;                                 // [N] origin id in sorted order
     uint32_t* s_oslot;                                  // [N] pool slot of the event's origin node (XNONE: none)
     uint32_t* ox_cnt;                                   // [8] OXC_* counters of the index pass
     uint32_t* ox_bflags;                                // [N / OX_TILE + 1] origin work of each OX_TILE block
+    uint2* ox_bseg;                                     // [N / OX_TILE + 1] first / last segment overlapping each block
+    uint4* ox_pairs; uint32_t ox_pairs_cap;             // (pool slot, segment start, end) of each short segment's pair
     uint32_t* ox_hmap; size_t ox_hmap_n;                // [ox_hmap_n] pool slot -> heavy pair id (XNONE between batches)
     uint32_t* ox_hslot; size_t ox_hslot_n;              // [ox_hslot_n] heavy pair id -> pool slot
     int64_t* ox_thr;                                    // [ox_hslot_n] thread delta per heavy pair
@@ -232,7 +240,7 @@ struct Work {
 // origin-node pass (sf_origin.hip): a block is OX_TILE sorted positions; a
 // segment of at most OX_LIGHT events is walked whole by the block it starts in
 constexpr uint32_t OX_TILE = 2048, OX_LIGHT = 512;
-enum : int { OXC_HEAVY = 0, OXC_LIGHT_BLOCKS = 1, OXC_HEAVY_BLOCKS = 2, OXC_OVERFLOW = 3 };
+enum : int { OXC_HEAVY = 0, OXC_PAIRS = 1, OXC_OVERFLOW = 3 };
 struct OxAcc {             // one heavy pair's sums in one window; min_rt encoded for a max (0: none)
     unsigned long long pass, block, succ, rt, exc, n_touch, min_rt_key;
 };
@@ -311,14 +319,19 @@ hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipSt
 hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,
                        uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing);
 struct OxWin { int64_t w0s, w0m; uint32_t ws, wm; };    // the batch's first second / minute window and counts
-struct OxPlan { uint32_t n_heavy; OxWin win; };         // the batch's origin-node pass (sf_origin.hip)
+struct OxPlan { uint32_t n_heavy, n_pairs; OxWin win; };   // the batch's origin-node pass (sf_origin.hip)
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                          hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing,
                          const OxPlan* ox = nullptr);
+// sf_packed_batch -> SoA (sf_kernels.hip); tile_cnt: [n / 4096 + 1] uint2
+hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64_t* xcts, const int32_t* cext,
+                            int64_t base, uint32_t n, uint32_t n_exit, uint32_t n_cext, uint2* tile_cnt,
+                            uint32_t* res, int64_t* ts, int32_t* cnt, uint8_t* flags, int64_t* eref, int64_t* cts,
+                            int32_t* err, hipStream_t s);
 // origin nodes (sf_origin.hip)
 hipError_t launch_ox_index(const DevState& st, Work& w, const DevBatch& b, uint32_t lim, hipStream_t s);
-hipError_t launch_ox_apply(const DevState& st, Work& w, const DevBatch& b, uint32_t n_heavy, const OxWin& win,
-                           hipStream_t s);
+hipError_t launch_ox_apply(const DevState& st, Work& w, const DevBatch& b, uint32_t n_heavy, uint32_t n_pairs,
+                           const OxWin& win, hipStream_t s);
 hipError_t launch_ox_rehash(const ParamSlot* old_tab, uint64_t old_n, ParamSlot* new_tab, uint64_t new_mask,
                             int32_t* err, hipStream_t s);
 hipError_t launch_aux_find(const DevState& st, uint64_t hi, uint64_t lo, uint32_t* out, hipStream_t s);

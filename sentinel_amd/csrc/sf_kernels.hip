@@ -98,11 +98,10 @@ __global__ void k_unpack(DevBatch b, const void* pvv, const uint32_t* keys, uint
     if (j == b.n - 1) { *n_seg = sid + 1; seg_start[sid + 1] = b.n; }
     if (j == 0 && *err == 0) *last_ts = b.ts[b.n - 1];   // k_keys_packed of this batch has read the old value
     PackedEv v;
-    uint32_t org = SF_ORIGIN_NONE;
     if constexpr (ORG) {
         const PackedEvO vo = ((const PackedEvO*)pvv)[j];
-        v.idx = vo.idx; v.meta = vo.meta; org = vo.origin;
-        s_origin[j] = org;
+        v.idx = vo.idx; v.meta = vo.meta;
+        s_origin[j] = vo.origin;
     } else {
         v = ((const PackedEv*)pvv)[j];
     }
@@ -113,14 +112,12 @@ __global__ void k_unpack(DevBatch b, const void* pvv, const uint32_t* keys, uint
     perm[j] = i;
     s_ts[j] = dts != PV_DTS_FAR ? b.ts[0] + (int64_t)dts : b.ts[i]; s_cnt[j] = c; s_flags[j] = f;
     // segment flags (k_classify's routing): the exits (read only by the ParamFlow
-    // routing, heavy_mode), origins (ClusterBuilderSlot.java:107-110: the
-    // origin-node pass, sf_origin.hip), prioritized / non-positive /
-    // blocked-before entries; OR-ed per segment within the wavefront, one
-    // atomic per segment and wavefront
+    // routing, heavy_mode), prioritized / non-positive / blocked-before
+    // entries; OR-ed per segment within the wavefront, one atomic per segment
+    // and wavefront (origins need no flag: sf_origin.hip finds them per event)
     {
         uint32_t mine = 0;
         if (exit_marks && (f & SF_EV_EXIT)) mine |= SEGF_EXIT;
-        if (org != SF_ORIGIN_NONE) mine |= SEGF_ORIGIN;
         if (!(f & SF_EV_EXIT))
             mine |= ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) | ((f & EVF_SYSBLK) ? SEGF_SYS : 0u);
         const unsigned long long any = __ballot(mine != 0);
@@ -133,9 +130,9 @@ __global__ void k_unpack(DevBatch b, const void* pvv, const uint32_t* keys, uint
             const int nxt = after ? __ffsll((long long)after) - 1 : 64;
             const unsigned long long range = (nxt == 64 ? ~0ull : (1ull << nxt) - 1ull) & ~below;
             uint32_t acc = 0;
-            const uint32_t kinds[5] = {SEGF_EXIT, SEGF_ORIGIN, SEGF_PRIO, SEGF_NONPOS, SEGF_SYS};
+            const uint32_t kinds[4] = {SEGF_EXIT, SEGF_PRIO, SEGF_NONPOS, SEGF_SYS};
 #pragma unroll
-            for (int k = 0; k < 5; k++)
+            for (int k = 0; k < 4; k++)
                 if (__ballot(mine & kinds[k]) & range) acc |= kinds[k];
             if (((heads >> lane) & 1ull) && acc) atomicOr(&segflag[sid], acc);
         }
@@ -434,7 +431,7 @@ __device__ void heavy_param(const DevState& st, const SegIO& io, const HeavyCtx&
     const uint32_t p0 = st.prule_off[res], np = st.prule_off[res + 1] - p0;
     const int32_t pidx = st.prules[p0].param_idx;
     const uint8_t pm_init = (uint8_t)(st.pm_init[res] | (1u << pidx));   // initParamMetricsFor on the first entry
-    ParamTable pt{st.ptab, st.pcap_mask, st.err};
+    ParamTable pt{st.ptab, st.pcap_mask, st.err, st.pins};
     for (uint32_t q = lo; q < hi; q += 64) {
         const uint32_t j = q + (uint32_t)lane;
         const bool valid = j < hi;
@@ -1214,6 +1211,11 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
 #define SF_VS_PER 8
 #endif
 constexpr uint32_t VS_T = SF_VS_T, VS_PER = SF_VS_PER, VS_TILE = VS_T * VS_PER;
+// k_vs_bucket's LDS: hist / lbase / gbase (3 x 4 KiB), part, buf (4 B per record)
+// and kb (2 B per record); a record's rank in its bucket is packed in 16 bits
+static_assert(VS_TILE < 65536u, "k_vs_bucket packs a record's rank into 16 bits");
+static_assert(3u * 1024u * 4u + VS_T * 4u + VS_TILE * 4u + VS_TILE * 2u <= 65536u,
+              "k_vs_bucket LDS footprint over 64 KiB: retune SF_VS_T / SF_VS_PER");
 constexpr uint32_t VS_DIRECT_MAX = 1u << 20;        // smaller batches: one direct scatter
 
 // A (FIRST: sorted positions [blockIdx * VS_TILE, +VS_TILE) -> bucket idx >> s1)
@@ -1261,7 +1263,7 @@ __global__ void __launch_bounds__(VS_T) k_vs_bucket(const uint32_t* perm, const 
         }
     }
     __syncthreads();
-    // exclusive scan of the bucket counts (<= 4 per thread), then one claim per bucket
+    // exclusive scan of the bucket counts (ceil(nk / VS_T) per thread), then one claim per bucket
     const uint32_t per = (nk + VS_T - 1) / VS_T;
     uint32_t sum = 0;
     for (uint32_t q = 0; q < per; q++) { const uint32_t k = tid * per + q; if (k < nk) sum += hist[k]; }
@@ -1479,13 +1481,124 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     // beside the verdict scatter
     if (ox) {
         hipStreamWaitEvent(s2, ev[13], 0);
-        const hipError_t e = launch_ox_apply(st, w, b, ox->n_heavy, ox->win, s2);
+        const hipError_t e = launch_ox_apply(st, w, b, ox->n_heavy, ox->n_pairs, ox->win, s2);
         if (e != hipSuccess) return e;
         hipEventRecord(ev[14], s2);
     }
     launch_scatter(w, n, out.status, s);
     if (ox) hipStreamWaitEvent(s, ev[14], 0);
     if (timing) hipEventRecord(ev[4], s);
+    return hipGetLastError();
+}
+
+// ============================================================ compact batches
+// sf_packed_batch -> the SoA DevBatch arrays (res, ts, count, flags, entry_ref,
+// create_ts).  EXIT events and count-0 events take the next value of the
+// sparse exit_ref / exit_cts / count_ext arrays: a per-tile count, one scan of
+// the tile counts, then each tile's own scan (PK_T threads x PK_PER events).
+constexpr uint32_t PK_T = 256, PK_PER = 16, PK_TILE = PK_T * PK_PER;
+struct PkIn { const uint64_t* ev; const int64_t* xref; const int64_t* xcts; const int32_t* cext; int64_t base;
+              uint32_t n, n_exit, n_cext; };
+struct PkOut { uint32_t* res; int64_t* ts; int32_t* cnt; uint8_t* flags; int64_t* eref; int64_t* cts; };
+
+__device__ __forceinline__ uint32_t pk_flags(uint64_t w) { return (uint32_t)(w >> SF_PK_FLAGS_SHIFT) & 0x1fu; }
+__device__ __forceinline__ uint32_t pk_count(uint64_t w) { return (uint32_t)(w >> SF_PK_COUNT_SHIFT) & 0x7fu; }
+
+__global__ void __launch_bounds__(PK_T) k_pk_count(PkIn in, uint2* tile_cnt) {
+    __shared__ uint32_t sx, sc;
+    if (threadIdx.x == 0) { sx = 0; sc = 0; }
+    __syncthreads();
+    uint32_t x = 0, c = 0;
+    const uint32_t t0 = blockIdx.x * PK_TILE;
+    for (uint32_t k = 0; k < PK_PER; k++) {
+        const uint32_t i = t0 + k * PK_T + threadIdx.x;
+        if (i >= in.n) break;
+        const uint64_t w = in.ev[i];
+        x += (pk_flags(w) & SF_EV_EXIT) ? 1u : 0u;
+        c += pk_count(w) == 0 ? 1u : 0u;
+    }
+    x = (uint32_t)wave_sum(x); c = (uint32_t)wave_sum(c);
+    if ((threadIdx.x & 63) == 0) { atomicAdd(&sx, x); atomicAdd(&sc, c); }
+    __syncthreads();
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = make_uint2(sx, sc);
+}
+
+// exclusive scan of the tile counts (one workgroup); err when a sparse array is short
+__global__ void __launch_bounds__(1024) k_pk_scan(uint2* tile_cnt, uint32_t nt, PkIn in, int32_t* err) {
+    __shared__ uint32_t wx[16], wc[16];
+    __shared__ uint32_t cx, cc;
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    if (threadIdx.x == 0) { cx = 0; cc = 0; }
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < nt; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint2 v = i < nt ? tile_cnt[i] : make_uint2(0u, 0u);
+        const uint32_t ix = (uint32_t)wave_scan_add((int)v.x), ic = (uint32_t)wave_scan_add((int)v.y);
+        if (lane == 63) { wx[wv] = ix; wc[wv] = ic; }
+        __syncthreads();
+        uint32_t bx = cx, bc = cc;
+        for (int k = 0; k < wv; k++) { bx += wx[k]; bc += wc[k]; }
+        if (i < nt) tile_cnt[i] = make_uint2(bx + ix - v.x, bc + ic - v.y);
+        __syncthreads();
+        if (threadIdx.x == 1023) { cx = bx + ix; cc = bc + ic; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && (cx > in.n_exit || cc > in.n_cext)) *err = SF_ERR_INVALID;
+}
+
+__global__ void __launch_bounds__(PK_T) k_pk_expand(PkIn in, const uint2* tile_base, PkOut out) {
+    __shared__ uint32_t wx[PK_T / 64], wc[PK_T / 64];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    // a thread's PK_PER consecutive events (their order is the scan order)
+    const uint32_t i0 = blockIdx.x * PK_TILE + threadIdx.x * PK_PER;
+    uint64_t w[PK_PER];
+    uint32_t x = 0, c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PK_PER; k++) {
+        w[k] = i0 + k < in.n ? in.ev[i0 + k] : 0ull;
+        x += (i0 + k < in.n && (pk_flags(w[k]) & SF_EV_EXIT)) ? 1u : 0u;
+        c += (i0 + k < in.n && pk_count(w[k]) == 0) ? 1u : 0u;
+    }
+    const uint32_t ix = (uint32_t)wave_scan_add((int)x), ic = (uint32_t)wave_scan_add((int)c);
+    if (lane == 63) { wx[wv] = ix; wc[wv] = ic; }
+    __syncthreads();
+    const uint2 tb = tile_base[blockIdx.x];
+    uint32_t bx = tb.x + ix - x, bc = tb.y + ic - c;
+    for (int k = 0; k < wv; k++) { bx += wx[k]; bc += wc[k]; }
+#pragma unroll
+    for (uint32_t k = 0; k < PK_PER; k++) {
+        const uint32_t i = i0 + k;
+        if (i >= in.n) break;
+        const uint32_t f = pk_flags(w[k]);
+        const uint32_t c8 = pk_count(w[k]);
+        out.res[i] = (uint32_t)w[k];
+        out.ts[i] = in.base + (int64_t)((w[k] >> 32) & 0xfffffu);
+        out.flags[i] = (uint8_t)f;
+        int32_t cnt = (int32_t)c8;
+        if (!c8) { cnt = bc < in.n_cext ? in.cext[bc] : 0; bc++; }
+        out.cnt[i] = cnt;
+        if (f & SF_EV_EXIT) {
+            out.eref[i] = bx < in.n_exit ? in.xref[bx] : -1;
+            if (out.cts) out.cts[i] = (in.xcts && bx < in.n_exit) ? in.xcts[bx] : 0;
+            bx++;
+        } else {
+            out.eref[i] = -1;
+            if (out.cts) out.cts[i] = 0;
+        }
+    }
+}
+
+hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64_t* xcts, const int32_t* cext,
+                            int64_t base, uint32_t n, uint32_t n_exit, uint32_t n_cext, uint2* tile_cnt,
+                            uint32_t* res, int64_t* ts, int32_t* cnt, uint8_t* flags, int64_t* eref, int64_t* cts,
+                            int32_t* err, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const PkIn in{ev, xref, xcts, cext, base, n, n_exit, n_cext};
+    const PkOut out{res, ts, cnt, flags, eref, cts};
+    const uint32_t nt = (n + PK_TILE - 1) / PK_TILE;
+    hipLaunchKernelGGL(k_pk_count, dim3(nt), dim3(PK_T), 0, s, in, tile_cnt);
+    hipLaunchKernelGGL(k_pk_scan, dim3(1), dim3(1024), 0, s, tile_cnt, nt, in, err);
+    hipLaunchKernelGGL(k_pk_expand, dim3(nt), dim3(PK_T), 0, s, in, (const uint2*)tile_cnt, out);
     return hipGetLastError();
 }
 

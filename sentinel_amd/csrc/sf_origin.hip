@@ -13,17 +13,21 @@
 // never read while the batch is decided, so they are brought up to date after
 // the verdicts, in bulk, on the ordinary pipeline's segments:
 //
-//   sort phase   k_ox_index   every (resource, origin) key of the batch -- and
-//                             the CHAIN context keys of xflow segments -- in the
-//                             pool's index table, a pool slot for each new one
-//                             (the host then grows the pool to cover them before
-//                             the decide phase: no batch fails on capacity), the
-//                             slot of each event (s_oslot), and a dense id for
-//                             each pair of a long segment
-//   decide phase k_ox_light   segments of at most OX_LIGHT events: one thread
-//                             per (resource, origin) pair replays the pair's
-//                             events in time order on its node (NodeWin, the
-//                             lane interpreter's window code)
+//   sort phase   k_ox_ilight  segments of at most OX_LIGHT events: the distinct
+//                             (resource, origin) pairs of the segments starting in
+//                             a block (LDS), each looked up in the pool's index
+//                             table or given a new pool slot, and listed (slot,
+//                             segment) for k_ox_lapply
+//                k_ox_index   longer segments and the xflow walk's segments: the
+//                             distinct keys of a tile (and the CHAIN context keys
+//                             of xflow segments), a dense id per pair of a long
+//                             segment
+//                             (the host then grows the pool to cover every new
+//                             slot before the decide phase: no batch fails on
+//                             capacity; both passes write each event's slot, s_oslot)
+//   decide phase k_ox_lapply  one thread per listed pair replays the pair's events
+//                             in time order on its node (NodeWin, the lane
+//                             interpreter's window code)
 //                k_ox_hacc    longer segments: per-window sums of every pair of
 //                             the block (LDS), then global atomics
 //                k_ox_happly  one thread per pair of a long segment: the latest
@@ -40,11 +44,14 @@ namespace sf {
 
 constexpr int OX_T = 256;
 constexpr uint32_t OX_ITILE = 1024;            // events per k_ox_index workgroup
-constexpr uint32_t OX_KCAP = 2048;             // its LDS key table (<= 2 keys per event)
+constexpr uint32_t OX_LTILE = 1024;            // sorted positions whose segments one k_ox_ilight workgroup lists
+constexpr uint32_t OX_KCAP = 2048;             // LDS key table (k_ox_index: <= 2 keys per event; k_ox_ilight: <= 1536 keys)
 constexpr uint64_t AX_CLAIM = 1ull << 63;      // index slot being claimed (pkey_hi never sets bit 63: R < 2^30)
+constexpr uint32_t KS_CLAIMED = 0x80000000u;   // kslot: index-table position claimed this round (pool slots < 2^31)
 constexpr uint32_t HX_CLAIM = 0xfffffffeu;     // heavy id being assigned
+enum : uint32_t { OXB_LIGHT = 1u, OXB_HEAVY = 2u };
 
-// LDS key of (local resource, kind, id): nonzero
+// LDS key: (local resource, kind, id) for k_ox_index, (segment - first + 1, origin) for k_ox_ilight; nonzero
 __device__ __forceinline__ unsigned long long ox_pack(uint32_t l, uint32_t kind, uint32_t id) {
     return ((unsigned long long)(l + 1u) << 34) | ((unsigned long long)kind << 32) | id;
 }
@@ -63,205 +70,269 @@ __device__ __forceinline__ uint32_t ox_lds_insert(unsigned long long* keys, unsi
     *fresh = false;
     return XNONE;                                   // (unreachable: at most OX_KCAP keys)
 }
+__device__ __forceinline__ uint32_t ox_lds_find(const unsigned long long* keys, unsigned long long k) {
+    uint32_t h = (uint32_t)(mix64(k) & (OX_KCAP - 1));
+    for (uint32_t p = 0; p < OX_KCAP; p++) {
+        const unsigned long long cur = keys[h];
+        if (cur == k) return h;
+        if (cur == 0ull) return XNONE;
+        h = (h + 1) & (OX_KCAP - 1);
+    }
+    return XNONE;
+}
 
 struct OxIdx {
     const uint32_t* head_scan; const uint32_t* seg_start; const uint32_t* seg_res; const uint8_t* seg_mode;
-    const uint32_t* segflag; const uint32_t* perm; const uint32_t* s_origin; uint32_t* s_oslot;
+    const uint32_t* perm; const uint32_t* s_origin; uint32_t* s_oslot;
     uint32_t* hmap; uint32_t hmap_n; uint32_t* hslot; uint32_t hslot_n; uint32_t* cnt;
-    uint32_t* bflags;          // [n / OX_TILE + 1] OXB_* work of each OX_TILE block for the decide-phase kernels
+    uint32_t* bflags;          // [n / OX_TILE + 1] OXB_* work of each OX_TILE block for the decide phase
+    uint2* bseg;               // [n / OX_TILE + 1] first and last segment overlapping each OX_TILE block
+    uint4* pairs; uint32_t pairs_cap;   // k_ox_lapply's work: (pool slot, segment start, segment end)
 };
-enum : uint32_t { OXB_LIGHT = 1u, OXB_HEAVY = 2u };
 
-// One workgroup per OX_ITILE sorted events.  Keys are deduplicated in LDS;
-// each distinct key is found in the index table or claimed (CAS of the key's
-// high word with AX_CLAIM), and the claims of a round get consecutive pool
-// slots from one atomic on ax_count, then are published.  A key another
-// workgroup is claiming is retried in the next round (no thread waits on
-// another workgroup across a barrier).  Once ax_count passes `lim` (the table's
-// load limit) nothing more is claimed: OXC_OVERFLOW tells the host to grow the
-// table and run the pass again (the pass is idempotent).
-__global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxIdx ox, uint32_t lim) {
-    __shared__ unsigned long long kk[OX_KCAP];
-    __shared__ uint32_t kslot[OX_KCAP];        // pool slot, XNONE until resolved
-    __shared__ uint32_t kclaim[OX_KCAP];       // index-table position claimed this round (XNONE: none)
-    __shared__ uint32_t ul[OX_KCAP];           // LDS positions of the distinct keys
-    __shared__ uint8_t kheavy[OX_KCAP];        // a pair of a long segment (dense heavy id wanted)
-    __shared__ uint32_t nu, nclaim, base, retry, stop, bfl;
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < OX_KCAP; k += OX_T) { kk[k] = 0; kslot[k] = XNONE; kclaim[k] = XNONE; kheavy[k] = 0; }
-    if (tid == 0) { nu = 0; bfl = 0; }
-    __syncthreads();
-    const uint32_t j0 = blockIdx.x * OX_ITILE, j1 = min(b.n, j0 + OX_ITILE);
-    // 1. the keys of the tile's events
-    for (uint32_t j = j0 + tid; j < j1; j += OX_T) {
-        const uint32_t sid = ox.head_scan[j] - 1u;
-        const uint32_t lo = ox.seg_start[sid], hi = ox.seg_start[sid + 1];
-        const uint32_t o = ox.s_origin ? ox.s_origin[j] : SF_ORIGIN_NONE;
-        bool fresh;
-        if (ox.seg_mode[sid] == SM_XFLOW) {
-            // the xflow walk's nodes: the origin node of every entry with an
-            // origin, the context node while a CHAIN rule names the context
-            // (decide_xgroup's want_on / want_dn)
-            const uint32_t i = ox.perm[j];
-            const uint32_t l = b.res[i] / st.shard_count;
-            if (o != SF_ORIGIN_NONE) {
-                const uint32_t p = ox_lds_insert(kk, ox_pack(l, AX_ORIGIN, o), &fresh);
-                if (fresh) ul[atomicAdd(&nu, 1u)] = p;
-            }
-            const uint32_t ctx = b.ctx ? b.ctx[i] : 0u;
-            bool want = false;
-            for (uint32_t k = st.rule_off[l]; k < st.rule_off[l + 1]; k++)
-                if (st.rules[k].strategy == SF_STRATEGY_CHAIN && st.rules[k].ref == ctx) want = true;
-            if (want) {
-                const uint32_t p = ox_lds_insert(kk, ox_pack(l, AX_CTX, ctx), &fresh);
-                if (fresh) ul[atomicAdd(&nu, 1u)] = p;
-            }
-        } else if (o != SF_ORIGIN_NONE) {
-            const uint32_t p = ox_lds_insert(kk, ox_pack(ox.seg_res[sid], AX_ORIGIN, o), &fresh);
-            if (fresh) ul[atomicAdd(&nu, 1u)] = p;
-            if (hi - lo > OX_LIGHT) { kheavy[p] = 1; atomicOr(&bfl, OXB_HEAVY); }
-            else atomicOr(&bfl, OXB_LIGHT);           // (its segment starts in this OX_TILE block or the one before)
-        }
-    }
-    __syncthreads();
-    if (tid == 0 && bfl) {
-        // a light segment is walked by the block it starts in
-        const uint32_t blk = j0 / OX_TILE;
-        atomicOr(&ox.bflags[blk], bfl);
-        if ((bfl & OXB_LIGHT) && ox.seg_start[ox.head_scan[j0] - 1u] < blk * OX_TILE) atomicOr(&ox.bflags[blk - 1], OXB_LIGHT);
-    }
-    // 2. resolve the distinct keys against the index table, in rounds
+// Resolve a workgroup's distinct LDS keys against the index table, in rounds:
+// each unresolved key is found, or claimed (CAS of the slot's high word to the
+// key | AX_CLAIM); the round's claims get consecutive pool slots from one
+// atomic on ax_count and are then published (lo, slot, then the high word with
+// release).  A key another workgroup is claiming is tried again next round --
+// no thread waits on another workgroup across a barrier, so the claimer always
+// publishes.  Once ax_count passes `lim` (the table's load limit) nothing more
+// is claimed: OXC_OVERFLOW makes the host grow the table and run the pass again
+// (it is idempotent).  key_of(p, &hi, &lo) gives LDS position p's table key.
+template <class KeyOf>
+__device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned long long* kk, uint32_t* kslot,
+                           uint32_t lim, uint32_t* sh, KeyOf key_of) {
     ParamTable t{st.xtab, st.xcap_mask, st.err};
     const uint64_t reach = t.mask < PT_MAX_PROBE ? t.mask : PT_MAX_PROBE;
+    const uint32_t tid = threadIdx.x;
     for (;;) {
         if (tid == 0) {
-            nclaim = 0; retry = 0;
-            stop = __hip_atomic_load(st.ax_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > lim;
+            sh[0] = 0; sh[1] = 0;
+            sh[2] = __hip_atomic_load(st.ax_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > lim;
         }
         __syncthreads();
-        for (uint32_t u = tid; u < nu; u += OX_T) {
-            const uint32_t p = ul[u];
-            if (kslot[p] != XNONE) continue;
-            const unsigned long long key = kk[p];
-            const uint64_t khi = pkey_hi(ox_l(key), PK_AUX, ox_kind(key), 0), klo = (uint32_t)key;
+        const bool stop = sh[2] != 0;
+        for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+            if (!kk[p] || kslot[p] != XNONE) continue;
+            uint64_t khi, klo;
+            key_of(p, &khi, &klo);
             uint64_t i = ParamTable::hash(khi, klo) & t.mask;
-            for (uint64_t probe = 0;; ) {
+            for (uint64_t probe = 0;;) {
                 ParamSlot& s = t.slots[i];
                 const uint64_t h = __hip_atomic_load(&s.hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 if (h == 0) {
-                    if (stop) { atomicOr((uint32_t*)&ox.cnt[OXC_OVERFLOW], 1u); break; }
+                    if (stop) { atomicOr(&cnt[OXC_OVERFLOW], 1u); break; }
                     unsigned long long expected = 0;
                     if (__hip_atomic_compare_exchange_strong((unsigned long long*)&s.hi, &expected,
                                                              (unsigned long long)(khi | AX_CLAIM), __ATOMIC_ACQUIRE,
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        kclaim[p] = (uint32_t)i;
-                        atomicAdd(&nclaim, 1u);
+                        kslot[p] = KS_CLAIMED | (uint32_t)i;
+                        atomicAdd(&sh[0], 1u);
                         break;
                     }
                     continue;                          // lost the race: this slot again
                 }
-                if (h & AX_CLAIM) { retry = 1; break; }   // being claimed by another workgroup
+                if (h & AX_CLAIM) { sh[1] = 1; break; }   // being claimed by another workgroup
                 if (h == khi && s.lo == klo) { kslot[p] = (uint32_t)s.a; break; }
                 i = (i + 1) & t.mask;
-                if (++probe > reach) { atomicOr((uint32_t*)&ox.cnt[OXC_OVERFLOW], 1u); break; }
+                if (++probe > reach) { atomicOr(&cnt[OXC_OVERFLOW], 1u); break; }
             }
         }
         __syncthreads();
-        if (tid == 0 && nclaim) base = atomicAdd(st.ax_count, nclaim);
-        if (tid == 0) nclaim = 0;
+        if (tid == 0) { if (sh[0]) sh[3] = atomicAdd(st.ax_count, sh[0]); sh[0] = 0; }
         __syncthreads();
-        for (uint32_t u = tid; u < nu; u += OX_T) {
-            const uint32_t p = ul[u];
-            if (kclaim[p] == XNONE) continue;
-            ParamSlot& s = t.slots[kclaim[p]];
-            const uint32_t a = base + atomicAdd(&nclaim, 1u);
-            const unsigned long long key = kk[p];
-            s.lo = (uint32_t)key; s.a = a; s.b = 0;
-            __hip_atomic_store(&s.hi, pkey_hi(ox_l(key), PK_AUX, ox_kind(key), 0), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+            const uint32_t ks = kslot[p];
+            if (ks == XNONE || !(ks & KS_CLAIMED)) continue;
+            ParamSlot& s = t.slots[ks & ~KS_CLAIMED];
+            const uint32_t a = sh[3] + atomicAdd(&sh[0], 1u);
+            uint64_t khi, klo;
+            key_of(p, &khi, &klo);
+            s.lo = klo; s.a = a; s.b = 0;
+            __hip_atomic_store(&s.hi, khi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             kslot[p] = a;
-            kclaim[p] = XNONE;
         }
         __syncthreads();
-        if (!retry) break;
+        if (!sh[1]) break;
         __syncthreads();
     }
-    // 3. dense ids of the pairs of long segments (k_ox_hacc / k_ox_happly), same rounds
+}
+
+// k_ox_ilight: one workgroup per OX_LTILE sorted positions; the segments of at
+// most OX_LIGHT events starting there (the ordinary pipeline's, not the xflow
+// walk's).  Their distinct (resource, origin) pairs are resolved to pool slots
+// and listed with their segment for k_ox_lapply; every event of those segments
+// gets its slot.
+__global__ void __launch_bounds__(OX_T) k_ox_ilight(DevState st, DevBatch b, OxIdx ox, uint32_t lim) {
+    __shared__ unsigned long long kk[OX_KCAP];
+    __shared__ uint32_t kslot[OX_KCAP];
+    __shared__ uint16_t krank[OX_KCAP];
+    __shared__ uint32_t sh[4], nu, sA, A, span, pbase;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t j0 = blockIdx.x * OX_LTILE, jend = min(b.n, j0 + OX_LTILE);
+    for (uint32_t k = tid; k < OX_KCAP; k += OX_T) { kk[k] = 0; kslot[k] = XNONE; }
+    if (tid == 0) {
+        uint32_t s0 = ox.head_scan[j0] - 1u;
+        if (ox.seg_start[s0] < j0) s0++;               // the first segment starting in the block
+        const uint32_t s1 = ox.head_scan[jend - 1] - 1u + 1u;
+        sA = s0; nu = 0;
+        A = s0 < s1 ? ox.seg_start[s0] : 0u;
+        span = s0 < s1 ? min(ox.seg_start[s1] - A, OX_LTILE + OX_LIGHT) : 0u;
+    }
+    __syncthreads();
+    if (!span) return;
+    bool any = false;
+    for (uint32_t q = A + tid; q < A + span; q += OX_T) {
+        const uint32_t sid = ox.head_scan[q] - 1u;
+        if (ox.seg_start[sid + 1] - ox.seg_start[sid] > OX_LIGHT || ox.seg_mode[sid] == SM_XFLOW) continue;
+        const uint32_t o = ox.s_origin[q];
+        if (o == SF_ORIGIN_NONE) { ox.s_oslot[q] = XNONE; continue; }
+        bool fresh;
+        const uint32_t p = ox_lds_insert(kk, ((unsigned long long)(sid - sA + 1u) << 32) | o, &fresh);
+        if (fresh) krank[p] = (uint16_t)atomicAdd(&nu, 1u);
+        any = true;
+    }
+    if (__syncthreads_or(any) == 0) return;
+    ox_resolve(st, ox.cnt, kk, kslot, lim, sh, [&](uint32_t p, uint64_t* hi, uint64_t* lo) {
+        const unsigned long long k = kk[p];
+        *hi = pkey_hi(ox.seg_res[sA + (uint32_t)(k >> 32) - 1u], PK_AUX, AX_ORIGIN, 0);
+        *lo = (uint32_t)k;
+    });
+    if (tid == 0) pbase = atomicAdd(&ox.cnt[OXC_PAIRS], nu);
+    __syncthreads();
+    for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+        const unsigned long long k = kk[p];
+        if (!k) continue;
+        const uint32_t sid = sA + (uint32_t)(k >> 32) - 1u;
+        const uint32_t w = pbase + krank[p];
+        if (w < ox.pairs_cap) ox.pairs[w] = make_uint4(kslot[p], ox.seg_start[sid], ox.seg_start[sid + 1], 0u);
+        else atomicOr(&ox.cnt[OXC_OVERFLOW], 4u);
+    }
+    for (uint32_t q = A + tid; q < A + span; q += OX_T) {
+        const uint32_t sid = ox.head_scan[q] - 1u;
+        if (ox.seg_start[sid + 1] - ox.seg_start[sid] > OX_LIGHT || ox.seg_mode[sid] == SM_XFLOW) continue;
+        const uint32_t o = ox.s_origin[q];
+        if (o == SF_ORIGIN_NONE) continue;
+        const uint32_t p = ox_lds_find(kk, ((unsigned long long)(sid - sA + 1u) << 32) | o);
+        ox.s_oslot[q] = p != XNONE ? kslot[p] : XNONE;
+    }
+}
+
+// k_ox_index: one workgroup per OX_ITILE sorted events of the long segments and
+// of the xflow walk's segments (the light ones are k_ox_ilight's).  Long
+// segments: the pairs' slots (s_oslot) and a dense id per pair for the
+// window sums; xflow segments: every node key the walk will look up (the
+// origin node of every entry with an origin, the context node while a CHAIN
+// rule names the context: decide_xgroup's want_on / want_dn).
+__global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxIdx ox, uint32_t lim) {
+    __shared__ unsigned long long kk[OX_KCAP];
+    __shared__ uint32_t kslot[OX_KCAP];
+    __shared__ uint8_t kheavy[OX_KCAP];
+    __shared__ uint32_t sh[4], bfl;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < OX_KCAP; k += OX_T) { kk[k] = 0; kslot[k] = XNONE; kheavy[k] = 0; }
+    if (tid == 0) bfl = 0;
+    __syncthreads();
+    const uint32_t j0 = blockIdx.x * OX_ITILE, j1 = min(b.n, j0 + OX_ITILE);
+    if (tid == 0 && j0 % OX_TILE == 0) {                  // the decide phase's segment range of this OX_TILE block
+        const uint32_t je = min(b.n, j0 + OX_TILE);
+        ox.bseg[j0 / OX_TILE] = make_uint2(ox.head_scan[j0] - 1u, ox.head_scan[je - 1] - 1u);
+    }
+    bool any = false;
+    for (uint32_t j = j0 + tid; j < j1; j += OX_T) {
+        const uint32_t sid = ox.head_scan[j] - 1u;
+        const uint32_t lo = ox.seg_start[sid], hi = ox.seg_start[sid + 1];
+        const bool xf = ox.seg_mode[sid] == SM_XFLOW;
+        if (!xf && hi - lo <= OX_LIGHT) continue;          // (k_ox_ilight)
+        const uint32_t o = ox.s_origin ? ox.s_origin[j] : SF_ORIGIN_NONE;
+        bool fresh;
+        if (xf) {
+            ox.s_oslot[j] = XNONE;
+            const uint32_t i = ox.perm[j];
+            const uint32_t l = b.res[i] / st.shard_count;
+            if (o != SF_ORIGIN_NONE) { ox_lds_insert(kk, ox_pack(l, AX_ORIGIN, o), &fresh); any = true; }
+            const uint32_t ctx = b.ctx ? b.ctx[i] : 0u;
+            bool want = false;
+            for (uint32_t k = st.rule_off[l]; k < st.rule_off[l + 1]; k++)
+                if (st.rules[k].strategy == SF_STRATEGY_CHAIN && st.rules[k].ref == ctx) want = true;
+            if (want) { ox_lds_insert(kk, ox_pack(l, AX_CTX, ctx), &fresh); any = true; }
+        } else if (o != SF_ORIGIN_NONE) {
+            const uint32_t p = ox_lds_insert(kk, ox_pack(ox.seg_res[sid], AX_ORIGIN, o), &fresh);
+            kheavy[p] = 1;
+            any = true;
+        } else {
+            ox.s_oslot[j] = XNONE;
+        }
+    }
+    if (__syncthreads_or(any) == 0) return;
+    ox_resolve(st, ox.cnt, kk, kslot, lim, sh, [&](uint32_t p, uint64_t* hi, uint64_t* lo) {
+        const unsigned long long k = kk[p];
+        *hi = pkey_hi(ox_l(k), PK_AUX, ox_kind(k), 0);
+        *lo = (uint32_t)k;
+    });
+    // dense ids of the pairs of long segments (k_ox_hacc / k_ox_happly), same rounds
     for (;;) {
-        if (tid == 0) { nclaim = 0; retry = 0; }
+        if (tid == 0) { sh[0] = 0; sh[1] = 0; }
         __syncthreads();
-        for (uint32_t u = tid; u < nu; u += OX_T) {
-            const uint32_t p = ul[u];
+        for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
             const uint32_t a = kslot[p];
-            if (!kheavy[p] || a == XNONE) continue;
-            if (a >= ox.hmap_n) { atomicOr((uint32_t*)&ox.cnt[OXC_OVERFLOW], 2u); kheavy[p] = 0; continue; }
+            if (!kheavy[p] || a == XNONE || (a & KS_CLAIMED)) continue;
+            if (a >= ox.hmap_n) { atomicOr(&ox.cnt[OXC_OVERFLOW], 2u); kheavy[p] = 0; continue; }
             const uint32_t h = __hip_atomic_load(&ox.hmap[a], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
             if (h == XNONE) {
                 uint32_t expected = XNONE;
                 if (__hip_atomic_compare_exchange_strong(&ox.hmap[a], &expected, HX_CLAIM, __ATOMIC_ACQUIRE,
                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    kclaim[p] = atomicAdd(&nclaim, 1u);
+                    kheavy[p] = 2;                         // claimed: gets an id below
+                    atomicAdd(&sh[0], 1u);
                     continue;
                 }
-                retry = 1;
+                sh[1] = 1;
             } else if (h == HX_CLAIM) {
-                retry = 1;
+                sh[1] = 1;
             } else {
-                kheavy[p] = 0;                         // has its id
+                kheavy[p] = 0;                             // has its id
+                bfl = OXB_HEAVY;
             }
         }
         __syncthreads();
-        if (tid == 0 && nclaim) base = atomicAdd(&ox.cnt[OXC_HEAVY], nclaim);
+        if (tid == 0) { if (sh[0]) sh[3] = atomicAdd(&ox.cnt[OXC_HEAVY], sh[0]); sh[0] = 0; }
         __syncthreads();
-        for (uint32_t u = tid; u < nu; u += OX_T) {
-            const uint32_t p = ul[u];
-            if (kclaim[p] == XNONE) continue;
-            const uint32_t hid = base + kclaim[p];
+        for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+            if (kheavy[p] != 2) continue;
+            const uint32_t hid = sh[3] + atomicAdd(&sh[0], 1u);
             const uint32_t a = kslot[p];
             if (hid < ox.hslot_n) ox.hslot[hid] = a;
-            else atomicOr((uint32_t*)&ox.cnt[OXC_OVERFLOW], 2u);
+            else atomicOr(&ox.cnt[OXC_OVERFLOW], 2u);
             __hip_atomic_store(&ox.hmap[a], hid < ox.hslot_n ? hid : XNONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            kclaim[p] = XNONE;
             kheavy[p] = 0;
+            bfl = OXB_HEAVY;
         }
         __syncthreads();
-        if (!retry) break;
+        if (!sh[1]) break;
         __syncthreads();
     }
-    // 4. the slot of every event (ordinary segments; the xflow walk finds its own)
+    if (tid == 0 && bfl) atomicOr(&ox.bflags[j0 / OX_TILE], bfl);
+    // the slot of every event of the long segments
     for (uint32_t j = j0 + tid; j < j1; j += OX_T) {
         const uint32_t sid = ox.head_scan[j] - 1u;
+        if (ox.seg_mode[sid] == SM_XFLOW || ox.seg_start[sid + 1] - ox.seg_start[sid] <= OX_LIGHT) continue;
         const uint32_t o = ox.s_origin ? ox.s_origin[j] : SF_ORIGIN_NONE;
-        uint32_t a = XNONE;
-        if (o != SF_ORIGIN_NONE && ox.seg_mode[sid] != SM_XFLOW) {
-            bool fresh;
-            const uint32_t p = ox_lds_insert(kk, ox_pack(ox.seg_res[sid], AX_ORIGIN, o), &fresh);
-            if (p != XNONE) a = kslot[p];
-        }
-        ox.s_oslot[j] = a;
+        if (o == SF_ORIGIN_NONE) continue;
+        const uint32_t p = ox_lds_find(kk, ox_pack(ox.seg_res[sid], AX_ORIGIN, o));
+        ox.s_oslot[j] = p != XNONE ? kslot[p] : XNONE;
     }
 }
 
 // ------------------------------------------------------------------ decide phase
 struct OxRun {
-    const uint32_t* seg_start; const uint32_t* seg_res; const uint8_t* seg_mode; const uint32_t* segflag;
-    const uint32_t* n_seg;
+    const uint32_t* seg_start; const uint8_t* seg_mode;
     const int64_t* ts; const int32_t* cnt; const uint8_t* flags; const int64_t* eref; const int64_t* cts;
     const uint8_t* v_status; const uint32_t* s_oslot;
     const uint32_t* hmap; const uint32_t* hslot; OxAcc* acc; int64_t* thr;
-    const uint32_t* bflags;
+    const uint32_t* bflags; const uint2* bseg; const uint4* pairs;
     uint32_t n; OxWin win;
 };
-
-// last segment whose start is <= j
-__device__ __forceinline__ uint32_t ox_seg_of(const OxRun& r, uint32_t j) {
-    uint32_t a = 0, e = *r.n_seg;                  // seg_start[a] <= j < seg_start[e]
-    while (e - a > 1) { const uint32_t m = (a + e) >> 1; if (r.seg_start[m] <= j) a = m; else e = m; }
-    return a;
-}
-__device__ __forceinline__ bool ox_origin_seg(const OxRun& r, uint32_t s) {
-    return r.seg_mode[s] != SM_XFLOW && (r.segflag[s] & SEGF_ORIGIN);
-}
 
 // StatisticSlot's update of the origin node for sorted event j (verdict known)
 template <int MAXS>
@@ -284,68 +355,23 @@ __device__ __forceinline__ void ox_apply_event(NodeWin<MAXS>& on, const OxRun& r
     }
 }
 
-// One workgroup per OX_TILE block: the segments of at most OX_LIGHT events that
-// start in it.  Each (resource, origin) pair is owned by one thread (the first
-// to put its pool slot into the block's LDS set), which walks the pair's
-// segment in time order and applies the pair's events to the node.
-constexpr uint32_t OX_LSPAN = OX_TILE + OX_LIGHT;
+// One thread per (resource, origin) pair of a short segment (k_ox_ilight's
+// list): the node is loaded, the pair's events of the segment are applied in
+// time order, the node is stored.  No LDS: many wavefronts keep the node loads
+// of many pairs in flight.
 template <int MAXS>
-__global__ void __launch_bounds__(OX_T) k_ox_light(DevState st, OxRun r) {
-    __shared__ uint32_t lslot[OX_LSPAN];        // s_oslot of [A, A + OX_LSPAN)
-    __shared__ uint32_t sstart[OX_TILE + 2];    // starts of the block's segments (+ the end of the last)
-    __shared__ uint32_t owners[OX_LSPAN];       // owner event positions (relative to A)
-    __shared__ uint32_t owseg[OX_LSPAN];        // their segment (index into sstart)
-    __shared__ uint32_t set[2 * OX_LSPAN];      // LDS set of the pool slots (XNONE: empty)
-    __shared__ uint32_t s0, ns, nown, A;
-    constexpr uint32_t SETN = 2 * OX_LSPAN;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t j0 = blockIdx.x * OX_TILE;
-    if (j0 >= r.n || !(r.bflags[blockIdx.x] & OXB_LIGHT)) return;
-    const uint32_t jend = min(r.n, j0 + OX_TILE);
-    if (tid == 0) {
-        uint32_t s = ox_seg_of(r, j0);
-        if (r.seg_start[s] < j0) s++;                // the first segment starting in the block
-        s0 = s; nown = 0;
-        const uint32_t nseg = *r.n_seg;
-        const uint32_t e = ox_seg_of(r, jend - 1) + 1; // one past the last segment starting in the block
-        ns = e > s ? e - s : 0;
-        A = s < nseg ? r.seg_start[s] : r.n;
-    }
-    for (uint32_t k = tid; k < SETN; k += OX_T) set[k] = XNONE;
-    __syncthreads();
-    if (ns == 0) return;
-    for (uint32_t k = tid; k <= ns; k += OX_T) sstart[k] = r.seg_start[s0 + k];
-    for (uint32_t q = tid; q < OX_LSPAN; q += OX_T) lslot[q] = A + q < r.n ? r.s_oslot[A + q] : XNONE;
-    __syncthreads();
-    // owners: per event of a light origin segment, the first insert of its slot
-    const uint32_t span = min(OX_LSPAN, sstart[ns] - A);
-    for (uint32_t q = tid; q < span; q += OX_T) {
-        const uint32_t a = lslot[q];
-        if (a == XNONE) continue;
-        uint32_t lo_ = 0, hi_ = ns;                  // segment k of A + q: sstart[k] <= A + q < sstart[k + 1]
-        while (hi_ - lo_ > 1) { const uint32_t m = (lo_ + hi_) >> 1; if (sstart[m] <= A + q) lo_ = m; else hi_ = m; }
-        const uint32_t k = lo_;
-        if (sstart[k + 1] - sstart[k] > OX_LIGHT || !ox_origin_seg(r, s0 + k)) continue;
-        uint32_t h = (uint32_t)(mix64(a) % SETN);
-        for (;;) {
-            const uint32_t prev = atomicCAS(&set[h], XNONE, a);
-            if (prev == XNONE) { const uint32_t w = atomicAdd(&nown, 1u); owners[w] = q; owseg[w] = k; break; }
-            if (prev == a) break;
-            h = h + 1 == SETN ? 0 : h + 1;
-        }
-    }
-    __syncthreads();
-    for (uint32_t w = tid; w < nown; w += OX_T) {
-        const uint32_t q = owners[w], k = owseg[w];
-        const uint32_t a = lslot[q];
-        const uint32_t lo = sstart[k], hi = sstart[k + 1];
-        const NodeRows rows = aux_rows(st, a);
-        NodeWin<MAXS> on;
-        nw_load(on, st, rows);
-        for (uint32_t j = lo; j < hi; j++)                   // the pair's events in time order
-            if (lslot[j - A] == a) ox_apply_event<MAXS>(on, r, j);
-        nw_store(on, st, rows);
-    }
+__global__ void __launch_bounds__(256) k_ox_lapply(DevState st, OxRun r, uint32_t npairs) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= npairs) return;
+    const uint4 pr = r.pairs[t];
+    const uint32_t a = pr.x;
+    if (a == XNONE) return;
+    const NodeRows rows = aux_rows(st, a);
+    NodeWin<MAXS> on;
+    nw_load(on, st, rows);
+    for (uint32_t j = pr.y; j < pr.z; j++)
+        if (r.s_oslot[j] == a) ox_apply_event<MAXS>(on, r, j);
+    nw_store(on, st, rows);
 }
 
 // ---- long segments: per-window sums
@@ -357,7 +383,7 @@ __device__ __forceinline__ int64_t ox_minrt_of(unsigned long long k) {
 }
 
 constexpr uint32_t OX_HCAP = 512;                 // LDS (pair, window) rows of a k_ox_hacc block
-struct OxRow { unsigned long long key; unsigned long long v[7]; };   // key: hid << 32 | kind << 31 | window + 1
+struct OxRow { unsigned long long key; unsigned long long v[7]; };   // key: pool slot << 32 | window + 1
 
 __device__ __forceinline__ void ox_add_row(unsigned long long* v, const unsigned long long* d) {
     for (int f = 0; f < 6; f++) if (d[f]) atomicAdd(&v[f], d[f]);
@@ -365,33 +391,33 @@ __device__ __forceinline__ void ox_add_row(unsigned long long* v, const unsigned
 }
 
 // One workgroup per OX_TILE block with events of long origin segments: the
-// block's (pair, window) sums in LDS, then one set of global atomics per row.
+// block's (pair, window) sums in LDS, keyed by pool slot; at the flush each
+// row's pair id (hmap) and one set of global atomics.  Rows: the second
+// window, the minute window, the thread delta (row W).
 __global__ void __launch_bounds__(OX_T) k_ox_hacc(DevState st, OxRun r) {
     __shared__ OxRow rows[OX_HCAP];
     __shared__ uint32_t sst[OX_TILE + 1];        // starts of the segments overlapping the block, then their end
-    __shared__ uint32_t sfirst, nseg_b;
     const uint32_t tid = threadIdx.x;
     const uint32_t j0 = blockIdx.x * OX_TILE;
     if (j0 >= r.n || !(r.bflags[blockIdx.x] & OXB_HEAVY)) return;
     const uint32_t j1 = min(r.n, j0 + OX_TILE);
-    if (tid == 0) { sfirst = ox_seg_of(r, j0); nseg_b = ox_seg_of(r, j1 - 1) - sfirst + 1; }
+    const uint2 bs = r.bseg[blockIdx.x];
+    const uint32_t nsb = bs.y - bs.x + 1;
     for (uint32_t k = tid; k < OX_HCAP; k += OX_T) {
         rows[k].key = 0;
         for (int f = 0; f < 7; f++) rows[k].v[f] = 0;
     }
-    __syncthreads();
-    for (uint32_t k = tid; k <= nseg_b; k += OX_T) sst[k] = r.seg_start[sfirst + k];
+    for (uint32_t k = tid; k <= nsb; k += OX_T) sst[k] = r.seg_start[bs.x + k];
     __syncthreads();
     const uint32_t W = r.win.ws + r.win.wm;
     const int64_t b_s = r.win.w0s * st.wl, b_m = r.win.w0m * 1000;
+    const uint32_t wl = (uint32_t)st.wl;
     for (uint32_t j = j0 + tid; j < j1; j += OX_T) {
-        uint32_t a_ = 0, e_ = nseg_b;                   // sst[a_] <= j < sst[a_ + 1]
+        uint32_t a_ = 0, e_ = nsb;                      // sst[a_] <= j < sst[a_ + 1]
         while (e_ - a_ > 1) { const uint32_t m = (a_ + e_) >> 1; if (sst[m] <= j) a_ = m; else e_ = m; }
-        if (sst[a_ + 1] - sst[a_] <= OX_LIGHT || !ox_origin_seg(r, sfirst + a_)) continue;
+        if (sst[a_ + 1] - sst[a_] <= OX_LIGHT || r.seg_mode[bs.x + a_] == SM_XFLOW) continue;
         const uint32_t a = r.s_oslot[j];
         if (a == XNONE) continue;
-        const uint32_t hid = r.hmap[a];
-        if (hid == XNONE) continue;                       // (cannot happen: k_ox_index gave every such pair an id)
         const uint8_t v = r.v_status[j], fl = r.flags[j];
         const int64_t t = r.ts[j];
         const int32_t c = r.cnt[j];
@@ -415,15 +441,15 @@ __global__ void __launch_bounds__(OX_T) k_ox_hacc(DevState st, OxRun r) {
             else d[0] = (unsigned long long)(int64_t)c;
         }
         d[5] = 1;
-        const uint32_t wsec = (uint32_t)((t - b_s) / st.wl), wmin = (uint32_t)((t - b_m) / 1000);
-        // rows: the second window, the minute window, the thread delta (row W)
+        // (the batch spans less than 2^32 ms: 32-bit window arithmetic)
+        const uint32_t wsec = (uint32_t)(t - b_s) / wl, wmin = (uint32_t)(t - b_m) / 1000u;
         for (int kind = 0; kind < 3; kind++) {
             if (kind < 2 && !touch) continue;
             if (kind == 2 && !dthr) continue;
             const uint32_t w = kind == 0 ? wsec : (kind == 1 ? r.win.ws + wmin : W);
             unsigned long long dt[7] = {(unsigned long long)dthr, 0, 0, 0, 0, 0, 0};
             const unsigned long long* dd = kind == 2 ? dt : d;
-            const unsigned long long key = ((unsigned long long)hid << 32) | (w + 1u);
+            const unsigned long long key = ((unsigned long long)a << 32) | (w + 1u);
             uint32_t h = (uint32_t)(mix64(key) & (OX_HCAP - 1));
             bool done = false;
             for (uint32_t p = 0; p < 16 && !done; p++) {
@@ -432,6 +458,7 @@ __global__ void __launch_bounds__(OX_T) k_ox_hacc(DevState st, OxRun r) {
                 else h = (h + 1) & (OX_HCAP - 1);
             }
             if (!done) {                                  // LDS rows full: straight to the global sums
+                const uint32_t hid = r.hmap[a];
                 if (kind == 2) atomicAdd((unsigned long long*)&r.thr[hid], (unsigned long long)dthr);
                 else ox_add_row(&r.acc[(size_t)hid * W + w].pass, dd);   // (OxAcc fields in v[] order)
             }
@@ -441,7 +468,7 @@ __global__ void __launch_bounds__(OX_T) k_ox_hacc(DevState st, OxRun r) {
     for (uint32_t k = tid; k < OX_HCAP; k += OX_T) {
         const unsigned long long key = rows[k].key;
         if (!key) continue;
-        const uint32_t hid = (uint32_t)(key >> 32), w = (uint32_t)key - 1u;
+        const uint32_t hid = r.hmap[(uint32_t)(key >> 32)], w = (uint32_t)key - 1u;
         if (w == W) { if (rows[k].v[0]) atomicAdd((unsigned long long*)&r.thr[hid], rows[k].v[0]); }
         else ox_add_row(&r.acc[(size_t)hid * W + w].pass, rows[k].v);
     }
@@ -508,35 +535,39 @@ static inline unsigned ox_blocks(size_t n, unsigned t) { return (unsigned)((n + 
 
 hipError_t launch_ox_index(const DevState& st, Work& w, const DevBatch& b, uint32_t lim, hipStream_t s) {
     if (!b.n) return hipSuccess;
-    OxIdx ox{w.head_scan, w.seg_start, w.seg_res, w.seg_mode, w.segflag, w.perm, b.origin ? w.s_origin : nullptr,
-             w.s_oslot,
+    OxIdx ox{w.head_scan, w.seg_start, w.seg_res, w.seg_mode, w.perm, b.origin ? w.s_origin : nullptr, w.s_oslot,
              w.ox_hmap, (uint32_t)std::min<size_t>(w.ox_hmap_n, 0xffffffffu), w.ox_hslot,
-             (uint32_t)std::min<size_t>(w.ox_hslot_n, 0xffffffffu), w.ox_cnt, w.ox_bflags};
+             (uint32_t)std::min<size_t>(w.ox_hslot_n, 0xffffffffu), w.ox_cnt, w.ox_bflags, w.ox_bseg, w.ox_pairs,
+             w.ox_pairs_cap};
     hipMemsetAsync(w.ox_cnt, 0, 8 * sizeof(uint32_t), s);
     hipMemsetAsync(w.ox_bflags, 0, ((size_t)b.n / OX_TILE + 1) * sizeof(uint32_t), s);
+    if (b.origin)
+        hipLaunchKernelGGL(k_ox_ilight, dim3(ox_blocks(b.n, OX_LTILE)), dim3(OX_T), 0, s, st, b, ox, lim);
     hipLaunchKernelGGL(k_ox_index, dim3(ox_blocks(b.n, OX_ITILE)), dim3(OX_T), 0, s, st, b, ox, lim);
     return hipGetLastError();
 }
 
-hipError_t launch_ox_apply(const DevState& st, Work& w, const DevBatch& b, uint32_t n_heavy, const OxWin& win,
-                           hipStream_t s) {
+hipError_t launch_ox_apply(const DevState& st, Work& w, const DevBatch& b, uint32_t n_heavy, uint32_t n_pairs,
+                           const OxWin& win, hipStream_t s) {
     if (!b.n) return hipSuccess;
     OxRun r{};
-    r.seg_start = w.seg_start; r.seg_res = w.seg_res; r.seg_mode = w.seg_mode; r.segflag = w.segflag;
-    r.n_seg = w.n_seg;
+    r.seg_start = w.seg_start; r.seg_mode = w.seg_mode;
     r.ts = w.s_ts; r.cnt = w.s_cnt; r.flags = w.s_flags;
     r.eref = b.eref ? w.s_eref : nullptr; r.cts = b.eref ? w.s_cts : nullptr;
     r.v_status = w.v_status; r.s_oslot = w.s_oslot;
-    r.hmap = w.ox_hmap; r.hslot = w.ox_hslot; r.acc = (OxAcc*)w.ox_acc; r.thr = w.ox_thr; r.bflags = w.ox_bflags;
+    r.hmap = w.ox_hmap; r.hslot = w.ox_hslot; r.acc = (OxAcc*)w.ox_acc; r.thr = w.ox_thr;
+    r.bflags = w.ox_bflags; r.bseg = w.ox_bseg; r.pairs = w.ox_pairs;
     r.n = b.n; r.win = win;
-    const unsigned nblk = ox_blocks(b.n, OX_TILE);
-    if (st.S <= 2) hipLaunchKernelGGL(k_ox_light<2>, dim3(nblk), dim3(OX_T), 0, s, st, r);
-    else hipLaunchKernelGGL(k_ox_light<SF_MAX_SAMPLE_COUNT>, dim3(nblk), dim3(OX_T), 0, s, st, r);
+    if (n_pairs) {
+        if (st.S <= 2) hipLaunchKernelGGL(k_ox_lapply<2>, dim3(ox_blocks(n_pairs, 256)), dim3(256), 0, s, st, r, n_pairs);
+        else hipLaunchKernelGGL(k_ox_lapply<SF_MAX_SAMPLE_COUNT>, dim3(ox_blocks(n_pairs, 256)), dim3(256), 0, s, st, r,
+                                n_pairs);
+    }
     if (n_heavy) {
         const size_t W = (size_t)win.ws + win.wm;
         hipMemsetAsync(w.ox_acc, 0, (size_t)n_heavy * W * sizeof(OxAcc), s);
         hipMemsetAsync(w.ox_thr, 0, (size_t)n_heavy * sizeof(int64_t), s);
-        hipLaunchKernelGGL(k_ox_hacc, dim3(nblk), dim3(OX_T), 0, s, st, r);
+        hipLaunchKernelGGL(k_ox_hacc, dim3(ox_blocks(b.n, OX_TILE)), dim3(OX_T), 0, s, st, r);
         hipLaunchKernelGGL(k_ox_happly, dim3(ox_blocks(n_heavy, 256)), dim3(256), 0, s, st, r, w.ox_cnt + OXC_HEAVY);
         hipLaunchKernelGGL(k_ox_reset, dim3(ox_blocks(n_heavy, 256)), dim3(256), 0, s, r, w.ox_hmap,
                            w.ox_cnt + OXC_HEAVY);

@@ -86,10 +86,12 @@ SF_HD uint32_t aux_get(const DevState& st, uint32_t l, uint32_t kind, uint32_t i
     if (s) return (uint32_t)s->a;
 #ifdef __HIP_DEVICE_COMPILE__
     const uint32_t k = atomicAdd(st.ax_count, 1u);
+    if (k >= st.ax_cap) { atomicSub(st.ax_count, 1u); *st.err = SF_ERR_CAPACITY; return XNONE; }   // (saturates)
 #else
-    const uint32_t k = (*st.ax_count)++;
-#endif
+    const uint32_t k = *st.ax_count;
     if (k >= st.ax_cap) { *st.err = SF_ERR_CAPACITY; return XNONE; }
+    (*st.ax_count)++;
+#endif
     s = t.insert(hi, id);
     if (!s) return XNONE;
     s->a = k;
@@ -128,7 +130,7 @@ SF_HD int xflow_select(const DevState& st, const DevRule& r, uint32_t r0, uint32
 // first, so a RELATE read of another member always sees HBM up to date.
 template <int MAXS>
 SF_HD void decide_xgroup(const DevState& st, const SegIO& io, uint32_t lo, uint32_t hi) {
-    const ParamTable pt{st.ptab, st.pcap_mask, st.err};
+    const ParamTable pt{st.ptab, st.pcap_mask, st.err, st.pins};
     NodeWin<MAXS> cn, on, dn;
     uint32_t cl = XNONE, oi = XNONE, di = XNONE;          // nodes held in cn / on / dn
     for (uint32_t j = lo; j < hi; j++) {

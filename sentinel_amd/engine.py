@@ -63,6 +63,8 @@ def _declare(L):
     f("sf_set_system_status", I, P, C.c_double, C.c_double)
     f("sf_submit", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
     f("sf_submit_async", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
+    f("sf_submit_packed", I, P, C.POINTER(abi.sf_packed_batch), C.POINTER(abi.sf_verdicts))
+    f("sf_submit_packed_async", I, P, C.POINTER(abi.sf_packed_batch), C.POINTER(abi.sf_verdicts))
     f("sf_load_namespaces", I, P, C.POINTER(abi.sf_namespace), U32)
     f("sf_load_cluster_rules", I, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
@@ -326,6 +328,19 @@ class FlowEngine:
         v = out.c_struct()
         _check(lib().sf_submit(self.h, C.byref(b), C.byref(v)))
         return out
+
+    def submit_packed(self, batch: abi.PackedBatch, out: abi.HostVerdicts = None) -> abi.HostVerdicts:
+        """sf_submit_packed: the compact 8-B-per-event form from host memory."""
+        out = abi.HostVerdicts(batch.n) if out is None else out
+        b, v = batch.c_struct(), out.c_struct()
+        _check(lib().sf_submit_packed(self.h, C.byref(b), C.byref(v)))
+        return out
+
+    def submit_packed_async(self, batch: abi.PackedBatch, out: abi.HostVerdicts):
+        """sf_submit_packed_async: enqueued; H2D of this batch overlaps the decision of the
+        previous one and the copy back of the one before.  Arrays stay untouched until sync()."""
+        b, v = batch.c_struct(), out.c_struct()
+        _check(lib().sf_submit_packed_async(self.h, C.byref(b), C.byref(v)))
 
     def submit_device(self, batch: DeviceBatch, out: DeviceVerdicts):
         b = batch.c_struct()

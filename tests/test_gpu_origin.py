@@ -165,3 +165,27 @@ def test_gpu_origin_with_system_rule():
     finally:
         eng.close()
         ora.close()
+
+
+def test_gpu_param_table_grows_between_batches():
+    """The exact ParamFlow table from 4096 slots under four batches of
+    Zipf-drawn values (many new keys per batch): the engine rebuilds it larger
+    before a batch that could fill it (sf_engine.cpp param_reserve), so no
+    batch fails, and every verdict, wait and rule index equals the oracle's."""
+    from sentinel_amd import engine
+    rules, b = trace.param_zipf(300, 200_000, 1_000_000, duration_ms=8000, seed=41)
+    batches = [b.subset(k * 50_000, (k + 1) * 50_000) for k in range(4)]
+    cfg = abi.default_config(max_resources=300, max_batch=50_000, param_capacity=4096)
+    eng, ora = engine.FlowEngine(cfg), OracleEngine(cfg)
+    try:
+        for x in (eng, ora):
+            x.load_param_rules(rules)
+        for k, bb in enumerate(batches):
+            parity.compare_verdicts(eng.submit(bb), ora.submit(bb), f"batch {k}")
+        st = eng.stats()
+        assert st.param_table_grows >= 1
+        used = eng.param_table_stats()["used"]
+        assert used > 4096
+    finally:
+        eng.close()
+        ora.close()

@@ -1,0 +1,78 @@
+"""Compact batches (sf_submit_packed, include/sentinel_flow.h): the 8-byte
+event words and sparse EXIT / acquireCount arrays a host stages for the PCIe
+trip.  CPU: the packing is lossless (numpy unpack of abi.PackedBatch).  GPU:
+packed batches -- synchronous, and asynchronous with H2D / decide / D2H
+overlapped over page-locked buffers -- give the verdicts and node state of the
+same batches submitted as SoA, against the oracle."""
+import numpy as np
+import pytest
+
+from sentinel_amd import abi, trace
+
+
+def _unpack(pb: abi.PackedBatch):
+    w = pb.ev
+    res = (w & np.uint64(0xffffffff)).astype(np.uint32)
+    ts = pb.ts_base + ((w >> np.uint64(32)) & np.uint64(0xfffff)).astype(np.int64)
+    c = ((w >> np.uint64(abi.PK_COUNT_SHIFT)) & np.uint64(0x7f)).astype(np.int32)
+    fl = ((w >> np.uint64(abi.PK_FLAGS_SHIFT)) & np.uint64(0x1f)).astype(np.uint8)
+    if pb.n_count_ext:
+        c[c == 0] = pb.count_ext
+    return res, ts, c, fl
+
+
+def _batch(seed=3, R=500, n=40_000):
+    hb = trace.mixed_zipf(R, n, duration_ms=3000, seed=seed)
+    rng = np.random.default_rng(seed)
+    cnt = hb.count.copy()
+    ent = np.nonzero((hb.flags & abi.EV_EXIT) == 0)[0]
+    cnt[ent[rng.random(ent.size) < 0.01]] = 300                  # outside 1..127: count_ext
+    return abi.HostBatch(hb.res_id, hb.ts_ms, cnt, hb.flags, entry_ref=hb.entry_ref), R
+
+
+def test_packing_roundtrip():
+    hb, _ = _batch()
+    pb = abi.PackedBatch(hb)
+    res, ts, c, fl = _unpack(pb)
+    assert np.array_equal(res, hb.res_id) and np.array_equal(ts, hb.ts_ms)
+    assert np.array_equal(c, hb.count) and np.array_equal(fl, hb.flags)
+    ex = np.nonzero(hb.flags & abi.EV_EXIT)[0]
+    assert np.array_equal(pb.exit_ref, hb.entry_ref[ex])
+    assert pb.nbytes() < 0.45 * (hb.n * 25)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("async_", [False, True])
+def test_gpu_packed_equals_oracle(async_):
+    from oracle.oracle import OracleEngine
+    from sentinel_amd import engine
+    from tests import parity
+    hb, R = _batch(seed=5, R=800, n=120_000)
+    hb = trace.with_origins(hb, n_origins=8, seed=6)
+    rules = trace.mixed_rules(R, seed=5)
+    cuts = [0, 40_000, 80_000, hb.n]
+    parts = [hb.subset(cuts[k], cuts[k + 1]) for k in range(3)]
+    cfg = abi.default_config(max_resources=R, max_batch=max(p.n for p in parts))
+    eng, ora = engine.FlowEngine(cfg), OracleEngine(cfg)
+    pin = engine.PinnedArrays(eng)
+    try:
+        for x in (eng, ora):
+            x.load_flow_rules(rules)
+        pbs = [abi.PackedBatch(p, alloc=pin.array) for p in parts]
+        outs = [pin.verdicts(p.n) for p in parts]
+        if async_:
+            for pb, o in zip(pbs, outs):
+                eng.submit_packed_async(pb, o)
+            eng.sync()
+        else:
+            for pb, o in zip(pbs, outs):
+                eng.submit_packed(pb, o)
+        for k, (p, o) in enumerate(zip(parts, outs)):
+            parity.compare_verdicts(o, ora.submit(p), f"batch {k}")
+        per_res = np.bincount(hb.res_id, minlength=R)
+        parity.compare_nodes(eng, ora, np.argsort(-per_res)[:40])
+        parity.compare_entry_node(eng, ora)
+    finally:
+        pin.free()
+        eng.close()
+        ora.close()
