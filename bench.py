@@ -46,11 +46,17 @@ def main():
     ap.add_argument("--no-degrade", action="store_true")
     ap.add_argument("--no-legs", action="store_true", help="skip the config2 / config4 / config5 / end-to-end legs")
     ap.add_argument("--legs", default="", help="comma-separated subset of the legs to run (default: all)")
+    ap.add_argument("--predict-ranks", type=int, default=0,
+                    help="predict the N-GPU run on this one GPU: build the node-wide N-component trace on the host, "
+                         "time the shard of the rank holding the Zipf head and of the lightest rank (one JSON line)")
     ap.add_argument("--origin-variants", default="no_origin_rules,other_rules_1pct",
                     help="config3_origin leg: the variants to run")
     ap.add_argument("--heavy-min", type=int, default=0,
                     help="segments of more events than this go to the heavy kernels (0: the engine default, 512)")
     args = ap.parse_args()
+    if args.predict_ranks > 1:
+        predict_ranks(args)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -387,6 +393,109 @@ def node_trace(R_total, n, world, rank, dist):
     er = er[mo]
     er = np.where(er >= 0, newpos[np.clip(er, 0, None)], -1)
     return abi.HostBatch(res[mo], ts[mo], cnt[mo], fl[mo], entry_ref=er)
+
+
+def predict_ranks(args, steps=None, warmup=None):
+    """The N-GPU run predicted on one GPU: the node-wide trace of bench.py's
+    N-rank mode (N config-3 components of 2^27 events over all resources,
+    seeds 3..3+N-1, merged in time order, hash-sharded res % N) is built on
+    this host without a process group, and the shards of two ranks are timed
+    like the headline step (HBM-resident, time-shifted batches pipelined): the
+    rank holding the Zipf head (the most events) and the lightest one.  With
+    weak scaling the N-rank step is the slowest rank's, so the implied 1 -> N
+    efficiency is the single-GPU config-3 step over the head rank's step."""
+    N, R = args.predict_ranks, args.resources
+    steps, warmup = steps or args.steps, warmup or args.warmup
+    t0 = time.time()
+    grade_all, beh_all, count_all = trace.mixed_rule_table(R, seed=3)
+    parts = {}
+    counts = None
+    node_entries = 0
+    single = None
+    for c in range(N):
+        comp = trace.mixed_zipf(R, args.events, duration_ms=DURATION_MS, seed=3 + c)
+        node_entries += int(((comp.flags & abi.EV_EXIT) == 0).sum())
+        if c == 0:                                               # the single-GPU step of the same run
+            single = time_shard(comp, abi.flow_rules_np(np.arange(R, dtype=np.uint32), grade_all, count_all,
+                                                        beh_all), R, 1, 0, steps, warmup)
+            log(f"[predict] single GPU: {single:.2f} ms/step")
+        rk = (comp.res_id % N).astype(np.int64)
+        if counts is None:
+            counts = np.bincount(rk, minlength=N).astype(np.int64) * N       # (component 0 scaled: the choice)
+            head = int(np.argmax(counts)); light = int(np.argmin(counts))
+            chosen = [head, light] if light != head else [head]
+        for r in chosen:
+            sel = np.nonzero(rk == r)[0]
+            pos = np.full(comp.n, -1, np.int64)
+            pos[sel] = np.arange(sel.size)
+            er = comp.entry_ref[sel]
+            er = np.where(er >= 0, pos[np.clip(er, 0, None)], -1)
+            parts.setdefault(r, []).append((comp.res_id[sel], comp.ts_ms[sel], comp.count[sel], comp.flags[sel], er))
+        del comp, rk
+        log(f"[predict] component {c + 1}/{N} in {time.time() - t0:.0f}s")
+    out = {"metric": METRIC, "mode": f"predict {N} ranks on one GPU", "n_ranks": N, "resources": R,
+           "component_events": args.events, "steps": steps, "warmup": warmup, "ranks": {}}
+    for r in chosen:
+        ps = parts.pop(r)
+        sizes = [p_[0].size for p_ in ps]
+        off = np.concatenate([[0], np.cumsum(sizes)])[:-1]
+        res = np.concatenate([p_[0] for p_ in ps]); ts = np.concatenate([p_[1] for p_ in ps])
+        cnt = np.concatenate([p_[2] for p_ in ps]); fl = np.concatenate([p_[3] for p_ in ps])
+        er = np.concatenate([np.where(p_[4] >= 0, p_[4] + o, -1) for p_, o in zip(ps, off)])
+        del ps
+        key = (ts - trace.T0).astype(np.uint16 if DURATION_MS < 65536 else np.uint32)
+        mo = np.argsort(key, kind="stable")                      # time order; a millisecond keeps component order
+        newpos = np.empty(mo.size, np.int64)
+        newpos[mo] = np.arange(mo.size)
+        er = er[mo]
+        er = np.where(er >= 0, newpos[np.clip(er, 0, None)], -1)
+        hb = abi.HostBatch(res[mo], ts[mo], cnt[mo], fl[mo], entry_ref=er)
+        del res, ts, cnt, fl, er, mo, newpos, key
+        mine = np.arange(r, R, N, dtype=np.uint32)
+        rules = abi.flow_rules_np(mine, grade_all[mine], count_all[mine], beh_all[mine])
+        R_local = (R - r + N - 1) // N
+        n_entry = int(((hb.flags & abi.EV_EXIT) == 0).sum())
+        log(f"[predict] rank {r}: {hb.n} events, t={time.time() - t0:.0f}s")
+        ms = time_shard(hb, rules, R_local, N, r, steps, warmup)
+        out["ranks"][str(r)] = {"role": "head (most events)" if r == chosen[0] else "lightest", "events": int(hb.n),
+                                "entries": int(n_entry), "ms_per_step": round(ms, 3),
+                                "events_vs_mean": round(hb.n / (N * args.events / N), 3)}
+        log(f"[predict] rank {r}: {ms:.2f} ms/step")
+        del hb
+    out["expected_events_per_rank"] = {str(k): int(v) for k, v in enumerate(counts)}
+    head_ms = out["ranks"][str(chosen[0])]["ms_per_step"]
+    out["single_gpu_ms_per_step"] = round(single, 3)
+    out["node_step_ms"] = head_ms
+    out["node_decisions_per_s"] = round(node_entries / (head_ms / 1e3), 1)
+    out["implied_efficiency"] = round(single / head_ms, 4)
+    out["note"] = ("weak scaling: every rank decides its shard of one node-wide trace (N x 2^27 events); the node "
+                   "step is the slowest rank's; implied efficiency = single-GPU step / head-rank step")
+    print(json.dumps(out), flush=True)
+
+
+def time_shard(hb, rules, R_local, N, r, steps, warmup):
+    """ms/step of one rank's shard: HBM-resident batches, pipelined as the headline run."""
+    eng = engine.FlowEngine(abi.default_config(max_resources=R_local, max_batch=hb.n, shard_count=N, shard_index=r))
+    try:
+        eng.load_flow_rules(rules)
+        base = engine.DeviceBatch(eng, hb)
+        bl = [base] + [engine.DeviceBatch.with_ts(eng, base, hb.ts_ms + k * DURATION_MS)
+                       for k in range(1, steps + warmup)]
+        ov = engine.DeviceVerdicts(eng, hb.n, with_wait=True, with_rule=False)
+        for k in range(warmup):
+            eng.submit_device_async(bl[k], ov)
+        eng.sync()
+        t = time.perf_counter()
+        for k in range(warmup, warmup + steps):
+            eng.submit_device_async(bl[k], ov)
+        eng.sync()
+        ms = (time.perf_counter() - t) / steps * 1e3
+        for b in bl:
+            b.free()
+        ov.free()
+        return ms
+    finally:
+        eng.close()
 
 
 def config3_origin_leg(hb, rules, R, c3_ms, steps=5, warmup=2, parity=True, n_origins=64,

@@ -175,7 +175,7 @@ static void free_work(Work& w) {
                     w.seg_nhw, w.seg_nsec, w.hticks, w.passbits, w.stream_list, w.sticks,
                     w.exit_of, w.lxfar, w.thr_rec, w.vs_cursor, w.tile_rc, w.seg_rb, w.seg_re,
                     w.s_origin, w.s_oslot, w.ox_cnt, w.ox_bflags, w.ox_hmap, w.ox_hslot, w.ox_thr, w.ox_acc,
-                    w.ox_bseg, w.ox_pairs};
+                    w.ox_bseg, w.ox_pairs, w.ox_plist};
     for (void* p : ptrs) if (p) hipFree(p);
     w = Work{};
 }
@@ -551,6 +551,7 @@ static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t
     { const int rc = ox_maps(e, w, false, ss); if (rc) return rc; }
     if (b.origin && !w.ox_pairs) {                 // (at most one pair per event)
         HIP_TRY(hipMalloc((void**)&w.ox_pairs, (size_t)e->cfg.max_batch * sizeof(uint4)));
+        HIP_TRY(hipMalloc((void**)&w.ox_plist, (size_t)e->cfg.max_batch * sizeof(uint32_t)));
         w.ox_pairs_cap = e->cfg.max_batch;
     }
     DevState stl = e->st;
@@ -570,9 +571,11 @@ static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t
         HIP_TRY(hipStreamSynchronize(ss));
         if (!cnt[OXC_OVERFLOW]) break;
         if (round > 12) return fail(SF_ERR_CAPACITY, "origin / context node index cannot grow");
-        // the table filled: everything drains, the table grows, the pass runs again
+        // no room for the keys: everything drains, the table grows to the keys
+        // reserved (every absent key counted, by each workgroup that missed it),
+        // the pass runs again
         HIP_TRY(hipDeviceSynchronize());
-        { const int rc = index_grow(e, (uint64_t)ax + b.n); if (rc) return rc; }
+        { const int rc = index_grow(e, std::max<uint64_t>((uint64_t)cnt[OXC_RESERVED], ax) * 3 / 2); if (rc) return rc; }
         { const int rc = ox_maps(e, w, true, ss); if (rc) return rc; }
     }
     { const int rc = pool_grow(e, ax); if (rc) return rc; }

@@ -231,7 +231,8 @@ hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64
     uint32_t* ox_cnt;                                   // [8] OXC_* counters of the index pass
     uint32_t* ox_bflags;                                // [N / OX_TILE + 1] origin work of each OX_TILE block
     uint2* ox_bseg;                                     // [N / OX_TILE + 1] first / last segment overlapping each block
-    uint4* ox_pairs; uint32_t ox_pairs_cap;             // (pool slot, segment start, end) of each short segment's pair
+    uint4* ox_pairs; uint32_t ox_pairs_cap;             // (pool slot, plist start, end) of each short segment's pair
+    uint32_t* ox_plist;                                 // [ox_pairs_cap] the pairs' events (sorted positions) in time order
     uint32_t* ox_hmap; size_t ox_hmap_n;                // [ox_hmap_n] pool slot -> heavy pair id (XNONE between batches)
     uint32_t* ox_hslot; size_t ox_hslot_n;              // [ox_hslot_n] heavy pair id -> pool slot
     int64_t* ox_thr;                                    // [ox_hslot_n] thread delta per heavy pair
@@ -240,7 +241,7 @@ hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64
 // origin-node pass (sf_origin.hip): a block is OX_TILE sorted positions; a
 // segment of at most OX_LIGHT events is walked whole by the block it starts in
 constexpr uint32_t OX_TILE = 2048, OX_LIGHT = 512;
-enum : int { OXC_HEAVY = 0, OXC_PAIRS = 1, OXC_OVERFLOW = 3 };
+enum : int { OXC_HEAVY = 0, OXC_PAIRS = 1, OXC_PLIST = 2, OXC_OVERFLOW = 3, OXC_RESERVED = 4 };
 struct OxAcc {             // one heavy pair's sums in one window; min_rt encoded for a max (0: none)
     unsigned long long pass, block, succ, rt, exc, n_touch, min_rt_key;
 };

@@ -1546,41 +1546,37 @@ __global__ void __launch_bounds__(1024) k_pk_scan(uint2* tile_cnt, uint32_t nt, 
     if (threadIdx.x == 0 && (cx > in.n_exit || cc > in.n_cext)) *err = SF_ERR_INVALID;
 }
 
+// coalesced: round k of a tile holds events t0 + 256 k + thread, scanned in
+// that (batch) order with a carry from round to round
 __global__ void __launch_bounds__(PK_T) k_pk_expand(PkIn in, const uint2* tile_base, PkOut out) {
     __shared__ uint32_t wx[PK_T / 64], wc[PK_T / 64];
     const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
-    // a thread's PK_PER consecutive events (their order is the scan order)
-    const uint32_t i0 = blockIdx.x * PK_TILE + threadIdx.x * PK_PER;
-    uint64_t w[PK_PER];
-    uint32_t x = 0, c = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < PK_PER; k++) {
-        w[k] = i0 + k < in.n ? in.ev[i0 + k] : 0ull;
-        x += (i0 + k < in.n && (pk_flags(w[k]) & SF_EV_EXIT)) ? 1u : 0u;
-        c += (i0 + k < in.n && pk_count(w[k]) == 0) ? 1u : 0u;
-    }
-    const uint32_t ix = (uint32_t)wave_scan_add((int)x), ic = (uint32_t)wave_scan_add((int)c);
-    if (lane == 63) { wx[wv] = ix; wc[wv] = ic; }
-    __syncthreads();
     const uint2 tb = tile_base[blockIdx.x];
-    uint32_t bx = tb.x + ix - x, bc = tb.y + ic - c;
-    for (int k = 0; k < wv; k++) { bx += wx[k]; bc += wc[k]; }
-#pragma unroll
+    uint32_t cx = tb.x, cc = tb.y;
     for (uint32_t k = 0; k < PK_PER; k++) {
-        const uint32_t i = i0 + k;
-        if (i >= in.n) break;
-        const uint32_t f = pk_flags(w[k]);
-        const uint32_t c8 = pk_count(w[k]);
-        out.res[i] = (uint32_t)w[k];
-        out.ts[i] = in.base + (int64_t)((w[k] >> 32) & 0xfffffu);
+        const uint32_t i = blockIdx.x * PK_TILE + k * PK_T + threadIdx.x;
+        const bool in_b = i < in.n;
+        const uint64_t w = in_b ? in.ev[i] : 0ull;
+        const uint32_t f = pk_flags(w), c8 = pk_count(w);
+        const uint32_t x = (in_b && (f & SF_EV_EXIT)) ? 1u : 0u, c = (in_b && c8 == 0) ? 1u : 0u;
+        const uint32_t ix = (uint32_t)wave_scan_add((int)x), ic = (uint32_t)wave_scan_add((int)c);
+        if (lane == 63) { wx[wv] = ix; wc[wv] = ic; }
+        __syncthreads();
+        uint32_t bx = cx + ix - x, bc = cc + ic - c, tx = 0, tc = 0;
+        for (int q = 0; q < PK_T / 64; q++) {
+            if (q < wv) { bx += wx[q]; bc += wc[q]; }
+            tx += wx[q]; tc += wc[q];
+        }
+        __syncthreads();
+        cx += tx; cc += tc;
+        if (!in_b) continue;
+        out.res[i] = (uint32_t)w;
+        out.ts[i] = in.base + (int64_t)((w >> 32) & 0xfffffu);
         out.flags[i] = (uint8_t)f;
-        int32_t cnt = (int32_t)c8;
-        if (!c8) { cnt = bc < in.n_cext ? in.cext[bc] : 0; bc++; }
-        out.cnt[i] = cnt;
+        out.cnt[i] = c8 ? (int32_t)c8 : (bc < in.n_cext ? in.cext[bc] : 0);
         if (f & SF_EV_EXIT) {
             out.eref[i] = bx < in.n_exit ? in.xref[bx] : -1;
             if (out.cts) out.cts[i] = (in.xcts && bx < in.n_exit) ? in.xcts[bx] : 0;
-            bx++;
         } else {
             out.eref[i] = -1;
             if (out.cts) out.cts[i] = 0;

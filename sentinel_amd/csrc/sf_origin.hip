@@ -37,6 +37,8 @@
 //                             the thread delta
 #include <cstring>
 
+#include <rocprim/block/block_radix_sort.hpp>
+
 #include "sf_heavy.h"
 #include "sf_xflow.h"
 
@@ -87,31 +89,57 @@ struct OxIdx {
     uint32_t* hmap; uint32_t hmap_n; uint32_t* hslot; uint32_t hslot_n; uint32_t* cnt;
     uint32_t* bflags;          // [n / OX_TILE + 1] OXB_* work of each OX_TILE block for the decide phase
     uint2* bseg;               // [n / OX_TILE + 1] first and last segment overlapping each OX_TILE block
-    uint4* pairs; uint32_t pairs_cap;   // k_ox_lapply's work: (pool slot, segment start, segment end)
+    uint4* pairs; uint32_t pairs_cap;   // k_ox_lapply's work: (pool slot, plist start, plist end)
+    uint32_t* plist; uint32_t plist_cap; // each pair's events (sorted positions), in time order
 };
 
-// Resolve a workgroup's distinct LDS keys against the index table, in rounds:
-// each unresolved key is found, or claimed (CAS of the slot's high word to the
-// key | AX_CLAIM); the round's claims get consecutive pool slots from one
-// atomic on ax_count and are then published (lo, slot, then the high word with
-// release).  A key another workgroup is claiming is tried again next round --
-// no thread waits on another workgroup across a barrier, so the claimer always
-// publishes.  Once ax_count passes `lim` (the table's load limit) nothing more
-// is claimed: OXC_OVERFLOW makes the host grow the table and run the pass again
-// (it is idempotent).  key_of(p, &hi, &lo) gives LDS position p's table key.
+// Resolve a workgroup's distinct LDS keys against the index table.  First a
+// find of every key (a probe stops at the key or at an empty slot); the
+// workgroup then reserves room for the keys it did not find with one atomic on
+// OXC_RESERVED (the table's keys plus every reservation so far): past `lim`
+// (the table's load limit) it claims nothing and sets OXC_OVERFLOW, and the
+// host grows the table to the reserved total and runs the pass again (it is
+// idempotent).  Otherwise the absent keys are claimed in rounds (CAS of the
+// slot's high word to the key | AX_CLAIM); a round's claims get consecutive
+// pool slots from one atomic on ax_count and are then published (lo, slot, the
+// high word with release).  A key another workgroup is claiming is tried again
+// next round -- no thread waits on another workgroup across a barrier, so a
+// claimer always publishes.  key_of(p, &hi, &lo) gives LDS position p's key.
 template <class KeyOf>
 __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned long long* kk, uint32_t* kslot,
                            uint32_t lim, uint32_t* sh, KeyOf key_of) {
     ParamTable t{st.xtab, st.xcap_mask, st.err};
     const uint64_t reach = t.mask < PT_MAX_PROBE ? t.mask : PT_MAX_PROBE;
     const uint32_t tid = threadIdx.x;
-    for (;;) {
-        if (tid == 0) {
-            sh[0] = 0; sh[1] = 0;
-            sh[2] = __hip_atomic_load(st.ax_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > lim;
+    if (tid == 0) sh[0] = 0;
+    __syncthreads();
+    for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {            // 1. find
+        if (!kk[p] || kslot[p] != XNONE) continue;
+        uint64_t khi, klo;
+        key_of(p, &khi, &klo);
+        uint64_t i = ParamTable::hash(khi, klo) & t.mask;
+        for (uint64_t probe = 0; probe <= reach; probe++) {
+            const ParamSlot& s = t.slots[i];
+            const uint64_t h = __hip_atomic_load(&s.hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (h == 0 || (h & AX_CLAIM)) break;               // absent (or being inserted: next rounds)
+            if (h == khi && s.lo == klo) { kslot[p] = (uint32_t)s.a; break; }
+            i = (i + 1) & t.mask;
         }
+        if (kslot[p] == XNONE) atomicAdd(&sh[0], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        sh[2] = 0;
+        if (sh[0]) {
+            const uint32_t r = atomicAdd(&cnt[OXC_RESERVED], sh[0]);
+            if ((uint64_t)r + sh[0] > lim) { sh[2] = 1; atomicOr(&cnt[OXC_OVERFLOW], 1u); }
+        }
+    }
+    __syncthreads();
+    if (!sh[0] || sh[2]) return;                                 // all found, or no room: the host grows the table
+    for (;;) {                                                   // 2. claim the absent keys, in rounds
+        if (tid == 0) { sh[0] = 0; sh[1] = 0; }
         __syncthreads();
-        const bool stop = sh[2] != 0;
         for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
             if (!kk[p] || kslot[p] != XNONE) continue;
             uint64_t khi, klo;
@@ -121,7 +149,6 @@ __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned lon
                 ParamSlot& s = t.slots[i];
                 const uint64_t h = __hip_atomic_load(&s.hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 if (h == 0) {
-                    if (stop) { atomicOr(&cnt[OXC_OVERFLOW], 1u); break; }
                     unsigned long long expected = 0;
                     if (__hip_atomic_compare_exchange_strong((unsigned long long*)&s.hi, &expected,
                                                              (unsigned long long)(khi | AX_CLAIM), __ATOMIC_ACQUIRE,
@@ -160,14 +187,22 @@ __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned lon
 
 // k_ox_ilight: one workgroup per OX_LTILE sorted positions; the segments of at
 // most OX_LIGHT events starting there (the ordinary pipeline's, not the xflow
-// walk's).  Their distinct (resource, origin) pairs are resolved to pool slots
-// and listed with their segment for k_ox_lapply; every event of those segments
-// gets its slot.
+// walk's).  Their distinct (resource, origin) pairs are resolved to pool
+// slots; a block radix sort of (pair rank, position) lists each pair's events
+// in time order (plist), and each pair is recorded (slot, its plist range) for
+// k_ox_lapply.
+constexpr uint32_t OX_LSPAN = OX_LTILE + OX_LIGHT;            // <= 1536 events of the block's light segments
+constexpr uint32_t OX_SORT_ITEMS = 8;                          // block radix sort: 256 x 8 >= OX_LSPAN
+static_assert(OX_T * OX_SORT_ITEMS >= OX_LSPAN && OX_LSPAN <= 2048, "k_ox_ilight: (rank, position) keys of 11 bits");
+using OxBlockSort = rocprim::block_radix_sort<uint32_t, OX_T, OX_SORT_ITEMS>;
 __global__ void __launch_bounds__(OX_T) k_ox_ilight(DevState st, DevBatch b, OxIdx ox, uint32_t lim) {
     __shared__ unsigned long long kk[OX_KCAP];
     __shared__ uint32_t kslot[OX_KCAP];
     __shared__ uint16_t krank[OX_KCAP];
-    __shared__ uint32_t sh[4], nu, sA, A, span, pbase;
+    __shared__ uint16_t rpos[OX_LSPAN];                        // pair rank -> LDS key position
+    __shared__ uint32_t sorted[OX_T * OX_SORT_ITEMS];
+    __shared__ typename OxBlockSort::storage_type sort_tmp;
+    __shared__ uint32_t sh[4], nu, nev, sA, A, span, pbase, lbase;
     const uint32_t tid = threadIdx.x;
     const uint32_t j0 = blockIdx.x * OX_LTILE, jend = min(b.n, j0 + OX_LTILE);
     for (uint32_t k = tid; k < OX_KCAP; k += OX_T) { kk[k] = 0; kslot[k] = XNONE; }
@@ -175,46 +210,66 @@ __global__ void __launch_bounds__(OX_T) k_ox_ilight(DevState st, DevBatch b, OxI
         uint32_t s0 = ox.head_scan[j0] - 1u;
         if (ox.seg_start[s0] < j0) s0++;               // the first segment starting in the block
         const uint32_t s1 = ox.head_scan[jend - 1] - 1u + 1u;
-        sA = s0; nu = 0;
+        sA = s0; nu = 0; nev = 0;
         A = s0 < s1 ? ox.seg_start[s0] : 0u;
-        span = s0 < s1 ? min(ox.seg_start[s1] - A, OX_LTILE + OX_LIGHT) : 0u;
+        span = s0 < s1 ? min(ox.seg_start[s1] - A, OX_LSPAN) : 0u;
     }
     __syncthreads();
     if (!span) return;
+    // the pairs and each event's (pair, position) sort key
+    uint32_t key8[OX_SORT_ITEMS];
+#pragma unroll
+    for (uint32_t k = 0; k < OX_SORT_ITEMS; k++) key8[k] = 0xffffffffu;
     bool any = false;
-    for (uint32_t q = A + tid; q < A + span; q += OX_T) {
+#pragma unroll
+    for (uint32_t k = 0; k < OX_SORT_ITEMS; k++) {
+        const uint32_t q = A + k * OX_T + tid;
+        if (k * OX_T + tid >= span) continue;
         const uint32_t sid = ox.head_scan[q] - 1u;
         if (ox.seg_start[sid + 1] - ox.seg_start[sid] > OX_LIGHT || ox.seg_mode[sid] == SM_XFLOW) continue;
         const uint32_t o = ox.s_origin[q];
         if (o == SF_ORIGIN_NONE) { ox.s_oslot[q] = XNONE; continue; }
         bool fresh;
         const uint32_t p = ox_lds_insert(kk, ((unsigned long long)(sid - sA + 1u) << 32) | o, &fresh);
-        if (fresh) krank[p] = (uint16_t)atomicAdd(&nu, 1u);
+        if (fresh) { const uint32_t r = atomicAdd(&nu, 1u); krank[p] = (uint16_t)r; rpos[r] = (uint16_t)p; }
         any = true;
     }
     if (__syncthreads_or(any) == 0) return;
-    ox_resolve(st, ox.cnt, kk, kslot, lim, sh, [&](uint32_t p, uint64_t* hi, uint64_t* lo) {
-        const unsigned long long k = kk[p];
-        *hi = pkey_hi(ox.seg_res[sA + (uint32_t)(k >> 32) - 1u], PK_AUX, AX_ORIGIN, 0);
-        *lo = (uint32_t)k;
-    });
-    if (tid == 0) pbase = atomicAdd(&ox.cnt[OXC_PAIRS], nu);
-    __syncthreads();
-    for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
-        const unsigned long long k = kk[p];
-        if (!k) continue;
-        const uint32_t sid = sA + (uint32_t)(k >> 32) - 1u;
-        const uint32_t w = pbase + krank[p];
-        if (w < ox.pairs_cap) ox.pairs[w] = make_uint4(kslot[p], ox.seg_start[sid], ox.seg_start[sid + 1], 0u);
-        else atomicOr(&ox.cnt[OXC_OVERFLOW], 4u);
-    }
-    for (uint32_t q = A + tid; q < A + span; q += OX_T) {
+#pragma unroll
+    for (uint32_t k = 0; k < OX_SORT_ITEMS; k++) {
+        const uint32_t q = A + k * OX_T + tid;
+        if (k * OX_T + tid >= span) continue;
         const uint32_t sid = ox.head_scan[q] - 1u;
         if (ox.seg_start[sid + 1] - ox.seg_start[sid] > OX_LIGHT || ox.seg_mode[sid] == SM_XFLOW) continue;
         const uint32_t o = ox.s_origin[q];
         if (o == SF_ORIGIN_NONE) continue;
         const uint32_t p = ox_lds_find(kk, ((unsigned long long)(sid - sA + 1u) << 32) | o);
-        ox.s_oslot[q] = p != XNONE ? kslot[p] : XNONE;
+        key8[k] = ((uint32_t)krank[p] << 11) | (q - A);
+        atomicAdd(&nev, 1u);
+    }
+    ox_resolve(st, ox.cnt, kk, kslot, lim, sh, [&](uint32_t p, uint64_t* hi, uint64_t* lo) {
+        const unsigned long long k = kk[p];
+        *hi = pkey_hi(ox.seg_res[sA + (uint32_t)(k >> 32) - 1u], PK_AUX, AX_ORIGIN, 0);
+        *lo = (uint32_t)k;
+    });
+    // each pair's events, in time order: sort by (rank, position)
+    OxBlockSort().sort(key8, sort_tmp, 0, 22);
+#pragma unroll
+    for (uint32_t k = 0; k < OX_SORT_ITEMS; k++) sorted[tid * OX_SORT_ITEMS + k] = key8[k];
+    if (tid == 0) { pbase = atomicAdd(&ox.cnt[OXC_PAIRS], nu); lbase = atomicAdd(&ox.cnt[OXC_PLIST], nev); }
+    __syncthreads();
+    for (uint32_t i = tid; i < nev; i += OX_T) {
+        const uint32_t k = sorted[i], r = k >> 11, q = A + (k & 2047u);
+        if (lbase + i < ox.plist_cap) ox.plist[lbase + i] = q;
+        const uint32_t a = kslot[rpos[r]];
+        ox.s_oslot[q] = a;
+        if (i == 0 || (sorted[i - 1] >> 11) != r) {           // the pair's first event: its record
+            uint32_t e = i + 1;
+            while (e < nev && (sorted[e] >> 11) == r) e++;
+            if (pbase + r < ox.pairs_cap && lbase + e <= ox.plist_cap)
+                ox.pairs[pbase + r] = make_uint4(a, lbase + i, lbase + e, 0u);
+            else atomicOr(&ox.cnt[OXC_OVERFLOW], 4u);
+        }
     }
 }
 
@@ -330,7 +385,7 @@ struct OxRun {
     const int64_t* ts; const int32_t* cnt; const uint8_t* flags; const int64_t* eref; const int64_t* cts;
     const uint8_t* v_status; const uint32_t* s_oslot;
     const uint32_t* hmap; const uint32_t* hslot; OxAcc* acc; int64_t* thr;
-    const uint32_t* bflags; const uint2* bseg; const uint4* pairs;
+    const uint32_t* bflags; const uint2* bseg; const uint4* pairs; const uint32_t* plist;
     uint32_t n; OxWin win;
 };
 
@@ -369,8 +424,7 @@ __global__ void __launch_bounds__(256) k_ox_lapply(DevState st, OxRun r, uint32_
     const NodeRows rows = aux_rows(st, a);
     NodeWin<MAXS> on;
     nw_load(on, st, rows);
-    for (uint32_t j = pr.y; j < pr.z; j++)
-        if (r.s_oslot[j] == a) ox_apply_event<MAXS>(on, r, j);
+    for (uint32_t k = pr.y; k < pr.z; k++) ox_apply_event<MAXS>(on, r, r.plist[k]);
     nw_store(on, st, rows);
 }
 
@@ -538,8 +592,10 @@ hipError_t launch_ox_index(const DevState& st, Work& w, const DevBatch& b, uint3
     OxIdx ox{w.head_scan, w.seg_start, w.seg_res, w.seg_mode, w.perm, b.origin ? w.s_origin : nullptr, w.s_oslot,
              w.ox_hmap, (uint32_t)std::min<size_t>(w.ox_hmap_n, 0xffffffffu), w.ox_hslot,
              (uint32_t)std::min<size_t>(w.ox_hslot_n, 0xffffffffu), w.ox_cnt, w.ox_bflags, w.ox_bseg, w.ox_pairs,
-             w.ox_pairs_cap};
+             w.ox_pairs_cap, w.ox_plist, w.ox_pairs_cap};
     hipMemsetAsync(w.ox_cnt, 0, 8 * sizeof(uint32_t), s);
+    // (reservations start from the table's key count: every pool slot is one key)
+    hipMemcpyAsync(w.ox_cnt + OXC_RESERVED, st.ax_count, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
     hipMemsetAsync(w.ox_bflags, 0, ((size_t)b.n / OX_TILE + 1) * sizeof(uint32_t), s);
     if (b.origin)
         hipLaunchKernelGGL(k_ox_ilight, dim3(ox_blocks(b.n, OX_LTILE)), dim3(OX_T), 0, s, st, b, ox, lim);
@@ -556,7 +612,7 @@ hipError_t launch_ox_apply(const DevState& st, Work& w, const DevBatch& b, uint3
     r.eref = b.eref ? w.s_eref : nullptr; r.cts = b.eref ? w.s_cts : nullptr;
     r.v_status = w.v_status; r.s_oslot = w.s_oslot;
     r.hmap = w.ox_hmap; r.hslot = w.ox_hslot; r.acc = (OxAcc*)w.ox_acc; r.thr = w.ox_thr;
-    r.bflags = w.ox_bflags; r.bseg = w.ox_bseg; r.pairs = w.ox_pairs;
+    r.bflags = w.ox_bflags; r.bseg = w.ox_bseg; r.pairs = w.ox_pairs; r.plist = w.ox_plist;
     r.n = b.n; r.win = win;
     if (n_pairs) {
         if (st.S <= 2) hipLaunchKernelGGL(k_ox_lapply<2>, dim3(ox_blocks(n_pairs, 256)), dim3(256), 0, s, st, r, n_pairs);
