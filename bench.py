@@ -420,6 +420,9 @@ def predict_ranks(args, steps=None, warmup=None):
                                                         beh_all), R, 1, 0, steps, warmup)
             log(f"[predict] single GPU: {single:.2f} ms/step")
         rk = (comp.res_id % N).astype(np.int64)
+        if c == 0:
+            sens = shard_share_sensitivity(np.bincount(comp.res_id, minlength=R), N)
+            log(f"[predict] shard shares: {sens}")
         if counts is None:
             counts = np.bincount(rk, minlength=N).astype(np.int64) * N       # (component 0 scaled: the choice)
             head = int(np.argmax(counts)); light = int(np.argmin(counts))
@@ -468,9 +471,40 @@ def predict_ranks(args, steps=None, warmup=None):
     out["node_step_ms"] = head_ms
     out["node_decisions_per_s"] = round(node_entries / (head_ms / 1e3), 1)
     out["implied_efficiency"] = round(single / head_ms, 4)
+    # the same step under a hash of the resource name instead of the trace's
+    # round-robin rank map: the head rank's time scaled by its share (time ~ events)
+    out["shard_share"] = sens
+    for q in ("p50", "p99"):
+        f = sens[f"random_hash_max_share_{q}"] / sens["trace_map_max_share"]
+        out[f"implied_efficiency_random_hash_{q}"] = round(single / (head_ms * f), 4)
     out["note"] = ("weak scaling: every rank decides its shard of one node-wide trace (N x 2^27 events); the node "
                    "step is the slowest rank's; implied efficiency = single-GPU step / head-rank step")
     print(json.dumps(out), flush=True)
+
+
+def shard_share_sensitivity(per_res, N, K=1000, top=20000, seed=5):
+    """How the busiest shard's share of the events depends on the id -> shard
+    map.  trace.scramble maps popularity rank k to k * a mod R with a = 1 mod 8
+    and 8 | R, so res % N == rank % N: the ranks are dealt round-robin, the
+    head shard holds ranks 0, N, 2N, ...  A hash of the resource name (what
+    a deployment shards by) deals the busiest resources at random instead.
+    The max shard share for the trace's map and its distribution over K
+    random assignments of the `top` busiest resources (the rest split evenly)."""
+    per_res = np.asarray(per_res, np.float64)
+    total = per_res.sum()
+    order = np.argsort(-per_res)[:top]
+    head = per_res[order]
+    rest = (total - head.sum()) / N
+    cur = np.bincount((order % N).astype(np.int64), weights=head, minlength=N) + rest
+    rng = np.random.default_rng(seed)
+    mx = np.empty(K)
+    for k in range(K):
+        mx[k] = (np.bincount(rng.integers(0, N, top), weights=head, minlength=N) + rest).max()
+    return {"trace_map_max_share": round(float(cur.max() / total), 4),
+            "random_hash_max_share_p50": round(float(np.percentile(mx, 50) / total), 4),
+            "random_hash_max_share_p90": round(float(np.percentile(mx, 90) / total), 4),
+            "random_hash_max_share_p99": round(float(np.percentile(mx, 99) / total), 4),
+            "even_share": round(1.0 / N, 4)}
 
 
 def time_shard(hb, rules, R_local, N, r, steps, warmup):

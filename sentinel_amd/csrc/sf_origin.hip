@@ -15,16 +15,18 @@
 //
 //   sort phase   k_ox_ilight  segments of at most OX_LIGHT events: the distinct
 //                             (resource, origin) pairs of the segments starting in
-//                             a block (LDS), each looked up in the pool's index
-//                             table or given a new pool slot, and listed (slot,
-//                             segment) for k_ox_lapply
+//                             a block (LDS) and each pair's events in time order
+//                             (block radix sort), listed for the next two kernels
+//                k_ox_lfind   one thread per listed pair: its pool slot from the
+//                             index table, or a new one
 //                k_ox_index   longer segments and the xflow walk's segments: the
 //                             distinct keys of a tile (and the CHAIN context keys
-//                             of xflow segments), a dense id per pair of a long
-//                             segment
+//                             of xflow segments) resolved per workgroup, a dense
+//                             id per pair of a long segment, each event's slot
+//                             (s_oslot)
 //                             (the host then grows the pool to cover every new
 //                             slot before the decide phase: no batch fails on
-//                             capacity; both passes write each event's slot, s_oslot)
+//                             capacity)
 //   decide phase k_ox_lapply  one thread per listed pair replays the pair's events
 //                             in time order on its node (NodeWin, the lane
 //                             interpreter's window code)
@@ -113,17 +115,50 @@ __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned lon
     const uint32_t tid = threadIdx.x;
     if (tid == 0) sh[0] = 0;
     __syncthreads();
-    for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {            // 1. find
+    // 1. find: the probes read the high words only, relaxed (no cache
+    // invalidation per probe); one acquire fence per thread, then the low word
+    // and slot of each candidate (a high word seen published by a release
+    // store: the fence makes the publisher's earlier stores visible).  A
+    // candidate of the same resource and another origin continues the probe
+    // with acquire loads (rare).
+    uint64_t cand[OX_KCAP / OX_T];
+    bool any_cand = false;
+#pragma unroll
+    for (uint32_t k = 0; k < OX_KCAP / OX_T; k++) {
+        const uint32_t p = k * OX_T + tid;
+        cand[k] = ~0ull;
         if (!kk[p] || kslot[p] != XNONE) continue;
         uint64_t khi, klo;
         key_of(p, &khi, &klo);
         uint64_t i = ParamTable::hash(khi, klo) & t.mask;
         for (uint64_t probe = 0; probe <= reach; probe++) {
-            const ParamSlot& s = t.slots[i];
-            const uint64_t h = __hip_atomic_load(&s.hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t h = __hip_atomic_load(&t.slots[i].hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (h == 0 || (h & AX_CLAIM)) break;               // absent (or being inserted: next rounds)
-            if (h == khi && s.lo == klo) { kslot[p] = (uint32_t)s.a; break; }
+            if (h == khi) { cand[k] = i; any_cand = true; break; }
             i = (i + 1) & t.mask;
+        }
+    }
+    if (any_cand) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+    for (uint32_t k = 0; k < OX_KCAP / OX_T; k++) {
+        const uint32_t p = k * OX_T + tid;
+        if (!kk[p] || kslot[p] != XNONE) continue;
+        if (cand[k] != ~0ull) {
+            uint64_t khi, klo;
+            key_of(p, &khi, &klo);
+            uint64_t i = cand[k];
+            if (t.slots[i].lo == klo) {
+                kslot[p] = (uint32_t)t.slots[i].a;
+            } else {
+                i = (i + 1) & t.mask;
+                for (uint64_t probe = 0; probe <= reach; probe++) {
+                    const ParamSlot& s = t.slots[i];
+                    const uint64_t h = __hip_atomic_load(&s.hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    if (h == 0 || (h & AX_CLAIM)) break;
+                    if (h == khi && s.lo == klo) { kslot[p] = (uint32_t)s.a; break; }
+                    i = (i + 1) & t.mask;
+                }
+            }
         }
         if (kslot[p] == XNONE) atomicAdd(&sh[0], 1u);
     }
@@ -187,25 +222,24 @@ __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned lon
 
 // k_ox_ilight: one workgroup per OX_LTILE sorted positions; the segments of at
 // most OX_LIGHT events starting there (the ordinary pipeline's, not the xflow
-// walk's).  Their distinct (resource, origin) pairs are resolved to pool
-// slots; a block radix sort of (pair rank, position) lists each pair's events
-// in time order (plist), and each pair is recorded (slot, its plist range) for
-// k_ox_lapply.
+// walk's).  A block radix sort of (pair rank, position) lists each distinct
+// (resource, origin) pair's events in time order (plist), and each pair is
+// recorded (resource, plist range, origin) for k_ox_lfind / k_ox_lapply.  No
+// index-table access here: the lookups are k_ox_lfind's, one thread per pair.
 constexpr uint32_t OX_LSPAN = OX_LTILE + OX_LIGHT;            // <= 1536 events of the block's light segments
 constexpr uint32_t OX_SORT_ITEMS = 8;                          // block radix sort: 256 x 8 >= OX_LSPAN
 static_assert(OX_T * OX_SORT_ITEMS >= OX_LSPAN && OX_LSPAN <= 2048, "k_ox_ilight: (rank, position) keys of 11 bits");
 using OxBlockSort = rocprim::block_radix_sort<uint32_t, OX_T, OX_SORT_ITEMS>;
-__global__ void __launch_bounds__(OX_T) k_ox_ilight(DevState st, DevBatch b, OxIdx ox, uint32_t lim) {
+__global__ void __launch_bounds__(OX_T) k_ox_ilight(DevBatch b, OxIdx ox) {
     __shared__ unsigned long long kk[OX_KCAP];
-    __shared__ uint32_t kslot[OX_KCAP];
     __shared__ uint16_t krank[OX_KCAP];
     __shared__ uint16_t rpos[OX_LSPAN];                        // pair rank -> LDS key position
     __shared__ uint32_t sorted[OX_T * OX_SORT_ITEMS];
     __shared__ typename OxBlockSort::storage_type sort_tmp;
-    __shared__ uint32_t sh[4], nu, nev, sA, A, span, pbase, lbase;
+    __shared__ uint32_t nu, nev, sA, A, span, pbase, lbase;
     const uint32_t tid = threadIdx.x;
     const uint32_t j0 = blockIdx.x * OX_LTILE, jend = min(b.n, j0 + OX_LTILE);
-    for (uint32_t k = tid; k < OX_KCAP; k += OX_T) { kk[k] = 0; kslot[k] = XNONE; }
+    for (uint32_t k = tid; k < OX_KCAP; k += OX_T) kk[k] = 0;
     if (tid == 0) {
         uint32_t s0 = ox.head_scan[j0] - 1u;
         if (ox.seg_start[s0] < j0) s0++;               // the first segment starting in the block
@@ -218,8 +252,9 @@ __global__ void __launch_bounds__(OX_T) k_ox_ilight(DevState st, DevBatch b, OxI
     if (!span) return;
     // the pairs and each event's (pair, position) sort key
     uint32_t key8[OX_SORT_ITEMS];
+    uint32_t kp[OX_SORT_ITEMS];
 #pragma unroll
-    for (uint32_t k = 0; k < OX_SORT_ITEMS; k++) key8[k] = 0xffffffffu;
+    for (uint32_t k = 0; k < OX_SORT_ITEMS; k++) { key8[k] = 0xffffffffu; kp[k] = XNONE; }
     bool any = false;
 #pragma unroll
     for (uint32_t k = 0; k < OX_SORT_ITEMS; k++) {
@@ -228,30 +263,19 @@ __global__ void __launch_bounds__(OX_T) k_ox_ilight(DevState st, DevBatch b, OxI
         const uint32_t sid = ox.head_scan[q] - 1u;
         if (ox.seg_start[sid + 1] - ox.seg_start[sid] > OX_LIGHT || ox.seg_mode[sid] == SM_XFLOW) continue;
         const uint32_t o = ox.s_origin[q];
-        if (o == SF_ORIGIN_NONE) { ox.s_oslot[q] = XNONE; continue; }
+        if (o == SF_ORIGIN_NONE) continue;
         bool fresh;
         const uint32_t p = ox_lds_insert(kk, ((unsigned long long)(sid - sA + 1u) << 32) | o, &fresh);
         if (fresh) { const uint32_t r = atomicAdd(&nu, 1u); krank[p] = (uint16_t)r; rpos[r] = (uint16_t)p; }
+        kp[k] = p;
         any = true;
     }
     if (__syncthreads_or(any) == 0) return;
+    uint32_t mine = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < OX_SORT_ITEMS; k++) {
-        const uint32_t q = A + k * OX_T + tid;
-        if (k * OX_T + tid >= span) continue;
-        const uint32_t sid = ox.head_scan[q] - 1u;
-        if (ox.seg_start[sid + 1] - ox.seg_start[sid] > OX_LIGHT || ox.seg_mode[sid] == SM_XFLOW) continue;
-        const uint32_t o = ox.s_origin[q];
-        if (o == SF_ORIGIN_NONE) continue;
-        const uint32_t p = ox_lds_find(kk, ((unsigned long long)(sid - sA + 1u) << 32) | o);
-        key8[k] = ((uint32_t)krank[p] << 11) | (q - A);
-        atomicAdd(&nev, 1u);
-    }
-    ox_resolve(st, ox.cnt, kk, kslot, lim, sh, [&](uint32_t p, uint64_t* hi, uint64_t* lo) {
-        const unsigned long long k = kk[p];
-        *hi = pkey_hi(ox.seg_res[sA + (uint32_t)(k >> 32) - 1u], PK_AUX, AX_ORIGIN, 0);
-        *lo = (uint32_t)k;
-    });
+    for (uint32_t k = 0; k < OX_SORT_ITEMS; k++)
+        if (kp[k] != XNONE) { key8[k] = ((uint32_t)krank[kp[k]] << 11) | (k * OX_T + tid); mine++; }
+    if (mine) atomicAdd(&nev, mine);
     // each pair's events, in time order: sort by (rank, position)
     OxBlockSort().sort(key8, sort_tmp, 0, 22);
 #pragma unroll
@@ -261,15 +285,67 @@ __global__ void __launch_bounds__(OX_T) k_ox_ilight(DevState st, DevBatch b, OxI
     for (uint32_t i = tid; i < nev; i += OX_T) {
         const uint32_t k = sorted[i], r = k >> 11, q = A + (k & 2047u);
         if (lbase + i < ox.plist_cap) ox.plist[lbase + i] = q;
-        const uint32_t a = kslot[rpos[r]];
-        ox.s_oslot[q] = a;
         if (i == 0 || (sorted[i - 1] >> 11) != r) {           // the pair's first event: its record
             uint32_t e = i + 1;
             while (e < nev && (sorted[e] >> 11) == r) e++;
+            const unsigned long long key = kk[rpos[r]];
             if (pbase + r < ox.pairs_cap && lbase + e <= ox.plist_cap)
-                ox.pairs[pbase + r] = make_uint4(a, lbase + i, lbase + e, 0u);
+                ox.pairs[pbase + r] = make_uint4(ox.seg_res[sA + (uint32_t)(key >> 32) - 1u], lbase + i, lbase + e,
+                                                 (uint32_t)key);
             else atomicOr(&ox.cnt[OXC_OVERFLOW], 4u);
         }
+    }
+}
+
+// k_ox_lfind: one thread per pair of k_ox_ilight's list (grid-stride): the
+// pair's origin node in the index table, or a new pool slot for it.  The
+// pairs are distinct keys (a resource's segment lies in one k_ox_ilight block,
+// which lists each of its origins once), so no two threads insert the same
+// key; a thread reserves room first (OXC_RESERVED against the load limit, as
+// in ox_resolve), then claims an empty slot (high word | AX_CLAIM), takes a
+// pool slot and publishes -- all in the same loop iteration, so a lane that
+// meets a claimed slot of its own resource (another origin being inserted)
+// only ever waits for a claimer that is not waiting itself.  Writes the pool
+// slot over the record's resource (XNONE when unresolved: overflow, the host
+// grows the table and the sort-phase passes run again).
+__global__ void __launch_bounds__(256) k_ox_lfind(DevState st, uint4* pairs, uint32_t* cnt, uint32_t lim) {
+    ParamTable t{st.xtab, st.xcap_mask, st.err};
+    const uint64_t reach = t.mask < PT_MAX_PROBE ? t.mask : PT_MAX_PROBE;
+    const uint32_t np = min(cnt[OXC_PAIRS], 0xffffffffu);
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x) {
+        const uint4 pr = pairs[q];
+        const uint64_t khi = pkey_hi(pr.x, PK_AUX, AX_ORIGIN, 0), klo = pr.w;
+        uint64_t i = ParamTable::hash(khi, klo) & t.mask;
+        uint32_t a = XNONE;
+        bool reserved = false, done = false;
+        for (uint64_t probe = 0; !done;) {
+            ParamSlot& s = t.slots[i];
+            const uint64_t h = __hip_atomic_load(&s.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (h == 0) {
+                if (!reserved) {
+                    if (atomicAdd(&cnt[OXC_RESERVED], 1u) >= lim) { atomicOr(&cnt[OXC_OVERFLOW], 1u); done = true; continue; }
+                    reserved = true;
+                }
+                unsigned long long expected = 0;
+                if (__hip_atomic_compare_exchange_strong((unsigned long long*)&s.hi, &expected,
+                                                         (unsigned long long)(khi | AX_CLAIM), __ATOMIC_ACQUIRE,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    a = atomicAdd(st.ax_count, 1u);
+                    s.lo = klo; s.a = a; s.b = 0;
+                    __hip_atomic_store(&s.hi, khi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    done = true;
+                }
+                continue;                                   // lost the race: this slot again
+            }
+            if (h == (khi | AX_CLAIM)) continue;            // same resource, another origin being published
+            if (h == khi) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // (the publisher's lo / a before its release of hi)
+                if (s.lo == klo) { a = (uint32_t)s.a; done = true; continue; }
+            }
+            i = (i + 1) & t.mask;
+            if (++probe > reach) { atomicOr(&cnt[OXC_OVERFLOW], 1u); done = true; }
+        }
+        pairs[q].x = a;
     }
 }
 
@@ -294,7 +370,12 @@ __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxId
         ox.bseg[j0 / OX_TILE] = make_uint2(ox.head_scan[j0] - 1u, ox.head_scan[je - 1] - 1u);
     }
     bool any = false;
-    for (uint32_t j = j0 + tid; j < j1; j += OX_T) {
+    uint32_t kp[OX_ITILE / OX_T];                         // LDS key position of each of this thread's long-segment events
+#pragma unroll
+    for (uint32_t k = 0; k < OX_ITILE / OX_T; k++) {
+        const uint32_t j = j0 + k * OX_T + tid;
+        kp[k] = XNONE;
+        if (j >= j1) continue;
         const uint32_t sid = ox.head_scan[j] - 1u;
         const uint32_t lo = ox.seg_start[sid], hi = ox.seg_start[sid + 1];
         const bool xf = ox.seg_mode[sid] == SM_XFLOW;
@@ -308,12 +389,13 @@ __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxId
             if (o != SF_ORIGIN_NONE) { ox_lds_insert(kk, ox_pack(l, AX_ORIGIN, o), &fresh); any = true; }
             const uint32_t ctx = b.ctx ? b.ctx[i] : 0u;
             bool want = false;
-            for (uint32_t k = st.rule_off[l]; k < st.rule_off[l + 1]; k++)
-                if (st.rules[k].strategy == SF_STRATEGY_CHAIN && st.rules[k].ref == ctx) want = true;
+            for (uint32_t r = st.rule_off[l]; r < st.rule_off[l + 1]; r++)
+                if (st.rules[r].strategy == SF_STRATEGY_CHAIN && st.rules[r].ref == ctx) want = true;
             if (want) { ox_lds_insert(kk, ox_pack(l, AX_CTX, ctx), &fresh); any = true; }
         } else if (o != SF_ORIGIN_NONE) {
             const uint32_t p = ox_lds_insert(kk, ox_pack(ox.seg_res[sid], AX_ORIGIN, o), &fresh);
-            kheavy[p] = 1;
+            if (fresh) kheavy[p] = 1;
+            kp[k] = p;
             any = true;
         } else {
             ox.s_oslot[j] = XNONE;
@@ -325,58 +407,45 @@ __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxId
         *hi = pkey_hi(ox_l(k), PK_AUX, ox_kind(k), 0);
         *lo = (uint32_t)k;
     });
-    // dense ids of the pairs of long segments (k_ox_hacc / k_ox_happly), same rounds
-    for (;;) {
-        if (tid == 0) { sh[0] = 0; sh[1] = 0; }
-        __syncthreads();
-        for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
-            const uint32_t a = kslot[p];
-            if (!kheavy[p] || a == XNONE || (a & KS_CLAIMED)) continue;
-            if (a >= ox.hmap_n) { atomicOr(&ox.cnt[OXC_OVERFLOW], 2u); kheavy[p] = 0; continue; }
-            const uint32_t h = __hip_atomic_load(&ox.hmap[a], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (h == XNONE) {
-                uint32_t expected = XNONE;
-                if (__hip_atomic_compare_exchange_strong(&ox.hmap[a], &expected, HX_CLAIM, __ATOMIC_ACQUIRE,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    kheavy[p] = 2;                         // claimed: gets an id below
-                    atomicAdd(&sh[0], 1u);
-                    continue;
-                }
-                sh[1] = 1;
-            } else if (h == HX_CLAIM) {
-                sh[1] = 1;
-            } else {
-                kheavy[p] = 0;                             // has its id
-                bfl = OXB_HEAVY;
-            }
+    // dense ids of the pairs of long segments (k_ox_hacc / k_ox_happly): the
+    // first workgroup to swing a slot's hmap entry from XNONE claims it and
+    // gives it an id; nothing in this kernel reads hmap, so no one waits
+    if (tid == 0) sh[0] = 0;
+    __syncthreads();
+    for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+        const uint32_t a = kslot[p];
+        if (!kheavy[p]) continue;
+        kheavy[p] = 0;
+        if (a == XNONE || (a & KS_CLAIMED)) continue;
+        if (a >= ox.hmap_n) { atomicOr(&ox.cnt[OXC_OVERFLOW], 2u); continue; }
+        bfl = OXB_HEAVY;
+        if (__hip_atomic_load(&ox.hmap[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != XNONE) continue;
+        uint32_t expected = XNONE;
+        if (__hip_atomic_compare_exchange_strong(&ox.hmap[a], &expected, HX_CLAIM, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            kheavy[p] = 2;
+            atomicAdd(&sh[0], 1u);
         }
-        __syncthreads();
-        if (tid == 0) { if (sh[0]) sh[3] = atomicAdd(&ox.cnt[OXC_HEAVY], sh[0]); sh[0] = 0; }
-        __syncthreads();
-        for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
-            if (kheavy[p] != 2) continue;
-            const uint32_t hid = sh[3] + atomicAdd(&sh[0], 1u);
-            const uint32_t a = kslot[p];
-            if (hid < ox.hslot_n) ox.hslot[hid] = a;
-            else atomicOr(&ox.cnt[OXC_OVERFLOW], 2u);
-            __hip_atomic_store(&ox.hmap[a], hid < ox.hslot_n ? hid : XNONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            kheavy[p] = 0;
-            bfl = OXB_HEAVY;
-        }
-        __syncthreads();
-        if (!sh[1]) break;
-        __syncthreads();
+    }
+    __syncthreads();
+    if (tid == 0) { if (sh[0]) sh[3] = atomicAdd(&ox.cnt[OXC_HEAVY], sh[0]); sh[0] = 0; }
+    __syncthreads();
+    for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+        if (kheavy[p] != 2) continue;
+        const uint32_t hid = sh[3] + atomicAdd(&sh[0], 1u);
+        const uint32_t a = kslot[p];
+        if (hid < ox.hslot_n) ox.hslot[hid] = a;
+        else atomicOr(&ox.cnt[OXC_OVERFLOW], 2u);
+        ox.hmap[a] = hid < ox.hslot_n ? hid : XNONE;
     }
     if (tid == 0 && bfl) atomicOr(&ox.bflags[j0 / OX_TILE], bfl);
     // the slot of every event of the long segments
-    for (uint32_t j = j0 + tid; j < j1; j += OX_T) {
-        const uint32_t sid = ox.head_scan[j] - 1u;
-        if (ox.seg_mode[sid] == SM_XFLOW || ox.seg_start[sid + 1] - ox.seg_start[sid] <= OX_LIGHT) continue;
-        const uint32_t o = ox.s_origin ? ox.s_origin[j] : SF_ORIGIN_NONE;
-        if (o == SF_ORIGIN_NONE) continue;
-        const uint32_t p = ox_lds_find(kk, ox_pack(ox.seg_res[sid], AX_ORIGIN, o));
-        ox.s_oslot[j] = p != XNONE ? kslot[p] : XNONE;
-    }
+#pragma unroll
+    for (uint32_t k = 0; k < OX_ITILE / OX_T; k++)
+        if (kp[k] != XNONE) {
+            const uint32_t a = kslot[kp[k]];
+            ox.s_oslot[j0 + k * OX_T + tid] = (a & KS_CLAIMED) ? XNONE : a;
+        }
 }
 
 // ------------------------------------------------------------------ decide phase
@@ -389,9 +458,59 @@ struct OxRun {
     uint32_t n; OxWin win;
 };
 
+// The origin node of one pair while its events are replayed in time order:
+// only the second-window and minute buckets the events touch are held (one of
+// each; a move to another slot stores the held one back), the thread count as
+// a delta.  Same window rules as NodeWin (sf_decide.h: sec_current with the
+// borrow seed of OccupiableBucketLeapArray.resetWindowTo, min_current, the
+// throwaway window of LeapArray.java:220-223) for the four adds StatisticSlot
+// makes on an origin node -- none reads the borrow array or another bucket,
+// so nothing else of the node is loaded.
+struct OxNode {
+    NodeRows rows;
+    Bucket sb; int32_t si = -1; int32_t sdirty = 0; int64_t s_ws = INT64_MIN;
+    Bucket mb; int32_t mi = -1; int32_t mdirty = 0; int64_t m_ws = INT64_MIN;
+    int64_t dthr = 0;
+    int32_t S, wl; int64_t max_rt;
+    __device__ void flush_sec() { if (sdirty) { rows.sec[si] = sb; sdirty = 0; } }
+    __device__ void flush_min() { if (mdirty) { rows.min[mi] = mb; mdirty = 0; } }
+    __device__ bool sec(int64_t t) {
+        if (!(t >= s_ws && t < s_ws + (int64_t)wl)) {
+            const int64_t q = t / wl;
+            s_ws = t - (t - q * wl);
+            const int32_t idx = (int32_t)(q % S);
+            if (idx != si) { flush_sec(); sb = rows.sec[idx]; si = idx; }
+        }
+        if (sb.ws == s_ws) return true;
+        if (s_ws < sb.ws) return false;                           // throwaway window
+        const Borrow br = rows.bor[si];
+        const int64_t bp = (br.ws <= s_ws && s_ws < br.ws + wl) ? br.pass : -1;
+        sb = fresh_bucket(s_ws, max_rt);
+        if (bp >= 0) sb.pass = (int64_t)(int32_t)bp;
+        sdirty = 1;
+        return true;
+    }
+    __device__ bool min(int64_t t) {
+        if (!(t >= m_ws && t < m_ws + 1000)) {
+            const int32_t idx = (int32_t)((t / 1000) % MINUTE);
+            m_ws = t - t % 1000;
+            if (idx != mi) { flush_min(); mb = rows.min[idx]; mi = idx; }
+        }
+        if (mb.ws == m_ws) return true;
+        if (m_ws < mb.ws) return false;
+        mb = fresh_bucket(m_ws, max_rt);
+        mdirty = 1;
+        return true;
+    }
+    template <class F> __device__ void add(int64_t t, F f) {
+        if (sec(t)) { f(sb); sdirty = 1; }
+        if (min(t)) { f(mb); mdirty = 1; }
+    }
+    __device__ void store() { flush_sec(); flush_min(); if (dthr) *rows.thr = wadd(*rows.thr, dthr); }
+};
+
 // StatisticSlot's update of the origin node for sorted event j (verdict known)
-template <int MAXS>
-__device__ __forceinline__ void ox_apply_event(NodeWin<MAXS>& on, const OxRun& r, uint32_t j) {
+__device__ __forceinline__ void ox_apply_event(OxNode& on, const OxRun& r, uint32_t j) {
     const uint8_t v = r.v_status[j], fl = r.flags[j];
     const int64_t t = r.ts[j];
     const int32_t c = r.cnt[j];
@@ -399,33 +518,34 @@ __device__ __forceinline__ void ox_apply_event(NodeWin<MAXS>& on, const OxRun& r
         if (v != SF_V_EXIT) return;                          // its entry was blocked: nothing is recorded
         const int64_t ref = r.eref ? r.eref[j] : -1;
         const int64_t cts = ref >= 0 ? r.ts[ref] : (r.cts ? r.cts[j] : t);
-        on.add_rt_success(t, t - cts, c);
-        on.threads--;
-        if (fl & SF_EV_ERROR) on.add_exception(t, c);
+        const int64_t rt = t - cts;
+        on.add(t, [&](Bucket& b) {                           // StatisticNode.addRtAndSuccess, MetricBucket.addRT
+            b.succ = wadd(b.succ, c); b.rt = wadd(b.rt, rt); if (rt < b.min_rt) b.min_rt = rt;
+        });
+        on.dthr--;
+        if (fl & SF_EV_ERROR) on.add(t, [&](Bucket& b) { b.exc = wadd(b.exc, c); });
     } else if (v_blocked(v)) {                               // :102-124 BlockException
-        on.add_block(t, c);
+        on.add(t, [&](Bucket& b) { b.block = wadd(b.block, c); });
     } else {
-        on.threads++;                                        // pass, or PriorityWaitException (:84-101)
-        if (v != SF_V_PRIORITY_WAIT) on.add_pass(t, c);
+        on.dthr++;                                           // pass, or PriorityWaitException (:84-101)
+        if (v != SF_V_PRIORITY_WAIT) on.add(t, [&](Bucket& b) { b.pass = wadd(b.pass, c); });
     }
 }
 
 // One thread per (resource, origin) pair of a short segment (k_ox_ilight's
-// list): the node is loaded, the pair's events of the segment are applied in
-// time order, the node is stored.  No LDS: many wavefronts keep the node loads
-// of many pairs in flight.
-template <int MAXS>
+// list, k_ox_lfind's slot): the pair's events applied in time order.  No LDS
+// and few registers: many wavefronts keep the bucket loads of many pairs in
+// flight.
 __global__ void __launch_bounds__(256) k_ox_lapply(DevState st, OxRun r, uint32_t npairs) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= npairs) return;
     const uint4 pr = r.pairs[t];
-    const uint32_t a = pr.x;
-    if (a == XNONE) return;
-    const NodeRows rows = aux_rows(st, a);
-    NodeWin<MAXS> on;
-    nw_load(on, st, rows);
-    for (uint32_t k = pr.y; k < pr.z; k++) ox_apply_event<MAXS>(on, r, r.plist[k]);
-    nw_store(on, st, rows);
+    if (pr.x == XNONE) return;
+    OxNode on;
+    on.rows = aux_rows(st, pr.x);
+    on.S = st.S; on.wl = st.wl; on.max_rt = st.max_rt;
+    for (uint32_t k = pr.y; k < pr.z; k++) ox_apply_event(on, r, r.plist[k]);
+    on.store();
 }
 
 // ---- long segments: per-window sums
@@ -597,8 +717,11 @@ hipError_t launch_ox_index(const DevState& st, Work& w, const DevBatch& b, uint3
     // (reservations start from the table's key count: every pool slot is one key)
     hipMemcpyAsync(w.ox_cnt + OXC_RESERVED, st.ax_count, sizeof(uint32_t), hipMemcpyDeviceToDevice, s);
     hipMemsetAsync(w.ox_bflags, 0, ((size_t)b.n / OX_TILE + 1) * sizeof(uint32_t), s);
-    if (b.origin)
-        hipLaunchKernelGGL(k_ox_ilight, dim3(ox_blocks(b.n, OX_LTILE)), dim3(OX_T), 0, s, st, b, ox, lim);
+    if (b.origin) {
+        hipLaunchKernelGGL(k_ox_ilight, dim3(ox_blocks(b.n, OX_LTILE)), dim3(OX_T), 0, s, b, ox);
+        const unsigned g = (unsigned)std::min<size_t>(ox_blocks(b.n, 256), 8192);
+        hipLaunchKernelGGL(k_ox_lfind, dim3(g), dim3(256), 0, s, st, w.ox_pairs, w.ox_cnt, lim);
+    }
     hipLaunchKernelGGL(k_ox_index, dim3(ox_blocks(b.n, OX_ITILE)), dim3(OX_T), 0, s, st, b, ox, lim);
     return hipGetLastError();
 }
@@ -615,9 +738,7 @@ hipError_t launch_ox_apply(const DevState& st, Work& w, const DevBatch& b, uint3
     r.bflags = w.ox_bflags; r.bseg = w.ox_bseg; r.pairs = w.ox_pairs; r.plist = w.ox_plist;
     r.n = b.n; r.win = win;
     if (n_pairs) {
-        if (st.S <= 2) hipLaunchKernelGGL(k_ox_lapply<2>, dim3(ox_blocks(n_pairs, 256)), dim3(256), 0, s, st, r, n_pairs);
-        else hipLaunchKernelGGL(k_ox_lapply<SF_MAX_SAMPLE_COUNT>, dim3(ox_blocks(n_pairs, 256)), dim3(256), 0, s, st, r,
-                                n_pairs);
+        hipLaunchKernelGGL(k_ox_lapply, dim3(ox_blocks(n_pairs, 256)), dim3(256), 0, s, st, r, n_pairs);
     }
     if (n_heavy) {
         const size_t W = (size_t)win.ws + win.wm;

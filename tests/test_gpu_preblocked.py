@@ -101,3 +101,69 @@ def test_preblocked_degrade_only_chain(eng_mod):
     outs = td.check_gpu(rules, w["batches"], R, "preblocked")
     allst = np.concatenate([x[0] for x in outs])
     assert (allst == abi.V_BLOCK_OTHER).sum() > 0 and (allst == abi.V_BLOCK_DEGRADE).sum() > 0
+
+
+SF_THR_RUN_AVG = 16          # sf_heavy.h thr_run_mode
+
+
+def _run_waves(R=2, waves=60, E=240, blocked_per_wave=3, seed=9):
+    """THREAD traffic in waves: E entries over E/4 ms, then their E exits
+    (random order, after every entry of the wave), with a few SF_EV_BLOCKED
+    entries (no exit) inside each entry run."""
+    rng = np.random.default_rng(seed)
+    res, ts, fl, cnt, ref_of = [], [], [], [], []
+    for r in range(R):
+        t = trace.T0 + 3 * r
+        for _ in range(waves):
+            ent_ts = t + np.sort(rng.integers(0, E // 4, E))
+            blk = set(rng.choice(np.arange(10, E - 10), blocked_per_wave, replace=False).tolist())
+            first = len(res)
+            for k in range(E):
+                res.append(r); ts.append(int(ent_ts[k])); cnt.append(1)
+                fl.append(abi.EV_IN | (abi.EV_BLOCKED if k in blk else 0)); ref_of.append(-1)
+            t_ex = int(ent_ts[-1]) + 1
+            live = [first + k for k in range(E) if k not in blk]
+            ex_ts = t_ex + np.sort(rng.integers(0, E // 4, len(live)))
+            for e, x in zip(rng.permutation(live), ex_ts):
+                res.append(r); ts.append(int(x)); cnt.append(1)
+                fl.append(abi.EV_EXIT | abi.EV_IN); ref_of.append(int(e))
+            t = int(ex_ts[-1]) + 1
+    res, ts, fl, cnt, ref_of = map(np.asarray, (res, ts, fl, cnt, ref_of))
+    order = np.lexsort((np.arange(ts.size), ts))
+    pos = np.empty(order.size, np.int64)
+    pos[order] = np.arange(order.size)
+    eref = np.where(ref_of[order] >= 0, pos[np.maximum(ref_of[order], 0)], -1)
+    return abi.HostBatch(res[order].astype(np.uint32), ts[order].astype(np.int64), cnt[order].astype(np.int32),
+                         fl[order].astype(np.uint8), entry_ref=eref)
+
+
+def _runs_per_segment(b):
+    """thr_run_mode's statistic per resource of a batch: events, runs of
+    checked entries vs everything else (k_thr_rid's heads)."""
+    out = {}
+    for r in np.unique(b.res_id):
+        f = b.flags[b.res_id == r]
+        checked = ((f & abi.EV_EXIT) == 0) & ((f & abi.EV_BLOCKED) == 0)
+        out[int(r)] = (f.size, 1 + int((checked[1:] != checked[:-1]).sum()))
+    return out
+
+
+def test_preblocked_thread_run_mode(eng_mod, so):
+    """Blocked entries inside the long entry runs of saturated THREAD head
+    resources: every segment meets thr_run_mode's bound (events >= 16 x runs,
+    so thr_runs_segment decides it run by run), the rules saturate, and every
+    verdict, node and rule state equals the oracle's, across three batches
+    (exits of entries from earlier batches included)."""
+    hb = _run_waves()
+    cuts = [0, hb.n // 3 + 7, 2 * hb.n // 3 - 11, hb.n]
+    batches = [hb.subset(cuts[i], cuts[i + 1]) for i in range(3)]
+    for b in batches:
+        for r, (n, runs) in _runs_per_segment(b).items():
+            assert n >= SF_THR_RUN_AVG * runs, (r, n, runs)
+    rules = [abi.sf_flow_rule(resource=r, grade=abi.GRADE_THREAD, count=float(30 + 20 * r), control_behavior=0)
+             for r in range(2)]
+    w = dict(cfg=abi.default_config(max_resources=2, max_batch=max(b.n for b in batches), heavy_min_events=8),
+             flow=rules, batches=batches, nodes=[0, 1], n_flow=2)
+    _, _, outs = workloads.run(eng_mod.FlowEngine, so.OracleEngine, w)
+    assert _count(outs, abi.V_BLOCK_OTHER) >= 60 * 3
+    assert _count(outs, abi.V_BLOCK_FLOW) > 1000
