@@ -115,6 +115,7 @@ struct sf_engine {
     void* dg_stage = nullptr; size_t dg_stage_bytes = 0;
     // xflow walk (sf_xflow.h): group keys and the origin / context node pool
     uint32_t* xmap_buf = nullptr;
+    uint8_t* xw_buf = nullptr;
     // the pool's chunks (host mirror of the device directory st.ax_chunks) and
     // the index table's growth (sf_origin.hip); counts for sf_stats
     std::vector<AuxChunk> ax_host;
@@ -205,7 +206,7 @@ void sf_destroy(sf_engine* e) {
                      e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
                      e->dgw.err, e->dg_stage, e->dgw.heavy, e->dgw.n_heavy, e->dgw.sev, e->dgw.inv};
     for (void* p : dptrs) if (p) hipFree(p);
-    void* xptrs[] = {e->xmap_buf, e->st.xtab, e->ax_dir, e->st.ax_count};
+    void* xptrs[] = {e->xmap_buf, e->xw_buf, e->st.xtab, e->ax_dir, e->st.ax_count};
     for (void* p : xptrs) if (p) hipFree(p);
     for (const AuxChunk& c : e->ax_host) hipFree(c.sec);          // (one allocation per chunk)
     for (auto& p : e->pk) {
@@ -294,6 +295,7 @@ static int alloc_work(sf_engine* e, Work& w) {
     WALLOC(w.hticks, (N / (w.heavy_min + 1) + 2) * 8);
     WALLOC(w.sticks, (N / (w.heavy_min + 1) + 2) * 8);
     WALLOC(w.stream_list, SC * 4);
+    WALLOC(w.xw_list, (N / XW_MIN + 1) * 4);
     WALLOC(w.passbits, (N / 64 + 2) * 8);
     WALLOC(w.exit_of, N * 4);
     WALLOC(w.lxfar, (N / 64 + 2) * 8);
@@ -674,6 +676,11 @@ int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
         if (!e->xmap_buf) HIP_TRY(hipMalloc((void**)&e->xmap_buf, (size_t)e->R * sizeof(uint32_t)));
         HIP_TRY(hipMemcpyAsync(e->xmap_buf, xmap.data(), (size_t)e->R * sizeof(uint32_t), hipMemcpyHostToDevice,
                                e->stream));
+        std::vector<uint8_t> xw;
+        build_xw(dr.data(), off.data(), e->R, xmap, xw);
+        if (!e->xw_buf) HIP_TRY(hipMalloc((void**)&e->xw_buf, (size_t)e->R));
+        HIP_TRY(hipMemcpyAsync(e->xw_buf, xw.data(), (size_t)e->R, hipMemcpyHostToDevice, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
     }
     e->n_flow = (uint32_t)valid.size();
     {   // which segment classes the rules allow (launches of absent classes are skipped)
@@ -695,6 +702,7 @@ int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
     HIP_TRY(hipMemcpyAsync((void*)e->st.rule_off, off.data(), off.size() * 4, hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->st.xmap = xflow ? e->xmap_buf : nullptr;
+    e->st.xw = xflow ? e->xw_buf : nullptr;
     return SF_OK;
 }
 

@@ -104,6 +104,10 @@ struct DevState {
     // grouped by RELATE references.  xmap[l] = the group's key (its smallest
     // member), XNONE for every other resource; null: no such rule loaded.
     const uint32_t* xmap;
+    // xw[l] (XWF_* bits): l's segments may take the wave walk (k_decide_xw): a
+    // group of one resource whose rules all check DIRECT; XWF_THREAD: a THREAD
+    // grade rule among them (exits stay in the serial part)
+    const uint8_t* xw;
     // origin / context nodes: index table (key (kind, resource, id) -> pool
     // slot) and the node pool in the layout of the resource rows, in chunks of
     // AX_CHUNK nodes (node k: chunk k >> AX_SHIFT), so the pool grows between
@@ -210,6 +214,7 @@ struct Work {
     uint32_t stream_grid;                               // persistent k_heavy_stream workgroups (2 per CU)
     uint64_t* hticks;                                   // [max heavy] k_heavy_decide clock per segment (timing)
     uint32_t* stream_list;                              // THREAD / RL heavy segments (k_heavy_stream)
+    uint32_t* xw_list;                                  // [N / XW_MIN + 1] xflow segments of the wave walk (counters[12])
     uint64_t* sticks;                                   // [max heavy] k_heavy_stream clock per segment (timing)
     unsigned long long* passbits;                       // [n/64+2] pass bit per sorted entry (heavy segments)
     uint32_t* exit_of;                                  // [n] sorted index of each entry's exit, ~0 if none

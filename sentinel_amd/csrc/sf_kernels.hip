@@ -220,6 +220,11 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     // do not route a segment there (their nodes: sf_origin.hip)
     const bool xs = valid && st.xmap && st.xmap[res] != XNONE;
     if (xs) w.seg_mode[s] = SM_XFLOW;
+    {   // long xflow segments the wave walk can take (k_decide_xw)
+        const bool xw = xs && xw_take(st, res, hi - lo);
+        const uint32_t p = wave_append(&w.counters[12], xw);
+        if (xw) w.xw_list[p] = s;
+    }
     bool light = valid && !xs && hi - lo <= w.heavy_min;
     // a ParamFlow-only segment of more than 32 events is faster on the
     // wavefront-by-value path (SM_PARAM) than as one lane's serial table walk
@@ -376,13 +381,221 @@ __global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_short(DevState st
     decide_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
 }
 
-// One lane per xflow group segment (sf_xflow.h): origin / context / RELATE rules.
+// One lane per xflow group segment (sf_xflow.h): origin / context / RELATE
+// rules (the long segments k_decide_xw takes excepted).
 template <int MAXS>
 __global__ void __launch_bounds__(64) k_decide_x(DevState st, SegIO io, const uint32_t* seg_start,
-                                                 const uint8_t* seg_mode, const uint32_t* n_seg) {
+                                                 const uint32_t* seg_res, const uint8_t* seg_mode,
+                                                 const uint32_t* n_seg) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= *n_seg || seg_mode[s] != SM_XFLOW) return;
+    if (xw_take(st, seg_res[s], seg_start[s + 1] - seg_start[s])) return;
     decide_xgroup<MAXS>(st, io, seg_start[s], seg_start[s + 1]);
+}
+
+// ---- the wave walk of a long xflow segment (one resource, DIRECT rules)
+// A wavefront takes the segment in chunks of at most 64 events that share
+// one second-window bucket and one minute bucket.  Per chunk:
+//  1. every lane checks its entry against the first rule that selects a node
+//     (FlowRuleComparator order: origin-specific and `other` rules before
+//     `default`), on the node and rule state as they stand at the chunk's
+//     start.  Within one bucket a node's pass count and a RateLimiter's
+//     latestPassedTime only grow, the WarmUp threshold is fixed for the second
+//     (syncToken reads the previous second), and a THREAD count can fall at
+//     most by the exits ahead of the lane in the chunk, so an entry blocked at
+//     the start state is blocked in the serial order too, by that rule;
+//  2. lane 0 runs the reference walk (xg_event) over the other entries --
+//     those the start state lets pass, prioritized entries, and the exits when
+//     a THREAD rule reads thread counts -- in order;
+//  3. the blocked entries' blocks and the remaining exits' completions only
+//     add to the chunk's buckets (which no check of this chunk reads), so they
+//     are summed per node in LDS and added once per node.
+// Verdicts, node state and rule state equal the serial walk's.
+enum : uint8_t { XWC_SERIAL = 1, XWC_BLOCK = 2, XWC_EXIT = 3 };
+constexpr uint32_t XW_KCAP = 128;                 // LDS node rows of a chunk (<= 64 origins + the ClusterNode)
+struct XwRow { unsigned long long blk, succ, rt, exc; long long thr, minrt; unsigned int nblk, ncmp, nexc, key; };
+__device__ __forceinline__ void xw_add(XwRow& r, int64_t blk, int nblk, int64_t succ, int64_t rt, int64_t minrt,
+                                       int64_t exc, int nexc, int64_t thr, int ncmp) {
+    if (nblk) { atomicAdd(&r.blk, (unsigned long long)blk); atomicAdd(&r.nblk, 1u); }
+    if (ncmp) {
+        atomicAdd(&r.succ, (unsigned long long)succ); atomicAdd(&r.rt, (unsigned long long)rt);
+        atomicMin(&r.minrt, (long long)minrt); atomicAdd((unsigned long long*)&r.thr, (unsigned long long)thr);
+        atomicAdd(&r.ncmp, 1u);
+    }
+    if (nexc) { atomicAdd(&r.exc, (unsigned long long)exc); atomicAdd(&r.nexc, 1u); }
+}
+// a row's sums into a node (all events of the chunk are in the bucket of t0)
+template <int MAXS>
+__device__ __forceinline__ void xw_apply(NodeWin<MAXS>& nd, const XwRow& r, int64_t t0) {
+    if (r.nblk) {
+        const int64_t b = (int64_t)r.blk;
+        nd.sec_apply(t0, [&](Bucket& x) { x.block = wadd(x.block, b); });
+        nd.min_apply(t0, [&](Bucket& x) { x.block = wadd(x.block, b); });
+    }
+    if (r.ncmp) {
+        const int64_t sc = (int64_t)r.succ, rt = (int64_t)r.rt, mr = r.minrt;
+        auto f = [&](Bucket& x) { x.succ = wadd(x.succ, sc); x.rt = wadd(x.rt, rt); if (mr < x.min_rt) x.min_rt = mr; };
+        nd.sec_apply(t0, f);
+        nd.min_apply(t0, f);
+        nd.threads = wadd(nd.threads, r.thr);
+    }
+    if (r.nexc) {
+        const int64_t e = (int64_t)r.exc;
+        nd.sec_apply(t0, [&](Bucket& x) { x.exc = wadd(x.exc, e); });
+        nd.min_apply(t0, [&](Bucket& x) { x.exc = wadd(x.exc, e); });
+    }
+}
+
+template <int MAXS>
+__global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const uint32_t* seg_start,
+                                                  const uint32_t* seg_res, const uint32_t* list,
+                                                  const uint32_t* n_list) {
+    __shared__ __align__(16) unsigned char snap_raw[sizeof(NodeWin<MAXS>)];
+    __shared__ uint8_t cls[64];
+    __shared__ XwRow rows[XW_KCAP];
+    NodeWin<MAXS>& snap = *reinterpret_cast<NodeWin<MAXS>*>(snap_raw);
+    const uint32_t lane = threadIdx.x;
+    const ParamTable pt{st.ptab, st.pcap_mask, st.err, st.pins};
+    const uint32_t nl = *n_list;
+    for (uint32_t q = blockIdx.x; q < nl; q += gridDim.x) {
+        const uint32_t s = list[q];
+        const uint32_t lo = seg_start[s], hi = seg_start[s + 1], l = seg_res[s];
+        const uint32_t r0 = st.rule_off[l], r1 = st.rule_off[l + 1];
+        const bool thr_sens = (st.xw[l] & XWF_THREAD) != 0;
+        NodeWin<MAXS> cn, on, dn;                          // lane 0's walk
+        uint32_t cl = XNONE, oi = XNONE, di = XNONE;
+        if (lane == 0) { nw_load(cn, st, cluster_rows(st, l)); cl = l; }
+        for (uint32_t j0 = lo; j0 < hi;) {
+            const int64_t t0 = io.ts[j0];
+            const int64_t bs = t0 - t0 % st.wl, bm = t0 - t0 % 1000;
+            const uint32_t j = j0 + lane;
+            const bool valid = j < hi;
+            const int64_t t = valid ? io.ts[j] : t0;
+            const bool same = valid && t >= bs && t < bs + st.wl && t >= bm && t < bm + 1000;
+            const unsigned long long nb = __ballot(!same);
+            const uint32_t L = nb ? (uint32_t)(__ffsll((long long)nb) - 1) : 64u;   // (lane 0 is always in)
+            for (uint32_t k = lane; k < XW_KCAP; k += 64) {
+                rows[k].blk = rows[k].succ = rows[k].rt = rows[k].exc = 0; rows[k].thr = 0; rows[k].minrt = INT64_MAX;
+                rows[k].nblk = rows[k].ncmp = rows[k].nexc = 0; rows[k].key = 0;
+            }
+            if (lane == 0) {
+                if (cl != l) { if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl)); nw_load(cn, st, cluster_rows(st, l)); cl = l; }
+                snap = cn;
+                if (oi != XNONE) { nw_store(on, st, aux_rows(st, oi)); oi = XNONE; }
+            }
+            __syncthreads();
+            // 1. classify
+            uint8_t myc = 0, mst = 0;
+            int mrule = 0;
+            uint32_t origin = SF_ORIGIN_NONE, gres = 0;
+            int32_t c = 0;
+            uint8_t fl = 0;
+            if (lane < L) {
+                fl = io.flags[j]; c = io.cnt[j];
+                const uint32_t i = io.perm[j];
+                gres = io.ev_res[i];
+                origin = io.ev_origin ? io.ev_origin[i] : SF_ORIGIN_NONE;
+                if (fl & SF_EV_EXIT) myc = thr_sens ? XWC_SERIAL : XWC_EXIT;
+                else if (fl & EVF_SYSBLK) { myc = XWC_BLOCK; mst = sysblk_status(fl); mrule = sysblk_rule(fl); }
+                else myc = XWC_SERIAL;
+            }
+            const unsigned long long exits = __ballot(lane < L && (fl & SF_EV_EXIT));
+            const int64_t ex_before = (int64_t)__popcll(exits & ((1ull << lane) - 1ull));
+            if (myc == XWC_SERIAL && !(fl & (SF_EV_EXIT | SF_EV_PRIO))) {
+                for (uint32_t k = r0; k < r1; k++) {
+                    const DevRule& r = st.rules[k];
+                    if (r.always_pass) continue;
+                    const int sel = xflow_select(st, r, r0, r1, origin, 0u);
+                    if (sel == XS_NONE) continue;
+                    DevRuleState rs = st.rstate[k];
+                    int64_t w = 0; bool pw = false; int ok = 1;
+                    if (sel == XS_CLUSTER) {
+                        NodeWin<MAXS> x = snap;
+                        x.mdirty = 0;                            // (a copy: never written back)
+                        x.threads -= ex_before;
+                        ok = can_pass<MAXS>(r, rs, x, t, c, false, st.occupy_timeout, &w, &pw);
+                    } else if (sel == XS_ORIGIN) {
+                        const uint32_t ko = aux_get(st, l, AX_ORIGIN, origin);
+                        if (ko != XNONE) {
+                            NodeWin<MAXS> x;
+                            nw_load(x, st, aux_rows(st, ko));
+                            x.threads -= ex_before;
+                            ok = can_pass<MAXS>(r, rs, x, t, c, false, st.occupy_timeout, &w, &pw);
+                        }
+                    }
+                    if (!ok) { myc = XWC_BLOCK; mst = SF_V_BLOCK_FLOW; mrule = (int)(k - r0); }
+                    break;                                   // only the first selecting rule decides here
+                }
+            }
+            if (lane < L) cls[lane] = myc;
+            if (myc == XWC_BLOCK) io.v_status[j] = mst;      // (before the walk: its exits read it)
+            __syncthreads();
+            // 2. the serial walk over the undecided events
+            if (lane == 0) {
+                for (uint32_t k = 0; k < L; k++)
+                    if (cls[k] == XWC_SERIAL) xg_event<MAXS>(st, io, pt, lo, j0 + k, cn, on, dn, cl, oi, di);
+                if (oi != XNONE) { nw_store(on, st, aux_rows(st, oi)); oi = XNONE; }
+            }
+            __syncthreads();
+            // 3. the blocks and completions, summed per node
+            int64_t blk = 0, succ = 0, rt = 0, exc = 0, thr = 0, minrt = INT64_MAX;
+            int nblk = 0, ncmp = 0, nexc = 0;
+            if (myc == XWC_BLOCK) {
+                emit_verdict(io, j, mst, 0, (uint16_t)mrule);
+                blk = c; nblk = 1;
+            } else if (myc == XWC_EXIT) {                    // decide_xgroup's exit (StatisticSlot.exit :134-165)
+                int64_t ref = io.eref ? io.eref[j] : -1;
+                bool blocked; int64_t cts;
+                if (ref >= 0) {
+                    if (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT) ||
+                        io.ev_res[io.perm[ref]] != gres) {
+                        *st.err = SF_ERR_INVALID;
+                        ref = j;
+                    }
+                    blocked = ref == (int64_t)j ? true : v_blocked(io.v_status[ref]);
+                    cts = io.ts[ref];
+                } else {
+                    blocked = ref == EREF_DEAD; cts = io.cts ? io.cts[j] : t;
+                }
+                uint8_t v = SF_V_EXIT_IGNORED;
+                if (!blocked) {
+                    v = SF_V_EXIT;
+                    succ = c; rt = t - cts; minrt = rt; thr = -1; ncmp = 1;
+                    if (fl & SF_EV_ERROR) { exc = c; nexc = 1; }
+                }
+                io.v_status[j] = v;
+                emit_verdict(io, j, v, 0, 0);
+            }
+            if (nblk || ncmp) {
+                xw_add(rows[0], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp);     // row 0: the ClusterNode
+                if (origin != SF_ORIGIN_NONE) {
+                    uint32_t h = 1 + (uint32_t)(mix64(origin) % (XW_KCAP - 1));
+                    for (;;) {
+                        const unsigned int prev = atomicCAS(&rows[h].key, 0u, origin + 1u);
+                        if (prev == 0u || prev == origin + 1u) break;
+                        h = h + 1 < XW_KCAP ? h + 1 : 1;
+                    }
+                    xw_add(rows[h], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp);
+                }
+            }
+            __syncthreads();
+            if (lane == 0) xw_apply<MAXS>(cn, rows[0], t0);
+            for (uint32_t k = 1 + lane; k < XW_KCAP; k += 64) {
+                if (!rows[k].key) continue;
+                const uint32_t ko = aux_get(st, l, AX_ORIGIN, rows[k].key - 1u);
+                if (ko == XNONE) continue;
+                NodeWin<MAXS> x;
+                const NodeRows nr = aux_rows(st, ko);
+                nw_load(x, st, nr);
+                xw_apply<MAXS>(x, rows[k], t0);
+                nw_store(x, st, nr);
+            }
+            __syncthreads();
+            j0 += L;
+        }
+        if (lane == 0 && cl != XNONE) nw_store(cn, st, cluster_rows(st, cl));
+        __syncthreads();
+    }
 }
 
 // One lane per short segment routed to the lean QPS walk (SM_LIGHTQ), from
@@ -1179,7 +1392,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags,
                            w.head_scan, w.seg_start, w.s_eref, w.s_cts, w.exit_of, st.err);
-    hipMemsetAsync(w.counters, 0, 10 * sizeof(uint32_t), s);
+    hipMemsetAsync(w.counters, 0, 16 * sizeof(uint32_t), s);
     hipMemsetAsync(w.lcounts, 0, 2 * LCLS * sizeof(uint32_t), s);
     hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
     if (st.n_stream_rules) hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
@@ -1466,10 +1679,19 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     if (st.xmap) {
         if (st.S <= 2)
             hipLaunchKernelGGL(k_decide_x<2>, dim3(blocks(max_seg, 64)), dim3(64), 0, s3, st, io, w.seg_start,
-                               w.seg_mode, w.n_seg);
+                               w.seg_res, w.seg_mode, w.n_seg);
         else
             hipLaunchKernelGGL(k_decide_x<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, 64)), dim3(64), 0, s3, st, io,
-                               w.seg_start, w.seg_mode, w.n_seg);
+                               w.seg_start, w.seg_res, w.seg_mode, w.n_seg);
+        if (st.xw) {                               // long one-resource segments: the wave walk
+            const unsigned g = (unsigned)std::min<size_t>((size_t)b.n / XW_MIN + 1, 2048);
+            if (st.S <= 2)
+                hipLaunchKernelGGL(k_decide_xw<2>, dim3(g), dim3(64), 0, s3, st, io, w.seg_start, w.seg_res,
+                                   w.xw_list, w.counters + 12);
+            else
+                hipLaunchKernelGGL(k_decide_xw<SF_MAX_SAMPLE_COUNT>, dim3(g), dim3(64), 0, s3, st, io, w.seg_start,
+                                   w.seg_res, w.xw_list, w.counters + 12);
+        }
     }
     hipEventRecord(ev[9], s3);                     // light done (also the join of C)
     hipEventRecord(ev[6], s2);                     // join B and C

@@ -123,6 +123,177 @@ SF_HD int xflow_select(const DevState& st, const DevRule& r, uint32_t r0, uint32
     return XS_NONE;
 }
 
+// One event j of a group segment starting at lo: SystemSlot (forced verdict)
+// -> ParamFlowSlot -> FlowSlot with per-rule node selection -> DegradeSlot,
+// then StatisticSlot's accounting.  cn / on / dn hold the nodes cl / oi / di
+// (XNONE: none held); a switch stores the held node back first.
+template <int MAXS>
+SF_HD void xg_event(const DevState& st, const SegIO& io, const ParamTable& pt, uint32_t lo, uint32_t j,
+                    NodeWin<MAXS>& cn, NodeWin<MAXS>& on, NodeWin<MAXS>& dn, uint32_t& cl, uint32_t& oi,
+                    uint32_t& di) {
+    const uint32_t i = io.perm[j];
+    const uint32_t gres = io.ev_res[i];
+    const uint32_t l = gres / io.shard_count;
+    const uint32_t origin = io.ev_origin ? io.ev_origin[i] : SF_ORIGIN_NONE;
+    const uint32_t ctx = io.ev_ctx ? io.ev_ctx[i] : 0u;
+    const int64_t now = io.ts[j];
+    const int32_t c = io.cnt[j];
+    const uint8_t fl = io.flags[j];
+    const uint32_t na = io.arg_slots ? (io.nargs ? io.nargs[j] : io.arg_slots) : 0;
+    const uint32_t r0 = st.rule_off[l], r1 = st.rule_off[l + 1];
+    // the origin node of every entry with an origin (ClusterBuilderSlot.java:107-110:
+    // getOrCreateOriginNode whatever the rules); a context DefaultNode while a CHAIN
+    // rule of the resource names the context (DESIGN.md §2 divergences)
+    const bool want_on = origin != SF_ORIGIN_NONE;
+    bool want_dn = false;
+    for (uint32_t k = r0; k < r1; k++) {
+        const DevRule& r = st.rules[k];
+        if (r.strategy == SF_STRATEGY_CHAIN && r.ref == ctx) want_dn = true;
+    }
+    if (l != cl) {
+        if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl));
+        nw_load(cn, st, cluster_rows(st, l));
+        cl = l;
+    }
+    {
+        const uint32_t k = want_on ? aux_get(st, l, AX_ORIGIN, origin) : XNONE;
+        if (k != oi) {
+            if (oi != XNONE) nw_store(on, st, aux_rows(st, oi));
+            if (k != XNONE) nw_load(on, st, aux_rows(st, k));
+            oi = k;
+        }
+        const uint32_t m = want_dn ? aux_get(st, l, AX_CTX, ctx) : XNONE;
+        if (m != di) {
+            if (di != XNONE) nw_store(dn, st, aux_rows(st, di));
+            if (m != XNONE) nw_load(dn, st, aux_rows(st, m));
+            di = m;
+        }
+    }
+    const uint32_t p0 = st.prule_off[l], p1 = st.prule_off[l + 1];
+    const int nprules = (int)(p1 - p0);
+    uint8_t pm_init = nprules ? st.pm_init[l] : 0;
+    bool pm_exists = pm_init != 0;
+    uint32_t cb0, cb1;
+    breakers_of(st, l, &cb0, &cb1);
+    uint8_t status; int64_t wait = 0; int rule_idx = 0;
+
+    if (fl & SF_EV_EXIT) {                                  // StatisticSlot.exit :134-165
+        int64_t ref = io.eref ? io.eref[j] : -1;
+        bool blocked; int64_t create_ts;
+        if (ref >= 0) {
+            if (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT) ||
+                io.ev_res[io.perm[ref]] != gres) {
+                *st.err = SF_ERR_INVALID;
+                ref = j;
+            }
+            blocked = ref == (int64_t)j ? true : v_blocked(io.v_status[ref]);
+            create_ts = io.ts[ref];
+        } else {
+            blocked = ref == EREF_DEAD; create_ts = io.cts ? io.cts[j] : now;
+        }
+        if (!blocked) {
+            const int64_t rt = now - create_ts;
+            const bool er = (fl & SF_EV_ERROR) != 0;
+            // recordCompleteFor(DefaultNode -> ClusterNode), recordCompleteFor(originNode) :150-151
+            if (di != XNONE) { dn.add_rt_success(now, rt, c); dn.threads--; if (er) dn.add_exception(now, c); }
+            cn.add_rt_success(now, rt, c); cn.threads--; if (er) cn.add_exception(now, c);
+            if (oi != XNONE) { on.add_rt_success(now, rt, c); on.threads--; if (er) on.add_exception(now, c); }
+            if (pm_exists) pm_thread_event(pt, l, pm_init, io, j, na, -1);
+            for (uint32_t cb = cb0; cb < cb1; cb++) {
+                sf_breaker_state bs = st.dg_state[cb];
+                dg_complete(bs, st.dg_rules[cb], now, rt, er);
+                st.dg_state[cb] = bs;
+            }
+            status = SF_V_EXIT;
+        } else {
+            status = SF_V_EXIT_IGNORED;
+        }
+    } else {
+        bool blocked = false, prio_wait = false;
+        status = SF_V_PASS;
+        if (fl & EVF_SYSBLK) {    // SF_EV_BLOCKED (AuthoritySlot) or a planned SystemBlockException
+            blocked = true; status = sysblk_status(fl); rule_idx = sysblk_rule(fl);
+        }
+        if (!blocked && nprules) {                          // ParamFlowSlot.checkFlow :82-103
+            pm_exists = true;
+            for (int k = 0; k < nprules && !blocked; k++) {
+                DevParamRule& pr = st.prules[p0 + k];
+                if (pr.param_idx < 0) {                     // applyRealParamIdx :56-66
+                    if (-pr.param_idx <= (int)na) pr.param_idx = (int)na + pr.param_idx;
+                    else pr.param_idx = -pr.param_idx;
+                }
+                if (pr.param_idx < 8) pm_init |= (uint8_t)(1u << pr.param_idx);
+                if ((int)na <= pr.param_idx) continue;
+                const uint32_t tg = io.atag[(size_t)pr.param_idx * io.n + j];
+                const uint64_t bt = io.abits[(size_t)pr.param_idx * io.n + j];
+                if (tg == SF_TAG_NULL) continue;
+                int64_t w = 0;
+                if (!param_pass_value(pt, l, k, pr, st.items, now, c, tg, bt, io, &w)) {
+                    blocked = true; status = SF_V_BLOCK_PARAM; rule_idx = k;
+                } else if (w > 0) {
+                    wait += w;
+                }
+            }
+        }
+        if (!blocked) {                                     // FlowRuleChecker.checkFlow :44-59
+            const bool prio = (fl & SF_EV_PRIO) != 0;
+            for (uint32_t k = 0; k < r1 - r0; k++) {
+                const DevRule& r = st.rules[r0 + k];
+                if (r.always_pass) continue;                // cluster rule, no fallback (:184-193)
+                const int sel = xflow_select(st, r, r0, r1, origin, ctx);
+                if (sel == XS_NONE) continue;
+                DevRuleState rs = st.rstate[r0 + k];
+                int64_t w = 0; bool pw = false; int ok = 1;
+                if (sel == XS_CLUSTER || (sel == XS_REF && r.ref == l)) {
+                    ok = can_pass<MAXS>(r, rs, cn, now, c, prio, st.occupy_timeout, &w, &pw);
+                } else if (sel == XS_ORIGIN) {
+                    if (oi != XNONE) ok = can_pass<MAXS>(r, rs, on, now, c, prio, st.occupy_timeout, &w, &pw);
+                } else if (sel == XS_CTX) {
+                    if (di != XNONE) ok = can_pass<MAXS>(r, rs, dn, now, c, prio, st.occupy_timeout, &w, &pw);
+                } else {                                    // RELATE: another resource of the group
+                    const NodeRows rr = cluster_rows(st, r.ref);
+                    if (node_created(st, rr)) {
+                        NodeWin<MAXS> rn;
+                        nw_load(rn, st, rr);
+                        ok = can_pass<MAXS>(r, rs, rn, now, c, prio, st.occupy_timeout, &w, &pw);
+                        nw_store(rn, st, rr);
+                    }
+                }
+                st.rstate[r0 + k] = rs;
+                if (pw) { prio_wait = true; wait += w; rule_idx = (int)k; break; }
+                if (!ok) { blocked = true; status = SF_V_BLOCK_FLOW; rule_idx = (int)k; break; }
+                wait += w;
+            }
+        }
+        if (!blocked && !prio_wait && cb1 > cb0) {          // DegradeSlot.entry (DegradeSlot.java:42-61)
+            const int k = dg_entry_check(st.dg_state, cb0, cb1, now);
+            if (k >= 0) { blocked = true; status = SF_V_BLOCK_DEGRADE; rule_idx = k; }
+        }
+        // StatisticSlot.entry accounting :64-123 (DefaultNode -> ClusterNode, origin node)
+        if (blocked) {
+            if (di != XNONE) dn.add_block(now, c);
+            cn.add_block(now, c);
+            if (oi != XNONE) on.add_block(now, c);
+        } else {
+            if (di != XNONE) dn.threads++;
+            cn.threads++;
+            if (oi != XNONE) on.threads++;
+            if (prio_wait) {
+                status = SF_V_PRIORITY_WAIT;
+            } else {
+                if (di != XNONE) dn.add_pass(now, c);
+                cn.add_pass(now, c);
+                if (oi != XNONE) on.add_pass(now, c);
+                status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS;
+            }
+            if (pm_exists) pm_thread_event(pt, l, pm_init, io, j, na, +1);
+        }
+    }
+    if (nprules) st.pm_init[l] = pm_init;
+    io.v_status[j] = status;
+    emit_verdict(io, j, status, (int32_t)wait, (uint16_t)rule_idx);
+}
+
 // One group segment [lo, hi) (events of several resources, submission order).
 // The current resource's ClusterNode and the last origin / context node stay
 // in registers while consecutive events use them (a group of one resource
@@ -133,175 +304,45 @@ SF_HD void decide_xgroup(const DevState& st, const SegIO& io, uint32_t lo, uint3
     const ParamTable pt{st.ptab, st.pcap_mask, st.err, st.pins};
     NodeWin<MAXS> cn, on, dn;
     uint32_t cl = XNONE, oi = XNONE, di = XNONE;          // nodes held in cn / on / dn
-    for (uint32_t j = lo; j < hi; j++) {
-        const uint32_t i = io.perm[j];
-        const uint32_t gres = io.ev_res[i];
-        const uint32_t l = gres / io.shard_count;
-        const uint32_t origin = io.ev_origin ? io.ev_origin[i] : SF_ORIGIN_NONE;
-        const uint32_t ctx = io.ev_ctx ? io.ev_ctx[i] : 0u;
-        const int64_t now = io.ts[j];
-        const int32_t c = io.cnt[j];
-        const uint8_t fl = io.flags[j];
-        const uint32_t na = io.arg_slots ? (io.nargs ? io.nargs[j] : io.arg_slots) : 0;
-        const uint32_t r0 = st.rule_off[l], r1 = st.rule_off[l + 1];
-        // the origin node of every entry with an origin (ClusterBuilderSlot.java:107-110:
-        // getOrCreateOriginNode whatever the rules); a context DefaultNode while a CHAIN
-        // rule of the resource names the context (DESIGN.md §2 divergences)
-        const bool want_on = origin != SF_ORIGIN_NONE;
-        bool want_dn = false;
-        for (uint32_t k = r0; k < r1; k++) {
-            const DevRule& r = st.rules[k];
-            if (r.strategy == SF_STRATEGY_CHAIN && r.ref == ctx) want_dn = true;
-        }
-        if (l != cl) {
-            if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl));
-            nw_load(cn, st, cluster_rows(st, l));
-            cl = l;
-        }
-        {
-            const uint32_t k = want_on ? aux_get(st, l, AX_ORIGIN, origin) : XNONE;
-            if (k != oi) {
-                if (oi != XNONE) nw_store(on, st, aux_rows(st, oi));
-                if (k != XNONE) nw_load(on, st, aux_rows(st, k));
-                oi = k;
-            }
-            const uint32_t m = want_dn ? aux_get(st, l, AX_CTX, ctx) : XNONE;
-            if (m != di) {
-                if (di != XNONE) nw_store(dn, st, aux_rows(st, di));
-                if (m != XNONE) nw_load(dn, st, aux_rows(st, m));
-                di = m;
-            }
-        }
-        const uint32_t p0 = st.prule_off[l], p1 = st.prule_off[l + 1];
-        const int nprules = (int)(p1 - p0);
-        uint8_t pm_init = nprules ? st.pm_init[l] : 0;
-        bool pm_exists = pm_init != 0;
-        uint32_t cb0, cb1;
-        breakers_of(st, l, &cb0, &cb1);
-        uint8_t status; int64_t wait = 0; int rule_idx = 0;
-
-        if (fl & SF_EV_EXIT) {                                  // StatisticSlot.exit :134-165
-            int64_t ref = io.eref ? io.eref[j] : -1;
-            bool blocked; int64_t create_ts;
-            if (ref >= 0) {
-                if (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT) ||
-                    io.ev_res[io.perm[ref]] != gres) {
-                    *st.err = SF_ERR_INVALID;
-                    ref = j;
-                }
-                blocked = ref == (int64_t)j ? true : v_blocked(io.v_status[ref]);
-                create_ts = io.ts[ref];
-            } else {
-                blocked = ref == EREF_DEAD; create_ts = io.cts ? io.cts[j] : now;
-            }
-            if (!blocked) {
-                const int64_t rt = now - create_ts;
-                const bool er = (fl & SF_EV_ERROR) != 0;
-                // recordCompleteFor(DefaultNode -> ClusterNode), recordCompleteFor(originNode) :150-151
-                if (di != XNONE) { dn.add_rt_success(now, rt, c); dn.threads--; if (er) dn.add_exception(now, c); }
-                cn.add_rt_success(now, rt, c); cn.threads--; if (er) cn.add_exception(now, c);
-                if (oi != XNONE) { on.add_rt_success(now, rt, c); on.threads--; if (er) on.add_exception(now, c); }
-                if (pm_exists) pm_thread_event(pt, l, pm_init, io, j, na, -1);
-                for (uint32_t cb = cb0; cb < cb1; cb++) {
-                    sf_breaker_state bs = st.dg_state[cb];
-                    dg_complete(bs, st.dg_rules[cb], now, rt, er);
-                    st.dg_state[cb] = bs;
-                }
-                status = SF_V_EXIT;
-            } else {
-                status = SF_V_EXIT_IGNORED;
-            }
-        } else {
-            bool blocked = false, prio_wait = false;
-            status = SF_V_PASS;
-            if (fl & EVF_SYSBLK) {    // SF_EV_BLOCKED (AuthoritySlot) or a planned SystemBlockException
-                blocked = true; status = sysblk_status(fl); rule_idx = sysblk_rule(fl);
-            }
-            if (!blocked && nprules) {                          // ParamFlowSlot.checkFlow :82-103
-                pm_exists = true;
-                for (int k = 0; k < nprules && !blocked; k++) {
-                    DevParamRule& pr = st.prules[p0 + k];
-                    if (pr.param_idx < 0) {                     // applyRealParamIdx :56-66
-                        if (-pr.param_idx <= (int)na) pr.param_idx = (int)na + pr.param_idx;
-                        else pr.param_idx = -pr.param_idx;
-                    }
-                    if (pr.param_idx < 8) pm_init |= (uint8_t)(1u << pr.param_idx);
-                    if ((int)na <= pr.param_idx) continue;
-                    const uint32_t tg = io.atag[(size_t)pr.param_idx * io.n + j];
-                    const uint64_t bt = io.abits[(size_t)pr.param_idx * io.n + j];
-                    if (tg == SF_TAG_NULL) continue;
-                    int64_t w = 0;
-                    if (!param_pass_value(pt, l, k, pr, st.items, now, c, tg, bt, io, &w)) {
-                        blocked = true; status = SF_V_BLOCK_PARAM; rule_idx = k;
-                    } else if (w > 0) {
-                        wait += w;
-                    }
-                }
-            }
-            if (!blocked) {                                     // FlowRuleChecker.checkFlow :44-59
-                const bool prio = (fl & SF_EV_PRIO) != 0;
-                for (uint32_t k = 0; k < r1 - r0; k++) {
-                    const DevRule& r = st.rules[r0 + k];
-                    if (r.always_pass) continue;                // cluster rule, no fallback (:184-193)
-                    const int sel = xflow_select(st, r, r0, r1, origin, ctx);
-                    if (sel == XS_NONE) continue;
-                    DevRuleState rs = st.rstate[r0 + k];
-                    int64_t w = 0; bool pw = false; int ok = 1;
-                    if (sel == XS_CLUSTER || (sel == XS_REF && r.ref == l)) {
-                        ok = can_pass<MAXS>(r, rs, cn, now, c, prio, st.occupy_timeout, &w, &pw);
-                    } else if (sel == XS_ORIGIN) {
-                        if (oi != XNONE) ok = can_pass<MAXS>(r, rs, on, now, c, prio, st.occupy_timeout, &w, &pw);
-                    } else if (sel == XS_CTX) {
-                        if (di != XNONE) ok = can_pass<MAXS>(r, rs, dn, now, c, prio, st.occupy_timeout, &w, &pw);
-                    } else {                                    // RELATE: another resource of the group
-                        const NodeRows rr = cluster_rows(st, r.ref);
-                        if (node_created(st, rr)) {
-                            NodeWin<MAXS> rn;
-                            nw_load(rn, st, rr);
-                            ok = can_pass<MAXS>(r, rs, rn, now, c, prio, st.occupy_timeout, &w, &pw);
-                            nw_store(rn, st, rr);
-                        }
-                    }
-                    st.rstate[r0 + k] = rs;
-                    if (pw) { prio_wait = true; wait += w; rule_idx = (int)k; break; }
-                    if (!ok) { blocked = true; status = SF_V_BLOCK_FLOW; rule_idx = (int)k; break; }
-                    wait += w;
-                }
-            }
-            if (!blocked && !prio_wait && cb1 > cb0) {          // DegradeSlot.entry (DegradeSlot.java:42-61)
-                const int k = dg_entry_check(st.dg_state, cb0, cb1, now);
-                if (k >= 0) { blocked = true; status = SF_V_BLOCK_DEGRADE; rule_idx = k; }
-            }
-            // StatisticSlot.entry accounting :64-123 (DefaultNode -> ClusterNode, origin node)
-            if (blocked) {
-                if (di != XNONE) dn.add_block(now, c);
-                cn.add_block(now, c);
-                if (oi != XNONE) on.add_block(now, c);
-            } else {
-                if (di != XNONE) dn.threads++;
-                cn.threads++;
-                if (oi != XNONE) on.threads++;
-                if (prio_wait) {
-                    status = SF_V_PRIORITY_WAIT;
-                } else {
-                    if (di != XNONE) dn.add_pass(now, c);
-                    cn.add_pass(now, c);
-                    if (oi != XNONE) on.add_pass(now, c);
-                    status = wait > 0 ? SF_V_PASS_WAIT : SF_V_PASS;
-                }
-                if (pm_exists) pm_thread_event(pt, l, pm_init, io, j, na, +1);
-            }
-        }
-        if (nprules) st.pm_init[l] = pm_init;
-        io.v_status[j] = status;
-        emit_verdict(io, j, status, (int32_t)wait, (uint16_t)rule_idx);
-    }
+    for (uint32_t j = lo; j < hi; j++) xg_event<MAXS>(st, io, pt, lo, j, cn, on, dn, cl, oi, di);
     if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl));
     if (oi != XNONE) nw_store(on, st, aux_rows(st, oi));
     if (di != XNONE) nw_store(dn, st, aux_rows(st, di));
 }
 
+// ============================================================ wave walk eligibility
+enum : uint8_t { XWF_ON = 1, XWF_THREAD = 2 };
+constexpr uint32_t XW_MIN = 256;               // shorter xflow segments stay on k_decide_x's lanes
+// a segment of resource l (its own group) with all-DIRECT rules, no ParamFlow
+// rule and no circuit breaker, at least XW_MIN events: k_decide_xw
+SF_HD bool xw_take(const DevState& st, uint32_t l, uint32_t len) {
+    if (len < XW_MIN || !st.xw || !(st.xw[l] & XWF_ON)) return false;
+    if (st.prule_off[l + 1] != st.prule_off[l]) return false;
+    uint32_t b0, b1;
+    breakers_of(st, l, &b0, &b1);
+    return b0 == b1;
+}
+
 // ============================================================ groups (host side)
+// xw[l] for the resources of one-member groups whose rules all check DIRECT
+// (their ClusterNode or an origin node: no RELATE / CHAIN)
+inline void build_xw(const DevRule* dr, const uint32_t* off, uint32_t R, const std::vector<uint32_t>& xmap,
+                     std::vector<uint8_t>& xw) {
+    xw.assign(R, 0);
+    std::vector<uint32_t> members(R, 0);
+    for (uint32_t l = 0; l < R; l++)
+        if (xmap[l] != XNONE) members[xmap[l]]++;
+    for (uint32_t l = 0; l < R; l++) {
+        if (xmap[l] != l || members[l] != 1) continue;
+        uint8_t f = XWF_ON;
+        for (uint32_t k = off[l]; k < off[l + 1]; k++) {
+            if (dr[k].strategy != SF_STRATEGY_DIRECT) { f = 0; break; }
+            if (dr[k].grade == SF_GRADE_THREAD) f |= XWF_THREAD;
+        }
+        xw[l] = f;
+    }
+}
+
 // A rule runs on the xflow walk unless it is limitApp "default" + DIRECT and
 // not a cluster rule without fallback.
 inline bool rule_is_ext(const DevRule& r) {
