@@ -47,6 +47,11 @@ final class SentinelFlowNative {
             FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, ADDRESS));
     // decisions
     static final MethodHandle SUBMIT = fn("sf_submit", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
+    static final MethodHandle SUBMIT_PACKED = fn("sf_submit_packed",
+            FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
+    // page-locked host memory (the batch arrays: the H2D copy runs at PCIe speed)
+    static final MethodHandle HOST_ALLOC = fn("sf_host_alloc",
+            FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));
     static final MethodHandle DEGRADE_SUBMIT = fn("sf_degrade_submit",
             FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
     // cluster token server
@@ -114,6 +119,14 @@ final class SentinelFlowNative {
             ADDRESS.withName("arg_elem_off"), ADDRESS.withName("elem_tag"), ADDRESS.withName("elem_bits"),
             JAVA_INT.withName("n_elems"), MemoryLayout.paddingLayout(4),
             ADDRESS.withName("origin"), ADDRESS.withName("context"));
+
+    /** sf_packed_batch: 8 bytes per event (res | ts - ts_base << 32 | count << 52 | flags << 59). */
+    static final StructLayout PACKED_BATCH = MemoryLayout.structLayout(
+            JAVA_INT.withName("n"), JAVA_INT.withName("mem"), JAVA_LONG.withName("ts_base"),
+            ADDRESS.withName("ev"), ADDRESS.withName("exit_ref"), ADDRESS.withName("exit_cts"),
+            ADDRESS.withName("count_ext"), ADDRESS.withName("origin"),
+            JAVA_INT.withName("n_exit"), JAVA_INT.withName("n_count_ext"));
+    static final int PK_COUNT_SHIFT = 52, PK_FLAGS_SHIFT = 59;
 
     /** sf_verdicts. */
     static final StructLayout VERDICTS = MemoryLayout.structLayout(

@@ -401,9 +401,12 @@ __global__ void __launch_bounds__(64) k_decide_x(DevState st, SegIO io, const ui
 //     `default`), on the node and rule state as they stand at the chunk's
 //     start.  Within one bucket a node's pass count and a RateLimiter's
 //     latestPassedTime only grow, the WarmUp threshold is fixed for the second
-//     (syncToken reads the previous second), and a THREAD count can fall at
-//     most by the exits ahead of the lane in the chunk, so an entry blocked at
-//     the start state is blocked in the serial order too, by that rule;
+//     (syncToken reads the previous second; on an origin node it waits until
+//     the walk has synced the second, since the rule's tokens are shared by
+//     every origin and the first check of the second decides them), and a
+//     THREAD count can fall at most by the exits ahead of the lane in the
+//     chunk, so an entry blocked at the start state is blocked in the serial
+//     order too, by that rule;
 //  2. lane 0 runs the reference walk (xg_event) over the other entries --
 //     those the start state lets pass, prioritized entries, and the exits when
 //     a THREAD rule reads thread counts -- in order;
@@ -480,6 +483,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             }
             if (lane == 0) {
                 if (cl != l) { if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl)); nw_load(cn, st, cluster_rows(st, l)); cl = l; }
+                cn.min_flush();                              // (a copy that moves to another minute slot reads HBM)
                 snap = cn;
                 if (oi != XNONE) { nw_store(on, st, aux_rows(st, oi)); oi = XNONE; }
             }
@@ -510,11 +514,16 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                     DevRuleState rs = st.rstate[k];
                     int64_t w = 0; bool pw = false; int ok = 1;
                     if (sel == XS_CLUSTER) {
-                        NodeWin<MAXS> x = snap;
-                        x.mdirty = 0;                            // (a copy: never written back)
+                        NodeWin<MAXS> x = snap;                  // (minute bucket clean: never written back)
                         x.threads -= ex_before;
                         ok = can_pass<MAXS>(r, rs, x, t, c, false, st.occupy_timeout, &w, &pw);
                     } else if (sel == XS_ORIGIN) {
+                        // a WarmUp rule shared by several origin nodes (`other`) syncs its
+                        // tokens at the second's first check, with THAT event's origin's
+                        // previous QPS: until the walk has synced this second, its entries
+                        // stay in the serial part
+                        const bool warm = r.kind == CT_WARM_UP || r.kind == CT_WARM_UP_RATE_LIMITER;
+                        if (warm && rs.last_filled < t - t % 1000) break;
                         const uint32_t ko = aux_get(st, l, AX_ORIGIN, origin);
                         if (ko != XNONE) {
                             NodeWin<MAXS> x;
