@@ -414,12 +414,19 @@ __global__ void __launch_bounds__(64) k_decide_x(DevState st, SegIO io, const ui
 //     add to the chunk's buckets (which no check of this chunk reads), so they
 //     are summed per node in LDS and added once per node.
 // Verdicts, node state and rule state equal the serial walk's.
-enum : uint8_t { XWC_SERIAL = 1, XWC_BLOCK = 2, XWC_EXIT = 3 };
+enum : uint8_t { XWC_SERIAL = 1, XWC_BLOCK = 2, XWC_EXIT = 3, XWC_PASS = 4 };
 constexpr uint32_t XW_KCAP = 128;                 // LDS node rows of a chunk (<= 64 origins + the ClusterNode)
-struct XwRow { unsigned long long blk, succ, rt, exc; long long thr, minrt; unsigned int nblk, ncmp, nexc, key; };
+struct XwRow {
+    unsigned long long blk, succ, rt, exc, pass; long long thr, minrt;
+    unsigned int nblk, ncmp, nexc, npass, key, pad;
+};
 __device__ __forceinline__ void xw_add(XwRow& r, int64_t blk, int nblk, int64_t succ, int64_t rt, int64_t minrt,
-                                       int64_t exc, int nexc, int64_t thr, int ncmp) {
+                                       int64_t exc, int nexc, int64_t thr, int ncmp, int64_t pass = 0, int npass = 0) {
     if (nblk) { atomicAdd(&r.blk, (unsigned long long)blk); atomicAdd(&r.nblk, 1u); }
+    if (npass) {
+        atomicAdd(&r.pass, (unsigned long long)pass); atomicAdd(&r.npass, 1u);
+        atomicAdd((unsigned long long*)&r.thr, 1ull);
+    }
     if (ncmp) {
         atomicAdd(&r.succ, (unsigned long long)succ); atomicAdd(&r.rt, (unsigned long long)rt);
         atomicMin(&r.minrt, (long long)minrt); atomicAdd((unsigned long long*)&r.thr, (unsigned long long)thr);
@@ -430,6 +437,11 @@ __device__ __forceinline__ void xw_add(XwRow& r, int64_t blk, int nblk, int64_t 
 // a row's sums into a node (all events of the chunk are in the bucket of t0)
 template <int MAXS>
 __device__ __forceinline__ void xw_apply(NodeWin<MAXS>& nd, const XwRow& r, int64_t t0) {
+    if (r.npass) {
+        const int64_t p = (int64_t)r.pass;
+        nd.sec_apply(t0, [&](Bucket& x) { x.pass = wadd(x.pass, p); });
+        nd.min_apply(t0, [&](Bucket& x) { x.pass = wadd(x.pass, p); });
+    }
     if (r.nblk) {
         const int64_t b = (int64_t)r.blk;
         nd.sec_apply(t0, [&](Bucket& x) { x.block = wadd(x.block, b); });
@@ -440,12 +452,262 @@ __device__ __forceinline__ void xw_apply(NodeWin<MAXS>& nd, const XwRow& r, int6
         auto f = [&](Bucket& x) { x.succ = wadd(x.succ, sc); x.rt = wadd(x.rt, rt); if (mr < x.min_rt) x.min_rt = mr; };
         nd.sec_apply(t0, f);
         nd.min_apply(t0, f);
-        nd.threads = wadd(nd.threads, r.thr);
     }
+    if (r.npass || r.ncmp) nd.threads = wadd(nd.threads, r.thr);
     if (r.nexc) {
         const int64_t e = (int64_t)r.exc;
         nd.sec_apply(t0, [&](Bucket& x) { x.exc = wadd(x.exc, e); });
         nd.min_apply(t0, [&](Bucket& x) { x.exc = wadd(x.exc, e); });
+    }
+}
+
+// ---- the exact chunk solve (S <= 2, no prioritized entry in the chunk)
+// The chunk's verdicts as the fixed point of the serial recurrence: each
+// entry's checks read its nodes' pass counts / thread counts and each
+// RateLimiter's latestPassedTime as left by the entries before it in the
+// chunk; given a guess of every verdict (all pass to start), every lane
+// re-evaluates its entry from prefix sums over the earlier lanes (pass counts
+// per node, thread deltas per node with the exits' liveness from their
+// entries' verdicts, a max-plus scan x -> max(x + cost, t) per RateLimiter
+// rule over the entries that passed it).  Each round makes at least the
+// earliest wrong lane right (its inputs come only from earlier lanes), so the
+// iteration reaches the serial result within L + 1 rounds; under saturation
+// two or three.  Node bases are read once per chunk: a pass count is its
+// window sum at the chunk's time plus the chunk's earlier passes (all events
+// of the chunk fall in the same current bucket, every older bucket stays
+// valid through it), the WarmUp threshold and the RateLimiter cost are fixed
+// for the second (the ClusterNode's syncToken is applied on a copy: its
+// previous-second QPS is the same for every event).
+struct XwRuleC { double thr, qps; int64_t lstart; DevRuleState rs; int32_t sync, pad; };
+struct XwScratch {
+    long long base[XW_KCAP], thr[XW_KCAP];
+    uint32_t ko[XW_KCAP];
+    int os[64];
+    long long cm[64], td[64];
+    XwRuleC rc[MAX_RULES];
+};
+constexpr long long XW_MPNEG = INT64_MIN / 4;                  // max-plus "minus infinity"
+
+__device__ __forceinline__ long long xw_excl_scan(long long v, uint32_t lane) {
+    long long x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(x, o);
+        if ((int)lane >= o) x += y;
+    }
+    return x - v;
+}
+// inclusive max-plus scan of f(x) = max(x + a, b) in lane order
+__device__ __forceinline__ void xw_mp_scan(long long& a, long long& b, uint32_t lane) {
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long pa = __shfl_up(a, o), pb = __shfl_up(b, o);
+        if ((int)lane >= o) {
+            const long long nb = max(pb + a, b);
+            a = pa + a;
+            b = nb;
+        }
+    }
+}
+
+__device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& snap, XwRow* rows, XwScratch& xs,
+                               uint32_t lane, uint32_t L, uint32_t lo, uint32_t j0, uint32_t j, int64_t t0, int64_t t,
+                               uint8_t fl, int32_t c, uint32_t origin, uint32_t gres, uint32_t l, uint32_t r0,
+                               uint32_t r1, uint8_t* myc, uint8_t* mst, int* mrule, int64_t* mwait) {
+    const bool valid = lane < L;
+    const bool is_exit = valid && (fl & SF_EV_EXIT);
+    const bool is_sys = valid && !is_exit && (fl & EVF_SYSBLK);
+    const bool is_solve = valid && !is_exit && !is_sys;
+    const uint32_t nrules = r1 - r0;
+    // the chunk's origin rows (row 0: the ClusterNode)
+    int osr = -1;
+    bool leader = false;
+    if (valid && origin != SF_ORIGIN_NONE) {
+        uint32_t h = 1 + (uint32_t)(mix64(origin) % (XW_KCAP - 1));
+        for (;;) {
+            const unsigned int prev = atomicCAS(&rows[h].key, 0u, origin + 1u);
+            if (prev == 0u) { leader = true; break; }
+            if (prev == origin + 1u) break;
+            h = h + 1 < XW_KCAP ? h + 1 : 1;
+        }
+        osr = (int)h;
+    }
+    xs.os[lane] = osr;
+    __syncthreads();
+    // node bases and the rules' constants for the chunk
+    if (leader) {
+        const uint32_t ko = aux_get(st, l, AX_ORIGIN, origin);
+        xs.ko[osr] = ko;
+        long long b = 0, th = 0;
+        if (ko != XNONE) {
+            NodeWin<2> x;
+            nw_load(x, st, aux_rows(st, ko));
+            b = x.sec_sum_pass(t0);
+            th = x.threads;
+        }
+        xs.base[osr] = b; xs.thr[osr] = th;
+    }
+    if (lane == 0) {
+        NodeWin<2> x = snap;
+        xs.base[0] = x.sec_sum_pass(t0);
+        xs.thr[0] = x.threads;
+        const int64_t prevq = j_d2l(x.previous_pass_qps(t0));
+        for (uint32_t k = r0; k < r1; k++) {
+            const DevRule& r = st.rules[k];
+            XwRuleC& q = xs.rc[k - r0];
+            q.rs = st.rstate[k];
+            q.sync = 0;
+            q.thr = r.count; q.qps = r.count;
+            if (r.kind == CT_WARM_UP || r.kind == CT_WARM_UP_RATE_LIMITER) {
+                if (r.limit_app == SF_APP_DEFAULT && q.rs.last_filled < t0 - t0 % 1000) {
+                    warm_sync(r, q.rs, t0, prevq);           // (the ClusterNode's previous second)
+                    q.sync = 1;
+                }
+                const int64_t rest = q.rs.stored_tokens;
+                if (rest >= r.warning_token) {
+                    const int64_t above = rest - r.warning_token;
+                    const double wq = j_next_up(1.0 / ((double)above * r.slope + 1.0 / r.count));
+                    q.thr = wq; q.qps = wq;
+                }
+            }
+            q.lstart = q.rs.latest_passed;
+        }
+    }
+    __syncthreads();
+    const double isec = st.interval / 1000.0;
+    uint64_t sm = 0;                                           // earlier lanes of the same origin
+    if (osr >= 0)
+        for (int q = 0; q < 64; q++)
+            if (xs.os[q] == osr) sm |= 1ull << q;
+    sm &= (1ull << lane) - 1ull;
+    uint8_t sel[MAX_RULES];                                    // 0 none, 1 ClusterNode, 2 origin node
+    long long cost[MAX_RULES];
+    for (uint32_t kr = 0; kr < (uint32_t)MAX_RULES; kr++) {
+        sel[kr] = 0; cost[kr] = -1;
+        if (kr >= nrules) continue;
+        const DevRule& r = st.rules[r0 + kr];
+        if (is_solve && !r.always_pass) {
+            const int s_ = xflow_select(st, r, r0, r1, origin, 0u);
+            if (s_ == XS_CLUSTER) sel[kr] = 1;
+            else if (s_ == XS_ORIGIN && osr >= 0 && xs.ko[osr] != XNONE) sel[kr] = 2;
+        }
+        if (r.kind == CT_RATE_LIMITER) {
+            if (c > 0 && r.count > 0) cost[kr] = j_round(1.0 * c / r.count * 1000);
+        } else if (r.kind == CT_WARM_UP_RATE_LIMITER) {
+            cost[kr] = j_round(1.0 * c / xs.rc[kr].qps * 1000);
+        }
+    }
+    // an exit's liveness: its entry passed (in this chunk: that lane's verdict)
+    int eidx = -1;
+    bool live_pre = false;
+    if (is_exit) {
+        const int64_t ref = io.eref ? io.eref[j] : -1;
+        if (ref >= 0) {
+            const bool bad = ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT) ||
+                             io.ev_res[io.perm[ref]] != gres;
+            if (!bad) {
+                if (ref >= (int64_t)j0) eidx = (int)(ref - j0);
+                else live_pre = !v_blocked(io.v_status[ref]);
+            }
+        } else {
+            live_pre = ref != EREF_DEAD;
+        }
+    }
+    int d = is_solve ? 1 : 0, ri = 0;
+    uint32_t reach = 0, passk = 0;
+    long long w = 0;
+    for (int it = 0; it < 72; it++) {
+        const int ed = __shfl(d, eidx >= 0 ? eidx : (int)lane);
+        const bool live = is_exit && (eidx >= 0 ? ed != 0 : live_pre);
+        const long long pc = (is_solve && d) ? (long long)c : 0;
+        const long long td = ((is_solve && d) ? 1 : 0) - (live ? 1 : 0);
+        const long long Pc = xw_excl_scan(pc, lane), Tc = xw_excl_scan(td, lane);
+        xs.cm[lane] = pc; xs.td[lane] = td;
+        __syncthreads();
+        long long Po = 0, To = 0;
+        for (uint64_t m = sm; m; m &= m - 1) {
+            const int q = __ffsll((long long)m) - 1;
+            Po += xs.cm[q]; To += xs.td[q];
+        }
+        __syncthreads();
+        int nd = is_solve ? 1 : 0, nri = 0;
+        uint32_t nreach = 0, npass = 0;
+        long long nw = 0;
+        for (uint32_t kr = 0; kr < nrules; kr++) {
+            const DevRule& r = st.rules[r0 + kr];
+            const bool rlk = r.kind == CT_RATE_LIMITER || r.kind == CT_WARM_UP_RATE_LIMITER;
+            long long lat = 0;
+            if (rlk) {                                         // latestPassedTime before this lane
+                long long a = 0, b = XW_MPNEG;
+                if (((passk >> kr) & 1u) && cost[kr] >= 0) { a = cost[kr]; b = t; }
+                xw_mp_scan(a, b, lane);
+                long long ea = __shfl_up(a, 1), eb = __shfl_up(b, 1);
+                if (lane == 0) { ea = 0; eb = XW_MPNEG; }
+                lat = max(xs.rc[kr].lstart + ea, eb);
+            }
+            if (!nd || !sel[kr]) continue;
+            nreach |= 1u << kr;
+            const bool on_c = sel[kr] == 1;
+            const long long base = on_c ? xs.base[0] : xs.base[osr];
+            const long long P = on_c ? Pc : Po;
+            const long long T = on_c ? xs.thr[0] + Tc : xs.thr[osr] + To;
+            bool ok = true;
+            long long ww = 0;
+            if (r.kind == CT_DEFAULT) {                        // DefaultController.canPass (prio excluded)
+                const int32_t cur = r.grade == SF_GRADE_THREAD ? (int32_t)T : j_d2i((double)(base + P) / isec);
+                ok = !((double)(int32_t)((uint32_t)cur + (uint32_t)c) > r.count);
+            } else if (r.kind == CT_WARM_UP) {                 // WarmUpController.canPass
+                const int64_t pq = j_d2l((double)(base + P) / isec);
+                ok = (double)(pq + c) <= xs.rc[kr].thr;
+            } else if (r.kind == CT_RATE_LIMITER && c <= 0) {
+                ok = true;
+            } else if (r.kind == CT_RATE_LIMITER && r.count <= 0) {
+                ok = false;
+            } else {                                           // RateLimiter / WarmUpRateLimiter
+                const long long expected = cost[kr] + lat;
+                if (expected > t) {
+                    ww = expected - t;
+                    ok = ww <= r.max_queue_ms;
+                    if (!ok) ww = 0;
+                }
+            }
+            if (!ok) { nd = 0; nri = (int)kr; }
+            else { npass |= 1u << kr; nw += ww; }
+        }
+        const bool changed = nd != d || nreach != reach || npass != passk || nw != w || nri != ri;
+        d = nd; reach = nreach; passk = npass; w = nw; ri = nri;
+        if (!__ballot(changed)) break;
+    }
+    // the rules' state after the chunk (lane 0 writes)
+    for (uint32_t kr = 0; kr < nrules; kr++) {
+        const DevRule& r = st.rules[r0 + kr];
+        const bool rlk = r.kind == CT_RATE_LIMITER || r.kind == CT_WARM_UP_RATE_LIMITER;
+        const bool any_reach = __ballot((reach >> kr) & 1u) != 0ull;
+        bool any_pass = false;
+        long long fin = 0;
+        if (rlk) {
+            long long a = 0, b = XW_MPNEG;
+            const bool el = ((passk >> kr) & 1u) && cost[kr] >= 0;
+            if (el) { a = cost[kr]; b = t; }
+            any_pass = __ballot(el) != 0ull;
+            xw_mp_scan(a, b, lane);
+            a = __shfl(a, 63); b = __shfl(b, 63);
+            fin = max(xs.rc[kr].lstart + a, b);
+        }
+        if (lane == 0 && ((xs.rc[kr].sync && any_reach) || any_pass)) {
+            DevRuleState rs = st.rstate[r0 + kr];
+            if (xs.rc[kr].sync && any_reach) { rs.stored_tokens = xs.rc[kr].rs.stored_tokens; rs.last_filled = xs.rc[kr].rs.last_filled; }
+            if (any_pass) rs.latest_passed = fin;
+            st.rstate[r0 + kr] = rs;
+        }
+    }
+    if (is_solve) {
+        *myc = d ? XWC_PASS : XWC_BLOCK;
+        *mst = d ? (uint8_t)(w > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : (uint8_t)SF_V_BLOCK_FLOW;
+        *mrule = d ? 0 : ri;
+        *mwait = w;
+    } else if (is_sys) {
+        *myc = XWC_BLOCK; *mst = sysblk_status(fl); *mrule = sysblk_rule(fl); *mwait = 0;
+    } else if (is_exit) {
+        *myc = XWC_EXIT;
     }
 }
 
@@ -456,6 +718,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
     __shared__ __align__(16) unsigned char snap_raw[sizeof(NodeWin<MAXS>)];
     __shared__ uint8_t cls[64];
     __shared__ XwRow rows[XW_KCAP];
+    __shared__ XwScratch xs;
     NodeWin<MAXS>& snap = *reinterpret_cast<NodeWin<MAXS>*>(snap_raw);
     const uint32_t lane = threadIdx.x;
     const ParamTable pt{st.ptab, st.pcap_mask, st.err, st.pins};
@@ -478,8 +741,9 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             const unsigned long long nb = __ballot(!same);
             const uint32_t L = nb ? (uint32_t)(__ffsll((long long)nb) - 1) : 64u;   // (lane 0 is always in)
             for (uint32_t k = lane; k < XW_KCAP; k += 64) {
-                rows[k].blk = rows[k].succ = rows[k].rt = rows[k].exc = 0; rows[k].thr = 0; rows[k].minrt = INT64_MAX;
-                rows[k].nblk = rows[k].ncmp = rows[k].nexc = 0; rows[k].key = 0;
+                rows[k].blk = rows[k].succ = rows[k].rt = rows[k].exc = rows[k].pass = 0; rows[k].thr = 0;
+                rows[k].minrt = INT64_MAX;
+                rows[k].nblk = rows[k].ncmp = rows[k].nexc = rows[k].npass = 0; rows[k].key = 0;
             }
             if (lane == 0) {
                 if (cl != l) { if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl)); nw_load(cn, st, cluster_rows(st, l)); cl = l; }
@@ -491,6 +755,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             // 1. classify
             uint8_t myc = 0, mst = 0;
             int mrule = 0;
+            int64_t mwait = 0;
             uint32_t origin = SF_ORIGIN_NONE, gres = 0;
             int32_t c = 0;
             uint8_t fl = 0;
@@ -499,45 +764,65 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                 const uint32_t i = io.perm[j];
                 gres = io.ev_res[i];
                 origin = io.ev_origin ? io.ev_origin[i] : SF_ORIGIN_NONE;
-                if (fl & SF_EV_EXIT) myc = thr_sens ? XWC_SERIAL : XWC_EXIT;
-                else if (fl & EVF_SYSBLK) { myc = XWC_BLOCK; mst = sysblk_status(fl); mrule = sysblk_rule(fl); }
-                else myc = XWC_SERIAL;
             }
-            const unsigned long long exits = __ballot(lane < L && (fl & SF_EV_EXIT));
-            const int64_t ex_before = (int64_t)__popcll(exits & ((1ull << lane) - 1ull));
-            if (myc == XWC_SERIAL && !(fl & (SF_EV_EXIT | SF_EV_PRIO))) {
-                for (uint32_t k = r0; k < r1; k++) {
+            // the exact chunk solve (below) unless a prioritized entry is in the chunk
+            // (its occupy path) or an origin-node WarmUp rule has not synced this second
+            bool jac = false;
+            if constexpr (MAXS == 2) {
+                jac = __ballot(lane < L && !(fl & (SF_EV_EXIT | EVF_SYSBLK)) && (fl & SF_EV_PRIO)) == 0ull;
+                for (uint32_t k = r0; k < r1 && jac; k++) {
                     const DevRule& r = st.rules[k];
-                    if (r.always_pass) continue;
-                    const int sel = xflow_select(st, r, r0, r1, origin, 0u);
-                    if (sel == XS_NONE) continue;
-                    DevRuleState rs = st.rstate[k];
-                    int64_t w = 0; bool pw = false; int ok = 1;
-                    if (sel == XS_CLUSTER) {
-                        NodeWin<MAXS> x = snap;                  // (minute bucket clean: never written back)
-                        x.threads -= ex_before;
-                        ok = can_pass<MAXS>(r, rs, x, t, c, false, st.occupy_timeout, &w, &pw);
-                    } else if (sel == XS_ORIGIN) {
-                        // a WarmUp rule shared by several origin nodes (`other`) syncs its
-                        // tokens at the second's first check, with THAT event's origin's
-                        // previous QPS: until the walk has synced this second, its entries
-                        // stay in the serial part
-                        const bool warm = r.kind == CT_WARM_UP || r.kind == CT_WARM_UP_RATE_LIMITER;
-                        if (warm && rs.last_filled < t - t % 1000) break;
-                        const uint32_t ko = aux_get(st, l, AX_ORIGIN, origin);
-                        if (ko != XNONE) {
-                            NodeWin<MAXS> x;
-                            nw_load(x, st, aux_rows(st, ko));
+                    if ((r.kind == CT_WARM_UP || r.kind == CT_WARM_UP_RATE_LIMITER) && r.limit_app != SF_APP_DEFAULT &&
+                        st.rstate[k].last_filled < t0 - t0 % 1000)
+                        jac = false;
+                }
+            }
+            if (jac) {
+                if constexpr (MAXS == 2)
+                    xw_solve_chunk(st, io, snap, rows, xs, lane, L, lo, j0, j, t0, t, fl, c, origin, gres, l, r0, r1,
+                                   &myc, &mst, &mrule, &mwait);
+            } else {
+                if (lane < L) {
+                    if (fl & SF_EV_EXIT) myc = thr_sens ? XWC_SERIAL : XWC_EXIT;
+                    else if (fl & EVF_SYSBLK) { myc = XWC_BLOCK; mst = sysblk_status(fl); mrule = sysblk_rule(fl); }
+                    else myc = XWC_SERIAL;
+                }
+                const unsigned long long exits = __ballot(lane < L && (fl & SF_EV_EXIT));
+                const int64_t ex_before = (int64_t)__popcll(exits & ((1ull << lane) - 1ull));
+                if (myc == XWC_SERIAL && !(fl & (SF_EV_EXIT | SF_EV_PRIO))) {
+                    for (uint32_t k = r0; k < r1; k++) {
+                        const DevRule& r = st.rules[k];
+                        if (r.always_pass) continue;
+                        const int sel = xflow_select(st, r, r0, r1, origin, 0u);
+                        if (sel == XS_NONE) continue;
+                        DevRuleState rs = st.rstate[k];
+                        int64_t w = 0; bool pw = false; int ok = 1;
+                        if (sel == XS_CLUSTER) {
+                            NodeWin<MAXS> x = snap;                  // (minute bucket clean: never written back)
                             x.threads -= ex_before;
                             ok = can_pass<MAXS>(r, rs, x, t, c, false, st.occupy_timeout, &w, &pw);
+                        } else if (sel == XS_ORIGIN) {
+                            // a WarmUp rule shared by several origin nodes (`other`) syncs its
+                            // tokens at the second's first check, with THAT event's origin's
+                            // previous QPS: until the walk has synced this second, its entries
+                            // stay in the serial part
+                            const bool warm = r.kind == CT_WARM_UP || r.kind == CT_WARM_UP_RATE_LIMITER;
+                            if (warm && rs.last_filled < t - t % 1000) break;
+                            const uint32_t ko = aux_get(st, l, AX_ORIGIN, origin);
+                            if (ko != XNONE) {
+                                NodeWin<MAXS> x;
+                                nw_load(x, st, aux_rows(st, ko));
+                                x.threads -= ex_before;
+                                ok = can_pass<MAXS>(r, rs, x, t, c, false, st.occupy_timeout, &w, &pw);
+                            }
                         }
+                        if (!ok) { myc = XWC_BLOCK; mst = SF_V_BLOCK_FLOW; mrule = (int)(k - r0); }
+                        break;                                   // only the first selecting rule decides here
                     }
-                    if (!ok) { myc = XWC_BLOCK; mst = SF_V_BLOCK_FLOW; mrule = (int)(k - r0); }
-                    break;                                   // only the first selecting rule decides here
                 }
             }
             if (lane < L) cls[lane] = myc;
-            if (myc == XWC_BLOCK) io.v_status[j] = mst;      // (before the walk: its exits read it)
+            if (myc == XWC_BLOCK || myc == XWC_PASS) io.v_status[j] = mst;   // (before the walk: its exits read it)
             __syncthreads();
             // 2. the serial walk over the undecided events
             if (lane == 0) {
@@ -549,9 +834,14 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             // 3. the blocks and completions, summed per node
             int64_t blk = 0, succ = 0, rt = 0, exc = 0, thr = 0, minrt = INT64_MAX;
             int nblk = 0, ncmp = 0, nexc = 0;
+            int64_t pss = 0;
+            int npss = 0;
             if (myc == XWC_BLOCK) {
-                emit_verdict(io, j, mst, 0, (uint16_t)mrule);
+                emit_verdict(io, j, mst, (int32_t)mwait, (uint16_t)mrule);
                 blk = c; nblk = 1;
+            } else if (myc == XWC_PASS) {
+                emit_verdict(io, j, mst, (int32_t)mwait, 0);
+                pss = c; npss = 1;
             } else if (myc == XWC_EXIT) {                    // decide_xgroup's exit (StatisticSlot.exit :134-165)
                 int64_t ref = io.eref ? io.eref[j] : -1;
                 bool blocked; int64_t cts;
@@ -575,8 +865,8 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                 io.v_status[j] = v;
                 emit_verdict(io, j, v, 0, 0);
             }
-            if (nblk || ncmp) {
-                xw_add(rows[0], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp);     // row 0: the ClusterNode
+            if (nblk || ncmp || npss) {
+                xw_add(rows[0], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp, pss, npss);   // row 0: the ClusterNode
                 if (origin != SF_ORIGIN_NONE) {
                     uint32_t h = 1 + (uint32_t)(mix64(origin) % (XW_KCAP - 1));
                     for (;;) {
@@ -584,7 +874,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                         if (prev == 0u || prev == origin + 1u) break;
                         h = h + 1 < XW_KCAP ? h + 1 : 1;
                     }
-                    xw_add(rows[h], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp);
+                    xw_add(rows[h], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp, pss, npss);
                 }
             }
             __syncthreads();

@@ -47,9 +47,10 @@
 namespace sf {
 
 constexpr int OX_T = 256;
-constexpr uint32_t OX_ITILE = 1024;            // events per k_ox_index workgroup
+constexpr uint32_t OX_ITILE = 2048;            // events per k_ox_index workgroup (one OX_TILE block)
 constexpr uint32_t OX_LTILE = 1024;            // sorted positions whose segments one k_ox_ilight workgroup lists
-constexpr uint32_t OX_KCAP = 2048;             // LDS key table (k_ox_index: <= 2 keys per event; k_ox_ilight: <= 1536 keys)
+constexpr uint32_t OX_KCAP = 2048;             // k_ox_ilight's LDS key table (<= 1536 keys)
+constexpr uint32_t OX_IKCAP = 4096;            // k_ox_index's (<= 2 keys per event)
 constexpr uint64_t AX_CLAIM = 1ull << 63;      // index slot being claimed (pkey_hi never sets bit 63: R < 2^30)
 constexpr uint32_t KS_CLAIMED = 0x80000000u;   // kslot: index-table position claimed this round (pool slots < 2^31)
 constexpr uint32_t HX_CLAIM = 0xfffffffeu;     // heavy id being assigned
@@ -63,24 +64,26 @@ __device__ __forceinline__ uint32_t ox_l(unsigned long long k) { return (uint32_
 __device__ __forceinline__ uint32_t ox_kind(unsigned long long k) { return (uint32_t)(k >> 32) & 3u; }
 
 // insert into a block's LDS key set; returns the position, *fresh when this call added it
+template <uint32_t CAP = OX_KCAP>
 __device__ __forceinline__ uint32_t ox_lds_insert(unsigned long long* keys, unsigned long long k, bool* fresh) {
-    uint32_t h = (uint32_t)(mix64(k) & (OX_KCAP - 1));
-    for (uint32_t p = 0; p < OX_KCAP; p++) {
+    uint32_t h = (uint32_t)(mix64(k) & (CAP - 1));
+    for (uint32_t p = 0; p < CAP; p++) {
         const unsigned long long prev = atomicCAS(&keys[h], 0ull, k);
         if (prev == 0ull) { *fresh = true; return h; }
         if (prev == k) { *fresh = false; return h; }
-        h = (h + 1) & (OX_KCAP - 1);
+        h = (h + 1) & (CAP - 1);
     }
     *fresh = false;
-    return XNONE;                                   // (unreachable: at most OX_KCAP keys)
+    return XNONE;                                   // (unreachable: at most CAP keys)
 }
+template <uint32_t CAP = OX_KCAP>
 __device__ __forceinline__ uint32_t ox_lds_find(const unsigned long long* keys, unsigned long long k) {
-    uint32_t h = (uint32_t)(mix64(k) & (OX_KCAP - 1));
-    for (uint32_t p = 0; p < OX_KCAP; p++) {
+    uint32_t h = (uint32_t)(mix64(k) & (CAP - 1));
+    for (uint32_t p = 0; p < CAP; p++) {
         const unsigned long long cur = keys[h];
         if (cur == k) return h;
         if (cur == 0ull) return XNONE;
-        h = (h + 1) & (OX_KCAP - 1);
+        h = (h + 1) & (CAP - 1);
     }
     return XNONE;
 }
@@ -107,7 +110,7 @@ struct OxIdx {
 // high word with release).  A key another workgroup is claiming is tried again
 // next round -- no thread waits on another workgroup across a barrier, so a
 // claimer always publishes.  key_of(p, &hi, &lo) gives LDS position p's key.
-template <class KeyOf>
+template <uint32_t CAP, class KeyOf>
 __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned long long* kk, uint32_t* kslot,
                            uint32_t lim, uint32_t* sh, KeyOf key_of) {
     ParamTable t{st.xtab, st.xcap_mask, st.err};
@@ -121,10 +124,10 @@ __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned lon
     // store: the fence makes the publisher's earlier stores visible).  A
     // candidate of the same resource and another origin continues the probe
     // with acquire loads (rare).
-    uint64_t cand[OX_KCAP / OX_T];
+    uint64_t cand[CAP / OX_T];
     bool any_cand = false;
 #pragma unroll
-    for (uint32_t k = 0; k < OX_KCAP / OX_T; k++) {
+    for (uint32_t k = 0; k < CAP / OX_T; k++) {
         const uint32_t p = k * OX_T + tid;
         cand[k] = ~0ull;
         if (!kk[p] || kslot[p] != XNONE) continue;
@@ -140,7 +143,7 @@ __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned lon
     }
     if (any_cand) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #pragma unroll
-    for (uint32_t k = 0; k < OX_KCAP / OX_T; k++) {
+    for (uint32_t k = 0; k < CAP / OX_T; k++) {
         const uint32_t p = k * OX_T + tid;
         if (!kk[p] || kslot[p] != XNONE) continue;
         if (cand[k] != ~0ull) {
@@ -175,7 +178,7 @@ __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned lon
     for (;;) {                                                   // 2. claim the absent keys, in rounds
         if (tid == 0) { sh[0] = 0; sh[1] = 0; }
         __syncthreads();
-        for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+        for (uint32_t p = tid; p < CAP; p += OX_T) {
             if (!kk[p] || kslot[p] != XNONE) continue;
             uint64_t khi, klo;
             key_of(p, &khi, &klo);
@@ -203,7 +206,7 @@ __device__ void ox_resolve(const DevState& st, uint32_t* cnt, const unsigned lon
         __syncthreads();
         if (tid == 0) { if (sh[0]) sh[3] = atomicAdd(st.ax_count, sh[0]); sh[0] = 0; }
         __syncthreads();
-        for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+        for (uint32_t p = tid; p < CAP; p += OX_T) {
             const uint32_t ks = kslot[p];
             if (ks == XNONE || !(ks & KS_CLAIMED)) continue;
             ParamSlot& s = t.slots[ks & ~KS_CLAIMED];
@@ -356,12 +359,12 @@ __global__ void __launch_bounds__(256) k_ox_lfind(DevState st, uint4* pairs, uin
 // origin node of every entry with an origin, the context node while a CHAIN
 // rule names the context: decide_xgroup's want_on / want_dn).
 __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxIdx ox, uint32_t lim) {
-    __shared__ unsigned long long kk[OX_KCAP];
-    __shared__ uint32_t kslot[OX_KCAP];
-    __shared__ uint8_t kheavy[OX_KCAP];
+    __shared__ unsigned long long kk[OX_IKCAP];
+    __shared__ uint32_t kslot[OX_IKCAP];
+    __shared__ uint8_t kheavy[OX_IKCAP];
     __shared__ uint32_t sh[4], bfl;
     const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < OX_KCAP; k += OX_T) { kk[k] = 0; kslot[k] = XNONE; kheavy[k] = 0; }
+    for (uint32_t k = tid; k < OX_IKCAP; k += OX_T) { kk[k] = 0; kslot[k] = XNONE; kheavy[k] = 0; }
     if (tid == 0) bfl = 0;
     __syncthreads();
     const uint32_t j0 = blockIdx.x * OX_ITILE, j1 = min(b.n, j0 + OX_ITILE);
@@ -386,14 +389,14 @@ __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxId
             ox.s_oslot[j] = XNONE;
             const uint32_t i = ox.perm[j];
             const uint32_t l = b.res[i] / st.shard_count;
-            if (o != SF_ORIGIN_NONE) { ox_lds_insert(kk, ox_pack(l, AX_ORIGIN, o), &fresh); any = true; }
+            if (o != SF_ORIGIN_NONE) { ox_lds_insert<OX_IKCAP>(kk, ox_pack(l, AX_ORIGIN, o), &fresh); any = true; }
             const uint32_t ctx = b.ctx ? b.ctx[i] : 0u;
             bool want = false;
             for (uint32_t r = st.rule_off[l]; r < st.rule_off[l + 1]; r++)
                 if (st.rules[r].strategy == SF_STRATEGY_CHAIN && st.rules[r].ref == ctx) want = true;
-            if (want) { ox_lds_insert(kk, ox_pack(l, AX_CTX, ctx), &fresh); any = true; }
+            if (want) { ox_lds_insert<OX_IKCAP>(kk, ox_pack(l, AX_CTX, ctx), &fresh); any = true; }
         } else if (o != SF_ORIGIN_NONE) {
-            const uint32_t p = ox_lds_insert(kk, ox_pack(ox.seg_res[sid], AX_ORIGIN, o), &fresh);
+            const uint32_t p = ox_lds_insert<OX_IKCAP>(kk, ox_pack(ox.seg_res[sid], AX_ORIGIN, o), &fresh);
             if (fresh) kheavy[p] = 1;
             kp[k] = p;
             any = true;
@@ -402,7 +405,7 @@ __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxId
         }
     }
     if (__syncthreads_or(any) == 0) return;
-    ox_resolve(st, ox.cnt, kk, kslot, lim, sh, [&](uint32_t p, uint64_t* hi, uint64_t* lo) {
+    ox_resolve<OX_IKCAP>(st, ox.cnt, kk, kslot, lim, sh, [&](uint32_t p, uint64_t* hi, uint64_t* lo) {
         const unsigned long long k = kk[p];
         *hi = pkey_hi(ox_l(k), PK_AUX, ox_kind(k), 0);
         *lo = (uint32_t)k;
@@ -412,7 +415,7 @@ __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxId
     // gives it an id; nothing in this kernel reads hmap, so no one waits
     if (tid == 0) sh[0] = 0;
     __syncthreads();
-    for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+    for (uint32_t p = tid; p < OX_IKCAP; p += OX_T) {
         const uint32_t a = kslot[p];
         if (!kheavy[p]) continue;
         kheavy[p] = 0;
@@ -430,7 +433,7 @@ __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxId
     __syncthreads();
     if (tid == 0) { if (sh[0]) sh[3] = atomicAdd(&ox.cnt[OXC_HEAVY], sh[0]); sh[0] = 0; }
     __syncthreads();
-    for (uint32_t p = tid; p < OX_KCAP; p += OX_T) {
+    for (uint32_t p = tid; p < OX_IKCAP; p += OX_T) {
         if (kheavy[p] != 2) continue;
         const uint32_t hid = sh[3] + atomicAdd(&sh[0], 1u);
         const uint32_t a = kslot[p];
