@@ -609,9 +609,11 @@ def config3_origin_leg(hb, rules, R, c3_ms, steps=5, warmup=2, parity=True, n_or
             res.update({"ms_per_step": round(ms, 3), "vs_config3": round(ms / c3_ms, 3),
                         "decisions_per_s": round(int(((ho.flags & abi.EV_EXIT) == 0).sum()) / (ms / 1e3), 1),
                         "origin_nodes": int(st.aux_nodes), "pool_capacity": int(st.aux_capacity),
+                        "wave_walk": {"chunks_exact": int(st.xw_chunks_exact), "chunks_serial": int(st.xw_chunks_serial),
+                                      "solve_rounds": int(st.xw_rounds), "serial_events": int(st.xw_serial_events)},
                         "index_grows": int(st.aux_index_grows)})
             log(f"[leg config3_origin] {name}: {ms:.2f} ms/step ({ms / c3_ms:.2f}x config 3), "
-                f"{st.aux_nodes} origin nodes")
+                f"{st.aux_nodes} origin nodes, wave walk {res['wave_walk']}")
             g0 = (out0.status.numpy(), out0.wait_ms.numpy(), out0.rule_idx.numpy())
             gl = (outv.status.numpy(), outv.wait_ms.numpy())
             gpu1 = {"origin": [abi.node_state_to_dict(e.read_origin_node(r, o)) for r, o in pairs],

@@ -380,6 +380,10 @@ typedef struct sf_stats {         /* device-clock timings, summed over sf_submit
     uint64_t aux_capacity;        /* pool slots backed by device memory (grows by chunks between batches) */
     uint64_t aux_index_grows;     /* times the pool's index table was rebuilt larger */
     uint64_t param_table_grows;   /* times the exact ParamFlow table was rebuilt larger (before a batch) */
+    /* the wave walk of long one-resource xflow segments (k_decide_xw): chunks
+     * settled by the exact solve, chunks on the serial path, solve rounds,
+     * events the serial part walked */
+    uint64_t xw_chunks_exact, xw_chunks_serial, xw_rounds, xw_serial_events;
 } sf_stats;
 
 typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last sf_submit */

@@ -198,7 +198,9 @@ class sf_stats(C.Structure):
                 ("heavy_fill_ms", C.c_double), ("classify_ms", C.c_double),
                 ("stream_ms", C.c_double), ("metric_scan_ms", C.c_double), ("metric_log_ms", C.c_double),
                 ("wire_ms", C.c_double), ("sys_rounds", C.c_uint64), ("aux_nodes", C.c_uint64),
-                ("aux_capacity", C.c_uint64), ("aux_index_grows", C.c_uint64), ("param_table_grows", C.c_uint64)]
+                ("aux_capacity", C.c_uint64), ("aux_index_grows", C.c_uint64), ("param_table_grows", C.c_uint64),
+                ("xw_chunks_exact", C.c_uint64), ("xw_chunks_serial", C.c_uint64), ("xw_rounds", C.c_uint64),
+                ("xw_serial_events", C.c_uint64)]
 
 
 class sf_heavy_profile(C.Structure):

@@ -188,7 +188,8 @@ void sf_destroy(sf_engine* e) {
     for (Work& w : e->w) free_work(w);
     void* ptrs[] = {e->st.second, e->st.borrow, e->st.minute, e->st.threads, (void*)e->st.rule_off,
                     (void*)e->st.rules, e->st.rstate, (void*)e->st.prule_off, e->st.prules, (void*)e->st.items,
-                    e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out, e->plan_stage, e->st.pins};
+                    e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out, e->plan_stage, e->st.pins,
+                    e->st.xw_stats};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     for (void* p : e->host_allocs) hipHostFree(p);
@@ -370,6 +371,8 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     HIP_TRY(hipMemsetAsync(st.pm_init, 0, R, e->stream));
     HIP_TRY(hipMemsetAsync(st.ptab, 0, pcap * sizeof(ParamSlot), e->stream));
     DALLOC(st.pins, 256 * 16 * sizeof(unsigned int));
+    DALLOC(st.xw_stats, 4 * sizeof(unsigned long long));
+    if (hipMemset(e->st.xw_stats, 0, 4 * sizeof(unsigned long long)) != hipSuccess) { sf_destroy(e); return fail(SF_ERR_DEVICE, "memset"); }
     HIP_TRY(hipMemsetAsync(st.pins, 0, 256 * 16 * sizeof(unsigned int), e->stream));
     HIP_TRY(hipMemsetAsync(st.err, 0, sizeof(int32_t), e->stream));
     HIP_TRY(launch_init_state(st, e->stream));
@@ -2133,6 +2136,11 @@ int sf_get_stats(sf_engine* e, sf_stats* out) {
     out->aux_capacity = e->st.ax_cap;
     out->aux_index_grows = e->aux_grows;
     out->param_table_grows = e->p_grows;
+    if (e->st.xw_stats) {
+        unsigned long long x[4];
+        HIP_TRY(hipMemcpy(x, e->st.xw_stats, sizeof x, hipMemcpyDeviceToHost));
+        out->xw_chunks_exact = x[0]; out->xw_chunks_serial = x[1]; out->xw_rounds = x[2]; out->xw_serial_events = x[3];
+    }
     return SF_OK;
 }
 int sf_set_timing(sf_engine* e, int enabled) {

@@ -89,6 +89,7 @@ struct DevState {
     ParamSlot* ptab;
     uint64_t pcap_mask;
     unsigned int* pins;            // [256 * 16] inserts into ptab (ParamTable::ins), null: not counted
+    unsigned long long* xw_stats;  // [4] wave walk: exact-solve chunks, serial-path chunks, solve rounds, serial events
     int32_t* err;                  // device error word (capacity, invalid input)
     int64_t* last_fetch;           // [R] StatisticNode.lastFetchTime (metric snapshot)
     int64_t* last_ts;              // engine clock: last event time of the previous batch (time never goes back)

@@ -487,6 +487,23 @@ struct XwScratch {
     XwRuleC rc[MAX_RULES];
 };
 constexpr long long XW_MPNEG = INT64_MIN / 4;                  // max-plus "minus infinity"
+// the segment's origin nodes held in LDS across chunks (exact-solve chunks
+// read and write them there; a chunk on the serial path, the end of the
+// segment, or a full cache writes them back)
+constexpr uint32_t XW_OC = XW_KCAP - 1;                        // (chunk row r = cache slot r - 1)
+struct XwCache { unsigned int key[XW_OC]; uint32_t ko[XW_OC]; unsigned int n; };
+__device__ __forceinline__ NodeWin<2>& xw_node(unsigned char* ocnw, uint32_t slot) {
+    return reinterpret_cast<NodeWin<2>*>(ocnw)[slot];
+}
+__device__ void xw_cache_flush(const DevState& st, XwCache& oc, unsigned char* ocnw, uint32_t lane) {
+    __syncthreads();
+    for (uint32_t k = lane; k < XW_OC; k += 64) {
+        if (oc.key[k] && oc.ko[k] != XNONE) nw_store(xw_node(ocnw, k), st, aux_rows(st, oc.ko[k]));
+        oc.key[k] = 0;
+    }
+    if (lane == 0) oc.n = 0;
+    __syncthreads();
+}
 
 __device__ __forceinline__ long long xw_excl_scan(long long v, uint32_t lane) {
     long long x = v;
@@ -509,37 +526,49 @@ __device__ __forceinline__ void xw_mp_scan(long long& a, long long& b, uint32_t 
 }
 
 __device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& snap, XwRow* rows, XwScratch& xs,
+                               XwCache& oc, unsigned char* ocnw,
                                uint32_t lane, uint32_t L, uint32_t lo, uint32_t j0, uint32_t j, int64_t t0, int64_t t,
                                uint8_t fl, int32_t c, uint32_t origin, uint32_t gres, uint32_t l, uint32_t r0,
-                               uint32_t r1, uint8_t* myc, uint8_t* mst, int* mrule, int64_t* mwait) {
+                               uint32_t r1, uint8_t* myc, uint8_t* mst, int* mrule, int64_t* mwait, int* my_row) {
     const bool valid = lane < L;
     const bool is_exit = valid && (fl & SF_EV_EXIT);
     const bool is_sys = valid && !is_exit && (fl & EVF_SYSBLK);
     const bool is_solve = valid && !is_exit && !is_sys;
     const uint32_t nrules = r1 - r0;
-    // the chunk's origin rows (row 0: the ClusterNode)
+    // the chunk's origin rows (row 0: the ClusterNode; row r: cache slot r - 1),
+    // a node loaded into the cache at its first event of the segment
+    if (oc.n + 64 > XW_OC) xw_cache_flush(st, oc, ocnw, lane);
     int osr = -1;
-    bool leader = false;
     if (valid && origin != SF_ORIGIN_NONE) {
-        uint32_t h = 1 + (uint32_t)(mix64(origin) % (XW_KCAP - 1));
+        uint32_t h = (uint32_t)(mix64(origin) % XW_OC);
         for (;;) {
-            const unsigned int prev = atomicCAS(&rows[h].key, 0u, origin + 1u);
-            if (prev == 0u) { leader = true; break; }
+            const unsigned int prev = atomicCAS(&oc.key[h], 0u, origin + 1u);
+            if (prev == 0u) {                                  // new in the cache: load it
+                atomicAdd(&oc.n, 1u);
+                const uint32_t ko = aux_get(st, l, AX_ORIGIN, origin);
+                oc.ko[h] = ko;
+                if (ko != XNONE) nw_load(xw_node(ocnw, h), st, aux_rows(st, ko));
+                break;
+            }
             if (prev == origin + 1u) break;
-            h = h + 1 < XW_KCAP ? h + 1 : 1;
+            h = h + 1 < XW_OC ? h + 1 : 0;
         }
-        osr = (int)h;
+        osr = (int)h + 1;
     }
     xs.os[lane] = osr;
     __syncthreads();
-    // node bases and the rules' constants for the chunk
-    if (leader) {
-        const uint32_t ko = aux_get(st, l, AX_ORIGIN, origin);
+    uint64_t sm = 0;                                           // earlier lanes of the same origin
+    if (osr >= 0)
+        for (int q = 0; q < 64; q++)
+            if (xs.os[q] == osr) sm |= 1ull << q;
+    sm &= (1ull << lane) - 1ull;
+    // node bases (the first lane of each origin) and the rules' constants
+    if (osr >= 0 && sm == 0) {
+        const uint32_t ko = oc.ko[osr - 1];
         xs.ko[osr] = ko;
         long long b = 0, th = 0;
         if (ko != XNONE) {
-            NodeWin<2> x;
-            nw_load(x, st, aux_rows(st, ko));
+            NodeWin<2> x = xw_node(ocnw, osr - 1);
             b = x.sec_sum_pass(t0);
             th = x.threads;
         }
@@ -573,11 +602,6 @@ __device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& 
     }
     __syncthreads();
     const double isec = st.interval / 1000.0;
-    uint64_t sm = 0;                                           // earlier lanes of the same origin
-    if (osr >= 0)
-        for (int q = 0; q < 64; q++)
-            if (xs.os[q] == osr) sm |= 1ull << q;
-    sm &= (1ull << lane) - 1ull;
     uint8_t sel[MAX_RULES];                                    // 0 none, 1 ClusterNode, 2 origin node
     long long cost[MAX_RULES];
     for (uint32_t kr = 0; kr < (uint32_t)MAX_RULES; kr++) {
@@ -674,6 +698,7 @@ __device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& 
         }
         const bool changed = nd != d || nreach != reach || npass != passk || nw != w || nri != ri;
         d = nd; reach = nreach; passk = npass; w = nw; ri = nri;
+        if (lane == 0 && st.xw_stats) atomicAdd(&st.xw_stats[2], 1ull);
         if (!__ballot(changed)) break;
     }
     // the rules' state after the chunk (lane 0 writes)
@@ -709,6 +734,7 @@ __device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& 
     } else if (is_exit) {
         *myc = XWC_EXIT;
     }
+    *my_row = osr;
 }
 
 template <int MAXS>
@@ -719,6 +745,8 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
     __shared__ uint8_t cls[64];
     __shared__ XwRow rows[XW_KCAP];
     __shared__ XwScratch xs;
+    __shared__ XwCache oc;
+    __shared__ __align__(16) unsigned char ocnw[MAXS == 2 ? XW_OC * sizeof(NodeWin<2>) : 16];
     NodeWin<MAXS>& snap = *reinterpret_cast<NodeWin<MAXS>*>(snap_raw);
     const uint32_t lane = threadIdx.x;
     const ParamTable pt{st.ptab, st.pcap_mask, st.err, st.pins};
@@ -731,7 +759,16 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
         NodeWin<MAXS> cn, on, dn;                          // lane 0's walk
         uint32_t cl = XNONE, oi = XNONE, di = XNONE;
         if (lane == 0) { nw_load(cn, st, cluster_rows(st, l)); cl = l; }
+        for (uint32_t k = lane; k < XW_OC; k += 64) oc.key[k] = 0;
+        if (lane == 0) oc.n = 0;
+        __syncthreads();
+#ifdef SF_XW_PROFILE
+        unsigned long long pf_setup = 0, pf_solve = 0, pf_post = 0, pf_n = 0, pf_t = 0;
+#endif
         for (uint32_t j0 = lo; j0 < hi;) {
+#ifdef SF_XW_PROFILE
+            pf_t = wall_clock64(); pf_n++;
+#endif
             const int64_t t0 = io.ts[j0];
             const int64_t bs = t0 - t0 % st.wl, bm = t0 - t0 % 1000;
             const uint32_t j = j0 + lane;
@@ -745,13 +782,6 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                 rows[k].minrt = INT64_MAX;
                 rows[k].nblk = rows[k].ncmp = rows[k].nexc = rows[k].npass = 0; rows[k].key = 0;
             }
-            if (lane == 0) {
-                if (cl != l) { if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl)); nw_load(cn, st, cluster_rows(st, l)); cl = l; }
-                cn.min_flush();                              // (a copy that moves to another minute slot reads HBM)
-                snap = cn;
-                if (oi != XNONE) { nw_store(on, st, aux_rows(st, oi)); oi = XNONE; }
-            }
-            __syncthreads();
             // 1. classify
             uint8_t myc = 0, mst = 0;
             int mrule = 0;
@@ -777,10 +807,24 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                         jac = false;
                 }
             }
+            if constexpr (MAXS == 2) {
+                if (!jac && oc.n) xw_cache_flush(st, oc, ocnw, lane);   // (the serial walk reads HBM)
+            }
+            if (lane == 0) {
+                if (cl != l) { if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl)); nw_load(cn, st, cluster_rows(st, l)); cl = l; }
+                cn.min_flush();                              // (a copy that moves to another minute slot reads HBM)
+                snap = cn;
+                if (oi != XNONE) { nw_store(on, st, aux_rows(st, oi)); oi = XNONE; }
+            }
+            __syncthreads();
+            int my_row = -1;
+#ifdef SF_XW_PROFILE
+            { const unsigned long long x = wall_clock64(); pf_setup += x - pf_t; pf_t = x; }
+#endif
             if (jac) {
                 if constexpr (MAXS == 2)
-                    xw_solve_chunk(st, io, snap, rows, xs, lane, L, lo, j0, j, t0, t, fl, c, origin, gres, l, r0, r1,
-                                   &myc, &mst, &mrule, &mwait);
+                    xw_solve_chunk(st, io, snap, rows, xs, oc, ocnw, lane, L, lo, j0, j, t0, t, fl, c, origin, gres, l,
+                                   r0, r1, &myc, &mst, &mrule, &mwait, &my_row);
             } else {
                 if (lane < L) {
                     if (fl & SF_EV_EXIT) myc = thr_sens ? XWC_SERIAL : XWC_EXIT;
@@ -821,13 +865,21 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                     }
                 }
             }
+#ifdef SF_XW_PROFILE
+            { const unsigned long long x = wall_clock64(); pf_solve += x - pf_t; pf_t = x; }
+#endif
             if (lane < L) cls[lane] = myc;
             if (myc == XWC_BLOCK || myc == XWC_PASS) io.v_status[j] = mst;   // (before the walk: its exits read it)
             __syncthreads();
             // 2. the serial walk over the undecided events
             if (lane == 0) {
+                unsigned long long nser = 0;
                 for (uint32_t k = 0; k < L; k++)
-                    if (cls[k] == XWC_SERIAL) xg_event<MAXS>(st, io, pt, lo, j0 + k, cn, on, dn, cl, oi, di);
+                    if (cls[k] == XWC_SERIAL) { xg_event<MAXS>(st, io, pt, lo, j0 + k, cn, on, dn, cl, oi, di); nser++; }
+                if (st.xw_stats) {
+                    atomicAdd(&st.xw_stats[jac ? 0 : 1], 1ull);
+                    if (nser) atomicAdd(&st.xw_stats[3], nser);
+                }
                 if (oi != XNONE) { nw_store(on, st, aux_rows(st, oi)); oi = XNONE; }
             }
             __syncthreads();
@@ -867,7 +919,9 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             }
             if (nblk || ncmp || npss) {
                 xw_add(rows[0], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp, pss, npss);   // row 0: the ClusterNode
-                if (origin != SF_ORIGIN_NONE) {
+                if (jac) {
+                    if (my_row > 0) xw_add(rows[my_row], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp, pss, npss);
+                } else if (origin != SF_ORIGIN_NONE) {
                     uint32_t h = 1 + (uint32_t)(mix64(origin) % (XW_KCAP - 1));
                     for (;;) {
                         const unsigned int prev = atomicCAS(&rows[h].key, 0u, origin + 1u);
@@ -879,7 +933,14 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             }
             __syncthreads();
             if (lane == 0) xw_apply<MAXS>(cn, rows[0], t0);
-            for (uint32_t k = 1 + lane; k < XW_KCAP; k += 64) {
+            if constexpr (MAXS == 2) {
+                if (jac) {                                       // into the cached origin nodes
+                    for (uint32_t k = 1 + lane; k < XW_KCAP; k += 64)
+                        if ((rows[k].nblk | rows[k].ncmp | rows[k].npass | rows[k].nexc) && oc.ko[k - 1] != XNONE)
+                            xw_apply<2>(xw_node(ocnw, k - 1), rows[k], t0);
+                }
+            }
+            for (uint32_t k = 1 + lane; k < XW_KCAP && !jac; k += 64) {
                 if (!rows[k].key) continue;
                 const uint32_t ko = aux_get(st, l, AX_ORIGIN, rows[k].key - 1u);
                 if (ko == XNONE) continue;
@@ -890,8 +951,17 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                 nw_store(x, st, nr);
             }
             __syncthreads();
+#ifdef SF_XW_PROFILE
+            pf_post += wall_clock64() - pf_t;
+#endif
             j0 += L;
         }
+#ifdef SF_XW_PROFILE
+        if (lane == 0 && hi - lo > 20000)
+            printf("xw seg n=%u chunks=%llu setup=%llu solve=%llu post=%llu (x10ns)\n", hi - lo, pf_n, pf_setup, pf_solve,
+                   pf_post);
+#endif
+        if constexpr (MAXS == 2) xw_cache_flush(st, oc, ocnw, lane);
         if (lane == 0 && cl != XNONE) nw_store(cn, st, cluster_rows(st, cl));
         __syncthreads();
     }
