@@ -908,7 +908,16 @@ def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
             if k == 0:
                 e.sync()                                   # batch 0 kept for parity
         e.sync()
-        ms = (time.perf_counter() - t) / timed * 1e3
+        total = time.perf_counter() - t
+        ms = total / timed * 1e3
+        # one batch alone (its latency: H2D, decision, D2H in sequence); the
+        # steady-state period of the pipeline is the rest over timed - 1 batches
+        pb.ts_base = base_ts + steps * DURATION_MS
+        t1 = time.perf_counter()
+        e.submit_packed_async(pb, outs[2])
+        e.sync()
+        lat = time.perf_counter() - t1
+        period = (total - lat) / max(1, timed - 1) * 1e3
         ent = int(((hb.flags & abi.EV_EXIT) == 0).sum())
         bad0 = {"status": int((outs[0].status != g0[0]).sum()), "wait_ms": int((outs[0].wait_ms != g0[1]).sum()),
                 "rule_idx": int((outs[0].rule_idx != g0[2]).sum())}
@@ -916,6 +925,9 @@ def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
         return {"what": "config3 batches from pinned host buffers in the compact form (sf_submit_packed_async: "
                         "H2D of batch k+1, decide of k and D2H of k-1 overlapped)",
                 "events": int(hb.n), "ms_per_batch": round(ms, 3), "decisions_per_s": round(ent / (ms / 1e3), 1),
+                "latency_ms": round(lat * 1e3, 3), "period_ms": round(period, 3),
+                "period_note": "ms_per_batch includes the drain of the last batch; period_ms = (timed wall - one "
+                               "batch's latency) / (timed - 1), the steady-state interval of the pipeline",
                 "timed_batches": timed, "h2d_bytes": int(pb.nbytes()), "d2h_bytes": int(hb.n * (1 + 4 + 2)),
                 "parity": {"what": "batch 0 and the last batch vs the headline run's verdicts", "batch0": bad0,
                            "last": badl, "exact": all(v == 0 for v in bad0.values()) and

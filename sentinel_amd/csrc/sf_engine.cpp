@@ -127,7 +127,8 @@ struct sf_engine {
     struct PkStage {
         char* buf = nullptr; size_t bytes = 0;
         hipEvent_t h2d = nullptr, d2h = nullptr;
-        bool d2h_pending = false;
+        hipEvent_t consumed = nullptr;     // the packed inputs expanded (the next H2D into them may start)
+        bool d2h_pending = false, consumed_pending = false;
     } pk[2];
     hipStream_t h2d = nullptr, d2h = nullptr;
 };
@@ -214,6 +215,7 @@ void sf_destroy(sf_engine* e) {
         if (p.buf) hipFree(p.buf);
         if (p.h2d) hipEventDestroy(p.h2d);
         if (p.d2h) hipEventDestroy(p.d2h);
+        if (p.consumed) hipEventDestroy(p.consumed);
     }
     if (e->h2d) { hipStreamSynchronize(e->h2d); hipStreamDestroy(e->h2d); }
     if (e->d2h) { hipStreamSynchronize(e->d2h); hipStreamDestroy(e->d2h); }
@@ -1121,6 +1123,7 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
         for (auto& p : e->pk) {
             HIP_TRY(hipEventCreateWithFlags(&p.h2d, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&p.d2h, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&p.consumed, hipEventDisableTiming));
         }
     }
     // (submit_core decides asynchronously only without SystemRules; the slot it takes is e->cur)
@@ -1128,8 +1131,13 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     if (!core_async) { const int rc = drain(e); if (rc) return rc; }
     const int slot = e->cur;
     auto& pk = e->pk[slot];
-    if (e->used[slot]) HIP_TRY(hipEventSynchronize(e->ev_done[slot]));   // its batch arrays are read until then
-    if (pk.d2h_pending) { HIP_TRY(hipEventSynchronize(pk.d2h)); pk.d2h_pending = false; }
+    // The slot's staging buffer: its packed inputs are free once the batch
+    // before in this slot has expanded them (early in its sort phase), its
+    // expanded arrays once that batch is decided (submit_core waits for it
+    // before the expansion), its staged verdicts once their D2H copy is done.
+    // All are waited for on the device, so the H2D of batch k+1 follows the
+    // H2D of batch k back to back and overlaps the decision of k and the D2H
+    // of k-1; the host blocks only to reallocate.
     const size_t N = e->cfg.max_batch;
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += align_up(bytes); return o; };
@@ -1138,6 +1146,9 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     const size_t o_ct = take(N * 8), o_tc = take((N / 4096 + 2) * 8);
     const size_t o_st = take(N), o_wt = take(N * 4), o_ru = take(N * 2);
     if (pk.bytes < off) {
+        if (e->used[slot]) HIP_TRY(hipEventSynchronize(e->ev_done[slot]));
+        if (pk.consumed_pending) { HIP_TRY(hipEventSynchronize(pk.consumed)); pk.consumed_pending = false; }
+        if (pk.d2h_pending) { HIP_TRY(hipEventSynchronize(pk.d2h)); pk.d2h_pending = false; }
         if (pk.buf) hipFree(pk.buf);
         pk.buf = nullptr; pk.bytes = 0;
         HIP_TRY(hipMalloc((void**)&pk.buf, off));
@@ -1149,6 +1160,7 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     const int32_t* ce = in->count_ext; const uint32_t* og = in->origin;
     if (host_in) {
         hipStream_t h = e->serial ? e->stream : e->h2d;
+        if (pk.consumed_pending) HIP_TRY(hipStreamWaitEvent(h, pk.consumed, 0));
         HIP_TRY(hipMemcpyAsync(B + o_ev, in->ev, (size_t)n * 8, hipMemcpyHostToDevice, h));
         ev = (const uint64_t*)(B + o_ev);
         if (in->n_exit) {
@@ -1173,11 +1185,16 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     const bool exits = in->n_exit != 0;
     const int64_t base = in->ts_base;
     const uint32_t n_exit = in->n_exit, n_cext = in->n_count_ext;
+    const hipEvent_t consumed = pk.consumed;
     const PreSort expand = [=](hipStream_t st_, int32_t* err) {
-        return launch_pk_expand(ev, xr, xc, ce, base, n, n_exit, n_cext, (uint2*)(B + o_tc), (uint32_t*)(B + o_res),
-                                (int64_t*)(B + o_ts), (int32_t*)(B + o_cnt), (uint8_t*)(B + o_fl),
-                                (int64_t*)(B + o_er), exits ? (int64_t*)(B + o_ct) : nullptr, err, st_);
+        const hipError_t le = launch_pk_expand(ev, xr, xc, ce, base, n, n_exit, n_cext, (uint2*)(B + o_tc),
+                                               (uint32_t*)(B + o_res), (int64_t*)(B + o_ts), (int32_t*)(B + o_cnt),
+                                               (uint8_t*)(B + o_fl), (int64_t*)(B + o_er),
+                                               exits ? (int64_t*)(B + o_ct) : nullptr, err, st_);
+        if (le != hipSuccess) return le;
+        return hipEventRecord(consumed, st_);
     };
+    if (pk.d2h_pending) { HIP_TRY(hipStreamWaitEvent(ss, pk.d2h, 0)); pk.d2h_pending = false; }
     sf_event_batch eb{};
     eb.n = n; eb.mem = SF_MEM_DEVICE;
     eb.res_id = (const uint32_t*)(B + o_res); eb.ts_ms = (const int64_t*)(B + o_ts);
@@ -1192,6 +1209,7 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     dv.rule_idx = out->rule_idx ? (host_out ? (uint16_t*)(B + o_ru) : out->rule_idx) : nullptr;
     const int rc = submit_core(e, &eb, &dv, core_async, nullptr, &expand);
     if (rc) return rc;
+    pk.consumed_pending = true;
     if (host_out) {
         hipStream_t d = e->serial ? e->stream : e->d2h;
         HIP_TRY(hipStreamWaitEvent(d, e->ev_done[slot], 0));
