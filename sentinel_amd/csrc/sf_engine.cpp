@@ -342,8 +342,12 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
         HIP_TRY(hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, a_first ? greatest : least));
         HIP_TRY(hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithPriority(&e->stream3, hipStreamNonBlocking, a_first ? least : greatest));
+        // the sort stream (batch k+1's sort phase runs beside batch k's decide phase)
+        const char* ps = getenv("SF_SORT_PRIO");
+        if (ps && ps[0] == '1') HIP_TRY(hipStreamCreateWithPriority(&e->sstream, hipStreamNonBlocking, greatest));
+        else if (ps && ps[0] == '0') HIP_TRY(hipStreamCreateWithPriority(&e->sstream, hipStreamNonBlocking, least));
+        else HIP_TRY(hipStreamCreateWithFlags(&e->sstream, hipStreamNonBlocking));
     }
-    HIP_TRY(hipStreamCreateWithFlags(&e->sstream, hipStreamNonBlocking));
     if (const char* v = getenv("SF_SERIAL_STREAMS")) e->serial = v[0] == '1';
     for (auto& a : e->evs) for (auto& x : a) HIP_TRY(hipEventCreate(&x));
     for (int k = 0; k < 2; k++) {
