@@ -306,7 +306,10 @@ def main():
         eng.close()
         c3_ms = wall / args.steps * 1e3
         for nm, fn in (("e2e_pinned", lambda: e2e_leg(hb, rules, R_local, steps, g0, glast)),
-                       ("config3_origin", lambda: config3_origin_leg(hb, rules, R_local, c3_ms, parity=not args.no_cpu,
+                       # (4 batches: the oracle replays every batch of both variants,
+                       # profiles/r04_config3_origin_parity.json holds a 7-batch run)
+                       ("config3_origin", lambda: config3_origin_leg(hb, rules, R_local, c3_ms, steps=3, warmup=1,
+                                                                       parity=not args.no_cpu,
                                                                        variants=args.origin_variants.split(","))),
                        ("config2", config2_leg), ("config4", config4_leg), ("config5", config5_leg)):
             if args.legs and nm not in args.legs.split(","):
