@@ -52,6 +52,7 @@ struct sf_engine {
     unsigned pending = 0;           // Work sets with an asynchronous batch not yet checked by sf_sync
     bool used[2] = {false, false};
     hipEvent_t ev_sorted[2]{}, ev_done[2]{};
+    hipEvent_t ev_core[2]{};                         // the verdicts of the slot's batch are written
     SysRule sys{};                  // SystemRuleManager statics; sys.check: batches go through the planner
     SysPlanDev* sys_plan = nullptr; SysExitQ* sys_pa = nullptr; SysEntQ* sys_pb = nullptr;
     uint8_t* sys_mask = nullptr;    // [max_batch] planner verdicts (sf_system.h)
@@ -226,6 +227,7 @@ void sf_destroy(sf_engine* e) {
     for (int k = 0; k < 2; k++) {
         if (e->ev_sorted[k]) hipEventDestroy(e->ev_sorted[k]);
         if (e->ev_done[k]) hipEventDestroy(e->ev_done[k]);
+        if (e->ev_core[k]) hipEventDestroy(e->ev_core[k]);
     }
     if (e->stream) hipStreamDestroy(e->stream);
     if (e->stream2) hipStreamDestroy(e->stream2);
@@ -353,6 +355,7 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     for (int k = 0; k < 2; k++) {
         HIP_TRY(hipEventCreateWithFlags(&e->ev_sorted[k], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&e->ev_done[k], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_core[k], hipEventDisableTiming));
     }
 
     DevState& st = e->st;
@@ -557,7 +560,7 @@ static int ox_maps(sf_engine* e, Work& w, bool reset, hipStream_t ss) {
 // the new slots -- all before the decide phase, so nothing is ever dropped.
 // The host waits for the sort stream here (the previous batch's decide phase
 // keeps running).  Fills `plan` for the origin-node pass of the decide phase.
-static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t ss, OxPlan* plan) {
+static int ox_prologue(sf_engine* e, Work& w, const DevBatch& b, hipStream_t ss) {
     { const int rc = ensure_aux(e); if (rc) return rc; }
     { const int rc = ox_maps(e, w, false, ss); if (rc) return rc; }
     if (b.origin && !w.ox_pairs) {                 // (at most one pair per event)
@@ -565,30 +568,22 @@ static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t
         HIP_TRY(hipMalloc((void**)&w.ox_plist, (size_t)e->cfg.max_batch * sizeof(uint32_t)));
         w.ox_pairs_cap = e->cfg.max_batch;
     }
+    return SF_OK;
+}
+static int ox_launch_index(sf_engine* e, Work& w, const DevBatch& b, hipStream_t ss) {
     DevState stl = e->st;
     stl.err = w.err;
-    uint32_t cnt[8] = {0};
-    uint32_t ax = 0;
-    for (int round = 0;; round++) {
-        const uint64_t xcap = e->st.xcap_mask + 1;
-        stl.xtab = e->st.xtab; stl.xcap_mask = e->st.xcap_mask;
-        const uint32_t lim = (uint32_t)std::min<uint64_t>(xcap * 7 / 10, 0xffffff00u);
-        DevBatch bi = b;
-        if (!w.s_origin || !b.origin) bi.origin = nullptr;
-        hipError_t le = launch_ox_index(stl, w, bi, lim, ss);
-        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("origin index: ") + hipGetErrorString(le));
-        HIP_TRY(hipMemcpyAsync(cnt, w.ox_cnt, sizeof cnt, hipMemcpyDeviceToHost, ss));
-        HIP_TRY(hipMemcpyAsync(&ax, e->st.ax_count, 4, hipMemcpyDeviceToHost, ss));
-        HIP_TRY(hipStreamSynchronize(ss));
-        if (!cnt[OXC_OVERFLOW]) break;
-        if (round > 12) return fail(SF_ERR_CAPACITY, "origin / context node index cannot grow");
-        // no room for the keys: everything drains, the table grows to the keys
-        // reserved (every absent key counted, by each workgroup that missed it),
-        // the pass runs again
-        HIP_TRY(hipDeviceSynchronize());
-        { const int rc = index_grow(e, std::max<uint64_t>((uint64_t)cnt[OXC_RESERVED], ax) * 3 / 2); if (rc) return rc; }
-        { const int rc = ox_maps(e, w, true, ss); if (rc) return rc; }
-    }
+    const uint64_t xcap = e->st.xcap_mask + 1;
+    const uint32_t lim = (uint32_t)std::min<uint64_t>(xcap * 7 / 10, 0xffffff00u);
+    DevBatch bi = b;
+    if (!w.s_origin || !b.origin) bi.origin = nullptr;
+    const hipError_t le = launch_ox_index(stl, w, bi, lim, ss);
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("origin index: ") + hipGetErrorString(le));
+    return SF_OK;
+}
+// after the index passes (counts read): the pool covers every slot, the index
+// stays at most half full, the plan of the origin-node pass
+static int ox_plan(sf_engine* e, Work& w, const uint32_t* cnt, uint32_t ax, const int64_t* t01, OxPlan* plan) {
     { const int rc = pool_grow(e, ax); if (rc) return rc; }
     // keep the index at most half full for the next batches
     if ((uint64_t)ax * 2 > e->st.xcap_mask + 1) {
@@ -613,10 +608,6 @@ static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t
     }
     plan->n_heavy = cnt[OXC_HEAVY];
     plan->n_pairs = cnt[OXC_PAIRS];
-    int64_t t01[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(&t01[0], b.ts, 8, hipMemcpyDeviceToHost, ss));
-    HIP_TRY(hipMemcpyAsync(&t01[1], b.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, ss));
-    HIP_TRY(hipStreamSynchronize(ss));
     const int64_t wl = e->st.wl;
     plan->win.w0s = t01[0] / wl; plan->win.w0m = t01[0] / 1000;
     plan->win.ws = (uint32_t)(t01[1] / wl - plan->win.w0s + 1);
@@ -631,6 +622,31 @@ static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t
     }
     return SF_OK;
 }
+static int prepare_origins(sf_engine* e, Work& w, const DevBatch& b, hipStream_t ss, OxPlan* plan) {
+    { const int rc = ox_prologue(e, w, b, ss); if (rc) return rc; }
+    uint32_t cnt[8] = {0};
+    uint32_t ax = 0;
+    for (int round = 0;; round++) {
+        { const int rc = ox_launch_index(e, w, b, ss); if (rc) return rc; }
+        HIP_TRY(hipMemcpyAsync(cnt, w.ox_cnt, sizeof cnt, hipMemcpyDeviceToHost, ss));
+        HIP_TRY(hipMemcpyAsync(&ax, e->st.ax_count, 4, hipMemcpyDeviceToHost, ss));
+        HIP_TRY(hipStreamSynchronize(ss));
+        if (!cnt[OXC_OVERFLOW]) break;
+        if (round > 12) return fail(SF_ERR_CAPACITY, "origin / context node index cannot grow");
+        // no room for the keys: everything drains, the table grows to the keys
+        // reserved (every absent key counted, by each workgroup that missed it),
+        // the pass runs again
+        HIP_TRY(hipDeviceSynchronize());
+        { const int rc = index_grow(e, std::max<uint64_t>((uint64_t)cnt[OXC_RESERVED], ax) * 3 / 2); if (rc) return rc; }
+        { const int rc = ox_maps(e, w, true, ss); if (rc) return rc; }
+    }
+    int64_t t01[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&t01[0], b.ts, 8, hipMemcpyDeviceToHost, ss));
+    HIP_TRY(hipMemcpyAsync(&t01[1], b.ts + (b.n - 1), 8, hipMemcpyDeviceToHost, ss));
+    HIP_TRY(hipStreamSynchronize(ss));
+    return ox_plan(e, w, cnt, ax, t01, plan);
+}
+
 
 int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
     if (!e || (n && !rules)) return fail(SF_ERR_INVALID, "null argument");
@@ -1019,6 +1035,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
             p = q;
             rounds++;
         }
+        HIP_TRY(hipEventRecord(e->ev_core[slot], s));
         HIP_TRY(hipEventRecord(e->ev_done[slot], s));
         e->used[slot] = true;
         e->last = slot;
@@ -1067,6 +1084,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         le = launch_entry_node(stl, b, dv.status, e->en, e->en_acc, s);
         if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
     }
+    HIP_TRY(hipEventRecord(e->ev_core[slot], s));
     HIP_TRY(hipEventRecord(e->ev_done[slot], s));
     e->used[slot] = true;
     e->timed[slot] = e->timing;
@@ -1216,7 +1234,7 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     pk.consumed_pending = true;
     if (host_out) {
         hipStream_t d = e->serial ? e->stream : e->d2h;
-        HIP_TRY(hipStreamWaitEvent(d, e->ev_done[slot], 0));
+        HIP_TRY(hipStreamWaitEvent(d, e->ev_core[slot], 0));
         HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, d));
         if (out->wait_ms) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait_ms, (size_t)n * 4, hipMemcpyDeviceToHost, d));
         if (out->rule_idx) HIP_TRY(hipMemcpyAsync(out->rule_idx, dv.rule_idx, (size_t)n * 2, hipMemcpyDeviceToHost, d));
