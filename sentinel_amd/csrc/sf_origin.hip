@@ -311,44 +311,101 @@ __global__ void __launch_bounds__(OX_T) k_ox_ilight(DevBatch b, OxIdx ox) {
 // only ever waits for a claimer that is not waiting itself.  Writes the pool
 // slot over the record's resource (XNONE when unresolved: overflow, the host
 // grows the table and the sort-phase passes run again).
+// one pair's lookup / insert from its home slot (the general path)
+__device__ uint32_t ox_lf_slow(const ParamTable& t, const DevState& st, uint32_t* cnt, uint32_t lim, uint64_t khi,
+                               uint64_t klo) {
+    const uint64_t reach = t.mask < PT_MAX_PROBE ? t.mask : PT_MAX_PROBE;
+    uint64_t i = ParamTable::hash(khi, klo) & t.mask;
+    uint32_t a = XNONE;
+    bool reserved = false, done = false;
+    for (uint64_t probe = 0; !done;) {
+        ParamSlot& s = t.slots[i];
+        const uint64_t h = __hip_atomic_load(&s.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (h == 0) {
+            if (!reserved) {
+                if (atomicAdd(&cnt[OXC_RESERVED], 1u) >= lim) { atomicOr(&cnt[OXC_OVERFLOW], 1u); done = true; continue; }
+                reserved = true;
+            }
+            unsigned long long expected = 0;
+            if (__hip_atomic_compare_exchange_strong((unsigned long long*)&s.hi, &expected,
+                                                     (unsigned long long)(khi | AX_CLAIM), __ATOMIC_ACQUIRE,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                a = atomicAdd(st.ax_count, 1u);
+                s.lo = klo; s.a = a; s.b = 0;
+                __hip_atomic_store(&s.hi, khi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                done = true;
+            }
+            continue;                                   // lost the race: this slot again
+        }
+        if (h == (khi | AX_CLAIM)) continue;            // same resource, another origin being published
+        if (h == khi) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // (the publisher's lo / a before its release of hi)
+            if (s.lo == klo) { a = (uint32_t)s.a; done = true; continue; }
+        }
+        i = (i + 1) & t.mask;
+        if (++probe > reach) { atomicOr(&cnt[OXC_OVERFLOW], 1u); done = true; }
+    }
+    return a;
+}
+
+// Each thread takes LF_B pairs at a time and probes them together (their
+// loads in flight at once); a pair found within LF_STEPS slots of its home
+// costs one acquire fence shared by the thread's pairs, the rest (absent
+// keys, claims in progress, long chains) take ox_lf_slow.
+constexpr int LF_B = 4, LF_STEPS = 6;
 __global__ void __launch_bounds__(256) k_ox_lfind(DevState st, uint4* pairs, uint32_t* cnt, uint32_t lim) {
     ParamTable t{st.xtab, st.xcap_mask, st.err};
-    const uint64_t reach = t.mask < PT_MAX_PROBE ? t.mask : PT_MAX_PROBE;
     const uint32_t np = min(cnt[OXC_PAIRS], 0xffffffffu);
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x) {
-        const uint4 pr = pairs[q];
-        const uint64_t khi = pkey_hi(pr.x, PK_AUX, AX_ORIGIN, 0), klo = pr.w;
-        uint64_t i = ParamTable::hash(khi, klo) & t.mask;
-        uint32_t a = XNONE;
-        bool reserved = false, done = false;
-        for (uint64_t probe = 0; !done;) {
-            ParamSlot& s = t.slots[i];
-            const uint64_t h = __hip_atomic_load(&s.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (h == 0) {
-                if (!reserved) {
-                    if (atomicAdd(&cnt[OXC_RESERVED], 1u) >= lim) { atomicOr(&cnt[OXC_OVERFLOW], 1u); done = true; continue; }
-                    reserved = true;
-                }
-                unsigned long long expected = 0;
-                if (__hip_atomic_compare_exchange_strong((unsigned long long*)&s.hi, &expected,
-                                                         (unsigned long long)(khi | AX_CLAIM), __ATOMIC_ACQUIRE,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                    a = atomicAdd(st.ax_count, 1u);
-                    s.lo = klo; s.a = a; s.b = 0;
-                    __hip_atomic_store(&s.hi, khi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    done = true;
-                }
-                continue;                                   // lost the race: this slot again
-            }
-            if (h == (khi | AX_CLAIM)) continue;            // same resource, another origin being published
-            if (h == khi) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // (the publisher's lo / a before its release of hi)
-                if (s.lo == klo) { a = (uint32_t)s.a; done = true; continue; }
-            }
-            i = (i + 1) & t.mask;
-            if (++probe > reach) { atomicOr(&cnt[OXC_OVERFLOW], 1u); done = true; }
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t q0 = blockIdx.x * blockDim.x + threadIdx.x; q0 < np; q0 += stride * LF_B) {
+        uint64_t khi[LF_B], klo[LF_B], pos[LF_B];
+        uint32_t a[LF_B];
+        int state[LF_B];                                // 0 probing, 1 candidate at pos, 2 slow path, 3 unused
+#pragma unroll
+        for (int k = 0; k < LF_B; k++) {
+            const uint32_t q = q0 + (uint32_t)k * stride;
+            a[k] = XNONE;
+            if (q >= np) { state[k] = 3; khi[k] = klo[k] = pos[k] = 0; continue; }
+            const uint4 pr = pairs[q];
+            khi[k] = pkey_hi(pr.x, PK_AUX, AX_ORIGIN, 0); klo[k] = pr.w;
+            pos[k] = ParamTable::hash(khi[k], klo[k]) & t.mask;
+            state[k] = 0;
         }
-        pairs[q].x = a;
+        for (int step = 0; step < LF_STEPS; step++) {
+            uint64_t h[LF_B];
+#pragma unroll
+            for (int k = 0; k < LF_B; k++)
+                h[k] = state[k] == 0 ? __hip_atomic_load(&t.slots[pos[k]].hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0ull;
+            bool more = false;
+#pragma unroll
+            for (int k = 0; k < LF_B; k++) {
+                if (state[k] != 0) continue;
+                if (h[k] == khi[k]) state[k] = 1;
+                else if (h[k] == 0 || (h[k] & AX_CLAIM)) state[k] = 2;
+                else { pos[k] = (pos[k] + 1) & t.mask; more = true; }
+            }
+            if (!more) break;
+        }
+        bool cand = false;
+#pragma unroll
+        for (int k = 0; k < LF_B; k++) {
+            if (state[k] == 0) state[k] = 2;            // (a long chain)
+            cand |= state[k] == 1;
+        }
+        if (cand) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (the publishers' lo / a before hi)
+#pragma unroll
+        for (int k = 0; k < LF_B; k++) {
+            if (state[k] != 1) continue;
+            const ParamSlot& s = t.slots[pos[k]];
+            if (s.lo == klo[k]) a[k] = (uint32_t)s.a;
+            else state[k] = 2;                          // same resource, another origin: on from its home
+        }
+#pragma unroll
+        for (int k = 0; k < LF_B; k++) {
+            if (state[k] == 2) a[k] = ox_lf_slow(t, st, cnt, lim, khi[k], klo[k]);
+            if (state[k] != 3) pairs[q0 + (uint32_t)k * stride].x = a[k];
+        }
     }
 }
 
@@ -373,17 +430,33 @@ __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxId
         ox.bseg[j0 / OX_TILE] = make_uint2(ox.head_scan[j0] - 1u, ox.head_scan[je - 1] - 1u);
     }
     bool any = false;
-    uint32_t kp[OX_ITILE / OX_T];                         // LDS key position of each of this thread's long-segment events
+    constexpr uint32_t PER = OX_ITILE / OX_T;
+    uint32_t kp[PER];                                     // LDS key position of each of this thread's long-segment events
+    // the loads of all PER events first (in flight together), then the inserts
+    uint32_t sidv[PER], lov[PER], hiv[PER], ov[PER], resv[PER];
+    uint8_t modev[PER];
 #pragma unroll
-    for (uint32_t k = 0; k < OX_ITILE / OX_T; k++) {
+    for (uint32_t k = 0; k < PER; k++) {
+        const uint32_t j = j0 + k * OX_T + tid;
+        sidv[k] = j < j1 ? ox.head_scan[j] - 1u : XNONE;
+        ov[k] = (j < j1 && ox.s_origin) ? ox.s_origin[j] : SF_ORIGIN_NONE;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        const uint32_t sid = sidv[k];
+        if (sid == XNONE) { lov[k] = hiv[k] = resv[k] = 0; modev[k] = 0; continue; }
+        lov[k] = ox.seg_start[sid]; hiv[k] = ox.seg_start[sid + 1];
+        modev[k] = ox.seg_mode[sid]; resv[k] = ox.seg_res[sid];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
         const uint32_t j = j0 + k * OX_T + tid;
         kp[k] = XNONE;
         if (j >= j1) continue;
-        const uint32_t sid = ox.head_scan[j] - 1u;
-        const uint32_t lo = ox.seg_start[sid], hi = ox.seg_start[sid + 1];
-        const bool xf = ox.seg_mode[sid] == SM_XFLOW;
+        const uint32_t lo = lov[k], hi = hiv[k];
+        const bool xf = modev[k] == SM_XFLOW;
         if (!xf && hi - lo <= OX_LIGHT) continue;          // (k_ox_ilight)
-        const uint32_t o = ox.s_origin ? ox.s_origin[j] : SF_ORIGIN_NONE;
+        const uint32_t o = ov[k];
         bool fresh;
         if (xf) {
             ox.s_oslot[j] = XNONE;
@@ -396,7 +469,7 @@ __global__ void __launch_bounds__(OX_T) k_ox_index(DevState st, DevBatch b, OxId
                 if (st.rules[r].strategy == SF_STRATEGY_CHAIN && st.rules[r].ref == ctx) want = true;
             if (want) { ox_lds_insert<OX_IKCAP>(kk, ox_pack(l, AX_CTX, ctx), &fresh); any = true; }
         } else if (o != SF_ORIGIN_NONE) {
-            const uint32_t p = ox_lds_insert<OX_IKCAP>(kk, ox_pack(ox.seg_res[sid], AX_ORIGIN, o), &fresh);
+            const uint32_t p = ox_lds_insert<OX_IKCAP>(kk, ox_pack(resv[k], AX_ORIGIN, o), &fresh);
             if (fresh) kheavy[p] = 1;
             kp[k] = p;
             any = true;
