@@ -323,13 +323,15 @@ hipError_t launch_fmt_write(const sf_metric_row* rows, const uint32_t* order, ui
                             const uint64_t* name_off, const int32_t* types, uint32_t n_names, int64_t tz,
                             const uint64_t* line_off, char* out, hipStream_t s);
 hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipStream_t s);   // out[0] used, out[1] max probe
+// classify = true: k_classify / k_fill_tiles end the sort phase (the origin
+// index passes read the routes); false: launch_decide runs them first
 hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,
-                       uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing);
+                       uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing, bool classify = true);
 struct OxWin { int64_t w0s, w0m; uint32_t ws, wm; };    // the batch's first second / minute window and counts
 struct OxPlan { uint32_t n_heavy, n_pairs; OxWin win; };   // the batch's origin-node pass (sf_origin.hip)
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                          hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing,
-                         const OxPlan* ox = nullptr);
+                         const OxPlan* ox = nullptr, bool classify = false);
 // sf_packed_batch -> SoA (sf_kernels.hip); tile_cnt: [n / 4096 + 1] uint2
 hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64_t* xcts, const int32_t* cext,
                             int64_t base, uint32_t n, uint32_t n_exit, uint32_t n_cext, uint2* tile_cnt,

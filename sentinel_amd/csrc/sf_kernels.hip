@@ -529,7 +529,8 @@ __device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& 
                                XwCache& oc, unsigned char* ocnw,
                                uint32_t lane, uint32_t L, uint32_t lo, uint32_t j0, uint32_t j, int64_t t0, int64_t t,
                                uint8_t fl, int32_t c, uint32_t origin, uint32_t gres, uint32_t l, uint32_t r0,
-                               uint32_t r1, uint8_t* myc, uint8_t* mst, int* mrule, int64_t* mwait, int* my_row) {
+                               uint32_t r1, uint8_t* myc, uint8_t* mst, int* mrule, int64_t* mwait, int* my_row,
+                               bool* x_live, int64_t* x_cts) {
     const bool valid = lane < L;
     const bool is_exit = valid && (fl & SF_EV_EXIT);
     const bool is_sys = valid && !is_exit && (fl & EVF_SYSBLK);
@@ -622,17 +623,23 @@ __device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& 
     // an exit's liveness: its entry passed (in this chunk: that lane's verdict)
     int eidx = -1;
     bool live_pre = false;
+    int64_t xcts = t;
     if (is_exit) {
         const int64_t ref = io.eref ? io.eref[j] : -1;
         if (ref >= 0) {
             const bool bad = ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT) ||
                              io.ev_res[io.perm[ref]] != gres;
             if (!bad) {
+                xcts = io.ts[ref];
                 if (ref >= (int64_t)j0) eidx = (int)(ref - j0);
                 else live_pre = !v_blocked(io.v_status[ref]);
+            } else {
+                *st.err = SF_ERR_INVALID;                      // (an exit of itself: blocked)
+                xcts = t;
             }
         } else {
             live_pre = ref != EREF_DEAD;
+            xcts = io.cts ? io.cts[j] : t;
         }
     }
     int d = is_solve ? 1 : 0, ri = 0;
@@ -734,6 +741,11 @@ __device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& 
     } else if (is_exit) {
         *myc = XWC_EXIT;
     }
+    {   // the exits' final liveness and create time, for the accounting
+        const int ed = __shfl(d, eidx >= 0 ? eidx : (int)lane);
+        *x_live = is_exit && (eidx >= 0 ? ed != 0 : live_pre);
+        *x_cts = xcts;
+    }
     *my_row = osr;
 }
 
@@ -818,13 +830,15 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             }
             __syncthreads();
             int my_row = -1;
+            bool x_live = false;
+            int64_t x_cts = 0;
 #ifdef SF_XW_PROFILE
             { const unsigned long long x = wall_clock64(); pf_setup += x - pf_t; pf_t = x; }
 #endif
             if (jac) {
                 if constexpr (MAXS == 2)
                     xw_solve_chunk(st, io, snap, rows, xs, oc, ocnw, lane, L, lo, j0, j, t0, t, fl, c, origin, gres, l,
-                                   r0, r1, &myc, &mst, &mrule, &mwait, &my_row);
+                                   r0, r1, &myc, &mst, &mrule, &mwait, &my_row, &x_live, &x_cts);
             } else {
                 if (lane < L) {
                     if (fl & SF_EV_EXIT) myc = thr_sens ? XWC_SERIAL : XWC_EXIT;
@@ -894,6 +908,15 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             } else if (myc == XWC_PASS) {
                 emit_verdict(io, j, mst, (int32_t)mwait, 0);
                 pss = c; npss = 1;
+            } else if (myc == XWC_EXIT && jac) {             // (liveness and create time from the solve)
+                uint8_t v = SF_V_EXIT_IGNORED;
+                if (x_live) {
+                    v = SF_V_EXIT;
+                    succ = c; rt = t - x_cts; minrt = rt; thr = -1; ncmp = 1;
+                    if (fl & SF_EV_ERROR) { exc = c; nexc = 1; }
+                }
+                io.v_status[j] = v;
+                emit_verdict(io, j, v, 0, 0);
             } else if (myc == XWC_EXIT) {                    // decide_xgroup's exit (StatisticSlot.exit :134-165)
                 int64_t ref = io.eref ? io.eref[j] : -1;
                 bool blocked; int64_t cts;
@@ -917,8 +940,26 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                 io.v_status[j] = v;
                 emit_verdict(io, j, v, 0, 0);
             }
+            // the ClusterNode's sums: wavefront reductions (every lane adds to it)
+            XwRow crow;
+            {
+                long long v[6] = {blk, succ, rt, exc, thr, pss};
+                long long mr = minrt;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+                    for (int f = 0; f < 6; f++) v[f] += __shfl_xor(v[f], o);
+                    const long long y = __shfl_xor(mr, o);
+                    mr = y < mr ? y : mr;
+                }
+                crow.blk = (unsigned long long)v[0]; crow.succ = (unsigned long long)v[1];
+                crow.rt = (unsigned long long)v[2]; crow.exc = (unsigned long long)v[3];
+                crow.thr = v[4] + (long long)__popcll(__ballot(npss != 0)); crow.pass = (unsigned long long)v[5];
+                crow.minrt = mr;
+                crow.nblk = (unsigned)__popcll(__ballot(nblk != 0)); crow.ncmp = (unsigned)__popcll(__ballot(ncmp != 0));
+                crow.nexc = (unsigned)__popcll(__ballot(nexc != 0)); crow.npass = (unsigned)__popcll(__ballot(npss != 0));
+            }
             if (nblk || ncmp || npss) {
-                xw_add(rows[0], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp, pss, npss);   // row 0: the ClusterNode
                 if (jac) {
                     if (my_row > 0) xw_add(rows[my_row], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp, pss, npss);
                 } else if (origin != SF_ORIGIN_NONE) {
@@ -932,7 +973,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                 }
             }
             __syncthreads();
-            if (lane == 0) xw_apply<MAXS>(cn, rows[0], t0);
+            if (lane == 0) xw_apply<MAXS>(cn, crow, t0);
             if constexpr (MAXS == 2) {
                 if (jac) {                                       // into the cached origin nodes
                     for (uint32_t k = 1 + lane; k < XW_KCAP; k += 64)
@@ -1720,8 +1761,26 @@ hipError_t launch_init_state(const DevState& st, hipStream_t s) {
 // sorted SoA, exit map, acquireCount prefix, classification and fill tiles.
 // Runs on its own stream into one of the engine's two Work sets, so the next
 // batch is sorted while the current one is decided.
+// segment routing (k_classify) and the heavy fill tiles: the end of the sort
+// phase when the origin index passes follow (they read the routes), else the
+// head of the decide phase (the sort phase is the longer of the two)
+static void launch_classify(const DevState& st, Work& w, const DevBatch& b, hipStream_t s, hipEvent_t* ev, bool timing) {
+    const uint32_t n = b.n;
+    hipMemsetAsync(w.counters, 0, 16 * sizeof(uint32_t), s);
+    hipMemsetAsync(w.lcounts, 0, 2 * LCLS * sizeof(uint32_t), s);
+    hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
+    if (st.n_stream_rules) hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
+    const uint32_t max_seg = n < st.R ? n : st.R;
+    if (timing) hipEventRecord(ev[10], s);
+    hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, 1024)), dim3(1024), 0, s, st, w, w.s_ts);
+    HeavyCtx hc = heavy_ctx(w);
+    StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, nullptr, w.counters + 7};
+    hipLaunchKernelGGL(k_fill_tiles, dim3(2), dim3(1024), 0, s, hc, sc, w.fill_tiles, w.fill_tile_cap, w.fill_ntiles);
+    if (timing) hipEventRecord(ev[2], s);
+}
+
 hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,
-                       uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing) {
+                       uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing, bool classify) {
     const uint32_t n = b.n;
     if (n == 0) return hipSuccess;
     const unsigned T = 256;
@@ -1757,21 +1816,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
                            w.perm, w.s_ts, w.s_cnt, w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan,
                            w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err, st.n_prule != 0,
                            (uint32_t*)nullptr);
-    if (b.eref || st.n_stream_rules) hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);   // (read by k_gather_exit, k_thr_rec)
-    if (b.eref)
-        hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, T)), dim3(T), 0, s, b, w.perm, w.s_flags,
-                           w.head_scan, w.seg_start, w.s_eref, w.s_cts, w.exit_of, st.err);
-    hipMemsetAsync(w.counters, 0, 16 * sizeof(uint32_t), s);
-    hipMemsetAsync(w.lcounts, 0, 2 * LCLS * sizeof(uint32_t), s);
-    hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
-    if (st.n_stream_rules) hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
-    const uint32_t max_seg = n < st.R ? n : st.R;
-    if (timing) hipEventRecord(ev[10], s);
-    hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, 1024)), dim3(1024), 0, s, st, w, w.s_ts);
-    HeavyCtx hc = heavy_ctx(w);
-    StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, nullptr, w.counters + 7};
-    hipLaunchKernelGGL(k_fill_tiles, dim3(2), dim3(1024), 0, s, hc, sc, w.fill_tiles, w.fill_tile_cap, w.fill_ntiles);
-    if (timing) hipEventRecord(ev[2], s);
+    if (classify) launch_classify(st, w, b, s, ev, timing);
     return hipGetLastError();
 }
 
@@ -1963,9 +2008,11 @@ static void launch_thr_prep(Work& w, const DevBatch& b, hipStream_t s) {
 // start first, on A; QPS/WarmUp heavy segments on B, the light lanes on C;
 // then the verdicts are scattered back to submission order.
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
-                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing, const OxPlan* ox) {
+                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing, const OxPlan* ox,
+                         bool classify) {
     const uint32_t n = b.n;
     if (n == 0) return hipSuccess;
+    if (classify) launch_classify(st, w, b, s, ev, timing);
     SegIO io;
     io.ts = w.s_ts; io.cnt = w.s_cnt; io.flags = w.s_flags;
     io.eref = b.eref ? w.s_eref : nullptr; io.cts = b.eref ? w.s_cts : nullptr;
@@ -1980,6 +2027,14 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     const uint32_t max_seg = n < st.R ? n : st.R;
     const uint32_t max_heavy = n / (w.heavy_min + 1) + 1;
     StreamCtx sc{w.stream_list, w.counters + 5, w.seg_cap, timing ? w.sticks : nullptr, w.counters + 7};
+    // each exit's entry (sorted position, exit_of) and create time: state-
+    // independent, but here at the head of the decide phase rather than in the
+    // sort phase, the longer of the two pipelined phases (k_classify does not
+    // read them; every deciding kernel does)
+    if (b.eref || st.n_stream_rules) hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);   // (read by k_gather_exit, k_thr_rec)
+    if (b.eref)
+        hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, 256)), dim3(256), 0, s, b, w.perm, w.s_flags,
+                           w.head_scan, w.seg_start, w.s_eref, w.s_cts, w.exit_of, st.err);
     // waits and rule indices are zero for almost every event: clear them with
     // coalesced stores, then the deciding kernels scatter only the nonzero ones
     if (out.wait) hipMemsetAsync(out.wait, 0, (size_t)n * sizeof(int32_t), s);
