@@ -1064,9 +1064,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     }
     DevState stl = e->st;
     stl.err = w.err;
-    // (k_classify ends the sort phase only when the origin index passes follow)
-    hipError_t le = launch_sort(stl, w, b, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, ss, e->evs[slot], e->timing,
-                                with_ox);
+    hipError_t le = launch_sort(stl, w, b, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, ss, e->evs[slot], e->timing);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
     OxPlan plan{};
     if (with_ox) {
@@ -1078,7 +1076,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     // decide phase in batch order on the main streams
     HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
     le = launch_decide(stl, w, b, dv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3, e->evs[slot], e->timing,
-                       with_ox ? &plan : nullptr, !with_ox);
+                       with_ox ? &plan : nullptr);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
     // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream
     // order); under the round protocol the node-wide stream updates it (sf_entry_node_add)
