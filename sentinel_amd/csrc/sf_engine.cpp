@@ -41,7 +41,7 @@ static int fail(int code, const std::string& msg) {
 
 struct sf_engine {
     sf_config cfg{};
-    hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
+    hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;   // 4: the wave walk
     hipStream_t sstream = nullptr;  // sort phase of the next batch (overlaps the decide phase on `stream`)
     bool serial = false;            // diagnostics (SF_SERIAL_STREAMS=1): every kernel on one stream
     uint32_t R = 0, key_bits = 1;
@@ -232,6 +232,7 @@ void sf_destroy(sf_engine* e) {
     if (e->stream) hipStreamDestroy(e->stream);
     if (e->stream2) hipStreamDestroy(e->stream2);
     if (e->stream3) hipStreamDestroy(e->stream3);
+    if (e->stream4) hipStreamDestroy(e->stream4);
     if (e->sstream) hipStreamDestroy(e->sstream);
     delete e;
 }
@@ -728,6 +729,10 @@ int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->st.xmap = xflow ? e->xmap_buf : nullptr;
     e->st.xw = xflow ? e->xw_buf : nullptr;
+    // the wave walk's stream, created at the first table that routes to it and
+    // after the pipeline's four (a stream created earlier changes which hardware
+    // queue each of those gets: config 3 lost 2.3 ms/step to a shared queue)
+    if (e->st.xw && !e->stream4) HIP_TRY(hipStreamCreateWithFlags(&e->stream4, hipStreamNonBlocking));
     return SF_OK;
 }
 
@@ -1029,6 +1034,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
             }
             if (le == hipSuccess)
                 le = launch_decide(stl, w, v, dvv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3,
+                                   e->serial ? s : e->stream4,
                                    e->evs[slot], false, with_ox ? &plan : nullptr);
             if (le == hipSuccess) le = launch_entry_node(stl, v, dvv.status, e->en, e->en_acc, s);
             if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
@@ -1075,7 +1081,8 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     HIP_TRY(hipEventRecord(e->ev_sorted[slot], ss));
     // decide phase in batch order on the main streams
     HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
-    le = launch_decide(stl, w, b, dv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3, e->evs[slot], e->timing,
+    le = launch_decide(stl, w, b, dv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3,
+                       e->serial ? s : e->stream4, e->evs[slot], e->timing,
                        with_ox ? &plan : nullptr);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
     // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream
@@ -2215,6 +2222,7 @@ int sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uin
     HIP_TRY(hipStreamSynchronize(e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream2));
     HIP_TRY(hipStreamSynchronize(e->stream3));
+    if (e->stream4) HIP_TRY(hipStreamSynchronize(e->stream4));
     HIP_TRY(hipMemcpy(cnt, lw.counters, sizeof cnt, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&nseg, lw.n_seg, 4, hipMemcpyDeviceToHost));
     const uint32_t n1 = cnt[1] + cnt[4], n2 = cnt[5] + cnt[6];

@@ -525,20 +525,34 @@ __device__ __forceinline__ void xw_mp_scan(long long& a, long long& b, uint32_t 
     }
 }
 
-__device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& snap, XwRow* rows, XwScratch& xs,
+__device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& snap, XwRow* rows, XwScratch& xs,
                                XwCache& oc, unsigned char* ocnw,
-                               uint32_t lane, uint32_t L, uint32_t lo, uint32_t j0, uint32_t j, int64_t t0, int64_t t,
-                               uint8_t fl, int32_t c, uint32_t origin, uint32_t gres, uint32_t l, uint32_t r0,
+                               uint32_t lane, uint32_t L, int64_t t0, int64_t t,
+                               uint8_t fl, int32_t c, uint32_t origin, int eidx, bool live_pre, uint32_t l, uint32_t r0,
                                uint32_t r1, uint8_t* myc, uint8_t* mst, int* mrule, int64_t* mwait, int* my_row,
-                               bool* x_live, int64_t* x_cts) {
+                               bool* x_live) {
     const bool valid = lane < L;
     const bool is_exit = valid && (fl & SF_EV_EXIT);
     const bool is_sys = valid && !is_exit && (fl & EVF_SYSBLK);
     const bool is_solve = valid && !is_exit && !is_sys;
     const uint32_t nrules = r1 - r0;
     // the chunk's origin rows (row 0: the ClusterNode; row r: cache slot r - 1),
-    // a node loaded into the cache at its first event of the segment
-    if (oc.n + 64 > XW_OC) xw_cache_flush(st, oc, ocnw, lane);
+    // a node loaded into the cache at its first event of the segment; the
+    // cache is written back only when this chunk's new origins do not fit
+    {
+        bool miss = false;
+        if (valid && origin != SF_ORIGIN_NONE) {
+            uint32_t h = (uint32_t)(mix64(origin) % XW_OC);
+            miss = true;
+            for (uint32_t q = 0; q < XW_OC; q++) {
+                const unsigned int k = oc.key[h];
+                if (k == origin + 1u) { miss = false; break; }
+                if (k == 0u) break;
+                h = h + 1 < XW_OC ? h + 1 : 0;
+            }
+        }
+        if (oc.n + (uint32_t)__popcll(__ballot(miss)) > XW_OC) xw_cache_flush(st, oc, ocnw, lane);
+    }
     int osr = -1;
     if (valid && origin != SF_ORIGIN_NONE) {
         uint32_t h = (uint32_t)(mix64(origin) % XW_OC);
@@ -620,28 +634,8 @@ __device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& 
             cost[kr] = j_round(1.0 * c / xs.rc[kr].qps * 1000);
         }
     }
-    // an exit's liveness: its entry passed (in this chunk: that lane's verdict)
-    int eidx = -1;
-    bool live_pre = false;
-    int64_t xcts = t;
-    if (is_exit) {
-        const int64_t ref = io.eref ? io.eref[j] : -1;
-        if (ref >= 0) {
-            const bool bad = ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT) ||
-                             io.ev_res[io.perm[ref]] != gres;
-            if (!bad) {
-                xcts = io.ts[ref];
-                if (ref >= (int64_t)j0) eidx = (int)(ref - j0);
-                else live_pre = !v_blocked(io.v_status[ref]);
-            } else {
-                *st.err = SF_ERR_INVALID;                      // (an exit of itself: blocked)
-                xcts = t;
-            }
-        } else {
-            live_pre = ref != EREF_DEAD;
-            xcts = io.cts ? io.cts[j] : t;
-        }
-    }
+    // an exit's liveness: its entry passed (in this chunk: that lane's verdict,
+    // eidx; before it: live_pre, from the walk's exit descriptor)
     int d = is_solve ? 1 : 0, ri = 0;
     uint32_t reach = 0, passk = 0;
     long long w = 0;
@@ -741,12 +735,52 @@ __device__ void xw_solve_chunk(const DevState& st, const SegIO& io, NodeWin<2>& 
     } else if (is_exit) {
         *myc = XWC_EXIT;
     }
-    {   // the exits' final liveness and create time, for the accounting
+    {   // the exits' final liveness, for the accounting
         const int ed = __shfl(d, eidx >= 0 ? eidx : (int)lane);
         *x_live = is_exit && (eidx >= 0 ? ed != 0 : live_pre);
-        *x_cts = xcts;
     }
     *my_row = osr;
+}
+
+// One chunk's event fields, loaded a chunk ahead: the walk is a chain of
+// dependent chunks, so HBM latency, not bandwidth, is its cost.  First level
+// (sorted position j): time, flags, count, submission index, entry ref;
+// second level (addresses from the first): the origin, and an exit's entry
+// flags / time and -- when the entry was decided before the chunk that issues
+// the loads (jd) -- its status; create time of an exit whose entry is older.
+// k_gather_exit leaves a ref >= 0 only inside the exit's own segment.
+struct XwEv {
+    int64_t t, ref, rts, cts;
+    int32_t c;
+    uint32_t i, origin;
+    uint8_t fl, rfl, rvs, pad;
+};
+__device__ __forceinline__ void xw_ld1(const SegIO& io, uint32_t j, uint32_t hi, XwEv& e) {
+    if (j < hi) {
+        e.t = io.ts[j]; e.fl = io.flags[j]; e.c = io.cnt[j]; e.i = io.perm[j];
+        e.ref = io.eref ? io.eref[j] : -1;
+    } else {
+        e.t = INT64_MAX; e.fl = 0; e.c = 0; e.i = 0; e.ref = -1;
+    }
+}
+__device__ __forceinline__ void xw_ld2(const SegIO& io, uint32_t j, uint32_t lo, uint32_t hi, uint32_t jd, XwEv& e) {
+    e.origin = SF_ORIGIN_NONE; e.rfl = 0; e.rvs = 0; e.rts = 0; e.cts = 0;
+    if (j >= hi) return;
+    if (io.ev_origin) e.origin = io.ev_origin[e.i];
+    if (e.fl & SF_EV_EXIT) {
+        if (e.ref >= (int64_t)lo && e.ref < (int64_t)j) {
+            e.rfl = io.flags[e.ref]; e.rts = io.ts[e.ref];
+            if (e.ref < (int64_t)jd) e.rvs = io.v_status[e.ref];
+        } else if (e.ref < 0 && io.cts) {
+            e.cts = io.cts[j];
+        }
+    }
+}
+// the o_wait / o_rule half of emit_verdict with the submission index at hand
+__device__ __forceinline__ void xw_emit(const SegIO& io, uint32_t i, int32_t wait, uint16_t rule) {
+    if (!io.perm) return;
+    if (io.o_wait && wait) io.o_wait[i] = wait;
+    if (io.o_rule && rule) io.o_rule[i] = rule;
 }
 
 template <int MAXS>
@@ -755,6 +789,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                                                   const uint32_t* n_list) {
     __shared__ __align__(16) unsigned char snap_raw[sizeof(NodeWin<MAXS>)];
     __shared__ uint8_t cls[64];
+    __shared__ uint8_t vch[64];                             // the previous chunk's final statuses
     __shared__ XwRow rows[XW_KCAP];
     __shared__ XwScratch xs;
     __shared__ XwCache oc;
@@ -768,27 +803,40 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
         const uint32_t lo = seg_start[s], hi = seg_start[s + 1], l = seg_res[s];
         const uint32_t r0 = st.rule_off[l], r1 = st.rule_off[l + 1];
         const bool thr_sens = (st.xw[l] & XWF_THREAD) != 0;
-        NodeWin<MAXS> cn, on, dn;                          // lane 0's walk
-        uint32_t cl = XNONE, oi = XNONE, di = XNONE;
+        // the ClusterNode lives in LDS (lane 0 updates it, every lane reads it):
+        // no registers held across the chunk loop for it
+        NodeWin<MAXS>& cn = snap;
+        uint32_t cl = XNONE;
         if (lane == 0) { nw_load(cn, st, cluster_rows(st, l)); cl = l; }
         for (uint32_t k = lane; k < XW_OC; k += 64) oc.key[k] = 0;
         if (lane == 0) oc.n = 0;
+        XwEv e;
+        xw_ld1(io, lo + lane, hi, e);
+        xw_ld2(io, lo + lane, lo, hi, lo, e);
+        uint32_t jprev = lo;                               // start of the previous chunk (vch)
         __syncthreads();
 #ifdef SF_XW_PROFILE
-        unsigned long long pf_setup = 0, pf_solve = 0, pf_post = 0, pf_n = 0, pf_t = 0;
+        unsigned long long pf_setup = 0, pf_solve = 0, pf_post = 0, pf_n = 0, pf_t = 0, pf_p[6] = {0, 0, 0, 0, 0, 0};
+#define XW_PF(k) { const unsigned long long x_ = wall_clock64(); pf_p[k] += x_ - pf_t; pf_t = x_; pf_post += 0; }
+#else
+#define XW_PF(k)
 #endif
         for (uint32_t j0 = lo; j0 < hi;) {
 #ifdef SF_XW_PROFILE
             pf_t = wall_clock64(); pf_n++;
 #endif
-            const int64_t t0 = io.ts[j0];
+            const int64_t t0 = __shfl(e.t, 0);
             const int64_t bs = t0 - t0 % st.wl, bm = t0 - t0 % 1000;
             const uint32_t j = j0 + lane;
             const bool valid = j < hi;
-            const int64_t t = valid ? io.ts[j] : t0;
+            const int64_t t = valid ? e.t : t0;
             const bool same = valid && t >= bs && t < bs + st.wl && t >= bm && t < bm + 1000;
             const unsigned long long nb = __ballot(!same);
             const uint32_t L = nb ? (uint32_t)(__ffsll((long long)nb) - 1) : 64u;   // (lane 0 is always in)
+            const uint32_t jn = j0 + L;
+            // the next chunk's first-level fields, in flight while this one is decided
+            XwEv nx;
+            xw_ld1(io, jn + lane, hi, nx);
             for (uint32_t k = lane; k < XW_KCAP; k += 64) {
                 rows[k].blk = rows[k].succ = rows[k].rt = rows[k].exc = rows[k].pass = 0; rows[k].thr = 0;
                 rows[k].minrt = INT64_MAX;
@@ -798,20 +846,35 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             uint8_t myc = 0, mst = 0;
             int mrule = 0;
             int64_t mwait = 0;
-            uint32_t origin = SF_ORIGIN_NONE, gres = 0;
-            int32_t c = 0;
-            uint8_t fl = 0;
-            if (lane < L) {
-                fl = io.flags[j]; c = io.cnt[j];
-                const uint32_t i = io.perm[j];
-                gres = io.ev_res[i];
-                origin = io.ev_origin ? io.ev_origin[i] : SF_ORIGIN_NONE;
+            const bool act = lane < L;
+            const uint32_t origin = act ? e.origin : SF_ORIGIN_NONE;
+            const int32_t c = act ? e.c : 0;
+            const uint8_t fl = act ? e.fl : 0;
+            // an exit's entry: in this chunk (eidx: that lane's verdict), or decided
+            // before it (live_pre), or before this batch (ref < 0)
+            int eidx = -1;
+            bool live_pre = false;
+            int64_t xcts = t;
+            if (act && (fl & SF_EV_EXIT)) {
+                const int64_t ref = e.ref;
+                if (ref >= 0) {
+                    if (ref < (int64_t)lo || ref >= (int64_t)j || (e.rfl & SF_EV_EXIT)) {
+                        *st.err = SF_ERR_INVALID;                  // (an exit of itself: blocked)
+                    } else {
+                        xcts = e.rts;
+                        if (ref >= (int64_t)j0) eidx = (int)(ref - j0);
+                        else live_pre = !v_blocked(ref >= (int64_t)jprev ? vch[ref - jprev] : e.rvs);
+                    }
+                } else {
+                    live_pre = ref != EREF_DEAD;
+                    xcts = io.cts ? e.cts : t;
+                }
             }
             // the exact chunk solve (below) unless a prioritized entry is in the chunk
             // (its occupy path) or an origin-node WarmUp rule has not synced this second
             bool jac = false;
             if constexpr (MAXS == 2) {
-                jac = __ballot(lane < L && !(fl & (SF_EV_EXIT | EVF_SYSBLK)) && (fl & SF_EV_PRIO)) == 0ull;
+                jac = __ballot(act && !(fl & (SF_EV_EXIT | EVF_SYSBLK)) && (fl & SF_EV_PRIO)) == 0ull;
                 for (uint32_t k = r0; k < r1 && jac; k++) {
                     const DevRule& r = st.rules[k];
                     if ((r.kind == CT_WARM_UP || r.kind == CT_WARM_UP_RATE_LIMITER) && r.limit_app != SF_APP_DEFAULT &&
@@ -825,27 +888,24 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             if (lane == 0) {
                 if (cl != l) { if (cl != XNONE) nw_store(cn, st, cluster_rows(st, cl)); nw_load(cn, st, cluster_rows(st, l)); cl = l; }
                 cn.min_flush();                              // (a copy that moves to another minute slot reads HBM)
-                snap = cn;
-                if (oi != XNONE) { nw_store(on, st, aux_rows(st, oi)); oi = XNONE; }
             }
             __syncthreads();
             int my_row = -1;
             bool x_live = false;
-            int64_t x_cts = 0;
 #ifdef SF_XW_PROFILE
             { const unsigned long long x = wall_clock64(); pf_setup += x - pf_t; pf_t = x; }
 #endif
             if (jac) {
                 if constexpr (MAXS == 2)
-                    xw_solve_chunk(st, io, snap, rows, xs, oc, ocnw, lane, L, lo, j0, j, t0, t, fl, c, origin, gres, l,
-                                   r0, r1, &myc, &mst, &mrule, &mwait, &my_row, &x_live, &x_cts);
+                    xw_solve_chunk(st, snap, rows, xs, oc, ocnw, lane, L, t0, t, fl, c, origin, eidx, live_pre, l,
+                                   r0, r1, &myc, &mst, &mrule, &mwait, &my_row, &x_live);
             } else {
-                if (lane < L) {
+                if (act) {
                     if (fl & SF_EV_EXIT) myc = thr_sens ? XWC_SERIAL : XWC_EXIT;
                     else if (fl & EVF_SYSBLK) { myc = XWC_BLOCK; mst = sysblk_status(fl); mrule = sysblk_rule(fl); }
                     else myc = XWC_SERIAL;
                 }
-                const unsigned long long exits = __ballot(lane < L && (fl & SF_EV_EXIT));
+                const unsigned long long exits = __ballot(act && (fl & SF_EV_EXIT));
                 const int64_t ex_before = (int64_t)__popcll(exits & ((1ull << lane) - 1ull));
                 if (myc == XWC_SERIAL && !(fl & (SF_EV_EXIT | SF_EV_PRIO))) {
                     for (uint32_t k = r0; k < r1; k++) {
@@ -882,63 +942,59 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
 #ifdef SF_XW_PROFILE
             { const unsigned long long x = wall_clock64(); pf_solve += x - pf_t; pf_t = x; }
 #endif
-            if (lane < L) cls[lane] = myc;
+            // the next chunk's second-level fields (its entries decided before this
+            // chunk are final; those in this chunk come from vch below)
+            xw_ld2(io, jn + lane, lo, hi, j0, nx);
+            if (act) cls[lane] = myc;
             if (myc == XWC_BLOCK || myc == XWC_PASS) io.v_status[j] = mst;   // (before the walk: its exits read it)
             __syncthreads();
-            // 2. the serial walk over the undecided events
-            if (lane == 0) {
-                unsigned long long nser = 0;
-                for (uint32_t k = 0; k < L; k++)
-                    if (cls[k] == XWC_SERIAL) { xg_event<MAXS>(st, io, pt, lo, j0 + k, cn, on, dn, cl, oi, di); nser++; }
-                if (st.xw_stats) {
-                    atomicAdd(&st.xw_stats[jac ? 0 : 1], 1ull);
-                    if (nser) atomicAdd(&st.xw_stats[3], nser);
+            XW_PF(0)
+            // 2. the serial walk over the undecided events (entered only when there
+            // are some: the walk's calls save and restore the live registers)
+            const unsigned long long nser = __popcll(__ballot(act && myc == XWC_SERIAL));
+            if (nser) {
+                if (lane == 0) {
+                    NodeWin<MAXS> on, dn;                    // (origin / context node of the walk)
+                    uint32_t oi = XNONE, di = XNONE;
+                    for (uint32_t k = 0; k < L; k++)
+                        if (cls[k] == XWC_SERIAL) xg_event<MAXS>(st, io, pt, lo, j0 + k, cn, on, dn, cl, oi, di);
+                    if (oi != XNONE) nw_store(on, st, aux_rows(st, oi));
+                    if (di != XNONE) nw_store(dn, st, aux_rows(st, di));
                 }
-                if (oi != XNONE) { nw_store(on, st, aux_rows(st, oi)); oi = XNONE; }
+                __syncthreads();
             }
-            __syncthreads();
+            if (lane == 0 && st.xw_stats) {
+                atomicAdd(&st.xw_stats[jac ? 0 : 1], 1ull);
+                if (nser) atomicAdd(&st.xw_stats[3], nser);
+            }
+            XW_PF(1)
             // 3. the blocks and completions, summed per node
             int64_t blk = 0, succ = 0, rt = 0, exc = 0, thr = 0, minrt = INT64_MAX;
             int nblk = 0, ncmp = 0, nexc = 0;
             int64_t pss = 0;
             int npss = 0;
+            uint8_t vfin = mst;                                  // this lane's final status (vch)
             if (myc == XWC_BLOCK) {
-                emit_verdict(io, j, mst, (int32_t)mwait, (uint16_t)mrule);
+                xw_emit(io, e.i, (int32_t)mwait, (uint16_t)mrule);
                 blk = c; nblk = 1;
             } else if (myc == XWC_PASS) {
-                emit_verdict(io, j, mst, (int32_t)mwait, 0);
+                xw_emit(io, e.i, (int32_t)mwait, 0);
                 pss = c; npss = 1;
-            } else if (myc == XWC_EXIT && jac) {             // (liveness and create time from the solve)
+            } else if (myc == XWC_EXIT) {                    // StatisticSlot.exit :134-165
+                // (liveness from the solve; on the serial path an entry of this
+                // chunk has its status in v_status by now)
+                const bool live = jac ? x_live
+                                      : (eidx >= 0 ? !v_blocked(io.v_status[j0 + eidx]) : live_pre);
                 uint8_t v = SF_V_EXIT_IGNORED;
-                if (x_live) {
+                if (live) {
                     v = SF_V_EXIT;
-                    succ = c; rt = t - x_cts; minrt = rt; thr = -1; ncmp = 1;
+                    succ = c; rt = t - xcts; minrt = rt; thr = -1; ncmp = 1;
                     if (fl & SF_EV_ERROR) { exc = c; nexc = 1; }
                 }
                 io.v_status[j] = v;
-                emit_verdict(io, j, v, 0, 0);
-            } else if (myc == XWC_EXIT) {                    // decide_xgroup's exit (StatisticSlot.exit :134-165)
-                int64_t ref = io.eref ? io.eref[j] : -1;
-                bool blocked; int64_t cts;
-                if (ref >= 0) {
-                    if (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT) ||
-                        io.ev_res[io.perm[ref]] != gres) {
-                        *st.err = SF_ERR_INVALID;
-                        ref = j;
-                    }
-                    blocked = ref == (int64_t)j ? true : v_blocked(io.v_status[ref]);
-                    cts = io.ts[ref];
-                } else {
-                    blocked = ref == EREF_DEAD; cts = io.cts ? io.cts[j] : t;
-                }
-                uint8_t v = SF_V_EXIT_IGNORED;
-                if (!blocked) {
-                    v = SF_V_EXIT;
-                    succ = c; rt = t - cts; minrt = rt; thr = -1; ncmp = 1;
-                    if (fl & SF_EV_ERROR) { exc = c; nexc = 1; }
-                }
-                io.v_status[j] = v;
-                emit_verdict(io, j, v, 0, 0);
+                vfin = v;
+            } else if (myc == XWC_SERIAL) {
+                vfin = io.v_status[j];                       // (lane 0's walk wrote it)
             }
             // the ClusterNode's sums: wavefront reductions (every lane adds to it)
             XwRow crow;
@@ -959,6 +1015,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                 crow.nblk = (unsigned)__popcll(__ballot(nblk != 0)); crow.ncmp = (unsigned)__popcll(__ballot(ncmp != 0));
                 crow.nexc = (unsigned)__popcll(__ballot(nexc != 0)); crow.npass = (unsigned)__popcll(__ballot(npss != 0));
             }
+            XW_PF(2)
             if (nblk || ncmp || npss) {
                 if (jac) {
                     if (my_row > 0) xw_add(rows[my_row], blk, nblk, succ, rt, minrt, exc, nexc, thr, ncmp, pss, npss);
@@ -973,6 +1030,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                 }
             }
             __syncthreads();
+            XW_PF(3)
             if (lane == 0) xw_apply<MAXS>(cn, crow, t0);
             if constexpr (MAXS == 2) {
                 if (jac) {                                       // into the cached origin nodes
@@ -991,16 +1049,19 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
                 xw_apply<MAXS>(x, rows[k], t0);
                 nw_store(x, st, nr);
             }
+            XW_PF(4)
+            // the next chunk: its exits of entries in this chunk read vch
+            if (act) vch[lane] = vfin;
             __syncthreads();
-#ifdef SF_XW_PROFILE
-            pf_post += wall_clock64() - pf_t;
-#endif
-            j0 += L;
+            jprev = j0;
+            e = nx;
+            XW_PF(5)
+            j0 = jn;
         }
 #ifdef SF_XW_PROFILE
         if (lane == 0 && hi - lo > 20000)
-            printf("xw seg n=%u chunks=%llu setup=%llu solve=%llu post=%llu (x10ns)\n", hi - lo, pf_n, pf_setup, pf_solve,
-                   pf_post);
+            printf("xw seg n=%u chunks=%llu setup=%llu solve=%llu post %llu %llu %llu %llu %llu %llu (x10ns)\n", hi - lo,
+                   pf_n, pf_setup, pf_solve, pf_p[0], pf_p[1], pf_p[2], pf_p[3], pf_p[4], pf_p[5]);
 #endif
         if constexpr (MAXS == 2) xw_cache_flush(st, oc, ocnw, lane);
         if (lane == 0 && cl != XNONE) nw_store(cn, st, cluster_rows(st, cl));
@@ -2008,8 +2069,8 @@ static void launch_thr_prep(Work& w, const DevBatch& b, hipStream_t s) {
 // start first, on A; QPS/WarmUp heavy segments on B, the light lanes on C;
 // then the verdicts are scattered back to submission order.
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
-                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipEvent_t* ev, bool timing, const OxPlan* ox,
-                         bool classify) {
+                         hipStream_t s, hipStream_t s2, hipStream_t s3, hipStream_t s4, hipEvent_t* ev, bool timing,
+                         const OxPlan* ox, bool classify) {
     const uint32_t n = b.n;
     if (n == 0) return hipSuccess;
     if (classify) launch_classify(st, w, b, s, ev, timing);
@@ -2048,6 +2109,24 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     hipEventRecord(ev[12], s);
     hipStreamWaitEvent(s2, ev[5], 0);
     hipStreamWaitEvent(s3, ev[5], 0);
+    // long one-resource xflow segments: the wave walk, on its own stream from
+    // the fork (its segments share no node or rule with any other kernel of the
+    // phase; the longest of them is usually the phase's critical path)
+    const bool xw_on = st.xmap && st.xw;
+    auto launch_xw = [&](hipStream_t sx) {
+        const unsigned g = (unsigned)std::min<size_t>((size_t)b.n / XW_MIN + 1, 2048);
+        if (st.S <= 2)
+            hipLaunchKernelGGL(k_decide_xw<2>, dim3(g), dim3(64), 0, sx, st, io, w.seg_start, w.seg_res,
+                               w.xw_list, w.counters + 12);
+        else
+            hipLaunchKernelGGL(k_decide_xw<SF_MAX_SAMPLE_COUNT>, dim3(g), dim3(64), 0, sx, st, io, w.seg_start,
+                               w.seg_res, w.xw_list, w.counters + 12);
+        hipEventRecord(ev[15], sx);
+    };
+    if (xw_on) {
+        hipStreamWaitEvent(s4, ev[5], 0);
+        launch_xw(s4);
+    }
     if (st.n_window_rules) {
         // acquireCount prefix of the entries (QPS / WarmUp window budgets, k_heavy_decide
         // only): state-independent, but here on stream B rather than in the sort phase,
@@ -2107,24 +2186,16 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
         else
             hipLaunchKernelGGL(k_decide_x<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, 64)), dim3(64), 0, s3, st, io,
                                w.seg_start, w.seg_res, w.seg_mode, w.n_seg);
-        if (st.xw) {                               // long one-resource segments: the wave walk
-            const unsigned g = (unsigned)std::min<size_t>((size_t)b.n / XW_MIN + 1, 2048);
-            if (st.S <= 2)
-                hipLaunchKernelGGL(k_decide_xw<2>, dim3(g), dim3(64), 0, s3, st, io, w.seg_start, w.seg_res,
-                                   w.xw_list, w.counters + 12);
-            else
-                hipLaunchKernelGGL(k_decide_xw<SF_MAX_SAMPLE_COUNT>, dim3(g), dim3(64), 0, s3, st, io, w.seg_start,
-                                   w.seg_res, w.xw_list, w.counters + 12);
-        }
     }
     hipEventRecord(ev[9], s3);                     // light done (also the join of C)
     hipEventRecord(ev[6], s2);                     // join B and C
     hipStreamWaitEvent(s, ev[6], 0);
     hipStreamWaitEvent(s, ev[9], 0);
-    hipEventRecord(ev[13], s);
+    hipEventRecord(ev[13], s);                     // (the origin pass below does not wait for the wave walk)
+    if (xw_on) hipStreamWaitEvent(s, ev[15], 0);
     if (timing) hipEventRecord(ev[3], s);
-    // origin nodes no rule reads (sf_origin.hip): from the sorted verdicts,
-    // beside the verdict scatter
+    // origin nodes no rule reads (sf_origin.hip): from the sorted verdicts
+    // of the other segments, beside the wave walk and the verdict scatter
     if (ox) {
         hipStreamWaitEvent(s2, ev[13], 0);
         const hipError_t e = launch_ox_apply(st, w, b, ox->n_heavy, ox->n_pairs, ox->win, s2);
