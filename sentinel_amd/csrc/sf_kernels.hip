@@ -505,24 +505,52 @@ __device__ void xw_cache_flush(const DevState& st, XwCache& oc, unsigned char* o
     __syncthreads();
 }
 
-__device__ __forceinline__ long long xw_excl_scan(long long v, uint32_t lane) {
-    long long x = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long y = __shfl_up(x, o);
-        if ((int)lane >= o) x += y;
-    }
-    return x - v;
+// wavefront scans on DPP (row shifts inside each 16-lane row, then the row
+// broadcasts of lanes 15 and 31): a handful of ALU cycles per step instead of
+// an LDS-crossbar shuffle; 64-bit values move as two 32-bit halves, lanes
+// without a source keep `idv` (the operation's identity)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ long long xw_dpp(long long v, long long idv) {
+    const unsigned long long u = (unsigned long long)v, iu = (unsigned long long)idv;
+    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)iu, (int)(unsigned)u, CTRL, ROWMASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(unsigned)(iu >> 32), (int)(unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned long long)(unsigned)lo);
 }
-// inclusive max-plus scan of f(x) = max(x + a, b) in lane order
-__device__ __forceinline__ void xw_mp_scan(long long& a, long long& b, uint32_t lane) {
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long pa = __shfl_up(a, o), pb = __shfl_up(b, o);
-        if ((int)lane >= o) {
-            const long long nb = max(pb + a, b);
-            a = pa + a;
-            b = nb;
-        }
-    }
+template <class F>
+__device__ __forceinline__ long long xw_scan_op(long long x, long long idv, F f) {
+    x = f(x, xw_dpp<0x111, 0xf>(x, idv));        // row_shr:1
+    x = f(x, xw_dpp<0x112, 0xf>(x, idv));        // row_shr:2
+    x = f(x, xw_dpp<0x114, 0xf>(x, idv));        // row_shr:4
+    x = f(x, xw_dpp<0x118, 0xf>(x, idv));        // row_shr:8
+    x = f(x, xw_dpp<0x142, 0xa>(x, idv));        // row_bcast:15 -> rows 1, 3
+    x = f(x, xw_dpp<0x143, 0xc>(x, idv));        // row_bcast:31 -> rows 2, 3
+    return x;
+}
+__device__ __forceinline__ long long xw_excl_scan(long long v, uint32_t) {
+    return xw_scan_op(v, 0, [](long long x, long long y) { return x + y; }) - v;
+}
+// wavefront total / minimum (lane 63 of the inclusive scan)
+__device__ __forceinline__ long long xw_wsum(long long v) {
+    return __shfl(xw_scan_op(v, 0, [](long long x, long long y) { return x + y; }), 63);
+}
+__device__ __forceinline__ long long xw_wmin(long long v) {
+    return __shfl(xw_scan_op(v, INT64_MAX, [](long long x, long long y) { return y < x ? y : x; }), 63);
+}
+// inclusive max-plus scan of f(x) = max(x + a, b) in lane order (an earlier
+// lane's (pa, pb) composed under this lane's: (pa + a, max(pb + a, b)))
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void xw_mp_step(long long& a, long long& b) {
+    const long long pa = xw_dpp<CTRL, ROWMASK>(a, 0), pb = xw_dpp<CTRL, ROWMASK>(b, XW_MPNEG);
+    b = max(pb + a, b);
+    a = pa + a;
+}
+__device__ __forceinline__ void xw_mp_scan(long long& a, long long& b, uint32_t) {
+    xw_mp_step<0x111, 0xf>(a, b);
+    xw_mp_step<0x112, 0xf>(a, b);
+    xw_mp_step<0x114, 0xf>(a, b);
+    xw_mp_step<0x118, 0xf>(a, b);
+    xw_mp_step<0x142, 0xa>(a, b);
+    xw_mp_step<0x143, 0xc>(a, b);
 }
 
 __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& snap, XwRow* rows, XwScratch& xs,
@@ -530,7 +558,13 @@ __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& s
                                uint32_t lane, uint32_t L, int64_t t0, int64_t t,
                                uint8_t fl, int32_t c, uint32_t origin, int eidx, bool live_pre, uint32_t l, uint32_t r0,
                                uint32_t r1, uint8_t* myc, uint8_t* mst, int* mrule, int64_t* mwait, int* my_row,
-                               bool* x_live) {
+                               bool* x_live, unsigned long long* pfs = nullptr) {
+#ifdef SF_XW_PROFILE
+    unsigned long long pt_ = wall_clock64();
+#define XS_PF(k) if (lane == 0 && pfs) { const unsigned long long x_ = wall_clock64(); pfs[k] += x_ - pt_; pt_ = x_; }
+#else
+#define XS_PF(k)
+#endif
     const bool valid = lane < L;
     const bool is_exit = valid && (fl & SF_EV_EXIT);
     const bool is_sys = valid && !is_exit && (fl & EVF_SYSBLK);
@@ -570,6 +604,7 @@ __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& s
         }
         osr = (int)h + 1;
     }
+    XS_PF(0)
     xs.os[lane] = osr;
     __syncthreads();
     uint64_t sm = 0;                                           // earlier lanes of the same origin
@@ -577,6 +612,7 @@ __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& s
         for (int q = 0; q < 64; q++)
             if (xs.os[q] == osr) sm |= 1ull << q;
     sm &= (1ull << lane) - 1ull;
+    XS_PF(1)
     // node bases (the first lane of each origin) and the rules' constants
     if (osr >= 0 && sm == 0) {
         const uint32_t ko = oc.ko[osr - 1];
@@ -616,6 +652,7 @@ __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& s
         }
     }
     __syncthreads();
+    XS_PF(2)
     const double isec = st.interval / 1000.0;
     uint8_t sel[MAX_RULES];                                    // 0 none, 1 ClusterNode, 2 origin node
     long long cost[MAX_RULES];
@@ -636,6 +673,7 @@ __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& s
     }
     // an exit's liveness: its entry passed (in this chunk: that lane's verdict,
     // eidx; before it: live_pre, from the walk's exit descriptor)
+    XS_PF(3)
     int d = is_solve ? 1 : 0, ri = 0;
     uint32_t reach = 0, passk = 0;
     long long w = 0;
@@ -702,6 +740,7 @@ __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& s
         if (lane == 0 && st.xw_stats) atomicAdd(&st.xw_stats[2], 1ull);
         if (!__ballot(changed)) break;
     }
+    XS_PF(4)
     // the rules' state after the chunk (lane 0 writes)
     for (uint32_t kr = 0; kr < nrules; kr++) {
         const DevRule& r = st.rules[r0 + kr];
@@ -725,6 +764,7 @@ __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& s
             st.rstate[r0 + kr] = rs;
         }
     }
+    XS_PF(5)
     if (is_solve) {
         *myc = d ? XWC_PASS : XWC_BLOCK;
         *mst = d ? (uint8_t)(w > 0 ? SF_V_PASS_WAIT : SF_V_PASS) : (uint8_t)SF_V_BLOCK_FLOW;
@@ -790,6 +830,11 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
     __shared__ __align__(16) unsigned char snap_raw[sizeof(NodeWin<MAXS>)];
     __shared__ uint8_t cls[64];
     __shared__ uint8_t vch[64];                             // the previous chunk's final statuses
+#ifdef SF_XW_PROFILE
+    __shared__ unsigned long long pfs[8];
+#else
+    unsigned long long* pfs = nullptr;
+#endif
     __shared__ XwRow rows[XW_KCAP];
     __shared__ XwScratch xs;
     __shared__ XwCache oc;
@@ -817,6 +862,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
         __syncthreads();
 #ifdef SF_XW_PROFILE
         unsigned long long pf_setup = 0, pf_solve = 0, pf_post = 0, pf_n = 0, pf_t = 0, pf_p[6] = {0, 0, 0, 0, 0, 0};
+        if (lane < 8) pfs[lane] = 0;
 #define XW_PF(k) { const unsigned long long x_ = wall_clock64(); pf_p[k] += x_ - pf_t; pf_t = x_; pf_post += 0; }
 #else
 #define XW_PF(k)
@@ -898,7 +944,7 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             if (jac) {
                 if constexpr (MAXS == 2)
                     xw_solve_chunk(st, snap, rows, xs, oc, ocnw, lane, L, t0, t, fl, c, origin, eidx, live_pre, l,
-                                   r0, r1, &myc, &mst, &mrule, &mwait, &my_row, &x_live);
+                                   r0, r1, &myc, &mst, &mrule, &mwait, &my_row, &x_live, pfs);
             } else {
                 if (act) {
                     if (fl & SF_EV_EXIT) myc = thr_sens ? XWC_SERIAL : XWC_EXIT;
@@ -1000,14 +1046,9 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
             XwRow crow;
             {
                 long long v[6] = {blk, succ, rt, exc, thr, pss};
-                long long mr = minrt;
 #pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-                    for (int f = 0; f < 6; f++) v[f] += __shfl_xor(v[f], o);
-                    const long long y = __shfl_xor(mr, o);
-                    mr = y < mr ? y : mr;
-                }
+                for (int f = 0; f < 6; f++) v[f] = xw_wsum(v[f]);
+                const long long mr = xw_wmin(minrt);
                 crow.blk = (unsigned long long)v[0]; crow.succ = (unsigned long long)v[1];
                 crow.rt = (unsigned long long)v[2]; crow.exc = (unsigned long long)v[3];
                 crow.thr = v[4] + (long long)__popcll(__ballot(npss != 0)); crow.pass = (unsigned long long)v[5];
@@ -1060,8 +1101,8 @@ __global__ void __launch_bounds__(64) k_decide_xw(DevState st, SegIO io, const u
         }
 #ifdef SF_XW_PROFILE
         if (lane == 0 && hi - lo > 20000)
-            printf("xw seg n=%u chunks=%llu setup=%llu solve=%llu post %llu %llu %llu %llu %llu %llu (x10ns)\n", hi - lo,
-                   pf_n, pf_setup, pf_solve, pf_p[0], pf_p[1], pf_p[2], pf_p[3], pf_p[4], pf_p[5]);
+            printf("xw seg n=%u chunks=%llu setup=%llu solve=%llu (%llu %llu %llu %llu %llu %llu) post %llu %llu %llu %llu %llu %llu (x10ns)\n", hi - lo,
+                   pf_n, pf_setup, pf_solve, pfs[0], pfs[1], pfs[2], pfs[3], pfs[4], pfs[5], pf_p[0], pf_p[1], pf_p[2], pf_p[3], pf_p[4], pf_p[5]);
 #endif
         if constexpr (MAXS == 2) xw_cache_flush(st, oc, ocnw, lane);
         if (lane == 0 && cl != XNONE) nw_store(cn, st, cluster_rows(st, cl));
