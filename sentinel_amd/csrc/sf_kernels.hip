@@ -434,31 +434,23 @@ __device__ __forceinline__ void xw_add(XwRow& r, int64_t blk, int nblk, int64_t 
     }
     if (nexc) { atomicAdd(&r.exc, (unsigned long long)exc); atomicAdd(&r.nexc, 1u); }
 }
-// a row's sums into a node (all events of the chunk are in the bucket of t0)
+// a row's sums into a node (all events of the chunk are in the bucket of t0):
+// one currentWindow lookup per window for all of the row's counters
 template <int MAXS>
 __device__ __forceinline__ void xw_apply(NodeWin<MAXS>& nd, const XwRow& r, int64_t t0) {
-    if (r.npass) {
-        const int64_t p = (int64_t)r.pass;
-        nd.sec_apply(t0, [&](Bucket& x) { x.pass = wadd(x.pass, p); });
-        nd.min_apply(t0, [&](Bucket& x) { x.pass = wadd(x.pass, p); });
-    }
-    if (r.nblk) {
-        const int64_t b = (int64_t)r.blk;
-        nd.sec_apply(t0, [&](Bucket& x) { x.block = wadd(x.block, b); });
-        nd.min_apply(t0, [&](Bucket& x) { x.block = wadd(x.block, b); });
-    }
-    if (r.ncmp) {
-        const int64_t sc = (int64_t)r.succ, rt = (int64_t)r.rt, mr = r.minrt;
-        auto f = [&](Bucket& x) { x.succ = wadd(x.succ, sc); x.rt = wadd(x.rt, rt); if (mr < x.min_rt) x.min_rt = mr; };
-        nd.sec_apply(t0, f);
-        nd.min_apply(t0, f);
-    }
-    if (r.npass || r.ncmp) nd.threads = wadd(nd.threads, r.thr);
-    if (r.nexc) {
-        const int64_t e = (int64_t)r.exc;
-        nd.sec_apply(t0, [&](Bucket& x) { x.exc = wadd(x.exc, e); });
-        nd.min_apply(t0, [&](Bucket& x) { x.exc = wadd(x.exc, e); });
-    }
+    const bool hp = r.npass != 0, hb = r.nblk != 0, hc = r.ncmp != 0, he = r.nexc != 0;
+    if (!(hp || hb || hc || he)) return;
+    const int64_t p = (int64_t)r.pass, b = (int64_t)r.blk, sc = (int64_t)r.succ, rt = (int64_t)r.rt, mr = r.minrt,
+                  e = (int64_t)r.exc;
+    auto f = [&](Bucket& x) {
+        if (hp) x.pass = wadd(x.pass, p);
+        if (hb) x.block = wadd(x.block, b);
+        if (hc) { x.succ = wadd(x.succ, sc); x.rt = wadd(x.rt, rt); if (mr < x.min_rt) x.min_rt = mr; }
+        if (he) x.exc = wadd(x.exc, e);
+    };
+    nd.sec_apply(t0, f);
+    nd.min_apply(t0, f);
+    if (hp || hc) nd.threads = wadd(nd.threads, r.thr);
 }
 
 // ---- the exact chunk solve (S <= 2, no prioritized entry in the chunk)
