@@ -621,7 +621,10 @@ __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& s
         NodeWin<2> x = snap;
         xs.base[0] = x.sec_sum_pass(t0);
         xs.thr[0] = x.threads;
-        const int64_t prevq = j_d2l(x.previous_pass_qps(t0));
+        // (the previous second's QPS: read only at a second's first sync -- it is
+        // a minute-bucket load from HBM)
+        int64_t prevq = 0;
+        bool have_prevq = false;
         for (uint32_t k = r0; k < r1; k++) {
             const DevRule& r = st.rules[k];
             XwRuleC& q = xs.rc[k - r0];
@@ -630,6 +633,7 @@ __device__ __forceinline__ void xw_solve_chunk(const DevState& st, NodeWin<2>& s
             q.thr = r.count; q.qps = r.count;
             if (r.kind == CT_WARM_UP || r.kind == CT_WARM_UP_RATE_LIMITER) {
                 if (r.limit_app == SF_APP_DEFAULT && q.rs.last_filled < t0 - t0 % 1000) {
+                    if (!have_prevq) { prevq = j_d2l(x.previous_pass_qps(t0)); have_prevq = true; }
                     warm_sync(r, q.rs, t0, prevq);           // (the ClusterNode's previous second)
                     q.sync = 1;
                 }
