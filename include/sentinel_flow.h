@@ -453,6 +453,13 @@ int  sf_submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out)
 /* Enqueued only; sf_sync waits and reports the first error.  Host arrays
  * (batch and verdicts) must stay untouched until sf_sync.                   */
 int  sf_submit_packed_async(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out);
+/* Waits for ONE sf_submit_packed_async batch with host verdicts -- the one
+ * whose verdicts go to out->status -- and returns that batch's error; the
+ * batch enqueued after it keeps running.  With two host verdict buffers used
+ * in turn, a caller double-buffers: enqueue k+1, sf_sync_packed(k), hand out
+ * k's verdicts, enqueue k+2 into k's buffers ...  (the Java flusher,
+ * EventBatcher.java).  SF_OK when that batch was already collected. */
+int  sf_sync_packed(sf_engine* e, const sf_verdicts* out);
 
 /* SystemRules on a resource-sharded node (shard_count > 1).
  * SystemRuleManager.checkSystem (SystemRuleManager.java:291-348) reads the

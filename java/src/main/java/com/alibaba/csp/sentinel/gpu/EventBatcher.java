@@ -25,8 +25,20 @@ import static java.lang.foreign.ValueLayout.JAVA_SHORT;
  * queue order, as the engine requires.  The arrays are page-locked host
  * memory from sf_host_alloc (the engine's H2D copy runs at PCIe speed, no
  * staging copy); a batch without ParamFlow arguments or context names, whose
- * clock spans less than 2^20 ms, goes as sf_packed_batch (8 bytes per event,
- * sf_submit_packed), every other one as the sf_event_batch SoA (sf_submit).
+ * clock spans less than 2^20 ms, goes as sf_packed_batch (8 bytes per event),
+ * every other one as the sf_event_batch SoA (sf_submit).
+ *
+ * Latency / throughput contract.  Packed batches are double-buffered: the
+ * flusher enqueues batch k+1 with sf_submit_packed_async into the buffer set
+ * batch k is not using, then waits for batch k alone (sf_sync_packed) and
+ * hands out its verdicts, so the H2D copy of k+1 overlaps the decision of k
+ * and the copy back of k-1.  A caller still waits only for its own batch: its
+ * verdict is delivered as soon as its batch is back, and a batch is never held
+ * for a later one -- when the queue is empty the flusher collects the batch in
+ * flight at once.  An EXIT can never refer to an entry of the batch in flight
+ * (its caller had that entry's verdict first), so exits need no ordering work.
+ * A SoA batch, a rule reload, and an engine with SystemRules (whose packed
+ * batches the engine decides synchronously) collect the batch in flight first.
  */
 final class EventBatcher implements Runnable {
     static final class Ticket {
@@ -49,7 +61,18 @@ final class EventBatcher implements Runnable {
     private final MemorySegment res, ts, cnt, flags, eref, cts, nArgs, argTag, argBits, elemOff, elemTag, elemBits;
     private final MemorySegment origin, context;
     private final MemorySegment status, waitMs, ruleIdx, batch, verdicts;
-    private final MemorySegment pev, pxref, pxcts, pcext, packed;   // sf_packed_batch arrays
+
+    /** One buffer set of the packed path: the batch arrays, its verdicts and its tickets. */
+    private final class PackedBuf {
+        final MemorySegment pev = pinned(8L * maxBatch), pxref = pinned(8L * maxBatch), pxcts = pinned(8L * maxBatch);
+        final MemorySegment pcext = pinned(4L * maxBatch), porigin = pinned(4L * maxBatch);
+        final MemorySegment pstatus = pinned(maxBatch), pwait = pinned(4L * maxBatch), prule = pinned(2L * maxBatch);
+        final MemorySegment packed = arena.allocate(PACKED_BATCH), pverdicts = arena.allocate(VERDICTS);
+        final List<Ticket> tickets = new ArrayList<>();
+    }
+    private final PackedBuf[] pbufs;
+    private int pcur;
+    private PackedBuf inFlight;                  // enqueued, verdicts not yet handed out
     private long seq, lastTs = Long.MIN_VALUE, loadedRuleVersion = -1;
     static final int ARG_SLOTS = Integer.getInteger("sentinel.gpu.argSlots", 2);
     static final int MAX_ELEMS = Integer.getInteger("sentinel.gpu.maxElems", 1 << 20);
@@ -66,9 +89,8 @@ final class EventBatcher implements Runnable {
         elemTag = pinned(MAX_ELEMS); elemBits = pinned(8L * MAX_ELEMS);
         origin = pinned(4L * maxBatch); context = pinned(4L * maxBatch);
         status = pinned(maxBatch); waitMs = pinned(4L * maxBatch); ruleIdx = pinned(2L * maxBatch);
-        pev = pinned(8L * maxBatch); pxref = pinned(8L * maxBatch); pxcts = pinned(8L * maxBatch);
-        pcext = pinned(4L * maxBatch);
-        batch = arena.allocate(EVENT_BATCH); verdicts = arena.allocate(VERDICTS); packed = arena.allocate(PACKED_BATCH);
+        batch = arena.allocate(EVENT_BATCH); verdicts = arena.allocate(VERDICTS);
+        pbufs = new PackedBuf[] {new PackedBuf(), new PackedBuf()};
         Thread t = new Thread(this, "sentinel-gpu-flusher");
         t.setDaemon(true);
         t.start();
@@ -102,22 +124,57 @@ final class EventBatcher implements Runnable {
         List<Ticket> drained = new ArrayList<>(maxBatch);
         while (true) {
             try {
-                Ticket first = queue.poll(1, TimeUnit.SECONDS);
-                if (first == null) continue;
-                drained.clear();
+                // with a batch in flight, an empty queue collects it at once (no caller waits on a later batch)
+                Ticket first = inFlight != null ? queue.poll() : queue.poll(1, TimeUnit.SECONDS);
+                if (first == null) {
+                    collect();
+                    continue;
+                }
+                drained = new ArrayList<>(maxBatch);
                 drained.add(first);
                 queue.drainTo(drained, maxBatch - 1);
                 flush(drained);
             } catch (Throwable t) {
-                // an engine error fails the batch open (the reference never blocks on
-                // an internal error, CtSph.java:155-158): every caller passes
-                for (Ticket k : drained) { k.waitMs = 0; k.ruleIdx = 0; k.status = V_PASS; LockSupport.unpark(k.caller); }
+                failOpen(drained);
             }
         }
     }
 
+    /** An engine error fails the batch open (the reference never blocks on an internal error, CtSph.java:155-158). */
+    private static void failOpen(List<Ticket> b) {
+        for (Ticket k : b) {
+            if (k.status >= 0) continue;
+            k.waitMs = 0; k.ruleIdx = 0; k.status = V_PASS; LockSupport.unpark(k.caller);
+        }
+    }
+
+    /** Waits for the batch in flight alone (sf_sync_packed) and hands out its verdicts. */
+    private void collect() {
+        PackedBuf f = inFlight;
+        if (f == null) return;
+        inFlight = null;
+        try {
+            check((int) SYNC_PACKED.invokeExact(engine.handle, f.pverdicts));
+            deliver(f.tickets, f.pstatus, f.pwait, f.prule);
+        } catch (Throwable t) {
+            failOpen(f.tickets);
+        }
+    }
+
+    private static void deliver(List<Ticket> b, MemorySegment st, MemorySegment wt, MemorySegment ru) {
+        for (int i = 0; i < b.size(); i++) {
+            Ticket t = b.get(i);
+            t.waitMs = wt.getAtIndex(JAVA_INT, i);
+            t.ruleIdx = Short.toUnsignedInt(ru.getAtIndex(JAVA_SHORT, i));
+            t.status = st.getAtIndex(JAVA_BYTE, i);
+            LockSupport.unpark(t.caller);
+        }
+    }
+
     private void flush(List<Ticket> b) throws Throwable {
+        engine.followRuleProperties();                       // a data source's property swapped in since
         if (engine.ruleVersion.get() != loadedRuleVersion) {
+            collect();                                       // decided under the rules it was sorted with
             loadedRuleVersion = engine.ruleVersion.get();
             engine.loadRulesNow();
         }
@@ -125,6 +182,7 @@ final class EventBatcher implements Runnable {
         final long bs = ++seq;
         int n = b.size(), ne = 0;
         if (flushPacked(b, bs)) return;
+        collect();                                           // the SoA path is synchronous
         boolean anyExit = false;
         elemOff.set(JAVA_INT, 0, 0);
         for (int i = 0; i < n; i++) {
@@ -195,18 +253,13 @@ final class EventBatcher implements Runnable {
         verdicts.set(ADDRESS, off(VERDICTS, "wait_ms"), waitMs);
         verdicts.set(ADDRESS, off(VERDICTS, "rule_idx"), ruleIdx);
         check((int) SUBMIT.invokeExact(engine.handle, batch, verdicts));
-        for (int i = 0; i < n; i++) {
-            Ticket t = b.get(i);
-            t.waitMs = waitMs.getAtIndex(JAVA_INT, i);
-            t.ruleIdx = Short.toUnsignedInt(ruleIdx.getAtIndex(JAVA_SHORT, i));
-            t.status = status.getAtIndex(JAVA_BYTE, i);
-            LockSupport.unpark(t.caller);
-        }
+        deliver(b, status, waitMs, ruleIdx);
     }
 
     /**
      * The batch as sf_packed_batch when it fits (no arguments, no context
-     * names, clock span < 2^20 ms); false: the caller builds the SoA batch.
+     * names, clock span < 2^20 ms): enqueued into the free buffer set, then the
+     * batch before it collected; false: the caller builds the SoA batch.
      */
     private boolean flushPacked(List<Ticket> b, long bs) throws Throwable {
         final int n = b.size();
@@ -217,46 +270,52 @@ final class EventBatcher implements Runnable {
             if (t0 == Long.MIN_VALUE) t0 = last;
         }
         if (last - t0 >= (1L << 20)) return false;
+        final PackedBuf p = pbufs[pcur];             // not the in-flight set: sets alternate
         int nx = 0, nc = 0;
         for (int i = 0; i < n; i++) {
             Ticket t = b.get(i);
             t.batchSeq = bs; t.batchIndex = i;
             lastTs = Math.max(lastTs, t.ts);
             long c = t.count;
-            if (c < 1 || c > 127) { pcext.setAtIndex(JAVA_INT, nc++, t.count); c = 0; }
+            if (c < 1 || c > 127) { p.pcext.setAtIndex(JAVA_INT, nc++, t.count); c = 0; }
             long f = t.flags & 0x1f;
-            pev.setAtIndex(JAVA_LONG, i, (t.resource & 0xffffffffL) | ((lastTs - t0) << 32)
+            p.pev.setAtIndex(JAVA_LONG, i, (t.resource & 0xffffffffL) | ((lastTs - t0) << 32)
                     | (c << PK_COUNT_SHIFT) | (f << PK_FLAGS_SHIFT));
-            origin.setAtIndex(JAVA_INT, i, t.origin);
+            p.porigin.setAtIndex(JAVA_INT, i, t.origin);
             if ((t.flags & EV_EXIT) != 0) {
                 boolean same = t.entry != null && t.entry.batchSeq == bs;
-                pxref.setAtIndex(JAVA_LONG, nx, same ? t.entry.batchIndex : -1L);
-                pxcts.setAtIndex(JAVA_LONG, nx, t.createTs);
+                p.pxref.setAtIndex(JAVA_LONG, nx, same ? t.entry.batchIndex : -1L);
+                p.pxcts.setAtIndex(JAVA_LONG, nx, t.createTs);
                 nx++;
             }
         }
-        packed.set(JAVA_INT, off(PACKED_BATCH, "n"), n);
-        packed.set(JAVA_INT, off(PACKED_BATCH, "mem"), SF_MEM_HOST_);
-        packed.set(JAVA_LONG, off(PACKED_BATCH, "ts_base"), t0);
-        packed.set(ADDRESS, off(PACKED_BATCH, "ev"), pev);
-        packed.set(ADDRESS, off(PACKED_BATCH, "exit_ref"), nx > 0 ? pxref : MemorySegment.NULL);
-        packed.set(ADDRESS, off(PACKED_BATCH, "exit_cts"), nx > 0 ? pxcts : MemorySegment.NULL);
-        packed.set(ADDRESS, off(PACKED_BATCH, "count_ext"), nc > 0 ? pcext : MemorySegment.NULL);
-        packed.set(ADDRESS, off(PACKED_BATCH, "origin"), origin);
-        packed.set(JAVA_INT, off(PACKED_BATCH, "n_exit"), nx);
-        packed.set(JAVA_INT, off(PACKED_BATCH, "n_count_ext"), nc);
-        verdicts.set(JAVA_INT, off(VERDICTS, "mem"), SF_MEM_HOST_);
-        verdicts.set(ADDRESS, off(VERDICTS, "status"), status);
-        verdicts.set(ADDRESS, off(VERDICTS, "wait_ms"), waitMs);
-        verdicts.set(ADDRESS, off(VERDICTS, "rule_idx"), ruleIdx);
-        check((int) SUBMIT_PACKED.invokeExact(engine.handle, packed, verdicts));
-        for (int i = 0; i < n; i++) {
-            Ticket t = b.get(i);
-            t.waitMs = waitMs.getAtIndex(JAVA_INT, i);
-            t.ruleIdx = Short.toUnsignedInt(ruleIdx.getAtIndex(JAVA_SHORT, i));
-            t.status = status.getAtIndex(JAVA_BYTE, i);
-            LockSupport.unpark(t.caller);
+        MemorySegment pk = p.packed;
+        pk.set(JAVA_INT, off(PACKED_BATCH, "n"), n);
+        pk.set(JAVA_INT, off(PACKED_BATCH, "mem"), SF_MEM_HOST_);
+        pk.set(JAVA_LONG, off(PACKED_BATCH, "ts_base"), t0);
+        pk.set(ADDRESS, off(PACKED_BATCH, "ev"), p.pev);
+        pk.set(ADDRESS, off(PACKED_BATCH, "exit_ref"), nx > 0 ? p.pxref : MemorySegment.NULL);
+        pk.set(ADDRESS, off(PACKED_BATCH, "exit_cts"), nx > 0 ? p.pxcts : MemorySegment.NULL);
+        pk.set(ADDRESS, off(PACKED_BATCH, "count_ext"), nc > 0 ? p.pcext : MemorySegment.NULL);
+        pk.set(ADDRESS, off(PACKED_BATCH, "origin"), p.porigin);
+        pk.set(JAVA_INT, off(PACKED_BATCH, "n_exit"), nx);
+        pk.set(JAVA_INT, off(PACKED_BATCH, "n_count_ext"), nc);
+        MemorySegment v = p.pverdicts;
+        v.set(JAVA_INT, off(VERDICTS, "mem"), SF_MEM_HOST_);
+        v.set(ADDRESS, off(VERDICTS, "status"), p.pstatus);
+        v.set(ADDRESS, off(VERDICTS, "wait_ms"), p.pwait);
+        v.set(ADDRESS, off(VERDICTS, "rule_idx"), p.prule);
+        p.tickets.clear();
+        p.tickets.addAll(b);
+        try {
+            check((int) SUBMIT_PACKED_ASYNC.invokeExact(engine.handle, pk, v));
+        } catch (Throwable t) {
+            collect();
+            throw t;
         }
+        collect();                                   // batch k-1 back while batch k runs
+        inFlight = p;
+        pcur ^= 1;
         return true;
     }
 

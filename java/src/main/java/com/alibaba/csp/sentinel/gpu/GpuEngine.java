@@ -1,6 +1,5 @@
 package com.alibaba.csp.sentinel.gpu;
 
-import com.alibaba.csp.sentinel.property.DynamicSentinelProperty;
 import com.alibaba.csp.sentinel.property.PropertyListener;
 import com.alibaba.csp.sentinel.property.SentinelProperty;
 import com.alibaba.csp.sentinel.slots.block.RuleConstant;
@@ -16,6 +15,8 @@ import com.alibaba.csp.sentinel.slots.system.SystemRuleManager;
 
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
+import java.lang.invoke.MethodHandles;
+import java.lang.invoke.VarHandle;
 import java.util.ArrayList;
 import java.util.HashMap;
 import java.util.List;
@@ -89,26 +90,56 @@ public final class GpuEngine {
     /**
      * Every FlowRuleManager / ParamFlowRuleManager / SystemRuleManager /
      * DegradeRuleManager.loadRules reaches the engine without a manual
-     * {@link #reloadRules()}: each manager gets a fresh property through its
-     * register2Property (FlowRuleManager.java:92-100, DegradeRuleManager.java:62-70;
-     * loadRules is currentProperty.updateValue, FlowRuleManager.java:120-122), the
-     * manager's own listener first, then ours, so the rule maps are up to date
-     * when the batcher sees the new version.  An application that registers its
-     * own data-source property afterwards adds {@link #ruleListener()} to it too.
+     * {@link #reloadRules()}.  The engine never calls a manager's
+     * register2Property: that would hand the manager a property whose value is
+     * null, and DynamicSentinelProperty.addListener runs configLoad(null) at once
+     * (DynamicSentinelProperty.java:37-40), which replaces the manager's rules by
+     * an empty map (FlowRuleUtil.java:85-88) and detaches whatever data-source
+     * property the application registered before (FlowRuleManager.java:92-100,
+     * NacosDataSourceDemo.java:67).  Instead our listener is added to the
+     * property each manager holds right now (its private static currentProperty;
+     * loadRules is currentProperty.updateValue, FlowRuleManager.java:120-122), and
+     * {@link #followRuleProperties()} re-attaches it whenever the application
+     * later swaps a manager's property (register2Property of a data source), so
+     * both orders -- loadRules / a data source before or after the first
+     * SphU.entry -- keep the manager's live rules and reach the engine.
      */
     private void installRuleListeners() {
-        DynamicSentinelProperty<List<FlowRule>> f = new DynamicSentinelProperty<>();
-        FlowRuleManager.register2Property(f);
-        f.addListener(ruleListener());
-        DynamicSentinelProperty<List<ParamFlowRule>> p = new DynamicSentinelProperty<>();
-        ParamFlowRuleManager.register2Property(p);
-        p.addListener(ruleListener());
-        DynamicSentinelProperty<List<SystemRule>> s = new DynamicSentinelProperty<>();
-        SystemRuleManager.register2Property(s);
-        s.addListener(ruleListener());
-        DynamicSentinelProperty<List<DegradeRule>> d = new DynamicSentinelProperty<>();
-        DegradeRuleManager.register2Property(d);
-        d.addListener(ruleListener());
+        followRuleProperties();
+    }
+
+    /** The four managers' property slots, read reflectively (private static currentProperty). */
+    private static final VarHandle[] PROPERTY_SLOTS = {
+            propertySlot(FlowRuleManager.class), propertySlot(ParamFlowRuleManager.class),
+            propertySlot(SystemRuleManager.class), propertySlot(DegradeRuleManager.class)};
+    private final Object[] followed = new Object[PROPERTY_SLOTS.length];
+    private final PropertyListener<Object> listener = ruleListener();
+
+    private static VarHandle propertySlot(Class<?> manager) {
+        try {
+            return MethodHandles.privateLookupIn(manager, MethodHandles.lookup())
+                    .findStaticVarHandle(manager, "currentProperty", SentinelProperty.class);
+        } catch (ReflectiveOperationException ex) {
+            throw new IllegalStateException("rule manager without currentProperty: " + manager.getName(), ex);
+        }
+    }
+
+    /**
+     * Adds our listener to every manager's current property it is not on yet
+     * (addListener's configLoad only bumps the rule version).  Called at start and
+     * by the flusher before each batch, so a property swapped in by a data source
+     * is followed from the next batch on; the old property keeps our listener,
+     * which is harmless (the manager no longer listens to it).
+     */
+    @SuppressWarnings("unchecked")
+    synchronized void followRuleProperties() {
+        for (int i = 0; i < PROPERTY_SLOTS.length; i++) {
+            Object p = PROPERTY_SLOTS[i].getVolatile();
+            if (p != null && p != followed[i]) {
+                followed[i] = p;
+                ((SentinelProperty<Object>) p).addListener(listener);
+            }
+        }
     }
 
     /** A property listener that bumps the rule version (add it to a data-source property). */

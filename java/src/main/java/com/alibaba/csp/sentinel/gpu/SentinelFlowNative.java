@@ -49,6 +49,10 @@ final class SentinelFlowNative {
     static final MethodHandle SUBMIT = fn("sf_submit", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
     static final MethodHandle SUBMIT_PACKED = fn("sf_submit_packed",
             FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
+    // double-buffered packed batches: enqueue k+1, then wait for k alone
+    static final MethodHandle SUBMIT_PACKED_ASYNC = fn("sf_submit_packed_async",
+            FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
+    static final MethodHandle SYNC_PACKED = fn("sf_sync_packed", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
     // page-locked host memory (the batch arrays: the H2D copy runs at PCIe speed)
     static final MethodHandle HOST_ALLOC = fn("sf_host_alloc",
             FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));

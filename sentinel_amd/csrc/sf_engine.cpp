@@ -130,6 +130,8 @@ struct sf_engine {
         hipEvent_t h2d = nullptr, d2h = nullptr;
         hipEvent_t consumed = nullptr;     // the packed inputs expanded (the next H2D into them may start)
         bool d2h_pending = false, consumed_pending = false;
+        const uint8_t* out_status = nullptr;   // host verdicts of the async batch in flight (sf_sync_packed)
+        int32_t* err_host = nullptr;           // its error flag, copied back with its verdicts (pinned)
     } pk[2];
     hipStream_t h2d = nullptr, d2h = nullptr;
 };
@@ -217,6 +219,7 @@ void sf_destroy(sf_engine* e) {
         if (p.h2d) hipEventDestroy(p.h2d);
         if (p.d2h) hipEventDestroy(p.d2h);
         if (p.consumed) hipEventDestroy(p.consumed);
+        if (p.err_host) hipHostFree(p.err_host);
     }
     if (e->h2d) { hipStreamSynchronize(e->h2d); hipStreamDestroy(e->h2d); }
     if (e->d2h) { hipStreamSynchronize(e->d2h); hipStreamDestroy(e->d2h); }
@@ -1153,6 +1156,8 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
             HIP_TRY(hipEventCreateWithFlags(&p.h2d, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&p.d2h, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&p.consumed, hipEventDisableTiming));
+            HIP_TRY(hipHostMalloc((void**)&p.err_host, 4, hipHostMallocDefault));
+            *p.err_host = 0;
         }
     }
     // (submit_core decides asynchronously only without SystemRules; the slot it takes is e->cur)
@@ -1245,8 +1250,10 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
         HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, d));
         if (out->wait_ms) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait_ms, (size_t)n * 4, hipMemcpyDeviceToHost, d));
         if (out->rule_idx) HIP_TRY(hipMemcpyAsync(out->rule_idx, dv.rule_idx, (size_t)n * 2, hipMemcpyDeviceToHost, d));
+        if (core_async) HIP_TRY(hipMemcpyAsync(pk.err_host, e->w[slot].err, 4, hipMemcpyDeviceToHost, d));
         HIP_TRY(hipEventRecord(pk.d2h, d));
         pk.d2h_pending = true;
+        pk.out_status = core_async ? out->status : nullptr;
         if (!core_async) { HIP_TRY(hipEventSynchronize(pk.d2h)); pk.d2h_pending = false; }
     }
     return SF_OK;
@@ -1257,6 +1264,29 @@ int sf_submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out) 
 }
 int sf_submit_packed_async(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out) {
     return submit_packed(e, in, out, true);
+}
+
+// Wait for ONE asynchronous packed batch: the one whose host verdicts go to
+// out->status (its D2H copy, which follows its decision on the device); the
+// batch submitted after it stays in flight.  Its error flag came back with the
+// verdicts.  A batch already collected (by sf_sync, a rule reload's drain, or
+// an earlier call) has nothing left to wait for: SF_OK.
+int sf_sync_packed(sf_engine* e, const sf_verdicts* out) {
+    if (!e || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    for (int k = 0; k < 2; k++) {
+        auto& pk = e->pk[k];
+        if (!pk.d2h_pending || pk.out_status != out->status) continue;
+        HIP_TRY(hipEventSynchronize(pk.d2h));
+        pk.d2h_pending = false;
+        pk.out_status = nullptr;
+        e->pending &= ~(1u << k);          // checked here, not again by sf_sync
+        const int32_t err = *pk.err_host;
+        if (err) return fail(err, err == SF_ERR_CAPACITY ? "capacity exceeded (param table, or the origin / context node pool: aux_capacity)"
+                                                         : "invalid batch (resource outside shard or bad entry_ref)");
+        return SF_OK;
+    }
+    return SF_OK;
 }
 
 // ---------------------------------------------------------------- node-wide SystemRule rounds

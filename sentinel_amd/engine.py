@@ -65,6 +65,7 @@ def _declare(L):
     f("sf_submit_async", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts))
     f("sf_submit_packed", I, P, C.POINTER(abi.sf_packed_batch), C.POINTER(abi.sf_verdicts))
     f("sf_submit_packed_async", I, P, C.POINTER(abi.sf_packed_batch), C.POINTER(abi.sf_verdicts))
+    f("sf_sync_packed", I, P, C.POINTER(abi.sf_verdicts))
     f("sf_load_namespaces", I, P, C.POINTER(abi.sf_namespace), U32)
     f("sf_load_cluster_rules", I, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
@@ -341,6 +342,12 @@ class FlowEngine:
         previous one and the copy back of the one before.  Arrays stay untouched until sync()."""
         b, v = batch.c_struct(), out.c_struct()
         _check(lib().sf_submit_packed_async(self.h, C.byref(b), C.byref(v)))
+
+    def sync_packed(self, out: abi.HostVerdicts):
+        """sf_sync_packed: waits for the one async packed batch whose verdicts go to `out`
+        (the batch enqueued after it keeps running); raises that batch's error."""
+        v = out.c_struct()
+        _check(lib().sf_sync_packed(self.h, C.byref(v)))
 
     def submit_device(self, batch: DeviceBatch, out: DeviceVerdicts):
         b = batch.c_struct()

@@ -125,3 +125,37 @@ def test_integration_md_quotes_the_sources():
         for line in body.split("\n"):
             if line.strip():
                 assert line.strip() in src, f"INTEGRATION.md line not in {fn}: {line.strip()}"
+
+
+def test_rule_listeners_keep_the_managers_rules():
+    """GpuEngine must not hand a manager an empty property: register2Property
+    moves the manager's listener onto it and DynamicSentinelProperty.addListener
+    runs configLoad(null) at once (DynamicSentinelProperty.java:37-40), which
+    wipes every rule loaded before the first SphU.entry (FlowRuleUtil.java:85-88)
+    and detaches an earlier data source.  The shim attaches its listener to each
+    manager's current property instead, and follows later swaps per batch."""
+    for fn in os.listdir(j.JDIR):
+        src = j.source(fn)
+        for m in re.finditer(r"register2Property\(([^)]*)\)", src):
+            assert False, f"{fn}: register2Property({m.group(1)}) would replace the manager's live rules"
+        assert "new DynamicSentinelProperty<>()" not in src, fn
+    eng = j.source("GpuEngine.java")
+    for mgr in ("FlowRuleManager", "ParamFlowRuleManager", "SystemRuleManager", "DegradeRuleManager"):
+        assert f"propertySlot({mgr}.class)" in eng, mgr
+    assert '"currentProperty"' in eng and ".addListener(listener)" in eng
+    assert "engine.followRuleProperties();" in j.source("EventBatcher.java")
+    readme = open(os.path.join(ROOT, "java", "README.md")).read()
+    assert "register2Property" in readme and "before or after" in readme
+
+
+def test_batcher_double_buffers_packed_batches():
+    """EventBatcher enqueues batch k+1 (sf_submit_packed_async) before it waits
+    for batch k alone (sf_sync_packed); two buffer sets alternate."""
+    src = j.source("EventBatcher.java")
+    fp = src[src.index("private boolean flushPacked"):]
+    assert fp.index("SUBMIT_PACKED_ASYNC.invokeExact") < fp.index("collect();                                   // batch k-1")
+    assert "SYNC_PACKED.invokeExact(engine.handle, f.pverdicts)" in src
+    assert "pbufs[pcur]" in fp and "pcur ^= 1" in fp
+    assert "SUBMIT_PACKED.invokeExact" not in src          # no synchronous packed path left
+    readme = open(os.path.join(ROOT, "java", "README.md")).read()
+    assert "sf_sync_packed" in readme and "latency" in readme.lower()

@@ -42,8 +42,11 @@ def test_packing_roundtrip():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("async_", [False, True])
-def test_gpu_packed_equals_oracle(async_):
+@pytest.mark.parametrize("mode", ["sync", "async", "double"])
+def test_gpu_packed_equals_oracle(mode):
+    """mode double: the Java flusher's double buffering -- batch k+1 enqueued,
+    then sf_sync_packed waits for batch k alone, whose verdicts are checked
+    while k+1 is still in flight."""
     from oracle.oracle import OracleEngine
     from sentinel_amd import engine
     from tests import parity
@@ -60,15 +63,25 @@ def test_gpu_packed_equals_oracle(async_):
             x.load_flow_rules(rules)
         pbs = [abi.PackedBatch(p, alloc=pin.array) for p in parts]
         outs = [pin.verdicts(p.n) for p in parts]
-        if async_:
+        if mode == "async":
             for pb, o in zip(pbs, outs):
                 eng.submit_packed_async(pb, o)
+            eng.sync()
+        elif mode == "double":
+            eng.submit_packed_async(pbs[0], outs[0])
+            for k in range(len(parts)):
+                if k + 1 < len(parts):
+                    eng.submit_packed_async(pbs[k + 1], outs[k + 1])
+                eng.sync_packed(outs[k])
+                parity.compare_verdicts(outs[k], ora.submit(parts[k]), f"batch {k}")
+            eng.sync_packed(outs[-1])              # already collected: a no-op
             eng.sync()
         else:
             for pb, o in zip(pbs, outs):
                 eng.submit_packed(pb, o)
         for k, (p, o) in enumerate(zip(parts, outs)):
-            parity.compare_verdicts(o, ora.submit(p), f"batch {k}")
+            if mode != "double":
+                parity.compare_verdicts(o, ora.submit(p), f"batch {k}")
         per_res = np.bincount(hb.res_id, minlength=R)
         parity.compare_nodes(eng, ora, np.argsort(-per_res)[:40])
         parity.compare_entry_node(eng, ora)
