@@ -788,22 +788,45 @@ def config4_leg(R=1000, n=1 << 24, keys=100_000_000, qps_frac=0.6, reps=3):
            "system_blocks": int((st[0] == abi.V_BLOCK_SYSTEM).sum()),
            "param_blocks": int((st[0] == abi.V_BLOCK_PARAM).sum()),
            "passed": int(np.isin(st[0], abi.PASSED).sum()), "reps_ms": [round(1e3 * w, 3) for w in walls]}
-    log(f"[leg config4] GPU {ms:.1f} ms per batch; oracle replay ...")
+    log(f"[leg config4] GPU {ms:.1f} ms per batch; oracle replays (exact maps, and LRU maps as the reference) ...")
     try:
+        import threading
         from oracle import oracle as so
-        o = so.OracleEngine(cfg)
-        o.load_system_rules(sysr)
-        o.load_param_rules(rules)
-        t = time.perf_counter()
-        want = o.submit(b)
-        dt = time.perf_counter() - t
-        o.close()
+
+        def replay(lru, slot):
+            o = so.OracleEngine(cfg)
+            if lru:
+                o.set_param_lru(True)           # ConcurrentLinkedHashMap capacities (ParameterMetric.java:37-39,99)
+            o.load_system_rules(sysr)
+            o.load_param_rules(rules)
+            t = time.perf_counter()
+            slot["v"] = o.submit(b)
+            slot["dt"] = time.perf_counter() - t
+            slot["lru"] = o.param_lru_stats() if lru else None
+            o.close()
+
+        ex, lr = {}, {}
+        th = [threading.Thread(target=replay, args=(False, ex)), threading.Thread(target=replay, args=(True, lr))]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        want, ref = ex["v"], lr["v"]
         bad = {"status": int((st[0] != want.status).sum()), "wait_ms": int((st[1] != want.wait_ms).sum()),
                "rule_idx": int((st[2] != want.rule_idx).sum())}
-        res["parity"] = {"what": "every verdict vs the one-core oracle replay", "mismatches": bad,
-                         "exact": all(v == 0 for v in bad.values())}
-        res["cpu_baseline"] = {"value": round(ent / dt, 1), "unit": "decisions/s", "cores": 1, "kind": "port",
-                               "sample": "the whole batch, one-core C oracle"}
+        bad_ref = {"status": int((st[0] != ref.status).sum()), "wait_ms": int((st[1] != ref.wait_ms).sum()),
+                   "rule_idx": int((st[2] != ref.rule_idx).sum())}
+        res["parity"] = {"what": "every verdict vs the one-core oracle replay (exact maps, as the engine)",
+                         "mismatches": bad, "exact": all(v == 0 for v in bad.values()),
+                         "lru_divergent_verdicts": int((want.status != ref.status).sum()
+                                                       + ((want.status == ref.status) & ((want.wait_ms != ref.wait_ms)
+                                                                                         | (want.rule_idx != ref.rule_idx))).sum()),
+                         "lru_evictions": lr["lru"][0], "lru_spins": lr["lru"][1],
+                         "vs_lru_reference": {"what": "every verdict vs the oracle with ParameterMetric's maps as the "
+                                                     "reference's LRUs (capacity min(4000*durationInSec, 200000) = 4000)",
+                                              "mismatches": bad_ref, "exact": all(v == 0 for v in bad_ref.values())}}
+        res["cpu_baseline"] = {"value": round(ent / ex["dt"], 1), "unit": "decisions/s", "cores": 1, "kind": "port",
+                               "sample": "the whole batch, one-core C oracle (exact maps)"}
     except Exception as ex:  # pragma: no cover
         res["parity"] = {"error": str(ex)[:200]}
     return res

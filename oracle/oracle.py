@@ -108,6 +108,10 @@ def _declare(L):
     f("so_ctrl_max_token", I32, P)
     f("so_ctrl_slope", D, P)
     f("so_pm_new", P)
+    f("so_pm_new_mode", P, C.c_int)
+    f("so_pm_evictions", U64, P)
+    f("so_set_param_lru", C.c_int, P, C.c_int)
+    f("so_param_lru_stats", C.c_int, P, C.POINTER(U64), C.POINTER(U64))
     f("so_pm_free", None, P)
     f("so_param_pass_single", C.c_int, P, C.c_int, C.POINTER(abi.sf_param_rule), C.POINTER(abi.sf_hot_item),
       I32, U8, U64, C.POINTER(I64))
@@ -369,8 +373,8 @@ class Controller:
 
 
 class ParameterMetric:
-    def __init__(self):
-        self.h = lib().so_pm_new()
+    def __init__(self, lru: bool = False):
+        self.h = lib().so_pm_new_mode(int(lru))
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -395,6 +399,9 @@ class ParameterMetric:
 
     def thread_count(self, idx, value):
         return lib().so_pm_thread_count(self.h, idx, *value)
+
+    def evictions(self):
+        return int(lib().so_pm_evictions(self.h))
 
 
 class ClusterMetric:
@@ -487,6 +494,18 @@ class OracleEngine:
 
     def set_system_status(self, load, cpu):
         lib().so_set_system_status(self.h, load, cpu)
+
+    def set_param_lru(self, on: bool = True):
+        """ParameterMetric's CacheMaps as the reference's ConcurrentLinkedHashMap
+        LRUs (capacity min(4000*durationInSec, 200000); thread maps 4000),
+        instead of the exact maps the engine keeps.  Before the first batch."""
+        lib().so_set_param_lru(self.h, int(on))
+
+    def param_lru_stats(self):
+        """(evictions, evicted-token spins) over every resource's maps."""
+        ev, sp = U64(0), U64(0)
+        lib().so_param_lru_stats(self.h, C.byref(ev), C.byref(sp))
+        return int(ev.value), int(sp.value)
 
     def submit(self, batch: abi.HostBatch) -> abi.HostVerdicts:
         out = abi.HostVerdicts(batch.n)

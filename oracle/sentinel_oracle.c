@@ -15,10 +15,12 @@
  * Thread.yield) are single-threaded no-ops.  Thread.sleep() does not
  * advance the mocked clock; the duration is reported as a wait.
  *
- * Declared divergence: ConcurrentLinkedHashMap (LRU, capacity
- * min(4000*durationInSec, 200000), ParameterMetric.java:37-39,99) is an
- * exact unbounded map here, as in the engine.  Parity holds while distinct
- * keys per rule stay within the reference capacity (SURVEY.md §7 part 6).
+ * ParameterMetric's maps (ConcurrentLinkedHashMap LRUs of capacity
+ * min(4000*durationInSec, 200000), ParameterMetric.java:37-39,99) are exact
+ * unbounded maps by default, as in the engine's exact table; so_set_param_lru
+ * bounds them like the reference (CacheMap section below).  The two agree
+ * while no rule's map sees more distinct keys than its capacity; where they
+ * differ, the LRU mode is the reference's behaviour (SURVEY.md §7 part 6).
  */
 #include "sentinel_oracle.h"
 
@@ -739,79 +741,232 @@ int so_ctrl_can_pass(so_controller* c, so_node* node, const so_mock_node* mock,
 }
 
 /* ======================================================================
+ * CacheMap (PF/slots/statistic/cache/CacheMap.java) — the maps ParameterMetric
+ * keeps per rule and per parameter index.  Two modes:
+ *   exact: an unbounded map, as in the engine (the default);
+ *   LRU:   ConcurrentLinkedHashMapWrapper (ConcurrentLinkedHashMapWrapper.java:
+ *          35-44): com.googlecode.concurrentlinkedhashmap 1.4.2 (not vendored;
+ *          sentinel-parameter-flow-control/pom.xml:26-30) with
+ *          maximumWeightedCapacity(size) and the singleton weigher.  Restated
+ *          from its published algorithm, single-threaded: get / putIfAbsent of
+ *          a present key record a read in the thread's read buffer (afterRead);
+ *          a buffer holding 32 undrained reads is drained, and every write
+ *          (putIfAbsent of an absent key -> AddTask, put of a present key,
+ *          remove -> RemovalTask) drains the read buffer first and then its
+ *          task (drainBuffers: drainReadBuffers, drainWriteBuffer).  A drained
+ *          read moves its node to the back of the eviction deque (applyRead,
+ *          a node no longer in the deque is skipped); AddTask appends the new
+ *          node and evicts from the front while weightedSize > capacity.  Since
+ *          every add drains all pending reads before it evicts, the deque at
+ *          each eviction is ordered by last access (read or insert): the map is
+ *          a strict LRU of `cap` entries, which is what this restates.
+ * ==================================================================== */
+#define SO_NIL 0xffffffffu
+typedef struct {
+    so_map ix;                          /* (tag, bits) -> node index            */
+    uint64_t cap;                       /* maximumWeightedCapacity (entries)    */
+    uint32_t n, pool, head, tail, free_list;   /* head: least recently used     */
+    uint32_t *prev, *next; uint8_t* tag; uint64_t* bits; int64_t* val;
+    uint64_t evictions;
+} so_lru;
+typedef struct { so_map map; so_lru* lru; } so_cmap;   /* lru NULL: exact */
+
+static so_lru* lru_new(uint64_t cap) {
+    so_lru* m = calloc(1, sizeof *m);
+    map_init(&m->ix, 16);
+    m->cap = cap; m->head = m->tail = m->free_list = SO_NIL;
+    return m;
+}
+static void lru_free(so_lru* m) {
+    if (!m) return;
+    map_free(&m->ix);
+    free(m->prev); free(m->next); free(m->tag); free(m->bits); free(m->val); free(m);
+}
+static void lru_unlink(so_lru* m, uint32_t x) {
+    if (m->prev[x] != SO_NIL) m->next[m->prev[x]] = m->next[x]; else m->head = m->next[x];
+    if (m->next[x] != SO_NIL) m->prev[m->next[x]] = m->prev[x]; else m->tail = m->prev[x];
+}
+static void lru_append(so_lru* m, uint32_t x) {
+    m->prev[x] = m->tail; m->next[x] = SO_NIL;
+    if (m->tail != SO_NIL) m->next[m->tail] = x; else m->head = x;
+    m->tail = x;
+}
+static void lru_touch(so_lru* m, uint32_t x) {           /* applyRead: moveToBack */
+    if (m->tail == x) return;
+    lru_unlink(m, x); lru_append(m, x);
+}
+static void lru_drop(so_lru* m, uint32_t x) {            /* remove from map + deque */
+    map_remove(&m->ix, m->tag[x], m->bits[x]);
+    lru_unlink(m, x);
+    m->next[x] = m->free_list; m->free_list = x; m->n--;
+}
+static int64_t* lru_get(so_lru* m, uint8_t tag, uint64_t bits, int touch) {
+    int64_t* x = map_find(&m->ix, tag, bits);
+    if (!x) return NULL;
+    if (touch) lru_touch(m, (uint32_t)*x);
+    return &m->val[*x];
+}
+/* putIfAbsent: the present entry (a read), or NULL after adding `v` (AddTask:
+ * append, then evict from the front while the map holds more than cap). */
+static int64_t* lru_put_if_absent(so_lru* m, uint8_t tag, uint64_t bits, int64_t v) {
+    int64_t* have = lru_get(m, tag, bits, 1);
+    if (have) return have;
+    uint32_t x = m->free_list;
+    if (x != SO_NIL) m->free_list = m->next[x];
+    else {
+        if (m->n == m->pool) {
+            uint32_t np = m->pool ? m->pool * 2 : 64;
+            m->prev = realloc(m->prev, np * 4ull); m->next = realloc(m->next, np * 4ull);
+            m->tag = realloc(m->tag, np); m->bits = realloc(m->bits, np * 8ull); m->val = realloc(m->val, np * 8ull);
+            for (uint32_t k = np; k-- > m->pool;) { m->next[k] = m->free_list; m->free_list = k; }
+            m->pool = np;
+        }
+        x = m->free_list; m->free_list = m->next[x];
+    }
+    m->tag[x] = tag; m->bits[x] = bits; m->val[x] = v; m->n++;
+    map_insert(&m->ix, tag, bits, x);
+    lru_append(m, x);
+    while (m->n > m->cap) { lru_drop(m, m->head); m->evictions++; }   /* evict() */
+    return NULL;
+}
+
+static void cm_init(so_cmap* c, uint64_t lru_cap) {
+    memset(c, 0, sizeof *c);
+    if (lru_cap) c->lru = lru_new(lru_cap); else map_init(&c->map, 16);
+}
+static void cm_free(so_cmap* c) { if (c->lru) lru_free(c->lru); else map_free(&c->map); memset(c, 0, sizeof *c); }
+/* CacheMap.get: an access (afterRead) */
+static int64_t* cm_get(so_cmap* c, uint8_t tag, uint64_t bits) {
+    return c->lru ? lru_get(c->lru, tag, bits, 1) : map_find(&c->map, tag, bits);
+}
+/* a look without an access (state readers for tests) */
+static int64_t* cm_peek(so_cmap* c, uint8_t tag, uint64_t bits) {
+    return c->lru ? lru_get(c->lru, tag, bits, 0) : map_find(&c->map, tag, bits);
+}
+/* CacheMap.putIfAbsent: the present value (an access), or NULL after the insert */
+static int64_t* cm_put_if_absent(so_cmap* c, uint8_t tag, uint64_t bits, int64_t v) {
+    if (c->lru) return lru_put_if_absent(c->lru, tag, bits, v);
+    int64_t* have = map_find(&c->map, tag, bits);
+    if (have) return have;
+    map_insert(&c->map, tag, bits, v);
+    return NULL;
+}
+/* CacheMap.put over a present or absent key: the value set, an access */
+static void cm_put(so_cmap* c, uint8_t tag, uint64_t bits, int64_t v) {
+    int64_t* have = cm_put_if_absent(c, tag, bits, v);
+    if (have) *have = v;
+}
+static void cm_remove(so_cmap* c, uint8_t tag, uint64_t bits) {
+    if (!c->lru) { map_remove(&c->map, tag, bits); return; }
+    int64_t* x = map_find(&c->lru->ix, tag, bits);
+    if (x) lru_drop(c->lru, (uint32_t)*x);
+}
+
+/* ======================================================================
  * ParameterMetric + ParamFlowChecker — PF/slots/block/flow/param/ (all)
  * ==================================================================== */
-typedef struct { int key; int present; so_map map; } rule_map;   /* Map<ParamFlowRule, CacheMap<Object,AtomicLong>> entry */
-typedef struct { int idx; so_map map; } thread_map;              /* Map<Integer, CacheMap<Object,AtomicInteger>> entry */
+typedef struct { int key; int present; so_cmap map; } rule_map;   /* Map<ParamFlowRule, CacheMap<Object,AtomicLong>> entry */
+typedef struct { int idx; so_cmap map; } thread_map;              /* Map<Integer, CacheMap<Object,AtomicInteger>> entry */
 struct so_param_metric {
     rule_map* time_counters; int n_time, cap_time;       /* ruleTimeCounters  ParameterMetric.java:46 */
     rule_map* token_counters; int n_token, cap_token;    /* ruleTokenCounter  :50 */
     thread_map* thread_counts; int n_thread, cap_thread; /* threadCountMap    :54 */
+    int lru;                                             /* CacheMaps are CLHM LRUs (else exact) */
+    uint64_t spins;                                      /* evicted-token spins reached (never, see below) */
 };
-so_param_metric* so_pm_new(void) { return calloc(1, sizeof(so_param_metric)); }
+so_param_metric* so_pm_new_mode(int lru) {
+    so_param_metric* pm = calloc(1, sizeof(so_param_metric));
+    pm->lru = lru;
+    return pm;
+}
+so_param_metric* so_pm_new(void) { return so_pm_new_mode(0); }
 void so_pm_free(so_param_metric* pm) {
     if (!pm) return;
-    for (int i = 0; i < pm->n_time; i++) map_free(&pm->time_counters[i].map);
-    for (int i = 0; i < pm->n_token; i++) map_free(&pm->token_counters[i].map);
-    for (int i = 0; i < pm->n_thread; i++) map_free(&pm->thread_counts[i].map);
+    for (int i = 0; i < pm->n_time; i++) cm_free(&pm->time_counters[i].map);
+    for (int i = 0; i < pm->n_token; i++) cm_free(&pm->token_counters[i].map);
+    for (int i = 0; i < pm->n_thread; i++) cm_free(&pm->thread_counts[i].map);
     free(pm->time_counters); free(pm->token_counters); free(pm->thread_counts); free(pm);
 }
-static so_map* rule_map_get(rule_map* arr, int n, int key) {
+/* LRU evictions so far over all of the metric's maps (LRU mode) */
+uint64_t so_pm_evictions(so_param_metric* pm) {
+    uint64_t n = 0;
+    if (!pm) return 0;
+    for (int i = 0; i < pm->n_time; i++) if (pm->time_counters[i].map.lru) n += pm->time_counters[i].map.lru->evictions;
+    for (int i = 0; i < pm->n_token; i++) if (pm->token_counters[i].map.lru) n += pm->token_counters[i].map.lru->evictions;
+    for (int i = 0; i < pm->n_thread; i++) if (pm->thread_counts[i].map.lru) n += pm->thread_counts[i].map.lru->evictions;
+    return n;
+}
+static so_cmap* rule_map_get(rule_map* arr, int n, int key) {
     for (int i = 0; i < n; i++) if (arr[i].key == key) return &arr[i].map;
     return NULL;
 }
-static so_map* thread_map_get(so_param_metric* pm, int idx) {
+static so_cmap* thread_map_get(so_param_metric* pm, int idx) {
     for (int i = 0; i < pm->n_thread; i++) if (pm->thread_counts[i].idx == idx) return &pm->thread_counts[i].map;
     return NULL;
 }
-/* ParameterMetric.initialize — :99-121 */
+/* ParameterMetric.initialize — :99-121.  LRU capacities: BASE_PARAM_MAX_CAPACITY
+ * (4000) x durationInSec capped at TOTAL_MAX_CAPACITY (200000) for the rule
+ * maps, THREAD_COUNT_MAX_CAPACITY (4000) for the thread maps (:37-39). */
 void so_pm_initialize(so_param_metric* pm, int key, const sf_param_rule* rule) {
-    (void)rule;
+    uint64_t cap = 0, tcap = 0;
+    if (pm->lru) {
+        int64_t c = jmul(4000, rule->duration_in_sec);
+        cap = (uint64_t)(c < 200000 ? c : 200000);
+        tcap = 4000;
+        if (c <= 0) cap = 1;   /* invalid rules never get here (ParamFlowRuleUtil.isValidRule) */
+    }
     if (!rule_map_get(pm->time_counters, pm->n_time, key)) {
         if (pm->n_time == pm->cap_time) { pm->cap_time = pm->cap_time ? pm->cap_time * 2 : 4;
             pm->time_counters = realloc(pm->time_counters, sizeof(rule_map) * pm->cap_time); }
-        rule_map* r = &pm->time_counters[pm->n_time++]; r->key = key; r->present = 1; map_init(&r->map, 16);
+        rule_map* r = &pm->time_counters[pm->n_time++]; r->key = key; r->present = 1; cm_init(&r->map, cap);
     }
     if (!rule_map_get(pm->token_counters, pm->n_token, key)) {
         if (pm->n_token == pm->cap_token) { pm->cap_token = pm->cap_token ? pm->cap_token * 2 : 4;
             pm->token_counters = realloc(pm->token_counters, sizeof(rule_map) * pm->cap_token); }
-        rule_map* r = &pm->token_counters[pm->n_token++]; r->key = key; r->present = 1; map_init(&r->map, 16);
+        rule_map* r = &pm->token_counters[pm->n_token++]; r->key = key; r->present = 1; cm_init(&r->map, cap);
     }
     if (!thread_map_get(pm, rule->param_idx)) {
         if (pm->n_thread == pm->cap_thread) { pm->cap_thread = pm->cap_thread ? pm->cap_thread * 2 : 4;
             pm->thread_counts = realloc(pm->thread_counts, sizeof(thread_map) * pm->cap_thread); }
-        thread_map* t = &pm->thread_counts[pm->n_thread++]; t->idx = rule->param_idx; map_init(&t->map, 16);
+        thread_map* t = &pm->thread_counts[pm->n_thread++]; t->idx = rule->param_idx; cm_init(&t->map, tcap);
     }
 }
 /* addThreadCount / decreaseThreadCount for one (index, value) — :184-239, :125-181 */
 void so_pm_add_thread(so_param_metric* pm, int idx, uint8_t tag, uint64_t bits) {
-    so_map* m = thread_map_get(pm, idx);
+    so_cmap* m = thread_map_get(pm, idx);
     if (!m || tag == SF_TAG_NULL) return;
-    int64_t* v = map_find(m, tag, bits);
-    if (v) (*v) = (int32_t)((uint32_t)*v + 1u);
-    else map_insert(m, tag, bits, 1);
+    int64_t* v = cm_put_if_absent(m, tag, bits, 0);            /* putIfAbsent(new AtomicInteger()) */
+    if (v) (*v) = (int32_t)((uint32_t)*v + 1u);                /* incrementAndGet */
+    else cm_put(m, tag, bits, 1);                              /* put(value, new AtomicInteger(1)) */
 }
 void so_pm_dec_thread(so_param_metric* pm, int idx, uint8_t tag, uint64_t bits) {
-    so_map* m = thread_map_get(pm, idx);
+    so_cmap* m = thread_map_get(pm, idx);
     if (!m || tag == SF_TAG_NULL) return;
-    int64_t* v = map_find(m, tag, bits);
-    if (!v) { map_insert(m, tag, bits, 0); return; }      /* putIfAbsent(new AtomicInteger()) */
-    int32_t cur = (int32_t)((uint32_t)*v - 1u);
+    int64_t* v = cm_put_if_absent(m, tag, bits, 0);            /* putIfAbsent(new AtomicInteger()) */
+    if (!v) return;
+    int32_t cur = (int32_t)((uint32_t)*v - 1u);                /* decrementAndGet */
     *v = cur;
-    if (cur <= 0) map_remove(m, tag, bits);
+    if (cur <= 0) cm_remove(m, tag, bits);
 }
-int64_t so_pm_thread_count(so_param_metric* pm, int idx, uint8_t tag, uint64_t bits) { /* :242-250 */
-    so_map* m = thread_map_get(pm, idx);
+/* getThreadCount — :242-250 (cacheMap.get: an access) */
+int64_t so_pm_thread_count(so_param_metric* pm, int idx, uint8_t tag, uint64_t bits) {
+    so_cmap* m = thread_map_get(pm, idx);
     if (!m) return 0;
-    int64_t* v = map_find(m, tag, bits);
+    int64_t* v = cm_get(m, tag, bits);
+    return v ? *v : 0;
+}
+int64_t so_pm_thread_peek(so_param_metric* pm, int idx, uint8_t tag, uint64_t bits) {
+    so_cmap* m = thread_map_get(pm, idx);
+    if (!m) return 0;
+    int64_t* v = cm_peek(m, tag, bits);
     return v ? *v : 0;
 }
 int so_pm_read(so_param_metric* pm, int key, uint8_t tag, uint64_t bits,
                int64_t* time_value, int64_t* tokens, int* has_tokens) {
-    so_map* tm = rule_map_get(pm->time_counters, pm->n_time, key);
-    so_map* km = rule_map_get(pm->token_counters, pm->n_token, key);
-    int64_t* t = tm ? map_find(tm, tag, bits) : NULL;
-    int64_t* k = km ? map_find(km, tag, bits) : NULL;
+    so_cmap* tm = rule_map_get(pm->time_counters, pm->n_time, key);
+    so_cmap* km = rule_map_get(pm->token_counters, pm->n_token, key);
+    int64_t* t = tm ? cm_peek(tm, tag, bits) : NULL;
+    int64_t* k = km ? cm_peek(km, tag, bits) : NULL;
     *time_value = t ? *t : 0; *tokens = k ? *k : 0; *has_tokens = k != NULL;
     return t != NULL;
 }
@@ -824,11 +979,12 @@ static const sf_hot_item* hot_item(const sf_param_rule* rule, const sf_hot_item*
     return NULL;
 }
 
-/* ParamFlowChecker.passDefaultLocalCheck — ParamFlowChecker.java:139-219 */
+/* ParamFlowChecker.passDefaultLocalCheck — ParamFlowChecker.java:139-219.
+ * The map operations are the reference's, in its order (each an LRU access). */
 static int pass_default_local(so_param_metric* pm, int key, const sf_param_rule* rule,
                               const sf_hot_item* items, int32_t acquire, uint8_t tag, uint64_t bits) {
-    so_map* token_counters = rule_map_get(pm->token_counters, pm->n_token, key);
-    so_map* time_counters = rule_map_get(pm->time_counters, pm->n_time, key);
+    so_cmap* token_counters = rule_map_get(pm->token_counters, pm->n_token, key);
+    so_cmap* time_counters = rule_map_get(pm->time_counters, pm->n_time, key);
     if (!token_counters || !time_counters) return 1;
     int64_t token_count = so_java_d2l(rule->count);
     const sf_hot_item* hi = tag == SF_TAG_NULL ? NULL : hot_item(rule, items, tag, bits);   /* no null hot item */
@@ -837,48 +993,48 @@ static int pass_default_local(so_param_metric* pm, int key, const sf_param_rule*
     int64_t max_count = jadd(token_count, rule->burst_count);
     if (acquire > max_count) return 0;
     if (tag == SF_TAG_NULL) return 2;       /* timeCounters.putIfAbsent(null): NullPointerException */
-    for (;;) {
-        int64_t current_time = g_now;
-        int64_t* last_add = map_find(time_counters, tag, bits);
-        if (!last_add) {                                            /* :165-169 */
-            map_insert(time_counters, tag, bits, current_time);
-            if (!map_find(token_counters, tag, bits)) map_insert(token_counters, tag, bits, max_count - acquire);
-            return 1;
-        }
-        int64_t pass_time = current_time - *last_add;
-        if (pass_time > jmul(rule->duration_in_sec, 1000)) {        /* :173-195 */
-            int64_t* old_qps = map_find(token_counters, tag, bits);
-            if (!old_qps) {
-                map_insert(token_counters, tag, bits, max_count - acquire);
-                *map_find(time_counters, tag, bits) = current_time;
-                return 1;
-            }
-            int64_t rest = *old_qps;
-            int64_t to_add = jdiv(jmul(pass_time, token_count), jmul(rule->duration_in_sec, 1000));
-            int64_t new_qps = jadd(to_add, rest) > max_count ? (max_count - acquire)
-                                                              : jsub(jadd(rest, to_add), acquire);
-            if (new_qps < 0) return 0;
-            *old_qps = new_qps;                                     /* CAS succeeds */
-            *map_find(time_counters, tag, bits) = current_time;
-            return 1;
-        } else {                                                    /* :196-215 */
-            int64_t* old_qps = map_find(token_counters, tag, bits);
-            if (old_qps) {
-                int64_t v = *old_qps;
-                if (v - acquire >= 0) { *old_qps = v - acquire; return 1; }
-                return 0;
-            }
-            /* token entry evicted while time entry present: the reference spins
-             * until the duration elapses (:204-217).  Unreachable with exact maps. */
-            return 0;
-        }
+    int64_t current_time = g_now;
+    int64_t* last_add = cm_put_if_absent(time_counters, tag, bits, current_time);   /* :165 */
+    if (!last_add) {                                                                 /* :166-169 */
+        cm_put_if_absent(token_counters, tag, bits, max_count - acquire);
+        return 1;
     }
+    int64_t pass_time = current_time - *last_add;
+    if (pass_time > jmul(rule->duration_in_sec, 1000)) {                              /* :173-195 */
+        int64_t* old_qps = cm_put_if_absent(token_counters, tag, bits, max_count - acquire);
+        if (!old_qps) {
+            *last_add = current_time;
+            return 1;
+        }
+        int64_t rest = *old_qps;
+        int64_t to_add = jdiv(jmul(pass_time, token_count), jmul(rule->duration_in_sec, 1000));
+        int64_t new_qps = jadd(to_add, rest) > max_count ? (max_count - acquire)
+                                                          : jsub(jadd(rest, to_add), acquire);
+        if (new_qps < 0) return 0;
+        *old_qps = new_qps;                                     /* CAS succeeds */
+        *last_add = current_time;
+        return 1;
+    }
+    int64_t* old_qps = cm_get(token_counters, tag, bits);                             /* :196-215 */
+    if (old_qps) {
+        int64_t v = *old_qps;
+        if (v - acquire >= 0) { *old_qps = v - acquire; return 1; }
+        return 0;
+    }
+    /* Time entry present, token entry absent: the reference yields and loops
+     * (:204-217) until a later clock passes the duration -- under the mocked
+     * clock, forever.  Single-threaded it is unreachable even in LRU mode: the
+     * two maps of a rule have one capacity and see the same operations in the
+     * same order (putIfAbsent / get of the same key, every call above), so they
+     * hold the same keys at all times.  Recorded, and answered as a block. */
+    pm->spins++;
+    return 0;
 }
 /* ParamFlowChecker.passThrottleLocalCheck — :222-273 */
 static int pass_throttle_local(so_param_metric* pm, int key, const sf_param_rule* rule,
                                const sf_hot_item* items, int32_t acquire, uint8_t tag, uint64_t bits,
                                int64_t* wait_ms) {
-    so_map* time_recorder = rule_map_get(pm->time_counters, pm->n_time, key);
+    so_cmap* time_recorder = rule_map_get(pm->time_counters, pm->n_time, key);
     if (!time_recorder) return 1;
     int64_t token_count = so_java_d2l(rule->count);
     const sf_hot_item* hi = tag == SF_TAG_NULL ? NULL : hot_item(rule, items, tag, bits);
@@ -887,11 +1043,12 @@ static int pass_throttle_local(so_param_metric* pm, int key, const sf_param_rule
     if (tag == SF_TAG_NULL) return 2;       /* timeRecorderMap.putIfAbsent(null): NullPointerException */
     int64_t cost = so_java_round(1.0 * 1000 * acquire * (double)rule->duration_in_sec / (double)token_count);
     int64_t current_time = g_now;
-    int64_t* rec = map_find(time_recorder, tag, bits);
-    if (!rec) { map_insert(time_recorder, tag, bits, current_time); return 1; }
+    int64_t* rec = cm_put_if_absent(time_recorder, tag, bits, current_time);
+    if (!rec) return 1;
     int64_t last_pass = *rec;
     int64_t expected = last_pass + cost;
     if (expected <= current_time || expected - current_time < rule->max_queueing_time_ms) {
+        rec = cm_get(time_recorder, tag, bits);                 /* timeRecorderMap.get(value) :255 */
         *rec = current_time;
         int64_t wait = expected - current_time;
         if (wait > 0) { *rec = expected; *wait_ms = wait; }
@@ -1091,7 +1248,19 @@ struct so_engine {
     cluster_rt* cl; uint32_t n_cl;
     sf_hot_item* cl_items; uint32_t n_cl_items;
     ns_rt* ns; uint32_t n_ns;
+    int param_lru;                    /* so_set_param_lru: ParameterMetric CacheMaps as CLHM LRUs */
 };
+
+/* ParameterMetric's CacheMaps bounded like the reference's (exact by default).
+ * Takes effect for the metrics created afterwards: call before the first batch. */
+int so_set_param_lru(so_engine* e, int on) { e->param_lru = on != 0; return 0; }
+int so_param_lru_stats(so_engine* e, uint64_t* evictions, uint64_t* spins) {
+    uint64_t ev = 0, sp = 0;
+    for (uint32_t r = 0; r < e->n_res; r++)
+        if (e->res[r].pm) { ev += so_pm_evictions(e->res[r].pm); sp += e->res[r].pm->spins; }
+    *evictions = ev; *spins = sp;
+    return 0;
+}
 
 static void apply_statics(const sf_config* cfg) {
     g_sample_count = cfg->sample_count; g_interval = cfg->interval_ms;
@@ -1554,7 +1723,7 @@ int so_submit(so_engine* e, const sf_event_batch* in, sf_verdicts* out) {
         }
         /* ParamFlowSlot.checkFlow :82-103 (args never null from SphU.entry) */
         if (!blocked && rr->n_param > 0) {
-            if (!rr->pm) rr->pm = so_pm_new();
+            if (!rr->pm) rr->pm = so_pm_new_mode(e->param_lru);
             for (int k = 0; k < rr->n_param && !blocked; k++) {
                 sf_param_rule* pr = &e->param[rr->param_rules[k]].rule;
                 /* applyRealParamIdx :56-66 (mutates the rule) */
@@ -1730,7 +1899,7 @@ int32_t so_param_rule_idx(so_engine* e, uint32_t pidx) {
 int64_t so_param_thread(so_engine* e, uint32_t res, int idx, uint8_t tag, uint64_t bits) {
     uint32_t l;
     if (!local_id(e, res, &l) || !e->res[l].pm) return 0;
-    return so_pm_thread_count(e->res[l].pm, idx, tag, bits);
+    return so_pm_thread_peek(e->res[l].pm, idx, tag, bits);
 }
 /* StatisticNode.metrics() :120-137 of one node: rows appended at out[*k] */
 static void node_metrics(so_node* n, int64_t now, uint32_t resource, sf_metric_row* out, uint32_t cap, uint32_t* k) {

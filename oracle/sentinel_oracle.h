@@ -142,6 +142,9 @@ double  so_ctrl_slope(const so_controller* c);
 /* ---- ParamFlowChecker (object level) ---- */
 typedef struct so_param_metric so_param_metric;      /* ParameterMetric */
 so_param_metric* so_pm_new(void);
+so_param_metric* so_pm_new_mode(int lru);   /* lru: CacheMaps as ConcurrentLinkedHashMap LRUs */
+uint64_t so_pm_evictions(so_param_metric* pm);
+int64_t so_pm_thread_peek(so_param_metric* pm, int param_idx, uint8_t tag, uint64_t bits);
 void so_pm_free(so_param_metric* pm);
 /* passSingleValueCheck(rule, acquireCount, value); rule_key identifies the
  * rule's counter maps inside pm (ParameterMetric maps keyed by rule).      */
@@ -183,6 +186,8 @@ void    so_rl_add(so_request_limiter* l, int32_t x);
 /* ---- replay engine: same ABI shapes as the product (host memory only) ---- */
 typedef struct so_engine so_engine;
 so_engine* so_create(const sf_config* cfg);
+int  so_set_param_lru(so_engine* e, int on);
+int  so_param_lru_stats(so_engine* e, uint64_t* evictions, uint64_t* spins);
 void so_destroy(so_engine* e);
 int  so_load_flow_rules(so_engine* e, const sf_flow_rule* rules, uint32_t n);
 int  so_load_param_rules(so_engine* e, const sf_param_rule* rules, uint32_t n,
