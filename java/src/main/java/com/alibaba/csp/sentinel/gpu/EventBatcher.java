@@ -183,7 +183,7 @@ final class EventBatcher implements Runnable {
         int n = b.size(), ne = 0;
         if (flushPacked(b, bs)) return;
         collect();                                           // the SoA path is synchronous
-        boolean anyExit = false;
+        boolean anyExit = false, anyOrigin = false;
         elemOff.set(JAVA_INT, 0, 0);
         for (int i = 0; i < n; i++) {
             Ticket t = b.get(i);
@@ -194,6 +194,7 @@ final class EventBatcher implements Runnable {
             cnt.setAtIndex(JAVA_INT, i, t.count);
             flags.setAtIndex(JAVA_BYTE, i, t.flags);
             origin.setAtIndex(JAVA_INT, i, t.origin);
+            anyOrigin |= t.origin != -1;
             context.setAtIndex(JAVA_INT, i, t.context);
             if ((t.flags & EV_EXIT) != 0) {
                 anyExit = true;
@@ -246,7 +247,7 @@ final class EventBatcher implements Runnable {
         batch.set(ADDRESS, off(EVENT_BATCH, "elem_tag"), elemTag);
         batch.set(ADDRESS, off(EVENT_BATCH, "elem_bits"), elemBits);
         batch.set(JAVA_INT, off(EVENT_BATCH, "n_elems"), ne);
-        batch.set(ADDRESS, off(EVENT_BATCH, "origin"), origin);
+        batch.set(ADDRESS, off(EVENT_BATCH, "origin"), anyOrigin ? origin : MemorySegment.NULL);
         batch.set(ADDRESS, off(EVENT_BATCH, "context"), context);
         verdicts.set(JAVA_INT, off(VERDICTS, "mem"), SF_MEM_HOST_);
         verdicts.set(ADDRESS, off(VERDICTS, "status"), status);
@@ -272,6 +273,7 @@ final class EventBatcher implements Runnable {
         if (last - t0 >= (1L << 20)) return false;
         final PackedBuf p = pbufs[pcur];             // not the in-flight set: sets alternate
         int nx = 0, nc = 0;
+        boolean anyOrigin = false;
         for (int i = 0; i < n; i++) {
             Ticket t = b.get(i);
             t.batchSeq = bs; t.batchIndex = i;
@@ -282,6 +284,7 @@ final class EventBatcher implements Runnable {
             p.pev.setAtIndex(JAVA_LONG, i, (t.resource & 0xffffffffL) | ((lastTs - t0) << 32)
                     | (c << PK_COUNT_SHIFT) | (f << PK_FLAGS_SHIFT));
             p.porigin.setAtIndex(JAVA_INT, i, t.origin);
+            anyOrigin |= t.origin != -1;
             if ((t.flags & EV_EXIT) != 0) {
                 boolean same = t.entry != null && t.entry.batchSeq == bs;
                 p.pxref.setAtIndex(JAVA_LONG, nx, same ? t.entry.batchIndex : -1L);
@@ -297,7 +300,8 @@ final class EventBatcher implements Runnable {
         pk.set(ADDRESS, off(PACKED_BATCH, "exit_ref"), nx > 0 ? p.pxref : MemorySegment.NULL);
         pk.set(ADDRESS, off(PACKED_BATCH, "exit_cts"), nx > 0 ? p.pxcts : MemorySegment.NULL);
         pk.set(ADDRESS, off(PACKED_BATCH, "count_ext"), nc > 0 ? p.pcext : MemorySegment.NULL);
-        pk.set(ADDRESS, off(PACKED_BATCH, "origin"), p.porigin);
+        // no origin at all: NULL, so the engine runs no origin-node pass for the batch
+        pk.set(ADDRESS, off(PACKED_BATCH, "origin"), anyOrigin ? p.porigin : MemorySegment.NULL);
         pk.set(JAVA_INT, off(PACKED_BATCH, "n_exit"), nx);
         pk.set(JAVA_INT, off(PACKED_BATCH, "n_count_ext"), nc);
         MemorySegment v = p.pverdicts;

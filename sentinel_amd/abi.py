@@ -259,7 +259,9 @@ class PackedBatch:
         self.n = n
         self.ts_base = int(hb.ts_ms[0]) if n else 0
         d = (hb.ts_ms - self.ts_base).astype(np.int64)
-        assert n == 0 or (d.min() >= 0 and d.max() < (1 << 20)), "batch spans more than 2^20 ms"
+        if n and (d.min() < 0 or d.max() >= (1 << 20)):
+            # the 20-bit delta would spill into the acquireCount bits (sf_packed_batch)
+            raise ValueError("a packed batch must be time-ordered and span less than 2^20 ms")
         c = hb.count.astype(np.int64)
         small = (c >= 1) & (c <= 127)
         w = hb.res_id.astype(np.uint64) | (d.astype(np.uint64) << np.uint64(32)) | \

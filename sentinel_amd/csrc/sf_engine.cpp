@@ -134,6 +134,7 @@ struct sf_engine {
         int32_t* err_host = nullptr;           // its error flag, copied back with its verdicts (pinned)
     } pk[2];
     hipStream_t h2d = nullptr, d2h = nullptr;
+    int32_t* rh_err = nullptr;            // rehash_table's overflow flag
 };
 
 static void free_tok_work(TokWork& w) {
@@ -209,7 +210,7 @@ void sf_destroy(sf_engine* e) {
     for (void* p : sptrs) if (p) hipFree(p);
     void* dptrs[] = {(void*)e->dg.rr_of, (void*)e->dg.off, (void*)e->dg.rules, e->dg.state, e->dgw.keys_in,
                      e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
-                     e->dgw.err, e->dg_stage, e->dgw.heavy, e->dgw.n_heavy, e->dgw.sev, e->dgw.inv};
+                     e->dgw.err, e->rh_err, e->dg_stage, e->dgw.heavy, e->dgw.n_heavy, e->dgw.sev, e->dgw.inv};
     for (void* p : dptrs) if (p) hipFree(p);
     void* xptrs[] = {e->xmap_buf, e->xw_buf, e->st.xtab, e->ax_dir, e->st.ax_count};
     for (void* p : xptrs) if (p) hipFree(p);
@@ -503,6 +504,29 @@ static int pool_grow(sf_engine* e, uint64_t need) {
     return SF_OK;
 }
 
+// Rebuild an open-addressed table (origin index or ParamFlow table) into a new
+// one of at least `ncap` slots; a key that would land farther than
+// PT_MAX_PROBE from its home slot makes k_ox_rehash raise its flag, and the
+// rebuild is retried at twice the size (nothing in flight).
+static int rehash_table(sf_engine* e, const ParamSlot* old, uint64_t old_n, uint64_t ncap,
+                        ParamSlot** out, uint64_t* out_cap, const char* what) {
+    if (!e->rh_err) HIP_TRY(hipMalloc((void**)&e->rh_err, sizeof(int32_t)));
+    for (;;) {
+        ParamSlot* nt = nullptr;
+        HIP_TRY(hipMalloc((void**)&nt, ncap * sizeof(ParamSlot)));
+        HIP_TRY(hipMemsetAsync(nt, 0, ncap * sizeof(ParamSlot), e->stream));
+        HIP_TRY(hipMemsetAsync(e->rh_err, 0, sizeof(int32_t), e->stream));
+        const hipError_t le = launch_ox_rehash(old, old_n, nt, ncap - 1, e->rh_err, e->stream);
+        if (le != hipSuccess) { hipFree(nt); return fail(SF_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(le)); }
+        int32_t flag = 0;
+        HIP_TRY(hipMemcpyAsync(&flag, e->rh_err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        if (!flag) { *out = nt; *out_cap = ncap; return SF_OK; }
+        HIP_TRY(hipFree(nt));
+        ncap *= 2;
+    }
+}
+
 static int ensure_aux(sf_engine* e) {
     DevState& st = e->st;
     if (st.xtab) return SF_OK;
@@ -527,11 +551,7 @@ static int index_grow(sf_engine* e, uint64_t need) {
     while (tcap < 2 * need) tcap <<= 1;
     ParamSlot* nt = nullptr;
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMalloc((void**)&nt, tcap * sizeof(ParamSlot)));
-    HIP_TRY(hipMemsetAsync(nt, 0, tcap * sizeof(ParamSlot), e->stream));
-    const hipError_t le = launch_ox_rehash(st.xtab, st.xcap_mask + 1, nt, tcap - 1, st.err, e->stream);
-    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("index rehash: ") + hipGetErrorString(le));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    { const int rc = rehash_table(e, st.xtab, st.xcap_mask + 1, tcap, &nt, &tcap, "index rehash"); if (rc) return rc; }
     HIP_TRY(hipFree(st.xtab));
     st.xtab = nt;
     st.xcap_mask = tcap - 1;
@@ -566,7 +586,9 @@ static int ox_maps(sf_engine* e, Work& w, bool reset, hipStream_t ss) {
 // keeps running).  Fills `plan` for the origin-node pass of the decide phase.
 static int ox_prologue(sf_engine* e, Work& w, const DevBatch& b, hipStream_t ss) {
     { const int rc = ensure_aux(e); if (rc) return rc; }
-    { const int rc = ox_maps(e, w, false, ss); if (rc) return rc; }
+    // a batch that stopped between its index pass and its origin apply (an
+    // early error return) left its heavy ids in ox_hmap: reset them
+    { const int rc = ox_maps(e, w, w.ox_dirty, ss); if (rc) return rc; }
     if (b.origin && !w.ox_pairs) {                 // (at most one pair per event)
         HIP_TRY(hipMalloc((void**)&w.ox_pairs, (size_t)e->cfg.max_batch * sizeof(uint4)));
         HIP_TRY(hipMalloc((void**)&w.ox_plist, (size_t)e->cfg.max_batch * sizeof(uint32_t)));
@@ -581,6 +603,7 @@ static int ox_launch_index(sf_engine* e, Work& w, const DevBatch& b, hipStream_t
     const uint32_t lim = (uint32_t)std::min<uint64_t>(xcap * 7 / 10, 0xffffff00u);
     DevBatch bi = b;
     if (!w.s_origin || !b.origin) bi.origin = nullptr;
+    w.ox_dirty = true;
     const hipError_t le = launch_ox_index(stl, w, bi, lim, ss);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("origin index: ") + hipGetErrorString(le));
     return SF_OK;
@@ -833,12 +856,32 @@ static int param_reserve(sf_engine* e, uint64_t bound) {
     if (!e->n_prule || !bound) return SF_OK;
     const uint64_t cap = e->st.pcap_mask + 1;
     if ((e->p_used + e->p_pending + bound) * 2 <= cap) { e->p_pending += bound; return SF_OK; }
+    auto read_used = [&](uint64_t* used) -> int {
+        std::vector<unsigned int> c(256 * 16);
+        HIP_TRY(hipMemcpy(c.data(), e->st.pins, c.size() * sizeof(unsigned int), hipMemcpyDeviceToHost));
+        uint64_t u = 0;
+        for (int k = 0; k < 256; k++) u += c[k * 16];
+        *used = u;
+        return SF_OK;
+    };
+    // The batches counted in p_pending may have finished already: when every
+    // enqueued decide phase is done (a non-blocking event query), the device
+    // counters give the exact fill without a drain, and the pending worst-case
+    // bounds are released (they only ever grew before).
+    bool idle = true;
+    for (int k = 0; k < 2 && idle; k++)
+        if (e->used[k] && hipEventQuery(e->ev_done[k]) != hipSuccess) idle = false;
+    if (idle) {
+        uint64_t used = 0;
+        { const int rc = read_used(&used); if (rc) return rc; }
+        e->p_used = used;
+        e->p_pending = 0;
+        if ((used + bound) * 2 <= cap) { e->p_pending = bound; return SF_OK; }
+    }
     { const int rc = drain(e); if (rc) return rc; }
     HIP_TRY(hipStreamSynchronize(e->stream));
-    std::vector<unsigned int> c(256 * 16);
-    HIP_TRY(hipMemcpy(c.data(), e->st.pins, c.size() * sizeof(unsigned int), hipMemcpyDeviceToHost));
     uint64_t used = 0;
-    for (int k = 0; k < 256; k++) used += c[k * 16];
+    { const int rc = read_used(&used); if (rc) return rc; }
     e->p_used = used;
     e->p_pending = 0;
     if ((used + bound) * 2 > cap) {
@@ -846,11 +889,7 @@ static int param_reserve(sf_engine* e, uint64_t bound) {
         while ((used + bound) * 2 > ncap) ncap <<= 1;
         ParamSlot* nt = nullptr;
         HIP_TRY(hipDeviceSynchronize());
-        HIP_TRY(hipMalloc((void**)&nt, ncap * sizeof(ParamSlot)));
-        HIP_TRY(hipMemsetAsync(nt, 0, ncap * sizeof(ParamSlot), e->stream));
-        const hipError_t le = launch_ox_rehash(e->st.ptab, cap, nt, ncap - 1, e->st.err, e->stream);
-        if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("param rehash: ") + hipGetErrorString(le));
-        HIP_TRY(hipStreamSynchronize(e->stream));
+        { const int rc = rehash_table(e, e->st.ptab, cap, ncap, &nt, &ncap, "param rehash"); if (rc) return rc; }
         HIP_TRY(hipFree(e->st.ptab));
         e->st.ptab = nt;
         e->st.pcap_mask = ncap - 1;
@@ -1039,6 +1078,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
                 le = launch_decide(stl, w, v, dvv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3,
                                    e->serial ? s : e->stream4,
                                    e->evs[slot], false, with_ox ? &plan : nullptr);
+            if (le == hipSuccess && with_ox) w.ox_dirty = false;     // k_ox_reset enqueued
             if (le == hipSuccess) le = launch_entry_node(stl, v, dvv.status, e->en, e->en_acc, s);
             if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
             p = q;
@@ -1088,6 +1128,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
                        e->serial ? s : e->stream4, e->evs[slot], e->timing,
                        with_ox ? &plan : nullptr);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
+    if (with_ox) w.ox_dirty = false;                                  // k_ox_reset enqueued
     // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream
     // order); under the round protocol the node-wide stream updates it (sf_entry_node_add)
     if (!forced) {

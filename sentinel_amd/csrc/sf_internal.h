@@ -188,6 +188,7 @@ struct Work {
     PackedEv* pv_in; PackedEv* pv_out;           // sort payload
     uint32_t* wide;                              // batch times exceed 32-bit offsets (k_unpack reads the batch)
     int32_t* err;                                // batch error flag (this Work set's batch)
+    bool ox_dirty;                               // index pass ran, origin apply (k_ox_reset) not enqueued
     uint32_t* head;      uint32_t* head_scan;    // segment flags and positions
     uint32_t* seg_start; uint32_t* seg_res; uint32_t* n_seg;
     int64_t* s_ts; int32_t* s_cnt; uint8_t* s_flags;

@@ -835,7 +835,10 @@ __global__ void k_ox_rehash(const ParamSlot* old_tab, uint64_t old_n, ParamSlot*
     const ParamSlot s = old_tab[k];
     if (s.hi == 0) return;
     uint64_t i = ParamTable::hash(s.hi, s.lo) & mask;
-    for (uint64_t p = 0; p <= mask; p++) {
+    // a key is never placed farther than PT_MAX_PROBE from its home slot (the
+    // probes of find / insert stop there): past it the host grows the table again
+    const uint64_t reach = mask < PT_MAX_PROBE ? mask : PT_MAX_PROBE;
+    for (uint64_t p = 0; p <= reach; p++) {
         unsigned long long expected = 0;
         if (__hip_atomic_compare_exchange_strong((unsigned long long*)&tab[i].hi, &expected, (unsigned long long)s.hi,
                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {

@@ -89,3 +89,12 @@ def test_gpu_packed_equals_oracle(mode):
         pin.free()
         eng.close()
         ora.close()
+
+
+def test_packing_refuses_a_long_span():
+    """The ts delta has 20 bits: a longer batch is refused (ValueError, also under python -O)."""
+    hb, _ = _batch(n=1000)
+    ts = hb.ts_ms.copy()
+    ts[-1] = ts[0] + (1 << 20)
+    with pytest.raises(ValueError):
+        abi.PackedBatch(abi.HostBatch(hb.res_id, ts, hb.count, hb.flags, entry_ref=hb.entry_ref))
