@@ -23,6 +23,7 @@
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
+#include "sf_rsort.h"
 #include "sf_stream.h"
 #include "sf_system.h"
 #include "sf_xflow.h"
@@ -148,6 +149,45 @@ __global__ void k_unpack(DevBatch b, const void* pvv, const uint32_t* keys, uint
                                                                   : b.abits[(size_t)a * b.arg_stride + i];
         }
     }
+}
+
+// After the hand-written sort (sf_rsort.h), whose last pass wrote the sorted
+// SoA: the segment table (segment id of sorted event j = inclusive count of
+// segment heads up to j, minus one: start, resource, count), the engine clock,
+// and the per-segment flags k_classify routes by.
+__global__ void k_segs(DevBatch b, const int32_t* s_cnt, const uint8_t* s_flags, const uint8_t* s_atag,
+                       const uint32_t* keys, const uint32_t* head_scan, uint32_t* seg_start, uint32_t* seg_res,
+                       uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts, const int32_t* err, bool exit_marks) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= b.n) return;
+    const uint32_t sid = head_scan[j] - 1;
+    if (j == 0 || head_scan[j - 1] != head_scan[j]) { seg_start[sid] = j; seg_res[sid] = keys[j]; }
+    if (j == b.n - 1) { *n_seg = sid + 1; seg_start[sid + 1] = b.n; }
+    if (j == 0 && *err == 0) *last_ts = b.ts[b.n - 1];   // the sort's first pass has read the old value
+    const uint8_t f = s_flags[j];
+    const int32_t c = s_cnt[j];
+    uint32_t mine = 0;
+    if (exit_marks && (f & SF_EV_EXIT)) mine |= SEGF_EXIT;
+    if (!(f & SF_EV_EXIT))
+        mine |= ((f & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (c <= 0 ? SEGF_NONPOS : 0u) | ((f & EVF_SYSBLK) ? SEGF_SYS : 0u);
+    for (uint32_t a = 0; a < b.arg_slots; a++)
+        if (s_atag[(size_t)a * b.n + j] == SF_TAG_COLLECTION) mine |= SEGF_COLL;
+    // OR-ed per segment within the wavefront, one atomic per segment and wavefront
+    const unsigned long long any = __ballot(mine != 0);
+    if (!any) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int psid = __shfl_up((int)sid, 1);
+    const unsigned long long heads = __ballot(lane == 0 || (uint32_t)psid != sid);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const unsigned long long after = heads & ~(below | (1ull << lane));
+    const int nxt = after ? __ffsll((long long)after) - 1 : 64;
+    const unsigned long long range = (nxt == 64 ? ~0ull : (1ull << nxt) - 1ull) & ~below;
+    uint32_t acc = 0;
+    const uint32_t kinds[5] = {SEGF_EXIT, SEGF_PRIO, SEGF_NONPOS, SEGF_SYS, SEGF_COLL};
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        if (__ballot(mine & kinds[k]) & range) acc |= kinds[k];
+    if (((heads >> lane) & 1ull) && acc) atomicOr(&segflag[sid], acc);
 }
 
 struct HeadFlag {       // 1 where a new resource segment starts in the sorted keys
@@ -1835,6 +1875,7 @@ hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_byte
                                   (PackedEvO*)nullptr, (PackedEvO*)nullptr, max_n, 0u, key_bits);
     if (e != hipSuccess) return e;
     if (packed_bytes > *sort_bytes) *sort_bytes = packed_bytes;
+    if (rs_scratch_bytes() > *sort_bytes) *sort_bytes = rs_scratch_bytes();
     HeadIter hit(rocprim::counting_iterator<uint32_t>(0), HeadFlag{nullptr});
     e = rocprim::inclusive_scan<HeadScanCfg>(nullptr, *scan_bytes, hit, (uint32_t*)nullptr, (size_t)max_n,
                                 rocprim::plus<uint32_t>());
@@ -1885,7 +1926,22 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     if (timing) hipEventRecord(ev[0], s);
     hipError_t e;
     const bool org = b.origin != nullptr;                       // the origin rides in a 12-B payload
-    if (org) {
+    // the hand-written chunked LSD sort (sf_rsort.h); SF_SORT_ROCPRIM=1: k_keys_packed + rocprim onesweep (A/B)
+    static const bool use_rocprim = [] { const char* v = getenv("SF_SORT_ROCPRIM"); return v && v[0] == '1'; }();
+    if (!use_rocprim) {
+        // middle passes in (keys_in, pv_in) and (head_scan, pv_out); the last pass writes keys_out and the sorted SoA
+        const RsBatchSrc src{b, shard_count, shard_index, st.R, st.err, st.last_ts, st.xmap};
+        if (org) {
+            const RsSinkFinal<PackedEvO> fin{b, w.keys_out, w.perm, w.s_ts, w.s_cnt, w.s_flags, w.s_origin,
+                                             w.s_nargs, w.s_atag, w.s_abits};
+            e = rs_sort(src, n, key_bits, w.keys_in, (PackedEvO*)w.pv_in, w.head_scan, (PackedEvO*)w.pv_out, fin,
+                        w.sort_tmp, s);
+        } else {
+            const RsSinkFinal<PackedEv> fin{b, w.keys_out, w.perm, w.s_ts, w.s_cnt, w.s_flags, nullptr,
+                                            w.s_nargs, w.s_atag, w.s_abits};
+            e = rs_sort(src, n, key_bits, w.keys_in, w.pv_in, w.head_scan, w.pv_out, fin, w.sort_tmp, s);
+        }
+    } else if (org) {
         hipLaunchKernelGGL(k_keys_packed<true>, dim3(blocks(n, T)), dim3(T), 0, s, b, w.keys_in, (void*)w.pv_in,
                            shard_count, shard_index, st.R, st.err, st.last_ts, st.xmap);
         e = rocprim::radix_sort_pairs(w.sort_tmp, w.sort_tmp_bytes, w.keys_in, w.keys_out, (PackedEvO*)w.pv_in,
@@ -1905,7 +1961,11 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     }
     hipMemsetAsync(w.segflag, 0, (size_t)(n < st.R ? n : st.R) * 4, s);
     if (timing) hipEventRecord(ev[1], s);
-    if (org)
+    if (!use_rocprim)
+        hipLaunchKernelGGL(k_segs, dim3(blocks(n, T)), dim3(T), 0, s, b, w.s_cnt, w.s_flags, w.s_atag, w.keys_out,
+                           w.head_scan, w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err,
+                           st.n_prule != 0);
+    else if (org)
         hipLaunchKernelGGL(k_unpack<true>, dim3(blocks(n, T)), dim3(T), 0, s, b, (const void*)w.pv_out, w.keys_out,
                            w.perm, w.s_ts, w.s_cnt, w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan,
                            w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err, st.n_prule != 0, w.s_origin);

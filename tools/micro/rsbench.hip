@@ -66,19 +66,22 @@ __global__ __launch_bounds__(T) void k_count(const uint32_t* key, uint32_t n, ui
     for (int b = threadIdx.x; b < NB; b += T) h[(size_t)blockIdx.x * NB + b] = hist[b];
 }
 
-// per bin: exclusive prefix over the chunks (in place), total in tot[bin]
+// per bin (one workgroup each, one chunk per thread): exclusive prefix over the chunks, bin total
 template <int DB>
-__global__ void k_scan_chunks(uint32_t* h, uint32_t nchunks, uint32_t* tot) {
+__global__ __launch_bounds__(1024) void k_scan_chunks(uint32_t* h, uint32_t nchunks, uint32_t* tot) {
     constexpr int NB = 1 << DB;
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= NB) return;
-    uint32_t acc = 0;
-    for (uint32_t c = 0; c < nchunks; c++) {
-        const uint32_t x = h[(size_t)c * NB + b];
-        h[(size_t)c * NB + b] = acc;
-        acc += x;
-    }
-    tot[b] = acc;
+    __shared__ uint32_t wsum[16];
+    const uint32_t b = blockIdx.x, c = threadIdx.x, lane = c & 63, wv = c >> 6;
+    const uint32_t x = c < nchunks ? h[(size_t)c * NB + b] : 0u;
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { const uint32_t y = __shfl_up(inc, o); if (lane >= (uint32_t)o) inc += y; }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t k = 0; k < wv; k++) base += wsum[k];
+    if (c < nchunks) h[(size_t)c * NB + b] = base + inc - x;
+    if (c == blockDim.x - 1) tot[b] = base + inc;
 }
 
 template <int DB, int W, int K, class V>
@@ -168,9 +171,132 @@ __global__ __launch_bounds__(W * 64) void k_pass(const uint32_t* kin, const V* v
     }
 }
 
+// LDS-staged variant: the tile's records are placed in LDS in (bin, rank)
+// order first, then written out by consecutive threads, so every store
+// instruction writes runs of consecutive addresses (one run per bin).
+template <int DB, int W, int K, class V>
+__global__ __launch_bounds__(W * 64) void k_pass_st(const uint32_t* kin, const V* vin, uint32_t* kout, V* vout,
+                                                    uint32_t n, uint32_t chunk, uint32_t shift, const uint32_t* h,
+                                                    const uint32_t* tot) {
+    constexpr int NB = 1 << DB, T = W * 64, TILE = W * K * 64, BPT = NB / T > 0 ? NB / T : 1;
+    __shared__ uint16_t wc[W][NB];
+    __shared__ uint16_t ttot[NB];
+    __shared__ uint16_t tstart[NB];
+    __shared__ uint32_t run[NB];
+    __shared__ uint32_t part[T];
+    __shared__ uint32_t skey[TILE];
+    __shared__ V sval[TILE];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    {
+        uint32_t loc[BPT], s = 0;
+#pragma unroll
+        for (int j = 0; j < BPT; j++) { const int b = tid * BPT + j; loc[j] = b < NB ? tot[b] : 0; s += loc[j]; }
+        part[tid] = s;
+        __syncthreads();
+        for (int o = 1; o < T; o <<= 1) {
+            const uint32_t x = tid >= o ? part[tid - o] : 0;
+            __syncthreads();
+            part[tid] += x;
+            __syncthreads();
+        }
+        uint32_t acc = part[tid] - s;
+#pragma unroll
+        for (int j = 0; j < BPT; j++) {
+            const int b = tid * BPT + j;
+            if (b < NB) run[b] = acc + h[(size_t)blockIdx.x * NB + b];
+            acc += loc[j];
+        }
+        for (int b = tid; b < NB; b += T) {
+#pragma unroll
+            for (int x = 0; x < W; x++) wc[x][b] = 0;
+        }
+        __syncthreads();
+    }
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint64_t t0 = lo; t0 < hi; t0 += TILE) {
+        const uint32_t nt = (uint32_t)(hi - t0 < TILE ? hi - t0 : TILE);
+        uint32_t key[K];
+        V val[K];
+        uint16_t rk[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint64_t i = t0 + (uint64_t)(w * K + k) * 64 + lane;
+            if (i < hi) { key[k] = kin[i]; val[k] = vin[i]; } else key[k] = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint64_t i = t0 + (uint64_t)(w * K + k) * 64 + lane;
+            const bool ok = i < hi;
+            const uint64_t act = __ballot(ok);
+            if (!act) { rk[k] = 0; continue; }
+            const uint32_t d = (key[k] >> shift) & (NB - 1);
+            const uint64_t m = match_bits<DB>(d, act);
+            const uint32_t before = ok ? wc[w][d] : 0;
+            const uint32_t r = (uint32_t)__popcll(m & lt);
+            rk[k] = (uint16_t)(before + r);
+            if (ok && r == 0) wc[w][d] = (uint16_t)(before + __popcll(m));
+        }
+        __syncthreads();
+        for (int b = tid; b < NB; b += T) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int x = 0; x < W; x++) { const uint32_t c = wc[x][b]; wc[x][b] = (uint16_t)acc; acc += c; }
+            ttot[b] = (uint16_t)acc;
+        }
+        __syncthreads();
+        {   // tile-local bin starts: exclusive scan of ttot
+            uint32_t loc[BPT], s = 0;
+#pragma unroll
+            for (int j = 0; j < BPT; j++) { const int b = tid * BPT + j; loc[j] = b < NB ? ttot[b] : 0; s += loc[j]; }
+            part[tid] = s;
+            __syncthreads();
+            for (int o = 1; o < T; o <<= 1) {
+                const uint32_t x = tid >= o ? part[tid - o] : 0;
+                __syncthreads();
+                part[tid] += x;
+                __syncthreads();
+            }
+            uint32_t acc = part[tid] - s;
+#pragma unroll
+            for (int j = 0; j < BPT; j++) {
+                const int b = tid * BPT + j;
+                if (b < NB) tstart[b] = (uint16_t)acc;
+                acc += loc[j];
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint64_t i = t0 + (uint64_t)(w * K + k) * 64 + lane;
+            if (i < hi) {
+                const uint32_t d = (key[k] >> shift) & (NB - 1);
+                const uint32_t p = tstart[d] + wc[w][d] + rk[k];
+                skey[p] = key[k];
+                sval[p] = val[k];
+            }
+        }
+        __syncthreads();
+        for (uint32_t p = tid; p < nt; p += T) {
+            const uint32_t kk = skey[p];
+            const uint32_t d = (kk >> shift) & (NB - 1);
+            const uint32_t dst = run[d] + (p - tstart[d]);
+            kout[dst] = kk;
+            vout[dst] = sval[p];
+        }
+        __syncthreads();
+        for (int b = tid; b < NB; b += T) {
+            run[b] += ttot[b];
+#pragma unroll
+            for (int x = 0; x < W; x++) wc[x][b] = 0;
+        }
+        __syncthreads();
+    }
+}
+
 struct Bufs { uint32_t *k0, *k1, *k2; uint64_t *v0, *v1, *v2; uint32_t *h, *tot; };
 
-template <int DB, int W, int K>
+template <int DB, int W, int K, bool ST = false>
 void lsd(Bufs& B, uint32_t n, uint32_t bits, uint32_t nchunks, hipStream_t s, uint32_t** kres, uint64_t** vres) {
     constexpr int NB = 1 << DB, TILE = W * K * 64;
     const int passes = (bits + DB - 1) / DB;
@@ -182,9 +308,13 @@ void lsd(Bufs& B, uint32_t n, uint32_t bits, uint32_t nchunks, hipStream_t s, ui
     for (int p = 0; p < passes; p++) {
         const uint32_t shift = p * DB;
         hipLaunchKernelGGL((k_count<DB, 256>), dim3(C), dim3(256), 0, s, kin, n, chunk, shift, B.h);
-        hipLaunchKernelGGL((k_scan_chunks<DB>), dim3((NB + 255) / 256), dim3(256), 0, s, B.h, C, B.tot);
-        hipLaunchKernelGGL((k_pass<DB, W, K, uint64_t>), dim3(C), dim3(W * 64), 0, s, kin, vin, ko[p & 1], vo[p & 1], n,
-                           chunk, shift, B.h, B.tot);
+        hipLaunchKernelGGL((k_scan_chunks<DB>), dim3(NB), dim3(1024), 0, s, B.h, C, B.tot);
+        if constexpr (ST)
+            hipLaunchKernelGGL((k_pass_st<DB, W, K, uint64_t>), dim3(C), dim3(W * 64), 0, s, kin, vin, ko[p & 1],
+                               vo[p & 1], n, chunk, shift, B.h, B.tot);
+        else
+            hipLaunchKernelGGL((k_pass<DB, W, K, uint64_t>), dim3(C), dim3(W * 64), 0, s, kin, vin, ko[p & 1], vo[p & 1],
+                               n, chunk, shift, B.h, B.tot);
         kin = ko[p & 1]; vin = vo[p & 1];
     }
     *kres = (uint32_t*)kin; *vres = (uint64_t*)vin;
@@ -231,21 +361,23 @@ int main(int argc, char** argv) {
         for (uint32_t i = 0; i < n; i++) bad += (gk[i] != hk[i]) | (gv[i] != hv[i]);
         printf("%-25s %.3f ms  mismatches %llu\n", name, t, (unsigned long long)bad);
     };
-#define RUN(NAME, DB, W, K)                                                                  \
+#define RUN(NAME, DB, W, K, ...)                                                             \
     {                                                                                      \
         uint32_t* ok; uint64_t* ov;                                                        \
-        lsd<DB, W, K>(B, n, bits, nchunks, 0, &ok, &ov);                                   \
+        lsd<DB, W, K, ##__VA_ARGS__>(B, n, bits, nchunks, 0, &ok, &ov);                    \
         CK(hipDeviceSynchronize());                                                        \
         hipEventRecord(a);                                                                 \
-        for (int r = 0; r < reps; r++) lsd<DB, W, K>(B, n, bits, nchunks, 0, &ok, &ov);    \
+        for (int r = 0; r < reps; r++) lsd<DB, W, K, ##__VA_ARGS__>(B, n, bits, nchunks, 0, &ok, &ov); \
         hipEventRecord(b); hipEventSynchronize(b); hipEventElapsedTime(&ms, a, b);         \
         check(NAME, ok, ov, ms / reps);                                                    \
     }
-    RUN("lsd 12-bit W4 K32", 12, 4, 32);
-    RUN("lsd 12-bit W4 K16", 12, 4, 16);
     RUN("lsd 12-bit W8 K16", 12, 8, 16);
-    RUN("lsd 8-bit W4 K32", 8, 4, 32);
     RUN("lsd 8-bit W4 K16", 8, 4, 16);
+    RUN("staged 8-bit W8 K8", 8, 8, 8, true);
+    RUN("staged 8-bit W8 K16", 8, 8, 16, true);
+    RUN("staged 8-bit W4 K16", 8, 4, 16, true);
+    RUN("staged 8-bit W16 K4", 8, 16, 4, true);
+    RUN("staged 12-bit W4 K16", 12, 4, 16, true);
     // per-kernel breakdown of the 12-bit variant
     {
         uint32_t* ok; uint64_t* ov;
@@ -259,7 +391,7 @@ int main(int argc, char** argv) {
         for (int p = 0; p < 2; p++) {
             hipEventRecord(ev[e++]);
             hipLaunchKernelGGL((k_count<DB, 256>), dim3(C), dim3(256), 0, 0, kin, n, chunk, p * DB, B.h);
-            hipLaunchKernelGGL((k_scan_chunks<DB>), dim3((NB + 255) / 256), dim3(256), 0, 0, B.h, C, B.tot);
+            hipLaunchKernelGGL((k_scan_chunks<DB>), dim3(NB), dim3(1024), 0, 0, B.h, C, B.tot);
             hipEventRecord(ev[e++]);
             hipLaunchKernelGGL((k_pass<DB, W, K, uint64_t>), dim3(C), dim3(W * 64), 0, 0, kin, vin, ko[p], vo[p], n,
                                chunk, (uint32_t)(p * DB), B.h, B.tot);
