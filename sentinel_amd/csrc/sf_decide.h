@@ -665,6 +665,17 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
 #endif
     constexpr uint32_t EV_CH = SF_EV_CH;
     int64_t t_[EV_CH]; int32_t c_[EV_CH]; uint8_t f_[EV_CH];
+    // statuses out eight at a time (decide_qps_segment)
+    uint32_t sblk = lo & ~7u;
+    uint64_t sbuf = 0;
+    auto st_flush = [&](uint32_t jend) {
+        if (sblk >= lo && jend == sblk + 8) { __builtin_memcpy(io.v_status + sblk, &sbuf, 8); return; }
+        for (uint32_t q = sblk > lo ? sblk : lo; q < jend; q++) io.v_status[q] = (uint8_t)(sbuf >> (8 * (q - sblk)));
+    };
+    auto st_put = [&](uint32_t j, uint8_t status) {
+        sbuf |= (uint64_t)status << (8 * (j - sblk));
+        if ((j & 7u) == 7u) { st_flush(j + 1); sblk = j + 1; sbuf = 0; }
+    };
     for (uint32_t j = lo; j < hi; j++) {
         const uint32_t k_ = (j - lo) % EV_CH;
         if (k_ == 0) {
@@ -692,7 +703,8 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
 #endif
                     ref = j;   // treat as this exit's own slot: reads as not blocked below
                 }
-                blocked = ref == (int64_t)j ? true : v_blocked(io.v_status[ref]);
+                const uint8_t est = ref >= (int64_t)sblk ? (uint8_t)(sbuf >> (8 * (uint32_t)(ref - sblk))) : io.v_status[ref];
+                blocked = ref == (int64_t)j ? true : v_blocked(est);
                 create_ts = io.ts[ref];
             }
             else { blocked = ref == EREF_DEAD; create_ts = io.cts ? io.cts[j] : now; }
@@ -711,7 +723,7 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
             } else {
                 status = SF_V_EXIT_IGNORED;
             }
-            io.v_status[j] = status;
+            st_put(j, status);
             emit_verdict(io, j, status, 0, 0);
             continue;
         }
@@ -771,9 +783,10 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
             }
             if (pm_exists) pm_thread_event(pt, res, pm_init, io, j, na, +1);
         }
-        io.v_status[j] = status;                             // (exits of this segment read it back)
+        st_put(j, status);                                   // (exits of this segment read it back)
         emit_verdict(io, j, status, (int32_t)wait, (uint16_t)rule_idx);
     }
+    if (hi > sblk) st_flush(hi);
 
     // write back (borrow and the first rule's controller state only when they can have changed)
     for (int i = 0; i < MAXS; i++)
@@ -814,7 +827,7 @@ SF_HD void decide_qps_segment(const DevState& st, const SegIO& io, uint32_t res,
     // unrolled selects: a lane walking a long segment then waits for memory
     // once per chunk instead of once per event
 #ifndef SF_QPS_CH
-#define SF_QPS_CH 8
+#define SF_QPS_CH 16
 #endif
     constexpr uint32_t QC = SF_QPS_CH;
     static_assert(QC % 4 == 0, "flags are packed four to a register");
@@ -822,6 +835,12 @@ SF_HD void decide_qps_segment(const DevState& st, const SegIO& io, uint32_t res,
     // or more falls back to per-event loads), flags four to a register
     int64_t t0_ = 0; uint32_t td_[QC]; int32_t c_[QC]; uint32_t f4_[QC / 4];
     bool wide_ = false;
+    uint32_t sblk = lo & ~7u;                                  // 8-aligned block of the buffered statuses
+    uint64_t sbuf = 0;
+    auto st_flush = [&](uint32_t jend) {                       // statuses [max(lo, sblk), jend)
+        if (sblk >= lo && jend == sblk + 8) { __builtin_memcpy(io.v_status + sblk, &sbuf, 8); return; }
+        for (uint32_t q = sblk > lo ? sblk : lo; q < jend; q++) io.v_status[q] = (uint8_t)(sbuf >> (8 * (q - sblk)));
+    };
     for (uint32_t j = lo; j < hi; j++) {
         const uint32_t k_ = (j - lo) % QC;
         if (k_ == 0) {
@@ -855,7 +874,9 @@ SF_HD void decide_qps_segment(const DevState& st, const SegIO& io, uint32_t res,
             bool blocked; int64_t create_ts;
             if (ref >= 0) {
                 if (ref < (int64_t)lo || ref >= (int64_t)j || (io.flags[ref] & SF_EV_EXIT)) { *st.err = SF_ERR_INVALID; ref = j; }
-                blocked = ref == (int64_t)j ? true : v_blocked(io.v_status[ref]);
+                // the entry's status: still in the store buffer, or stored
+                const uint8_t est = ref >= (int64_t)sblk ? (uint8_t)(sbuf >> (8 * (uint32_t)(ref - sblk))) : io.v_status[ref];
+                blocked = ref == (int64_t)j ? true : v_blocked(est);
                 create_ts = io.ts[ref];
             } else {
                 blocked = ref == EREF_DEAD; create_ts = io.cts ? io.cts[j] : now;
@@ -876,8 +897,13 @@ SF_HD void decide_qps_segment(const DevState& st, const SegIO& io, uint32_t res,
                 nd.threads++; nd.add_pass(now, c); status = SF_V_PASS;
             }
         }
-        io.v_status[j] = status;                            // (waits and rule indices are 0 here)
+        // statuses go out eight at a time (one aligned 8-byte store per block of
+        // the segment's own; byte stores at its ends): a byte store per event
+        // costs a partial-line write each
+        sbuf |= (uint64_t)status << (8 * (j - sblk));
+        if ((j & 7u) == 7u) { st_flush(j + 1); sblk = j + 1; sbuf = 0; }
     }
+    if (hi > sblk) st_flush(hi);
     for (int i = 0; i < MAXS; i++)
         if (i < st.S) {
             st.second[(size_t)res * st.S + i] = nd.sec[i];

@@ -1,12 +1,17 @@
-# GPU box: GPU parity tests, one leg under a kernel trace, then the default bench (A/B of a kernel change)
+# GPU box: GPU parity tests, then an A/B of an environment switch on the default bench
+# (VAR=<env name>; variants "new" = unset, "old" = VAR=1), and optionally a leg (LEG=config2) per variant
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 NAME=${NAME:-ab}; OUT=gpurun_out/$NAME; rm -rf $OUT; mkdir -p $OUT
-timeout -k 10 300 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${TESTS_K:+-k "$TESTS_K"} > $OUT/tests.log 2>&1 || { echo TESTS_FAILED; tail -30 $OUT/tests.log; exit 1; }
-tail -2 $OUT/tests.log
-if [ -n "$LEG" ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format rocpd -d $OUT/kt -o kt -- python3 tools/leg_run.py $LEG $LEG_ARGS > $OUT/leg.json 2> $OUT/leg.err || { echo KT_FAILED; tail $OUT/leg.err; exit 1; }
-  cat $OUT/leg.json
-  python3 tools/prof_summary.py --kt $(find $OUT/kt -name '*.db' | head -1) --out $OUT/summary && head -25 $OUT/summary_kernels.txt
+if [ -z "$NO_TESTS" ]; then
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${TESTS_K:+-k "$TESTS_K"} > $OUT/tests.log 2>&1 || { echo TESTS_FAILED; tail -40 $OUT/tests.log; exit 1; }
+  tail -2 $OUT/tests.log
 fi
-timeout -k 10 600 python3 -u bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAILED; tail -20 $OUT/bench.err; exit 1; }
-cat $OUT/bench.json
+for v in ${VARIANTS:-new old new old}; do
+  if [ $v = old ]; then export $VAR=1; else unset $VAR; fi
+  timeout -k 10 300 python3 -u bench.py --steps 10 --warmup 3 --no-legs --no-degrade --no-metric-log ${BENCH_ARGS} > $OUT/b_$v.json 2> $OUT/b_$v.err || { echo BENCH_FAILED $v; tail -20 $OUT/b_$v.err; exit 1; }
+  python3 -c "import json,sys; d=json.load(open('$OUT/b_$v.json')); print('$v', d['ms_per_step'], d.get('parity',{}).get('exact'), d.get('parity',{}).get('steady_state',{}).get('exact'))"
+  if [ -n "$LEG" ]; then
+    timeout -k 10 300 python3 tools/leg_run.py $LEG $LEG_ARGS > $OUT/leg_$v.json 2> $OUT/leg_$v.err || { echo LEG_FAILED $v; tail -20 $OUT/leg_$v.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$OUT/leg_$v.json')); print('$v leg', d.get('ms_per_step', d.get('ms_per_batch')), d.get('parity'))"
+  fi
+done
