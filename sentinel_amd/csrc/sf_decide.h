@@ -256,15 +256,23 @@ struct NodeWin {
     template <class F> SF_HD void min_apply(int64_t t, F f) {
         if (min_current(t)) { f(mb); mdirty = 1; }
     }
-    // ArrayMetric.previousWindowPass (:279-286) -> getPreviousWindow (LeapArray.java:234-251)
+    // ArrayMetric.previousWindowPass (:279-286) -> getPreviousWindow (LeapArray.java:234-251).
+    // The answer is fixed within a second: the previous second's bucket is a
+    // slot this walk no longer writes (its own is the current second's), and
+    // both deprecation tests give the same result at every time of the second
+    // -- so it is read once per second, not at every WarmUp check.
+    int64_t pp_sec = INT64_MIN, pp_val = 0;
     SF_HD int64_t min_previous_pass(int64_t now) {
         min_current(now);
+        if (m_ws == pp_sec) return pp_val;
         int64_t tp = now - 1000;
         int idx = (int)((tp / 1000) % MINUTE);
         Bucket b = (idx == mi) ? mb : gmin[idx];
-        if (wsub(now, b.ws) > 60000) return 0;           // isWindowDeprecated (TimeUtil now)
-        if (b.ws + 1000 < tp) return 0;
-        return b.pass;
+        int64_t v = b.pass;
+        if (wsub(now, b.ws) > 60000) v = 0;              // isWindowDeprecated (TimeUtil now)
+        if (b.ws + 1000 < tp) v = 0;
+        pp_sec = m_ws; pp_val = v;
+        return v;
     }
 
     // ---- StatisticNode ----
@@ -628,7 +636,10 @@ SF_HD void breakers_of(const DevState& st, uint32_t res, uint32_t* b0, uint32_t*
 
 // SystemRules: a SystemBlockException of an IN entry is decided by the
 // planner (sf_system.h) and arrives as EVF_SYSBLK on the event.
-template <int MAXS>
+#ifndef SF_EV_CH
+#define SF_EV_CH 8
+#endif
+template <int MAXS, uint32_t EV_CH = SF_EV_CH>
 SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi) {
     NodeWin<MAXS> nd;
     nd.S = st.S; nd.wl = st.wl; nd.interval = st.interval; nd.max_rt = st.max_rt;
@@ -660,10 +671,6 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
     // (each cache line of the sorted arrays is then fetched once, not once per
     // event after the lines of the other lanes' segments evicted it), and picked
     // out of registers by unrolled selects (no dynamic register indexing).
-#ifndef SF_EV_CH
-#define SF_EV_CH 8
-#endif
-    constexpr uint32_t EV_CH = SF_EV_CH;
     int64_t t_[EV_CH]; int32_t c_[EV_CH]; uint8_t f_[EV_CH];
     // statuses out eight at a time (decide_qps_segment)
     uint32_t sblk = lo & ~7u;

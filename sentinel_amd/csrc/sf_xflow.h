@@ -58,7 +58,7 @@ SF_HD void nw_load(NodeWin<MAXS>& nd, const DevState& st, const NodeRows& r) {
     }
     nd.threads = *r.thr;
     nd.gmin = r.min; nd.mi = -1; nd.mdirty = 0; nd.mb = fresh_bucket(WS_NONE, st.max_rt);
-    nd.c_ws = INT64_MIN; nd.c_idx = 0; nd.bdirty = 0; nd.m_ws = INT64_MIN;
+    nd.c_ws = INT64_MIN; nd.c_idx = 0; nd.bdirty = 0; nd.m_ws = INT64_MIN; nd.pp_sec = INT64_MIN;
 }
 template <int MAXS>
 SF_HD void nw_store(NodeWin<MAXS>& nd, const DevState& st, const NodeRows& r) {
