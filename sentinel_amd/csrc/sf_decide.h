@@ -612,6 +612,37 @@ SF_HD void pm_thread_event(const ParamTable& pt, uint32_t res, uint8_t pm_init, 
     }
 }
 
+// A lane's resource row into / out of a NodeWin: second-window buckets,
+// borrow buckets (only once a prioritized entry has been submitted: before
+// that every borrow bucket is the initial empty one, st.prio_seen), thread
+// count, minute row (buckets loaded on demand)
+template <int MAXS>
+SF_HD void nw_load_row(NodeWin<MAXS>& nd, const DevState& st, uint32_t res) {
+    nd.S = st.S; nd.wl = st.wl; nd.interval = st.interval; nd.max_rt = st.max_rt;
+    nd.interval_sec = st.interval / 1000.0;
+    const bool bor = *st.prio_seen != 0;
+    for (int i = 0; i < MAXS; i++) {
+        if (i < st.S) nd.sec[i] = st.second[(size_t)res * st.S + i];
+        else nd.sec[i] = fresh_bucket(WS_NONE, st.max_rt);
+        if (i < st.S && bor) nd.bor[i] = st.borrow[(size_t)res * st.S + i];
+        else { nd.bor[i].ws = WS_NONE; nd.bor[i].pass = 0; }
+    }
+    nd.threads = st.threads[res];
+    nd.gmin = st.minute + (size_t)res * MINUTE;
+    nd.mi = -1; nd.mdirty = 0;
+    nd.mb = fresh_bucket(WS_NONE, st.max_rt);
+}
+template <int MAXS>
+SF_HD void nw_store_row(NodeWin<MAXS>& nd, const DevState& st, uint32_t res) {
+    for (int i = 0; i < MAXS; i++)
+        if (i < st.S) {
+            st.second[(size_t)res * st.S + i] = nd.sec[i];
+            if (nd.bdirty) st.borrow[(size_t)res * st.S + i] = nd.bor[i];
+        }
+    nd.min_flush();
+    st.threads[res] = nd.threads;
+}
+
 SF_HD bool v_blocked(uint8_t v) {
     return v == SF_V_BLOCK_FLOW || v == SF_V_BLOCK_PARAM || v == SF_V_BLOCK_SYSTEM || v == SF_V_BLOCK_DEGRADE ||
            v == SF_V_BLOCK_OTHER;
@@ -642,30 +673,22 @@ SF_HD void breakers_of(const DevState& st, uint32_t res, uint32_t* b0, uint32_t*
 template <int MAXS, uint32_t EV_CH = SF_EV_CH>
 SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi) {
     NodeWin<MAXS> nd;
-    nd.S = st.S; nd.wl = st.wl; nd.interval = st.interval; nd.max_rt = st.max_rt;
-    nd.interval_sec = st.interval / 1000.0;
-    for (int i = 0; i < MAXS; i++) {
-        if (i < st.S) { nd.sec[i] = st.second[(size_t)res * st.S + i]; nd.bor[i] = st.borrow[(size_t)res * st.S + i]; }
-        else { nd.sec[i] = fresh_bucket(WS_NONE, st.max_rt); nd.bor[i].ws = WS_NONE; nd.bor[i].pass = 0; }
-    }
-    nd.threads = st.threads[res];
-    nd.gmin = st.minute + (size_t)res * MINUTE;
-    nd.mi = -1; nd.mdirty = 0;
-    nd.mb = fresh_bucket(WS_NONE, st.max_rt);
-
-    const uint32_t r0 = st.rule_off[res], r1 = st.rule_off[res + 1];
-    const int nrules = (int)(r1 - r0);
+    nw_load_row(nd, st, res);
+    const RDesc rd = st.rdesc[res];
+    const uint32_t r0 = rd.r0;
+    const int nrules = rd.nrules;
     // controller state of the first rule stays in registers; further rules of
     // the resource (rare) are read-modified-written in place in HBM, which
-    // is exact because this lane owns the resource
-    DevRuleState rs0 = nrules ? st.rstate[r0] : fresh_rule_state();
-    const uint32_t p0 = st.prule_off[res], p1 = st.prule_off[res + 1];
+    // is exact because this lane owns the resource (a DefaultController keeps none)
+    DevRuleState rs0 = (rd.flags & RD_STATE0) ? st.rstate[r0] : fresh_rule_state();
+    uint32_t p0 = 0, p1 = 0;
+    if (rd.flags & RD_PRULE) { p0 = st.prule_off[res]; p1 = st.prule_off[res + 1]; }
     const int nprules = (int)(p1 - p0);
     uint8_t pm_init = nprules ? st.pm_init[res] : 0;
     bool pm_exists = pm_init != 0;
     ParamTable pt{st.ptab, st.pcap_mask, st.err, st.pins};
-    uint32_t cb0, cb1;                                         // DegradeSlot breakers (this lane owns them)
-    breakers_of(st, res, &cb0, &cb1);
+    uint32_t cb0 = 0, cb1 = 0;                                 // DegradeSlot breakers (this lane owns them)
+    if (rd.flags & RD_BRK) breakers_of(st, res, &cb0, &cb1);
 
     // The lane's events are read EV_CH at a time with all loads in flight together
     // (each cache line of the sorted arrays is then fetched once, not once per
@@ -796,14 +819,8 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
     if (hi > sblk) st_flush(hi);
 
     // write back (borrow and the first rule's controller state only when they can have changed)
-    for (int i = 0; i < MAXS; i++)
-        if (i < st.S) {
-            st.second[(size_t)res * st.S + i] = nd.sec[i];
-            if (nd.bdirty) st.borrow[(size_t)res * st.S + i] = nd.bor[i];
-        }
-    nd.min_flush();
-    st.threads[res] = nd.threads;
-    if (nrules && st.rules[r0].kind != CT_DEFAULT) st.rstate[r0] = rs0;   // DefaultController keeps no state
+    nw_store_row(nd, st, res);
+    if (rd.flags & RD_STATE0) st.rstate[r0] = rs0;           // DefaultController keeps no state
     if (nprules) st.pm_init[res] = pm_init;
 }
 
@@ -818,17 +835,8 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
 template <int MAXS>
 SF_HD void decide_qps_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi) {
     NodeWin<MAXS> nd;
-    nd.S = st.S; nd.wl = st.wl; nd.interval = st.interval; nd.max_rt = st.max_rt;
-    nd.interval_sec = st.interval / 1000.0;
-    for (int i = 0; i < MAXS; i++) {
-        if (i < st.S) { nd.sec[i] = st.second[(size_t)res * st.S + i]; nd.bor[i] = st.borrow[(size_t)res * st.S + i]; }
-        else { nd.sec[i] = fresh_bucket(WS_NONE, st.max_rt); nd.bor[i].ws = WS_NONE; nd.bor[i].pass = 0; }
-    }
-    nd.threads = st.threads[res];
-    nd.gmin = st.minute + (size_t)res * MINUTE;
-    nd.mi = -1; nd.mdirty = 0;
-    nd.mb = fresh_bucket(WS_NONE, st.max_rt);
-    const double count = st.rules[st.rule_off[res]].count;
+    nw_load_row(nd, st, res);
+    const double count = st.rdesc[res].count0;
     // events read QC at a time with every load in flight together (time,
     // acquireCount and flags), picked out of registers by
     // unrolled selects: a lane walking a long segment then waits for memory
@@ -911,24 +919,32 @@ SF_HD void decide_qps_segment(const DevState& st, const SegIO& io, uint32_t res,
         if ((j & 7u) == 7u) { st_flush(j + 1); sblk = j + 1; sbuf = 0; }
     }
     if (hi > sblk) st_flush(hi);
-    for (int i = 0; i < MAXS; i++)
-        if (i < st.S) {
-            st.second[(size_t)res * st.S + i] = nd.sec[i];
-            if (nd.bdirty) st.borrow[(size_t)res * st.S + i] = nd.bor[i];
-        }
-    nd.min_flush();
-    st.threads[res] = nd.threads;
+    nw_store_row(nd, st, res);
 }
 
 // k_classify: the lean walk applies to this segment (SM_LIGHTQ)
 constexpr uint32_t SEGF_PRIO_ = 1u, SEGF_SYS_ = 4u;   // = SEGF_PRIO / SEGF_SYS (sf_heavy.h)
 SF_HD bool qps_lean(const DevState& st, uint32_t res, uint32_t segflags) {
     if (segflags & (SEGF_PRIO_ | SEGF_SYS_)) return false;
-    const uint32_t r0 = st.rule_off[res];
-    if (st.rule_off[res + 1] != r0 + 1 || st.prule_off[res + 1] != st.prule_off[res]) return false;
-    if (st.dg_rr_of && st.dg_rr_of[res] < st.dg_n) return false;
-    const DevRule& r = st.rules[r0];
-    return r.kind == CT_DEFAULT && r.grade == SF_GRADE_QPS;
+    return (st.rdesc[res].flags & RD_LEAN) != 0;
+}
+
+// the resource's RDesc from the rule tables (k_rdesc; the host simulator's refresh)
+SF_HD RDesc make_rdesc(const DevState& st, uint32_t res) {
+    RDesc d{};
+    const uint32_t r0 = st.rule_off[res], n = st.rule_off[res + 1] - r0;
+    d.r0 = r0;
+    d.nrules = (uint8_t)n;
+    const bool prule = st.prule_off[res + 1] != st.prule_off[res];
+    const bool brk = st.dg_rr_of && st.dg_rr_of[res] < st.dg_n;
+    d.flags = (uint8_t)((prule ? RD_PRULE : 0) | (brk ? RD_BRK : 0));
+    if (n) {
+        const DevRule& r = st.rules[r0];
+        d.count0 = r.count;
+        if (r.kind != CT_DEFAULT) d.flags |= RD_STATE0;
+        if (n == 1 && !prule && !brk && r.kind == CT_DEFAULT && r.grade == SF_GRADE_QPS) d.flags |= RD_LEAN;
+    }
+    return d;
 }
 
 // ============================================================ rule tables (host side)

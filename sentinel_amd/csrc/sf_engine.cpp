@@ -194,7 +194,7 @@ void sf_destroy(sf_engine* e) {
     void* ptrs[] = {e->st.second, e->st.borrow, e->st.minute, e->st.threads, (void*)e->st.rule_off,
                     (void*)e->st.rules, e->st.rstate, (void*)e->st.prule_off, e->st.prules, (void*)e->st.items,
                     e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out, e->plan_stage, e->st.pins,
-                    e->st.xw_stats};
+                    e->st.xw_stats, (void*)e->st.rdesc, e->st.prio_seen};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
     for (void* p : e->host_allocs) hipHostFree(p);
@@ -375,6 +375,8 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     DALLOC(st.rule_off, (R + 1) * sizeof(uint32_t));
     DALLOC(st.prule_off, (R + 1) * sizeof(uint32_t));
     DALLOC(st.pm_init, R);
+    DALLOC(st.rdesc, R * sizeof(RDesc));
+    DALLOC(st.prio_seen, sizeof(int32_t));
     DALLOC(st.err, sizeof(int32_t));
     uint64_t pcap = 16;
     while (pcap < (uint64_t)c.param_capacity) pcap <<= 1;
@@ -383,6 +385,8 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     HIP_TRY(hipMemsetAsync((void*)st.rule_off, 0, (R + 1) * sizeof(uint32_t), e->stream));
     HIP_TRY(hipMemsetAsync((void*)st.prule_off, 0, (R + 1) * sizeof(uint32_t), e->stream));
     HIP_TRY(hipMemsetAsync(st.pm_init, 0, R, e->stream));
+    HIP_TRY(hipMemsetAsync((void*)st.rdesc, 0, R * sizeof(RDesc), e->stream));   // (= no rules)
+    HIP_TRY(hipMemsetAsync(st.prio_seen, 0, sizeof(int32_t), e->stream));
     HIP_TRY(hipMemsetAsync(st.ptab, 0, pcap * sizeof(ParamSlot), e->stream));
     DALLOC(st.pins, 256 * 16 * sizeof(unsigned int));
     DALLOC(st.xw_stats, 4 * sizeof(unsigned long long));
@@ -752,6 +756,7 @@ int sf_load_flow_rules(sf_engine* e, const sf_flow_rule* rules, uint32_t n) {
         HIP_TRY(hipMemcpyAsync(e->st.rstate, ds.data(), ds.size() * sizeof(DevRuleState), hipMemcpyHostToDevice, e->stream));
     }
     HIP_TRY(hipMemcpyAsync((void*)e->st.rule_off, off.data(), off.size() * 4, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(launch_rdesc(e->st, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->st.xmap = xflow ? e->xmap_buf : nullptr;
     e->st.xw = xflow ? e->xw_buf : nullptr;
@@ -804,6 +809,7 @@ int sf_load_param_rules(sf_engine* e, const sf_param_rule* rules, uint32_t n, co
     uint32_t kmax = 0;
     for (uint32_t r = 0; r < e->R; r++) kmax = std::max(kmax, counts[r]);
     e->p_kmax = 2ull * kmax;
+    HIP_TRY(launch_rdesc(e->st, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     return SF_OK;
 }
@@ -2450,6 +2456,11 @@ int sf_load_degrade_rules(sf_engine* e, const sf_degrade_rule* rules, uint32_t n
     e->dg.key_bits = kb;
     e->dgw.sort_tmp_bytes = 0;                                  // re-sized for the new key width
     if (e->dgw.sort_tmp) { hipFree(e->dgw.sort_tmp); e->dgw.sort_tmp = nullptr; }
+    {   // the routing summary reads dg_rr_of
+        hipError_t re = launch_rdesc(e->st, e->stream);
+        if (re == hipSuccess) re = hipStreamSynchronize(e->stream);
+        if (re != hipSuccess) return fail(SF_ERR_DEVICE, std::string("rdesc: ") + hipGetErrorString(re));
+    }
     if (n_loaded) *n_loaded = nv;
     return SF_OK;
 }

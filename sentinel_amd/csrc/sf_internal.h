@@ -52,6 +52,25 @@ struct DevRuleState {    // AtomicLong fields of the controllers
     int64_t stored_tokens, last_filled, latest_passed, pad;
 };
 
+// Per-resource summary of the rule tables, rebuilt on the device after every
+// flow / param / degrade rule load (k_rdesc): the routing and the light lanes
+// read this one 16-B record instead of rule_off, prule_off, dg_rr_of and the
+// first DevRule (four lines of four arrays per segment)
+struct RDesc {
+    double count0;                 // the first flow rule's count
+    uint32_t r0;                   // rule_off[res]
+    uint8_t nrules;                // rule_off[res + 1] - r0 (<= SF_MAX_RULES_PER_RESOURCE)
+    uint8_t flags;                 // RD_*
+    uint16_t pad;
+};
+static_assert(sizeof(RDesc) == 16, "RDesc layout");
+enum : uint8_t {
+    RD_LEAN = 1,                   // one QPS DefaultController rule and nothing else in the chain
+    RD_PRULE = 2,                  // ParamFlow rules on the resource
+    RD_BRK = 4,                    // circuit breakers on the resource
+    RD_STATE0 = 8,                 // the first rule's controller keeps state (not a DefaultController)
+};
+
 struct DevParamRule {    // ParamFlowRule (ParamFlowRule.java:45-83)
     int32_t grade, param_idx, behavior, max_queue_ms;
     double count;
@@ -93,6 +112,11 @@ struct DevState {
     int32_t* err;                  // device error word (capacity, invalid input)
     int64_t* last_fetch;           // [R] StatisticNode.lastFetchTime (metric snapshot)
     int64_t* last_ts;              // engine clock: last event time of the previous batch (time never goes back)
+    const RDesc* rdesc;            // [R] (k_rdesc)
+    // nonzero once any prioritized entry was submitted (k_segs): only those
+    // write borrow buckets (tryOccupyNext), so until then every borrow bucket is
+    // the initial empty one and the light lanes need not read it
+    int32_t* prio_seen;
     // DegradeSlot (after FlowSlot): breakers of local resource l are
     // [dg_off[k], dg_off[k+1]) with k = dg_rr_of[l] < dg_n; dg_rr_of null = none
     const uint32_t* dg_rr_of;
@@ -296,6 +320,7 @@ constexpr int64_t EREF_DEAD = -2;
 hipError_t query_temp_bytes(uint32_t max_n, uint32_t key_bits, size_t* sort_bytes, size_t* scan_bytes,
                             size_t* pscan_bytes);
 hipError_t launch_init_state(const DevState& st, hipStream_t s);
+hipError_t launch_rdesc(const DevState& st, hipStream_t s);   // RDesc of every resource from the rule tables
 hipError_t launch_entry_node(const DevState& st, const DevBatch& b, const uint8_t* vstatus, EntryNode* en,
                              EntryAcc* acc, hipStream_t s);
 hipError_t launch_entry_init(EntryNode* en, int64_t max_rt, hipStream_t s);

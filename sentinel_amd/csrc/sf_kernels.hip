@@ -91,7 +91,7 @@ __global__ void k_unpack(DevBatch b, const void* pvv, const uint32_t* keys, uint
                          int32_t* s_cnt, uint8_t* s_flags, uint8_t* s_nargs, uint8_t* s_atag,
                          uint64_t* s_abits, const uint32_t* head_scan, uint32_t* seg_start, uint32_t* seg_res,
                          uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts, const int32_t* err, bool exit_marks,
-                         uint32_t* s_origin) {
+                         uint32_t* s_origin, int32_t* prio_seen) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
     const uint32_t sid = head_scan[j] - 1;
@@ -124,6 +124,7 @@ __global__ void k_unpack(DevBatch b, const void* pvv, const uint32_t* keys, uint
         const unsigned long long any = __ballot(mine != 0);
         if (any) {
             const int lane = (int)(threadIdx.x & 63);
+            if (__ballot(mine & SEGF_PRIO) && lane == 0) atomicOr(prio_seen, 1);
             const int psid = __shfl_up((int)sid, 1);
             const unsigned long long heads = __ballot(lane == 0 || (uint32_t)psid != sid);
             const unsigned long long below = (1ull << lane) - 1ull;
@@ -157,7 +158,8 @@ __global__ void k_unpack(DevBatch b, const void* pvv, const uint32_t* keys, uint
 // and the per-segment flags k_classify routes by.
 __global__ void k_segs(DevBatch b, const int32_t* s_cnt, const uint8_t* s_flags, const uint8_t* s_atag,
                        const uint32_t* keys, const uint32_t* head_scan, uint32_t* seg_start, uint32_t* seg_res,
-                       uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts, const int32_t* err, bool exit_marks) {
+                       uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts, const int32_t* err, bool exit_marks,
+                       int32_t* prio_seen) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= b.n) return;
     const uint32_t sid = head_scan[j] - 1;
@@ -176,6 +178,7 @@ __global__ void k_segs(DevBatch b, const int32_t* s_cnt, const uint8_t* s_flags,
     const unsigned long long any = __ballot(mine != 0);
     if (!any) return;
     const int lane = (int)(threadIdx.x & 63);
+    if (__ballot(mine & SEGF_PRIO) && lane == 0) atomicOr(prio_seen, 1);   // (sticky: st.prio_seen)
     const int psid = __shfl_up((int)sid, 1);
     const unsigned long long heads = __ballot(lane == 0 || (uint32_t)psid != sid);
     const unsigned long long below = (1ull << lane) - 1ull;
@@ -268,7 +271,7 @@ __global__ void k_classify(DevState st, Work w, const int64_t* s_ts) {
     bool light = valid && !xs && hi - lo <= w.heavy_min;
     // a ParamFlow-only segment of more than 32 events is faster on the
     // wavefront-by-value path (SM_PARAM) than as one lane's serial table walk
-    if (light && hi - lo > 32 && st.prule_off[res + 1] != st.prule_off[res] &&
+    if (light && hi - lo > 32 && (st.rdesc[res].flags & RD_PRULE) &&
         heavy_mode(st, res, w.segflag[s], s_ts[lo]) == SM_PARAM)
         light = false;
     // light list slot: workgroup histogram of the length classes in LDS, one
@@ -1890,6 +1893,16 @@ hipError_t rocprim_scan_bytes(uint32_t n, size_t* bytes) {
                                    rocprim::plus<uint32_t>());
 }
 
+__global__ void k_rdesc(DevState st, RDesc* out) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < st.R) out[r] = make_rdesc(st, r);
+}
+// after any change of rule_off / rules / prule_off / dg_rr_of
+hipError_t launch_rdesc(const DevState& st, hipStream_t s) {
+    hipLaunchKernelGGL(k_rdesc, dim3(blocks(st.R, 256)), dim3(256), 0, s, st, (RDesc*)st.rdesc);
+    return hipGetLastError();
+}
+
 hipError_t launch_init_state(const DevState& st, hipStream_t s) {
     size_t n_sec = (size_t)st.R * st.S, n_min = (size_t)st.R * MINUTE;
     hipLaunchKernelGGL(k_init_state, dim3(2048), dim3(256), 0, s, st, n_sec, n_min);
@@ -1964,16 +1977,17 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     if (!use_rocprim)
         hipLaunchKernelGGL(k_segs, dim3(blocks(n, T)), dim3(T), 0, s, b, w.s_cnt, w.s_flags, w.s_atag, w.keys_out,
                            w.head_scan, w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err,
-                           st.n_prule != 0);
+                           st.n_prule != 0, st.prio_seen);
     else if (org)
         hipLaunchKernelGGL(k_unpack<true>, dim3(blocks(n, T)), dim3(T), 0, s, b, (const void*)w.pv_out, w.keys_out,
                            w.perm, w.s_ts, w.s_cnt, w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan,
-                           w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err, st.n_prule != 0, w.s_origin);
+                           w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err, st.n_prule != 0, w.s_origin,
+                           st.prio_seen);
     else
         hipLaunchKernelGGL(k_unpack<false>, dim3(blocks(n, T)), dim3(T), 0, s, b, (const void*)w.pv_out, w.keys_out,
                            w.perm, w.s_ts, w.s_cnt, w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan,
                            w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err, st.n_prule != 0,
-                           (uint32_t*)nullptr);
+                           (uint32_t*)nullptr, st.prio_seen);
     if (classify) launch_classify(st, w, b, s, ev, timing);
     return hipGetLastError();
 }

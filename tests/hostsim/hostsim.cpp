@@ -28,6 +28,8 @@ struct hs_engine {
     std::vector<DevParamRule> prules;
     std::vector<DevHotItem> items;
     std::vector<uint8_t> pm_init;
+    std::vector<RDesc> rdesc;
+    int32_t prio_seen = 0;                         // (k_segs: any prioritized entry submitted so far)
     std::vector<ParamSlot> ptab;
     std::vector<uint32_t> dg_rr, dg_off;
     std::vector<DevBreakerRule> dg_rules;
@@ -45,7 +47,7 @@ struct hs_engine {
     uint32_t R;
     uint32_t heavy_min;
     uint64_t n_heavy_segments = 0, n_heavy_item_segments = 0, mode_count[8] = {};
-    void refresh() {
+    void refresh(bool rules_changed = true) {
         st.second = second.data(); st.borrow = borrow.data(); st.minute = minute.data();
         st.threads = threads.data(); st.rule_off = rule_off.data(); st.rules = rules.data();
         st.rstate = rstate.data(); st.prule_off = prule_off.data(); st.prules = prules.data();
@@ -62,6 +64,12 @@ struct hs_engine {
             ax_chunks.push_back(AuxChunk{ax_second.data() + c * AX_CHUNK * S_, ax_borrow.data() + c * AX_CHUNK * S_,
                                          ax_minute.data() + c * AX_CHUNK * MINUTE, ax_threads.data() + c * AX_CHUNK});
         st.ax_chunks = ax_chunks.data(); st.ax_count = &ax_count; st.ax_cap = (uint32_t)ax_threads.size();
+        st.prio_seen = &prio_seen;
+        if (rules_changed) {
+            rdesc.resize(R);
+            st.rdesc = rdesc.data();
+            for (uint32_t r = 0; r < R; r++) rdesc[r] = make_rdesc(st, r);
+        }
     }
 };
 
@@ -197,7 +205,7 @@ int hs_read_breaker(hs_engine* e, uint32_t k, sf_breaker_state* out) {
 }
 
 int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
-    if (in->origin) { ensure_pool(e); e->refresh(); }        // origin nodes of every entry with an origin
+    if (in->origin) { ensure_pool(e); e->refresh(false); }        // origin nodes of every entry with an origin
     const uint32_t n = in->n;
     e->err = 0;
     std::vector<uint32_t> key(n), perm(n), inv(n);
@@ -253,9 +261,11 @@ int hs_submit(hs_engine* e, const sf_event_batch* in, sf_verdicts* out) {
     for (uint32_t j = 0; j < n; j++) {
         if (j == 0 || key[perm[j]] != key[perm[j - 1]]) { seg_start.push_back(j); seg_res.push_back(key[perm[j]]); segflag.push_back(0); }
         if (in->origin && in->origin[perm[j]] != SF_ORIGIN_NONE) segflag.back() |= SEGF_ORIGIN;
-        if (!(fl[j] & SF_EV_EXIT) && ((fl[j] & (SF_EV_PRIO | EVF_SYSBLK)) || cnt[j] <= 0))
+        if (!(fl[j] & SF_EV_EXIT) && ((fl[j] & (SF_EV_PRIO | EVF_SYSBLK)) || cnt[j] <= 0)) {
+            if (fl[j] & SF_EV_PRIO) e->prio_seen = 1;           // (sticky, as k_segs sets it)
             segflag.back() |= ((fl[j] & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (cnt[j] <= 0 ? SEGF_NONPOS : 0u) |
                               ((fl[j] & EVF_SYSBLK) ? SEGF_SYS : 0u);
+        }
     }
     const uint32_t ns = (uint32_t)seg_start.size();
     seg_start.push_back(n);
