@@ -737,7 +737,7 @@ def config2_leg(R=1_000_000, n=1 << 27, steps=3, parity=1):
         e.close()
 
 
-def config4_leg(R=1000, n=1 << 24, keys=100_000_000, qps_frac=0.6, reps=3):
+def config4_leg(R=1000, n=1 << 24, keys=100_000_000, qps_frac=0.6, reps=3, parity=1):
     """BASELINE config 4 (its own engine): 1k resources with one QPS
     ParamFlowRule each (+10 % with a throttle rule), keys Zipf(1.1) over 100M
     distinct values, every event EntryType.IN, and the inbound-QPS SystemRule
@@ -788,6 +788,8 @@ def config4_leg(R=1000, n=1 << 24, keys=100_000_000, qps_frac=0.6, reps=3):
            "system_blocks": int((st[0] == abi.V_BLOCK_SYSTEM).sum()),
            "param_blocks": int((st[0] == abi.V_BLOCK_PARAM).sum()),
            "passed": int(np.isin(st[0], abi.PASSED).sum()), "reps_ms": [round(1e3 * w, 3) for w in walls]}
+    if not parity:
+        return res
     log(f"[leg config4] GPU {ms:.1f} ms per batch; oracle replays (exact maps, and LRU maps as the reference) ...")
     try:
         import threading

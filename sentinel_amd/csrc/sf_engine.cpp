@@ -1058,11 +1058,13 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         uint32_t p = 0, rounds = 0;
         while (p < n) {
             hipError_t le = sys_plan(stl, b, dv.status, e->sys_mask, e->sys, e->en, p, e->sys_plan, e->sys_pa,
-                                     e->sys_pb, s);
+                                     e->sys_pb, s, true);
             if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("system plan: ") + hipGetErrorString(le));
-            uint32_t q = 0;
-            HIP_TRY(hipMemcpyAsync(&q, &e->sys_plan->q, 4, hipMemcpyDeviceToHost, s));
+            uint32_t qi[2] = {0, 0};                        // q, inert entries planned
+            static_assert(offsetof(SysPlanDev, n_inert) == offsetof(SysPlanDev, q) + 4, "q, n_inert adjacent");
+            HIP_TRY(hipMemcpyAsync(qi, &e->sys_plan->q, 8, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
+            const uint32_t q = qi[0];
             if (q <= p || q > n) return fail(SF_ERR_DEVICE, "system planner made no progress");
             DevBatch v = b;                        // the view [p, q)
             v.n = q - p; v.base = p;
@@ -1085,6 +1087,9 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
                                    e->serial ? s : e->stream4,
                                    e->evs[slot], false, with_ox ? &plan : nullptr);
             if (le == hipSuccess && with_ox) w.ox_dirty = false;     // k_ox_reset enqueued
+            // the system verdicts of the inert entries (ENTRY_NODE is still at p)
+            if (le == hipSuccess && qi[1])
+                le = sys_plan_fix(stl, b, dv, e->sys_mask, e->sys, p, q, e->sys_plan, e->sys_pa, e->sys_pb, s);
             if (le == hipSuccess) le = launch_entry_node(stl, v, dvv.status, e->en, e->en_acc, s);
             if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
             p = q;

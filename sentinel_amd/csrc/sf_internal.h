@@ -308,6 +308,10 @@ struct DevVerdicts { uint8_t* status; int32_t* wait; uint16_t* rule; };
 constexpr uint8_t EVF_SYSBLK = 0x80u;
 constexpr uint8_t EVF_SYSREASON_SHIFT = 4;
 constexpr uint8_t SYS_NONE = 0xFFu;      // planner mask: no forced block
+// planner mask: the system verdict is not known yet, but should the entry pass
+// SystemSlot its first ParamFlow rule certainly blocks it (sf_system.h,
+// "inert entries"): decided as not forced, its reason settled after the sub-batch
+constexpr uint8_t SYS_INERT = 0xFEu;
 // EVF_SYSBLK reason of an SF_EV_BLOCKED entry: blocked by a slot StatisticSlot
 // wraps but the engine does not run (AuthoritySlot), verdict SF_V_BLOCK_OTHER.
 // Like a SystemBlockException it is only a block count to every other slot.

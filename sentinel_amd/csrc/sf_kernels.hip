@@ -70,7 +70,7 @@ __global__ void k_keys_packed(DevBatch b, uint32_t* keys, void* pvv, uint32_t sh
         fl |= EVF_SYSBLK | ((uint32_t)SYSR_OTHER << EVF_SYSREASON_SHIFT);
     else if (b.sys && (f & SF_EV_IN) && !(f & SF_EV_EXIT)) {     // SystemBlockException forced by the planner
         const uint8_t sr = b.sys[i];
-        if (sr != SYS_NONE) fl |= EVF_SYSBLK | ((uint32_t)sr << EVF_SYSREASON_SHIFT);
+        if (sr < SYS_INERT) fl |= EVF_SYSBLK | ((uint32_t)sr << EVF_SYSREASON_SHIFT);   // (SYS_INERT / SYS_NONE: none)
     }
     const int32_t c = b.cnt[i];
     const uint32_t c8 = (c >= 1 && c <= 255) ? (uint32_t)c : 0u;

@@ -208,16 +208,67 @@ SF_HD SysExitQ sys_exit_q(const int64_t* ts, const int32_t* cnt, const uint8_t* 
     return q;
 }
 
+// Inert entries.  Between SystemSlot and FlowSlot sits ParamFlowSlot
+// (ParamFlowSlot.checkFlow :82-103): an IN entry that passes SystemSlot is
+// checked by its resource's ParamFlow rules in order.  When the first one is a
+// QPS rule with the default behaviour whose value's token counter already
+// exists, holds fewer tokens than the entry asks for, and is not due for a
+// refill at the entry's time (ParamFlowChecker.passDefaultLocalCheck :139-219:
+// without a refill the counter only falls, and a refill is due at no earlier
+// event when none is due at this one), that rule certainly blocks the entry
+// whatever the undecided events before it do.  Blocked by SystemSlot or by that
+// rule, the entry then changes nothing but the block counters, which count it
+// either way (StatisticSlot.entry :107-123), so it never adds to a pass or
+// thread bound, and its own system verdict can be settled once the sub-batch is
+// decided (sys_plan_fix).  param_inert tells, from the table as it is at p
+// (the events before p are decided and no event at or after p has run).
+SF_HD bool param_inert(const DevState& st, const DevBatch& b, uint32_t i, int32_t acq, int64_t now) {
+    if (st.shard_count != 1 || !st.rdesc || !b.atag) return false;
+    const uint32_t l = b.res[i];
+    if (l >= st.R || (st.xmap && st.xmap[l] != XNONE)) return false;
+    if (!(st.rdesc[l].flags & RD_PRULE)) return false;
+    const DevParamRule& r = st.prules[st.prule_off[l]];
+    if (r.grade != SF_GRADE_QPS || r.behavior == SF_BEHAVIOR_RATE_LIMITER || r.param_idx < 0) return false;
+    const uint32_t na = b.nargs ? b.nargs[i] : b.arg_slots;
+    if ((uint32_t)r.param_idx >= na || (uint32_t)r.param_idx >= b.arg_slots) return false;   // passCheck :53-56
+    const uint32_t tag = b.atag[(size_t)r.param_idx * b.arg_stride + i];
+    if (tag == SF_TAG_NULL || tag == SF_TAG_COLLECTION) return false;
+    const uint64_t bits = b.abits[(size_t)r.param_idx * b.arg_stride + i];
+    int64_t token_count = j_d2l(r.count);
+    for (int k = 0; k < r.item_cnt; k++) {
+        const DevHotItem& it = st.items[r.item_off + k];
+        if (it.tag == tag && it.bits == bits) { token_count = it.count; break; }
+    }
+    if (token_count == 0) return true;                       // :156-158
+    if (acq > wadd(token_count, r.burst)) return true;       // :160-163
+    const ParamTable pt{st.ptab, st.pcap_mask, st.err, nullptr};
+    const ParamSlot* sl = pt.find(pkey_hi(l, PK_RULE, 0u, tag), bits);
+    if (!sl) return false;                                   // first sight passes
+    if (wsub(now, sl->a) > wmul(r.duration_sec, 1000)) return false;   // a refill is due
+    return sl->b - acq < 0;                                  // :196-215
+}
+
 // planner state in HBM (one per engine)
 struct SysPlanDev {
     SysBase base;
     uint32_t wend, lim, first_unc, q;
+    uint32_t n_inert, pad;         // IN entries planned SYS_INERT (read with q)
 };
 
 // Plan the events from p of batch b (whole batch, base 0): mask[i] for the
 // IN entries of [p, q), plan->q.  vstatus: the batch's verdicts (before p).
+// inert: this engine decides the entries (not a merged node stream), so an
+// unknown entry its first ParamFlow rule certainly blocks is planned SYS_INERT
+// instead of ending the sub-batch (param_inert).
 hipError_t sys_plan(const DevState& st, const DevBatch& b, const uint8_t* vstatus, uint8_t* mask, const SysRule& r,
-                    const EntryNode* en, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb, hipStream_t s);
+                    const EntryNode* en, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb, hipStream_t s,
+                    bool inert = false);
+// After [p, q) is decided (verdicts in out, ENTRY_NODE still at p): the exact
+// system verdict of every SYS_INERT entry of [p, q); a fired check turns its
+// ParamFlow block into the SystemBlockException SystemSlot threw first.
+hipError_t sys_plan_fix(const DevState& st, const DevBatch& b, const DevVerdicts& out, const uint8_t* mask,
+                        const SysRule& r, uint32_t p, uint32_t q, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb,
+                        hipStream_t s);
 constexpr uint32_t SYS_PLAN_BLOCKS = 512;       // SP_NB (sf_system.hip): size of pa / pb
 
 }  // namespace sf

@@ -33,6 +33,13 @@ struct SysPlanArgs {
     double interval_sec;
     SysPlanDev* plan;
     SysExitQ* pa; SysEntQ* pb;              // [SP_NB] block totals
+    // inert entries (sf_system.h param_inert): the engine's state and the
+    // batch (args) to probe; exact: sys_plan_fix (every event of [p, lim)
+    // decided, verdicts in vstatus / ostatus)
+    bool inert, exact;
+    DevState st;
+    DevBatch b;
+    uint8_t* ostatus; uint16_t* orule;
 };
 
 __global__ void k_sp_init(SysPlanArgs a, const EntryNode* en) {
@@ -45,7 +52,12 @@ __global__ void k_sp_init(SysPlanArgs a, const EntryNode* en) {
     pl.wend = lo;
     pl.lim = min(lo, a.p + SP_CAP);
     pl.first_unc = pl.lim;
+    pl.n_inert = 0;
     pl.base = sys_base(en->second, a.S, a.wl, a.interval, a.max_rt, en->threads, t);
+}
+// sys_plan_fix: the range is the decided sub-batch [p, q); base is still ENTRY_NODE at p
+__global__ void k_sp_fix_init(SysPlanDev* pl) {
+    if (threadIdx.x == 0) pl->lim = pl->q;
 }
 
 // block-wide inclusive scan of a struct with clear()/add() (Hillis-Steele in LDS)
@@ -81,7 +93,11 @@ __device__ Q block_prefix(const Q* tot, uint32_t k, Q* lds) {
 }
 
 __device__ __forceinline__ SysExitQ exit_q(const SysPlanArgs& a, uint32_t i) {
-    return sys_exit_q(a.ts, a.cnt, a.flags, a.eref, a.cts, a.vstatus, a.p, i, a.r.max_rt);
+    // (exact: every entry before lim is decided)
+    return sys_exit_q(a.ts, a.cnt, a.flags, a.eref, a.cts, a.vstatus, a.exact ? a.plan->lim : a.p, i, a.r.max_rt);
+}
+__device__ __forceinline__ bool inert_at(const SysPlanArgs& a, uint32_t i) {
+    return a.inert && param_inert(a.st, a.b, i, a.cnt[i], a.ts[i]);
 }
 // IN entries that reach SystemSlot (an SF_EV_BLOCKED entry was blocked by
 // AuthoritySlot before it: certainly blocked, no system verdict)
@@ -110,8 +126,13 @@ __device__ __forceinline__ SysEntQ ent_q(const SysPlanArgs& a, const SysBase& ba
     const int32_t c = a.cnt[i];
     SysEntQ none;
     none.clear();
+    if (a.exact) {                                          // decided: the entries that passed, signed counts
+        if (!v_blocked_any(a.vstatus[i])) { e.nb = 1; e.nb_c = c; }
+        return e;
+    }
     bool fire = false;
     sys_classify(a.r, base, a.S, a.interval_sec, x, none, c, &fire);
+    if (!fire && inert_at(a, i)) fire = true;               // never passes either way
     if (!fire) { e.nb = 1; e.nb_c = c > 0 ? c : 0; e.nb_neg = c < 0 ? 1 : 0; }
     return e;
 }
@@ -180,39 +201,97 @@ __global__ void __launch_bounds__(SP_T) k_sp_c(SysPlanArgs a) {
     __syncthreads();
     en.add(eex);
     // classify
+    uint32_t n_inert = 0;
     for (uint32_t i = r0; i < r1; i++) {
         if (in_entry(a, i)) {
             const int32_t c = a.cnt[i];
+            if (a.exact) {
+                // sys_plan_fix: everything before i decided, so the bounds are one
+                // value (the passes folded into the base); an inert entry's system
+                // verdict, settled
+                if (a.mask[i] == SYS_INERT) {
+                    SysBase be = base;
+                    be.P = wadd(base.P, en.nb_c); be.T = base.T + en.nb;
+                    SysExitQ xx = x;
+                    xx.nneg = 0;
+                    SysEntQ none;
+                    none.clear();
+                    bool f2 = false;
+                    const int res = sys_classify(a.r, be, a.S, a.interval_sec, xx, none, c, &f2);
+                    if (res == -1 || a.ostatus[i] != SF_V_BLOCK_PARAM) *a.st.err = SF_ERR_INVALID;   // (cannot happen)
+                    else if (res >= 0) {
+                        a.ostatus[i] = SF_V_BLOCK_SYSTEM;
+                        if (a.orule) a.orule[i] = (uint16_t)res;
+                    }
+                } else if (!v_blocked_any(a.vstatus[i])) {
+                    en.nb++; en.nb_c = wadd(en.nb_c, c);
+                }
+                x.add(exit_q(a, i));
+                continue;
+            }
             bool fire = false;
             const int res = sys_classify(a.r, base, a.S, a.interval_sec, x, en, c, &fire);
-            if (res == -1) { atomicMin(&pl.first_unc, i); break; }
-            a.mask[i] = res >= 0 ? (uint8_t)res : SYS_NONE;
-            if (!fire) { en.nb++; en.nb_c = wadd(en.nb_c, c > 0 ? c : 0); en.nb_neg += c < 0 ? 1 : 0; }
-        } else if ((a.flags[i] & (SF_EV_IN | SF_EV_EXIT | SF_EV_BLOCKED)) == (SF_EV_IN | SF_EV_BLOCKED)) {
+            bool counts = !fire;
+            if (res == -1) {
+                if (!inert_at(a, i)) { atomicMin(&pl.first_unc, i); break; }
+                a.mask[i] = SYS_INERT;                     // never passes: settled after the sub-batch
+                n_inert++;
+                counts = false;
+            } else {
+                a.mask[i] = res >= 0 ? (uint8_t)res : SYS_NONE;
+                if (counts && inert_at(a, i)) counts = false;
+            }
+            if (counts) { en.nb++; en.nb_c = wadd(en.nb_c, c > 0 ? c : 0); en.nb_neg += c < 0 ? 1 : 0; }
+        } else if (!a.exact && (a.flags[i] & (SF_EV_IN | SF_EV_EXIT | SF_EV_BLOCKED)) == (SF_EV_IN | SF_EV_BLOCKED)) {
             a.mask[i] = SYS_NONE;                          // blocked before SystemSlot: no system verdict
         }
         x.add(exit_q(a, i));
     }
+    if (n_inert) atomicAdd(&pl.n_inert, n_inert);
 }
 
 __global__ void k_sp_done(SysPlanDev* pl) {
     if (threadIdx.x == 0) pl->q = min(pl->first_unc, pl->lim);
 }
 
-hipError_t sys_plan(const DevState& st, const DevBatch& b, const uint8_t* vstatus, uint8_t* mask, const SysRule& r,
-                    const EntryNode* en, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb, hipStream_t s) {
-    SysPlanArgs a;
+static SysPlanArgs plan_args(const DevState& st, const DevBatch& b, const uint8_t* vstatus, uint8_t* mask,
+                             const SysRule& r, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb) {
+    SysPlanArgs a{};
     a.ts = b.ts; a.cnt = b.cnt; a.flags = b.flags; a.eref = b.eref; a.cts = b.cts;
     a.vstatus = vstatus; a.mask = mask; a.n = b.n; a.p = p; a.r = r;
     a.S = st.S; a.wl = st.wl; a.interval = st.interval; a.max_rt = st.max_rt;
     a.interval_sec = st.interval / 1000.0;
     a.plan = plan; a.pa = pa; a.pb = pb;
+    a.st = st; a.b = b;
+    return a;
+}
+
+hipError_t sys_plan(const DevState& st, const DevBatch& b, const uint8_t* vstatus, uint8_t* mask, const SysRule& r,
+                    const EntryNode* en, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb, hipStream_t s,
+                    bool inert) {
+    SysPlanArgs a = plan_args(st, b, vstatus, mask, r, p, plan, pa, pb);
+    a.inert = inert && st.n_prule != 0;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(SP_NB, ((uint64_t)(b.n - p) + SP_BLK - 1) / SP_BLK);
     hipLaunchKernelGGL(k_sp_init, dim3(1), dim3(64), 0, s, a, en);
     hipLaunchKernelGGL(k_sp_a, dim3(nb), dim3(SP_T), 0, s, a);
     hipLaunchKernelGGL(k_sp_b, dim3(nb), dim3(SP_T), 0, s, a);
     hipLaunchKernelGGL(k_sp_c, dim3(nb), dim3(SP_T), 0, s, a);
     hipLaunchKernelGGL(k_sp_done, dim3(1), dim3(64), 0, s, plan);
+    return hipGetLastError();
+}
+
+hipError_t sys_plan_fix(const DevState& st, const DevBatch& b, const DevVerdicts& out, const uint8_t* mask,
+                        const SysRule& r, uint32_t p, uint32_t q, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb,
+                        hipStream_t s) {
+    if (q <= p) return hipSuccess;
+    SysPlanArgs a = plan_args(st, b, out.status, (uint8_t*)mask, r, p, plan, pa, pb);
+    a.exact = true;
+    a.ostatus = out.status; a.orule = out.rule;
+    const uint32_t nb = (uint32_t)(((uint64_t)(q - p) + SP_BLK - 1) / SP_BLK);
+    hipLaunchKernelGGL(k_sp_fix_init, dim3(1), dim3(64), 0, s, plan);
+    hipLaunchKernelGGL(k_sp_a, dim3(nb), dim3(SP_T), 0, s, a);
+    hipLaunchKernelGGL(k_sp_b, dim3(nb), dim3(SP_T), 0, s, a);
+    hipLaunchKernelGGL(k_sp_c, dim3(nb), dim3(SP_T), 0, s, a);
     return hipGetLastError();
 }
 

@@ -186,7 +186,7 @@ def test_system_rule(eng_mod, so, kind):
     assert 0 < eng.stats().sys_rounds < n // 4, eng.stats().sys_rounds   # planned sub-batches, not a replay
 
 
-@pytest.mark.parametrize("kind", ["param", "mixed"])
+@pytest.mark.parametrize("kind", ["param", "param06", "mixed"])
 def test_system_rule_large(eng_mod, so, kind):
     """SystemRules at scale through the planner: config 4's shape (2 Mi
     events, 1k resources, param rules, inbound QPS at 0.8x the offered rate)

@@ -226,10 +226,13 @@ def system_large(kind, seed=43):
     ``frac`` x the offered rate; "mixed" = config 3's traffic (flow rules of all
     four controllers, THREAD exits, acquireCount 1-5) with an inbound-QPS rule
     and a thread rule that both fire; three batches."""
-    if kind == "param":
+    if kind in ("param", "param06"):
+        # param06: the inbound-QPS rule at 0.6x, where it fires between the
+        # ParamFlow blocks (the planner's inert entries, sf_system.h)
         R, n = 1000, 1 << 21
         rules, batch = trace.param_zipf(R, n, 200_000, duration_ms=4000, seed=seed)
-        sysr = [abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=0.8 * n / 4.0,
+        frac = 0.8 if kind == "param" else 0.6
+        sysr = [abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=frac * n / 4.0,
                                    avg_rt=-1, max_thread=-1)]
         return dict(cfg=abi.default_config(max_resources=R, max_batch=batch.n, param_capacity=1 << 22),
                     param=rules, batches=[batch], nodes=list(range(0, R, 9)), system=sysr, status=(0.0, 0.0))
