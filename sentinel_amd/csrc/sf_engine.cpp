@@ -55,6 +55,7 @@ struct sf_engine {
     hipEvent_t ev_core[2]{};                         // the verdicts of the slot's batch are written
     SysRule sys{};                  // SystemRuleManager statics; sys.check: batches go through the planner
     SysPlanDev* sys_plan = nullptr; SysExitQ* sys_pa = nullptr; SysEntQ* sys_pb = nullptr;
+    uint8_t* sys_ibuf = nullptr;                  // the planner's inert flags (sys_plan)
     uint8_t* sys_mask = nullptr;    // [max_batch] planner verdicts (sf_system.h)
     // rules
     std::vector<uint32_t> flow_pos;        // loaded valid rule index -> CSR position
@@ -206,7 +207,7 @@ void sf_destroy(sf_engine* e) {
                      e->ml_order, e->ml_len, e->ml_off, e->ml_bytes, e->ml_out, e->ml_tmp};
     for (void* p : tptrs) if (p) hipFree(p);
     if (e->agg) hipFree(e->agg);
-    void* sptrs[] = {e->sys_plan, e->sys_pa, e->sys_pb, e->sys_mask};
+    void* sptrs[] = {e->sys_plan, e->sys_pa, e->sys_pb, e->sys_mask, e->sys_ibuf};
     for (void* p : sptrs) if (p) hipFree(p);
     void* dptrs[] = {(void*)e->dg.rr_of, (void*)e->dg.off, (void*)e->dg.rules, e->dg.state, e->dgw.keys_in,
                      e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
@@ -1046,6 +1047,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
             HIP_TRY(hipMalloc((void**)&e->sys_pb, SYS_PLAN_BLOCKS * sizeof(SysEntQ)));
             HIP_TRY(hipMalloc((void**)&e->sys_mask, e->cfg.max_batch));
         }
+        if (!e->sys_ibuf && e->st.n_prule) HIP_TRY(hipMalloc((void**)&e->sys_ibuf, SYS_PLAN_CAP));
         HIP_TRY(hipMemsetAsync(w.err, 0, sizeof(int32_t), ss));
         if (pre) {
             const hipError_t pe = (*pre)(ss, w.err);
@@ -1058,7 +1060,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         uint32_t p = 0, rounds = 0;
         while (p < n) {
             hipError_t le = sys_plan(stl, b, dv.status, e->sys_mask, e->sys, e->en, p, e->sys_plan, e->sys_pa,
-                                     e->sys_pb, s, true);
+                                     e->sys_pb, s, e->sys_ibuf);
             if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("system plan: ") + hipGetErrorString(le));
             uint32_t qi[2] = {0, 0};                        // q, inert entries planned
             static_assert(offsetof(SysPlanDev, n_inert) == offsetof(SysPlanDev, q) + 4, "q, n_inert adjacent");

@@ -257,12 +257,12 @@ struct SysPlanDev {
 
 // Plan the events from p of batch b (whole batch, base 0): mask[i] for the
 // IN entries of [p, q), plan->q.  vstatus: the batch's verdicts (before p).
-// inert: this engine decides the entries (not a merged node stream), so an
-// unknown entry its first ParamFlow rule certainly blocks is planned SYS_INERT
-// instead of ending the sub-batch (param_inert).
+// ibuf ([SYS_PLAN_CAP] scratch, or null): this engine decides the entries (not
+// a merged node stream), so an unknown entry its first ParamFlow rule certainly
+// blocks is planned SYS_INERT instead of ending the sub-batch (param_inert).
 hipError_t sys_plan(const DevState& st, const DevBatch& b, const uint8_t* vstatus, uint8_t* mask, const SysRule& r,
                     const EntryNode* en, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb, hipStream_t s,
-                    bool inert = false);
+                    uint8_t* ibuf = nullptr);
 // After [p, q) is decided (verdicts in out, ENTRY_NODE still at p): the exact
 // system verdict of every SYS_INERT entry of [p, q); a fired check turns its
 // ParamFlow block into the SystemBlockException SystemSlot threw first.
@@ -270,5 +270,6 @@ hipError_t sys_plan_fix(const DevState& st, const DevBatch& b, const DevVerdicts
                         const SysRule& r, uint32_t p, uint32_t q, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb,
                         hipStream_t s);
 constexpr uint32_t SYS_PLAN_BLOCKS = 512;       // SP_NB (sf_system.hip): size of pa / pb
+constexpr uint32_t SYS_PLAN_CAP = SYS_PLAN_BLOCKS * 4096;   // events per plan (size of ibuf)
 
 }  // namespace sf

@@ -21,6 +21,7 @@ namespace sf {
 constexpr int SP_T = 256, SP_RUN = 16, SP_BLK = SP_T * SP_RUN;   // 4096 events per block
 constexpr uint32_t SP_NB = SYS_PLAN_BLOCKS;                       // blocks per plan
 constexpr uint32_t SP_CAP = SP_NB * SP_BLK;                       // 2 Mi events per plan
+static_assert(SP_CAP == SYS_PLAN_CAP, "sf_system.h SYS_PLAN_CAP");
 
 struct SysPlanArgs {
     const int64_t* ts; const int32_t* cnt; const uint8_t* flags; const int64_t* eref; const int64_t* cts;
@@ -40,6 +41,7 @@ struct SysPlanArgs {
     DevState st;
     DevBatch b;
     uint8_t* ostatus; uint16_t* orule;
+    uint8_t* ibuf;                          // [SP_CAP] param_inert of event p + k (k_sp_inert)
 };
 
 __global__ void k_sp_init(SysPlanArgs a, const EntryNode* en) {
@@ -97,7 +99,16 @@ __device__ __forceinline__ SysExitQ exit_q(const SysPlanArgs& a, uint32_t i) {
     return sys_exit_q(a.ts, a.cnt, a.flags, a.eref, a.cts, a.vstatus, a.exact ? a.plan->lim : a.p, i, a.r.max_rt);
 }
 __device__ __forceinline__ bool inert_at(const SysPlanArgs& a, uint32_t i) {
-    return a.inert && param_inert(a.st, a.b, i, a.cnt[i], a.ts[i]);
+    return a.inert && a.ibuf[i - a.p] != 0;
+}
+// one thread per event of [p, lim): the table probes of param_inert, all in
+// flight at once (the passes read the flags)
+__global__ void k_sp_inert(SysPlanArgs a) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x, i = a.p + k;
+    if (i >= a.plan->lim) return;
+    const uint8_t f = a.flags[i];
+    const bool in = (f & SF_EV_IN) && !(f & (SF_EV_EXIT | SF_EV_BLOCKED));
+    a.ibuf[k] = (in && param_inert(a.st, a.b, i, a.cnt[i], a.ts[i])) ? 1 : 0;
 }
 // IN entries that reach SystemSlot (an SF_EV_BLOCKED entry was blocked by
 // AuthoritySlot before it: certainly blocked, no system verdict)
@@ -255,7 +266,8 @@ __global__ void k_sp_done(SysPlanDev* pl) {
 }
 
 static SysPlanArgs plan_args(const DevState& st, const DevBatch& b, const uint8_t* vstatus, uint8_t* mask,
-                             const SysRule& r, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb) {
+                             const SysRule& r, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb,
+                             uint8_t* ibuf) {
     SysPlanArgs a{};
     a.ts = b.ts; a.cnt = b.cnt; a.flags = b.flags; a.eref = b.eref; a.cts = b.cts;
     a.vstatus = vstatus; a.mask = mask; a.n = b.n; a.p = p; a.r = r;
@@ -263,16 +275,18 @@ static SysPlanArgs plan_args(const DevState& st, const DevBatch& b, const uint8_
     a.interval_sec = st.interval / 1000.0;
     a.plan = plan; a.pa = pa; a.pb = pb;
     a.st = st; a.b = b;
+    a.ibuf = ibuf;
     return a;
 }
 
 hipError_t sys_plan(const DevState& st, const DevBatch& b, const uint8_t* vstatus, uint8_t* mask, const SysRule& r,
                     const EntryNode* en, uint32_t p, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb, hipStream_t s,
-                    bool inert) {
-    SysPlanArgs a = plan_args(st, b, vstatus, mask, r, p, plan, pa, pb);
-    a.inert = inert && st.n_prule != 0;
+                    uint8_t* ibuf) {
+    SysPlanArgs a = plan_args(st, b, vstatus, mask, r, p, plan, pa, pb, ibuf);
+    a.inert = ibuf && st.n_prule != 0;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(SP_NB, ((uint64_t)(b.n - p) + SP_BLK - 1) / SP_BLK);
     hipLaunchKernelGGL(k_sp_init, dim3(1), dim3(64), 0, s, a, en);
+    if (a.inert) hipLaunchKernelGGL(k_sp_inert, dim3(nb * (SP_BLK / 256)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_sp_a, dim3(nb), dim3(SP_T), 0, s, a);
     hipLaunchKernelGGL(k_sp_b, dim3(nb), dim3(SP_T), 0, s, a);
     hipLaunchKernelGGL(k_sp_c, dim3(nb), dim3(SP_T), 0, s, a);
@@ -284,7 +298,7 @@ hipError_t sys_plan_fix(const DevState& st, const DevBatch& b, const DevVerdicts
                         const SysRule& r, uint32_t p, uint32_t q, SysPlanDev* plan, SysExitQ* pa, SysEntQ* pb,
                         hipStream_t s) {
     if (q <= p) return hipSuccess;
-    SysPlanArgs a = plan_args(st, b, out.status, (uint8_t*)mask, r, p, plan, pa, pb);
+    SysPlanArgs a = plan_args(st, b, out.status, (uint8_t*)mask, r, p, plan, pa, pb, nullptr);
     a.exact = true;
     a.ostatus = out.status; a.orule = out.rule;
     const uint32_t nb = (uint32_t)(((uint64_t)(q - p) + SP_BLK - 1) / SP_BLK);
