@@ -548,6 +548,69 @@ SF_HD int param_pass_single(const ParamTable& pt, uint32_t res, int rule_k, cons
     return 1;
 }
 
+// One QPS-grade rule (default or throttle behaviour) over the occurrences of
+// one value, in order, with the (rule, value) state in registers: exactly
+// param_pass_single applied occurrence by occurrence (ParamFlowChecker
+// :139-219 / :222-273), one table find before and one write after.  `live`
+// (bit o: occurrence o reaches this rule) loses the occurrences it blocks;
+// now_of / acq_of / wait_of index the occurrences.
+template <class NOW, class ACQ, class WAIT>
+SF_HD uint64_t param_run_rule(const ParamTable& pt, uint32_t res, int rule_k, const DevParamRule& r,
+                              const DevHotItem* items, uint32_t tag, uint64_t bits, uint64_t live, NOW now_of,
+                              ACQ acq_of, WAIT wait_of) {
+    int64_t token_count = j_d2l(r.count);
+    for (int k = 0; k < r.item_cnt; k++) {
+        const DevHotItem& it = items[r.item_off + k];
+        if (it.tag == tag && it.bits == bits) { token_count = it.count; break; }
+    }
+    const uint64_t hi = pkey_hi(res, PK_RULE, (uint32_t)rule_k, tag);
+    ParamSlot* sl = pt.find(hi, bits);
+    bool ex = sl != nullptr, dirty = false;
+    int64_t A = ex ? sl->a : 0, B = ex ? sl->b : 0;
+    const bool rl = r.behavior == SF_BEHAVIOR_RATE_LIMITER;
+    const int64_t max_count = wadd(token_count, r.burst);
+    for (uint64_t m = live; m; m &= m - 1) {
+        const int o = __builtin_ctzll(m);
+        const int64_t now = now_of(o);
+        const int32_t acq = acq_of(o);
+        bool ok;
+        if (token_count == 0) ok = false;
+        else if (rl) {
+            const int64_t cost = j_round(1.0 * 1000 * acq * (double)r.duration_sec / (double)token_count);
+            if (!ex) { ex = true; A = now; ok = true; }
+            else {
+                const int64_t expected = A + cost;
+                ok = expected <= now || expected - now < r.max_queue_ms;
+                if (ok) {
+                    A = now;
+                    const int64_t w = expected - now;
+                    if (w > 0) { A = expected; wait_of(o, w); }
+                }
+            }
+        } else if (acq > max_count) ok = false;
+        else if (!ex) { ex = true; A = now; B = max_count - acq; ok = true; }
+        else {
+            const int64_t pass_time = now - A;
+            if (pass_time > wmul(r.duration_sec, 1000)) {
+                const int64_t to_add = jdiv(wmul(pass_time, token_count), wmul(r.duration_sec, 1000));
+                const int64_t nq = wadd(to_add, B) > max_count ? (max_count - acq) : wsub(wadd(B, to_add), acq);
+                ok = nq >= 0;
+                if (ok) { B = nq; A = now; }
+            } else {
+                ok = B - acq >= 0;
+                if (ok) B -= acq;
+            }
+        }
+        if (ok) dirty = true;
+        else live &= ~(1ull << o);
+    }
+    if (dirty) {
+        if (!sl) sl = pt.insert(hi, bits);
+        if (sl) { sl->a = A; sl->b = B; }
+    }
+    return live;
+}
+
 // ============================================================ the segment
 struct SegIO {          // sorted-order batch arrays
     const int64_t* ts; const int32_t* cnt; const uint8_t* flags;

@@ -1182,15 +1182,20 @@ static HeavyCtx heavy_ctx(const Work& w) {
 // argument index (heavy_mode).  ParamFlowChecker's state is per (rule, value)
 // (ParameterMetric token / time maps) and the node counters are only summed,
 // so events of different values are independent: the wavefront takes 64
-// events at a time and runs them in rounds, round r holding every lane whose
-// value occurred r times before in the 64 (an event sees its value's state
-// after all earlier events of that value).  Lanes of one round only touch
-// different keys; the table's finds all complete before any insert of the
-// round (lock-step).  Verdict inputs go to the pass bits, v_wait (throttled
-// passes) and v_rule (the blocking rule); k_heavy_fill and k_heavy_apply
-// then do the StatisticSlot accounting as for the other window modes.
+// events at a time, and the first lane of each distinct value in the 64 runs
+// that value's events in order, rule by rule, with the (rule, value) state in
+// registers (param_run_rule: one table find and one write per rule, however
+// often the value recurs -- a Zipf head value recurs in most groups).  The
+// finds of a rule all complete before any of its inserts (the wavefront runs
+// them in lock-step; distinct values never share a key).  Verdict inputs go to
+// the pass bits, v_wait (throttled passes) and v_rule (the blocking rule);
+// k_heavy_fill and k_heavy_apply then do the StatisticSlot accounting as for
+// the other window modes.
 __device__ void heavy_param(const DevState& st, const SegIO& io, const HeavyCtx& hc, uint32_t res, uint32_t lo,
                             uint32_t hi) {
+    __shared__ int64_t s_now[64], s_wait[64];
+    __shared__ int32_t s_c[64];
+    __shared__ uint8_t s_rule[64], s_ok[64];
     const int lane = (int)(threadIdx.x & 63);
     const uint32_t p0 = st.prule_off[res], np = st.prule_off[res + 1] - p0;
     const int32_t pidx = st.prules[p0].param_idx;
@@ -1207,43 +1212,41 @@ __device__ void heavy_param(const DevState& st, const SegIO& io, const HeavyCtx&
         if ((int32_t)na > pidx) { tag = io.atag[(size_t)pidx * io.n + jc]; bits = io.abits[(size_t)pidx * io.n + jc]; }
         const bool sysb = valid && (io.flags[jc] & EVF_SYSBLK);   // blocked before ParamFlowSlot
         const bool key = valid && !sysb && tag != SF_TAG_NULL;  // a null value skips every rule (passCheck :53-60)
-        // rank of this event among the earlier events of its value in the 64
-        unsigned long long pend = __ballot(key);
-        int rank = 0, maxr = 0;
+        s_now[lane] = now; s_c[lane] = c; s_wait[lane] = 0; s_rule[lane] = 0; s_ok[lane] = 0;
+        // the lanes of each distinct value: `mine` on the value's first lane
+        unsigned long long pend = __ballot(key), mine = 0;
         while (pend) {
             const int l = __ffsll((long long)pend) - 1;
             const uint32_t kt = (uint32_t)__builtin_amdgcn_readlane((int)tag, l);
             const uint64_t kb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits >> 32), l) << 32) |
                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, l);
             const unsigned long long same = __ballot(key && tag == kt && bits == kb);
-            if ((same >> lane) & 1ull) rank = __popcll(same & ((1ull << lane) - 1ull));
-            maxr = max(maxr, __popcll(same) - 1);
+            if (lane == l) mine = same;
             pend &= ~same;
         }
-        bool blocked = sysb;
-        int64_t wait = 0;
-        int rule = 0;
-        for (int r = 0; r <= maxr; r++) {
-            if (valid && !sysb && rank == r) {
-                if (key) {
-                    for (uint32_t k = 0; k < np; k++) {
-                        int64_t w = 0;
-                        if (!param_pass_value(pt, res, (int)k, st.prules[p0 + k], st.items, now, c, tag, bits, io, &w)) {
-                            blocked = true; rule = (int)k; break;
-                        }
-                        if (w > 0) wait += w;
-                    }
-                }
-                if (!blocked) pm_thread_event(pt, res, pm_init, io, j, na, +1);   // ParamFlowStatisticEntryCallback
+        __syncthreads();
+        if (mine) {
+            uint64_t live = mine;
+            for (uint32_t k = 0; k < np && live; k++) {
+                const uint64_t before = live;
+                live = param_run_rule(pt, res, (int)k, st.prules[p0 + k], st.items, tag, bits, live,
+                                      [&](int o) { return s_now[o]; }, [&](int o) { return s_c[o]; },
+                                      [&](int o, int64_t w) { s_wait[o] += w; });
+                for (uint64_t m = before & ~live; m; m &= m - 1) s_rule[__builtin_ctzll(m)] = (uint8_t)k;
             }
+            for (uint64_t m = live; m; m &= m - 1) s_ok[__builtin_ctzll(m)] = 1;
+            // ParamFlowStatisticEntryCallback: the value's thread count, once for all its passes
+            if (live && ((pm_init >> pidx) & 1)) pm_thread_add(pt, res, pidx, tag, bits, __popcll(live));
         }
+        __syncthreads();
+        const bool blocked = sysb || (key && !s_ok[lane]);
         const unsigned long long pm = __ballot(valid && !blocked);
         if (lane == 0 && pm) {
             const uint32_t sh = q & 63;
             atomicOr(hc.passbits + (q >> 6), pm << sh);
             if (sh) atomicOr(hc.passbits + (q >> 6) + 1, pm >> (64 - sh));
         }
-        if (valid) { io.v_wait[j] = blocked ? 0 : (int32_t)wait; io.v_rule[j] = (uint16_t)rule; }
+        if (valid) { io.v_wait[j] = blocked ? 0 : (int32_t)s_wait[lane]; io.v_rule[j] = blocked && key ? s_rule[lane] : 0; }
     }
     if (lane == 0) st.pm_init[res] = pm_init;
 }
