@@ -1850,6 +1850,41 @@ hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipSt
 
 static inline unsigned blocks(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
+// Several buffer fills in one launch (each hipMemsetAsync is a launch of its
+// own: the SystemRule planner's small sub-batches paid more for the launch gaps
+// than for the bytes).  Range blockIdx.y: a byte head up to 16-B alignment,
+// 16-B stores, a byte tail.
+struct FillSet {
+    static constexpr int MAX = 8;
+    uint8_t* p[MAX]; size_t n[MAX]; uint32_t v[MAX];   // v: the byte repeated
+    int k = 0;
+    void add(void* ptr, size_t bytes, uint8_t byte) {
+        if (!ptr || !bytes) return;
+        p[k] = (uint8_t*)ptr; n[k] = bytes; v[k] = 0x01010101u * byte; k++;
+    }
+};
+__global__ void k_fill(FillSet f) {
+    const int r = blockIdx.y;
+    uint8_t* p = f.p[r];
+    const size_t n = f.n[r];
+    const uint32_t v = f.v[r];
+    size_t head = (16 - ((uintptr_t)p & 15)) & 15;
+    if (head > n) head = n;
+    const size_t body = (n - head) / 16, tail0 = head + body * 16;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+    if (t < head) p[t] = (uint8_t)v;
+    if (t < n - tail0) p[tail0 + t] = (uint8_t)v;
+    uint4* q = (uint4*)(p + head);
+    const uint4 w = make_uint4(v, v, v, v);
+    for (size_t i = t; i < body; i += stride) q[i] = w;
+}
+static void launch_fill(const FillSet& f, hipStream_t s) {
+    if (!f.k) return;
+    size_t most = 0;
+    for (int r = 0; r < f.k; r++) most = std::max(most, f.n[r] / 16 + 16);
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)std::min<size_t>(2048, (most + 255) / 256), (unsigned)f.k), dim3(256), 0, s, f);
+}
+
 using PcIter = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, EntryCount, int64_t>;
 using HeadIter = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, HeadFlag, uint32_t>;
 // rocprim has no tuned scan configs for gfx950 (its default is 256 threads x
@@ -1921,10 +1956,12 @@ hipError_t launch_init_state(const DevState& st, hipStream_t s) {
 // head of the decide phase (the sort phase is the longer of the two)
 static void launch_classify(const DevState& st, Work& w, const DevBatch& b, hipStream_t s, hipEvent_t* ev, bool timing) {
     const uint32_t n = b.n;
-    hipMemsetAsync(w.counters, 0, 16 * sizeof(uint32_t), s);
-    hipMemsetAsync(w.lcounts, 0, 2 * LCLS * sizeof(uint32_t), s);
-    hipMemsetAsync(w.passbits, 0, ((size_t)n / 64 + 2) * 8, s);
-    if (st.n_stream_rules) hipMemsetAsync(w.lxfar, 0, ((size_t)n / 64 + 2) * 8, s);
+    FillSet f;
+    f.add(w.counters, 16 * sizeof(uint32_t), 0);
+    f.add(w.lcounts, 2 * LCLS * sizeof(uint32_t), 0);
+    f.add(w.passbits, ((size_t)n / 64 + 2) * 8, 0);
+    if (st.n_stream_rules) f.add(w.lxfar, ((size_t)n / 64 + 2) * 8, 0);
+    launch_fill(f, s);
     const uint32_t max_seg = n < st.R ? n : st.R;
     if (timing) hipEventRecord(ev[10], s);
     hipLaunchKernelGGL(k_classify, dim3(blocks(max_seg, 1024)), dim3(1024), 0, s, st, w, w.s_ts);
@@ -2206,14 +2243,18 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     // independent, but here at the head of the decide phase rather than in the
     // sort phase, the longer of the two pipelined phases (k_classify does not
     // read them; every deciding kernel does)
-    if (b.eref || st.n_stream_rules) hipMemsetAsync(w.exit_of, 0xff, (size_t)n * 4, s);   // (read by k_gather_exit, k_thr_rec)
+    {
+        FillSet f;
+        if (b.eref || st.n_stream_rules) f.add(w.exit_of, (size_t)n * 4, 0xff);   // (read by k_gather_exit, k_thr_rec)
+        // waits and rule indices are zero for almost every event: clear them with
+        // coalesced stores, then the deciding kernels scatter only the nonzero ones
+        f.add(out.wait, (size_t)n * sizeof(int32_t), 0);
+        f.add(out.rule, (size_t)n * sizeof(uint16_t), 0);
+        launch_fill(f, s);
+    }
     if (b.eref)
         hipLaunchKernelGGL(k_gather_exit, dim3(blocks(n, 256)), dim3(256), 0, s, b, w.perm, w.s_flags,
                            w.head_scan, w.seg_start, w.s_eref, w.s_cts, w.exit_of, st.err);
-    // waits and rule indices are zero for almost every event: clear them with
-    // coalesced stores, then the deciding kernels scatter only the nonzero ones
-    if (out.wait) hipMemsetAsync(out.wait, 0, (size_t)n * sizeof(int32_t), s);
-    if (out.rule) hipMemsetAsync(out.rule, 0, (size_t)n * sizeof(uint16_t), s);
     hipEventRecord(ev[5], s);                      // fork
     // (the THREAD / RateLimiter class exists only with such rules loaded)
     if (st.n_stream_rules) launch_thr_prep(w, b, s);
