@@ -7,7 +7,7 @@ if [ -z "$NO_TESTS" ]; then
   tail -2 $OUT/tests.log
 fi
 for v in ${VARIANTS:-new old new old}; do
-  if [ $v = old ]; then export $VAR=1; else unset $VAR; fi
+  if [ $v = old ]; then export $VAR=${VAR_VALUE:-1}; else unset $VAR; fi
   timeout -k 10 300 python3 -u bench.py --steps 10 --warmup 3 --no-legs --no-degrade --no-metric-log ${BENCH_ARGS} > $OUT/b_$v.json 2> $OUT/b_$v.err || { echo BENCH_FAILED $v; tail -20 $OUT/b_$v.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open('$OUT/b_$v.json')); print('$v', d['ms_per_step'], d.get('parity',{}).get('exact'), d.get('parity',{}).get('steady_state',{}).get('exact'))"
   if [ -n "$LEG" ]; then
