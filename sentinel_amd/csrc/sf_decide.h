@@ -733,7 +733,10 @@ SF_HD void breakers_of(const DevState& st, uint32_t res, uint32_t* b0, uint32_t*
 #ifndef SF_EV_CH
 #define SF_EV_CH 8
 #endif
-template <int MAXS, uint32_t EV_CH = SF_EV_CH>
+// PF false: the engine has no ParamFlow and no degrade rules loaded (the host
+// knows it per launch), so that code is compiled out of the lane (fewer live
+// registers, more wavefronts per SIMD)
+template <int MAXS, uint32_t EV_CH = SF_EV_CH, bool PF = true>
 SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uint32_t lo, uint32_t hi) {
     NodeWin<MAXS> nd;
     nw_load_row(nd, st, res);
@@ -745,13 +748,13 @@ SF_HD void decide_segment(const DevState& st, const SegIO& io, uint32_t res, uin
     // is exact because this lane owns the resource (a DefaultController keeps none)
     DevRuleState rs0 = (rd.flags & RD_STATE0) ? st.rstate[r0] : fresh_rule_state();
     uint32_t p0 = 0, p1 = 0;
-    if (rd.flags & RD_PRULE) { p0 = st.prule_off[res]; p1 = st.prule_off[res + 1]; }
+    if (PF && (rd.flags & RD_PRULE)) { p0 = st.prule_off[res]; p1 = st.prule_off[res + 1]; }
     const int nprules = (int)(p1 - p0);
     uint8_t pm_init = nprules ? st.pm_init[res] : 0;
     bool pm_exists = pm_init != 0;
     ParamTable pt{st.ptab, st.pcap_mask, st.err, st.pins};
     uint32_t cb0 = 0, cb1 = 0;                                 // DegradeSlot breakers (this lane owns them)
-    if (rd.flags & RD_BRK) breakers_of(st, res, &cb0, &cb1);
+    if (PF && (rd.flags & RD_BRK)) breakers_of(st, res, &cb0, &cb1);
 
     // The lane's events are read EV_CH at a time with all loads in flight together
     // (each cache line of the sorted arrays is then fetched once, not once per

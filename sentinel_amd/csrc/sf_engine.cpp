@@ -39,6 +39,9 @@ static int fail(int code, const std::string& msg) {
                         std::string(#expr ": ") + hipGetErrorString(_e));               \
     } while (0)
 
+// a device copy of host event arrays, remembered by their addresses (stage_in_events)
+struct StageBuf { void* p = nullptr; size_t bytes = 0; const void* key[5] = {}; uint32_t n = 0; };
+
 struct sf_engine {
     sf_config cfg{};
     hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;   // 4: the wave walk
@@ -67,7 +70,7 @@ struct sf_engine {
     // staging for host-memory batches
     void* stage_in = nullptr; size_t stage_in_bytes = 0;
     void* stage_out = nullptr; size_t stage_out_bytes = 0;
-    void* plan_stage = nullptr; size_t plan_stage_bytes = 0;   // sf_system_plan / sf_entry_node_add inputs
+    StageBuf plan_sb, en_sb;                       // sf_system_plan / sf_entry_node_add inputs
     hipEvent_t evs[2][SF_NUM_EVENTS]{};   // per Work set: fork/join and timing events of its batch
     bool timed[2] = {false, false};       // that batch ran with timing on and is not yet in stats
     bool timing = false;
@@ -194,7 +197,7 @@ void sf_destroy(sf_engine* e) {
     for (Work& w : e->w) free_work(w);
     void* ptrs[] = {e->st.second, e->st.borrow, e->st.minute, e->st.threads, (void*)e->st.rule_off,
                     (void*)e->st.rules, e->st.rstate, (void*)e->st.prule_off, e->st.prules, (void*)e->st.items,
-                    e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out, e->plan_stage, e->st.pins,
+                    e->st.pm_init, e->st.ptab, e->st.err, e->stage_in, e->stage_out, e->plan_sb.p, e->en_sb.p, e->st.pins,
                     e->st.xw_stats, (void*)e->st.rdesc, e->st.prio_seen};
     for (void* p : ptrs) if (p) hipFree(p);
     for (void* p : e->user_allocs) hipFree(p);
@@ -1353,9 +1356,11 @@ int sf_submit_forced(sf_engine* e, const sf_event_batch* in, sf_verdicts* out, c
 }
 
 // stage host IN-event arrays (ts, count, flags, entry_ref, create_ts) + optional
-// verdicts at a device scratch; DevBatch over them
-static int stage_in_events(sf_engine* e, const sf_event_batch* in, const uint8_t* status, uint32_t n_status,
-                           DevBatch& b, uint8_t** dstatus) {
+// verdicts at a device scratch (StageBuf); DevBatch over them.  keep: the
+// scratch already holds these event arrays (a later round of the same merged
+// stream): only the verdicts are copied.
+static int stage_in_events(sf_engine* e, StageBuf& sb, const sf_event_batch* in, const uint8_t* status,
+                           uint32_t n_status, DevBatch& b, uint8_t** dstatus, bool keep = false) {
     const uint32_t n = in->n;
     size_t need = 0;
     const size_t o_ts = need; need += align_up((size_t)n * 8);
@@ -1364,19 +1369,25 @@ static int stage_in_events(sf_engine* e, const sf_event_batch* in, const uint8_t
     const size_t o_er = need; need += align_up((size_t)n * 8);
     const size_t o_ct = need; need += align_up((size_t)n * 8);
     const size_t o_st = need; need += align_up((size_t)n + 1);
-    if (need > e->plan_stage_bytes) {
-        if (e->plan_stage) hipFree(e->plan_stage);
-        e->plan_stage = nullptr; e->plan_stage_bytes = 0;
-        HIP_TRY(hipMalloc(&e->plan_stage, need));
-        e->plan_stage_bytes = need;
+    const void* key[5] = {in->ts_ms, in->count, in->flags, in->entry_ref, in->create_ts};
+    keep = keep && sb.p && sb.n == n && std::equal(key, key + 5, sb.key) && need <= sb.bytes;
+    if (need > sb.bytes) {
+        if (sb.p) hipFree(sb.p);
+        sb.p = nullptr; sb.bytes = 0; sb.n = 0;
+        HIP_TRY(hipMalloc(&sb.p, need));
+        sb.bytes = need;
     }
-    char* base = (char*)e->plan_stage;
+    char* base = (char*)sb.p;
     hipStream_t s = e->stream;
-    HIP_TRY(hipMemcpyAsync(base + o_ts, in->ts_ms, (size_t)n * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(base + o_cnt, in->count, (size_t)n * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(base + o_fl, in->flags, n, hipMemcpyHostToDevice, s));
-    if (in->entry_ref) HIP_TRY(hipMemcpyAsync(base + o_er, in->entry_ref, (size_t)n * 8, hipMemcpyHostToDevice, s));
-    if (in->create_ts) HIP_TRY(hipMemcpyAsync(base + o_ct, in->create_ts, (size_t)n * 8, hipMemcpyHostToDevice, s));
+    if (!keep) {
+        HIP_TRY(hipMemcpyAsync(base + o_ts, in->ts_ms, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(base + o_cnt, in->count, (size_t)n * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(base + o_fl, in->flags, n, hipMemcpyHostToDevice, s));
+        if (in->entry_ref) HIP_TRY(hipMemcpyAsync(base + o_er, in->entry_ref, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        if (in->create_ts) HIP_TRY(hipMemcpyAsync(base + o_ct, in->create_ts, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        std::copy(key, key + 5, sb.key);
+        sb.n = n;
+    }
     if (status && n_status) HIP_TRY(hipMemcpyAsync(base + o_st, status, n_status, hipMemcpyHostToDevice, s));
     b = DevBatch{};
     b.n = n;
@@ -1410,7 +1421,9 @@ int sf_system_plan(sf_engine* e, const sf_event_batch* in, const uint8_t* status
     }
     DevBatch b;
     uint8_t* dstatus = nullptr;
-    { const int rc = stage_in_events(e, in, status, p, b, &dstatus); if (rc) return rc; }
+    // a later round of the same merged stream (p > 0, same arrays): the events
+    // staged for the round before are reused, only the verdicts are copied
+    { const int rc = stage_in_events(e, e->plan_sb, in, status, p, b, &dstatus, p > 0); if (rc) return rc; }
     hipStream_t s = e->stream;
     DevState stl = e->st;
     hipError_t le = sys_plan(stl, b, dstatus, e->sys_mask, e->sys, e->en, p, e->sys_plan, e->sys_pa, e->sys_pb, s);
@@ -1434,7 +1447,7 @@ int sf_entry_node_add(sf_engine* e, const sf_event_batch* in, const uint8_t* sta
     if (!in->n) return SF_OK;
     DevBatch b;
     uint8_t* dstatus = nullptr;
-    { const int rc = stage_in_events(e, in, status, in->n, b, &dstatus); if (rc) return rc; }
+    { const int rc = stage_in_events(e, e->en_sb, in, status, in->n, b, &dstatus); if (rc) return rc; }
     hipError_t le = launch_entry_node(e->st, b, dstatus, e->en, e->en_acc, e->stream);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
     HIP_TRY(hipStreamSynchronize(e->stream));

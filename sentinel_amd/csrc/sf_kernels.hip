@@ -224,8 +224,18 @@ __global__ void k_gather_exit(DevBatch b, const uint32_t* perm, const uint8_t* s
         s_cts[j] = b.ts[r];
         return;
     }
-    uint32_t a = seg_start[head_scan[j] - 1], e = j;          // entry in [segment start, j)
+    const uint32_t lo = seg_start[head_scan[j] - 1];          // entry in [segment start, j)
     if (r >= (int64_t)i) { *err = SF_ERR_INVALID; s_eref[j] = -1; s_cts[j] = 0; return; }
+    // galloping back from j (an entry is usually a few of its resource's events
+    // before its exit: the probes stay on the lines the neighbours read), then
+    // a binary search of the bracket
+    uint32_t a = lo, e = j;
+    for (uint32_t step = 1; j - lo > step; step <<= 1) {
+        const uint32_t m = j - step;
+        if ((int64_t)perm[m] < r) { a = m + 1; break; }
+        e = m;
+        if ((int64_t)perm[m] == r) { a = m; break; }
+    }
     while (a < e) { const uint32_t m = (a + e) >> 1; if ((int64_t)perm[m] < r) a = m + 1; else e = m; }
     if (a >= j || (int64_t)perm[a] != r) { *err = SF_ERR_INVALID; s_eref[j] = -1; s_cts[j] = 0; return; }
     s_eref[j] = a;
@@ -377,11 +387,14 @@ struct LightLists { const uint32_t* list; const uint32_t* counts; uint32_t off[L
 // One lane per light segment; thread t walks the length classes from the
 // longest down, so a wavefront holds segments of one class (similar length)
 // and the long ones are dispatched first.
-template <int MAXS>
 #ifndef SF_LIGHT_MINB
 #define SF_LIGHT_MINB 1
 #endif
-__global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_light(DevState st, SegIO io, const uint32_t* seg_start,
+#ifndef SF_LIGHT_NOPF_MINB
+#define SF_LIGHT_NOPF_MINB 1          // (3 wavefronts per SIMD: 96 B of spills, config 3 15.2 vs 14.1 ms)
+#endif
+template <int MAXS, bool PF>
+__global__ void __launch_bounds__(128, PF ? SF_LIGHT_MINB : SF_LIGHT_NOPF_MINB) k_decide_light(DevState st, SegIO io, const uint32_t* seg_start,
                                                       const uint32_t* seg_res, LightLists ll) {
     uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     int c = LCLS - 1;
@@ -392,7 +405,7 @@ __global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_light(DevState st
     }
     if (c < 0) return;
     const uint32_t s = ll.list[ll.off[c] + t];
-    decide_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
+    decide_segment<MAXS, SF_EV_CH, PF>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
 }
 
 // The lean QPS light segments (SM_LIGHTQ, > SHORT_MAX events) from the back
@@ -414,14 +427,14 @@ __global__ void __launch_bounds__(128) k_decide_light_qps(DevState st, SegIO io,
 
 // One lane per short light segment, from the dense short list (k_classify;
 // see SHORT_MAX).
-template <int MAXS>
-__global__ void __launch_bounds__(128, SF_LIGHT_MINB) k_decide_short(DevState st, SegIO io, const uint32_t* seg_start,
+template <int MAXS, bool PF>
+__global__ void __launch_bounds__(128, PF ? SF_LIGHT_MINB : SF_LIGHT_NOPF_MINB) k_decide_short(DevState st, SegIO io, const uint32_t* seg_start,
                                                       const uint32_t* seg_res, LightLists ll,
                                                       const uint32_t* n_short) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_short[0]) return;
     const uint32_t s = ll.list[ll.off[0] + t];
-    decide_segment<MAXS>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
+    decide_segment<MAXS, SF_EV_CH, PF>(st, io, seg_res[s], seg_start[s], seg_start[s + 1]);
 }
 
 // One lane per xflow group segment (sf_xflow.h): origin / context / RELATE
@@ -2216,6 +2229,24 @@ static void launch_thr_prep(Work& w, const DevBatch& b, hipStream_t s) {
                        w.segflag);
 }
 
+// the light lanes of a batch (k_classify's lists), longest class first; the
+// lean QPS walks only where a QPS DefaultController rule is loaded
+template <int MAXS, bool PF>
+static void launch_light(const DevState& st, const SegIO& io, const Work& w, const LightLists& ll, uint32_t max_seg,
+                         hipStream_t s3) {
+    const unsigned TD = 128;
+    hipLaunchKernelGGL((k_decide_light<MAXS, PF>), dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+                       w.seg_res, ll);
+    if (st.n_window_rules) {
+        hipLaunchKernelGGL(k_decide_light_qps<MAXS>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+                           w.seg_res, ll);
+        hipLaunchKernelGGL(k_decide_short_qps<MAXS>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+                           w.seg_res, ll, w.counters + 8);
+    }
+    hipLaunchKernelGGL((k_decide_short<MAXS, PF>), dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+                       w.seg_res, ll, w.counters + 8);
+}
+
 // Decide phase (stateful, batch order): the serial chains (k_heavy_stream)
 // start first, on A; QPS/WarmUp heavy segments on B, the light lanes on C;
 // then the verdicts are scattered back to submission order.
@@ -2308,31 +2339,16 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
                            w.seg_nsec, 1);
     }
 
-    const unsigned TD = 128;
     LightLists ll{w.light_list, w.lcounts, {}, {}};
     for (int c = 0; c < LCLS; c++) { ll.off[c] = w.loff[c]; ll.cap[c] = w.lcap[c]; }
+    // (no ParamFlow / degrade rule loaded: the lanes without that code)
+    const bool pf = st.n_prule != 0 || st.dg_rr_of != nullptr;
     if (st.S <= 2) {
-        hipLaunchKernelGGL(k_decide_light<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
-                           w.seg_res, ll);
-        if (st.n_window_rules) {   // (the lean QPS walk needs a QPS DefaultController rule)
-            hipLaunchKernelGGL(k_decide_light_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
-                               w.seg_res, ll);
-            hipLaunchKernelGGL(k_decide_short_qps<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
-                               w.seg_res, ll, w.counters + 8);
-        }
-        hipLaunchKernelGGL(k_decide_short<2>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
-                           w.seg_res, ll, w.counters + 8);
+        if (pf) launch_light<2, true>(st, io, w, ll, max_seg, s3);
+        else launch_light<2, false>(st, io, w, ll, max_seg, s3);
     } else {
-        hipLaunchKernelGGL(k_decide_light<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
-                           w.seg_start, w.seg_res, ll);
-        if (st.n_window_rules) {
-            hipLaunchKernelGGL(k_decide_light_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3,
-                               st, io, w.seg_start, w.seg_res, ll);
-            hipLaunchKernelGGL(k_decide_short_qps<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3,
-                               st, io, w.seg_start, w.seg_res, ll, w.counters + 8);
-        }
-        hipLaunchKernelGGL(k_decide_short<SF_MAX_SAMPLE_COUNT>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io,
-                           w.seg_start, w.seg_res, ll, w.counters + 8);
+        if (pf) launch_light<SF_MAX_SAMPLE_COUNT, true>(st, io, w, ll, max_seg, s3);
+        else launch_light<SF_MAX_SAMPLE_COUNT, false>(st, io, w, ll, max_seg, s3);
     }
     if (st.xmap) {
         if (st.S <= 2)

@@ -174,13 +174,13 @@ def submit_node(eng, batch: abi.HostBatch, seq: np.ndarray, comm=None) -> abi.Ho
         # this rank's events before merged[q] (all remaining ones after the last round)
         lq = n if q == m else int(np.searchsorted(seq, mseq[q]))
         mask = np.full(lq - lp, SYS_NONE, np.uint8)
-        sel = (li >= lp) & (li < lq)
-        mask[li[sel] - lp] = m_mask[my_m[sel]]
+        a, z = np.searchsorted(li, [lp, lq])                # (li and my_m are increasing: ranges, not masks)
+        mask[li[a:z] - lp] = m_mask[my_m[a:z]]
         decide_local(lq, mask)
         # verdicts of merged[p, q): owner's value, max over ranks
         vals = np.zeros(q - p, np.int32)
-        own = (my_m >= p) & (my_m < q)
-        vals[my_m[own] - p] = out.status[li[own]]
+        a, z = np.searchsorted(my_m, [p, q])
+        vals[my_m[a:z] - p] = out.status[li[a:z]]
         m_status[p:q] = comm.allreduce_max_i32(vals).astype(np.uint8)
         seg = abi.HostBatch(np.zeros(q - p, np.uint32), merged.ts_ms[p:q], merged.count[p:q], merged.flags[p:q],
                             entry_ref=np.where(m_eref[p:q] >= p, m_eref[p:q] - p,
