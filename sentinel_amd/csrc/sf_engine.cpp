@@ -444,6 +444,11 @@ static void acc_timing(sf_engine* e, int slot) {
     float cl = 0, li = 0, hd = 0, hf = 0, hs = 0;
     hipEventElapsedTime(&cl, ev[10], ev[2]);
     hipEventElapsedTime(&li, ev[5], ev[9]);
+    if (e->st.n_window_rules) {                    // the lean walks end on stream B
+        float lq = 0;
+        hipEventElapsedTime(&lq, ev[5], ev[16]);
+        li = std::max(li, lq);
+    }
     hipEventElapsedTime(&hd, ev[5], ev[7]);
     hipEventElapsedTime(&hf, ev[7], ev[8]);
     hipEventElapsedTime(&hs, ev[11], ev[12]);

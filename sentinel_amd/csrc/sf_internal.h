@@ -379,6 +379,6 @@ constexpr size_t ACC_BYTES = 72;                         // sizeof(Acc)
 // 5 fork, 6 join (stream B), 7 heavy decided, 8 heavy filled, 9 light decided, 10 before classify,
 // 11 stream start (stream C), 12 stream done (stream C), 13 stream fill + apply done (stream C),
 // 14 origin-node pass done (stream B)
-constexpr int SF_NUM_EVENTS = 16;
+constexpr int SF_NUM_EVENTS = 17;
 
 }  // namespace sf

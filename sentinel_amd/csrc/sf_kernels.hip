@@ -2231,16 +2231,18 @@ static void launch_thr_prep(Work& w, const DevBatch& b, hipStream_t s) {
 
 // the light lanes of a batch (k_classify's lists), longest class first; the
 // lean QPS walks only where a QPS DefaultController rule is loaded
+// (the lean QPS walks go on stream B after its heavy kernels, beside the
+// generic walks on C: different segments, different resources)
 template <int MAXS, bool PF>
 static void launch_light(const DevState& st, const SegIO& io, const Work& w, const LightLists& ll, uint32_t max_seg,
-                         hipStream_t s3) {
+                         hipStream_t s3, hipStream_t s2) {
     const unsigned TD = 128;
     hipLaunchKernelGGL((k_decide_light<MAXS, PF>), dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
                        w.seg_res, ll);
     if (st.n_window_rules) {
-        hipLaunchKernelGGL(k_decide_light_qps<MAXS>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+        hipLaunchKernelGGL(k_decide_light_qps<MAXS>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s2, st, io, w.seg_start,
                            w.seg_res, ll);
-        hipLaunchKernelGGL(k_decide_short_qps<MAXS>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
+        hipLaunchKernelGGL(k_decide_short_qps<MAXS>, dim3(blocks(max_seg, TD)), dim3(TD), 0, s2, st, io, w.seg_start,
                            w.seg_res, ll, w.counters + 8);
     }
     hipLaunchKernelGGL((k_decide_short<MAXS, PF>), dim3(blocks(max_seg, TD)), dim3(TD), 0, s3, st, io, w.seg_start,
@@ -2344,11 +2346,11 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     // (no ParamFlow / degrade rule loaded: the lanes without that code)
     const bool pf = st.n_prule != 0 || st.dg_rr_of != nullptr;
     if (st.S <= 2) {
-        if (pf) launch_light<2, true>(st, io, w, ll, max_seg, s3);
-        else launch_light<2, false>(st, io, w, ll, max_seg, s3);
+        if (pf) launch_light<2, true>(st, io, w, ll, max_seg, s3, s2);
+        else launch_light<2, false>(st, io, w, ll, max_seg, s3, s2);
     } else {
-        if (pf) launch_light<SF_MAX_SAMPLE_COUNT, true>(st, io, w, ll, max_seg, s3);
-        else launch_light<SF_MAX_SAMPLE_COUNT, false>(st, io, w, ll, max_seg, s3);
+        if (pf) launch_light<SF_MAX_SAMPLE_COUNT, true>(st, io, w, ll, max_seg, s3, s2);
+        else launch_light<SF_MAX_SAMPLE_COUNT, false>(st, io, w, ll, max_seg, s3, s2);
     }
     if (st.xmap) {
         if (st.S <= 2)
@@ -2359,6 +2361,7 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
                                w.seg_start, w.seg_res, w.seg_mode, w.n_seg);
     }
     hipEventRecord(ev[9], s3);                     // light done (also the join of C)
+    hipEventRecord(ev[16], s2);                    // the lean QPS walks done (after B's heavy kernels)
     hipEventRecord(ev[6], s2);                     // join B and C
     hipStreamWaitEvent(s, ev[6], 0);
     hipStreamWaitEvent(s, ev[9], 0);
