@@ -11,7 +11,8 @@ prefix [p, q) of the IN stream are fixed by the ENTRY_NODE at p alone.  Here
 the same planner runs on every rank over the node's merged IN stream:
 
 1. all-gather the IN events of the batch (global submission sequence numbers
-   order them; an exit's entry is found by its sequence number);
+   order them; an exit's entry is found by its sequence number): 24 B per IN
+   event, plus the exits' entry references and create times;
 2. ``sf_system_plan`` on the merged stream -> q and the forced SystemRule
    verdicts of merged[p, q) -- identical on every rank (same stream, same
    ENTRY_NODE, same rules);
@@ -52,6 +53,8 @@ class TorchComm:
         ns = [torch.zeros_like(n) for _ in range(world)]
         dist.all_gather(ns, n, group=self.group)
         ns = [int(v.item()) for v in ns]
+        if max(ns) == 0:                                  # (every rank knows: no second collective)
+            return np.zeros((x.shape[0], 0), np.int64)
         pad = np.zeros((x.shape[0], max(ns)), np.int64)
         pad[:, :x.shape[1]] = x
         t = torch.from_numpy(pad).to(self.device)
@@ -128,20 +131,30 @@ def submit_node(eng, batch: abi.HostBatch, seq: np.ndarray, comm=None) -> abi.Ho
     if eref is not None:
         r = eref[li]
         ref_seq = np.where(r >= 0, seq[np.clip(r, 0, None)], r)
-    mine = np.stack([seq[li], batch.ts_ms[li], batch.count[li].astype(np.int64), fl[li].astype(np.int64),
-                     ref_seq, cts])
-    allv = comm.allgather_i64(mine)
+    # every IN event as 3 words (sequence number, time, acquireCount | flags << 32);
+    # the exits' entry sequence numbers and create times in a second gather of
+    # the exits alone (24 B per IN entry instead of 48)
+    cnt_fl = (batch.count[li].astype(np.int64) & 0xFFFFFFFF) | (fl[li].astype(np.int64) << 32)
+    allv = comm.allgather_i64(np.stack([seq[li], batch.ts_ms[li], cnt_fl]))
+    xi = np.nonzero(fl[li] & abi.EV_EXIT)[0]
+    allx = comm.allgather_i64(np.stack([seq[li][xi], ref_seq[xi], cts[xi]]))
     order = np.argsort(allv[0], kind="stable")
     allv = allv[:, order]
     mseq = allv[0]
     m = mseq.size
-    rs = allv[4]
+    m_cnt = (allv[2] & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+    m_fl = ((allv[2] >> 32) & 0xFF).astype(np.uint8)
+    rs = np.full(m, -1, np.int64)
+    m_cts = np.zeros(m, np.int64)
+    if allx.shape[1]:
+        xp = np.searchsorted(mseq, allx[0])
+        rs[xp] = allx[1]
+        m_cts[xp] = allx[2]
     pos = np.searchsorted(mseq, np.clip(rs, 0, None))
     m_eref = np.where(rs >= 0, pos, rs)
     if m and (rs >= 0).any():
         assert (mseq[pos[rs >= 0]] == rs[rs >= 0]).all(), "exit of an IN entry that no rank holds"
-    merged = abi.HostBatch(np.zeros(m, np.uint32), allv[1], allv[2].astype(np.int32), allv[3].astype(np.uint8),
-                           entry_ref=m_eref, create_ts=allv[5])
+    merged = abi.HostBatch(np.zeros(m, np.uint32), allv[1], m_cnt, m_fl, entry_ref=m_eref, create_ts=m_cts)
     # where this rank's IN events sit in the merged stream
     my_m = np.searchsorted(mseq, seq[li]) if li.size else np.zeros(0, np.int64)
     m_status = np.zeros(m, np.uint8)
