@@ -483,8 +483,9 @@ int  sf_sync_packed(sf_engine* e, const sf_verdicts* out);
  *      sf_entry_node_add; p = q.
  * Host arrays; calls of one batch use increasing p.  A call with p > 0 and
  * the same event arrays (addresses and n) as the call before continues that
- * merged stream: its events are not copied to the device again (only the
- * verdicts of merged[0, p)), so the arrays must not change within a batch. */
+ * merged stream: its events are not copied to the device again, nor the
+ * verdicts already passed (only those added since the call before), so the
+ * arrays must not change within a batch except by appending verdicts. */
 int  sf_system_plan(sf_engine* e, const sf_event_batch* in_events, const uint8_t* status, uint32_t p,
                     uint32_t* q, uint8_t* sys_mask);
 int  sf_submit_forced(sf_engine* e, const sf_event_batch* in, sf_verdicts* out, const uint8_t* sys_mask);

@@ -40,7 +40,10 @@ static int fail(int code, const std::string& msg) {
     } while (0)
 
 // a device copy of host event arrays, remembered by their addresses (stage_in_events)
-struct StageBuf { void* p = nullptr; size_t bytes = 0; const void* key[5] = {}; uint32_t n = 0; };
+struct StageBuf {
+    void* p = nullptr; size_t bytes = 0; const void* key[5] = {}; uint32_t n = 0;
+    const uint8_t* st_src = nullptr; uint32_t st_n = 0;    // verdicts [0, st_n) of st_src already staged
+};
 
 struct sf_engine {
     sf_config cfg{};
@@ -1393,7 +1396,16 @@ static int stage_in_events(sf_engine* e, StageBuf& sb, const sf_event_batch* in,
         std::copy(key, key + 5, sb.key);
         sb.n = n;
     }
-    if (status && n_status) HIP_TRY(hipMemcpyAsync(base + o_st, status, n_status, hipMemcpyHostToDevice, s));
+    if (status && n_status) {
+        // a continued stream: the verdicts staged for the round before are
+        // final (the caller only appends), only the new ones are copied
+        const uint32_t from = (keep && sb.st_src == status && sb.st_n <= n_status) ? sb.st_n : 0;
+        if (n_status > from)
+            HIP_TRY(hipMemcpyAsync(base + o_st + from, status + from, n_status - from, hipMemcpyHostToDevice, s));
+        sb.st_src = status; sb.st_n = n_status;
+    } else {
+        sb.st_src = nullptr; sb.st_n = 0;
+    }
     b = DevBatch{};
     b.n = n;
     b.ts = (const int64_t*)(base + o_ts); b.cnt = (const int32_t*)(base + o_cnt); b.flags = (const uint8_t*)(base + o_fl);
