@@ -614,6 +614,26 @@ int  sf_metric_log(sf_engine* e, int64_t now_ms, int64_t tz_offset_ms, int inclu
 int  sf_format_metric_rows(sf_engine* e, const sf_metric_row* rows, uint32_t n, int64_t tz_offset_ms, char* out,
                            uint64_t cap, uint64_t* len_out);
 
+/* SystemRules on a resource-sharded node, the per-window exchange (DESIGN.md
+ * §5; replaces SystemSlot's reads of Constants.ENTRY_NODE,
+ * SystemRuleManager.checkSystem SystemRuleManager.java:291-348, when the node's
+ * resources are split over engines).  Every rank calls it with its shard's
+ * events of the same node batch, in submission order, and `seq` = their
+ * global sequence numbers (increasing; time non-decreasing in them).  The
+ * ranks exchange per-window aggregates only (a rank's ENTRY_NODE contribution
+ * and a 128-bin histogram of its undecided IN entries per level, 4.2 KB): with
+ * `allgather` NULL over the engine's RCCL communicator (sf_comm_init; device
+ * buffers, stream-ordered), else through the callback, which must return
+ * rank 0's `bytes`, rank 1's, ... in `recv` (0 = success; host buffers).  The
+ * verdicts, and every rank's ENTRY_NODE, equal one engine deciding the whole
+ * node batch.  SF_ERR_UNSUPPORTED (every rank alike) when a loaded SystemRule
+ * has thread / average-RT / BBR checks or an IN entry has acquireCount < 0:
+ * use the event all-gather protocol (sf_system_plan, sf_submit_forced,
+ * sf_entry_node_add).  Without SystemRules it is sf_submit. */
+typedef int (*sf_allgather_fn)(void* ctx, const void* send, void* recv, uint64_t bytes);
+int  sf_submit_node(sf_engine* e, const sf_event_batch* in, const int64_t* seq, sf_verdicts* out,
+                    sf_allgather_fn allgather, void* ctx);
+
 /* Node-wide Constants.ENTRY_NODE over the resource shards of a node: one
  * engine per GPU, joined by RCCL (xGMI).  Rank 0 creates the id, the host
  * distributes it (any channel), every rank calls sf_comm_init.  The merge is
@@ -740,6 +760,10 @@ int  sf_set_timing(sf_engine* e, int enabled);
  * slots, capacity, and the longest probe distance from a key's home slot
  * (at most 4096: an insert that would go farther is SF_ERR_CAPACITY). */
 int  sf_param_table_stats(sf_engine* e, uint64_t* used, uint64_t* capacity, uint32_t* max_probe);
+/* ParameterMetric.getThreadCount(paramIdx, value) (ParameterMetric.java:241-253)
+ * of a resource's ParamFlow statistics: the live thread count of one typed
+ * parameter value (tag, bits as in sf_event_batch), 0 when it has none. */
+int  sf_read_param_thread(sf_engine* e, uint32_t resource, int param_idx, uint8_t tag, uint64_t bits, int64_t* out);
 /* diagnostics: per heavy segment of the last sf_submit (timing must be on) */
 int  sf_heavy_profile_read(sf_engine* e, sf_heavy_profile* out, uint32_t cap, uint32_t* n_out);
 

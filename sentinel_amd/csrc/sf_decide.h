@@ -465,14 +465,16 @@ SF_HD uint64_t pkey_hi(uint32_t res, uint64_t kind, uint32_t idx, uint32_t tag) 
     return ((uint64_t)(res + 1u) << 32) | (kind << 24) | ((uint64_t)(idx & 0xffff) << 8) | (tag & 0xff);
 }
 
-// ParameterMetric.addThreadCount / decreaseThreadCount for one value (:184-239, :125-181)
+// ParameterMetric.addThreadCount / decreaseThreadCount for one value (:184-239, :125-181).
+// delta > 0: that many addThreadCount calls (heavy_param adds a value's passes
+// of a 64-event group at once); delta < 0: one decreaseThreadCount.
 SF_HD void pm_thread_add(const ParamTable& pt, uint32_t res, int idx, uint32_t tag, uint64_t bits, int delta) {
     if (tag == SF_TAG_NULL) return;
     uint64_t hi = pkey_hi(res, PK_THREAD, (uint32_t)idx, tag);
     ParamSlot* s = pt.find(hi, bits);
     if (delta > 0) {
-        if (!s) { s = pt.insert(hi, bits); if (s) s->a = 1; }
-        else s->a = (int32_t)((uint32_t)s->a + 1u);
+        if (!s) { s = pt.insert(hi, bits); if (s) s->a = delta; }
+        else s->a = (int32_t)((uint32_t)s->a + (uint32_t)delta);
     } else {
         if (!s) { pt.insert(hi, bits); return; }              // putIfAbsent(new AtomicInteger())
         int32_t cur = (int32_t)((uint32_t)s->a - 1u);

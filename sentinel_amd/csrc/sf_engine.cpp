@@ -15,7 +15,7 @@
 
 #include "sf_decide.h"
 #include "sf_xflow.h"
-#include "sf_system.h"
+#include "sf_sysx.h"
 #include "sf_token.h"
 #include "sf_wire.h"
 #include "sf_degrade.h"
@@ -114,6 +114,13 @@ struct sf_engine {
     hipEvent_t ml_ev[3]{};
     // node-wide aggregate over the ranks of a node (RCCL over xGMI)
     ncclComm_t comm = nullptr;
+    // sharded SystemRules, the per-window exchange (sf_sysx.h, sf_submit_node)
+    int64_t* sx_msg = nullptr;            // this rank's message [SX_WORDS] (+ the setup words)
+    int64_t* sx_recv = nullptr; size_t sx_recv_words = 0;
+    int64_t* sx_seq = nullptr;            // [max_batch] device copy of host sequence numbers
+    uint8_t* sx_ibuf = nullptr;           // [max_batch] inert flags of the round
+    std::vector<int64_t> sx_hsend, sx_hrecv;   // host side of a callback all-gather
+    uint64_t sx_levels = 0;               // exchange levels run (diagnostics)
     int64_t* agg = nullptr;               // [ws (S+60) | gws (S+60) | vals ((S+60)*6+1) | minrt (S+60)]
     // DegradeSlot circuit breakers (sf_degrade.hip)
     DegradeDev dg{};
@@ -213,7 +220,8 @@ void sf_destroy(sf_engine* e) {
                      e->ml_order, e->ml_len, e->ml_off, e->ml_bytes, e->ml_out, e->ml_tmp};
     for (void* p : tptrs) if (p) hipFree(p);
     if (e->agg) hipFree(e->agg);
-    void* sptrs[] = {e->sys_plan, e->sys_pa, e->sys_pb, e->sys_mask, e->sys_ibuf};
+    void* sptrs[] = {e->sys_plan, e->sys_pa, e->sys_pb, e->sys_mask, e->sys_ibuf, e->sx_msg, e->sx_recv,
+                     e->sx_seq, e->sx_ibuf};
     for (void* p : sptrs) if (p) hipFree(p);
     void* dptrs[] = {(void*)e->dg.rr_of, (void*)e->dg.off, (void*)e->dg.rules, e->dg.state, e->dgw.keys_in,
                      e->dgw.keys_out, e->dgw.idx_in, e->dgw.idx_out, e->dgw.beg, e->dgw.end, e->dgw.sort_tmp,
@@ -917,6 +925,113 @@ static int param_reserve(sf_engine* e, uint64_t bound) {
     return SF_OK;
 }
 
+// the caller's batch and verdict arrays as device pointers: host arrays are
+// copied to the engine's staging buffers on stream ss (verdicts come back
+// from stage_out after the decision)
+static int stage_batch(sf_engine* e, const sf_event_batch* in, const sf_verdicts* out, hipStream_t ss,
+                       DevBatch& b, DevVerdicts& dv) {
+    const uint32_t n = in->n;
+    if (in->mem == SF_MEM_HOST) {
+        size_t need = 0;
+        size_t o_res = need; need += align_up((size_t)n * 4);
+        size_t o_ts = need; need += align_up((size_t)n * 8);
+        size_t o_cnt = need; need += align_up((size_t)n * 4);
+        size_t o_fl = need; need += align_up((size_t)n);
+        size_t o_er = need; need += in->entry_ref ? align_up((size_t)n * 8) : 0;
+        size_t o_ct = need; need += (in->entry_ref && in->create_ts) ? align_up((size_t)n * 8) : 0;
+        size_t o_na = need; need += in->n_args ? align_up((size_t)n) : 0;
+        size_t o_at = need; need += align_up((size_t)n * in->arg_slots);
+        size_t o_ab = need; need += align_up((size_t)n * in->arg_slots * 8);
+        const bool coll = in->arg_elem_off != nullptr;
+        size_t o_eo = need; need += coll ? align_up(((size_t)n * in->arg_slots + 1) * 4) : 0;
+        size_t o_et = need; need += coll ? align_up((size_t)in->n_elems) : 0;
+        size_t o_eb = need; need += coll ? align_up((size_t)in->n_elems * 8) : 0;
+        size_t o_og = need; need += in->origin ? align_up((size_t)n * 4) : 0;
+        size_t o_cx = need; need += in->context ? align_up((size_t)n * 4) : 0;
+        if (need > e->stage_in_bytes) {
+            if (e->stage_in) hipFree(e->stage_in);
+            e->stage_in = nullptr;
+            HIP_TRY(hipMalloc(&e->stage_in, need));
+            e->stage_in_bytes = need;
+        }
+        char* base = (char*)e->stage_in;
+        auto up = [&](size_t off, const void* src, size_t bytes) -> const void* {
+            if (!src || !bytes) return nullptr;
+            hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, ss);
+            return base + off;
+        };
+        b.res = (const uint32_t*)up(o_res, in->res_id, (size_t)n * 4);
+        b.ts = (const int64_t*)up(o_ts, in->ts_ms, (size_t)n * 8);
+        b.cnt = (const int32_t*)up(o_cnt, in->count, (size_t)n * 4);
+        b.flags = (const uint8_t*)up(o_fl, in->flags, n);
+        b.eref = (const int64_t*)up(o_er, in->entry_ref, in->entry_ref ? (size_t)n * 8 : 0);
+        b.cts = (const int64_t*)up(o_ct, in->entry_ref ? in->create_ts : nullptr, (size_t)n * 8);
+        b.nargs = (const uint8_t*)up(o_na, in->n_args, n);
+        b.atag = (const uint8_t*)up(o_at, in->arg_tag, (size_t)n * in->arg_slots);
+        b.abits = (const uint64_t*)up(o_ab, in->arg_bits, (size_t)n * in->arg_slots * 8);
+        if (coll) {
+            b.aoff = (const uint32_t*)up(o_eo, in->arg_elem_off, ((size_t)n * in->arg_slots + 1) * 4);
+            b.etag = (const uint8_t*)up(o_et, in->elem_tag, in->n_elems);
+            b.ebits = (const uint64_t*)up(o_eb, in->elem_bits, (size_t)in->n_elems * 8);
+        }
+        b.origin = (const uint32_t*)up(o_og, in->origin, (size_t)n * 4);
+        b.ctx = (const uint32_t*)up(o_cx, in->context, (size_t)n * 4);
+    } else {
+        b.res = in->res_id; b.ts = in->ts_ms; b.cnt = in->count; b.flags = in->flags;
+        b.eref = in->entry_ref; b.cts = in->entry_ref ? in->create_ts : nullptr;
+        b.nargs = in->n_args; b.atag = in->arg_tag; b.abits = in->arg_bits;
+        b.aoff = in->arg_elem_off; b.etag = in->elem_tag; b.ebits = in->elem_bits;
+        b.origin = in->origin; b.ctx = in->context;
+    }
+    if (out->mem == SF_MEM_HOST) {
+        size_t need = align_up((size_t)n) + align_up((size_t)n * 4) + align_up((size_t)n * 2);
+        if (need > e->stage_out_bytes) {
+            if (e->stage_out) hipFree(e->stage_out);
+            e->stage_out = nullptr;
+            HIP_TRY(hipMalloc(&e->stage_out, need));
+            e->stage_out_bytes = need;
+        }
+        char* base = (char*)e->stage_out;
+        dv.status = (uint8_t*)base;
+        dv.wait = out->wait_ms ? (int32_t*)(base + align_up(n)) : nullptr;
+        dv.rule = out->rule_idx ? (uint16_t*)(base + align_up(n) + align_up((size_t)n * 4)) : nullptr;
+    } else {
+        dv.status = out->status; dv.wait = out->wait_ms; dv.rule = out->rule_idx;
+    }
+    return SF_OK;
+}
+
+// Sort and decide the view [p, q) of a staged batch (a SystemRule sub-batch):
+// its IN entries' system verdicts are in e->sys_mask, the verdicts of the
+// events before it in dv; stream e->stream (the caller fenced the batch's
+// staging).  v / dvv: the view, for the caller's ENTRY_NODE step.
+static int decide_view(sf_engine* e, Work& w, int slot, DevState& stl, const DevBatch& b, const DevVerdicts& dv,
+                       uint32_t p, uint32_t q, bool with_ox, DevBatch& v, DevVerdicts& dvv) {
+    hipStream_t s = e->stream;
+    v = b;
+    v.n = q - p; v.base = p;
+    v.res = b.res + p; v.ts = b.ts + p; v.cnt = b.cnt + p; v.flags = b.flags + p;
+    v.eref = b.eref ? b.eref + p : nullptr; v.cts = b.cts ? b.cts + p : nullptr;
+    v.nargs = b.nargs ? b.nargs + p : nullptr;
+    v.atag = b.atag ? b.atag + p : nullptr; v.abits = b.abits ? b.abits + p : nullptr;
+    v.origin = b.origin ? b.origin + p : nullptr; v.ctx = b.ctx ? b.ctx + p : nullptr;
+    v.sys = e->sys_mask + p; v.vprev = dv.status + p;
+    dvv = DevVerdicts{dv.status + p, dv.wait ? dv.wait + p : nullptr, dv.rule ? dv.rule + p : nullptr};
+    hipError_t le = launch_sort(stl, w, v, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s, e->evs[slot], false);
+    OxPlan plan{};
+    if (le == hipSuccess && with_ox) {
+        const int rc = prepare_origins(e, w, v, s, &plan);
+        if (rc) return rc;
+        stl.xtab = e->st.xtab; stl.xcap_mask = e->st.xcap_mask; stl.ax_cap = e->st.ax_cap;
+    }
+    if (le == hipSuccess)
+        le = launch_decide(stl, w, v, dvv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3,
+                           e->serial ? s : e->stream4, e->evs[slot], false, with_ox ? &plan : nullptr);
+    if (le == hipSuccess && with_ox) w.ox_dirty = false;     // k_ox_reset enqueued
+    if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
+    return SF_OK;
+}
+
 // pre: launched on the sort stream after the batch's error flag is cleared and
 // before its sort (sf_submit_packed's expansion of the packed words)
 using PreSort = std::function<hipError_t(hipStream_t, int32_t*)>;
@@ -972,74 +1087,8 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         HIP_TRY(hipEventSynchronize(e->ev_done[slot]));
         acc_timing(e, slot);
     }
-    if (in->mem == SF_MEM_HOST) {
-        size_t need = 0;
-        size_t o_res = need; need += align_up((size_t)n * 4);
-        size_t o_ts = need; need += align_up((size_t)n * 8);
-        size_t o_cnt = need; need += align_up((size_t)n * 4);
-        size_t o_fl = need; need += align_up((size_t)n);
-        size_t o_er = need; need += in->entry_ref ? align_up((size_t)n * 8) : 0;
-        size_t o_ct = need; need += (in->entry_ref && in->create_ts) ? align_up((size_t)n * 8) : 0;
-        size_t o_na = need; need += in->n_args ? align_up((size_t)n) : 0;
-        size_t o_at = need; need += align_up((size_t)n * in->arg_slots);
-        size_t o_ab = need; need += align_up((size_t)n * in->arg_slots * 8);
-        const bool coll = in->arg_elem_off != nullptr;
-        size_t o_eo = need; need += coll ? align_up(((size_t)n * in->arg_slots + 1) * 4) : 0;
-        size_t o_et = need; need += coll ? align_up((size_t)in->n_elems) : 0;
-        size_t o_eb = need; need += coll ? align_up((size_t)in->n_elems * 8) : 0;
-        size_t o_og = need; need += in->origin ? align_up((size_t)n * 4) : 0;
-        size_t o_cx = need; need += in->context ? align_up((size_t)n * 4) : 0;
-        if (need > e->stage_in_bytes) {
-            if (e->stage_in) hipFree(e->stage_in);
-            e->stage_in = nullptr;
-            HIP_TRY(hipMalloc(&e->stage_in, need));
-            e->stage_in_bytes = need;
-        }
-        char* base = (char*)e->stage_in;
-        auto up = [&](size_t off, const void* src, size_t bytes) -> const void* {
-            if (!src || !bytes) return nullptr;
-            hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, ss);
-            return base + off;
-        };
-        b.res = (const uint32_t*)up(o_res, in->res_id, (size_t)n * 4);
-        b.ts = (const int64_t*)up(o_ts, in->ts_ms, (size_t)n * 8);
-        b.cnt = (const int32_t*)up(o_cnt, in->count, (size_t)n * 4);
-        b.flags = (const uint8_t*)up(o_fl, in->flags, n);
-        b.eref = (const int64_t*)up(o_er, in->entry_ref, in->entry_ref ? (size_t)n * 8 : 0);
-        b.cts = (const int64_t*)up(o_ct, in->entry_ref ? in->create_ts : nullptr, (size_t)n * 8);
-        b.nargs = (const uint8_t*)up(o_na, in->n_args, n);
-        b.atag = (const uint8_t*)up(o_at, in->arg_tag, (size_t)n * in->arg_slots);
-        b.abits = (const uint64_t*)up(o_ab, in->arg_bits, (size_t)n * in->arg_slots * 8);
-        if (coll) {
-            b.aoff = (const uint32_t*)up(o_eo, in->arg_elem_off, ((size_t)n * in->arg_slots + 1) * 4);
-            b.etag = (const uint8_t*)up(o_et, in->elem_tag, in->n_elems);
-            b.ebits = (const uint64_t*)up(o_eb, in->elem_bits, (size_t)in->n_elems * 8);
-        }
-        b.origin = (const uint32_t*)up(o_og, in->origin, (size_t)n * 4);
-        b.ctx = (const uint32_t*)up(o_cx, in->context, (size_t)n * 4);
-    } else {
-        b.res = in->res_id; b.ts = in->ts_ms; b.cnt = in->count; b.flags = in->flags;
-        b.eref = in->entry_ref; b.cts = in->entry_ref ? in->create_ts : nullptr;
-        b.nargs = in->n_args; b.atag = in->arg_tag; b.abits = in->arg_bits;
-        b.aoff = in->arg_elem_off; b.etag = in->elem_tag; b.ebits = in->elem_bits;
-        b.origin = in->origin; b.ctx = in->context;
-    }
     DevVerdicts dv{};
-    if (out->mem == SF_MEM_HOST) {
-        size_t need = align_up((size_t)n) + align_up((size_t)n * 4) + align_up((size_t)n * 2);
-        if (need > e->stage_out_bytes) {
-            if (e->stage_out) hipFree(e->stage_out);
-            e->stage_out = nullptr;
-            HIP_TRY(hipMalloc(&e->stage_out, need));
-            e->stage_out_bytes = need;
-        }
-        char* base = (char*)e->stage_out;
-        dv.status = (uint8_t*)base;
-        dv.wait = out->wait_ms ? (int32_t*)(base + align_up(n)) : nullptr;
-        dv.rule = out->rule_idx ? (uint16_t*)(base + align_up(n) + align_up((size_t)n * 4)) : nullptr;
-    } else {
-        dv.status = out->status; dv.wait = out->wait_ms; dv.rule = out->rule_idx;
-    }
+    { const int rc = stage_batch(e, in, out, ss, b, dv); if (rc) return rc; }
     b.arg_stride = n;
     if (forced) {
         // the forced SystemRule verdicts of this (sub-)batch, planned node-wide
@@ -1079,27 +1128,9 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
             HIP_TRY(hipStreamSynchronize(s));
             const uint32_t q = qi[0];
             if (q <= p || q > n) return fail(SF_ERR_DEVICE, "system planner made no progress");
-            DevBatch v = b;                        // the view [p, q)
-            v.n = q - p; v.base = p;
-            v.res = b.res + p; v.ts = b.ts + p; v.cnt = b.cnt + p; v.flags = b.flags + p;
-            v.eref = b.eref ? b.eref + p : nullptr; v.cts = b.cts ? b.cts + p : nullptr;
-            v.nargs = b.nargs ? b.nargs + p : nullptr;
-            v.atag = b.atag ? b.atag + p : nullptr; v.abits = b.abits ? b.abits + p : nullptr;
-            v.origin = b.origin ? b.origin + p : nullptr; v.ctx = b.ctx ? b.ctx + p : nullptr;
-            v.sys = e->sys_mask + p; v.vprev = dv.status + p;
-            DevVerdicts dvv{dv.status + p, dv.wait ? dv.wait + p : nullptr, dv.rule ? dv.rule + p : nullptr};
-            le = launch_sort(stl, w, v, e->cfg.shard_count, e->cfg.shard_index, e->key_bits, s, e->evs[slot], false);
-            OxPlan plan{};
-            if (le == hipSuccess && with_ox) {
-                const int rc = prepare_origins(e, w, v, s, &plan);
-                if (rc) return rc;
-                stl.xtab = e->st.xtab; stl.xcap_mask = e->st.xcap_mask; stl.ax_cap = e->st.ax_cap;
-            }
-            if (le == hipSuccess)
-                le = launch_decide(stl, w, v, dvv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3,
-                                   e->serial ? s : e->stream4,
-                                   e->evs[slot], false, with_ox ? &plan : nullptr);
-            if (le == hipSuccess && with_ox) w.ox_dirty = false;     // k_ox_reset enqueued
+            DevBatch v;
+            DevVerdicts dvv;
+            { const int rc = decide_view(e, w, slot, stl, b, dv, p, q, with_ox, v, dvv); if (rc) return rc; }
             // the system verdicts of the inert entries (ENTRY_NODE is still at p)
             if (le == hipSuccess && qi[1])
                 le = sys_plan_fix(stl, b, dv, e->sys_mask, e->sys, p, q, e->sys_plan, e->sys_pa, e->sys_pb, s);
@@ -1412,6 +1443,226 @@ static int stage_in_events(sf_engine* e, StageBuf& sb, const sf_event_batch* in,
     b.eref = in->entry_ref ? (const int64_t*)(base + o_er) : nullptr;
     b.cts = in->create_ts ? (const int64_t*)(base + o_ct) : nullptr;
     *dstatus = (uint8_t*)(base + o_st);
+    return SF_OK;
+}
+
+// ---------------------------------------------------------------- sharded SystemRules: the per-window exchange
+// (sf_sysx.h; sentinel_flow.h sf_submit_node).  All ranks run the same number
+// of all-gathers in the same order: every decision that shapes the loop is
+// made from exchanged data (plan windows, the plan's levels and q).  RCCL:
+// device buffers into d_recv; a callback: host buffers, the result in sx_hrecv.
+static int sx_exchange(sf_engine* e, sf_allgather_fn fn, void* ctx, const int64_t* d_send, int64_t* d_recv,
+                       size_t words) {
+    const size_t bytes = words * 8, N = e->cfg.shard_count;
+    hipStream_t s = e->stream;
+    if (!fn) {
+        const ncclResult_t r = ncclAllGather(d_send, d_recv, bytes, ncclInt8, e->comm, s);
+        if (r != ncclSuccess) return fail(SF_ERR_DEVICE, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        return SF_OK;
+    }
+    e->sx_hsend.resize(words);
+    e->sx_hrecv.resize(words * N);
+    HIP_TRY(hipMemcpyAsync(e->sx_hsend.data(), d_send, bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (fn(ctx, e->sx_hsend.data(), e->sx_hrecv.data(), bytes) != 0) return fail(SF_ERR_DEVICE, "all-gather callback failed");
+    return SF_OK;                               // (every rank's message in sx_hrecv; the plan step reads it there)
+}
+
+static int sx_recv_reserve(sf_engine* e, size_t words) {
+    if (e->sx_recv_words >= words) return SF_OK;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->sx_recv) hipFree(e->sx_recv);
+    e->sx_recv = nullptr; e->sx_recv_words = 0;
+    HIP_TRY(hipMalloc((void**)&e->sx_recv, words * 8));
+    e->sx_recv_words = words;
+    return SF_OK;
+}
+
+int sf_submit_node(sf_engine* e, const sf_event_batch* in, const int64_t* seq, sf_verdicts* out,
+                   sf_allgather_fn allgather, void* ctx) {
+    if (!e || !in || !out) return fail(SF_ERR_INVALID, "null argument");
+    if (in->n && (!seq || !out->status || !in->res_id || !in->ts_ms || !in->count || !in->flags))
+        return fail(SF_ERR_INVALID, "missing event array");
+    if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
+    if (in->arg_slots > SF_MAX_ARGS || (in->arg_slots && (!in->arg_tag || !in->arg_bits)))
+        return fail(SF_ERR_INVALID, "bad arg arrays");
+    if (in->arg_elem_off && in->n_elems && (!in->elem_tag || !in->elem_bits))
+        return fail(SF_ERR_INVALID, "collection arguments without element arrays");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->sys.check) return in->n ? submit_core(e, in, out, false) : SF_OK;   // nothing node-wide to decide
+    if (!sx_rule_ok(e->sys))
+        return fail(SF_ERR_UNSUPPORTED, "SystemRule with thread / RT / BBR checks: the event all-gather protocol "
+                                        "(sf_system_plan + sf_submit_forced + sf_entry_node_add)");
+    if (!allgather && !e->comm) return fail(SF_ERR_INVALID, "no exchange: sf_comm_init or an all-gather callback");
+    { const int rc = drain(e); if (rc) return rc; }
+    const uint32_t n = in->n, N = e->cfg.shard_count;
+    hipStream_t s = e->stream;
+    if (!e->sx_msg) {
+        HIP_TRY(hipMalloc((void**)&e->sx_msg, SX_WORDS * 8));
+        HIP_TRY(hipMalloc((void**)&e->sx_ibuf, e->cfg.max_batch));
+    }
+    if (!e->sys_mask) HIP_TRY(hipMalloc((void**)&e->sys_mask, e->cfg.max_batch));
+    { const int rc = sx_recv_reserve(e, (size_t)N * SX_WORDS); if (rc) return rc; }
+    const bool with_ox = in->origin || e->st.xmap;
+    if (with_ox && !e->st.xtab) { const int rc = ensure_aux(e); if (rc) return rc; HIP_TRY(hipStreamSynchronize(s)); }
+    {
+        const uint64_t elems = in->arg_elem_off ? in->n_elems : 0;
+        const int rc = param_reserve(e, ((uint64_t)n + elems) * e->p_kmax);
+        if (rc) return rc;
+    }
+    const int slot = e->cur;
+    Work& w = e->w[slot];
+    if (e->used[slot]) { HIP_TRY(hipEventSynchronize(e->ev_done[slot])); acc_timing(e, slot); }
+    DevBatch b{};
+    b.n = n; b.arg_slots = in->arg_slots;
+    DevVerdicts dv{};
+    { const int rc = stage_batch(e, in, out, s, b, dv); if (rc) return rc; }
+    b.arg_stride = n;
+    const int64_t* dseq = seq;
+    if (in->mem == SF_MEM_HOST && n) {
+        if (!e->sx_seq) HIP_TRY(hipMalloc((void**)&e->sx_seq, (size_t)e->cfg.max_batch * 8));
+        HIP_TRY(hipMemcpyAsync(e->sx_seq, seq, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        dseq = e->sx_seq;
+    }
+    HIP_TRY(hipMemsetAsync(w.err, 0, sizeof(int32_t), s));
+    DevState stl = e->st;
+    stl.err = w.err;
+    SxArgs a{};
+    a.b = b; a.seq = dseq; a.msg = e->sx_msg;
+    a.r = e->sys; a.S = stl.S; a.wl = stl.wl; a.interval = stl.interval; a.max_rt = stl.max_rt;
+    a.interval_sec = stl.interval / 1000.0; a.st = stl;
+    a.ibuf = e->st.n_prule ? e->sx_ibuf : nullptr;
+    a.g = std::__gcd((int64_t)stl.wl, (int64_t)1000);
+    // every rank's message on the host: the plan step runs there (one sync per level)
+    auto gather = [&](const int64_t* d_send, size_t words, std::vector<int64_t>& h) -> int {
+        const int rc = sx_exchange(e, allgather, ctx, d_send, e->sx_recv, words);
+        if (rc) return rc;
+        if (allgather) { h.assign(e->sx_hrecv.begin(), e->sx_hrecv.begin() + words * N); return SF_OK; }
+        h.resize(words * N);
+        HIP_TRY(hipMemcpyAsync(h.data(), e->sx_recv, words * N * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        return SF_OK;
+    };
+    // ---- per batch: the node's plan windows (cells of g ms) and where each starts
+    int64_t C0 = INT64_MAX, C1 = INT64_MIN, seq_end = INT64_MIN;
+    bool neg = false;
+    std::vector<int64_t> h;
+    {
+        HIP_TRY(sx_header(a, e->sx_msg, s));
+        { const int rc = gather(e->sx_msg, 5, h); if (rc) return rc; }
+        for (uint32_t k = 0; k < N; k++) {
+            const int64_t* x = &h[(size_t)k * 5];
+            if (!x[4]) continue;
+            C0 = std::min(C0, x[0]); C1 = std::max(C1, x[1]); seq_end = std::max(seq_end, x[2]);
+            neg |= x[3] != 0;
+        }
+    }
+    if (neg) return fail(SF_ERR_UNSUPPORTED, "an IN entry with acquireCount < 0: the event all-gather protocol");
+    std::vector<int64_t> wseq;                  // start sequence number of each non-empty plan window
+    std::vector<int64_t> wkey;                  // its index (cell - C0)
+    if (seq_end != INT64_MIN) {
+        const uint64_t nw = (uint64_t)(C1 - C0) + 1;
+        if (nw > (1u << 22)) return fail(SF_ERR_CAPACITY, "batch spans too many plan windows");
+        { const int rc = sx_recv_reserve(e, (size_t)N * nw); if (rc) return rc; }
+        int64_t* wbuf = nullptr;
+        HIP_TRY(hipMalloc((void**)&wbuf, nw * 8));
+        a.c0 = C0;
+        const hipError_t le = sx_winfirst(a, wbuf, (uint32_t)nw, s);
+        const int rc = le == hipSuccess ? gather(wbuf, nw, h)
+                                        : fail(SF_ERR_DEVICE, std::string("plan windows: ") + hipGetErrorString(le));
+        hipFree(wbuf);
+        if (rc) return rc;
+        for (uint64_t k = 0; k < nw; k++) {
+            int64_t m = INT64_MAX;
+            for (uint32_t r = 0; r < N; r++) m = std::min(m, h[(size_t)r * nw + k]);
+            if (m != INT64_MAX) { wseq.push_back(m); wkey.push_back((int64_t)k); }
+        }
+    }
+    a.c0 = C0;
+    // ENTRY_NODE, identical on every rank, advanced on the host by the node's deltas (no
+    // kernel reads it while the batch is decided: the system verdicts are forced)
+    EntryNode enh;
+    HIP_TRY(hipMemcpyAsync(&enh, e->en, sizeof enh, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    uint32_t* d_lq = (uint32_t*)e->sx_recv;     // (sx_locate's result: the recv buffer is free then)
+    // ---- rounds
+    HIP_TRY(sx_nodelta(e->sx_msg, s));
+    int64_t sp = wseq.empty() ? INT64_MAX : wseq[0];
+    uint32_t lp = 0, rounds = 0;
+    size_t j = 0;
+    uint64_t levels = 0;
+    for (;;) {
+        const bool fin = wseq.empty() || sp >= seq_end;
+        while (!fin && j + 1 < wseq.size() && wseq[j + 1] <= sp) j++;
+        const int64_t lo = fin ? 0 : sp, hi = fin ? 0 : (j + 1 < wseq.size() ? wseq[j + 1] : seq_end);
+        const int64_t wstart = fin ? 0 : (C0 + wkey[j]) * a.g;
+        SxPlan hp;
+        sx_begin(&hp, lo, hi);
+        for (int level = 0;; level++) {
+            const hipError_t le = sx_stats(a, hp, lp, level == 0, s);
+            if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("exchange stats: ") + hipGetErrorString(le));
+            { const int rc = gather(e->sx_msg, SX_WORDS, h); if (rc) return rc; }
+            levels++;
+            if (level == 0) {
+                // the node's ENTRY_NODE contribution of the last sub-batch (its plan window is the key)
+                int64_t key = -1;
+                for (uint32_t k = 0; k < N; k++) key = std::max(key, h[(size_t)k * SX_WORDS + SXD_KEY]);
+                if (key >= 0) {
+                    const int64_t W = (C0 + key) * a.g;
+                    sx_apply_delta(h.data(), (int)N, &enh, W - W % a.wl, a.S, a.wl, W - W % 1000, a.max_rt);
+                }
+                hp.P = sys_base(enh.second, a.S, a.wl, a.interval, a.max_rt, enh.threads, wstart).P;
+            }
+            sx_reduce(h.data(), (int)N, &hp, a.r, a.interval_sec);
+            if (hp.done) break;
+            if (level > 64) return fail(SF_ERR_DEVICE, "exchange plan did not converge");
+        }
+        if (fin) break;
+        if (hp.q <= sp || hp.q > hi) return fail(SF_ERR_DEVICE, "exchange plan made no progress");
+        uint32_t lq;
+        if (in->mem == SF_MEM_HOST) {
+            lq = (uint32_t)(std::lower_bound(seq + lp, seq + n, hp.q) - seq);
+        } else {
+            HIP_TRY(sx_locate(a, lp, hp.q, d_lq, s));
+            HIP_TRY(hipMemcpyAsync(&lq, d_lq, 4, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
+        if (lq < lp || lq > n) return fail(SF_ERR_DEVICE, "exchange plan: bad local range");
+        if (lq > lp) {
+            hipError_t le = sx_mask(a, e->sys_mask, lp, lq, hp.P, s);
+            if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("exchange mask: ") + hipGetErrorString(le));
+            DevBatch v;
+            DevVerdicts dvv;
+            { const int rc = decide_view(e, w, slot, stl, b, dv, lp, lq, with_ox, v, dvv); if (rc) return rc; }
+            le = launch_entry_delta(stl, v, dvv.status, e->en_acc, e->sx_msg, wkey[j], s);
+            if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("exchange delta: ") + hipGetErrorString(le));
+        } else {
+            HIP_TRY(sx_nodelta(e->sx_msg, s));
+        }
+        lp = lq;
+        sp = hp.q;
+        rounds++;
+    }
+    HIP_TRY(hipMemcpyAsync(e->en, &enh, sizeof enh, hipMemcpyHostToDevice, s));
+    if (lp != n) return fail(SF_ERR_DEVICE, "exchange rounds left events undecided");
+    HIP_TRY(hipEventRecord(e->ev_core[slot], s));
+    HIP_TRY(hipEventRecord(e->ev_done[slot], s));
+    e->used[slot] = true;
+    e->last = slot;
+    e->stats.n_events = n;
+    e->stats.n_launches++;
+    e->stats.sys_rounds += rounds;
+    e->sx_levels += levels;
+    if (out->mem == SF_MEM_HOST && n) {
+        HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, s));
+        if (dv.wait) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        if (dv.rule) HIP_TRY(hipMemcpyAsync(out->rule_idx, dv.rule, (size_t)n * 2, hipMemcpyDeviceToHost, s));
+    }
+    int32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, w.err, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (err) return fail(err, err == SF_ERR_CAPACITY ? "capacity exceeded (param table, or the origin / context node pool: aux_capacity)"
+                                                     : "invalid batch (resource outside shard or bad entry_ref)");
     return SF_OK;
 }
 
@@ -2308,6 +2559,24 @@ int sf_set_timing(sf_engine* e, int enabled) {
     if (!e) return fail(SF_ERR_INVALID, "null engine");
     e->timing = enabled != 0;
     std::memset(&e->stats, 0, sizeof e->stats);
+    return SF_OK;
+}
+
+int sf_read_param_thread(sf_engine* e, uint32_t resource, int param_idx, uint8_t tag, uint64_t bits, int64_t* out) {
+    if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
+    uint32_t l = 0;
+    if (!local_of(e, resource, &l)) return fail(SF_ERR_INVALID, "resource outside this shard");
+    std::lock_guard<std::mutex> g(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }
+    long long* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, 8));
+    long long h = 0;
+    hipError_t he = launch_param_thread_read(e->st, l, param_idx, tag, bits, d, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    hipFree(d);
+    if (he != hipSuccess) return fail(SF_ERR_DEVICE, std::string("param thread read: ") + hipGetErrorString(he));
+    *out = h;
     return SF_OK;
 }
 

@@ -18,7 +18,7 @@
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
-#include "sf_decide.h"
+#include "sf_sysx.h"
 
 namespace sf {
 
@@ -246,6 +246,29 @@ hipError_t launch_entry_node(const DevState& st, const DevBatch& b, const uint8_
     const unsigned nb = (unsigned)((b.n + EN_T * EN_PER - 1) / (EN_T * EN_PER));
     hipLaunchKernelGGL(k_entry_acc, dim3(nb), dim3(EN_T), 0, s, st, b, vstatus, acc);
     hipLaunchKernelGGL(k_entry_apply_if, dim3(1), dim3(256), 0, s, st, b, en, acc, vstatus);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ sharded SystemRule exchange (sf_sysx.h)
+// a decided view of one plan window: its ENTRY_NODE sums (row 0 of the
+// reduction: every event is in the window of the view's first event) as the
+// delta words of this rank's next message
+__global__ void k_sx_pack(const EntryAcc* acc, int64_t* msg, int64_t key) {
+    if (threadIdx.x != 0) return;
+    msg[SXD_KEY] = key;
+    for (int f = 0; f < 6; f++) { msg[SXD_SEC + f] = (int64_t)acc->sec[0][f]; msg[SXD_MIN + f] = (int64_t)acc->min[0][f]; }
+    msg[SXD_MRS] = acc->minrt_sec[0]; msg[SXD_MRM] = acc->minrt_min[0];
+    msg[SXD_THR] = acc->threads;
+    if (acc->overflow) msg[SXD_KEY] = INT64_MIN;          // (cannot happen: one window)
+}
+hipError_t launch_entry_delta(const DevState& st, const DevBatch& v, const uint8_t* vstatus, EntryAcc* acc,
+                              int64_t* msg, int64_t key, hipStream_t s) {
+    if (!v.n) return sx_nodelta(msg, s);
+    hipMemsetAsync(acc, 0, sizeof(EntryAcc), s);
+    hipLaunchKernelGGL(k_entry_minrt_init, dim3((EN_TBL + 255) / 256), dim3(256), 0, s, acc);
+    const unsigned nb = (unsigned)((v.n + EN_T * EN_PER - 1) / (EN_T * EN_PER));
+    hipLaunchKernelGGL(k_entry_acc, dim3(nb), dim3(EN_T), 0, s, st, v, vstatus, acc);
+    hipLaunchKernelGGL(k_sx_pack, dim3(1), dim3(64), 0, s, acc, msg, key);
     return hipGetLastError();
 }
 

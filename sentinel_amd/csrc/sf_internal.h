@@ -353,6 +353,8 @@ hipError_t launch_fmt_write(const sf_metric_row* rows, const uint32_t* order, ui
                             const uint64_t* name_off, const int32_t* types, uint32_t n_names, int64_t tz,
                             const uint64_t* line_off, char* out, hipStream_t s);
 hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipStream_t s);   // out[0] used, out[1] max probe
+hipError_t launch_param_thread_read(const DevState& st, uint32_t l, int idx, uint32_t tag, uint64_t bits,
+                                    long long* out, hipStream_t s);
 // classify = true: k_classify / k_fill_tiles end the sort phase (the origin
 // index passes read the routes); false: launch_decide runs them first
 hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,

@@ -1861,6 +1861,19 @@ hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipSt
     return hipGetLastError();
 }
 
+// ParameterMetric.getThreadCount(index, value) (ParameterMetric.java:241-253) of one
+// (local resource, param index, typed value): 0 when the value has no counter
+__global__ void k_param_thread_read(DevState st, uint32_t l, int idx, uint32_t tag, uint64_t bits, long long* out) {
+    if (threadIdx.x != 0) return;
+    const ParamTable pt{st.ptab, st.pcap_mask, st.err, nullptr};
+    *out = (long long)pm_thread_get(pt, l, idx, tag, bits);
+}
+hipError_t launch_param_thread_read(const DevState& st, uint32_t l, int idx, uint32_t tag, uint64_t bits,
+                                    long long* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_param_thread_read, dim3(1), dim3(64), 0, s, st, l, idx, tag, bits, out);
+    return hipGetLastError();
+}
+
 static inline unsigned blocks(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 // Several buffer fills in one launch (each hipMemsetAsync is a launch of its

@@ -221,10 +221,11 @@ SF_HD SysExitQ sys_exit_q(const int64_t* ts, const int32_t* cnt, const uint8_t* 
 // either way (StatisticSlot.entry :107-123), so it never adds to a pass or
 // thread bound, and its own system verdict can be settled once the sub-batch is
 // decided (sys_plan_fix).  param_inert tells, from the table as it is at p
-// (the events before p are decided and no event at or after p has run).
+// (the events before p are decided and no event at or after p has run).  The
+// batch is this engine's (a sharded engine's own events under sf_sysx.h).
 SF_HD bool param_inert(const DevState& st, const DevBatch& b, uint32_t i, int32_t acq, int64_t now) {
-    if (st.shard_count != 1 || !st.rdesc || !b.atag) return false;
-    const uint32_t l = b.res[i];
+    if (!st.rdesc || !b.atag) return false;
+    const uint32_t l = b.res[i] / st.shard_count;             // (this engine's events: res % shards == index)
     if (l >= st.R || (st.xmap && st.xmap[l] != XNONE)) return false;
     if (!(st.rdesc[l].flags & RD_PRULE)) return false;
     const DevParamRule& r = st.prules[st.prule_off[l]];

@@ -14,7 +14,7 @@
 // (classifying with A's prefix), C classifies every entry with both.  A
 // block's prefix is the sum of the earlier blocks' totals (at most SP_NB
 // partials, summed by the block itself: no separate scan launch).
-#include "sf_system.h"
+#include "sf_sysx.h"
 
 namespace sf {
 
@@ -306,6 +306,144 @@ hipError_t sys_plan_fix(const DevState& st, const DevBatch& b, const DevVerdicts
     hipLaunchKernelGGL(k_sp_a, dim3(nb), dim3(SP_T), 0, s, a);
     hipLaunchKernelGGL(k_sp_b, dim3(nb), dim3(SP_T), 0, s, a);
     hipLaunchKernelGGL(k_sp_c, dim3(nb), dim3(SP_T), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace sf
+
+// ------------------------------------------------------------------ the per-window exchange (sf_sysx.h)
+namespace sf {
+
+__device__ __forceinline__ bool sx_in_entry(const DevBatch& b, uint32_t i) {
+    const uint8_t f = b.flags[i];
+    return (f & SF_EV_IN) && !(f & (SF_EV_EXIT | SF_EV_BLOCKED));
+}
+__device__ __forceinline__ int64_t sx_cell(int64_t t, int64_t g) { return t >= 0 ? t / g : -((-t + g - 1) / g); }
+// first i in [lo, hi) with seq[i] >= key
+__device__ uint32_t sx_lower(const int64_t* seq, uint32_t lo, uint32_t hi, int64_t key) {
+    while (lo < hi) { const uint32_t m = lo + (hi - lo) / 2; if (seq[m] >= key) hi = m; else lo = m + 1; }
+    return lo;
+}
+
+__global__ void k_sx_header(SxArgs a, int64_t* out) {
+    const uint32_t n = a.b.n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out[0] = n ? sx_cell(a.b.ts[0], a.g) : INT64_MAX;
+        out[1] = n ? sx_cell(a.b.ts[n - 1], a.g) : INT64_MIN;
+        out[2] = n ? a.seq[n - 1] + 1 : INT64_MIN;
+        out[4] = n;
+    }
+    bool neg = false;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        neg |= sx_in_entry(a.b, i) && a.b.cnt[i] < 0;
+    if (__ballot(neg) && (threadIdx.x & 63) == 0) atomicOr((unsigned long long*)&out[3], 1ull);
+}
+__global__ void k_sx_fill(int64_t* p, uint32_t n, int64_t v) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+__global__ void k_sx_winfirst(SxArgs a, int64_t* out, uint32_t nw) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.b.n) return;
+    const int64_t c = sx_cell(a.b.ts[i], a.g);
+    if (i > 0 && sx_cell(a.b.ts[i - 1], a.g) == c) return;
+    const int64_t k = c - a.c0;
+    if (k >= 0 && k < (int64_t)nw) out[k] = a.seq[i];
+}
+hipError_t sx_header(const SxArgs& a, int64_t* out, hipStream_t s) {
+    hipMemsetAsync(out, 0, 5 * sizeof(int64_t), s);
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(1024, ((uint64_t)a.b.n + 255) / 256 + 1);
+    hipLaunchKernelGGL(k_sx_header, dim3(nb), dim3(256), 0, s, a, out);
+    return hipGetLastError();
+}
+hipError_t sx_winfirst(const SxArgs& a, int64_t* out, uint32_t nw, hipStream_t s) {
+    hipLaunchKernelGGL(k_sx_fill, dim3((nw + 255) / 256), dim3(256), 0, s, out, nw, INT64_MAX);
+    if (a.b.n) hipLaunchKernelGGL(k_sx_winfirst, dim3((a.b.n + 255) / 256), dim3(256), 0, s, a, out, nw);
+    return hipGetLastError();
+}
+
+__global__ void k_sx_clear(int64_t* msg, bool keep_delta) {
+    const int i = threadIdx.x + blockIdx.x * blockDim.x;
+    if (i < SX_DELTA) { if (!keep_delta) msg[i] = i == SXD_KEY ? -1 : 0; }
+    else if (i < SXM_CMIN) msg[i] = 0;
+    else if (i < SXM_CMAX) msg[i] = INT64_MAX;
+    else if (i < SX_WORDS) msg[i] = INT64_MIN;
+}
+hipError_t sx_nodelta(int64_t* msg, hipStream_t s) {
+    hipLaunchKernelGGL(k_sx_clear, dim3((SX_WORDS + 255) / 256), dim3(256), 0, s, msg, false);
+    return hipGetLastError();
+}
+
+constexpr int SX_T = 256;
+// One thread per contiguous run of the level's local events (sequence
+// numbers increase, so a run's bin changes rarely): sums in registers, one set
+// of atomics per (run, bin).
+__global__ void __launch_bounds__(SX_T) k_sx_stats(SxArgs a, uint32_t lp, bool level0, int64_t lo, int64_t hi,
+                                                   int64_t w) {
+    __shared__ uint32_t rng[2];
+    if (threadIdx.x == 0) {
+        rng[0] = sx_lower(a.seq, lp, a.b.n, lo);
+        rng[1] = sx_lower(a.seq, rng[0], a.b.n, hi);
+    }
+    __syncthreads();
+    const uint32_t i0 = rng[0], i1 = rng[1];
+    const uint64_t nth = (uint64_t)gridDim.x * SX_T, len = i1 - i0;
+    const uint32_t per = (uint32_t)((len + nth - 1) / nth);
+    const uint64_t t = (uint64_t)blockIdx.x * SX_T + threadIdx.x;
+    const uint64_t r0 = (uint64_t)i0 + t * per;
+    const uint32_t r1 = (uint32_t)std::min<uint64_t>(r0 + per, i1);
+    int64_t bin = -1, u = 0, n = 0, cmn = INT64_MAX, cmx = INT64_MIN;
+    auto flush = [&]() {
+        if (bin < 0 || !n) return;
+        atomicAdd((unsigned long long*)&a.msg[SXM_U + bin], (unsigned long long)u);
+        atomicAdd((unsigned long long*)&a.msg[SXM_N + bin], (unsigned long long)n);
+        atomicMin((long long*)&a.msg[SXM_CMIN + bin], (long long)cmn);
+        atomicMax((long long*)&a.msg[SXM_CMAX + bin], (long long)cmx);
+    };
+    for (uint64_t i = r0; i < r1; i++) {
+        if (!sx_in_entry(a.b, (uint32_t)i)) continue;
+        const int32_t c = a.b.cnt[i];
+        bool inert;
+        if (level0) {
+            inert = a.ibuf && param_inert(a.st, a.b, (uint32_t)i, c, a.b.ts[i]);
+            if (a.ibuf) a.ibuf[i] = inert ? 1 : 0;
+        } else {
+            inert = a.ibuf && a.ibuf[i];
+        }
+        const int64_t k = (a.seq[i] - lo) / w;
+        if (k != bin) { flush(); bin = k; u = 0; n = 0; cmn = INT64_MAX; cmx = INT64_MIN; }
+        if (!inert && c > 0) u = sx_sat(u, c);
+        n++;
+        if (c < cmn) cmn = c;
+        if (c > cmx) cmx = c;
+    }
+    flush();
+}
+hipError_t sx_stats(const SxArgs& a, const SxPlan& pl, uint32_t lp, bool level0, hipStream_t s) {
+    hipLaunchKernelGGL(k_sx_clear, dim3((SX_WORDS + 255) / 256), dim3(256), 0, s, a.msg, level0);
+    if (pl.done) return hipGetLastError();
+    const uint64_t rest = a.b.n > lp ? a.b.n - lp : 0;
+    const uint32_t nb = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (rest + 16 * SX_T - 1) / (16 * SX_T)));
+    hipLaunchKernelGGL(k_sx_stats, dim3(nb), dim3(SX_T), 0, s, a, lp, level0, pl.lo, pl.hi, pl.w);
+    return hipGetLastError();
+}
+
+// this rank's first event with seq >= q (batches whose sequence numbers are in HBM)
+__global__ void k_sx_locate(SxArgs a, uint32_t lp, int64_t q, uint32_t* out) {
+    if (threadIdx.x == 0) *out = sx_lower(a.seq, lp, a.b.n, q);
+}
+hipError_t sx_locate(const SxArgs& a, uint32_t lp, int64_t q, uint32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_sx_locate, dim3(1), dim3(64), 0, s, a, lp, q, out);
+    return hipGetLastError();
+}
+
+__global__ void k_sx_mask(SxArgs a, uint8_t* mask, uint32_t lp, uint32_t lq, int64_t P) {
+    const uint32_t i = lp + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= lq) return;
+    mask[i] = sx_in_entry(a.b, i) ? sx_reason(a.r, P, a.interval_sec, a.b.cnt[i]) : SYS_NONE;
+}
+hipError_t sx_mask(const SxArgs& a, uint8_t* mask, uint32_t lp, uint32_t lq, int64_t P, hipStream_t s) {
+    if (lq > lp) hipLaunchKernelGGL(k_sx_mask, dim3((lq - lp + 255) / 256), dim3(256), 0, s, a, mask, lp, lq, P);
     return hipGetLastError();
 }
 

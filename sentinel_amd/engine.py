@@ -23,6 +23,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SENTINEL_FLOW_LIB") or os.path.join(_HERE, "libsentinel_flow.so")
 
 
+# sf_allgather_fn: (ctx, send, recv, bytes) -> 0 on success
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+
+
 class EngineError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"sentinel_flow error {code}: {msg}")
@@ -101,11 +105,13 @@ def _declare(L):
     f("sf_set_timing", I, P, I)
     f("sf_heavy_profile_read", I, P, C.POINTER(abi.sf_heavy_profile), U32, C.POINTER(U32))
     f("sf_param_table_stats", I, P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(U32))
+    f("sf_read_param_thread", I, P, U32, C.c_int, C.c_uint8, C.c_uint64, C.POINTER(C.c_int64))
     f("sf_token_shard", I, C.POINTER(abi.sf_cluster_flow_rule), U32, C.POINTER(abi.sf_cluster_param_rule), U32,
       C.POINTER(abi.sf_namespace), U32, U32, P, P, U32, P)
     f("sf_system_plan", I, P, C.POINTER(abi.sf_event_batch), P, U32, C.POINTER(U32), P)
     f("sf_submit_forced", I, P, C.POINTER(abi.sf_event_batch), C.POINTER(abi.sf_verdicts), P)
     f("sf_entry_node_add", I, P, C.POINTER(abi.sf_event_batch), P)
+    f("sf_submit_node", I, P, C.POINTER(abi.sf_event_batch), P, C.POINTER(abi.sf_verdicts), ALLGATHER_FN, P)
     f("sf_flow_rule_order", I, C.POINTER(abi.sf_flow_rule), C.POINTER(abi.sf_rule_key), U32, P, C.POINTER(U32))
     f("sf_param_rule_order", I, C.POINTER(abi.sf_param_rule), C.POINTER(abi.sf_rule_key), U32,
       C.POINTER(abi.sf_hot_item), U32, P, C.POINTER(U32))
@@ -383,6 +389,43 @@ class FlowEngine:
         b = batch.c_struct()
         _check(lib().sf_entry_node_add(self.h, C.byref(b), st.ctypes.data))
 
+    def submit_node(self, batch: abi.HostBatch, seq: np.ndarray, comm=None) -> abi.HostVerdicts:
+        """sf_submit_node: this rank's shard of a node batch (``seq`` = the
+        events' global sequence numbers) with the node-wide SystemRule
+        semantics, by the per-window exchange (sf_sysx.h).  ``comm``: an object
+        with ``allgather_bytes(np.uint8 array) -> [rank 0's bytes, rank 1's,
+        ...]`` (e.g. system_shard.TorchComm over gloo), or None for the
+        engine's RCCL communicator (sf_comm_init).  Raises EngineError with
+        code SF_ERR_UNSUPPORTED on every rank alike when the SystemRules need
+        the event all-gather protocol."""
+        out = abi.HostVerdicts(batch.n)
+        b, v = batch.c_struct(), out.c_struct()
+        sq = np.ascontiguousarray(seq, np.int64)
+        assert sq.shape == (batch.n,)
+        errs = []
+        if comm is None:
+            cb = ALLGATHER_FN()
+        else:
+            def fn(ctx, send, recv, nbytes):
+                try:
+                    x = np.ctypeslib.as_array(C.cast(send, C.POINTER(C.c_uint8)), shape=(nbytes,))
+                    off = 0
+                    for p in comm.allgather_bytes(x):
+                        p = np.ascontiguousarray(p, np.uint8).reshape(-1)
+                        assert p.nbytes == nbytes
+                        C.memmove(recv + off, p.ctypes.data, nbytes)
+                        off += nbytes
+                    return 0
+                except BaseException as ex:          # noqa: BLE001 -- re-raised after the call
+                    errs.append(ex)
+                    return 1
+            cb = ALLGATHER_FN(fn)
+        rc = lib().sf_submit_node(self.h, C.byref(b), sq.ctypes.data if batch.n else None, C.byref(v), cb, None)
+        if errs:
+            raise errs[0]
+        _check(rc)
+        return out
+
     def submit_device_async(self, batch: DeviceBatch, out: DeviceVerdicts):
         """Enqueue a batch (HBM arrays; keep them alive until sync()): batch k+1 is
         sorted while batch k is decided; sync() waits and reports errors."""
@@ -519,6 +562,12 @@ class FlowEngine:
         _check(lib().sf_param_table_stats(self.h, C.byref(u), C.byref(c), C.byref(m)))
         return dict(used=u.value, capacity=c.value, load_factor=round(u.value / max(1, c.value), 4),
                     max_probe=m.value)
+
+    def param_thread(self, res, idx, value) -> int:
+        """ParameterMetric.getThreadCount(idx, value) of resource ``res``; value = (tag, bits)."""
+        out = C.c_int64()
+        _check(lib().sf_read_param_thread(self.h, res, idx, value[0], value[1], C.byref(out)))
+        return out.value
 
     def set_timing(self, on=True):
         _check(lib().sf_set_timing(self.h, int(on)))

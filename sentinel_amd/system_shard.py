@@ -1,4 +1,15 @@
-"""SystemRules on a resource-sharded node: the node-wide round protocol.
+"""SystemRules on a resource-sharded node.
+
+Two protocols.  ``submit_node`` uses the engine's per-window exchange
+(sf_submit_node, sentinel_amd/csrc/sf_sysx.h): the ranks all-gather per-window
+aggregates (each rank's ENTRY_NODE contribution and a 128-bin histogram of its
+undecided IN entries, 4.2 KB per rank and level) over RCCL or the ``comm``
+callback, for SystemRules that read only the inbound-QPS (and CPU) check.
+Every other SystemRule (thread, average RT, BBR) and batches with a negative
+acquireCount fall back to ``submit_node_gather``, the event all-gather round
+protocol below.
+
+The event all-gather round protocol.
 
 SystemRuleManager.checkSystem (SystemRuleManager.java:291-348) reads
 Constants.ENTRY_NODE, the one ClusterNode every EntryType.IN event of every
@@ -69,6 +80,16 @@ class TorchComm:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t.cpu().numpy()
 
+    def allgather_bytes(self, x: np.ndarray):
+        """Every rank's equal-sized byte message, rank order (the engine's
+        sf_allgather_fn)."""
+        import torch
+        import torch.distributed as dist
+        t = torch.from_numpy(np.ascontiguousarray(x, np.uint8)).to(self.device)
+        parts = [torch.empty_like(t) for _ in range(dist.get_world_size(self.group))]
+        dist.all_gather(parts, t, group=self.group)
+        return [p.cpu().numpy() for p in parts]
+
 
 class LocalComm:
     """The same collectives between engines of one process, one thread per
@@ -97,6 +118,10 @@ class LocalComm:
     def allreduce_max_i32(self, x: np.ndarray) -> np.ndarray:
         return np.maximum.reduce(self._exchange(np.asarray(x, np.int32)))
 
+    def allgather_bytes(self, x: np.ndarray):
+        # (x may be a view of the engine's send buffer: the slot holds a copy)
+        return self._exchange(np.array(x, np.uint8, copy=True))
+
 
 def _sub(b: abi.HostBatch, lo: int, hi: int, eref, cts) -> abi.HostBatch:
     """Events [lo, hi) of b with the given entry refs / create timestamps."""
@@ -111,6 +136,23 @@ def _sub(b: abi.HostBatch, lo: int, hi: int, eref, cts) -> abi.HostBatch:
 
 
 def submit_node(eng, batch: abi.HostBatch, seq: np.ndarray, comm=None) -> abi.HostVerdicts:
+    """This rank's ``batch`` (its shard's events in submission order, ``seq``
+    their increasing sequence numbers in the node's stream) with the node-wide
+    SystemRule semantics: the engine's per-window exchange when the engine has
+    one and its rules allow it, else the event all-gather protocol.  ``comm``
+    None: a TorchComm over the default process group."""
+    comm = comm or TorchComm()
+    if hasattr(eng, "submit_node"):
+        from .engine import EngineError
+        try:
+            return eng.submit_node(batch, seq, comm)
+        except EngineError as ex:
+            if ex.code != abi.SF_ERR_UNSUPPORTED:
+                raise
+    return submit_node_gather(eng, batch, seq, comm)
+
+
+def submit_node_gather(eng, batch: abi.HostBatch, seq: np.ndarray, comm=None) -> abi.HostVerdicts:
     """Decides this rank's ``batch`` (its shard's events, in submission order;
     ``seq`` = their increasing sequence numbers in the node's stream) with the
     node-wide SystemRule semantics.  Every rank of ``comm`` (default: a

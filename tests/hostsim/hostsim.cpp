@@ -12,6 +12,7 @@
 
 #include "../../sentinel_amd/csrc/sf_heavy.h"
 #include "../../sentinel_amd/csrc/sf_xflow.h"
+#include "../../sentinel_amd/csrc/sf_sysx.h"
 
 using namespace sf;
 
@@ -412,6 +413,13 @@ int hs_read_rule_state(hs_engine* e, uint32_t idx, sf_rule_state* out) {
     const DevRuleState& s = e->rstate[e->flow_pos[idx]];
     out->stored_tokens = s.stored_tokens; out->last_filled_time = s.last_filled; out->latest_passed_time = s.latest_passed;
     return SF_OK;
+}
+
+// the per-window exchange's plan step (sf_sysx.h sx_reduce) on host arrays
+void hs_sx_reduce(const int64_t* msgs, int N, SxPlan* pl, double qps, double interval_sec) {
+    SysRule r{};
+    r.qps = qps;
+    sx_reduce(msgs, N, pl, r, interval_sec);
 }
 
 }  // extern "C"

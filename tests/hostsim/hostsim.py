@@ -31,6 +31,7 @@ def lib():
         L.hs_read_context_node.argtypes = [P, C.c_uint32, C.c_uint32, C.POINTER(abi.sf_node_state)]
         L.hs_load_degrade_rules.argtypes = [P, C.POINTER(abi.sf_degrade_rule), C.c_uint32, C.POINTER(C.c_uint32)]
         L.hs_read_breaker.argtypes = [P, C.c_uint32, C.POINTER(abi.sf_breaker_state)]
+        L.hs_sx_reduce.argtypes = [P, C.c_int, P, C.c_double, C.c_double]
         _lib = L
     return _lib
 

@@ -235,3 +235,37 @@ def test_gpu_config4_shape_over_capacity_matches_the_lru_reference():
     assert (got.status == abi.V_BLOCK_PARAM).sum() > 1000 and (got.status == abi.V_BLOCK_SYSTEM).sum() > 1000
     assert np.array_equal(got.status, lru.status)
     assert np.array_equal(got.wait_ms, lru.wait_ms) and np.array_equal(got.rule_idx, lru.rule_idx)
+
+
+@pytest.mark.gpu
+def test_gpu_param_thread_counts_on_the_wave_path():
+    """ParameterMetric's thread counts after a Zipf batch whose ParamFlow
+    segments run on the wavefront path (heavy_param, one table update per
+    distinct value of a 64-event group): every counted value of every
+    resource equals the oracle's (ParamFlowStatisticEntryCallback adds one
+    per passing entry, ParameterMetric.addThreadCount :184-239)."""
+    from oracle import oracle as so
+    from sentinel_amd import engine, trace
+    R = 24
+    rules, b = trace.param_zipf(R, 200_000, 5000, duration_ms=2000, seed=7)
+    cfg = abi.default_config(max_resources=R, max_batch=b.n, param_capacity=1 << 20)
+    e = engine.FlowEngine(cfg)
+    o = so.OracleEngine(cfg)
+    try:
+        e.load_param_rules(rules)
+        o.load_param_rules(rules)
+        got = e.submit(b)
+        want = o.submit(b)
+        assert np.array_equal(got.status, want.status)
+        checked = big = 0
+        for r in range(R):
+            sel = b.res_id == r
+            vals, cnt = np.unique(b.arg_bits[0][sel], return_counts=True)
+            for v in vals[np.argsort(-cnt)][:40]:
+                w = o.param_thread(r, 0, (abi.TAG_LONG, int(v)))
+                assert e.param_thread(r, 0, (abi.TAG_LONG, int(v))) == w, (r, int(v))
+                checked += 1
+                big += w > 1
+        assert checked > 500 and big > 50
+    finally:
+        e.close()

@@ -1,5 +1,6 @@
-"""The sharded SystemRule round protocol (sentinel_amd/system_shard.py) timed
-with two ranks on one GPU: two processes (gloo on 127.0.0.1), each an engine
+"""The sharded SystemRule protocols (sentinel_amd/system_shard.py) timed
+with two ranks on one GPU: the per-window exchange (sf_submit_node, the
+default) or, with --gather, the event all-gather round protocol: two processes (gloo on 127.0.0.1), each an engine
 on cuda:0 holding the resources ``res % 2 == rank`` of a config-4-shaped batch
 (ParamFlow rules, Zipf keys, inbound-QPS SystemRule at 0.6x the offered
 rate).  Rank 0 prints one JSON line: wall time, planner rounds, bytes and
@@ -45,6 +46,12 @@ class CountingComm:
         self.log.append(("allreduce_max_i32", int(r.nbytes), time.perf_counter() - t))
         return r
 
+    def allgather_bytes(self, x):
+        t = time.perf_counter()
+        r = self.inner.allgather_bytes(x)
+        self.log.append(("allgather_bytes", int(x.nbytes), time.perf_counter() - t))
+        return r
+
 
 def worker(rank, world, port, a, q):
     import numpy as np
@@ -63,11 +70,15 @@ def worker(rank, world, port, a, q):
     comm = CountingComm(system_shard.TorchComm())
     dist.barrier()
     t = time.perf_counter()
-    v = system_shard.submit_node(e, part, sel, comm)
+    if a.gather:
+        v = system_shard.submit_node_gather(e, part, sel, comm)
+    else:
+        v = system_shard.submit_node(e, part, sel, comm)
     dist.barrier()
     wall = time.perf_counter() - t
+    rounds = int(e.stats().sys_rounds)
     e.close()
-    q.put((rank, sel, v.status, v.wait_ms, v.rule_idx, wall, comm.log))
+    q.put((rank, sel, v.status, v.wait_ms, v.rule_idx, wall, comm.log, rounds))
     dist.destroy_process_group()
 
 
@@ -76,6 +87,7 @@ def main():
     ap.add_argument("--events", type=int, default=1 << 21)
     ap.add_argument("--resources", type=int, default=1000)
     ap.add_argument("--frac", type=float, default=0.6)
+    ap.add_argument("--gather", action="store_true", help="the event all-gather protocol instead of the exchange")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     import numpy as np
@@ -89,6 +101,7 @@ def main():
     for p in procs:
         p.start()
     parts = dict((x[0], x[1:]) for x in (q.get(timeout=900) for _ in range(2)))
+    # (parts[r]: sel, status, wait, rule, wall, log, rounds)
     for p in procs:
         p.join(timeout=120)
     from sentinel_amd import abi, engine
@@ -107,14 +120,19 @@ def main():
     e.close()
     want = np.stack([v.status, v.wait_ms, v.rule_idx]).astype(np.int64)
     log = parts[0][5]
-    rounds = sum(1 for k, _, _ in log if k == "allreduce_max_i32")
     ag = [x for x in log if x[0] == "allgather_i64"]
     ar = [x for x in log if x[0] == "allreduce_max_i32"]
-    res = {"what": "sharded SystemRule round protocol (system_shard.submit_node), 2 ranks (gloo) on one GPU, "
+    xb = [x for x in log if x[0] == "allgather_bytes"]
+    proto = ("event all-gather round protocol (system_shard.submit_node_gather)" if a.gather else
+             "per-window exchange (sf_submit_node via system_shard.submit_node)")
+    res = {"what": f"sharded SystemRule, {proto}, 2 ranks (gloo) on one GPU, "
                    f"config-4 shape: {a.resources} resources with ParamFlow rules, Zipf keys, "
                    f"inbound QPS at {a.frac}x offered", "events": int(b.n),
            "wall_ms_max_over_ranks": round(1e3 * max(parts[r][4] for r in range(2)), 3),
-           "planner_rounds": rounds,
+           "planner_rounds": parts[0][6] if not a.gather else len(ar),
+           "exchange": {"calls": len(xb), "bytes_sent_per_rank": int(sum(x[1] for x in xb)),
+                        "bytes_per_call_max": int(max((x[1] for x in xb), default=0)),
+                        "ms": round(1e3 * sum(x[2] for x in xb), 3)},
            "allgather": {"calls": len(ag), "bytes": int(sum(x[1] for x in ag)),
                          "ms": round(1e3 * sum(x[2] for x in ag), 3)},
            "allreduce_per_round": {"calls": len(ar), "bytes_mean": round(float(np.mean([x[1] for x in ar])), 1)
