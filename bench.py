@@ -51,6 +51,10 @@ def main():
                          "time the shard of the rank holding the Zipf head and of the lightest rank (one JSON line)")
     ap.add_argument("--origin-variants", default="no_origin_rules,other_rules_1pct",
                     help="config3_origin leg: the variants to run")
+    ap.add_argument("--placement", type=int, default=16384,
+                    help="N > 1: move the top-K resources (by the previous batch's counts) across the ranks, LPT "
+                         "greedy (sentinel_amd/placement.py); 0 = every resource at res % N")
+    ap.add_argument("--no-system-leg", action="store_true", help="N > 1: skip the RCCL SystemRule exchange leg")
     ap.add_argument("--heavy-min", type=int, default=0,
                     help="segments of more events than this go to the heavy kernels (0: the engine default, 512)")
     args = ap.parse_args()
@@ -75,19 +79,34 @@ def main():
     assert world == args.gpus or world == 1, "launch N>1 with torch.distributed.run"
 
     R_total = args.resources
-    R_local = (R_total - rank + world - 1) // world
     t0 = time.time()
-    # rules of the whole node (config 3's table over the 10M resources), this
-    # rank's shard res % N == rank
-    grade_all, beh_all, count_all = trace.mixed_rule_table(R_total, seed=3)
-    mine = np.arange(rank, R_total, world, dtype=np.uint32)
-    grade, beh, count = grade_all[mine], beh_all[mine], count_all[mine]
-    rules = abi.flow_rules_np(mine, grade, count, beh)
-    del grade_all, beh_all, count_all
     # the node-wide trace: N = 1 is config 3's batch; N > 1 superposes N
     # config-3 traces over all 10M resources (component c = seed 3 + c, built
-    # by rank c) and hash-shards the result, rank r keeping res % N == r
-    hb = node_trace(R_total, args.events, world, rank, dist)
+    # by rank c) and shards the result, rank r keeping the resources the
+    # placement gives it (the top-K by count spread LPT-greedy, the rest at
+    # res % N; sentinel_amd/placement.py), renamed to their engine ids
+    hb, pl = node_trace(R_total, args.events, world, rank, dist, args.placement)
+    # rules of the whole node (config 3's table over the 10M resources), this
+    # rank's shard, by engine id; per engine row (id // N) for the roofline model
+    grade_all, beh_all, count_all = trace.mixed_rule_table(R_total, seed=3)
+    if pl is None:
+        mine_res = np.arange(rank, R_total, world, dtype=np.int64)
+        mine_eid = mine_res
+        R_local = (R_total - rank + world - 1) // world
+    else:
+        mine_res = np.nonzero(pl.owner(np.arange(R_total)) == rank)[0]
+        mine_eid = pl.engine_id(mine_res)
+        R_local = pl.local_rows()
+    rules = abi.flow_rules_np(mine_eid.astype(np.uint32), grade_all[mine_res], count_all[mine_res], beh_all[mine_res])
+    grade = np.zeros(R_local, np.int32)
+    beh = np.zeros(R_local, np.int32)
+    grade[mine_eid // world] = grade_all[mine_res]
+    beh[mine_eid // world] = beh_all[mine_res]
+    res_of_eid = None
+    if pl is not None:
+        res_of_eid = np.full(pl.R_pad + world * pl.extra, -1, np.int64)
+        res_of_eid[pl.eid] = np.arange(R_total)
+    del grade_all, beh_all, count_all, mine_res, mine_eid
     n_entry = int(((hb.flags & abi.EV_EXIT) == 0).sum())
     n_exit = hb.n - n_entry
     log(f"[rank {rank}] trace {hb.n} events ({n_entry} entries) over {R_local} resources in {time.time()-t0:.1f}s")
@@ -295,7 +314,7 @@ def main():
     metric_log = None
     if not args.no_metric_log:
         try:
-            metric_log = metric_log_leg(eng, hb, R_total, R_local, world, rank, steps)
+            metric_log = metric_log_leg(eng, hb, R_total, R_local, world, rank, steps, res_of_eid)
         except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
             metric_log = {"error": str(ex)[:200]}
 
@@ -335,6 +354,15 @@ def main():
             except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
                 legs[nm] = {"error": str(ex)[:300]}
 
+    # SystemRules on the sharded node (N > 1): config 4's shape decided through
+    # the per-window exchange over RCCL (sf_submit_node)
+    system_exchange = None
+    if dist and not args.no_system_leg:
+        try:
+            system_exchange = system_exchange_leg(world, rank, int(os.environ.get("LOCAL_RANK", "0")), dist)
+        except Exception as ex:  # pragma: no cover - reported, not fatal for the decision bench
+            system_exchange = {"error": str(ex)[:300]}
+
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 1), "unit": "decisions/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 3),
@@ -345,11 +373,15 @@ def main():
                            "resources": R_total, "events_per_batch_per_gpu": hb.n, "entries_per_batch_per_gpu": n_entry,
                            "resources_touched": n_seg, "pass_fraction": round(n_pass / max(1, n_entry), 4),
                            "parallelism": f"resource-sharded x{world}",
+                           "placement": None if pl is None else
+                           {"what": "top-K resources by count spread LPT-greedy over the ranks, the rest at res % N "
+                                    "(counts of the previous batch: the bench's batches repeat one trace shifted "
+                                    "in time)", "K": int(pl.moved.size), "engine_rows_per_rank": R_local},
                            "trace": "one node-wide trace: N config-3 batches of 2^27 events over all 10M resources "
                                     "(seeds 3..3+N-1, the same 4 s) superposed, rank r deciding res % N == r"
                                     if world > 1 else "config-3 batch, seed 3", "per_rank": per_rank},
                 "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "aggregate": aggregate,
-                "metric_log": metric_log, "degrade": degrade, **legs}
+                "metric_log": metric_log, "degrade": degrade, "system_exchange": system_exchange, **legs}
         print(json.dumps(line), flush=True)
     for b in batches[1:]:
         b.free()
@@ -359,20 +391,31 @@ def main():
         dist.destroy_process_group()
 
 
-def node_trace(R_total, n, world, rank, dist):
-    """This rank's shard of one node-wide trace.  Component c (built by rank
-    c) is a config-3 batch of n events over all R_total resources (seed 3 + c,
-    the same 4 s of trace time); the node's trace is the superposition of the
-    N components (N times the traffic of one), merged in time order (events of
-    one millisecond in component order), and hash-sharded: rank r keeps the
-    events of res % N == r, so the rank holding the Zipf head gets more events
-    than the others.  Exits stay with their entries (same resource).  The
-    components' parts travel between ranks by all_to_all over the host
+def node_trace(R_total, n, world, rank, dist, placement_k=0):
+    """This rank's shard of one node-wide trace, and the placement.  Component
+    c (built by rank c) is a config-3 batch of n events over all R_total
+    resources (seed 3 + c, the same 4 s of trace time); the node's trace is
+    the superposition of the N components (N times the traffic of one),
+    merged in time order (events of one millisecond in component order), and
+    sharded: by default rank r keeps the events of res % N == r, so the rank
+    holding the Zipf head gets more events than the others; with placement_k
+    the top-K resources by the node's counts (all-reduced over the ranks) are
+    spread LPT-greedy (sentinel_amd/placement.py) and every event carries its
+    resource's engine id.  Exits stay with their entries (same resource).
+    The components' parts travel between ranks by all_to_all over the host
     process group."""
     comp = trace.mixed_zipf(R_total, n, duration_ms=DURATION_MS, seed=3 + rank)
     if world == 1:
-        return comp
+        return comp, None
     import torch
+    pl = None
+    if placement_k:
+        from sentinel_amd.placement import Placement
+        cnt_t = torch.from_numpy(np.bincount(comp.res_id, minlength=R_total).astype(np.int64))
+        dist.all_reduce(cnt_t)
+        pl = Placement.balanced(cnt_t.numpy(), world, placement_k)
+        del cnt_t
+        comp.res_id = pl.engine_id(comp.res_id).astype(np.uint32)
     dest = (comp.res_id % world).astype(np.uint8)
     order = np.argsort(dest, kind="stable")
     send = np.bincount(dest, minlength=world).astype(np.int64)
@@ -408,7 +451,7 @@ def node_trace(R_total, n, world, rank, dist):
     newpos[mo] = np.arange(mo.size)
     er = er[mo]
     er = np.where(er >= 0, newpos[np.clip(er, 0, None)], -1)
-    return abi.HostBatch(res[mo], ts[mo], cnt[mo], fl[mo], entry_ref=er)
+    return abi.HostBatch(res[mo], ts[mo], cnt[mo], fl[mo], entry_ref=er), pl
 
 
 def predict_ranks(args, steps=None, warmup=None):
@@ -435,10 +478,17 @@ def predict_ranks(args, steps=None, warmup=None):
             single = time_shard(comp, abi.flow_rules_np(np.arange(R, dtype=np.uint32), grade_all, count_all,
                                                         beh_all), R, 1, 0, steps, warmup)
             log(f"[predict] single GPU: {single:.2f} ms/step")
-        rk = (comp.res_id % N).astype(np.int64)
         if c == 0:
-            sens = shard_share_sensitivity(np.bincount(comp.res_id, minlength=R), N)
+            per0 = np.bincount(comp.res_id, minlength=R)
+            sens = shard_share_sensitivity(per0, N)
             log(f"[predict] shard shares: {sens}")
+            pl = None
+            if args.placement:
+                from sentinel_amd.placement import Placement
+                pl = Placement.balanced(per0 * N, N, args.placement)   # (component 0 scaled: the previous batch)
+            del per0
+        eid = comp.res_id.astype(np.int64) if pl is None else pl.engine_id(comp.res_id)
+        rk = eid % N
         if counts is None:
             counts = np.bincount(rk, minlength=N).astype(np.int64) * N       # (component 0 scaled: the choice)
             head = int(np.argmax(counts)); light = int(np.argmin(counts))
@@ -449,8 +499,9 @@ def predict_ranks(args, steps=None, warmup=None):
             pos[sel] = np.arange(sel.size)
             er = comp.entry_ref[sel]
             er = np.where(er >= 0, pos[np.clip(er, 0, None)], -1)
-            parts.setdefault(r, []).append((comp.res_id[sel], comp.ts_ms[sel], comp.count[sel], comp.flags[sel], er))
-        del comp, rk
+            parts.setdefault(r, []).append((eid[sel].astype(np.uint32), comp.ts_ms[sel], comp.count[sel],
+                                            comp.flags[sel], er))
+        del comp, rk, eid
         log(f"[predict] component {c + 1}/{N} in {time.time() - t0:.0f}s")
     out = {"metric": METRIC, "mode": f"predict {N} ranks on one GPU", "n_ranks": N, "resources": R,
            "component_events": args.events, "steps": steps, "warmup": warmup, "ranks": {}}
@@ -470,9 +521,13 @@ def predict_ranks(args, steps=None, warmup=None):
         er = np.where(er >= 0, newpos[np.clip(er, 0, None)], -1)
         hb = abi.HostBatch(res[mo], ts[mo], cnt[mo], fl[mo], entry_ref=er)
         del res, ts, cnt, fl, er, mo, newpos, key
-        mine = np.arange(r, R, N, dtype=np.uint32)
-        rules = abi.flow_rules_np(mine, grade_all[mine], count_all[mine], beh_all[mine])
-        R_local = (R - r + N - 1) // N
+        if pl is None:
+            mine = np.arange(r, R, N, dtype=np.int64)
+            mine_eid, R_local = mine, (R - r + N - 1) // N
+        else:
+            mine = np.nonzero(pl.owner(np.arange(R)) == r)[0]
+            mine_eid, R_local = pl.engine_id(mine), pl.local_rows()
+        rules = abi.flow_rules_np(mine_eid.astype(np.uint32), grade_all[mine], count_all[mine], beh_all[mine])
         n_entry = int(((hb.flags & abi.EV_EXIT) == 0).sum())
         log(f"[predict] rank {r}: {hb.n} events, t={time.time() - t0:.0f}s")
         ms = time_shard(hb, rules, R_local, N, r, steps, warmup)
@@ -482,6 +537,10 @@ def predict_ranks(args, steps=None, warmup=None):
         log(f"[predict] rank {r}: {ms:.2f} ms/step")
         del hb
     out["expected_events_per_rank"] = {str(k): int(v) for k, v in enumerate(counts)}
+    out["placement"] = None if pl is None else {
+        "what": "top-K resources by component 0's counts spread LPT-greedy over the ranks, the rest at res % N "
+                "(sentinel_amd/placement.py)", "K": int(pl.moved.size),
+        "max_over_mean_events_expected": round(float(counts.max() / counts.mean()), 4)}
     head_ms = out["ranks"][str(chosen[0])]["ms_per_step"]
     out["single_gpu_ms_per_step"] = round(single, 3)
     out["node_step_ms"] = head_ms
@@ -489,10 +548,11 @@ def predict_ranks(args, steps=None, warmup=None):
     out["implied_efficiency"] = round(single / head_ms, 4)
     # the same step under a hash of the resource name instead of the trace's
     # round-robin rank map: the head rank's time scaled by its share (time ~ events)
-    out["shard_share"] = sens
-    for q in ("p50", "p99"):
-        f = sens[f"random_hash_max_share_{q}"] / sens["trace_map_max_share"]
-        out[f"implied_efficiency_random_hash_{q}"] = round(single / (head_ms * f), 4)
+    out["shard_share"] = sens                    # (of the default map res % N)
+    if pl is None:
+        for q in ("p50", "p99"):
+            f = sens[f"random_hash_max_share_{q}"] / sens["trace_map_max_share"]
+            out[f"implied_efficiency_random_hash_{q}"] = round(single / (head_ms * f), 4)
     out["note"] = ("weak scaling: every rank decides its shard of one node-wide trace (N x 2^27 events); the node "
                    "step is the slowest rank's; implied efficiency = single-GPU step / head-rank step")
     print(json.dumps(out), flush=True)
@@ -735,6 +795,90 @@ def config2_leg(R=1_000_000, n=1 << 27, steps=3, parity=1):
         return res
     finally:
         e.close()
+
+
+def system_exchange_leg(world, rank, device, dist, R=1000, n_per_rank=1 << 21, keys=1_000_000, qps_frac=0.6):
+    """SystemRules on the sharded node (N > 1):
+    config 4's shape over the whole node -- R x N resources with QPS /
+    throttle ParamFlowRules, n x N events of Zipf(1.1) keys (weak scaling),
+    the inbound-QPS SystemRule at qps_frac x the node's offered rate -- every
+    rank deciding its shard res % N with sf_submit_node, the per-window
+    exchange over RCCL (device buffers, ncclAllGather of 4224 B per rank and
+    plan level).  Two runs on fresh engines, the second timed (barriers,
+    max over ranks).  Rank 0 then decides the whole node batch on one engine
+    (its GPU) and compares every verdict."""
+    from sentinel_amd import dist as sdist
+    RN, n = R * world, n_per_rank * world
+    rules, b = trace.param_zipf(RN, n, keys, duration_ms=DURATION_MS, seed=4)
+    sysr = [abi.sf_system_rule(highest_system_load=-1, highest_cpu_usage=-1, qps=qps_frac * n / (DURATION_MS / 1e3),
+                               avg_rt=-1, max_thread=-1)]
+    sel = np.nonzero(b.res_id % world == rank)[0]
+    part = b.shard(world, rank)
+    mine = [r for r in rules if r.resource % world == rank]
+    cap = 1 << int(np.ceil(np.log2(max(8 * part.n, 1 << 16))))
+    walls, v, st = [], None, None
+    backend, comm = "rccl", None
+    for rep in range(2):
+        e = engine.FlowEngine(abi.default_config(max_resources=R, max_batch=part.n, shard_count=world,
+                                                 shard_index=rank, device=device, param_capacity=cap))
+        try:
+            e.load_system_rules(sysr)
+            e.load_param_rules(mine)
+            if backend == "rccl":
+                sys.stdout.flush()
+                saved = os.dup(1)
+                os.dup2(2, 1)              # RCCL's banner: stdout keeps the one JSON line
+                try:
+                    sdist.rccl_join(e)
+                except engine.EngineError as ex:
+                    # (ranks sharing one device -- the one-GPU rehearsal: RCCL refuses
+                    # them; every rank alike, the communicator init is collective)
+                    backend = f"gloo (RCCL refused: {str(ex)[:80]})"
+                    from sentinel_amd import system_shard
+                    comm = system_shard.TorchComm()
+                finally:
+                    os.dup2(saved, 1)
+                    os.close(saved)
+            dist.barrier()
+            t = time.perf_counter()
+            v = e.submit_node(part, sel, comm)
+            wall = time.perf_counter() - t
+            dist.barrier()
+            walls.append(wall)
+            st = e.stats()
+        finally:
+            e.close()
+    import torch
+    tt = torch.tensor([walls[-1]], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    ms = tt.item() * 1e3
+    box = [None] * world if rank == 0 else None
+    dist.gather_object((sel, v.status, v.wait_ms, v.rule_idx), box, dst=0)
+    if rank != 0:
+        return None
+    got = np.full((3, b.n), -1, np.int64)
+    for s_, a_, w_, r_ in box:
+        got[:, s_] = np.stack([a_, w_, r_])
+    e = engine.FlowEngine(abi.default_config(max_resources=RN, max_batch=b.n, device=device,
+                                             param_capacity=1 << int(np.ceil(np.log2(max(8 * b.n, 1 << 16))))))
+    try:
+        e.load_system_rules(sysr)
+        e.load_param_rules(rules)
+        t = time.perf_counter()
+        one = e.submit(b)
+        one_ms = (time.perf_counter() - t) * 1e3
+    finally:
+        e.close()
+    want = np.stack([one.status, one.wait_ms, one.rule_idx]).astype(np.int64)
+    return {"what": f"config-4 shape on the sharded node: {RN} resources (ParamFlow, Zipf keys), {n} events, "
+                    f"inbound QPS SystemRule at {qps_frac}x the node's offered rate; sf_submit_node per rank over "
+                    "RCCL (per-window exchange, sf_sysx.h)", "ranks": world, "backend": backend,
+            "ms_per_batch_max_over_ranks": round(ms, 3), "decisions_per_s": round(n / (ms / 1e3), 1),
+            "planner_rounds": int(st.sys_rounds), "exchanges": int(st.sys_exchanges),
+            "bytes_per_exchange_per_rank": 4224, "one_engine_whole_batch_ms": round(one_ms, 3),
+            "system_blocks": int((want[0] == abi.V_BLOCK_SYSTEM).sum()),
+            "parity": {"vs": "one engine deciding the whole node batch", "mismatches":
+                       int((got != want).any(axis=0).sum()), "exact": bool((got == want).all())}}
 
 
 def config4_leg(R=1000, n=1 << 24, keys=100_000_000, qps_frac=0.6, reps=3, parity=1):
@@ -1015,15 +1159,17 @@ def degrade_leg(R=1_000_000, entries=1 << 22, steps=3):
         e.close()
 
 
-def metric_log_leg(eng, hb, R_total, R_local, world, rank, steps):
-    """Resource names "/r/NNNNNNNN" (global id) and types; a drain fetch at
+def metric_log_leg(eng, hb, R_total, R_local, world, rank, steps, res_of_eid=None):
+    """Resource names "/r/NNNNNNNN" (global id) and types, indexed by engine id
+    (res_of_eid: a placement's inverse map); a drain fetch at
     T_last + 2 s (cap 0: rows counted, lastFetchTime advanced, nothing
     copied), then the timed fetch at T_last + 3 s: the second [T_last + 2 s,
     T_last + 3 s) of every node (and ENTRY_NODE), formatted as metrics.log."""
-    ids = np.arange(R_total, dtype=np.int64)
+    ids = np.arange(R_total, dtype=np.int64) if res_of_eid is None else np.maximum(res_of_eid, 0)
+    n_ids = ids.size
     digits = ((ids[:, None] // (10 ** np.arange(7, -1, -1))) % 10 + 48).astype(np.uint8)
-    names = np.concatenate([np.frombuffer(b"/r/" * R_total, np.uint8).reshape(R_total, 3), digits], axis=1)
-    off = np.arange(R_total + 1, dtype=np.uint64) * 11
+    names = np.concatenate([np.frombuffer(b"/r/" * n_ids, np.uint8).reshape(n_ids, 3), digits], axis=1)
+    off = np.arange(n_ids + 1, dtype=np.uint64) * 11
     eng.load_resource_names_raw(names.tobytes(), off, (ids % 3).astype(np.int32))
     t_last = int(hb.ts_ms[0]) + (steps - 1) * DURATION_MS
     try:

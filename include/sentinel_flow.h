@@ -384,6 +384,7 @@ typedef struct sf_stats {         /* device-clock timings, summed over sf_submit
      * settled by the exact solve, chunks on the serial path, solve rounds,
      * events the serial part walked */
     uint64_t xw_chunks_exact, xw_chunks_serial, xw_rounds, xw_serial_events;
+    uint64_t sys_exchanges;       /* all-gathers of sf_submit_node's per-window exchange (SF_SYSX_MSG_BYTES each, plan step) */
 } sf_stats;
 
 typedef struct sf_heavy_profile { /* diagnostics: one heavy segment of the last sf_submit */
@@ -631,6 +632,7 @@ int  sf_format_metric_rows(sf_engine* e, const sf_metric_row* rows, uint32_t n, 
  * use the event all-gather protocol (sf_system_plan, sf_submit_forced,
  * sf_entry_node_add).  Without SystemRules it is sf_submit. */
 typedef int (*sf_allgather_fn)(void* ctx, const void* send, void* recv, uint64_t bytes);
+#define SF_SYSX_MSG_BYTES 4224     /* one rank's message of a plan level (sf_sysx.h SX_WORDS * 8) */
 int  sf_submit_node(sf_engine* e, const sf_event_batch* in, const int64_t* seq, sf_verdicts* out,
                     sf_allgather_fn allgather, void* ctx);
 

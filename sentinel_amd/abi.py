@@ -200,7 +200,7 @@ class sf_stats(C.Structure):
                 ("wire_ms", C.c_double), ("sys_rounds", C.c_uint64), ("aux_nodes", C.c_uint64),
                 ("aux_capacity", C.c_uint64), ("aux_index_grows", C.c_uint64), ("param_table_grows", C.c_uint64),
                 ("xw_chunks_exact", C.c_uint64), ("xw_chunks_serial", C.c_uint64), ("xw_rounds", C.c_uint64),
-                ("xw_serial_events", C.c_uint64)]
+                ("xw_serial_events", C.c_uint64), ("sys_exchanges", C.c_uint64)]
 
 
 class sf_heavy_profile(C.Structure):

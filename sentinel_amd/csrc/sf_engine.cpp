@@ -120,7 +120,6 @@ struct sf_engine {
     int64_t* sx_seq = nullptr;            // [max_batch] device copy of host sequence numbers
     uint8_t* sx_ibuf = nullptr;           // [max_batch] inert flags of the round
     std::vector<int64_t> sx_hsend, sx_hrecv;   // host side of a callback all-gather
-    uint64_t sx_levels = 0;               // exchange levels run (diagnostics)
     int64_t* agg = nullptr;               // [ws (S+60) | gws (S+60) | vals ((S+60)*6+1) | minrt (S+60)]
     // DegradeSlot circuit breakers (sf_degrade.hip)
     DegradeDev dg{};
@@ -189,7 +188,7 @@ static void free_work(Work& w) {
                     w.seg_start, w.seg_res, w.n_seg, w.s_ts, w.s_cnt, w.s_flags, w.s_eref,
                     w.s_cts, w.s_nargs, w.s_atag, w.s_abits, w.v_status, w.v_wait,
                     w.v_rule, w.sort_tmp, w.scan_tmp,
-                    w.segflag, w.seg_mode, w.light_list, w.lcounts, w.heavy_list, w.counters, w.pcg,
+                    w.segflag, w.seg_mode, w.light_list, w.lcounts, w.heavy_list, w.counters, w.pcg, w.segs_lb,
                     w.pscan_tmp, w.fill_tiles, w.fill_ntiles, w.acc_hw,
                     w.acc_sec, w.acc_hw_base, w.acc_sec_base, w.seg_hw0, w.seg_sec0,
                     w.seg_nhw, w.seg_nsec, w.hticks, w.passbits, w.stream_list, w.sticks,
@@ -308,7 +307,7 @@ static int alloc_work(sf_engine* e, Work& w) {
         WALLOC(w.light_list, off * 4);
     }
     WALLOC(w.heavy_list, SC * 4);
-    WALLOC(w.counters, 16 * 4); WALLOC(w.pcg, N * 8);
+    WALLOC(w.counters, 16 * 4); WALLOC(w.pcg, N * 8); WALLOC(w.segs_lb, segs_lb_bytes((uint32_t)N));
     // <= len/TILE + 2 tiles per heavy segment; a ParamFlow-only segment of more
     // than 32 events is heavy too (SM_PARAM, k_classify), whatever heavy_min
     w.fill_tile_cap = (uint32_t)(N / FILL_TILE + 2 * (N / (std::min<uint32_t>(w.heavy_min, 32u) + 1)) + 2);
@@ -1652,7 +1651,7 @@ int sf_submit_node(sf_engine* e, const sf_event_batch* in, const int64_t* seq, s
     e->stats.n_events = n;
     e->stats.n_launches++;
     e->stats.sys_rounds += rounds;
-    e->sx_levels += levels;
+    e->stats.sys_exchanges += levels;
     if (out->mem == SF_MEM_HOST && n) {
         HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, s));
         if (dv.wait) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait, (size_t)n * 4, hipMemcpyDeviceToHost, s));

@@ -230,6 +230,7 @@ struct Work {
     uint32_t lcap[LCLS];                                //   front, lean QPS (SM_LIGHTQ) from the back                                // light_list region of each length class   // [0] n_light [1] n_heavy front [2] hw slots [3] sec slots [4] n_heavy back
                                                                       // [5] n_stream front [6] n_stream back
     int64_t* pcg; void* pscan_tmp; size_t pscan_tmp_bytes;
+    void* segs_lb;                                      // k_segs_lb's tile states (segs_lb_bytes)
     uint2* fill_tiles; uint32_t fill_tile_cap;         // [2][cap] (segment, tile) of each class for k_heavy_fill
     uint32_t* fill_ntiles;                              // [2] tiles per class
     uint32_t fill_grid;                                 // persistent k_heavy_fill workgroups (8 per CU)
@@ -353,6 +354,7 @@ hipError_t launch_fmt_write(const sf_metric_row* rows, const uint32_t* order, ui
                             const uint64_t* name_off, const int32_t* types, uint32_t n_names, int64_t tz,
                             const uint64_t* line_off, char* out, hipStream_t s);
 hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipStream_t s);   // out[0] used, out[1] max probe
+size_t segs_lb_bytes(uint32_t max_n);
 hipError_t launch_param_thread_read(const DevState& st, uint32_t l, int idx, uint32_t tag, uint64_t bits,
                                     long long* out, hipStream_t s);
 // classify = true: k_classify / k_fill_tiles end the sort phase (the origin

@@ -193,6 +193,207 @@ __global__ void k_segs(DevBatch b, const int32_t* s_cnt, const uint8_t* s_flags,
     if (((heads >> lane) & 1ull) && acc) atomicOr(&segflag[sid], acc);
 }
 
+// ============================================================ segment table + prefixes in one pass
+// One single-pass scan over the sorted keys (decoupled look-back, tiles taken
+// in order through an atomic counter so every tile's predecessors are running
+// or done): per position the inclusive count of segment heads (head_scan,
+// the segment id + 1) and, when the decide phase's window budgets need it,
+// the inclusive prefix of the entries' acquireCounts (pcg: 0 for exits and
+// EVF_SYSBLK entries, k_heavy_decide's greedy prefix), and the segment table
+// (start, resource, flags) -- what the rocprim head scan, k_segs and the
+// rocprim acquireCount scan wrote in three passes.
+constexpr int SL_T = 256, SL_K = 16, SL_TILE = SL_T * SL_K;       // 4096 positions per tile
+constexpr unsigned long long SL_AGG = 1ull << 32, SL_INC = 2ull << 32;
+size_t segs_lb_bytes(uint32_t max_n) { return ((size_t)max_n / SL_TILE + 2) * 24 + 64; }   // (sf_internal.h)
+
+struct SegsLB {
+    unsigned long long* status;   // [tiles] flag << 32 | heads (aggregate, then inclusive)
+    long long* acq_agg;           // [tiles]
+    long long* acq_inc;           // [tiles]
+    unsigned int* ticket;
+};
+
+__device__ __forceinline__ unsigned long long sl_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sl_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool PCG>
+__global__ void __launch_bounds__(SL_T) k_segs_lb(DevBatch b, const int32_t* s_cnt, const uint8_t* s_flags,
+                                                  const uint8_t* s_atag, const uint32_t* keys, uint32_t* head_scan,
+                                                  int64_t* pcg, uint32_t* seg_start, uint32_t* seg_res,
+                                                  uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts,
+                                                  const int32_t* err, bool exit_marks, int32_t* prio_seen, SegsLB lb) {
+    __shared__ uint32_t s_tile;
+    __shared__ uint32_t w_heads[SL_T / 64];
+    __shared__ long long w_acq[SL_T / 64];
+    __shared__ uint32_t p_heads;
+    __shared__ long long p_acq;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(lb.ticket, 1u);
+    __syncthreads();
+    const uint32_t t = s_tile, n = b.n;
+    const uint32_t p0 = t * SL_TILE + (uint32_t)tid * SL_K;
+    // this thread's 16 keys and the one before them
+    uint32_t k[SL_K];
+    uint32_t hmask = 0;
+    int32_t c[SL_K];
+    uint8_t f[SL_K];
+    if (p0 + SL_K <= n) {
+        const uint4* kp = (const uint4*)(keys + p0);
+#pragma unroll
+        for (int q = 0; q < SL_K / 4; q++) { const uint4 v = kp[q]; k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w; }
+        const uint4 fv = *(const uint4*)(s_flags + p0);
+        const uint32_t fw[4] = {fv.x, fv.y, fv.z, fv.w};
+#pragma unroll
+        for (int q = 0; q < SL_K; q++) f[q] = (uint8_t)(fw[q >> 2] >> (8 * (q & 3)));
+        if (PCG) {
+            const int4* cp = (const int4*)(s_cnt + p0);
+#pragma unroll
+            for (int q = 0; q < SL_K / 4; q++) { const int4 v = cp[q]; c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w; }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < SL_K; q++) {
+            const bool in = p0 + q < n;
+            k[q] = in ? keys[p0 + q] : 0u;
+            f[q] = in ? s_flags[p0 + q] : (uint8_t)SF_EV_EXIT;
+            c[q] = (PCG && in) ? s_cnt[p0 + q] : 0;
+        }
+    }
+    const uint32_t kprev = (p0 > 0 && p0 < n) ? keys[p0 - 1] : ~0u;
+    uint32_t heads = 0;
+    long long acq = 0;
+#pragma unroll
+    for (int q = 0; q < SL_K; q++) {
+        const bool in = p0 + q < n;
+        const bool h = in && (p0 + q == 0 || k[q] != (q ? k[q - 1] : kprev));
+        hmask |= (h ? 1u : 0u) << q;
+        heads += h;
+        if (PCG) acq += (in && !(f[q] & (SF_EV_EXIT | EVF_SYSBLK))) ? (long long)c[q] : 0;
+    }
+    // block exclusive scan of (heads, acq) over the threads
+    uint32_t hx = heads;
+    long long ax = acq;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t h2 = __shfl_up(hx, d);
+        const long long a2 = __shfl_up(ax, d);
+        if (lane >= d) { hx += h2; ax += a2; }
+    }
+    if (lane == 63) { w_heads[wv] = hx; w_acq[wv] = ax; }
+    __syncthreads();
+    uint32_t hbase = 0, htot = 0;
+    long long abase = 0, atot = 0;
+#pragma unroll
+    for (int w = 0; w < SL_T / 64; w++) {
+        if (w < wv) { hbase += w_heads[w]; abase += w_acq[w]; }
+        htot += w_heads[w]; atot += w_acq[w];
+    }
+    hx = hx - heads + hbase;               // exclusive within the tile
+    ax = ax - acq + abase;
+    // publish the aggregate, look back for the exclusive prefix, publish the inclusive value
+    if (wv == 0) {
+        uint32_t ph = 0;
+        long long pa = 0;
+        if (t == 0) {
+            if (lane == 0) {
+                __hip_atomic_store(&lb.acq_inc[0], atot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sl_store(&lb.status[0], SL_INC | htot);
+            }
+        } else {
+            if (lane == 0) {
+                __hip_atomic_store(&lb.acq_agg[t], atot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sl_store(&lb.status[t], SL_AGG | htot);
+            }
+            int64_t base = (int64_t)t - 1;
+            for (;;) {
+                const int64_t idx = base - lane;
+                const unsigned long long w = idx >= 0 ? sl_load(&lb.status[idx]) : SL_INC;
+                const unsigned long long flag = w >> 32;
+                const unsigned long long pm = __ballot(flag == 2);
+                const int firstp = pm ? __ffsll((long long)pm) - 1 : 64;
+                const unsigned long long upto = firstp == 64 ? ~0ull : ((2ull << firstp) - 1ull);
+                if (__ballot(flag == 0) & upto) continue;            // a predecessor not published yet
+                uint32_t vh = 0;
+                long long va = 0;
+                if (lane <= firstp && idx >= 0) {
+                    vh = (uint32_t)w;
+                    va = flag == 2 ? __hip_atomic_load(&lb.acq_inc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : __hip_atomic_load(&lb.acq_agg[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+#pragma unroll
+                for (int d = 32; d > 0; d >>= 1) { vh += __shfl_xor(vh, d); va += __shfl_xor(va, d); }
+                ph += vh; pa += va;
+                if (firstp < 64) break;
+                base -= 64;
+            }
+            if (lane == 0) {
+                __hip_atomic_store(&lb.acq_inc[t], pa + atot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sl_store(&lb.status[t], SL_INC | (ph + htot));
+            }
+        }
+        if (lane == 0) { p_heads = ph; p_acq = pa; }
+    }
+    __syncthreads();
+    if (p0 >= n) return;
+    uint32_t hs = p_heads + hx;            // heads before this thread's first position
+    long long run = p_acq + ax;
+    uint32_t hsv[SL_K];
+    long long pv[SL_K];
+    uint32_t acc = 0, prio = 0;
+    int64_t cur = hs ? (int64_t)hs - 1 : -1;   // the segment of the position before this thread's first
+#pragma unroll
+    for (int q = 0; q < SL_K; q++) {
+        const uint32_t p = p0 + q;
+        const bool in = p < n;
+        if ((hmask >> q) & 1u) {
+            if (acc && cur >= 0) atomicOr(&segflag[cur], acc);
+            acc = 0;
+            hs++;
+            cur = (int64_t)hs - 1;
+            seg_start[hs - 1] = p;
+            seg_res[hs - 1] = k[q];
+        }
+        hsv[q] = hs;
+        if (PCG) { run += (in && !(f[q] & (SF_EV_EXIT | EVF_SYSBLK))) ? (long long)c[q] : 0; pv[q] = run; }
+        if (!in) continue;
+        uint32_t mine = 0;
+        if (exit_marks && (f[q] & SF_EV_EXIT)) mine |= SEGF_EXIT;
+        if (!(f[q] & SF_EV_EXIT)) {
+            const int32_t cq = PCG ? c[q] : s_cnt[p];
+            mine |= ((f[q] & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (cq <= 0 ? SEGF_NONPOS : 0u) |
+                    ((f[q] & EVF_SYSBLK) ? SEGF_SYS : 0u);
+        }
+        for (uint32_t a = 0; a < b.arg_slots; a++)
+            if (s_atag[(size_t)a * n + p] == SF_TAG_COLLECTION) mine |= SEGF_COLL;
+        acc |= mine;
+        prio |= mine & SEGF_PRIO;
+        if (p == n - 1) { *n_seg = hs; seg_start[hs] = n; }
+        if (p == 0 && *err == 0) *last_ts = b.ts[n - 1];      // the sort's first pass has read the old value
+    }
+    if (acc && cur >= 0) atomicOr(&segflag[cur], acc);
+    if (__ballot(prio != 0) && lane == 0) atomicOr(prio_seen, 1);
+    if (p0 + SL_K <= n) {
+        uint4* hp = (uint4*)(head_scan + p0);
+#pragma unroll
+        for (int q = 0; q < SL_K / 4; q++) hp[q] = make_uint4(hsv[4 * q], hsv[4 * q + 1], hsv[4 * q + 2], hsv[4 * q + 3]);
+        if (PCG) {
+            longlong2* pp = (longlong2*)(pcg + p0);
+#pragma unroll
+            for (int q = 0; q < SL_K / 2; q++) pp[q] = make_longlong2(pv[2 * q], pv[2 * q + 1]);
+        }
+    } else {
+        for (int q = 0; q < SL_K; q++) {
+            if (p0 + q >= n) break;
+            head_scan[p0 + q] = hsv[q];
+            if (PCG) pcg[p0 + q] = pv[q];
+        }
+    }
+}
+
 struct HeadFlag {       // 1 where a new resource segment starts in the sorted keys
     const uint32_t* keys;
     __device__ uint32_t operator()(uint32_t j) const { return (j == 0 || keys[j] != keys[j - 1]) ? 1u : 0u; }
@@ -1997,6 +2198,16 @@ static void launch_classify(const DevState& st, Work& w, const DevBatch& b, hipS
     if (timing) hipEventRecord(ev[2], s);
 }
 
+static bool sort_uses_rocprim() {
+    static const bool v = [] { const char* x = getenv("SF_SORT_ROCPRIM"); return x && x[0] == '1'; }();
+    return v;
+}
+// k_segs_lb (one pass) or, SF_SEGS_LB=0, the rocprim head scan + k_segs + the rocprim acquireCount scan (A/B)
+static bool segs_one_pass() {
+    static const bool v = [] { const char* x = getenv("SF_SEGS_LB"); return !(x && x[0] == '0'); }();
+    return v && !sort_uses_rocprim();
+}
+
 hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t shard_count, uint32_t shard_index,
                        uint32_t key_bits, hipStream_t s, hipEvent_t* ev, bool timing, bool classify) {
     const uint32_t n = b.n;
@@ -2006,7 +2217,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     hipError_t e;
     const bool org = b.origin != nullptr;                       // the origin rides in a 12-B payload
     // the hand-written chunked LSD sort (sf_rsort.h); SF_SORT_ROCPRIM=1: k_keys_packed + rocprim onesweep (A/B)
-    static const bool use_rocprim = [] { const char* v = getenv("SF_SORT_ROCPRIM"); return v && v[0] == '1'; }();
+    const bool use_rocprim = sort_uses_rocprim();
     if (!use_rocprim) {
         // middle passes in (keys_in, pv_in) and (head_scan, pv_out); the last pass writes keys_out and the sorted SoA
         const RsBatchSrc src{b, shard_count, shard_index, st.R, st.err, st.last_ts, st.xmap};
@@ -2032,7 +2243,7 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
                                       key_bits, s);
     }
     if (e != hipSuccess) return e;
-    {
+    if (!segs_one_pass()) {
         HeadIter hit(rocprim::counting_iterator<uint32_t>(0), HeadFlag{w.keys_out});
         e = rocprim::inclusive_scan<HeadScanCfg>(w.scan_tmp, w.scan_tmp_bytes, hit, w.head_scan, (size_t)n,
                                     rocprim::plus<uint32_t>(), s);
@@ -2040,11 +2251,27 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
     }
     hipMemsetAsync(w.segflag, 0, (size_t)(n < st.R ? n : st.R) * 4, s);
     if (timing) hipEventRecord(ev[1], s);
-    if (!use_rocprim)
+    if (!use_rocprim && !segs_one_pass()) {
         hipLaunchKernelGGL(k_segs, dim3(blocks(n, T)), dim3(T), 0, s, b, w.s_cnt, w.s_flags, w.s_atag, w.keys_out,
                            w.head_scan, w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err,
                            st.n_prule != 0, st.prio_seen);
-    else if (org)
+    } else if (!use_rocprim) {
+        // segment table, head scan and (window rules loaded) the acquireCount prefix in one pass
+        const uint32_t tiles = (n + SL_TILE - 1) / SL_TILE;
+        char* lbp = (char*)w.segs_lb;
+        const SegsLB lb{(unsigned long long*)lbp, (long long*)(lbp + ((size_t)tiles + 1) * 8),
+                        (long long*)(lbp + ((size_t)tiles + 1) * 16), (unsigned int*)(lbp + ((size_t)tiles + 1) * 24)};
+        hipMemsetAsync(lbp, 0, ((size_t)tiles + 1) * 8, s);
+        hipMemsetAsync(lb.ticket, 0, 4, s);
+        if (st.n_window_rules)
+            hipLaunchKernelGGL(k_segs_lb<true>, dim3(tiles), dim3(SL_T), 0, s, b, w.s_cnt, w.s_flags, w.s_atag,
+                               w.keys_out, w.head_scan, w.pcg, w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts,
+                               st.err, st.n_prule != 0, st.prio_seen, lb);
+        else
+            hipLaunchKernelGGL(k_segs_lb<false>, dim3(tiles), dim3(SL_T), 0, s, b, w.s_cnt, w.s_flags, w.s_atag,
+                               w.keys_out, w.head_scan, w.pcg, w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts,
+                               st.err, st.n_prule != 0, st.prio_seen, lb);
+    } else if (org)
         hipLaunchKernelGGL(k_unpack<true>, dim3(blocks(n, T)), dim3(T), 0, s, b, (const void*)w.pv_out, w.keys_out,
                            w.perm, w.s_ts, w.s_cnt, w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan,
                            w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err, st.n_prule != 0, w.s_origin,
@@ -2328,10 +2555,10 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
         hipStreamWaitEvent(s4, ev[5], 0);
         launch_xw(s4);
     }
-    if (st.n_window_rules) {
+    if (st.n_window_rules && !segs_one_pass()) {
         // acquireCount prefix of the entries (QPS / WarmUp window budgets, k_heavy_decide
-        // only): state-independent, but here on stream B rather than in the sort phase,
-        // the longer of the two pipelined phases
+        // only; the hand-written sort path writes it in k_segs_lb): state-independent, but
+        // here on stream B rather than in the sort phase, the longer of the two pipelined phases
         PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
         const hipError_t e = rocprim::inclusive_scan<PcScanCfg>(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg,
                                                                 (size_t)n, rocprim::plus<int64_t>(), s2);

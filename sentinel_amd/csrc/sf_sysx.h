@@ -48,6 +48,7 @@ namespace sf {
 constexpr int SX_B = 128;                 // bins per level
 constexpr int SX_DELTA = 16;              // int64 words of a rank's ENTRY_NODE contribution
 constexpr int SX_WORDS = SX_DELTA + 4 * SX_B;
+static_assert(SX_WORDS * 8 == SF_SYSX_MSG_BYTES, "sentinel_flow.h SF_SYSX_MSG_BYTES");
 // message words: delta [0, 16): key (plan window index, -1: none), second
 // bucket (pass, block, succ, rt, exc, touched), minute bucket (same), minRt of
 // each, threads; then u[SX_B], n[SX_B], cmin[SX_B], cmax[SX_B]

@@ -331,7 +331,8 @@ def _node_trace_worker(rank, world, port, q):
     import bench
     os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    hb = bench.node_trace(5000, 200_000, world, rank, dist)
+    hb, pl = bench.node_trace(5000, 200_000, world, rank, dist)
+    assert pl is None
     q.put((rank, hb.res_id, hb.ts_ms, hb.count, hb.flags, hb.entry_ref))
     dist.destroy_process_group()
 
@@ -370,3 +371,72 @@ def test_node_trace_two_ranks():
         assert ex.size > 0 and np.all(er[ex] >= 0) and np.all(er[ex] < ex)
         assert np.all(res[er[ex]] == res[ex]) and np.all((fl[er[ex]] & abi.EV_EXIT) == 0)
     assert got[0][0].size + got[1][0].size == 400_000
+
+
+def _placement_worker(rank, world, port, q):
+    """bench.py's N > 1 trace with the placement: this rank's shard (engine
+    ids) decided by an oracle engine holding its placed resources' rules."""
+    import torch.distributed as dist
+    import bench
+    from oracle import oracle as so
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    R = 5000
+    hb, pl = bench.node_trace(R, 200_000, world, rank, dist, placement_k=64)
+    grade, beh, count = trace.mixed_rule_table(R, seed=3)
+    mine = np.nonzero(pl.owner(np.arange(R)) == rank)[0]
+    o = so.OracleEngine(abi.default_config(max_resources=pl.local_rows(), max_batch=hb.n, shard_count=world,
+                                           shard_index=rank))
+    o.load_flow_rules(abi.flow_rules_np(pl.engine_id(mine).astype(np.uint32), grade[mine], count[mine], beh[mine]))
+    v = o.submit(hb)
+    inv = np.full(pl.R_pad + world * pl.extra, -1, np.int64)
+    inv[pl.eid] = np.arange(R)
+    q.put((rank, inv[hb.res_id], hb.ts_ms, hb.flags, v.status, v.wait_ms, pl.loads(np.bincount(
+        inv[hb.res_id], minlength=R)), int(pl.moved.size)))
+    dist.destroy_process_group()
+
+
+def test_node_trace_placement_two_ranks():
+    """The placement of bench.py's N > 1 mode (sentinel_amd/placement.py: the
+    top-K resources by the node's counts spread LPT-greedy, renamed to fresh
+    engine ids) keeps every verdict: the two ranks' oracle replays of their
+    shards equal one replay of the whole node trace (original ids), and the
+    ranks' event counts are balanced."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_placement_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((x[0], x[1:]) for x in (q.get(timeout=300), q.get(timeout=300)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from oracle import oracle as so
+    R = 5000
+    comps = [trace.mixed_zipf(R, 200_000, duration_ms=4000, seed=3 + c) for c in range(2)]
+    # the node trace on one host: components merged in time order (a millisecond in component order)
+    ts = np.concatenate([b.ts_ms for b in comps])
+    cid = np.concatenate([np.full(b.n, c) for c, b in enumerate(comps)])
+    o = np.lexsort((cid, ts))
+    pos = np.empty(o.size, np.int64)
+    pos[o] = np.arange(o.size)
+    off = np.array([0, comps[0].n])
+    er = np.concatenate([np.where(b.entry_ref >= 0, b.entry_ref + off[c], -1) for c, b in enumerate(comps)])[o]
+    er = np.where(er >= 0, pos[np.clip(er, 0, None)], -1)
+    node = abi.HostBatch(np.concatenate([b.res_id for b in comps])[o], ts[o],
+                         np.concatenate([b.count for b in comps])[o], np.concatenate([b.flags for b in comps])[o],
+                         entry_ref=er)
+    grade, beh, count = trace.mixed_rule_table(R, seed=3)
+    ref = so.OracleEngine(abi.default_config(max_resources=R, max_batch=node.n))
+    ref.load_flow_rules(abi.flow_rules_np(np.arange(R, dtype=np.uint32), grade, count, beh))
+    want = ref.submit(node)
+    for r in range(2):
+        res, ts_r, fl_r, st, wt, loads, k = got[r]
+        sel = np.nonzero(np.isin(node.res_id, np.unique(res)))[0]
+        # this rank's events are exactly the node's events of its resources, in node order
+        assert np.array_equal(node.res_id[sel], res) and np.array_equal(node.ts_ms[sel], ts_r)
+        assert np.array_equal(st, want.status[sel]) and np.array_equal(wt, want.wait_ms[sel])
+        assert k == 64
+    sizes = np.array([got[0][0].size, got[1][0].size])
+    assert sizes.sum() == node.n and sizes.max() / sizes.mean() < 1.02

@@ -159,3 +159,26 @@ def test_batcher_double_buffers_packed_batches():
     assert "SUBMIT_PACKED.invokeExact" not in src          # no synchronous packed path left
     readme = open(os.path.join(ROOT, "java", "README.md")).read()
     assert "sf_sync_packed" in readme and "latency" in readme.lower()
+
+
+def test_node_placement_twin():
+    """java NodePlacement and sentinel_amd/placement.py give moved resources
+    the same engine ids (R_pad + N * j + rank, LPT to the least-loaded rank,
+    ties to the lowest rank, stable top-K by count): the Java source carries
+    the same expressions, and the Python placement on a Zipf count vector
+    balances the ranks (checked statically: no JDK here)."""
+    import numpy as np
+    from sentinel_amd.placement import Placement
+    src = open(os.path.join(ROOT, "java/src/main/java/com/alibaba/csp/sentinel/gpu/NodePlacement.java")).read()
+    assert "e[res] = rPad + n * slot[best] + best;" in src
+    assert "if (load[q] < load[best]) best = q;" in src
+    assert "Long.compare(counts[b], counts[a])" in src
+    counts = (1e6 / np.arange(1, 20001) ** 1.1).astype(np.int64)
+    p = Placement.balanced(counts, 8, 16384)
+    loads = p.loads(counts)
+    head = counts[0] * 8 / counts.sum()              # the busiest resource alone, in mean-rank units
+    default = Placement(20000, 8).loads(counts)
+    assert loads.max() / loads.mean() < 1.05 * max(1.0, head) < default.max() / default.mean()
+    assert p.moved.size == 16384
+    assert np.all(p.owner(np.arange(20000)) == p.engine_id(np.arange(20000)) % 8)
+    assert np.unique(p.engine_id(np.arange(20000))).size == 20000

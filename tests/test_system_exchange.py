@@ -270,3 +270,30 @@ def test_gpu_exchange_thread_rule_falls_back():
     batches = w["batches"]
     parts = _threads(lambda r, c: _gpu_rank(w, batches, 2, r, c), 2)
     _check(w, batches, parts)
+
+
+@pytest.mark.gpu
+def test_gpu_exchange_rccl_single_rank():
+    """The exchange over the engine's RCCL communicator (device buffers,
+    ncclAllGather on the engine's stream) on a one-rank node: equal to one
+    engine deciding the batches with sf_submit, ENTRY_NODE included."""
+    from sentinel_amd import engine
+    w, batches = exchange_workload("mixed", 30_000)
+    c = w["cfg"]
+    e, ref = engine.FlowEngine(c), engine.FlowEngine(c)
+    try:
+        for x in (e, ref):
+            _load(x, w)
+        e.comm_init(1, 0, engine.comm_unique_id())
+        off = 0
+        for b in batches:
+            got = e.submit_node(b, np.arange(off, off + b.n, dtype=np.int64), None)
+            want = ref.submit(b)
+            off += b.n
+            assert np.array_equal(got.status, want.status) and np.array_equal(got.wait_ms, want.wait_ms)
+            assert np.array_equal(got.rule_idx, want.rule_idx)
+            assert (want.status == abi.V_BLOCK_SYSTEM).sum() > 0
+        assert abi.node_state_to_dict(e.read_entry_node()) == abi.node_state_to_dict(ref.read_entry_node())
+    finally:
+        e.close()
+        ref.close()
