@@ -454,6 +454,25 @@ int  sf_submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out)
 /* Enqueued only; sf_sync waits and reports the first error.  Host arrays
  * (batch and verdicts) must stay untouched until sf_sync.                   */
 int  sf_submit_packed_async(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out);
+/* Sparse host verdicts of a packed batch: the copy back is 1 byte per event
+ * plus the exceptions.  status [n] as in sf_verdicts; the events whose
+ * wait_ms is not 0 (queued passes) as (index << 32 | (uint32_t)wait_ms) in
+ * waits, the events whose rule_idx is not 0 (blocks by a resource's later
+ * rule) as (index << 32 | rule_idx) in rules, each list in any order, its
+ * length in counts[0] / counts[1].  waits and rules hold n entries; the first
+ * `prefetch` of each list come back with the status bytes, the rest (if any)
+ * at sf_sync_packed_sparse.  Every wait / rule not listed is 0. */
+typedef struct sf_sparse_verdicts {
+    uint8_t*  status;             /* [n]                                       */
+    uint64_t* waits;              /* [n]                                       */
+    uint64_t* rules;              /* [n]                                       */
+    uint32_t* counts;             /* [2]                                       */
+    uint32_t  prefetch;
+    uint32_t  pad;
+} sf_sparse_verdicts;
+int  sf_submit_packed_sparse_async(sf_engine* e, const sf_packed_batch* in, sf_sparse_verdicts* out);
+/* Waits for that batch (like sf_sync_packed) and completes its lists. */
+int  sf_sync_packed_sparse(sf_engine* e, const sf_sparse_verdicts* out);
 /* Waits for ONE sf_submit_packed_async batch with host verdicts -- the one
  * whose verdicts go to out->status -- and returns that batch's error; the
  * batch enqueued after it keeps running.  With two host verdict buffers used

@@ -145,6 +145,12 @@ struct sf_engine {
         bool d2h_pending = false, consumed_pending = false;
         const uint8_t* out_status = nullptr;   // host verdicts of the async batch in flight (sf_sync_packed)
         int32_t* err_host = nullptr;           // its error flag, copied back with its verdicts (pinned)
+        // sf_sparse_verdicts of that batch: the caller's struct, the list lengths
+        // (pinned, copied back with the status bytes), the device lists
+        bool sparse = false;
+        sf_sparse_verdicts sp{};
+        uint32_t* sp_counts = nullptr;
+        const unsigned long long* sp_wl = nullptr; const unsigned long long* sp_rl = nullptr;
     } pk[2];
     hipStream_t h2d = nullptr, d2h = nullptr;
     int32_t* rh_err = nullptr;            // rehash_table's overflow flag
@@ -235,6 +241,7 @@ void sf_destroy(sf_engine* e) {
         if (p.d2h) hipEventDestroy(p.d2h);
         if (p.consumed) hipEventDestroy(p.consumed);
         if (p.err_host) hipHostFree(p.err_host);
+        if (p.sp_counts) hipHostFree(p.sp_counts);
     }
     if (e->h2d) { hipStreamSynchronize(e->h2d); hipStreamDestroy(e->h2d); }
     if (e->d2h) { hipStreamSynchronize(e->d2h); hipStreamDestroy(e->d2h); }
@@ -470,22 +477,33 @@ static void acc_timing(sf_engine* e, int slot) {
     e->stats.total_ms += a + b2 + c + d;
 }
 
+static int sparse_complete(sf_engine::PkStage& pk);
 // Drain asynchronously submitted batches: wait for both streams, then report
-// the first error flag raised by any of them.
-static int drain(sf_engine* e) {
+// the first error flag raised by any of them.  An async packed batch whose
+// verdicts the caller has not collected keeps its error for its own
+// sf_sync_packed, unless `all` (sf_sync: every batch collected here).
+static int drain(sf_engine* e, bool all = false) {
     if (!e->pending) return SF_OK;
     HIP_TRY(hipStreamSynchronize(e->sstream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     if (e->d2h) HIP_TRY(hipStreamSynchronize(e->d2h));
     for (auto& p : e->pk) p.d2h_pending = false;
     int first = 0;
+    unsigned keep = 0;
     for (int k = 0; k < 2; k++) {
         if (!(e->pending & (1u << k))) continue;
+        // an async packed batch whose verdicts the caller has not collected: its
+        // error came back with them and is reported by its own sf_sync_packed
+        if (e->pk[k].out_status && !all) { keep |= 1u << k; continue; }
+        if (e->pk[k].out_status) {
+            e->pk[k].out_status = nullptr;
+            if (e->pk[k].sparse) { const int rc = sparse_complete(e->pk[k]); if (rc) return rc; }
+        }
         int32_t err = 0;
         HIP_TRY(hipMemcpy(&err, e->w[k].err, 4, hipMemcpyDeviceToHost));
         if (err && !first) first = err;
     }
-    e->pending = 0;
+    e->pending = keep;
     for (int k = 0; k < 2; k++) acc_timing(e, k);
     {
         uint32_t nseg = 0;
@@ -1235,15 +1253,27 @@ int sf_submit_async(sf_engine* e, const sf_event_batch* in, sf_verdicts* out) {
 // the Work set's device stage on the H2D stream, are expanded to the SoA batch
 // on the sort stream, decided by submit_core (asynchronously when asked), and
 // the verdicts come back on the D2H stream once the batch is decided.
-static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out, bool async) {
+// the rest of a sparse batch's lists (beyond the prefetch) and their lengths, once its copies are done
+static int sparse_complete(sf_engine::PkStage& pk) {
+    const uint32_t nw = pk.sp_counts[0], nr = pk.sp_counts[1], pre = pk.sp.prefetch;
+    if (nw > pre) HIP_TRY(hipMemcpy(pk.sp.waits + pre, pk.sp_wl + pre, (size_t)(nw - pre) * 8, hipMemcpyDeviceToHost));
+    if (nr > pre) HIP_TRY(hipMemcpy(pk.sp.rules + pre, pk.sp_rl + pre, (size_t)(nr - pre) * 8, hipMemcpyDeviceToHost));
+    pk.sp.counts[0] = nw; pk.sp.counts[1] = nr;
+    pk.sparse = false;
+    return SF_OK;
+}
+
+static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out, bool async,
+                         const sf_sparse_verdicts* sp = nullptr) {
     if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
+    if (sp && (!sp->waits || !sp->rules || !sp->counts)) return fail(SF_ERR_INVALID, "null sparse list");
     if (in->n == 0) return SF_OK;
     if (!in->ev || (in->n_exit && !in->exit_ref) || (in->n_count_ext && !in->count_ext))
         return fail(SF_ERR_INVALID, "missing packed arrays");
     if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
     std::lock_guard<std::mutex> lk(e->mu);
     const uint32_t n = in->n;
-    const bool host_in = in->mem == SF_MEM_HOST, host_out = out->mem == SF_MEM_HOST;
+    const bool host_in = in->mem == SF_MEM_HOST, host_out = sp || out->mem == SF_MEM_HOST;
     if (!e->h2d) {
         HIP_TRY(hipStreamCreateWithFlags(&e->h2d, hipStreamNonBlocking));
         HIP_TRY(hipStreamCreateWithFlags(&e->d2h, hipStreamNonBlocking));
@@ -1253,6 +1283,7 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
             HIP_TRY(hipEventCreateWithFlags(&p.consumed, hipEventDisableTiming));
             HIP_TRY(hipHostMalloc((void**)&p.err_host, 4, hipHostMallocDefault));
             *p.err_host = 0;
+            HIP_TRY(hipHostMalloc((void**)&p.sp_counts, 8, hipHostMallocDefault));
         }
     }
     // (submit_core decides asynchronously only without SystemRules; the slot it takes is e->cur)
@@ -1274,6 +1305,7 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     const size_t o_res = take(N * 4), o_ts = take(N * 8), o_cnt = take(N * 4), o_fl = take(N), o_er = take(N * 8);
     const size_t o_ct = take(N * 8), o_tc = take((N / 4096 + 2) * 8);
     const size_t o_st = take(N), o_wt = take(N * 4), o_ru = take(N * 2);
+    const size_t o_wl = sp ? take(N * 8) : 0, o_rl = sp ? take(N * 8) : 0, o_sc = sp ? take(16) : 0;
     if (pk.bytes < off) {
         if (e->used[slot]) HIP_TRY(hipEventSynchronize(e->ev_done[slot]));
         if (pk.consumed_pending) { HIP_TRY(hipEventSynchronize(pk.consumed)); pk.consumed_pending = false; }
@@ -1334,8 +1366,8 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     sf_verdicts dv{};
     dv.mem = SF_MEM_DEVICE;
     dv.status = host_out ? (uint8_t*)(B + o_st) : out->status;
-    dv.wait_ms = out->wait_ms ? (host_out ? (int32_t*)(B + o_wt) : out->wait_ms) : nullptr;
-    dv.rule_idx = out->rule_idx ? (host_out ? (uint16_t*)(B + o_ru) : out->rule_idx) : nullptr;
+    dv.wait_ms = (sp || out->wait_ms) ? (host_out ? (int32_t*)(B + o_wt) : out->wait_ms) : nullptr;
+    dv.rule_idx = (sp || out->rule_idx) ? (host_out ? (uint16_t*)(B + o_ru) : out->rule_idx) : nullptr;
     const int rc = submit_core(e, &eb, &dv, core_async, nullptr, &expand);
     if (rc) return rc;
     pk.consumed_pending = true;
@@ -1343,13 +1375,34 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
         hipStream_t d = e->serial ? e->stream : e->d2h;
         HIP_TRY(hipStreamWaitEvent(d, e->ev_core[slot], 0));
         HIP_TRY(hipMemcpyAsync(out->status, dv.status, n, hipMemcpyDeviceToHost, d));
-        if (out->wait_ms) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait_ms, (size_t)n * 4, hipMemcpyDeviceToHost, d));
-        if (out->rule_idx) HIP_TRY(hipMemcpyAsync(out->rule_idx, dv.rule_idx, (size_t)n * 2, hipMemcpyDeviceToHost, d));
+        pk.sparse = sp != nullptr;
+        if (sp) {
+            // 1 byte per event plus the exceptions: the nonzero waits / rule indices
+            // compacted on the device, their first `prefetch` back with the statuses
+            unsigned long long* wl = (unsigned long long*)(B + o_wl);
+            unsigned long long* rl = (unsigned long long*)(B + o_rl);
+            uint32_t* sc = (uint32_t*)(B + o_sc);
+            HIP_TRY(launch_sparse_verdicts(dv.wait_ms, dv.rule_idx, n, wl, rl, sc, d));
+            HIP_TRY(hipMemcpyAsync(pk.sp_counts, sc, 8, hipMemcpyDeviceToHost, d));
+            const size_t pre = std::min<size_t>(sp->prefetch, n) * 8;
+            if (pre) {
+                HIP_TRY(hipMemcpyAsync(sp->waits, wl, pre, hipMemcpyDeviceToHost, d));
+                HIP_TRY(hipMemcpyAsync(sp->rules, rl, pre, hipMemcpyDeviceToHost, d));
+            }
+            pk.sp = *sp; pk.sp_wl = wl; pk.sp_rl = rl;
+        } else {
+            if (out->wait_ms) HIP_TRY(hipMemcpyAsync(out->wait_ms, dv.wait_ms, (size_t)n * 4, hipMemcpyDeviceToHost, d));
+            if (out->rule_idx) HIP_TRY(hipMemcpyAsync(out->rule_idx, dv.rule_idx, (size_t)n * 2, hipMemcpyDeviceToHost, d));
+        }
         if (core_async) HIP_TRY(hipMemcpyAsync(pk.err_host, e->w[slot].err, 4, hipMemcpyDeviceToHost, d));
         HIP_TRY(hipEventRecord(pk.d2h, d));
         pk.d2h_pending = true;
         pk.out_status = core_async ? out->status : nullptr;
-        if (!core_async) { HIP_TRY(hipEventSynchronize(pk.d2h)); pk.d2h_pending = false; }
+        if (!core_async) {
+            HIP_TRY(hipEventSynchronize(pk.d2h));
+            pk.d2h_pending = false;
+            if (sp) { const int rc = sparse_complete(pk); if (rc) return rc; }
+        }
     }
     return SF_OK;
 }
@@ -1366,22 +1419,41 @@ int sf_submit_packed_async(sf_engine* e, const sf_packed_batch* in, sf_verdicts*
 // batch submitted after it stays in flight.  Its error flag came back with the
 // verdicts.  A batch already collected (by sf_sync, a rule reload's drain, or
 // an earlier call) has nothing left to wait for: SF_OK.
-int sf_sync_packed(sf_engine* e, const sf_verdicts* out) {
-    if (!e || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
-    std::lock_guard<std::mutex> lk(e->mu);
+static int sync_packed(sf_engine* e, const uint8_t* status) {
     for (int k = 0; k < 2; k++) {
         auto& pk = e->pk[k];
-        if (!pk.d2h_pending || pk.out_status != out->status) continue;
-        HIP_TRY(hipEventSynchronize(pk.d2h));
+        if (!status || pk.out_status != status) continue;
+        // (a drain may have waited for its copies already; its error stays this batch's)
+        if (pk.d2h_pending) HIP_TRY(hipEventSynchronize(pk.d2h));
         pk.d2h_pending = false;
         pk.out_status = nullptr;
         e->pending &= ~(1u << k);          // checked here, not again by sf_sync
+        if (pk.sparse) { const int rc = sparse_complete(pk); if (rc) return rc; }
         const int32_t err = *pk.err_host;
         if (err) return fail(err, err == SF_ERR_CAPACITY ? "capacity exceeded (param table, or the origin / context node pool: aux_capacity)"
                                                          : "invalid batch (resource outside shard or bad entry_ref)");
         return SF_OK;
     }
     return SF_OK;
+}
+
+int sf_sync_packed(sf_engine* e, const sf_verdicts* out) {
+    if (!e || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return sync_packed(e, out->status);
+}
+
+int sf_submit_packed_sparse_async(sf_engine* e, const sf_packed_batch* in, sf_sparse_verdicts* out) {
+    if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
+    sf_verdicts v{};
+    v.mem = SF_MEM_HOST; v.status = out->status;
+    return submit_packed(e, in, &v, true, out);
+}
+
+int sf_sync_packed_sparse(sf_engine* e, const sf_sparse_verdicts* out) {
+    if (!e || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return sync_packed(e, out->status);
 }
 
 // ---------------------------------------------------------------- node-wide SystemRule rounds
@@ -2533,7 +2605,7 @@ int sf_sync(sf_engine* e) {
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipStreamSynchronize(e->sstream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    return drain(e);
+    return drain(e, true);
 }
 int sf_get_stats(sf_engine* e, sf_stats* out) {
     if (!e || !out) return fail(SF_ERR_INVALID, "null argument");

@@ -230,7 +230,7 @@ struct Work {
     uint32_t lcap[LCLS];                                //   front, lean QPS (SM_LIGHTQ) from the back                                // light_list region of each length class   // [0] n_light [1] n_heavy front [2] hw slots [3] sec slots [4] n_heavy back
                                                                       // [5] n_stream front [6] n_stream back
     int64_t* pcg; void* pscan_tmp; size_t pscan_tmp_bytes;
-    void* segs_lb;                                      // k_segs_lb's tile states (segs_lb_bytes)
+    void* segs_lb;                                      // k_segs_red / k_segs_out tile totals (segs_lb_bytes)
     uint2* fill_tiles; uint32_t fill_tile_cap;         // [2][cap] (segment, tile) of each class for k_heavy_fill
     uint32_t* fill_ntiles;                              // [2] tiles per class
     uint32_t fill_grid;                                 // persistent k_heavy_fill workgroups (8 per CU)
@@ -371,6 +371,9 @@ hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64
                             int64_t base, uint32_t n, uint32_t n_exit, uint32_t n_cext, uint2* tile_cnt,
                             uint32_t* res, int64_t* ts, int32_t* cnt, uint8_t* flags, int64_t* eref, int64_t* cts,
                             int32_t* err, hipStream_t s);
+// sf_sparse_verdicts: the nonzero waits / rule indices of n verdicts as (index << 32 | value) lists
+hipError_t launch_sparse_verdicts(const int32_t* wait, const uint16_t* rule, uint32_t n, unsigned long long* wl,
+                                  unsigned long long* rl, uint32_t* counts, hipStream_t s);
 // origin nodes (sf_origin.hip)
 hipError_t launch_ox_index(const DevState& st, Work& w, const DevBatch& b, uint32_t lim, hipStream_t s);
 hipError_t launch_ox_apply(const DevState& st, Work& w, const DevBatch& b, uint32_t n_heavy, uint32_t n_pairs,

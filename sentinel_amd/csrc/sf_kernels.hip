@@ -193,90 +193,71 @@ __global__ void k_segs(DevBatch b, const int32_t* s_cnt, const uint8_t* s_flags,
     if (((heads >> lane) & 1ull) && acc) atomicOr(&segflag[sid], acc);
 }
 
-// ============================================================ segment table + prefixes in one pass
-// One single-pass scan over the sorted keys (decoupled look-back, tiles taken
-// in order through an atomic counter so every tile's predecessors are running
-// or done): per position the inclusive count of segment heads (head_scan,
-// the segment id + 1) and, when the decide phase's window budgets need it,
-// the inclusive prefix of the entries' acquireCounts (pcg: 0 for exits and
-// EVF_SYSBLK entries, k_heavy_decide's greedy prefix), and the segment table
-// (start, resource, flags) -- what the rocprim head scan, k_segs and the
-// rocprim acquireCount scan wrote in three passes.
+// ============================================================ segment table + prefixes (reduce, scan, rescan)
+// The segment heads of the sorted keys and their inclusive count per
+// position (head_scan = segment id + 1), the segment table (start, resource,
+// flags) and, when the decide phase's window budgets need it, the inclusive
+// prefix of the entries' acquireCounts (pcg: 0 for exits and EVF_SYSBLK
+// entries; k_heavy_decide's greedy prefix) -- what the rocprim head scan,
+// k_segs and the rocprim acquireCount scan wrote in three passes.  Three
+// launches without any cross-workgroup waiting: per-tile totals, one
+// workgroup scanning the tile totals, then every tile again from its prefix.
+// (A decoupled look-back single pass measured 5 ms per batch on gfx950: its
+// agent-scope release / acquire publishes write back and bypass the per-XCD
+// L2 on every tile.)
 constexpr int SL_T = 256, SL_K = 16, SL_TILE = SL_T * SL_K;       // 4096 positions per tile
-constexpr unsigned long long SL_AGG = 1ull << 32, SL_INC = 2ull << 32;
-size_t segs_lb_bytes(uint32_t max_n) { return ((size_t)max_n / SL_TILE + 2) * 24 + 64; }   // (sf_internal.h)
+size_t segs_lb_bytes(uint32_t max_n) { return ((size_t)max_n / SL_TILE + 2) * 16 + 64; }   // (sf_internal.h)
 
-struct SegsLB {
-    unsigned long long* status;   // [tiles] flag << 32 | heads (aggregate, then inclusive)
-    long long* acq_agg;           // [tiles]
-    long long* acq_inc;           // [tiles]
-    unsigned int* ticket;
-};
-
-__device__ __forceinline__ unsigned long long sl_load(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void sl_store(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <bool PCG>
-__global__ void __launch_bounds__(SL_T) k_segs_lb(DevBatch b, const int32_t* s_cnt, const uint8_t* s_flags,
-                                                  const uint8_t* s_atag, const uint32_t* keys, uint32_t* head_scan,
-                                                  int64_t* pcg, uint32_t* seg_start, uint32_t* seg_res,
-                                                  uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts,
-                                                  const int32_t* err, bool exit_marks, int32_t* prio_seen, SegsLB lb) {
-    __shared__ uint32_t s_tile;
-    __shared__ uint32_t w_heads[SL_T / 64];
-    __shared__ long long w_acq[SL_T / 64];
-    __shared__ uint32_t p_heads;
-    __shared__ long long p_acq;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(lb.ticket, 1u);
-    __syncthreads();
-    const uint32_t t = s_tile, n = b.n;
-    const uint32_t p0 = t * SL_TILE + (uint32_t)tid * SL_K;
-    // this thread's 16 keys and the one before them
+struct SegTile {                 // one thread's 16 positions
     uint32_t k[SL_K];
-    uint32_t hmask = 0;
     int32_t c[SL_K];
     uint8_t f[SL_K];
+    uint32_t hmask, heads;
+    long long acq;
+};
+template <bool PCG>
+__device__ __forceinline__ void seg_load(SegTile& t, const uint32_t* keys, const uint8_t* s_flags, const int32_t* s_cnt,
+                                         uint32_t p0, uint32_t n) {
     if (p0 + SL_K <= n) {
         const uint4* kp = (const uint4*)(keys + p0);
 #pragma unroll
-        for (int q = 0; q < SL_K / 4; q++) { const uint4 v = kp[q]; k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w; }
+        for (int q = 0; q < SL_K / 4; q++) { const uint4 v = kp[q]; t.k[4 * q] = v.x; t.k[4 * q + 1] = v.y; t.k[4 * q + 2] = v.z; t.k[4 * q + 3] = v.w; }
         const uint4 fv = *(const uint4*)(s_flags + p0);
         const uint32_t fw[4] = {fv.x, fv.y, fv.z, fv.w};
 #pragma unroll
-        for (int q = 0; q < SL_K; q++) f[q] = (uint8_t)(fw[q >> 2] >> (8 * (q & 3)));
+        for (int q = 0; q < SL_K; q++) t.f[q] = (uint8_t)(fw[q >> 2] >> (8 * (q & 3)));
         if (PCG) {
             const int4* cp = (const int4*)(s_cnt + p0);
 #pragma unroll
-            for (int q = 0; q < SL_K / 4; q++) { const int4 v = cp[q]; c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w; }
+            for (int q = 0; q < SL_K / 4; q++) { const int4 v = cp[q]; t.c[4 * q] = v.x; t.c[4 * q + 1] = v.y; t.c[4 * q + 2] = v.z; t.c[4 * q + 3] = v.w; }
         }
     } else {
 #pragma unroll
         for (int q = 0; q < SL_K; q++) {
             const bool in = p0 + q < n;
-            k[q] = in ? keys[p0 + q] : 0u;
-            f[q] = in ? s_flags[p0 + q] : (uint8_t)SF_EV_EXIT;
-            c[q] = (PCG && in) ? s_cnt[p0 + q] : 0;
+            t.k[q] = in ? keys[p0 + q] : 0u;
+            t.f[q] = in ? s_flags[p0 + q] : (uint8_t)SF_EV_EXIT;
+            t.c[q] = (PCG && in) ? s_cnt[p0 + q] : 0;
         }
     }
     const uint32_t kprev = (p0 > 0 && p0 < n) ? keys[p0 - 1] : ~0u;
-    uint32_t heads = 0;
-    long long acq = 0;
+    t.hmask = 0; t.heads = 0; t.acq = 0;
 #pragma unroll
     for (int q = 0; q < SL_K; q++) {
         const bool in = p0 + q < n;
-        const bool h = in && (p0 + q == 0 || k[q] != (q ? k[q - 1] : kprev));
-        hmask |= (h ? 1u : 0u) << q;
-        heads += h;
-        if (PCG) acq += (in && !(f[q] & (SF_EV_EXIT | EVF_SYSBLK))) ? (long long)c[q] : 0;
+        const bool h = in && (p0 + q == 0 || t.k[q] != (q ? t.k[q - 1] : kprev));
+        t.hmask |= (h ? 1u : 0u) << q;
+        t.heads += h;
+        if (PCG) t.acq += (in && !(t.f[q] & (SF_EV_EXIT | EVF_SYSBLK))) ? (long long)t.c[q] : 0;
     }
-    // block exclusive scan of (heads, acq) over the threads
-    uint32_t hx = heads;
-    long long ax = acq;
+}
+// block-wide exclusive scan of (heads, acq) over the threads; totals out
+__device__ __forceinline__ void seg_block_scan(uint32_t& hx, long long& ax, uint32_t* htot, long long* atot) {
+    __shared__ uint32_t w_heads[SL_T / 64];
+    __shared__ long long w_acq[SL_T / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t h0 = hx;
+    const long long a0 = ax;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t h2 = __shfl_up(hx, d);
@@ -285,87 +266,96 @@ __global__ void __launch_bounds__(SL_T) k_segs_lb(DevBatch b, const int32_t* s_c
     }
     if (lane == 63) { w_heads[wv] = hx; w_acq[wv] = ax; }
     __syncthreads();
-    uint32_t hbase = 0, htot = 0;
-    long long abase = 0, atot = 0;
+    uint32_t hb = 0, ht = 0;
+    long long ab = 0, at = 0;
 #pragma unroll
     for (int w = 0; w < SL_T / 64; w++) {
-        if (w < wv) { hbase += w_heads[w]; abase += w_acq[w]; }
-        htot += w_heads[w]; atot += w_acq[w];
+        if (w < wv) { hb += w_heads[w]; ab += w_acq[w]; }
+        ht += w_heads[w]; at += w_acq[w];
     }
-    hx = hx - heads + hbase;               // exclusive within the tile
-    ax = ax - acq + abase;
-    // publish the aggregate, look back for the exclusive prefix, publish the inclusive value
-    if (wv == 0) {
-        uint32_t ph = 0;
-        long long pa = 0;
-        if (t == 0) {
-            if (lane == 0) {
-                __hip_atomic_store(&lb.acq_inc[0], atot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                sl_store(&lb.status[0], SL_INC | htot);
-            }
-        } else {
-            if (lane == 0) {
-                __hip_atomic_store(&lb.acq_agg[t], atot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                sl_store(&lb.status[t], SL_AGG | htot);
-            }
-            int64_t base = (int64_t)t - 1;
-            for (;;) {
-                const int64_t idx = base - lane;
-                const unsigned long long w = idx >= 0 ? sl_load(&lb.status[idx]) : SL_INC;
-                const unsigned long long flag = w >> 32;
-                const unsigned long long pm = __ballot(flag == 2);
-                const int firstp = pm ? __ffsll((long long)pm) - 1 : 64;
-                const unsigned long long upto = firstp == 64 ? ~0ull : ((2ull << firstp) - 1ull);
-                if (__ballot(flag == 0) & upto) continue;            // a predecessor not published yet
-                uint32_t vh = 0;
-                long long va = 0;
-                if (lane <= firstp && idx >= 0) {
-                    vh = (uint32_t)w;
-                    va = flag == 2 ? __hip_atomic_load(&lb.acq_inc[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : __hip_atomic_load(&lb.acq_agg[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-#pragma unroll
-                for (int d = 32; d > 0; d >>= 1) { vh += __shfl_xor(vh, d); va += __shfl_xor(va, d); }
-                ph += vh; pa += va;
-                if (firstp < 64) break;
-                base -= 64;
-            }
-            if (lane == 0) {
-                __hip_atomic_store(&lb.acq_inc[t], pa + atot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                sl_store(&lb.status[t], SL_INC | (ph + htot));
-            }
-        }
-        if (lane == 0) { p_heads = ph; p_acq = pa; }
-    }
+    hx = hx - h0 + hb;
+    ax = ax - a0 + ab;
+    *htot = ht; *atot = at;
+}
+
+template <bool PCG>
+__global__ void __launch_bounds__(SL_T) k_segs_red(const uint32_t* keys, const uint8_t* s_flags, const int32_t* s_cnt,
+                                                   uint32_t n, uint32_t* t_heads, long long* t_acq) {
+    SegTile t;
+    seg_load<PCG>(t, keys, s_flags, s_cnt, blockIdx.x * SL_TILE + threadIdx.x * SL_K, n);
+    uint32_t hx = t.heads, ht;
+    long long ax = t.acq, at;
+    seg_block_scan(hx, ax, &ht, &at);
+    if (threadIdx.x == 0) { t_heads[blockIdx.x] = ht; t_acq[blockIdx.x] = at; }
+}
+// one workgroup: exclusive prefix of the tile totals, in place
+__global__ void __launch_bounds__(1024) k_segs_tscan(uint32_t* t_heads, long long* t_acq, uint32_t tiles) {
+    __shared__ uint32_t sh[1024];
+    __shared__ long long sa[1024];
+    const uint32_t per = (tiles + 1023) / 1024, i0 = threadIdx.x * per, i1 = min(i0 + per, tiles);
+    uint32_t h = 0;
+    long long a = 0;
+    for (uint32_t i = i0; i < i1; i++) { h += t_heads[i]; a += t_acq[i]; }
+    sh[threadIdx.x] = h; sa[threadIdx.x] = a;
     __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const uint32_t h2 = threadIdx.x >= (unsigned)d ? sh[threadIdx.x - d] : 0u;
+        const long long a2 = threadIdx.x >= (unsigned)d ? sa[threadIdx.x - d] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += h2; sa[threadIdx.x] += a2;
+        __syncthreads();
+    }
+    h = sh[threadIdx.x] - h; a = sa[threadIdx.x] - a;        // exclusive prefix of this thread's run
+    for (uint32_t i = i0; i < i1; i++) {
+        const uint32_t th = t_heads[i];
+        const long long ta = t_acq[i];
+        t_heads[i] = h; t_acq[i] = a;
+        h += th; a += ta;
+    }
+}
+
+template <bool PCG>
+__global__ void __launch_bounds__(SL_T) k_segs_out(DevBatch b, const int32_t* s_cnt, const uint8_t* s_flags,
+                                                   const uint8_t* s_atag, const uint32_t* keys, uint32_t* head_scan,
+                                                   int64_t* pcg, uint32_t* seg_start, uint32_t* seg_res,
+                                                   uint32_t* n_seg, uint32_t* segflag, int64_t* last_ts,
+                                                   const int32_t* err, bool exit_marks, int32_t* prio_seen,
+                                                   const uint32_t* t_heads, const long long* t_acq) {
+    const uint32_t n = b.n, p0 = blockIdx.x * SL_TILE + threadIdx.x * SL_K;
+    SegTile t;
+    seg_load<PCG>(t, keys, s_flags, s_cnt, p0, n);
+    uint32_t hx = t.heads, ht;
+    long long ax = t.acq, at;
+    seg_block_scan(hx, ax, &ht, &at);
     if (p0 >= n) return;
-    uint32_t hs = p_heads + hx;            // heads before this thread's first position
-    long long run = p_acq + ax;
+    uint32_t hs = t_heads[blockIdx.x] + hx;   // heads before this thread's first position
+    long long run = PCG ? t_acq[blockIdx.x] + ax : 0;
     uint32_t hsv[SL_K];
     long long pv[SL_K];
     uint32_t acc = 0, prio = 0;
     int64_t cur = hs ? (int64_t)hs - 1 : -1;   // the segment of the position before this thread's first
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int q = 0; q < SL_K; q++) {
         const uint32_t p = p0 + q;
         const bool in = p < n;
-        if ((hmask >> q) & 1u) {
+        if ((t.hmask >> q) & 1u) {
             if (acc && cur >= 0) atomicOr(&segflag[cur], acc);
             acc = 0;
             hs++;
             cur = (int64_t)hs - 1;
             seg_start[hs - 1] = p;
-            seg_res[hs - 1] = k[q];
+            seg_res[hs - 1] = t.k[q];
         }
         hsv[q] = hs;
-        if (PCG) { run += (in && !(f[q] & (SF_EV_EXIT | EVF_SYSBLK))) ? (long long)c[q] : 0; pv[q] = run; }
+        if (PCG) { run += (in && !(t.f[q] & (SF_EV_EXIT | EVF_SYSBLK))) ? (long long)t.c[q] : 0; pv[q] = run; }
         if (!in) continue;
         uint32_t mine = 0;
-        if (exit_marks && (f[q] & SF_EV_EXIT)) mine |= SEGF_EXIT;
-        if (!(f[q] & SF_EV_EXIT)) {
-            const int32_t cq = PCG ? c[q] : s_cnt[p];
-            mine |= ((f[q] & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (cq <= 0 ? SEGF_NONPOS : 0u) |
-                    ((f[q] & EVF_SYSBLK) ? SEGF_SYS : 0u);
+        if (exit_marks && (t.f[q] & SF_EV_EXIT)) mine |= SEGF_EXIT;
+        if (!(t.f[q] & SF_EV_EXIT)) {
+            const int32_t cq = PCG ? t.c[q] : s_cnt[p];
+            mine |= ((t.f[q] & SF_EV_PRIO) ? SEGF_PRIO : 0u) | (cq <= 0 ? SEGF_NONPOS : 0u) |
+                    ((t.f[q] & EVF_SYSBLK) ? SEGF_SYS : 0u);
         }
         for (uint32_t a = 0; a < b.arg_slots; a++)
             if (s_atag[(size_t)a * n + p] == SF_TAG_COLLECTION) mine |= SEGF_COLL;
@@ -392,6 +382,18 @@ __global__ void __launch_bounds__(SL_T) k_segs_lb(DevBatch b, const int32_t* s_c
             if (PCG) pcg[p0 + q] = pv[q];
         }
     }
+}
+
+template <bool PCG>
+static void launch_segs3(const DevState& st, Work& w, const DevBatch& b, hipStream_t s) {
+    const uint32_t n = b.n, tiles = (n + SL_TILE - 1) / SL_TILE;
+    uint32_t* th = (uint32_t*)w.segs_lb;
+    long long* ta = (long long*)((char*)w.segs_lb + (((size_t)tiles * 4 + 15) & ~(size_t)15));
+    hipLaunchKernelGGL(k_segs_red<PCG>, dim3(tiles), dim3(SL_T), 0, s, w.keys_out, w.s_flags, w.s_cnt, n, th, ta);
+    hipLaunchKernelGGL(k_segs_tscan, dim3(1), dim3(1024), 0, s, th, ta, tiles);
+    hipLaunchKernelGGL(k_segs_out<PCG>, dim3(tiles), dim3(SL_T), 0, s, b, w.s_cnt, w.s_flags, w.s_atag, w.keys_out,
+                       w.head_scan, w.pcg, w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err,
+                       st.n_prule != 0, st.prio_seen, th, ta);
 }
 
 struct HeadFlag {       // 1 where a new resource segment starts in the sorted keys
@@ -2202,7 +2204,7 @@ static bool sort_uses_rocprim() {
     static const bool v = [] { const char* x = getenv("SF_SORT_ROCPRIM"); return x && x[0] == '1'; }();
     return v;
 }
-// k_segs_lb (one pass) or, SF_SEGS_LB=0, the rocprim head scan + k_segs + the rocprim acquireCount scan (A/B)
+// k_segs_red / _tscan / _out or, SF_SEGS_LB=0, the rocprim head scan + k_segs + the rocprim acquireCount scan (A/B)
 static bool segs_one_pass() {
     static const bool v = [] { const char* x = getenv("SF_SEGS_LB"); return !(x && x[0] == '0'); }();
     return v && !sort_uses_rocprim();
@@ -2256,21 +2258,9 @@ hipError_t launch_sort(const DevState& st, Work& w, const DevBatch& b, uint32_t 
                            w.head_scan, w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts, st.err,
                            st.n_prule != 0, st.prio_seen);
     } else if (!use_rocprim) {
-        // segment table, head scan and (window rules loaded) the acquireCount prefix in one pass
-        const uint32_t tiles = (n + SL_TILE - 1) / SL_TILE;
-        char* lbp = (char*)w.segs_lb;
-        const SegsLB lb{(unsigned long long*)lbp, (long long*)(lbp + ((size_t)tiles + 1) * 8),
-                        (long long*)(lbp + ((size_t)tiles + 1) * 16), (unsigned int*)(lbp + ((size_t)tiles + 1) * 24)};
-        hipMemsetAsync(lbp, 0, ((size_t)tiles + 1) * 8, s);
-        hipMemsetAsync(lb.ticket, 0, 4, s);
-        if (st.n_window_rules)
-            hipLaunchKernelGGL(k_segs_lb<true>, dim3(tiles), dim3(SL_T), 0, s, b, w.s_cnt, w.s_flags, w.s_atag,
-                               w.keys_out, w.head_scan, w.pcg, w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts,
-                               st.err, st.n_prule != 0, st.prio_seen, lb);
-        else
-            hipLaunchKernelGGL(k_segs_lb<false>, dim3(tiles), dim3(SL_T), 0, s, b, w.s_cnt, w.s_flags, w.s_atag,
-                               w.keys_out, w.head_scan, w.pcg, w.seg_start, w.seg_res, w.n_seg, w.segflag, st.last_ts,
-                               st.err, st.n_prule != 0, st.prio_seen, lb);
+        // segment table, head scan and (window rules loaded) the acquireCount prefix: reduce, scan, rescan
+        if (st.n_window_rules) launch_segs3<true>(st, w, b, s);
+        else launch_segs3<false>(st, w, b, s);
     } else if (org)
         hipLaunchKernelGGL(k_unpack<true>, dim3(blocks(n, T)), dim3(T), 0, s, b, (const void*)w.pv_out, w.keys_out,
                            w.perm, w.s_ts, w.s_cnt, w.s_flags, w.s_nargs, w.s_atag, w.s_abits, w.head_scan,
@@ -2557,7 +2547,7 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
     }
     if (st.n_window_rules && !segs_one_pass()) {
         // acquireCount prefix of the entries (QPS / WarmUp window budgets, k_heavy_decide
-        // only; the hand-written sort path writes it in k_segs_lb): state-independent, but
+        // only; the hand-written sort path writes it in k_segs_out): state-independent, but
         // here on stream B rather than in the sort phase, the longer of the two pipelined phases
         PcIter it(rocprim::counting_iterator<uint32_t>(0), EntryCount{w.s_cnt, w.s_flags});
         const hipError_t e = rocprim::inclusive_scan<PcScanCfg>(w.pscan_tmp, w.pscan_tmp_bytes, it, w.pcg,
@@ -2713,6 +2703,37 @@ __global__ void __launch_bounds__(PK_T) k_pk_expand(PkIn in, const uint2* tile_b
             if (out.cts) out.cts[i] = 0;
         }
     }
+}
+
+// Sparse copy back of a packed batch's verdicts (sf_sparse_verdicts): the
+// nonzero waits and rule indices as (index << 32 | value), appended with one
+// atomic per wavefront and list (any order).  counts[0], counts[1]: lengths.
+__global__ void k_sparse_verdicts(const int32_t* wait, const uint16_t* rule, uint32_t n, unsigned long long* wl,
+                                  unsigned long long* rl, uint32_t* counts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int32_t w = i < n ? wait[i] : 0;
+    const uint16_t r = i < n ? rule[i] : (uint16_t)0;
+    const int lane = (int)(threadIdx.x & 63);
+    const unsigned long long mw = __ballot(w != 0), mr = __ballot(r != 0);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    if (mw) {
+        uint32_t b0 = 0;
+        if (lane == __ffsll((long long)mw) - 1) b0 = atomicAdd(&counts[0], (uint32_t)__popcll(mw));
+        b0 = __shfl(b0, __ffsll((long long)mw) - 1);
+        if (w != 0) wl[b0 + __popcll(mw & below)] = ((unsigned long long)i << 32) | (uint32_t)w;
+    }
+    if (mr) {
+        uint32_t b0 = 0;
+        if (lane == __ffsll((long long)mr) - 1) b0 = atomicAdd(&counts[1], (uint32_t)__popcll(mr));
+        b0 = __shfl(b0, __ffsll((long long)mr) - 1);
+        if (r != 0) rl[b0 + __popcll(mr & below)] = ((unsigned long long)i << 32) | r;
+    }
+}
+hipError_t launch_sparse_verdicts(const int32_t* wait, const uint16_t* rule, uint32_t n, unsigned long long* wl,
+                                  unsigned long long* rl, uint32_t* counts, hipStream_t s) {
+    hipMemsetAsync(counts, 0, 8, s);
+    if (n) hipLaunchKernelGGL(k_sparse_verdicts, dim3((n + 255) / 256), dim3(256), 0, s, wait, rule, n, wl, rl, counts);
+    return hipGetLastError();
 }
 
 hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64_t* xcts, const int32_t* cext,
