@@ -1078,7 +1078,10 @@ def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
         t0 = time.perf_counter()
         pb = abi.PackedBatch(hb, alloc=pin.array)
         log(f"[leg e2e_pinned] packed {hb.n} events into {pb.nbytes() / 1e9:.2f} GB in {time.perf_counter() - t0:.1f}s")
-        outs = [pin.verdicts(hb.n) for _ in range(3)]
+        # sparse copy back (sf_submit_packed_sparse_async): 1 status byte per event plus
+        # the nonzero waits / rule indices, n/16 entries of each list prefetched with it
+        pre = hb.n // 16
+        outs = [pin.sparse_verdicts(hb.n, pre) for _ in range(3)]
         base_ts = pb.ts_base
         timed = timed or max(3, steps - 2)
         walls = []
@@ -1089,7 +1092,7 @@ def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
                 t = time.perf_counter()
             pb.ts_base = base_ts + k * DURATION_MS
             o = outs[0] if k == 0 else (outs[1] if k == steps - 1 else outs[2])
-            e.submit_packed_async(pb, o)
+            e.submit_packed_sparse_async(pb, o)
             if k == 0:
                 e.sync()                                   # batch 0 kept for parity
         e.sync()
@@ -1099,21 +1102,40 @@ def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
         # steady-state period of the pipeline is the rest over timed - 1 batches
         pb.ts_base = base_ts + steps * DURATION_MS
         t1 = time.perf_counter()
-        e.submit_packed_async(pb, outs[2])
+        e.submit_packed_sparse_async(pb, outs[2])
         e.sync()
         lat = time.perf_counter() - t1
         period = (total - lat) / max(1, timed - 1) * 1e3
         ent = int(((hb.flags & abi.EV_EXIT) == 0).sum())
-        bad0 = {"status": int((outs[0].status != g0[0]).sum()), "wait_ms": int((outs[0].wait_ms != g0[1]).sum()),
-                "rule_idx": int((outs[0].rule_idx != g0[2]).sum())}
-        badl = {"status": int((outs[1].status != glast[0]).sum()), "wait_ms": int((outs[1].wait_ms != glast[1]).sum())}
-        return {"what": "config3 batches from pinned host buffers in the compact form (sf_submit_packed_async: "
-                        "H2D of batch k+1, decide of k and D2H of k-1 overlapped)",
+        # the H2D-bound time: the packed arrays copied alone (pinned -> HBM, synchronous)
+        import ctypes as C
+        arrs = [a for a in (pb.ev, pb.exit_ref, pb.exit_cts, pb.count_ext, pb.origin) if a is not None and a.nbytes]
+        dptr = C.c_void_p()
+        engine._check(engine.lib().sf_device_alloc(e.h, max(a.nbytes for a in arrs), C.byref(dptr)))
+        h2d = []
+        for _ in range(3):
+            t2 = time.perf_counter()
+            for a in arrs:
+                engine._check(engine.lib().sf_memcpy(e.h, dptr.value, a.ctypes.data, a.nbytes, 0))
+            h2d.append(time.perf_counter() - t2)
+        engine._check(engine.lib().sf_device_free(e.h, dptr.value))
+        h2d_ms = 1e3 * min(h2d)
+        d0, dl = outs[0].dense(), outs[1].dense()
+        bad0 = {"status": int((d0.status != g0[0]).sum()), "wait_ms": int((d0.wait_ms != g0[1]).sum()),
+                "rule_idx": int((d0.rule_idx != g0[2]).sum())}
+        badl = {"status": int((dl.status != glast[0]).sum()), "wait_ms": int((dl.wait_ms != glast[1]).sum())}
+        lists = [int(outs[1].counts[0]), int(outs[1].counts[1])]
+        d2h = int(hb.n + 8 + 2 * 8 * pre + 8 * sum(max(0, c - pre) for c in lists))
+        return {"what": "config3 batches from pinned host buffers in the compact form (sf_submit_packed_sparse_async: "
+                        "H2D of batch k+1, decide of k and the sparse D2H of k-1 overlapped)",
                 "events": int(hb.n), "ms_per_batch": round(ms, 3), "decisions_per_s": round(ent / (ms / 1e3), 1),
                 "latency_ms": round(lat * 1e3, 3), "period_ms": round(period, 3),
                 "period_note": "ms_per_batch includes the drain of the last batch; period_ms = (timed wall - one "
                                "batch's latency) / (timed - 1), the steady-state interval of the pipeline",
-                "timed_batches": timed, "h2d_bytes": int(pb.nbytes()), "d2h_bytes": int(hb.n * (1 + 4 + 2)),
+                "timed_batches": timed, "h2d_bytes": int(pb.nbytes()), "d2h_bytes": d2h,
+                "d2h_bytes_per_event": round(d2h / hb.n, 3), "d2h_dense_bytes": int(hb.n * (1 + 4 + 2)),
+                "h2d_alone_ms": round(h2d_ms, 3), "period_over_h2d": round(period / h2d_ms, 3),
+                "sparse_lists": {"waits": lists[0], "rules": lists[1], "prefetch_each": pre},
                 "parity": {"what": "batch 0 and the last batch vs the headline run's verdicts", "batch0": bad0,
                            "last": badl, "exact": all(v == 0 for v in bad0.values()) and
                            all(v == 0 for v in badl.values())}}

@@ -29,9 +29,10 @@ import static java.lang.foreign.ValueLayout.JAVA_SHORT;
  * every other one as the sf_event_batch SoA (sf_submit).
  *
  * Latency / throughput contract.  Packed batches are double-buffered: the
- * flusher enqueues batch k+1 with sf_submit_packed_async into the buffer set
- * batch k is not using, then waits for batch k alone (sf_sync_packed) and
- * hands out its verdicts, so the H2D copy of k+1 overlaps the decision of k
+ * flusher enqueues batch k+1 with sf_submit_packed_sparse_async into the
+ * buffer set batch k is not using, then waits for batch k alone
+ * (sf_sync_packed_sparse) and hands out its verdicts (copied back as a status
+ * byte per event plus the nonzero waits / rule indices), so the H2D copy of k+1 overlaps the decision of k
  * and the copy back of k-1.  A caller still waits only for its own batch: its
  * verdict is delivered as soon as its batch is back, and a batch is never held
  * for a later one -- when the queue is empty the flusher collects the batch in
@@ -66,8 +67,11 @@ final class EventBatcher implements Runnable {
     private final class PackedBuf {
         final MemorySegment pev = pinned(8L * maxBatch), pxref = pinned(8L * maxBatch), pxcts = pinned(8L * maxBatch);
         final MemorySegment pcext = pinned(4L * maxBatch), porigin = pinned(4L * maxBatch);
-        final MemorySegment pstatus = pinned(maxBatch), pwait = pinned(4L * maxBatch), prule = pinned(2L * maxBatch);
-        final MemorySegment packed = arena.allocate(PACKED_BATCH), pverdicts = arena.allocate(VERDICTS);
+        // verdicts copied back sparse: a status byte per event, the nonzero waits / rule
+        // indices as (index << 32 | value) lists, maxBatch / 16 of each with the batch
+        final MemorySegment pstatus = pinned(maxBatch), pwaits = pinned(8L * maxBatch), prules = pinned(8L * maxBatch);
+        final MemorySegment pcounts = pinned(8);
+        final MemorySegment packed = arena.allocate(PACKED_BATCH), pverdicts = arena.allocate(SPARSE_VERDICTS);
         final List<Ticket> tickets = new ArrayList<>();
     }
     private final PackedBuf[] pbufs;
@@ -154,8 +158,8 @@ final class EventBatcher implements Runnable {
         if (f == null) return;
         inFlight = null;
         try {
-            check((int) SYNC_PACKED.invokeExact(engine.handle, f.pverdicts));
-            deliver(f.tickets, f.pstatus, f.pwait, f.prule);
+            check((int) SYNC_PACKED_SPARSE.invokeExact(engine.handle, f.pverdicts));
+            deliverSparse(f.tickets, f.pstatus, f.pwaits, f.prules, f.pcounts);
         } catch (Throwable t) {
             failOpen(f.tickets);
         }
@@ -166,6 +170,26 @@ final class EventBatcher implements Runnable {
             Ticket t = b.get(i);
             t.waitMs = wt.getAtIndex(JAVA_INT, i);
             t.ruleIdx = Short.toUnsignedInt(ru.getAtIndex(JAVA_SHORT, i));
+            t.status = st.getAtIndex(JAVA_BYTE, i);
+            LockSupport.unpark(t.caller);
+        }
+    }
+
+    /** Statuses, then the listed waits / rule indices (every other one is 0). */
+    private static void deliverSparse(List<Ticket> b, MemorySegment st, MemorySegment waits, MemorySegment rules,
+                                      MemorySegment counts) {
+        for (Ticket t : b) { t.waitMs = 0; t.ruleIdx = 0; }
+        final int nw = counts.getAtIndex(JAVA_INT, 0), nr = counts.getAtIndex(JAVA_INT, 1);
+        for (int k = 0; k < nw; k++) {
+            long x = waits.getAtIndex(JAVA_LONG, k);
+            b.get((int) (x >>> 32)).waitMs = (int) x;
+        }
+        for (int k = 0; k < nr; k++) {
+            long x = rules.getAtIndex(JAVA_LONG, k);
+            b.get((int) (x >>> 32)).ruleIdx = (int) (x & 0xffff);
+        }
+        for (int i = 0; i < b.size(); i++) {
+            Ticket t = b.get(i);
             t.status = st.getAtIndex(JAVA_BYTE, i);
             LockSupport.unpark(t.caller);
         }
@@ -305,14 +329,15 @@ final class EventBatcher implements Runnable {
         pk.set(JAVA_INT, off(PACKED_BATCH, "n_exit"), nx);
         pk.set(JAVA_INT, off(PACKED_BATCH, "n_count_ext"), nc);
         MemorySegment v = p.pverdicts;
-        v.set(JAVA_INT, off(VERDICTS, "mem"), SF_MEM_HOST_);
-        v.set(ADDRESS, off(VERDICTS, "status"), p.pstatus);
-        v.set(ADDRESS, off(VERDICTS, "wait_ms"), p.pwait);
-        v.set(ADDRESS, off(VERDICTS, "rule_idx"), p.prule);
+        v.set(ADDRESS, off(SPARSE_VERDICTS, "status"), p.pstatus);
+        v.set(ADDRESS, off(SPARSE_VERDICTS, "waits"), p.pwaits);
+        v.set(ADDRESS, off(SPARSE_VERDICTS, "rules"), p.prules);
+        v.set(ADDRESS, off(SPARSE_VERDICTS, "counts"), p.pcounts);
+        v.set(JAVA_INT, off(SPARSE_VERDICTS, "prefetch"), Math.max(64, maxBatch / 16));
         p.tickets.clear();
         p.tickets.addAll(b);
         try {
-            check((int) SUBMIT_PACKED_ASYNC.invokeExact(engine.handle, pk, v));
+            check((int) SUBMIT_PACKED_SPARSE_ASYNC.invokeExact(engine.handle, pk, v));
         } catch (Throwable t) {
             collect();
             throw t;

@@ -53,6 +53,10 @@ final class SentinelFlowNative {
     static final MethodHandle SUBMIT_PACKED_ASYNC = fn("sf_submit_packed_async",
             FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
     static final MethodHandle SYNC_PACKED = fn("sf_sync_packed", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
+    static final MethodHandle SUBMIT_PACKED_SPARSE_ASYNC = fn("sf_submit_packed_sparse_async",
+            FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
+    static final MethodHandle SYNC_PACKED_SPARSE = fn("sf_sync_packed_sparse",
+            FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
     // page-locked host memory (the batch arrays: the H2D copy runs at PCIe speed)
     static final MethodHandle HOST_ALLOC = fn("sf_host_alloc",
             FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));
@@ -136,6 +140,12 @@ final class SentinelFlowNative {
     static final StructLayout VERDICTS = MemoryLayout.structLayout(
             JAVA_INT.withName("mem"), MemoryLayout.paddingLayout(4),
             ADDRESS.withName("status"), ADDRESS.withName("wait_ms"), ADDRESS.withName("rule_idx"));
+
+    /** sf_sparse_verdicts: 1 status byte per event plus (index << 32 | value) lists of the
+     *  nonzero waits and rule indices (the copy back of a packed batch). */
+    static final StructLayout SPARSE_VERDICTS = MemoryLayout.structLayout(
+            ADDRESS.withName("status"), ADDRESS.withName("waits"), ADDRESS.withName("rules"),
+            ADDRESS.withName("counts"), JAVA_INT.withName("prefetch"), JAVA_INT.withName("pad"));
 
     /** sf_token_batch. */
     static final StructLayout TOKEN_BATCH = MemoryLayout.structLayout(

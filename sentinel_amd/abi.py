@@ -181,6 +181,38 @@ class sf_node_state(C.Structure):
     ]
 
 
+class sf_sparse_verdicts(C.Structure):
+    _fields_ = [("status", C.c_void_p), ("waits", C.c_void_p), ("rules", C.c_void_p), ("counts", C.c_void_p),
+                ("prefetch", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class HostSparseVerdicts:
+    """sf_sparse_verdicts in numpy arrays: 1 status byte per event plus the
+    lists of nonzero waits / rule indices (index << 32 | value, any order)."""
+
+    def __init__(self, n: int, prefetch: int = 0, alloc=None):
+        alloc = alloc or (lambda shape, dtype: np.zeros(shape, dtype))
+        self.n = n
+        self.status = alloc((n,), np.uint8)
+        self.waits = alloc((max(n, 1),), np.uint64)
+        self.rules = alloc((max(n, 1),), np.uint64)
+        self.counts = alloc((2,), np.uint32)
+        self.prefetch = int(prefetch)
+
+    def c_struct(self) -> sf_sparse_verdicts:
+        return sf_sparse_verdicts(self.status.ctypes.data, self.waits.ctypes.data, self.rules.ctypes.data,
+                                  self.counts.ctypes.data, self.prefetch, 0)
+
+    def dense(self) -> "HostVerdicts":
+        v = HostVerdicts(self.n)
+        v.status[:] = self.status
+        w = self.waits[:int(self.counts[0])]
+        r = self.rules[:int(self.counts[1])]
+        v.wait_ms[(w >> np.uint64(32)).astype(np.int64)] = (w & np.uint64(0xffffffff)).astype(np.uint32).view(np.int32)
+        v.rule_idx[(r >> np.uint64(32)).astype(np.int64)] = (r & np.uint64(0xffff)).astype(np.uint16)
+        return v
+
+
 class sf_rule_state(C.Structure):
     _fields_ = [("stored_tokens", C.c_int64), ("last_filled_time", C.c_int64), ("latest_passed_time", C.c_int64)]
 

@@ -70,6 +70,8 @@ def _declare(L):
     f("sf_submit_packed", I, P, C.POINTER(abi.sf_packed_batch), C.POINTER(abi.sf_verdicts))
     f("sf_submit_packed_async", I, P, C.POINTER(abi.sf_packed_batch), C.POINTER(abi.sf_verdicts))
     f("sf_sync_packed", I, P, C.POINTER(abi.sf_verdicts))
+    f("sf_submit_packed_sparse_async", I, P, C.POINTER(abi.sf_packed_batch), C.POINTER(abi.sf_sparse_verdicts))
+    f("sf_sync_packed_sparse", I, P, C.POINTER(abi.sf_sparse_verdicts))
     f("sf_load_namespaces", I, P, C.POINTER(abi.sf_namespace), U32)
     f("sf_load_cluster_rules", I, P, C.POINTER(abi.sf_cluster_flow_rule), U32,
       C.POINTER(abi.sf_cluster_param_rule), U32, C.POINTER(abi.sf_hot_item), U32)
@@ -223,6 +225,9 @@ class PinnedArrays:
         v.rule_idx = self.array((n,), np.uint16) if with_rule else None
         return v
 
+    def sparse_verdicts(self, n: int, prefetch: int) -> abi.HostSparseVerdicts:
+        return abi.HostSparseVerdicts(n, prefetch, alloc=self.array)
+
     def free(self):
         for p in self.ptrs:
             lib().sf_host_free(self.eng.h, p)
@@ -354,6 +359,16 @@ class FlowEngine:
         (the batch enqueued after it keeps running); raises that batch's error."""
         v = out.c_struct()
         _check(lib().sf_sync_packed(self.h, C.byref(v)))
+
+    def submit_packed_sparse_async(self, batch: abi.PackedBatch, out: abi.HostSparseVerdicts):
+        """sf_submit_packed_sparse_async: as submit_packed_async, the verdicts copied back
+        sparse (1 B per event plus the nonzero waits / rule indices)."""
+        b, v = batch.c_struct(), out.c_struct()
+        _check(lib().sf_submit_packed_sparse_async(self.h, C.byref(b), C.byref(v)))
+
+    def sync_packed_sparse(self, out: abi.HostSparseVerdicts):
+        v = out.c_struct()
+        _check(lib().sf_sync_packed_sparse(self.h, C.byref(v)))
 
     def submit_device(self, batch: DeviceBatch, out: DeviceVerdicts):
         b = batch.c_struct()

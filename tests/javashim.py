@@ -11,7 +11,8 @@ SIZES = {"JAVA_INT": 4, "JAVA_LONG": 8, "JAVA_DOUBLE": 8, "ADDRESS": 8, "JAVA_BY
 C_STRUCT = {"CONFIG": "sf_config", "FLOW_RULE": "sf_flow_rule", "HOT_ITEM": "sf_hot_item",
             "PARAM_RULE": "sf_param_rule", "SYSTEM_RULE": "sf_system_rule", "DEGRADE_RULE": "sf_degrade_rule",
             "EVENT_BATCH": "sf_event_batch", "VERDICTS": "sf_verdicts", "TOKEN_BATCH": "sf_token_batch",
-            "TOKEN_RESULTS": "sf_token_results", "PACKED_BATCH": "sf_packed_batch"}
+            "TOKEN_RESULTS": "sf_token_results", "PACKED_BATCH": "sf_packed_batch",
+            "SPARSE_VERDICTS": "sf_sparse_verdicts"}
 
 
 def source(name):

@@ -149,14 +149,23 @@ def test_rule_listeners_keep_the_managers_rules():
 
 
 def test_batcher_double_buffers_packed_batches():
-    """EventBatcher enqueues batch k+1 (sf_submit_packed_async) before it waits
-    for batch k alone (sf_sync_packed); two buffer sets alternate."""
+    """EventBatcher enqueues batch k+1 (sf_submit_packed_sparse_async) before
+    it waits for batch k alone (sf_sync_packed_sparse); two buffer sets
+    alternate; the verdicts come back sparse (a status byte per event plus the
+    (index << 32 | value) lists of nonzero waits / rule indices, every other
+    one 0), as include/sentinel_flow.h sf_sparse_verdicts lays them out."""
     src = j.source("EventBatcher.java")
     fp = src[src.index("private boolean flushPacked"):]
-    assert fp.index("SUBMIT_PACKED_ASYNC.invokeExact") < fp.index("collect();                                   // batch k-1")
-    assert "SYNC_PACKED.invokeExact(engine.handle, f.pverdicts)" in src
+    assert fp.index("SUBMIT_PACKED_SPARSE_ASYNC.invokeExact") < fp.index("collect();                                   // batch k-1")
+    assert "SYNC_PACKED_SPARSE.invokeExact(engine.handle, f.pverdicts)" in src
     assert "pbufs[pcur]" in fp and "pcur ^= 1" in fp
     assert "SUBMIT_PACKED.invokeExact" not in src          # no synchronous packed path left
+    ds = src[src.index("private static void deliverSparse"):]
+    ds = ds[:ds.index("private void flush(")]
+    assert "t.waitMs = 0; t.ruleIdx = 0;" in ds and "(int) (x >>> 32)" in ds and "(int) (x & 0xffff)" in ds
+    assert ds.index("t.waitMs = 0") < ds.index("getAtIndex(JAVA_LONG, k)") < ds.index("LockSupport.unpark")
+    hdr = open(HEADER).read()
+    assert "index << 32 | (uint32_t)wait_ms" in hdr and "index << 32 | rule_idx" in hdr
     readme = open(os.path.join(ROOT, "java", "README.md")).read()
     assert "sf_sync_packed" in readme and "latency" in readme.lower()
 

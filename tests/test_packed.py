@@ -98,3 +98,75 @@ def test_packing_refuses_a_long_span():
     ts[-1] = ts[0] + (1 << 20)
     with pytest.raises(ValueError):
         abi.PackedBatch(abi.HostBatch(hb.res_id, ts, hb.count, hb.flags, entry_ref=hb.entry_ref))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prefetch", [0, 64, 1 << 20])
+def test_gpu_packed_sparse_verdicts(prefetch):
+    """sf_submit_packed_sparse_async: 1 status byte per event back with the
+    batch plus the nonzero waits / rule indices (the first `prefetch` of each
+    list with it, the rest at sf_sync_packed_sparse or sf_sync): the dense
+    verdicts of the same batches, double-buffered as the Java flusher does."""
+    from oracle.oracle import OracleEngine
+    from sentinel_amd import engine
+    from tests import parity
+    hb, R = _batch(seed=7, R=600, n=90_000)
+    # a second, tighter QPS rule on every third resource: its blocks carry rule index 1
+    rules = list(trace.mixed_rules(R, seed=7)) + [
+        abi.sf_flow_rule(resource=r, grade=abi.GRADE_QPS, count=4.0, strategy=0, control_behavior=0,
+                         warm_up_period_sec=10, max_queueing_time_ms=500) for r in range(0, R, 3)]
+    cuts = [0, 30_000, 60_000, hb.n]
+    parts = [hb.subset(cuts[k], cuts[k + 1]) for k in range(3)]
+    cfg = abi.default_config(max_resources=R, max_batch=max(p.n for p in parts))
+    eng, ora = engine.FlowEngine(cfg), OracleEngine(cfg)
+    pin = engine.PinnedArrays(eng)
+    try:
+        for x in (eng, ora):
+            x.load_flow_rules(rules)
+        pbs = [abi.PackedBatch(p, alloc=pin.array) for p in parts]
+        outs = [pin.sparse_verdicts(p.n, prefetch) for p in parts]
+        eng.submit_packed_sparse_async(pbs[0], outs[0])
+        waits = rules_n = 0
+        for k in range(len(parts)):
+            if k + 1 < len(parts):
+                eng.submit_packed_sparse_async(pbs[k + 1], outs[k + 1])
+            if k < len(parts) - 1:
+                eng.sync_packed_sparse(outs[k])
+            else:
+                eng.sync()                                  # sf_sync completes the lists too
+            want = ora.submit(parts[k])
+            parity.compare_verdicts(outs[k].dense(), want, f"batch {k}")
+            waits += int(outs[k].counts[0]); rules_n += int(outs[k].counts[1])
+            assert outs[k].counts[0] == (want.wait_ms != 0).sum() and outs[k].counts[1] == (want.rule_idx != 0).sum()
+        assert waits > 64 and rules_n > 64
+    finally:
+        pin.free()
+        eng.close()
+        ora.close()
+
+
+@pytest.mark.gpu
+def test_gpu_packed_error_stays_with_its_batch():
+    """An async packed batch that raises an error (an exit whose entry ref is
+    past the batch) keeps it: a synchronous submit in between drains the
+    engine and succeeds, and the failing batch's own sf_sync_packed reports it."""
+    from sentinel_amd import engine
+    hb, R = _batch(seed=9, R=300, n=20_000)
+    cfg = abi.default_config(max_resources=R, max_batch=hb.n)
+    eng = engine.FlowEngine(cfg)
+    pin = engine.PinnedArrays(eng)
+    try:
+        eng.load_flow_rules(trace.mixed_rules(R, seed=9))
+        bad = abi.PackedBatch(hb, alloc=pin.array)
+        bad.exit_ref[0] = hb.n + 5                          # no such entry in the batch
+        ob = pin.verdicts(hb.n)
+        eng.submit_packed_async(bad, ob)
+        good = hb.subset(0, 1000)
+        good = abi.HostBatch(good.res_id, good.ts_ms + 4000, good.count, good.flags, entry_ref=good.entry_ref,
+                             create_ts=good.create_ts)
+        eng.submit(good)                                    # drains; not the other batch's error
+        with pytest.raises(engine.EngineError):
+            eng.sync_packed(ob)
+    finally:
+        pin.free()
+        eng.close()
