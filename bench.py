@@ -1079,8 +1079,9 @@ def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
         pb = abi.PackedBatch(hb, alloc=pin.array)
         log(f"[leg e2e_pinned] packed {hb.n} events into {pb.nbytes() / 1e9:.2f} GB in {time.perf_counter() - t0:.1f}s")
         # sparse copy back (sf_submit_packed_sparse_async): 1 status byte per event plus
-        # the nonzero waits / rule indices, n/16 entries of each list prefetched with it
-        pre = hb.n // 16
+        # the nonzero waits / rule indices, n/64 entries of each list prefetched with it
+        # (config 3 queues 1.3 % of its events; a longer list is completed at the sync)
+        pre = hb.n // 64
         outs = [pin.sparse_verdicts(hb.n, pre) for _ in range(3)]
         base_ts = pb.ts_base
         timed = timed or max(3, steps - 2)

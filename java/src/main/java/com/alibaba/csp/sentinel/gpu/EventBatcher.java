@@ -68,7 +68,7 @@ final class EventBatcher implements Runnable {
         final MemorySegment pev = pinned(8L * maxBatch), pxref = pinned(8L * maxBatch), pxcts = pinned(8L * maxBatch);
         final MemorySegment pcext = pinned(4L * maxBatch), porigin = pinned(4L * maxBatch);
         // verdicts copied back sparse: a status byte per event, the nonzero waits / rule
-        // indices as (index << 32 | value) lists, maxBatch / 16 of each with the batch
+        // indices as (index << 32 | value) lists, maxBatch / 64 of each with the batch
         final MemorySegment pstatus = pinned(maxBatch), pwaits = pinned(8L * maxBatch), prules = pinned(8L * maxBatch);
         final MemorySegment pcounts = pinned(8);
         final MemorySegment packed = arena.allocate(PACKED_BATCH), pverdicts = arena.allocate(SPARSE_VERDICTS);
@@ -333,7 +333,7 @@ final class EventBatcher implements Runnable {
         v.set(ADDRESS, off(SPARSE_VERDICTS, "waits"), p.pwaits);
         v.set(ADDRESS, off(SPARSE_VERDICTS, "rules"), p.prules);
         v.set(ADDRESS, off(SPARSE_VERDICTS, "counts"), p.pcounts);
-        v.set(JAVA_INT, off(SPARSE_VERDICTS, "prefetch"), Math.max(64, maxBatch / 16));
+        v.set(JAVA_INT, off(SPARSE_VERDICTS, "prefetch"), Math.max(64, maxBatch / 64));
         p.tickets.clear();
         p.tickets.addAll(b);
         try {

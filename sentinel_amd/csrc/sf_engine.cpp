@@ -42,6 +42,7 @@ static int fail(int code, const std::string& msg) {
 // a device copy of host event arrays, remembered by their addresses (stage_in_events)
 struct StageBuf {
     void* p = nullptr; size_t bytes = 0; const void* key[5] = {}; uint32_t n = 0;
+    int64_t fp[3] = {};                                     // ts[0], ts[n-1], flags[0] of the staged arrays
     const uint8_t* st_src = nullptr; uint32_t st_n = 0;    // verdicts [0, st_n) of st_src already staged
 };
 
@@ -1480,7 +1481,12 @@ static int stage_in_events(sf_engine* e, StageBuf& sb, const sf_event_batch* in,
     const size_t o_ct = need; need += align_up((size_t)n * 8);
     const size_t o_st = need; need += align_up((size_t)n + 1);
     const void* key[5] = {in->ts_ms, in->count, in->flags, in->entry_ref, in->create_ts};
-    keep = keep && sb.p && sb.n == n && std::equal(key, key + 5, sb.key) && need <= sb.bytes;
+    // the same host arrays as the round before: a cheap fingerprint of their
+    // contents must match too (the contract is that the caller only appends
+    // verdicts between rounds; an edited event array is restaged, not trusted)
+    const int64_t fp[3] = {n ? in->ts_ms[0] : 0, n ? in->ts_ms[n - 1] : 0, n ? (int64_t)in->flags[0] : 0};
+    keep = keep && sb.p && sb.n == n && std::equal(key, key + 5, sb.key) && std::equal(fp, fp + 3, sb.fp) &&
+           need <= sb.bytes;
     if (need > sb.bytes) {
         if (sb.p) hipFree(sb.p);
         sb.p = nullptr; sb.bytes = 0; sb.n = 0;
@@ -1496,6 +1502,7 @@ static int stage_in_events(sf_engine* e, StageBuf& sb, const sf_event_batch* in,
         if (in->entry_ref) HIP_TRY(hipMemcpyAsync(base + o_er, in->entry_ref, (size_t)n * 8, hipMemcpyHostToDevice, s));
         if (in->create_ts) HIP_TRY(hipMemcpyAsync(base + o_ct, in->create_ts, (size_t)n * 8, hipMemcpyHostToDevice, s));
         std::copy(key, key + 5, sb.key);
+        std::copy(fp, fp + 3, sb.fp);
         sb.n = n;
     }
     if (status && n_status) {
