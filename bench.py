@@ -1231,8 +1231,8 @@ def oracle_leg(rules, hb, R, out0, out_last, eng, steps, per_res):
        latestPassedTime, WarmUp tokens).  Batch 0's replay time is the
        multi-core CPU baseline (its verdicts must equal the one-core replay);
        the last batch's verdicts (status, wait) are compared with the GPU's
-       last timed batch, and so are the node state and controller state of a
-       sample of resources (the 64 busiest and 1024 others) and ENTRY_NODE."""
+       last timed batch, and so are the node state (per-row digests) and the
+       controller state of every resource and ENTRY_NODE."""
     try:
         from oracle import oracle as so
         from oracle import sharded
@@ -1278,18 +1278,13 @@ def oracle_leg(rules, hb, R, out0, out_last, eng, steps, per_res):
                                  f"replay: {same})", "seconds": round(dtk, 2), "single_core": single}
         t_all = time.perf_counter() - t_all
         gs, gw = out_last.status.numpy(), out_last.wait_ms.numpy()
-        busiest = np.argsort(-per_res)[:64]
-        rng = np.random.default_rng(99)
-        touched = np.nonzero(per_res)[0]
-        sample = np.unique(np.concatenate([busiest, rng.choice(touched, size=min(1024, touched.size), replace=False)]))
-        node_bad = rule_bad = 0
-        for r in sample:
-            if abi.node_state_to_dict(eng.read_node(int(r))) != abi.node_state_to_dict(sh.read_node(int(r))):
-                node_bad += 1
-            a, b = eng.read_rule_state(int(r)), sh.read_rule_state(int(r))
-            if (a.stored_tokens, a.last_filled_time, a.latest_passed_time) != \
-                    (b.stored_tokens, b.last_filled_time, b.latest_passed_time):
-                rule_bad += 1
+        # every node and every rule's controller state: the engine's per-row
+        # digests (sf_node_digests, on the device) against the oracle shards'
+        t_d = time.perf_counter()
+        node_bad = int((eng.node_digests(R) != sh.node_digests(R)).sum())
+        rule_bad = int((eng.rule_states(0, R) != sh.rule_states(R)).any(axis=1).sum())
+        log(f"[oracle] whole-node comparison: {node_bad} node / {rule_bad} rule-state mismatches "
+            f"in {time.perf_counter() - t_d:.1f}s")
         from sentinel_amd import dist as sdist
         en_same = abi.node_state_to_dict(eng.read_entry_node()) == \
             abi.node_state_to_dict(sdist.merge_entry_nodes(sh.entry_nodes()))
@@ -1299,7 +1294,9 @@ def oracle_leg(rules, hb, R, out0, out_last, eng, steps, per_res):
         steady = {"what": f"every batch of the run ({steps}: warmup + timed, state carried across batches, "
                           f"{steps * DURATION_MS // 1000} s of trace time) replayed by the resource-sharded oracle; "
                           f"batch {steps - 1} (the last timed one) compared",
-                  "batch": steps - 1, "events": int(hb.n), "nodes_compared": int(sample.size),
+                  "batch": steps - 1, "events": int(hb.n), "nodes_compared": int(R), "rule_states_compared": int(R),
+                  "how": "every resource's node (FNV-1a 64 digest of its canonical sf_node_state, sf_node_digests "
+                         "vs so_node_digests) and every rule's controller state, plus ENTRY_NODE",
                   "mismatches": lm, "exact": all(x == 0 for x in lm.values()), "replay_s": round(t_all, 1)}
     except Exception as ex:  # pragma: no cover - the one-core figure stays
         cpu = dict(single, multicore_error=str(ex)[:200])

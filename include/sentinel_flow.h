@@ -601,6 +601,16 @@ int  sf_cluster_sum(sf_engine* e, int64_t flow_id, int event, int64_t now_ms, in
 int  sf_read_node(sf_engine* e, uint32_t resource, sf_node_state* out);
 int  sf_read_entry_node(sf_engine* e, sf_node_state* out);
 int  sf_read_rule_state(sf_engine* e, uint32_t rule_index, sf_rule_state* out);
+/* Bulk forms of the two reads above, for whole-engine state comparison.
+ * sf_node_digests: out[l] for local rows l < n_rows (row l holds resource
+ * l * shard_count + shard_index) = FNV-1a 64 (h ^= word; h *= 0x100000001b3,
+ * seed 0xcbf29ce484222325) over the row's sf_node_state as sf_read_node gives
+ * it, word by word: for i < sample_count second[i] (window_start, pass, block,
+ * exception, success, rt, occupied_pass, min_rt), borrow_ws[i],
+ * borrow_pass[i]; then the SF_MINUTE_BUCKETS minute buckets; then
+ * cur_thread_num.  sf_read_rule_states: rules first .. first + n - 1. */
+int  sf_node_digests(sf_engine* e, uint64_t* out, uint32_t n_rows);
+int  sf_read_rule_states(sf_engine* e, uint32_t first, uint32_t n, sf_rule_state* out);
 /* The origin node of (resource, origin) (ClusterNode.getOrCreateOriginNode,
  * ClusterNode.java:101-120) and the DefaultNode of (context, resource)
  * (NodeSelectorSlot), for the resources whose rules read them.  The engine

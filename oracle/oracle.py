@@ -156,6 +156,9 @@ def _declare(L):
     f("so_load_degrade_rules", C.c_int, P, C.POINTER(abi.sf_degrade_rule), U32, C.POINTER(U32))
     f("so_read_breaker", C.c_int, P, U32, C.POINTER(abi.sf_breaker_state))
     f("so_read_rule_state", C.c_int, P, U32, C.POINTER(abi.sf_rule_state))
+    f("so_node_digest", U64, C.POINTER(abi.sf_node_state), C.c_int)
+    f("so_node_digests", C.c_int, P, P, U32)
+    f("so_read_rule_states", C.c_int, P, U32, U32, P)
     f("so_read_param", C.c_int, P, U32, U8, U64, C.POINTER(I64), C.POINTER(I64), C.POINTER(C.c_int))
     f("so_param_thread", I64, P, U32, C.c_int, U8, U64)
     f("so_snapshot", C.c_int, P, I64, C.POINTER(abi.sf_metric_row), U32, C.POINTER(U32))
@@ -588,6 +591,18 @@ class OracleEngine:
         s = abi.sf_rule_state()
         assert lib().so_read_rule_state(self.h, idx, C.byref(s)) == 0
         return s
+
+    def node_digests(self, n_rows):
+        """FNV-1a digest of every local row's canonical node state (so_node_digests)."""
+        out = np.empty(n_rows, np.uint64)
+        assert lib().so_node_digests(self.h, out.ctypes.data, n_rows) == 0
+        return out
+
+    def rule_states(self, first, n):
+        """(n, 3) int64: stored_tokens, last_filled_time, latest_passed_time of rules first..first+n-1."""
+        out = np.empty((n, 3), np.int64)
+        assert lib().so_read_rule_states(self.h, first, n, out.ctypes.data) == 0
+        return out
 
     def read_param(self, rule_idx, value):
         t, k, h = I64(0), I64(0), C.c_int(0)

@@ -1885,6 +1885,39 @@ int so_read_rule_state(so_engine* e, uint32_t idx, sf_rule_state* out) {
     so_ctrl_state(e->flow[idx].ctrl, out);
     return SF_OK;
 }
+/* Whole-engine state comparison (bench.py steady-state check, tests): one
+ * FNV-1a digest per local resource row over its canonical sf_node_state words
+ * -- for i < sample_count: second[i] (window_start, pass, block, exception,
+ * success, rt, occupied_pass, min_rt), borrow_ws[i], borrow_pass[i]; then the
+ * 60 minute buckets; then cur_thread_num -- the same word order
+ * include/sentinel_flow.h sf_node_digests gives the engine's rows. */
+static uint64_t fnv_words(uint64_t h, const int64_t* w, int n) {
+    for (int i = 0; i < n; i++) { h ^= (uint64_t)w[i]; h *= 0x100000001b3ull; }
+    return h;
+}
+uint64_t so_node_digest(const sf_node_state* s, int sample_count) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (int i = 0; i < sample_count; i++) {
+        h = fnv_words(h, &s->second[i].window_start, 8);
+        h = fnv_words(h, &s->borrow_ws[i], 1);
+        h = fnv_words(h, &s->borrow_pass[i], 1);
+    }
+    for (int i = 0; i < SF_MINUTE_BUCKETS; i++) h = fnv_words(h, &s->minute[i].window_start, 8);
+    return fnv_words(h, &s->cur_thread_num, 1);
+}
+int so_node_digests(so_engine* e, uint64_t* out, uint32_t n) {
+    sf_node_state st;
+    for (uint32_t l = 0; l < n; l++) {
+        so_node_read(l < e->n_res ? e->res[l].node : NULL, &st);
+        out[l] = so_node_digest(&st, e->cfg.sample_count);
+    }
+    return SF_OK;
+}
+int so_read_rule_states(so_engine* e, uint32_t first, uint32_t n, sf_rule_state* out) {
+    if ((uint64_t)first + n > e->n_flow) return SF_ERR_INVALID;
+    for (uint32_t i = 0; i < n; i++) so_ctrl_state(e->flow[first + i].ctrl, &out[i]);
+    return SF_OK;
+}
 int so_read_param(so_engine* e, uint32_t pidx, uint8_t tag, uint64_t bits,
                   int64_t* time_value, int64_t* tokens, int* has_tokens) {
     if (pidx >= e->n_param) return SF_ERR_INVALID;

@@ -210,6 +210,9 @@ enum { SO_SEL_NONE = 0, SO_SEL_CLUSTER = 1, SO_SEL_ORIGIN = 2, SO_SEL_CONTEXT = 
 int  so_select_node(so_engine* e, uint32_t rule_index, uint32_t origin, uint32_t context);
 int  so_read_entry_node(so_engine* e, sf_node_state* out);
 int  so_read_rule_state(so_engine* e, uint32_t rule_index, sf_rule_state* out);
+uint64_t so_node_digest(const sf_node_state* s, int sample_count);
+int  so_node_digests(so_engine* e, uint64_t* out, uint32_t n_rows);      /* one per local row l < n_rows */
+int  so_read_rule_states(so_engine* e, uint32_t first, uint32_t n, sf_rule_state* out);
 int  so_read_param(so_engine* e, uint32_t param_rule_index, uint8_t tag, uint64_t bits,
                    int64_t* time_value, int64_t* tokens, int* has_tokens);
 int32_t so_param_rule_idx(so_engine* e, uint32_t param_rule_index);

@@ -156,6 +156,34 @@ class ShardedOracle:
         """Rule state of the resource's single rule (one rule per resource)."""
         return self.engines[res_rule % self.T].read_rule_state(res_rule // self.T)
 
+    def node_digests(self, R: int):
+        """so_node_digests of every resource 0..R-1 (shard res % T, row res // T)."""
+        parts = [None] * self.T
+
+        def run(k):
+            n = (R - k + self.T - 1) // self.T
+            parts[k] = self.engines[k].node_digests(n) if n > 0 else None
+
+        ths = [threading.Thread(target=run, args=(k,)) for k in range(self.T)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        out = np.empty(R, np.uint64)
+        for k in range(self.T):
+            if parts[k] is not None:
+                out[k::self.T] = parts[k]
+        return out
+
+    def rule_states(self, R: int):
+        """(R, 3) controller states of rules 0..R-1, rule r being resource r's single rule."""
+        out = np.empty((R, 3), np.int64)
+        for k, e in enumerate(self.engines):
+            n = (R - k + self.T - 1) // self.T
+            if n > 0:
+                out[k::self.T] = e.rule_states(0, n)
+        return out
+
     def entry_nodes(self):
         return [e.read_entry_node() for e in self.engines]
 

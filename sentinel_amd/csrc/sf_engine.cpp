@@ -1901,6 +1901,40 @@ int sf_read_rule_state(sf_engine* e, uint32_t idx, sf_rule_state* out) {
     return SF_OK;
 }
 
+int sf_node_digests(sf_engine* e, uint64_t* out, uint32_t n_rows) {
+    if (!e || (n_rows && !out)) return fail(SF_ERR_INVALID, "null argument");
+    if (n_rows > e->R) return fail(SF_ERR_INVALID, "n_rows above max_resources");
+    std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }
+    if (!n_rows) return SF_OK;
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, (size_t)n_rows * 8));
+    hipError_t he = launch_node_digests(e->st, n_rows, d, e->stream);
+    if (he == hipSuccess) he = hipMemcpyAsync(out, d, (size_t)n_rows * 8, hipMemcpyDeviceToHost, e->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    hipFree(d);
+    if (he != hipSuccess) return fail(SF_ERR_DEVICE, std::string("node digests: ") + hipGetErrorString(he));
+    return SF_OK;
+}
+
+int sf_read_rule_states(sf_engine* e, uint32_t first, uint32_t n, sf_rule_state* out) {
+    if (!e || (n && !out)) return fail(SF_ERR_INVALID, "null argument");
+    if ((uint64_t)first + n > e->n_flow) return fail(SF_ERR_INVALID, "rule index");
+    std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = drain(e); if (rc) return rc; }
+    if (!n) return SF_OK;
+    std::vector<DevRuleState> all(e->n_flow);      // CSR order: the positions of a range are not contiguous
+    HIP_TRY(hipMemcpyAsync(all.data(), e->st.rstate, all.size() * sizeof(DevRuleState), hipMemcpyDeviceToHost,
+                           e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (uint32_t i = 0; i < n; i++) {
+        const DevRuleState& s = all[e->flow_pos[first + i]];
+        out[i].stored_tokens = s.stored_tokens; out[i].last_filled_time = s.last_filled;
+        out[i].latest_passed_time = s.latest_passed;
+    }
+    return SF_OK;
+}
+
 int sf_snapshot(sf_engine* e, int64_t now_ms, sf_metric_row* out, uint32_t cap, uint32_t* n_out) {
     if (!e || !n_out || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);

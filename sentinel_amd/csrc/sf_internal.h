@@ -355,6 +355,7 @@ hipError_t launch_fmt_write(const sf_metric_row* rows, const uint32_t* order, ui
                             const uint64_t* line_off, char* out, hipStream_t s);
 hipError_t launch_param_stats(const DevState& st, unsigned long long* out, hipStream_t s);   // out[0] used, out[1] max probe
 size_t segs_lb_bytes(uint32_t max_n);
+hipError_t launch_node_digests(const DevState& st, uint32_t n, unsigned long long* out, hipStream_t s);
 hipError_t launch_param_thread_read(const DevState& st, uint32_t l, int idx, uint32_t tag, uint64_t bits,
                                     long long* out, hipStream_t s);
 // classify = true: k_classify / k_fill_tiles end the sort phase (the origin

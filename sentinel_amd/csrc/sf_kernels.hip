@@ -2077,6 +2077,40 @@ hipError_t launch_param_thread_read(const DevState& st, uint32_t l, int idx, uin
     return hipGetLastError();
 }
 
+// sf_node_digests: one FNV-1a digest per resource row over its canonical
+// sf_node_state words (absent buckets: SF_WS_ABSENT and zeros), in the word
+// order of include/sentinel_flow.h.  A verification read, not a hot path: one
+// thread per row walks the row's ~4 KB.
+__device__ __forceinline__ uint64_t fnv_w(uint64_t h, int64_t w) { h ^= (uint64_t)w; return h * 0x100000001b3ull; }
+__device__ __forceinline__ uint64_t fnv_bucket(uint64_t h, const Bucket& b) {
+    if (b.ws == WS_NONE) {
+        h = fnv_w(h, SF_WS_ABSENT);
+        for (int k = 0; k < 7; k++) h = fnv_w(h, 0);
+        return h;
+    }
+    h = fnv_w(h, b.ws); h = fnv_w(h, b.pass); h = fnv_w(h, b.block); h = fnv_w(h, b.exc);
+    h = fnv_w(h, b.succ); h = fnv_w(h, b.rt); h = fnv_w(h, b.occ); return fnv_w(h, b.min_rt);
+}
+__global__ void k_node_digests(DevState st, uint32_t n, unsigned long long* out) {
+    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= n) return;
+    const NodeRows r = cluster_rows(st, l);
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (int i = 0; i < st.S; i++) {
+        h = fnv_bucket(h, r.sec[i]);
+        const Borrow b = r.bor[i];
+        h = fnv_w(h, b.ws == WS_NONE ? SF_WS_ABSENT : b.ws);
+        h = fnv_w(h, b.ws == WS_NONE ? 0 : b.pass);
+    }
+    for (int i = 0; i < MINUTE; i++) h = fnv_bucket(h, r.min[i]);
+    out[l] = fnv_w(h, *r.thr);
+}
+hipError_t launch_node_digests(const DevState& st, uint32_t n, unsigned long long* out, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_node_digests, dim3((n + 255) / 256), dim3(256), 0, s, st, n, out);
+    return hipGetLastError();
+}
+
 static inline unsigned blocks(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
 // Several buffer fills in one launch (each hipMemsetAsync is a launch of its

@@ -86,6 +86,8 @@ def _declare(L):
     f("sf_read_node", I, P, U32, C.POINTER(abi.sf_node_state))
     f("sf_read_entry_node", I, P, C.POINTER(abi.sf_node_state))
     f("sf_read_rule_state", I, P, U32, C.POINTER(abi.sf_rule_state))
+    f("sf_node_digests", I, P, P, U32)
+    f("sf_read_rule_states", I, P, U32, U32, P)
     f("sf_read_origin_node", I, P, U32, U32, C.POINTER(abi.sf_node_state))
     f("sf_read_context_node", I, P, U32, U32, C.POINTER(abi.sf_node_state))
     f("sf_load_degrade_rules", I, P, C.POINTER(abi.sf_degrade_rule), U32, C.POINTER(U32))
@@ -570,6 +572,19 @@ class FlowEngine:
         s = abi.sf_rule_state()
         _check(lib().sf_read_rule_state(self.h, idx, C.byref(s)))
         return s
+
+    def node_digests(self, n_rows=None) -> np.ndarray:
+        """One FNV-1a 64 digest per local row's canonical node state (sf_node_digests)."""
+        n = self.cfg.max_resources if n_rows is None else n_rows
+        out = np.empty(n, np.uint64)
+        _check(lib().sf_node_digests(self.h, out.ctypes.data, n))
+        return out
+
+    def rule_states(self, first=0, n=None) -> np.ndarray:
+        """(n, 3) int64 stored_tokens, last_filled_time, latest_passed_time (sf_read_rule_states)."""
+        out = np.empty((n, 3), np.int64)
+        _check(lib().sf_read_rule_states(self.h, first, n, out.ctypes.data))
+        return out
 
     def param_table_stats(self) -> dict:
         """Exact hot-parameter table: occupied slots, capacity, load factor, longest probe."""

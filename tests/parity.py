@@ -33,6 +33,23 @@ def compare_rule_states(eng, ora, n_rules, what=""):
         assert ta == tb, f"{what}: rule {k} state engine={ta} oracle={tb}"
 
 
+def compare_all_nodes(eng, ora, n_rows, sample_count=2, what=""):
+    """Every row at once: the engine's per-row digests (sf_node_digests, on the
+    device) against the oracle's (so_node_digests); a differing row is then
+    compared field by field."""
+    a, b = eng.node_digests(n_rows), ora.node_digests(n_rows)
+    bad = np.nonzero(a != b)[0]
+    if bad.size:
+        compare_nodes(eng, ora, bad[:4], sample_count, what)
+        raise AssertionError(f"{what}: {bad.size} node digests differ (first rows {bad[:8].tolist()})")
+
+
+def compare_all_rule_states(eng, ora, n_rules, what=""):
+    a, b = eng.rule_states(0, n_rules), ora.rule_states(0, n_rules)
+    bad = np.nonzero((a != b).any(axis=1))[0]
+    assert bad.size == 0, f"{what}: {bad.size} rule states differ; first {bad[0]}: engine={a[bad[0]]} oracle={b[bad[0]]}"
+
+
 def run_both(make_engine, make_oracle, cfg, flow_rules=(), param_rules=(), items=(), batches=(), system=(),
              status=None):
     eng, ora = make_engine(cfg), make_oracle(cfg)

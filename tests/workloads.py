@@ -397,6 +397,10 @@ def run(make_engine, make_oracle, w):
     for k, (a, b) in enumerate(outs):
         parity.compare_verdicts(a, b, f"batch{k}")
     parity.compare_nodes(eng, ora, w["nodes"], sample_count=w["cfg"].sample_count)
+    if hasattr(eng, "node_digests"):           # every row, not only the sampled ones
+        parity.compare_all_nodes(eng, ora, w["cfg"].max_resources, sample_count=w["cfg"].sample_count)
+        if w.get("n_flow"):
+            parity.compare_all_rule_states(eng, ora, w["n_flow"])
     if getattr(eng, "has_entry_node", False):
         parity.compare_entry_node(eng, ora, sample_count=w["cfg"].sample_count)
     if w.get("n_flow"):
