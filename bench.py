@@ -492,7 +492,20 @@ def predict_ranks(args, steps=None, warmup=None):
         if counts is None:
             counts = np.bincount(rk, minlength=N).astype(np.int64) * N       # (component 0 scaled: the choice)
             head = int(np.argmax(counts)); light = int(np.argmin(counts))
-            chosen = [head, light] if light != head else [head]
+            # A resource is one serial chain on its rank whatever the placement: the
+            # ranks that own the busiest THREAD / RateLimiter resource (k_heavy_stream)
+            # and the busiest resource overall (k_heavy_decide) are timed as well.
+            per0c = np.bincount(comp.res_id, minlength=R)
+            stream_res = np.nonzero((grade_all == abi.GRADE_THREAD) | (beh_all == abi.BEHAVIOR_RATE_LIMITER))[0]
+            chain = int(stream_res[np.argmax(per0c[stream_res])])
+            top = int(np.argmax(per0c))
+            del per0c
+            own = (lambda r_: int(r_ % N)) if pl is None else (lambda r_: int(pl.owner(np.array([r_]))[0]))
+            roles = {head: "head (most events)"}
+            roles.setdefault(own(chain), f"owns the busiest THREAD / RateLimiter resource ({chain})")
+            roles.setdefault(own(top), f"owns the busiest resource ({top})")
+            roles.setdefault(light, "lightest")
+            chosen = list(roles)
         for r in chosen:
             sel = np.nonzero(rk == r)[0]
             pos = np.full(comp.n, -1, np.int64)
@@ -531,7 +544,7 @@ def predict_ranks(args, steps=None, warmup=None):
         n_entry = int(((hb.flags & abi.EV_EXIT) == 0).sum())
         log(f"[predict] rank {r}: {hb.n} events, t={time.time() - t0:.0f}s")
         ms = time_shard(hb, rules, R_local, N, r, steps, warmup)
-        out["ranks"][str(r)] = {"role": "head (most events)" if r == chosen[0] else "lightest", "events": int(hb.n),
+        out["ranks"][str(r)] = {"role": roles[r], "events": int(hb.n),
                                 "entries": int(n_entry), "ms_per_step": round(ms, 3),
                                 "events_vs_mean": round(hb.n / (N * args.events / N), 3)}
         log(f"[predict] rank {r}: {ms:.2f} ms/step")
@@ -541,7 +554,8 @@ def predict_ranks(args, steps=None, warmup=None):
         "what": "top-K resources by component 0's counts spread LPT-greedy over the ranks, the rest at res % N "
                 "(sentinel_amd/placement.py)", "K": int(pl.moved.size),
         "max_over_mean_events_expected": round(float(counts.max() / counts.mean()), 4)}
-    head_ms = out["ranks"][str(chosen[0])]["ms_per_step"]
+    head_ms = max(v["ms_per_step"] for v in out["ranks"].values())          # the slowest timed rank
+    out["slowest_rank"] = max(out["ranks"], key=lambda k: out["ranks"][k]["ms_per_step"])
     out["single_gpu_ms_per_step"] = round(single, 3)
     out["node_step_ms"] = head_ms
     out["node_decisions_per_s"] = round(node_entries / (head_ms / 1e3), 1)
@@ -554,7 +568,8 @@ def predict_ranks(args, steps=None, warmup=None):
             f = sens[f"random_hash_max_share_{q}"] / sens["trace_map_max_share"]
             out[f"implied_efficiency_random_hash_{q}"] = round(single / (head_ms * f), 4)
     out["note"] = ("weak scaling: every rank decides its shard of one node-wide trace (N x 2^27 events); the node "
-                   "step is the slowest rank's; implied efficiency = single-GPU step / head-rank step")
+                   "step is the slowest rank's; implied efficiency = single-GPU step / slowest timed rank's step "
+                   "(the ranks timed: most events, the owners of the busiest serial chains, the lightest)")
     print(json.dumps(out), flush=True)
 
 

@@ -2740,33 +2740,55 @@ __global__ void __launch_bounds__(PK_T) k_pk_expand(PkIn in, const uint2* tile_b
 }
 
 // Sparse copy back of a packed batch's verdicts (sf_sparse_verdicts): the
-// nonzero waits and rule indices as (index << 32 | value), appended with one
-// atomic per wavefront and list (any order).  counts[0], counts[1]: lengths.
-__global__ void k_sparse_verdicts(const int32_t* wait, const uint16_t* rule, uint32_t n, unsigned long long* wl,
-                                  unsigned long long* rl, uint32_t* counts) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int32_t w = i < n ? wait[i] : 0;
-    const uint16_t r = i < n ? rule[i] : (uint16_t)0;
-    const int lane = (int)(threadIdx.x & 63);
-    const unsigned long long mw = __ballot(w != 0), mr = __ballot(r != 0);
-    const unsigned long long below = (1ull << lane) - 1ull;
-    if (mw) {
-        uint32_t b0 = 0;
-        if (lane == __ffsll((long long)mw) - 1) b0 = atomicAdd(&counts[0], (uint32_t)__popcll(mw));
-        b0 = __shfl(b0, __ffsll((long long)mw) - 1);
-        if (w != 0) wl[b0 + __popcll(mw & below)] = ((unsigned long long)i << 32) | (uint32_t)w;
+// nonzero waits and rule indices as (index << 32 | value), any order.
+// counts[0], counts[1]: lengths.  One workgroup per SV_TILE events and one
+// atomic per workgroup and list: a counter bumped once per wavefront (2M
+// atomics on one address per 2^27 events) serialised the kernel to 13-17 ms
+// beside the next batch (profiles/r06_e2e_trace.txt).  Each thread keeps its
+// SV_PT values in registers between the count and the write.
+constexpr int SV_T = 256, SV_PT = 16;
+constexpr uint32_t SV_TILE = SV_T * SV_PT;
+__global__ void __launch_bounds__(SV_T) k_sparse_verdicts(const int32_t* wait, const uint16_t* rule, uint32_t n,
+                                                          unsigned long long* wl, unsigned long long* rl,
+                                                          uint32_t* counts) {
+    __shared__ uint32_t wsum[2][SV_T / 64];
+    __shared__ uint32_t base[2];
+    const uint32_t t0 = blockIdx.x * SV_TILE;
+    const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    int32_t w[SV_PT];
+    uint16_t r[SV_PT];
+    uint32_t cw = 0, cr = 0;
+#pragma unroll
+    for (int k = 0; k < SV_PT; k++) {
+        const uint32_t i = t0 + (uint32_t)k * SV_T + threadIdx.x;
+        w[k] = i < n ? wait[i] : 0;
+        r[k] = i < n ? rule[i] : (uint16_t)0;
+        cw += w[k] != 0;
+        cr += r[k] != 0;
     }
-    if (mr) {
-        uint32_t b0 = 0;
-        if (lane == __ffsll((long long)mr) - 1) b0 = atomicAdd(&counts[1], (uint32_t)__popcll(mr));
-        b0 = __shfl(b0, __ffsll((long long)mr) - 1);
-        if (r != 0) rl[b0 + __popcll(mr & below)] = ((unsigned long long)i << 32) | r;
+    const uint32_t sw = (uint32_t)wave_scan_add((int)cw), sr = (uint32_t)wave_scan_add((int)cr);
+    if (lane == 63) { wsum[0][wave] = sw; wsum[1][wave] = sr; }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        uint32_t tot = 0;
+        for (int k = 0; k < SV_T / 64; k++) tot += wsum[threadIdx.x][k];
+        base[threadIdx.x] = tot ? atomicAdd(&counts[threadIdx.x], tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t ow = base[0] + sw - cw, orr = base[1] + sr - cr;
+    for (int k = 0; k < wave; k++) { ow += wsum[0][k]; orr += wsum[1][k]; }
+#pragma unroll
+    for (int k = 0; k < SV_PT; k++) {
+        const unsigned long long i = t0 + (uint32_t)k * SV_T + threadIdx.x;
+        if (w[k] != 0) wl[ow++] = (i << 32) | (uint32_t)w[k];
+        if (r[k] != 0) rl[orr++] = (i << 32) | r[k];
     }
 }
 hipError_t launch_sparse_verdicts(const int32_t* wait, const uint16_t* rule, uint32_t n, unsigned long long* wl,
                                   unsigned long long* rl, uint32_t* counts, hipStream_t s) {
     hipMemsetAsync(counts, 0, 8, s);
-    if (n) hipLaunchKernelGGL(k_sparse_verdicts, dim3((n + 255) / 256), dim3(256), 0, s, wait, rule, n, wl, rl, counts);
+    if (n) hipLaunchKernelGGL(k_sparse_verdicts, dim3((n + SV_TILE - 1) / SV_TILE), dim3(SV_T), 0, s, wait, rule, n,
+                              wl, rl, counts);
     return hipGetLastError();
 }
 
