@@ -50,6 +50,13 @@ struct sf_engine {
     sf_config cfg{};
     hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr, stream4 = nullptr;   // 4: the wave walk
     hipStream_t sstream = nullptr;  // sort phase of the next batch (overlaps the decide phase on `stream`)
+    // ENTRY_NODE's update of an asynchronous batch (after its verdicts, beside
+    // the next batch's decide phase: decisions read ENTRY_NODE only with
+    // SystemRules, whose batches are synchronous); ev_en: the last one enqueued,
+    // en_async: `stream` is not yet ordered after it (en_fence)
+    hipStream_t enstream = nullptr;
+    hipEvent_t ev_en = nullptr;
+    bool en_async = false;
     bool serial = false;            // diagnostics (SF_SERIAL_STREAMS=1): every kernel on one stream
     uint32_t R = 0, key_bits = 1;
     DevState st{};
@@ -260,6 +267,8 @@ void sf_destroy(sf_engine* e) {
     if (e->stream3) hipStreamDestroy(e->stream3);
     if (e->stream4) hipStreamDestroy(e->stream4);
     if (e->sstream) hipStreamDestroy(e->sstream);
+    if (e->enstream) hipStreamDestroy(e->enstream);
+    if (e->ev_en) hipEventDestroy(e->ev_en);
     delete e;
 }
 
@@ -378,6 +387,8 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
         else HIP_TRY(hipStreamCreateWithFlags(&e->sstream, hipStreamNonBlocking));
     }
     if (const char* v = getenv("SF_SERIAL_STREAMS")) e->serial = v[0] == '1';
+    HIP_TRY(hipStreamCreateWithFlags(&e->enstream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&e->ev_en, hipEventDisableTiming));
     for (auto& a : e->evs) for (auto& x : a) HIP_TRY(hipEventCreate(&x));
     for (int k = 0; k < 2; k++) {
         HIP_TRY(hipEventCreateWithFlags(&e->ev_sorted[k], hipEventDisableTiming));
@@ -483,7 +494,21 @@ static int sparse_complete(sf_engine::PkStage& pk);
 // the first error flag raised by any of them.  An async packed batch whose
 // verdicts the caller has not collected keeps its error for its own
 // sf_sync_packed, unless `all` (sf_sync: every batch collected here).
+// order `stream` after the last asynchronous ENTRY_NODE update (every host
+// call that reads or writes ENTRY_NODE on `stream` does this first)
+static bool en_on_main() {            // diagnostics (SF_EN_MAIN=1): ENTRY_NODE on `stream` as before round 6
+    static const bool v = getenv("SF_EN_MAIN") && getenv("SF_EN_MAIN")[0] == '1';
+    return v;
+}
+static int en_fence(sf_engine* e) {
+    if (!e->en_async) return SF_OK;
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_en, 0));
+    e->en_async = false;
+    return SF_OK;
+}
+
 static int drain(sf_engine* e, bool all = false) {
+    if (e->en_async) { HIP_TRY(hipStreamSynchronize(e->enstream)); e->en_async = false; }
     if (!e->pending) return SF_OK;
     HIP_TRY(hipStreamSynchronize(e->sstream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1133,6 +1158,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         }
         HIP_TRY(hipEventRecord(e->ev_sorted[slot], ss));
         HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
+        { const int rc = en_fence(e); if (rc) return rc; }
         DevState stl = e->st;
         stl.err = w.err;
         uint32_t p = 0, rounds = 0;
@@ -1204,12 +1230,25 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     if (with_ox) w.ox_dirty = false;                                  // k_ox_reset enqueued
     // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream
     // order); under the round protocol the node-wide stream updates it (sf_entry_node_add)
-    if (!forced) {
-        le = launch_entry_node(stl, b, dv.status, e->en, e->en_acc, s);
+    if (!forced && async && !e->serial && !en_on_main()) {
+        // asynchronous: on the ENTRY_NODE stream, after the verdicts; the Work set
+        // (and the caller's batch, which k_entry_acc reads) is free after it
+        HIP_TRY(hipEventRecord(e->ev_core[slot], s));
+        HIP_TRY(hipStreamWaitEvent(e->enstream, e->ev_core[slot], 0));
+        le = launch_entry_node(stl, b, dv.status, e->en, e->en_acc, e->enstream);
         if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
+        HIP_TRY(hipEventRecord(e->ev_done[slot], e->enstream));
+        HIP_TRY(hipEventRecord(e->ev_en, e->enstream));
+        e->en_async = true;
+    } else {
+        if (!forced) {
+            { const int rc = en_fence(e); if (rc) return rc; }
+            le = launch_entry_node(stl, b, dv.status, e->en, e->en_acc, s);
+            if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
+        }
+        HIP_TRY(hipEventRecord(e->ev_core[slot], s));
+        HIP_TRY(hipEventRecord(e->ev_done[slot], s));
     }
-    HIP_TRY(hipEventRecord(e->ev_core[slot], s));
-    HIP_TRY(hipEventRecord(e->ev_done[slot], s));
     e->used[slot] = true;
     e->timed[slot] = e->timing;
     e->last = slot;
@@ -1880,6 +1919,7 @@ int sf_read_context_node(sf_engine* e, uint32_t context, uint32_t resource, sf_n
 int sf_read_entry_node(sf_engine* e, sf_node_state* out) {
     if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = en_fence(e); if (rc) return rc; }
     EntryNode en;
     HIP_TRY(hipMemcpyAsync(&en, e->en, sizeof en, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -1938,6 +1978,7 @@ int sf_read_rule_states(sf_engine* e, uint32_t first, uint32_t n, sf_rule_state*
 int sf_snapshot(sf_engine* e, int64_t now_ms, sf_metric_row* out, uint32_t cap, uint32_t* n_out) {
     if (!e || !n_out || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = en_fence(e); if (rc) return rc; }
     *n_out = 0;
     hipStream_t s = e->stream;
     if (!e->snap_counts) {
@@ -2052,6 +2093,7 @@ int sf_metric_log(sf_engine* e, int64_t now_ms, int64_t tz_offset_ms, int includ
                   uint64_t cap, uint64_t* len_out, uint32_t* n_lines) {
     if (!e || !len_out || (cap && !out)) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = en_fence(e); if (rc) return rc; }
     *len_out = 0;
     if (n_lines) *n_lines = 0;
     int rc = ml_reserve(e, 0);
@@ -2554,6 +2596,7 @@ int sf_comm_init(sf_engine* e, int nranks, int rank, const uint8_t* id, size_t l
 int sf_set_report_entry_node(sf_engine* e, const sf_node_state* node) {
     if (!e) return fail(SF_ERR_INVALID, "null engine");
     std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = en_fence(e); if (rc) return rc; }
     if (!node) { e->report_set = false; return SF_OK; }
     EntryNode& r = e->report;
     r = EntryNode{};
@@ -2569,6 +2612,7 @@ int sf_set_report_entry_node(sf_engine* e, const sf_node_state* node) {
 int sf_entry_node_allreduce(sf_engine* e, sf_node_state* out) {
     if (!e || !out) return fail(SF_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
+    { const int rc = en_fence(e); if (rc) return rc; }
     if (!e->comm) return fail(SF_ERR_INVALID, "sf_comm_init first");
     const int S = e->cfg.sample_count, nb = S + MINUTE;
     hipStream_t s = e->stream;
