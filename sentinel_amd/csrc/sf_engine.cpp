@@ -55,6 +55,8 @@ struct sf_engine {
     // SystemRules, whose batches are synchronous); ev_en: the last one enqueued,
     // en_async: `stream` is not yet ordered after it (en_fence)
     hipStream_t enstream = nullptr;
+    bool en_own = false;            // enstream is a stream of its own (else one of the decide streams)
+    int side_mode = 3;
     hipEvent_t ev_en = nullptr;
     bool en_async = false;
     bool serial = false;            // diagnostics (SF_SERIAL_STREAMS=1): every kernel on one stream
@@ -267,7 +269,7 @@ void sf_destroy(sf_engine* e) {
     if (e->stream3) hipStreamDestroy(e->stream3);
     if (e->stream4) hipStreamDestroy(e->stream4);
     if (e->sstream) hipStreamDestroy(e->sstream);
-    if (e->enstream) hipStreamDestroy(e->enstream);
+    if (e->enstream && e->en_own) hipStreamDestroy(e->enstream);
     if (e->ev_en) hipEventDestroy(e->ev_en);
     delete e;
 }
@@ -387,7 +389,20 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
         else HIP_TRY(hipStreamCreateWithFlags(&e->sstream, hipStreamNonBlocking));
     }
     if (const char* v = getenv("SF_SERIAL_STREAMS")) e->serial = v[0] == '1';
-    HIP_TRY(hipStreamCreateWithFlags(&e->enstream, hipStreamNonBlocking));
+    {   // the side stream of asynchronous batches: stream C, whose light lanes end
+        // first (diagnostics SF_SIDE: 0 none -- on `stream` as before round 6 --,
+        // 1 a stream of its own, 2 stream B, 3 stream C).  Same-box means of the
+        // driver's step (tools/gpu_var.sh, 3-4 runs each): 13.32 / 13.65 / 13.24 /
+        // 13.15 ms; a stream of its own is slower even with GPU_MAX_HW_QUEUES=8.
+        const char* v = getenv("SF_SIDE");
+        e->side_mode = v ? v[0] - '0' : 3;
+        if (e->side_mode == 1) {
+            HIP_TRY(hipStreamCreateWithFlags(&e->enstream, hipStreamNonBlocking));
+            e->en_own = true;
+        } else if (e->side_mode == 2) e->enstream = e->stream2;
+        else if (e->side_mode == 3) e->enstream = e->stream3;
+        else e->side_mode = 0;
+    }
     HIP_TRY(hipEventCreateWithFlags(&e->ev_en, hipEventDisableTiming));
     for (auto& a : e->evs) for (auto& x : a) HIP_TRY(hipEventCreate(&x));
     for (int k = 0; k < 2; k++) {
@@ -496,10 +511,6 @@ static int sparse_complete(sf_engine::PkStage& pk);
 // sf_sync_packed, unless `all` (sf_sync: every batch collected here).
 // order `stream` after the last asynchronous ENTRY_NODE update (every host
 // call that reads or writes ENTRY_NODE on `stream` does this first)
-static bool en_on_main() {            // diagnostics (SF_EN_MAIN=1): ENTRY_NODE on `stream` as before round 6
-    static const bool v = getenv("SF_EN_MAIN") && getenv("SF_EN_MAIN")[0] == '1';
-    return v;
-}
 static int en_fence(sf_engine* e) {
     if (!e->en_async) return SF_OK;
     HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_en, 0));
@@ -1223,18 +1234,20 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     HIP_TRY(hipEventRecord(e->ev_sorted[slot], ss));
     // decide phase in batch order on the main streams
     HIP_TRY(hipStreamWaitEvent(s, e->ev_sorted[slot], 0));
+    // an asynchronous batch's verdict scatter and ENTRY_NODE update run on the
+    // ENTRY_NODE stream, beside the next batch's decide phase
+    const bool side = !forced && async && !e->serial && e->side_mode != 0;
     le = launch_decide(stl, w, b, dv, s, e->serial ? s : e->stream2, e->serial ? s : e->stream3,
                        e->serial ? s : e->stream4, e->evs[slot], e->timing,
-                       with_ox ? &plan : nullptr);
+                       with_ox ? &plan : nullptr, false, side ? e->enstream : nullptr);
     if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("launch: ") + hipGetErrorString(le));
     if (with_ox) w.ox_dirty = false;                                  // k_ox_reset enqueued
     // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream
     // order); under the round protocol the node-wide stream updates it (sf_entry_node_add)
-    if (!forced && async && !e->serial && !en_on_main()) {
-        // asynchronous: on the ENTRY_NODE stream, after the verdicts; the Work set
+    if (side) {
+        // asynchronous: on the ENTRY_NODE stream after the scatter; the Work set
         // (and the caller's batch, which k_entry_acc reads) is free after it
-        HIP_TRY(hipEventRecord(e->ev_core[slot], s));
-        HIP_TRY(hipStreamWaitEvent(e->enstream, e->ev_core[slot], 0));
+        HIP_TRY(hipEventRecord(e->ev_core[slot], e->enstream));
         le = launch_entry_node(stl, b, dv.status, e->en, e->en_acc, e->enstream);
         if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
         HIP_TRY(hipEventRecord(e->ev_done[slot], e->enstream));

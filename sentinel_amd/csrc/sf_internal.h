@@ -366,7 +366,7 @@ struct OxWin { int64_t w0s, w0m; uint32_t ws, wm; };    // the batch's first sec
 struct OxPlan { uint32_t n_heavy, n_pairs; OxWin win; };   // the batch's origin-node pass (sf_origin.hip)
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                          hipStream_t s, hipStream_t s2, hipStream_t s3, hipStream_t s4, hipEvent_t* ev, bool timing,
-                         const OxPlan* ox = nullptr, bool classify = false);
+                         const OxPlan* ox = nullptr, bool classify = false, hipStream_t sv = nullptr);
 // sf_packed_batch -> SoA (sf_kernels.hip); tile_cnt: [n / 4096 + 1] uint2
 hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64_t* xcts, const int32_t* cext,
                             int64_t base, uint32_t n, uint32_t n_exit, uint32_t n_cext, uint2* tile_cnt,
@@ -387,6 +387,6 @@ constexpr size_t ACC_BYTES = 72;                         // sizeof(Acc)
 // 5 fork, 6 join (stream B), 7 heavy decided, 8 heavy filled, 9 light decided, 10 before classify,
 // 11 stream start (stream C), 12 stream done (stream C), 13 stream fill + apply done (stream C),
 // 14 origin-node pass done (stream B)
-constexpr int SF_NUM_EVENTS = 17;
+constexpr int SF_NUM_EVENTS = 18;
 
 }  // namespace sf

@@ -2518,7 +2518,7 @@ static void launch_light(const DevState& st, const SegIO& io, const Work& w, con
 // then the verdicts are scattered back to submission order.
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                          hipStream_t s, hipStream_t s2, hipStream_t s3, hipStream_t s4, hipEvent_t* ev, bool timing,
-                         const OxPlan* ox, bool classify) {
+                         const OxPlan* ox, bool classify, hipStream_t sv) {
     const uint32_t n = b.n;
     if (n == 0) return hipSuccess;
     if (classify) launch_classify(st, w, b, s, ev, timing);
@@ -2640,9 +2640,19 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
         if (e != hipSuccess) return e;
         hipEventRecord(ev[14], s2);
     }
-    launch_scatter(w, n, out.status, s);
-    if (ox) hipStreamWaitEvent(s, ev[14], 0);
-    if (timing) hipEventRecord(ev[4], s);
+    // the verdict scatter on sv when given (an asynchronous batch: beside the
+    // next batch's decide phase, which reads no status of this one)
+    hipStream_t vs = sv ? sv : s;
+    if (vs != s) {
+        hipEventRecord(ev[17], s);
+        hipStreamWaitEvent(vs, ev[17], 0);
+    }
+    launch_scatter(w, n, out.status, vs);
+    if (ox) {
+        hipStreamWaitEvent(s, ev[14], 0);          // the next batch reads the origin nodes
+        if (vs != s) hipStreamWaitEvent(vs, ev[14], 0);
+    }
+    if (timing) hipEventRecord(ev[4], vs);
     return hipGetLastError();
 }
 
