@@ -1077,6 +1077,19 @@ def config5_leg(n_req=1 << 22, n_streams=500, steps=3):
 
 
 def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
+    """Both compact forms: the narrow 4-byte words (resource ids below 2^24,
+    the time as a per-millisecond table; the line's numbers) and the 8-byte
+    words the Java shim sends (its numbers under form_8byte)."""
+    narrow = int(hb.res_id.max()) < (1 << 24)
+    out = e2e_form(hb, rules, R, steps, g0, glast, timed, narrow=narrow)
+    if narrow:
+        w = e2e_form(hb, rules, R, steps, g0, glast, timed, narrow=False)
+        out["form_8byte"] = {k: w[k] for k in ("ms_per_batch", "decisions_per_s", "latency_ms", "period_ms",
+                                               "h2d_bytes", "h2d_alone_ms", "period_over_h2d", "parity")}
+    return out
+
+
+def e2e_form(hb, rules, R, steps, g0, glast, timed=None, narrow=False):
     """Config 3 end to end from page-locked host memory: the headline run's
     batches (the same trace, shifted by DURATION_MS per step) submitted from
     host buffers in the compact form (sf_submit_packed_async: 8 bytes per event
@@ -1091,8 +1104,8 @@ def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
     try:
         e.load_flow_rules(rules)
         t0 = time.perf_counter()
-        pb = abi.PackedBatch(hb, alloc=pin.array)
-        log(f"[leg e2e_pinned] packed {hb.n} events into {pb.nbytes() / 1e9:.2f} GB in {time.perf_counter() - t0:.1f}s")
+        pb = abi.PackedBatch(hb, alloc=pin.array, narrow=narrow)
+        log(f"[leg e2e_pinned] {'narrow ' if narrow else ''}packed {hb.n} events into {pb.nbytes() / 1e9:.2f} GB in {time.perf_counter() - t0:.1f}s")
         # sparse copy back (sf_submit_packed_sparse_async): 1 status byte per event plus
         # the nonzero waits / rule indices, n/64 entries of each list prefetched with it
         # (config 3 queues 1.3 % of its events; a longer list is completed at the sync)
@@ -1125,7 +1138,8 @@ def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
         ent = int(((hb.flags & abi.EV_EXIT) == 0).sum())
         # the H2D-bound time: the packed arrays copied alone (pinned -> HBM, synchronous)
         import ctypes as C
-        arrs = [a for a in (pb.ev, pb.exit_ref, pb.exit_cts, pb.count_ext, pb.origin) if a is not None and a.nbytes]
+        arrs = [a for a in (pb.ev, pb.ev4, pb.ms_end, pb.exit_ref, pb.exit_cts, pb.count_ext, pb.origin)
+                if a is not None and a.nbytes]
         dptr = C.c_void_p()
         engine._check(engine.lib().sf_device_alloc(e.h, max(a.nbytes for a in arrs), C.byref(dptr)))
         h2d = []
@@ -1144,6 +1158,7 @@ def e2e_leg(hb, rules, R, steps, g0, glast, timed=None):
         d2h = int(hb.n + 8 + 2 * 8 * pre + 8 * sum(max(0, c - pre) for c in lists))
         return {"what": "config3 batches from pinned host buffers in the compact form (sf_submit_packed_sparse_async: "
                         "H2D of batch k+1, decide of k and the sparse D2H of k-1 overlapped)",
+                "form": "narrow: 4 B per event + per-ms time table" if narrow else "8 B per event",
                 "events": int(hb.n), "ms_per_batch": round(ms, 3), "decisions_per_s": round(ent / (ms / 1e3), 1),
                 "latency_ms": round(lat * 1e3, 3), "period_ms": round(period, 3),
                 "period_note": "ms_per_batch includes the drain of the last batch; period_ms = (timed wall - one "

@@ -435,9 +435,23 @@ int  sf_submit_async(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
  * exit_ref / exit_cts hold, for the EXIT events in batch order, what
  * entry_ref / create_ts hold for them in sf_event_batch (create_ts read where
  * exit_ref < 0; NULL: 0).  origin (per event) as in sf_event_batch.
- * The verdicts are sf_verdicts in the same memory kind as the batch.        */
+ * The verdicts are sf_verdicts in the same memory kind as the batch.
+ *
+ * The narrow form (4 bytes per event; ev NULL, ev4 set) for resource ids below
+ * 2^24: the time leaves the word for a table of the batch's milliseconds,
+ *   ev4 bits  0..23  resource id
+ *       bits 24..26  acquireCount 1..7; 0: the next value of count_ext
+ *       bits 27..31  flags
+ *   ms_end[m] = the number of events with ts_ms - ts_base <= m (m < n_ms,
+ *   non-decreasing, ms_end[n_ms - 1] == n; else SF_ERR_INVALID at sync), so
+ *   event i is at ts_base + the first m with ms_end[m] > i.  n_ms <= 2^20.
+ * A config-3 batch (2^27 events over 4 s) crosses PCIe in 0.63 GB instead of
+ * 1.16 GB.                                                                 */
 #define SF_PK_COUNT_SHIFT 52
 #define SF_PK_FLAGS_SHIFT 59
+#define SF_PK4_COUNT_SHIFT 24
+#define SF_PK4_FLAGS_SHIFT 27
+#define SF_PK4_MAX_MS (1u << 20)
 typedef struct sf_packed_batch {
     uint32_t        n;
     int32_t         mem;          /* SF_MEM_HOST or SF_MEM_DEVICE (all arrays)  */
@@ -449,6 +463,10 @@ typedef struct sf_packed_batch {
     const uint32_t* origin;       /* [n] or NULL                                */
     uint32_t        n_exit;
     uint32_t        n_count_ext;
+    const uint32_t* ev4;          /* [n]: the narrow form (ev NULL), or NULL    */
+    const uint32_t* ms_end;       /* [n_ms]: the narrow form's time table       */
+    uint32_t        n_ms;
+    uint32_t        pad0;
 } sf_packed_batch;
 int  sf_submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* out);
 /* Enqueued only; sf_sync waits and reports the first error.  Host arrays

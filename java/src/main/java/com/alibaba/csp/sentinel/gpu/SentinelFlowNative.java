@@ -128,12 +128,15 @@ final class SentinelFlowNative {
             JAVA_INT.withName("n_elems"), MemoryLayout.paddingLayout(4),
             ADDRESS.withName("origin"), ADDRESS.withName("context"));
 
-    /** sf_packed_batch: 8 bytes per event (res | ts - ts_base << 32 | count << 52 | flags << 59). */
+    /** sf_packed_batch: 8 bytes per event (res | ts - ts_base << 32 | count << 52 | flags << 59); the
+     *  narrow form's fields (ev4, ms_end, n_ms) stay NULL / 0 here: EventBatcher sends the 8-byte form. */
     static final StructLayout PACKED_BATCH = MemoryLayout.structLayout(
             JAVA_INT.withName("n"), JAVA_INT.withName("mem"), JAVA_LONG.withName("ts_base"),
             ADDRESS.withName("ev"), ADDRESS.withName("exit_ref"), ADDRESS.withName("exit_cts"),
             ADDRESS.withName("count_ext"), ADDRESS.withName("origin"),
-            JAVA_INT.withName("n_exit"), JAVA_INT.withName("n_count_ext"));
+            JAVA_INT.withName("n_exit"), JAVA_INT.withName("n_count_ext"),
+            ADDRESS.withName("ev4"), ADDRESS.withName("ms_end"), JAVA_INT.withName("n_ms"),
+            JAVA_INT.withName("pad0"));
     static final int PK_COUNT_SHIFT = 52, PK_FLAGS_SHIFT = 59;
 
     /** sf_verdicts. */

@@ -267,12 +267,14 @@ def _ptr(a):
 
 
 PK_COUNT_SHIFT, PK_FLAGS_SHIFT = 52, 59
+PK4_COUNT_SHIFT, PK4_FLAGS_SHIFT = 24, 27
 
 
 class sf_packed_batch(C.Structure):
     _fields_ = [("n", C.c_uint32), ("mem", C.c_int32), ("ts_base", C.c_int64), ("ev", C.c_void_p),
                 ("exit_ref", C.c_void_p), ("exit_cts", C.c_void_p), ("count_ext", C.c_void_p),
-                ("origin", C.c_void_p), ("n_exit", C.c_uint32), ("n_count_ext", C.c_uint32)]
+                ("origin", C.c_void_p), ("n_exit", C.c_uint32), ("n_count_ext", C.c_uint32),
+                ("ev4", C.c_void_p), ("ms_end", C.c_void_p), ("n_ms", C.c_uint32), ("pad0", C.c_uint32)]
 
 
 STRUCT_SIZES["sf_packed_batch"] = C.sizeof(sf_packed_batch)
@@ -285,7 +287,10 @@ class PackedBatch:
     sparse arrays).  ``alloc`` places the arrays (np.empty by default; a
     PinnedArrays.array for page-locked memory)."""
 
-    def __init__(self, hb: "HostBatch", alloc=None):
+    def __init__(self, hb: "HostBatch", alloc=None, narrow=False):
+        """narrow: the 4-byte form (resource ids below 2^24; acquireCounts 1..7
+        inline, the time as the per-millisecond table ms_end); "auto" picks it
+        when the resource ids fit."""
         alloc = alloc or (lambda shape, dtype: np.empty(shape, dtype))
         n = hb.n
         self.n = n
@@ -294,13 +299,32 @@ class PackedBatch:
         if n and (d.min() < 0 or d.max() >= (1 << 20)):
             # the 20-bit delta would spill into the acquireCount bits (sf_packed_batch)
             raise ValueError("a packed batch must be time-ordered and span less than 2^20 ms")
+        if narrow == "auto":
+            narrow = n > 0 and int(hb.res_id.max()) < (1 << 24)
+        if narrow and n and int(hb.res_id.max()) >= (1 << 24):
+            raise ValueError("the narrow packed form takes resource ids below 2^24")
+        self.narrow = bool(narrow)
+        if self.narrow and n and (np.diff(d) < 0).any():
+            raise ValueError("the narrow packed form takes a time-ordered batch")
         c = hb.count.astype(np.int64)
-        small = (c >= 1) & (c <= 127)
-        w = hb.res_id.astype(np.uint64) | (d.astype(np.uint64) << np.uint64(32)) | \
-            (np.where(small, c, 0).astype(np.uint64) << np.uint64(PK_COUNT_SHIFT)) | \
-            ((hb.flags.astype(np.uint64) & np.uint64(0x1f)) << np.uint64(PK_FLAGS_SHIFT))
-        self.ev = alloc((n,), np.uint64)
-        self.ev[...] = w
+        self.ev = self.ev4 = self.ms_end = None
+        self.n_ms = 0
+        if self.narrow:
+            small = (c >= 1) & (c <= 7)
+            w = hb.res_id.astype(np.uint32) | (np.where(small, c, 0).astype(np.uint32) << np.uint32(PK4_COUNT_SHIFT)) | \
+                ((hb.flags.astype(np.uint32) & np.uint32(0x1f)) << np.uint32(PK4_FLAGS_SHIFT))
+            self.ev4 = alloc((n,), np.uint32)
+            self.ev4[...] = w
+            self.n_ms = int(d[-1]) + 1 if n else 1
+            self.ms_end = alloc((self.n_ms,), np.uint32)
+            self.ms_end[...] = np.cumsum(np.bincount(d, minlength=self.n_ms)).astype(np.uint32)
+        else:
+            small = (c >= 1) & (c <= 127)
+            w = hb.res_id.astype(np.uint64) | (d.astype(np.uint64) << np.uint64(32)) | \
+                (np.where(small, c, 0).astype(np.uint64) << np.uint64(PK_COUNT_SHIFT)) | \
+                ((hb.flags.astype(np.uint64) & np.uint64(0x1f)) << np.uint64(PK_FLAGS_SHIFT))
+            self.ev = alloc((n,), np.uint64)
+            self.ev[...] = w
         ex = np.nonzero(hb.flags & EV_EXIT)[0]
         self.n_exit = int(ex.size)
         self.exit_ref = self.exit_cts = None
@@ -322,8 +346,8 @@ class PackedBatch:
             self.origin[...] = hb.origin
 
     def nbytes(self) -> int:
-        return sum(a.nbytes for a in (self.ev, self.exit_ref, self.exit_cts, self.count_ext, self.origin)
-                   if a is not None)
+        return sum(a.nbytes for a in (self.ev, self.ev4, self.ms_end, self.exit_ref, self.exit_cts, self.count_ext,
+                                      self.origin) if a is not None)
 
     def c_struct(self) -> sf_packed_batch:
         b = sf_packed_batch()
@@ -331,6 +355,7 @@ class PackedBatch:
         b.ev, b.exit_ref, b.exit_cts = _ptr(self.ev), _ptr(self.exit_ref), _ptr(self.exit_cts)
         b.count_ext, b.origin = _ptr(self.count_ext), _ptr(self.origin)
         b.n_exit, b.n_count_ext = self.n_exit, self.n_count_ext
+        b.ev4, b.ms_end, b.n_ms = _ptr(self.ev4), _ptr(self.ms_end), self.n_ms
         return b
 
 

@@ -1321,8 +1321,11 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     if (!e || !in || !out || !out->status) return fail(SF_ERR_INVALID, "null argument");
     if (sp && (!sp->waits || !sp->rules || !sp->counts)) return fail(SF_ERR_INVALID, "null sparse list");
     if (in->n == 0) return SF_OK;
-    if (!in->ev || (in->n_exit && !in->exit_ref) || (in->n_count_ext && !in->count_ext))
+    const bool narrow = !in->ev && in->ev4;
+    if ((!in->ev && !narrow) || (in->n_exit && !in->exit_ref) || (in->n_count_ext && !in->count_ext) ||
+        (narrow && (!in->ms_end || in->n_ms == 0)))
         return fail(SF_ERR_INVALID, "missing packed arrays");
+    if (narrow && in->n_ms > SF_PK4_MAX_MS) return fail(SF_ERR_INVALID, "narrow packed batch spans more than 2^20 ms");
     if (in->n > e->cfg.max_batch) return fail(SF_ERR_CAPACITY, "batch larger than max_batch");
     std::lock_guard<std::mutex> lk(e->mu);
     const uint32_t n = in->n;
@@ -1359,6 +1362,7 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     const size_t o_ct = take(N * 8), o_tc = take((N / 4096 + 2) * 8);
     const size_t o_st = take(N), o_wt = take(N * 4), o_ru = take(N * 2);
     const size_t o_wl = sp ? take(N * 8) : 0, o_rl = sp ? take(N * 8) : 0, o_sc = sp ? take(16) : 0;
+    const size_t o_ms = narrow ? take((size_t)SF_PK4_MAX_MS * 4) : 0;   // (the narrow words use o_ev's room)
     if (pk.bytes < off) {
         if (e->used[slot]) HIP_TRY(hipEventSynchronize(e->ev_done[slot]));
         if (pk.consumed_pending) { HIP_TRY(hipEventSynchronize(pk.consumed)); pk.consumed_pending = false; }
@@ -1371,12 +1375,21 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     char* B = pk.buf;
     hipStream_t ss = e->serial ? e->stream : e->sstream;
     const uint64_t* ev = in->ev; const int64_t* xr = in->exit_ref; const int64_t* xc = in->exit_cts;
+    const uint32_t* ev4 = narrow ? in->ev4 : nullptr; const uint32_t* mse = narrow ? in->ms_end : nullptr;
+    const uint32_t n_ms = narrow ? in->n_ms : 0;
     const int32_t* ce = in->count_ext; const uint32_t* og = in->origin;
     if (host_in) {
         hipStream_t h = e->serial ? e->stream : e->h2d;
         if (pk.consumed_pending) HIP_TRY(hipStreamWaitEvent(h, pk.consumed, 0));
-        HIP_TRY(hipMemcpyAsync(B + o_ev, in->ev, (size_t)n * 8, hipMemcpyHostToDevice, h));
-        ev = (const uint64_t*)(B + o_ev);
+        if (narrow) {
+            HIP_TRY(hipMemcpyAsync(B + o_ev, in->ev4, (size_t)n * 4, hipMemcpyHostToDevice, h));
+            HIP_TRY(hipMemcpyAsync(B + o_ms, in->ms_end, (size_t)n_ms * 4, hipMemcpyHostToDevice, h));
+            ev4 = (const uint32_t*)(B + o_ev);
+            mse = (const uint32_t*)(B + o_ms);
+        } else {
+            HIP_TRY(hipMemcpyAsync(B + o_ev, in->ev, (size_t)n * 8, hipMemcpyHostToDevice, h));
+            ev = (const uint64_t*)(B + o_ev);
+        }
         if (in->n_exit) {
             HIP_TRY(hipMemcpyAsync(B + o_xr, in->exit_ref, (size_t)in->n_exit * 8, hipMemcpyHostToDevice, h));
             xr = (const int64_t*)(B + o_xr);
@@ -1401,7 +1414,7 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     const uint32_t n_exit = in->n_exit, n_cext = in->n_count_ext;
     const hipEvent_t consumed = pk.consumed;
     const PreSort expand = [=](hipStream_t st_, int32_t* err) {
-        const hipError_t le = launch_pk_expand(ev, xr, xc, ce, base, n, n_exit, n_cext, (uint2*)(B + o_tc),
+        const hipError_t le = launch_pk_expand(ev, ev4, mse, n_ms, xr, xc, ce, base, n, n_exit, n_cext, (uint2*)(B + o_tc),
                                                (uint32_t*)(B + o_res), (int64_t*)(B + o_ts), (int32_t*)(B + o_cnt),
                                                (uint8_t*)(B + o_fl), (int64_t*)(B + o_er),
                                                exits ? (int64_t*)(B + o_ct) : nullptr, err, st_);

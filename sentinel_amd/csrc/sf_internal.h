@@ -252,11 +252,6 @@ struct Work {
     // (THREAD run mode also borrows buffers dead after the sort: rid = keys_in,
     //  run_start = head_scan, run_pre = keys_out, entry records = pv_in; sf_kernels.hip heavy_ctx)
     uint32_t* vs_cursor;                                // [VS_CURSORS(N)] fill counts of the verdict scatter's buckets
-    // sf_packed_batch -> SoA (sf_kernels.hip); tile_cnt: [n / 4096 + 1] uint2
-hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64_t* xcts, const int32_t* cext,
-                            int64_t base, uint32_t n, uint32_t n_exit, uint32_t n_cext, uint2* tile_cnt,
-                            uint32_t* res, int64_t* ts, int32_t* cnt, uint8_t* flags, int64_t* eref, int64_t* cts,
-                            int32_t* err, hipStream_t s);
 // origin nodes (sf_origin.hip), batches with origins only
     uint32_t* s_origin;                                 // [N] origin id in sorted order
     uint32_t* s_oslot;                                  // [N] pool slot of the event's origin node (XNONE: none)
@@ -367,8 +362,10 @@ struct OxPlan { uint32_t n_heavy, n_pairs; OxWin win; };   // the batch's origin
 hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const DevVerdicts& out,
                          hipStream_t s, hipStream_t s2, hipStream_t s3, hipStream_t s4, hipEvent_t* ev, bool timing,
                          const OxPlan* ox = nullptr, bool classify = false, hipStream_t sv = nullptr);
-// sf_packed_batch -> SoA (sf_kernels.hip); tile_cnt: [n / 4096 + 1] uint2
-hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64_t* xcts, const int32_t* cext,
+// sf_packed_batch -> SoA (sf_kernels.hip); tile_cnt: [n / 4096 + 1] uint2.  ev4 / ms_end /
+// n_ms: the narrow form (ev null)
+hipError_t launch_pk_expand(const uint64_t* ev, const uint32_t* ev4, const uint32_t* ms_end, uint32_t n_ms,
+                            const int64_t* xref, const int64_t* xcts, const int32_t* cext,
                             int64_t base, uint32_t n, uint32_t n_exit, uint32_t n_cext, uint2* tile_cnt,
                             uint32_t* res, int64_t* ts, int32_t* cnt, uint8_t* flags, int64_t* eref, int64_t* cts,
                             int32_t* err, hipStream_t s);

@@ -2663,11 +2663,26 @@ hipError_t launch_decide(const DevState& st, Work& w, const DevBatch& b, const D
 // the tile counts, then each tile's own scan (PK_T threads x PK_PER events).
 constexpr uint32_t PK_T = 256, PK_PER = 16, PK_TILE = PK_T * PK_PER;
 struct PkIn { const uint64_t* ev; const int64_t* xref; const int64_t* xcts; const int32_t* cext; int64_t base;
-              uint32_t n, n_exit, n_cext; };
+              uint32_t n, n_exit, n_cext;
+              const uint32_t* ev4; const uint32_t* ms_end; uint32_t n_ms; };   // the narrow form: ev null
 struct PkOut { uint32_t* res; int64_t* ts; int32_t* cnt; uint8_t* flags; int64_t* eref; int64_t* cts; };
 
 __device__ __forceinline__ uint32_t pk_flags(uint64_t w) { return (uint32_t)(w >> SF_PK_FLAGS_SHIFT) & 0x1fu; }
 __device__ __forceinline__ uint32_t pk_count(uint64_t w) { return (uint32_t)(w >> SF_PK_COUNT_SHIFT) & 0x7fu; }
+// the narrow form's word as the 8-byte one without the time (res, acquireCount, flags)
+__device__ __forceinline__ uint64_t pk_widen(uint32_t w) {
+    return (uint64_t)(w & 0xffffffu) | ((uint64_t)((w >> SF_PK4_COUNT_SHIFT) & 7u) << SF_PK_COUNT_SHIFT) |
+           ((uint64_t)(w >> SF_PK4_FLAGS_SHIFT) << SF_PK_FLAGS_SHIFT);
+}
+__device__ __forceinline__ uint64_t pk_word(const PkIn& in, uint32_t i) {
+    return in.ev4 ? pk_widen(in.ev4[i]) : in.ev[i];
+}
+// first m in [lo, hi) with ms_end[m] > i (hi when none)
+__device__ __forceinline__ uint32_t pk_ms_search(const uint32_t* ms_end, uint32_t lo, uint32_t hi, uint32_t i) {
+    while (lo < hi) { const uint32_t m = lo + (hi - lo) / 2; if (ms_end[m] > i) hi = m; else lo = m + 1; }
+    return lo;
+}
+constexpr uint32_t PK_ME = 1024;   // ms_end entries of a tile staged in LDS (longer spans search HBM)
 
 __global__ void __launch_bounds__(PK_T) k_pk_count(PkIn in, uint2* tile_cnt) {
     __shared__ uint32_t sx, sc;
@@ -2678,7 +2693,7 @@ __global__ void __launch_bounds__(PK_T) k_pk_count(PkIn in, uint2* tile_cnt) {
     for (uint32_t k = 0; k < PK_PER; k++) {
         const uint32_t i = t0 + k * PK_T + threadIdx.x;
         if (i >= in.n) break;
-        const uint64_t w = in.ev[i];
+        const uint64_t w = pk_word(in, i);
         x += (pk_flags(w) & SF_EV_EXIT) ? 1u : 0u;
         c += pk_count(w) == 0 ? 1u : 0u;
     }
@@ -2709,19 +2724,34 @@ __global__ void __launch_bounds__(1024) k_pk_scan(uint2* tile_cnt, uint32_t nt, 
         __syncthreads();
     }
     if (threadIdx.x == 0 && (cx > in.n_exit || cc > in.n_cext)) *err = SF_ERR_INVALID;
+    // the narrow form's time table must cover every event
+    if (threadIdx.x == 0 && in.ev4 && (in.n_ms == 0 || in.ms_end[in.n_ms - 1] != in.n)) *err = SF_ERR_INVALID;
 }
 
 // coalesced: round k of a tile holds events t0 + 256 k + thread, scanned in
 // that (batch) order with a carry from round to round
+// The narrow form's time: event i is at ts_base + the first m with
+// ms_end[m] > i; the tile's first millisecond is searched once, the next
+// PK_ME entries staged in LDS.
 __global__ void __launch_bounds__(PK_T) k_pk_expand(PkIn in, const uint2* tile_base, PkOut out) {
     __shared__ uint32_t wx[PK_T / 64], wc[PK_T / 64];
+    __shared__ uint32_t sme[PK_ME];
+    __shared__ uint32_t s_m0;
     const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
     const uint2 tb = tile_base[blockIdx.x];
     uint32_t cx = tb.x, cc = tb.y;
+    uint32_t m0 = 0;
+    if (in.ev4) {
+        if (threadIdx.x == 0) s_m0 = pk_ms_search(in.ms_end, 0, in.n_ms, blockIdx.x * PK_TILE);
+        __syncthreads();
+        m0 = s_m0;
+        for (uint32_t j = threadIdx.x; j < PK_ME; j += PK_T) sme[j] = m0 + j < in.n_ms ? in.ms_end[m0 + j] : 0xffffffffu;
+        __syncthreads();
+    }
     for (uint32_t k = 0; k < PK_PER; k++) {
         const uint32_t i = blockIdx.x * PK_TILE + k * PK_T + threadIdx.x;
         const bool in_b = i < in.n;
-        const uint64_t w = in_b ? in.ev[i] : 0ull;
+        const uint64_t w = in_b ? pk_word(in, i) : 0ull;
         const uint32_t f = pk_flags(w), c8 = pk_count(w);
         const uint32_t x = (in_b && (f & SF_EV_EXIT)) ? 1u : 0u, c = (in_b && c8 == 0) ? 1u : 0u;
         const uint32_t ix = (uint32_t)wave_scan_add((int)x), ic = (uint32_t)wave_scan_add((int)c);
@@ -2736,7 +2766,19 @@ __global__ void __launch_bounds__(PK_T) k_pk_expand(PkIn in, const uint2* tile_b
         cx += tx; cc += tc;
         if (!in_b) continue;
         out.res[i] = (uint32_t)w;
-        out.ts[i] = in.base + (int64_t)((w >> 32) & 0xfffffu);
+        if (in.ev4) {
+            uint32_t m;
+            if (sme[PK_ME - 1] > i) {
+                uint32_t lo = 0, hi = PK_ME;
+                while (lo < hi) { const uint32_t md = (lo + hi) / 2; if (sme[md] > i) hi = md; else lo = md + 1; }
+                m = m0 + lo;
+            } else {
+                m = pk_ms_search(in.ms_end, m0 + PK_ME, in.n_ms, i);
+            }
+            out.ts[i] = in.base + (int64_t)m;
+        } else {
+            out.ts[i] = in.base + (int64_t)((w >> 32) & 0xfffffu);
+        }
         out.flags[i] = (uint8_t)f;
         out.cnt[i] = c8 ? (int32_t)c8 : (bc < in.n_cext ? in.cext[bc] : 0);
         if (f & SF_EV_EXIT) {
@@ -2802,12 +2844,13 @@ hipError_t launch_sparse_verdicts(const int32_t* wait, const uint16_t* rule, uin
     return hipGetLastError();
 }
 
-hipError_t launch_pk_expand(const uint64_t* ev, const int64_t* xref, const int64_t* xcts, const int32_t* cext,
+hipError_t launch_pk_expand(const uint64_t* ev, const uint32_t* ev4, const uint32_t* ms_end, uint32_t n_ms,
+                            const int64_t* xref, const int64_t* xcts, const int32_t* cext,
                             int64_t base, uint32_t n, uint32_t n_exit, uint32_t n_cext, uint2* tile_cnt,
                             uint32_t* res, int64_t* ts, int32_t* cnt, uint8_t* flags, int64_t* eref, int64_t* cts,
                             int32_t* err, hipStream_t s) {
     if (!n) return hipSuccess;
-    const PkIn in{ev, xref, xcts, cext, base, n, n_exit, n_cext};
+    const PkIn in{ev, xref, xcts, cext, base, n, n_exit, n_cext, ev ? nullptr : ev4, ms_end, n_ms};
     const PkOut out{res, ts, cnt, flags, eref, cts};
     const uint32_t nt = (n + PK_TILE - 1) / PK_TILE;
     hipLaunchKernelGGL(k_pk_count, dim3(nt), dim3(PK_T), 0, s, in, tile_cnt);

@@ -21,6 +21,18 @@ def _unpack(pb: abi.PackedBatch):
     return res, ts, c, fl
 
 
+def _unpack4(pb: abi.PackedBatch):
+    w = pb.ev4
+    res = (w & np.uint32(0xffffff)).astype(np.uint32)
+    ms = np.searchsorted(pb.ms_end, np.arange(pb.n), side="right")     # first m with ms_end[m] > i
+    ts = pb.ts_base + ms.astype(np.int64)
+    c = ((w >> np.uint32(abi.PK4_COUNT_SHIFT)) & np.uint32(7)).astype(np.int32)
+    fl = (w >> np.uint32(abi.PK4_FLAGS_SHIFT)).astype(np.uint8)
+    if pb.n_count_ext:
+        c[c == 0] = pb.count_ext
+    return res, ts, c, fl
+
+
 def _batch(seed=3, R=500, n=40_000):
     hb = trace.mixed_zipf(R, n, duration_ms=3000, seed=seed)
     rng = np.random.default_rng(seed)
@@ -89,6 +101,87 @@ def test_gpu_packed_equals_oracle(mode):
         pin.free()
         eng.close()
         ora.close()
+
+
+def test_narrow_packing_roundtrip():
+    """The 4-byte form: resource (24 bits), acquireCount 1..7 (else
+    count_ext), flags, and the time as the per-millisecond table ms_end."""
+    hb, _ = _batch()
+    pb = abi.PackedBatch(hb, narrow=True)
+    assert pb.ev is None and pb.ev4.dtype == np.uint32 and pb.ms_end[-1] == hb.n
+    res, ts, c, fl = _unpack4(pb)
+    assert np.array_equal(res, hb.res_id) and np.array_equal(ts, hb.ts_ms)
+    assert np.array_equal(c, hb.count) and np.array_equal(fl, hb.flags)
+    assert pb.nbytes() < 0.6 * abi.PackedBatch(hb).nbytes()
+    assert abi.PackedBatch(hb, narrow="auto").narrow
+    big = abi.HostBatch(hb.res_id + np.uint32(1 << 24), hb.ts_ms, hb.count, hb.flags, entry_ref=hb.entry_ref)
+    assert not abi.PackedBatch(big, narrow="auto").narrow
+    with pytest.raises(ValueError):
+        abi.PackedBatch(big, narrow=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["dense", "sparse_time"])
+def test_gpu_narrow_packed_equals_oracle(kind):
+    """The narrow form decided async (double-buffered) equals the oracle:
+    dense traffic (a tile's milliseconds staged in LDS) and traffic so
+    sparse in time that one 4096-event tile spans more than 1024 ms (the
+    table searched in HBM)."""
+    from oracle.oracle import OracleEngine
+    from sentinel_amd import engine
+    from tests import parity
+    if kind == "dense":
+        hb, R = _batch(seed=11, R=700, n=100_000)
+    else:
+        R = 300
+        hb = trace.mixed_zipf(R, 12_000, duration_ms=60_000, seed=12)
+    rules = trace.mixed_rules(R, seed=11)
+    cuts = np.linspace(0, hb.n, 4).astype(int)
+    parts = [hb.subset(int(cuts[k]), int(cuts[k + 1])) for k in range(3)]
+    cfg = abi.default_config(max_resources=R, max_batch=max(p.n for p in parts))
+    eng, ora = engine.FlowEngine(cfg), OracleEngine(cfg)
+    pin = engine.PinnedArrays(eng)
+    try:
+        for x in (eng, ora):
+            x.load_flow_rules(rules)
+        pbs = [abi.PackedBatch(p, alloc=pin.array, narrow=True) for p in parts]
+        if kind == "sparse_time":
+            assert pbs[0].n_ms > 4096
+        outs = [pin.verdicts(p.n) for p in parts]
+        eng.submit_packed_async(pbs[0], outs[0])
+        for k in range(len(parts)):
+            if k + 1 < len(parts):
+                eng.submit_packed_async(pbs[k + 1], outs[k + 1])
+            eng.sync_packed(outs[k])
+            parity.compare_verdicts(outs[k], ora.submit(parts[k]), f"batch {k}")
+        eng.sync()
+        per_res = np.bincount(hb.res_id, minlength=R)
+        parity.compare_nodes(eng, ora, np.argsort(-per_res)[:40])
+        parity.compare_all_nodes(eng, ora, R)
+        parity.compare_entry_node(eng, ora)
+    finally:
+        pin.free()
+        eng.close()
+        ora.close()
+
+
+@pytest.mark.gpu
+def test_gpu_narrow_packed_bad_time_table():
+    """A time table that does not end at n is refused at sync (SF_ERR_INVALID)."""
+    from sentinel_amd import engine
+    hb, R = _batch(seed=13, R=200, n=10_000)
+    eng = engine.FlowEngine(abi.default_config(max_resources=R, max_batch=hb.n))
+    pin = engine.PinnedArrays(eng)
+    try:
+        eng.load_flow_rules(trace.mixed_rules(R, seed=13))
+        pb = abi.PackedBatch(hb, alloc=pin.array, narrow=True)
+        pb.ms_end[-1] = hb.n - 1
+        o = pin.verdicts(hb.n)
+        with pytest.raises(engine.EngineError):
+            eng.submit_packed(pb, o)
+    finally:
+        pin.free()
+        eng.close()
 
 
 def test_packing_refuses_a_long_span():
