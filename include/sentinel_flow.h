@@ -451,7 +451,7 @@ int  sf_submit_async(sf_engine* e, const sf_event_batch* in, sf_verdicts* out);
 #define SF_PK_FLAGS_SHIFT 59
 #define SF_PK4_COUNT_SHIFT 24
 #define SF_PK4_FLAGS_SHIFT 27
-#define SF_PK4_MAX_MS (1u << 20)
+#define SF_PK4_MAX_MS 1048576u
 typedef struct sf_packed_batch {
     uint32_t        n;
     int32_t         mem;          /* SF_MEM_HOST or SF_MEM_DEVICE (all arrays)  */

@@ -25,8 +25,10 @@ import static java.lang.foreign.ValueLayout.JAVA_SHORT;
  * queue order, as the engine requires.  The arrays are page-locked host
  * memory from sf_host_alloc (the engine's H2D copy runs at PCIe speed, no
  * staging copy); a batch without ParamFlow arguments or context names, whose
- * clock spans less than 2^20 ms, goes as sf_packed_batch (8 bytes per event),
- * every other one as the sf_event_batch SoA (sf_submit).
+ * clock spans less than 2^20 ms, goes as sf_packed_batch -- in the narrow form
+ * (4 bytes per event plus a table of the batch's milliseconds) when every
+ * resource id is below 2^24, else 8 bytes per event --, every other one as
+ * the sf_event_batch SoA (sf_submit).
  *
  * Latency / throughput contract.  Packed batches are double-buffered: the
  * flusher enqueues batch k+1 with sf_submit_packed_sparse_async into the
@@ -66,6 +68,8 @@ final class EventBatcher implements Runnable {
     /** One buffer set of the packed path: the batch arrays, its verdicts and its tickets. */
     private final class PackedBuf {
         final MemorySegment pev = pinned(8L * maxBatch), pxref = pinned(8L * maxBatch), pxcts = pinned(8L * maxBatch);
+        // the narrow form: 4-byte words and ms_end, the events up to each millisecond of the batch
+        final MemorySegment pev4 = pinned(4L * maxBatch), pms = pinned(4L * PK4_MAX_MS);
         final MemorySegment pcext = pinned(4L * maxBatch), porigin = pinned(4L * maxBatch);
         // verdicts copied back sparse: a status byte per event, the nonzero waits / rule
         // indices as (index << 32 | value) lists, maxBatch / 64 of each with the batch
@@ -289,24 +293,35 @@ final class EventBatcher implements Runnable {
     private boolean flushPacked(List<Ticket> b, long bs) throws Throwable {
         final int n = b.size();
         long t0 = Long.MIN_VALUE, last = lastTs;
+        boolean narrow = true;
         for (Ticket t : b) {
             if ((t.args != null && t.args.length > 0) || t.context != 0) return false;
             last = Math.max(last, t.ts);
             if (t0 == Long.MIN_VALUE) t0 = last;
+            narrow &= (t.resource & 0xffffffffL) < (1L << 24);
         }
         if (last - t0 >= (1L << 20)) return false;
         final PackedBuf p = pbufs[pcur];             // not the in-flight set: sets alternate
-        int nx = 0, nc = 0;
+        int nx = 0, nc = 0, ms = 0;
         boolean anyOrigin = false;
         for (int i = 0; i < n; i++) {
             Ticket t = b.get(i);
             t.batchSeq = bs; t.batchIndex = i;
             lastTs = Math.max(lastTs, t.ts);
+            final int d = (int) (lastTs - t0);
             long c = t.count;
-            if (c < 1 || c > 127) { p.pcext.setAtIndex(JAVA_INT, nc++, t.count); c = 0; }
             long f = t.flags & 0x1f;
-            p.pev.setAtIndex(JAVA_LONG, i, (t.resource & 0xffffffffL) | ((lastTs - t0) << 32)
-                    | (c << PK_COUNT_SHIFT) | (f << PK_FLAGS_SHIFT));
+            if (narrow) {
+                if (c < 1 || c > 7) { p.pcext.setAtIndex(JAVA_INT, nc++, t.count); c = 0; }
+                // ms_end[m] = events with delta <= m: the milliseconds before this event's end at i
+                for (; ms < d; ms++) p.pms.setAtIndex(JAVA_INT, ms, i);
+                p.pev4.setAtIndex(JAVA_INT, i, (int) ((t.resource & 0xffffffL) | (c << PK4_COUNT_SHIFT)
+                        | (f << PK4_FLAGS_SHIFT)));
+            } else {
+                if (c < 1 || c > 127) { p.pcext.setAtIndex(JAVA_INT, nc++, t.count); c = 0; }
+                p.pev.setAtIndex(JAVA_LONG, i, (t.resource & 0xffffffffL) | ((long) d << 32)
+                        | (c << PK_COUNT_SHIFT) | (f << PK_FLAGS_SHIFT));
+            }
             p.porigin.setAtIndex(JAVA_INT, i, t.origin);
             anyOrigin |= t.origin != -1;
             if ((t.flags & EV_EXIT) != 0) {
@@ -320,7 +335,11 @@ final class EventBatcher implements Runnable {
         pk.set(JAVA_INT, off(PACKED_BATCH, "n"), n);
         pk.set(JAVA_INT, off(PACKED_BATCH, "mem"), SF_MEM_HOST_);
         pk.set(JAVA_LONG, off(PACKED_BATCH, "ts_base"), t0);
-        pk.set(ADDRESS, off(PACKED_BATCH, "ev"), p.pev);
+        if (narrow) p.pms.setAtIndex(JAVA_INT, ms, n);             // the last millisecond ends the batch
+        pk.set(ADDRESS, off(PACKED_BATCH, "ev"), narrow ? MemorySegment.NULL : p.pev);
+        pk.set(ADDRESS, off(PACKED_BATCH, "ev4"), narrow ? p.pev4 : MemorySegment.NULL);
+        pk.set(ADDRESS, off(PACKED_BATCH, "ms_end"), narrow ? p.pms : MemorySegment.NULL);
+        pk.set(JAVA_INT, off(PACKED_BATCH, "n_ms"), narrow ? ms + 1 : 0);
         pk.set(ADDRESS, off(PACKED_BATCH, "exit_ref"), nx > 0 ? p.pxref : MemorySegment.NULL);
         pk.set(ADDRESS, off(PACKED_BATCH, "exit_cts"), nx > 0 ? p.pxcts : MemorySegment.NULL);
         pk.set(ADDRESS, off(PACKED_BATCH, "count_ext"), nc > 0 ? p.pcext : MemorySegment.NULL);

@@ -129,7 +129,7 @@ final class SentinelFlowNative {
             ADDRESS.withName("origin"), ADDRESS.withName("context"));
 
     /** sf_packed_batch: 8 bytes per event (res | ts - ts_base << 32 | count << 52 | flags << 59); the
-     *  narrow form's fields (ev4, ms_end, n_ms) stay NULL / 0 here: EventBatcher sends the 8-byte form. */
+     *  narrow form (ev NULL): ev4 words res | count << 24 | flags << 27 and the table ms_end[n_ms]. */
     static final StructLayout PACKED_BATCH = MemoryLayout.structLayout(
             JAVA_INT.withName("n"), JAVA_INT.withName("mem"), JAVA_LONG.withName("ts_base"),
             ADDRESS.withName("ev"), ADDRESS.withName("exit_ref"), ADDRESS.withName("exit_cts"),
@@ -138,6 +138,7 @@ final class SentinelFlowNative {
             ADDRESS.withName("ev4"), ADDRESS.withName("ms_end"), JAVA_INT.withName("n_ms"),
             JAVA_INT.withName("pad0"));
     static final int PK_COUNT_SHIFT = 52, PK_FLAGS_SHIFT = 59;
+    static final int PK4_COUNT_SHIFT = 24, PK4_FLAGS_SHIFT = 27, PK4_MAX_MS = 1048576;
 
     /** sf_verdicts. */
     static final StructLayout VERDICTS = MemoryLayout.structLayout(

@@ -191,3 +191,28 @@ def test_node_placement_twin():
     assert p.moved.size == 16384
     assert np.all(p.owner(np.arange(20000)) == p.engine_id(np.arange(20000)) % 8)
     assert np.unique(p.engine_id(np.arange(20000))).size == 20000
+
+
+def test_batcher_narrow_form_twin():
+    """EventBatcher's narrow packing (no JDK: checked statically plus a Python
+    twin of its loop): 4-byte words res | count << 24 | flags << 27 and
+    ms_end[m] = the events with delta <= m, built in one pass over the
+    time-ordered batch, equal abi.PackedBatch(narrow=True)'s."""
+    import numpy as np
+    from sentinel_amd import abi, trace
+    src = j.source("EventBatcher.java")
+    fp = src[src.index("private boolean flushPacked"):]
+    assert "narrow &= (t.resource & 0xffffffffL) < (1L << 24);" in fp
+    assert "for (; ms < d; ms++) p.pms.setAtIndex(JAVA_INT, ms, i);" in fp
+    assert "if (narrow) p.pms.setAtIndex(JAVA_INT, ms, n);" in fp
+    assert '"n_ms"), narrow ? ms + 1 : 0);' in fp and "(c < 1 || c > 7)" in fp
+    hb = trace.mixed_zipf(300, 20_000, duration_ms=5000, seed=3)
+    d = (hb.ts_ms - hb.ts_ms[0]).astype(np.int64)
+    ms_end, ms = [], 0
+    for i, di in enumerate(d):                 # the Java loop
+        while ms < di:
+            ms_end.append(i)
+            ms += 1
+    ms_end.append(hb.n)
+    pb = abi.PackedBatch(hb, narrow=True)
+    assert pb.n_ms == ms + 1 and np.array_equal(np.array(ms_end, np.uint32), pb.ms_end)
