@@ -68,6 +68,7 @@ struct sf_engine {
     unsigned pending = 0;           // Work sets with an asynchronous batch not yet checked by sf_sync
     bool used[2] = {false, false};
     hipEvent_t ev_sorted[2]{}, ev_done[2]{};
+    hipEvent_t ev_end[2]{};                          // ev_done and the batch's ENTRY_NODE update (reads the batch)
     hipEvent_t ev_core[2]{};                         // the verdicts of the slot's batch are written
     SysRule sys{};                  // SystemRuleManager statics; sys.check: batches go through the planner
     SysPlanDev* sys_plan = nullptr; SysExitQ* sys_pa = nullptr; SysEntQ* sys_pb = nullptr;
@@ -262,6 +263,7 @@ void sf_destroy(sf_engine* e) {
     for (int k = 0; k < 2; k++) {
         if (e->ev_sorted[k]) hipEventDestroy(e->ev_sorted[k]);
         if (e->ev_done[k]) hipEventDestroy(e->ev_done[k]);
+        if (e->ev_end[k]) hipEventDestroy(e->ev_end[k]);
         if (e->ev_core[k]) hipEventDestroy(e->ev_core[k]);
     }
     if (e->stream) hipStreamDestroy(e->stream);
@@ -408,6 +410,7 @@ int sf_create(const sf_config* cfg, sf_engine** out) {
     for (int k = 0; k < 2; k++) {
         HIP_TRY(hipEventCreateWithFlags(&e->ev_sorted[k], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&e->ev_done[k], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_end[k], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&e->ev_core[k], hipEventDisableTiming));
     }
 
@@ -1196,6 +1199,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         }
         HIP_TRY(hipEventRecord(e->ev_core[slot], s));
         HIP_TRY(hipEventRecord(e->ev_done[slot], s));
+    HIP_TRY(hipEventRecord(e->ev_end[slot], s));
         e->used[slot] = true;
         e->last = slot;
         e->stats.n_events = n;
@@ -1245,12 +1249,14 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
     // ENTRY_NODE: every IN event's StatisticSlot updates (after the verdicts, stream
     // order); under the round protocol the node-wide stream updates it (sf_entry_node_add)
     if (side) {
-        // asynchronous: on the ENTRY_NODE stream after the scatter; the Work set
-        // (and the caller's batch, which k_entry_acc reads) is free after it
+        // asynchronous: on the side stream after the scatter.  The Work set is
+        // free after the scatter (ev_done: the sort of the batch after next waits
+        // for it), the batch k_entry_acc reads after the update (ev_end)
         HIP_TRY(hipEventRecord(e->ev_core[slot], e->enstream));
+        HIP_TRY(hipEventRecord(e->ev_done[slot], e->enstream));
         le = launch_entry_node(stl, b, dv.status, e->en, e->en_acc, e->enstream);
         if (le != hipSuccess) return fail(SF_ERR_DEVICE, std::string("entry node: ") + hipGetErrorString(le));
-        HIP_TRY(hipEventRecord(e->ev_done[slot], e->enstream));
+        HIP_TRY(hipEventRecord(e->ev_end[slot], e->enstream));
         HIP_TRY(hipEventRecord(e->ev_en, e->enstream));
         e->en_async = true;
     } else {
@@ -1261,6 +1267,7 @@ static int submit_core(sf_engine* e, const sf_event_batch* in, sf_verdicts* out,
         }
         HIP_TRY(hipEventRecord(e->ev_core[slot], s));
         HIP_TRY(hipEventRecord(e->ev_done[slot], s));
+    HIP_TRY(hipEventRecord(e->ev_end[slot], s));
     }
     e->used[slot] = true;
     e->timed[slot] = e->timing;
@@ -1364,7 +1371,7 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     const size_t o_wl = sp ? take(N * 8) : 0, o_rl = sp ? take(N * 8) : 0, o_sc = sp ? take(16) : 0;
     const size_t o_ms = narrow ? take((size_t)SF_PK4_MAX_MS * 4) : 0;   // (the narrow words use o_ev's room)
     if (pk.bytes < off) {
-        if (e->used[slot]) HIP_TRY(hipEventSynchronize(e->ev_done[slot]));
+        if (e->used[slot]) HIP_TRY(hipEventSynchronize(e->ev_end[slot]));
         if (pk.consumed_pending) { HIP_TRY(hipEventSynchronize(pk.consumed)); pk.consumed_pending = false; }
         if (pk.d2h_pending) { HIP_TRY(hipEventSynchronize(pk.d2h)); pk.d2h_pending = false; }
         if (pk.buf) hipFree(pk.buf);
@@ -1434,6 +1441,9 @@ static int submit_packed(sf_engine* e, const sf_packed_batch* in, sf_verdicts* o
     dv.status = host_out ? (uint8_t*)(B + o_st) : out->status;
     dv.wait_ms = (sp || out->wait_ms) ? (host_out ? (int32_t*)(B + o_wt) : out->wait_ms) : nullptr;
     dv.rule_idx = (sp || out->rule_idx) ? (host_out ? (uint16_t*)(B + o_ru) : out->rule_idx) : nullptr;
+    // (the expansion rewrites the arrays the ENTRY_NODE update of this slot's
+    // previous batch reads)
+    if (e->used[slot]) HIP_TRY(hipStreamWaitEvent(ss, e->ev_end[slot], 0));
     const int rc = submit_core(e, &eb, &dv, core_async, nullptr, &expand);
     if (rc) return rc;
     pk.consumed_pending = true;
@@ -1790,6 +1800,7 @@ int sf_submit_node(sf_engine* e, const sf_event_batch* in, const int64_t* seq, s
     if (lp != n) return fail(SF_ERR_DEVICE, "exchange rounds left events undecided");
     HIP_TRY(hipEventRecord(e->ev_core[slot], s));
     HIP_TRY(hipEventRecord(e->ev_done[slot], s));
+    HIP_TRY(hipEventRecord(e->ev_end[slot], s));
     e->used[slot] = true;
     e->last = slot;
     e->stats.n_events = n;
