@@ -42,6 +42,7 @@ struct SysPlanArgs {
     DevBatch b;
     uint8_t* ostatus; uint16_t* orule;
     uint8_t* ibuf;                          // [SP_CAP] param_inert of event p + k (k_sp_inert)
+    bool qcap;                              // limit the plan by the qps budget (k_sp_init)
 };
 
 __global__ void k_sp_init(SysPlanArgs a, const EntryNode* en) {
@@ -56,6 +57,22 @@ __global__ void k_sp_init(SysPlanArgs a, const EntryNode* en) {
     pl.first_unc = pl.lim;
     pl.n_inert = 0;
     pl.base = sys_base(en->second, a.S, a.wl, a.interval, a.max_rt, en->threads, t);
+    // A plan ends at its first entry whose qps check can go either way, which
+    // comes within about B = qps * intervalSec - P passing entries of p while
+    // the budget B is at least 1: plan only that far (4 B + 64 Ki events) instead
+    // of the window's end.  Near a window's crossing B is small, and the
+    // planner's passes over up to 2 Mi events were most of a round's cost.  A
+    // plan cut short only costs one more round (every event before lim is
+    // classified as before).
+    if (a.qcap) {
+        const double B = a.r.qps * a.interval_sec - (double)pl.base.P;
+        // (B < 1: every entry with acquireCount >= 1 certainly fires until the
+        // window ends -- a long round, not capped)
+        if (B >= 1.0 && B < (double)SP_CAP) {
+            const uint64_t cap = (uint64_t)a.p + 4ull * (uint64_t)B + 65536ull;
+            if (cap < pl.lim) { pl.lim = (uint32_t)cap; pl.first_unc = pl.lim; }
+        }
+    }
 }
 // sys_plan_fix: the range is the decided sub-batch [p, q); base is still ENTRY_NODE at p
 __global__ void k_sp_fix_init(SysPlanDev* pl) {
@@ -284,6 +301,8 @@ hipError_t sys_plan(const DevState& st, const DevBatch& b, const uint8_t* vstatu
                     uint8_t* ibuf) {
     SysPlanArgs a = plan_args(st, b, vstatus, mask, r, p, plan, pa, pb, ibuf);
     a.inert = ibuf && st.n_prule != 0;
+    static const bool qcap = [] { const char* x = getenv("SF_PLAN_QCAP"); return !(x && x[0] == '0'); }();
+    a.qcap = qcap;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(SP_NB, ((uint64_t)(b.n - p) + SP_BLK - 1) / SP_BLK);
     hipLaunchKernelGGL(k_sp_init, dim3(1), dim3(64), 0, s, a, en);
     if (a.inert) hipLaunchKernelGGL(k_sp_inert, dim3(nb * (SP_BLK / 256)), dim3(256), 0, s, a);
