@@ -42,7 +42,7 @@ struct SysPlanArgs {
     DevBatch b;
     uint8_t* ostatus; uint16_t* orule;
     uint8_t* ibuf;                          // [SP_CAP] param_inert of event p + k (k_sp_inert)
-    bool qcap;                              // limit the plan by the qps budget (k_sp_init)
+    uint32_t qcap;                          // limit the plan to qcap x the qps budget (k_sp_init; 0: off)
 };
 
 __global__ void k_sp_init(SysPlanArgs a, const EntryNode* en) {
@@ -59,7 +59,7 @@ __global__ void k_sp_init(SysPlanArgs a, const EntryNode* en) {
     pl.base = sys_base(en->second, a.S, a.wl, a.interval, a.max_rt, en->threads, t);
     // A plan ends at its first entry whose qps check can go either way, which
     // comes within about B = qps * intervalSec - P passing entries of p while
-    // the budget B is at least 1: plan only that far (4 B + 64 Ki events) instead
+    // the budget B is at least 1: plan only that far (2 B + 64 Ki events) instead
     // of the window's end.  Near a window's crossing B is small, and the
     // planner's passes over up to 2 Mi events were most of a round's cost.  A
     // plan cut short only costs one more round (every event before lim is
@@ -69,7 +69,7 @@ __global__ void k_sp_init(SysPlanArgs a, const EntryNode* en) {
         // (B < 1: every entry with acquireCount >= 1 certainly fires until the
         // window ends -- a long round, not capped)
         if (B >= 1.0 && B < (double)SP_CAP) {
-            const uint64_t cap = (uint64_t)a.p + 4ull * (uint64_t)B + 65536ull;
+            const uint64_t cap = (uint64_t)a.p + (uint64_t)a.qcap * (uint64_t)B + 65536ull;
             if (cap < pl.lim) { pl.lim = (uint32_t)cap; pl.first_unc = pl.lim; }
         }
     }
@@ -301,7 +301,7 @@ hipError_t sys_plan(const DevState& st, const DevBatch& b, const uint8_t* vstatu
                     uint8_t* ibuf) {
     SysPlanArgs a = plan_args(st, b, vstatus, mask, r, p, plan, pa, pb, ibuf);
     a.inert = ibuf && st.n_prule != 0;
-    static const bool qcap = [] { const char* x = getenv("SF_PLAN_QCAP"); return !(x && x[0] == '0'); }();
+    static const uint32_t qcap = [] { const char* x = getenv("SF_PLAN_QCAP"); return x ? (uint32_t)atoi(x) : 2u; }();
     a.qcap = qcap;
     const uint32_t nb = (uint32_t)std::min<uint64_t>(SP_NB, ((uint64_t)(b.n - p) + SP_BLK - 1) / SP_BLK);
     hipLaunchKernelGGL(k_sp_init, dim3(1), dim3(64), 0, s, a, en);
